@@ -1,0 +1,225 @@
+/*
+ * pifpaf_amd.h — C ABI of libpifpaf_amd.so, the MI355X (gfx950) CIF/CAF pose decoder.
+ *
+ * Drop-in boundary for openpifpaf v0.11.6's decoder hot path.  The reference exposes
+ * this path as the Cython extension module `openpifpaf.functional`
+ * (openpifpaf/functional.pyx) plus the pure-Python decoder classes in
+ * openpifpaf/decoder/ (cif_hr.py, cif_seeds.py, caf_scored.py, generator/cifcaf.py,
+ * nms.py, occupancy.py).  Every entry point below names the reference interface it
+ * replaces (file:line).  The Python mirror of those interfaces is the package
+ * openpifpaf_amd (ctypes over this header).
+ *
+ * Conventions (all entry points):
+ *   - plain pointers + sizes, no C++/torch types; arrays are C-contiguous float32 unless
+ *     a pitch/stride argument says otherwise.  Element strides, not byte strides.
+ *   - every pointer named d_* is DEVICE memory (hipMalloc / torch device tensors).
+ *     The caller owns all buffers; the library never allocates or frees them.
+ *   - calls are asynchronous on `stream` (a hipStream_t; NULL = legacy default stream).
+ *     No host synchronisation inside (graph-capturable).
+ *   - return 0 on success or a negative pp_status; pp_last_error() returns a
+ *     thread-local message for the last failure on the calling thread.
+ *   - the library has no global mutable state; calls on distinct streams are thread-safe.
+ */
+#ifndef PIFPAF_AMD_H
+#define PIFPAF_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PP_ABI_VERSION 1
+
+/* capacities of one annotation record (COCO person: 17 keypoints, 19 or 44 edges) */
+#define PP_MAX_KP 24
+#define PP_MAX_EDGES 64
+#define PP_MAX_FRONTIER (4 * PP_MAX_EDGES)
+
+typedef enum pp_status {
+    PP_OK = 0,
+    PP_EINVAL = -1,     /* bad argument (NULL pointer, negative size, bad enum) */
+    PP_ESHAPE = -2,     /* shape outside the supported envelope                 */
+    PP_EOVERFLOW = -3,  /* a capacity was exceeded; see the per-image status     */
+    PP_EHIP = -4,       /* HIP runtime error (launch / device)                   */
+    PP_ENOMEM = -5      /* workspace too small                                   */
+} pp_status;
+
+/*
+ * Decoder configuration.  The reference keeps these as CLASS ATTRIBUTES written by
+ * decoder/factory.py:configure (factory.py:64-98); pp_default_config() fills the
+ * reference defaults (eval_coco: force_complete=1, seed_threshold=0.2).
+ */
+typedef struct pp_config {
+    float cif_threshold;          /* CifHr.v_threshold                cif_hr.py:16          */
+    float seed_threshold;         /* CifSeeds.threshold               cif_seeds.py:14       */
+    float seed_score_scale;       /* CifSeeds.score_scale             cif_seeds.py:15       */
+    float caf_threshold;          /* CafScored.default_score_th       caf_scored.py:14      */
+    float complete_caf_threshold; /* score_th of the force-complete CafScored cifcaf.py:337 */
+    float cif_floor;              /* CafScored(cif_floor=0.1)         caf_scored.py:16      */
+    float keypoint_threshold;     /* CifCaf.keypoint_threshold        cifcaf.py:33          */
+    float nms_keypoint_threshold; /* nms.Keypoints.keypoint_threshold nms.py:14             */
+    float nms_instance_threshold; /* nms.Keypoints.instance_threshold nms.py:13             */
+    float nms_suppression;        /* nms.Keypoints.suppression        nms.py:12             */
+    int32_t stride;               /* FieldConfig.cif_strides[0] == caf_strides[0]  field_config.py:9-10 */
+    int32_t cif_neighbors;        /* CifHr.neighbors                  cif_hr.py:15          */
+    int32_t force_complete;       /* CifCaf.force_complete            cifcaf.py:31          */
+    int32_t greedy;               /* CifCaf.greedy                    cifcaf.py:32          */
+    int32_t connection_method;    /* CifCaf.connection_method: 0 'blend', 1 'max'  cifcaf.py:29 */
+    int32_t apply_nms;            /* CifCaf(nms=True) -> nms.Keypoints()  cifcaf.py:43-44   */
+    int32_t occupancy_reduction;  /* Occupancy(shape, 2, min_scale=4)  cifcaf.py:84         */
+    int32_t occupancy_min_scale;
+} pp_config;
+
+/*
+ * One output annotation (openpifpaf/annotation.py:9-28).  data/joint_scales are the
+ * reference's float32 arrays; score is Annotation.score() (float64, annotation.py:60-71).
+ * decoding_order entries (jsi, jti, xyv_jsi, xyv_jti) and frontier_order pairs as
+ * appended by CifCaf._grow (cifcaf.py:263,305-306), 0-based joint indices.
+ */
+typedef struct pp_ann {
+    float data[PP_MAX_KP][3];
+    float joint_scales[PP_MAX_KP];
+    double score;
+    int32_t n_keypoints;
+    int32_t n_decoding;
+    int32_t n_frontier;
+    int32_t image;
+    uint8_t decoding_pairs[PP_MAX_KP][2];
+    float decoding_xyv[PP_MAX_KP][6];
+    uint8_t frontier_pairs[PP_MAX_FRONTIER][2];
+} pp_ann;
+
+/* one seed (cif_seeds.py:47 tuple (v, field, x, y, s)) */
+typedef struct pp_seed {
+    float v;
+    int32_t field;
+    float x;
+    float y;
+    float s;
+} pp_seed;
+
+/* per-image status bits written by pp_decode_batch (d_status) */
+#define PP_ST_ANN_OVERFLOW 1   /* more annotations than ann_capacity               */
+#define PP_ST_NMS_OVERFLOW 2   /* NMS occupancy larger than the occupancy workspace */
+#define PP_ST_SEED_OVERFLOW 4  /* more seeds than the seed workspace               */
+#define PP_ST_DEC_OVERFLOW 8   /* decoding/frontier order longer than the record   */
+
+int pp_version(void);
+const char *pp_last_error(void);
+void pp_default_config(pp_config *cfg);
+
+/* ---------------------------------------------------------------------------------
+ * Decoder stages.  Batched: n_img images, fields (n_img, K, 5, H, W) and
+ * (n_img, C, 9, H, W) resident in device memory.  The high-resolution CIF map is laid
+ * out (n_img, K, H', pitch) with H' = (H-1)*stride+1, W' = (W-1)*stride+1 and
+ * pitch = pp_cifhr_pitch(W') (a multiple of 32 floats, so each row starts on a 128-B line).
+ * --------------------------------------------------------------------------------- */
+int64_t pp_cifhr_pitch(int64_t w_hr);
+
+/* bytes of scratch pp_decode_batch needs (pass the same arguments) */
+size_t pp_decode_workspace_size(int32_t n_img, int32_t K, int32_t C, int32_t H, int32_t W,
+                                const pp_config *cfg, int32_t ann_capacity);
+
+/*
+ * CifHr (cif_hr.py:14-81): zero-init + accumulate every CIF cell with c > cif_threshold
+ * as a truncate=1 Gaussian splat (functional.pyx:105-141) into d_cifhr.  Bit-exact.
+ * d_workspace >= pp_cifhr_workspace_size(n_img, K, H, W).
+ */
+size_t pp_cifhr_workspace_size(int32_t n_img, int32_t K, int32_t H, int32_t W);
+int pp_cifhr(const float *d_cif, int32_t n_img, int32_t K, int32_t H, int32_t W,
+             const pp_config *cfg, float *d_cifhr, void *d_workspace, size_t workspace_bytes,
+             void *stream);
+
+/*
+ * CifSeeds (cif_seeds.py:23-64): per image, the seeds sorted as
+ * sorted(seeds, reverse=True) (cif_seeds.py:54).  d_seeds (n_img, seed_capacity),
+ * d_counts (n_img) = true count (may exceed capacity -> PP_ST_SEED_OVERFLOW semantics).
+ */
+int pp_seeds(const float *d_cif, const float *d_cifhr, int32_t n_img, int32_t K, int32_t H,
+             int32_t W, const pp_config *cfg, pp_seed *d_seeds, int32_t seed_capacity,
+             int32_t *d_counts, void *stream);
+
+/*
+ * CafScored (caf_scored.py:32-98) for one score threshold: per image and CAF field, the
+ * backward and forward (9, N) column sets.  Layout d_cols (n_img, C, 2, 9, H*W) with
+ * direction 0 = backward, 1 = forward; d_counts (n_img, C, 2).
+ */
+int pp_caf_scored(const float *d_caf, const float *d_cifhr, int32_t n_img, int32_t K,
+                  int32_t C, int32_t H, int32_t W, const int32_t *skeleton, float score_th,
+                  const pp_config *cfg, float *d_cols, int32_t *d_counts, void *stream);
+
+/*
+ * Full decode, CifCaf.__call__ (cifcaf.py:67-122) for a batch: CifHr -> CifSeeds ->
+ * CafScored -> seed loop / _grow -> complete_annotations -> nms.Keypoints.
+ *   skeleton      HOST array (C, 2) of 1-based joint pairs (cifcaf.py:50)
+ *   d_anns        (n_img, ann_capacity) records, image-major, in the reference's final order
+ *   d_counts      (n_img) number of annotations per image (true count)
+ *   d_status      (n_img) PP_ST_* bits; a non-zero bit means "re-run with more capacity"
+ *   d_cifhr       optional (n_img, K, H', pitch) output of the CifHr stage (NULL: scratch)
+ */
+int pp_decode_batch(const float *d_cif, const float *d_caf, int32_t n_img, int32_t K,
+                    int32_t C, int32_t H, int32_t W, const int32_t *skeleton,
+                    const pp_config *cfg, float *d_cifhr, pp_ann *d_anns,
+                    int32_t ann_capacity, int32_t *d_counts, int32_t *d_status,
+                    void *d_workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------------
+ * openpifpaf.functional primitives (functional.pyx).  `field` arguments are
+ * (h, w) float32 with row pitch `pitch` (elements).  Point lists are length-n device
+ * arrays.  All are bit-exact restatements run as HIP kernels.
+ * --------------------------------------------------------------------------------- */
+
+/* functional.pyx:105-141 */
+int pp_scalar_square_add_gauss_with_max(float *d_field, int64_t h, int64_t w, int64_t pitch,
+                                        const float *d_x, const float *d_y,
+                                        const float *d_sigma, const float *d_v, int64_t n,
+                                        float truncate, float max_value, void *stream);
+/* functional.pyx:71-102 */
+int pp_scalar_square_add_gauss(float *d_field, int64_t h, int64_t w, int64_t pitch,
+                               const float *d_x, const float *d_y, const float *d_sigma,
+                               const float *d_v, int64_t n, float truncate, void *stream);
+/* functional.pyx:7-26 */
+int pp_scalar_square_add_constant(float *d_field, int64_t h, int64_t w, int64_t pitch,
+                                  const float *d_x, const float *d_y, const float *d_width,
+                                  const float *d_v, int64_t n, void *stream);
+/* functional.pyx:144-169 */
+int pp_scalar_square_max_gauss(float *d_field, int64_t h, int64_t w, int64_t pitch,
+                               const float *d_x, const float *d_y, const float *d_sigma,
+                               const float *d_v, int64_t n, float truncate, void *stream);
+/* functional.pyx:29-54 */
+int pp_cumulative_average(float *d_cuma, float *d_cumw, int64_t h, int64_t w, int64_t pitch,
+                          const float *d_x, const float *d_y, const float *d_width,
+                          const float *d_v, const float *d_w, int64_t n, void *stream);
+/* functional.pyx:172-211: x (n, d) row pitch x_pitch, y (>=2) updated in place,
+ * d_denom (n) out; d_out_steps (1 int32) = iterations run */
+int pp_weiszfeld_nd(const float *d_x, int64_t n, int64_t d, int64_t x_pitch, float *d_y,
+                    const float *d_weights, float epsilon, int64_t max_steps, float *d_denom,
+                    void *stream);
+/* functional.pyx:231-244 */
+int pp_scalar_values(const float *d_field, int64_t h, int64_t w, int64_t pitch,
+                     const float *d_x, const float *d_y, int64_t n, float default_value,
+                     float *d_out, void *stream);
+/*
+ * Single-point lookups, batched (functional.pyx:247-286).  mode:
+ *   0 scalar_value(default)  1 scalar_value_clipped  (float field, float out)
+ *   2 scalar_nonzero(default) 3 scalar_nonzero_clipped 4 ..._with_reduction(r)  (u8 field)
+ */
+int pp_scalar_lookup(const void *d_field, int64_t h, int64_t w, int64_t pitch, int32_t mode,
+                     const float *d_x, const float *d_y, int64_t n, float default_value,
+                     float reduction, void *d_out, void *stream);
+/*
+ * Column filters over a (rows, n) field with row pitch `pitch` (functional.pyx:214-228,
+ * 289-359), order preserving.  mode: 0 caf_center_s, 1 paf_center, 2 paf_center_b,
+ * 3 paf_mask_center (d_out = u8 mask (n)).  Modes 0-2 write the kept columns to
+ * d_out (rows, out_pitch) and the kept count to d_count (1 int32).
+ */
+int pp_center_filter(const float *d_field, int64_t rows, int64_t n, int64_t pitch, int32_t mode,
+                     float x, float y, float sigma, void *d_out, int64_t out_pitch,
+                     int32_t *d_count, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PIFPAF_AMD_H */

@@ -1,0 +1,90 @@
+"""NumPy / ctypes mirrors of the plain-data types in include/pifpaf_amd.h."""
+import ctypes
+
+import numpy as np
+
+PP_ABI_VERSION = 1
+PP_MAX_KP = 24
+PP_MAX_EDGES = 64
+PP_MAX_FRONTIER = 4 * PP_MAX_EDGES
+
+PP_ST_ANN_OVERFLOW = 1
+PP_ST_NMS_OVERFLOW = 2
+PP_ST_SEED_OVERFLOW = 4
+PP_ST_DEC_OVERFLOW = 8
+
+STATUS_NAMES = {
+    0: 'PP_OK', -1: 'PP_EINVAL', -2: 'PP_ESHAPE', -3: 'PP_EOVERFLOW', -4: 'PP_EHIP',
+    -5: 'PP_ENOMEM',
+}
+
+ANN_DTYPE = np.dtype([
+    ('data', np.float32, (PP_MAX_KP, 3)),
+    ('joint_scales', np.float32, (PP_MAX_KP,)),
+    ('score', np.float64),
+    ('n_keypoints', np.int32),
+    ('n_decoding', np.int32),
+    ('n_frontier', np.int32),
+    ('image', np.int32),
+    ('decoding_pairs', np.uint8, (PP_MAX_KP, 2)),
+    ('decoding_xyv', np.float32, (PP_MAX_KP, 6)),
+    ('frontier_pairs', np.uint8, (PP_MAX_FRONTIER, 2)),
+], align=True)
+assert ANN_DTYPE.itemsize == 1544, ANN_DTYPE.itemsize
+
+SEED_DTYPE = np.dtype([
+    ('v', np.float32), ('field', np.int32), ('x', np.float32), ('y', np.float32),
+    ('s', np.float32),
+])
+
+
+class PPConfig(ctypes.Structure):
+    """struct pp_config (include/pifpaf_amd.h)."""
+    _fields_ = [
+        ('cif_threshold', ctypes.c_float),
+        ('seed_threshold', ctypes.c_float),
+        ('seed_score_scale', ctypes.c_float),
+        ('caf_threshold', ctypes.c_float),
+        ('complete_caf_threshold', ctypes.c_float),
+        ('cif_floor', ctypes.c_float),
+        ('keypoint_threshold', ctypes.c_float),
+        ('nms_keypoint_threshold', ctypes.c_float),
+        ('nms_instance_threshold', ctypes.c_float),
+        ('nms_suppression', ctypes.c_float),
+        ('stride', ctypes.c_int32),
+        ('cif_neighbors', ctypes.c_int32),
+        ('force_complete', ctypes.c_int32),
+        ('greedy', ctypes.c_int32),
+        ('connection_method', ctypes.c_int32),
+        ('apply_nms', ctypes.c_int32),
+        ('occupancy_reduction', ctypes.c_int32),
+        ('occupancy_min_scale', ctypes.c_int32),
+    ]
+
+
+def make_config(*, cif_threshold=0.1, seed_threshold=0.2, seed_score_scale=1.0,
+                caf_threshold=0.1, complete_caf_threshold=0.0001, cif_floor=0.1,
+                keypoint_threshold=0.0, nms_keypoint_threshold=0.0,
+                nms_instance_threshold=0.0, nms_suppression=0.0, stride=8, cif_neighbors=16,
+                force_complete=True, greedy=False, connection_method='blend', apply_nms=True,
+                occupancy_reduction=2, occupancy_min_scale=4):
+    """Defaults = eval_coco defaults (decoder/factory.py:17-22, eval_coco.py:215)."""
+    if connection_method not in ('blend', 'max'):
+        raise Exception('connection method not known')
+    return PPConfig(
+        cif_threshold, seed_threshold, seed_score_scale, caf_threshold,
+        complete_caf_threshold, cif_floor, keypoint_threshold, nms_keypoint_threshold,
+        nms_instance_threshold, nms_suppression, int(stride), int(cif_neighbors),
+        int(bool(force_complete)), int(bool(greedy)),
+        0 if connection_method == 'blend' else 1, int(bool(apply_nms)),
+        int(occupancy_reduction), int(occupancy_min_scale))
+
+
+EVAL_CONFIG = dict(seed_threshold=0.2, force_complete=True, keypoint_threshold=0.0,
+                   nms_keypoint_threshold=0.0, nms_instance_threshold=0.0)
+PREDICT_CONFIG = dict(seed_threshold=0.5, force_complete=False, keypoint_threshold=0.001,
+                      nms_keypoint_threshold=0.001, nms_instance_threshold=0.1)
+
+
+def skeleton_array(skeleton):
+    return np.ascontiguousarray(np.asarray(skeleton, dtype=np.int32).reshape(-1, 2))

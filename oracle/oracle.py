@@ -1,0 +1,202 @@
+"""ctypes wrapper over oracle/liboracle.so (oracle/pp_oracle.c).
+
+TEST INFRASTRUCTURE: the CPU restatement of the reference decoder used as the parity
+checker by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.  The product
+package never imports this module.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from openpifpaf_amd._abi import ANN_DTYPE, SEED_DTYPE, make_config, skeleton_array
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+_f32p = np.ctypeslib.ndpointer(np.float32, flags='C_CONTIGUOUS')
+_vp = ctypes.c_void_p
+_l = ctypes.c_long
+_i = ctypes.c_int
+_f = ctypes.c_float
+
+
+def build():
+    subprocess.check_call(['make', '-s', '-C', HERE])
+
+
+def lib():
+    global _LIB  # pylint: disable=global-statement
+    if _LIB is None:
+        path = os.path.join(HERE, 'liboracle.so')
+        if not os.path.exists(path):
+            build()
+        _LIB = ctypes.CDLL(path)
+        _LIB.orc_decode.restype = ctypes.c_long
+        _LIB.orc_seeds.restype = ctypes.c_long
+        _LIB.orc_weiszfeld_nd.restype = ctypes.c_long
+        _LIB.orc_center_filter.restype = ctypes.c_long
+        _LIB.orc_ann_score.restype = ctypes.c_double
+        assert _LIB.orc_sizeof_ann() == ANN_DTYPE.itemsize
+    return _LIB
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _c32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def hr_shape(h, w, stride=8):
+    return (h - 1) * stride + 1, (w - 1) * stride + 1
+
+
+def cifhr(cif, cfg=None):
+    cfg = cfg or make_config()
+    cif = _c32(cif)
+    k, _, h, w = cif.shape
+    hh, ww = hr_shape(h, w, cfg.stride)
+    out = np.empty((k, hh, ww), np.float32)
+    lib().orc_cifhr(_p(cif), _i(k), _i(h), _i(w), ctypes.byref(cfg), _p(out))
+    return out
+
+
+def seeds(cif, hr, cfg=None):
+    cfg = cfg or make_config()
+    cif = _c32(cif)
+    hr = _c32(hr)
+    k, _, h, w = cif.shape
+    cap = k * h * w
+    out = np.empty(cap, SEED_DTYPE)
+    n = lib().orc_seeds(_p(cif), _p(hr), _l(hr.shape[-1]), _i(k), _i(h), _i(w),
+                        ctypes.byref(cfg), _p(out), _l(cap))
+    return out[:n]
+
+
+def caf_scored(caf, hr, skeleton, score_th, cfg=None):
+    """Returns (forward, backward): lists of (9, N_i) arrays (caf_scored.py:23-24)."""
+    cfg = cfg or make_config()
+    caf = _c32(caf)
+    hr = _c32(hr)
+    c, _, h, w = caf.shape
+    k = hr.shape[0]
+    skel = skeleton_array(skeleton)
+    cols = np.zeros((c, 2, 9, h * w), np.float32)
+    counts = np.zeros((c, 2), np.int32)
+    lib().orc_caf_scored(_p(caf), _p(hr), _l(hr.shape[-1]), _i(k), _i(c), _i(h), _i(w),
+                         _p(skel), _f(score_th), ctypes.byref(cfg), _p(cols), _p(counts))
+    forward = [cols[i, 1, :, :counts[i, 1]].copy() for i in range(c)]
+    backward = [cols[i, 0, :, :counts[i, 0]].copy() for i in range(c)]
+    return forward, backward
+
+
+def decode(cif, caf, skeleton, cfg=None):
+    """One image, CifCaf.__call__ -> structured array of pp_ann records."""
+    cfg = cfg or make_config()
+    cif = _c32(cif)
+    caf = _c32(caf)
+    k, _, h, w = cif.shape
+    c = caf.shape[0]
+    skel = skeleton_array(skeleton)
+    cap = 64
+    while True:
+        out = np.zeros(cap, ANN_DTYPE)
+        n = lib().orc_decode(_p(cif), _p(caf), _i(k), _i(c), _i(h), _i(w), _p(skel),
+                             ctypes.byref(cfg), _p(out), _l(cap))
+        if n < 0:
+            raise ValueError('oracle decode rejected the shapes')
+        if n <= cap:
+            return out[:n]
+        cap = int(n)
+
+
+def ann_score(v):
+    v = _c32(np.stack([np.zeros_like(v), np.zeros_like(v), v], axis=1))
+    return lib().orc_ann_score(_p(v.reshape(-1)), _i(len(v)))
+
+
+# ---- functional.pyx primitives (field arrays mutated in place, like the reference) ----
+
+def _field_args(field):
+    assert field.dtype == np.float32 or field.dtype == np.uint8
+    item = field.dtype.itemsize
+    return (_l(field.shape[0]), _l(field.shape[1]),
+            _l(field.strides[0] // item), _l(field.strides[1] // item))
+
+
+def scalar_square_add_gauss_with_max(field, x, y, sigma, v, truncate=2.0, max_value=1.0):
+    x, y, sigma, v = map(_c32, (x, y, sigma, v))
+    lib().orc_scalar_square_add_gauss_with_max(
+        _p(field), *_field_args(field), _p(x), _p(y), _p(sigma), _p(v), _l(len(x)),
+        _f(truncate), _f(max_value))
+
+
+def scalar_square_add_gauss(field, x, y, sigma, v, truncate=2.0):
+    x, y, sigma, v = map(_c32, (x, y, sigma, v))
+    lib().orc_scalar_square_add_gauss(
+        _p(field), *_field_args(field), _p(x), _p(y), _p(sigma), _p(v), _l(len(x)),
+        _f(truncate))
+
+
+def scalar_square_max_gauss(field, x, y, sigma, v, truncate=2.0):
+    x, y, sigma, v = map(_c32, (x, y, sigma, v))
+    lib().orc_scalar_square_max_gauss(
+        _p(field), *_field_args(field), _p(x), _p(y), _p(sigma), _p(v), _l(len(x)),
+        _f(truncate))
+
+
+def scalar_square_add_constant(field, x, y, width, v):
+    x, y, width, v = map(_c32, (x, y, width, v))
+    lib().orc_scalar_square_add_constant(
+        _p(field), *_field_args(field), _p(x), _p(y), _p(width), _p(v), _l(len(x)))
+
+
+def cumulative_average(cuma, cumw, x, y, width, v, w):
+    assert cuma.strides == cumw.strides
+    x, y, width, v, w = map(_c32, (x, y, width, v, w))
+    lib().orc_cumulative_average(
+        _p(cuma), _p(cumw), *_field_args(cuma), _p(x), _p(y), _p(width), _p(v), _p(w),
+        _l(len(x)))
+
+
+def weiszfeld_nd(x_np, y_np, weights, epsilon=1e-8, max_steps=20):
+    x = _c32(x_np)
+    weights = _c32(weights)
+    denom = np.zeros_like(weights)
+    lib().orc_weiszfeld_nd(_p(x), _l(x.shape[0]), _l(x.shape[1]), _l(x.shape[1]), _l(1),
+                           _p(y_np), _p(weights), _f(epsilon), _l(max_steps), _p(denom))
+    return y_np, denom
+
+
+def scalar_values(field, x, y, default=-1):
+    x, y = _c32(x), _c32(y)
+    out = np.empty(len(x), np.float32)
+    lib().orc_scalar_values(_p(field), *_field_args(field), _p(x), _p(y), _l(len(x)),
+                            _f(default), _p(out))
+    return out
+
+
+def scalar_lookup(field, x, y, mode, default=0.0, reduction=1.0):
+    x, y = _c32(np.atleast_1d(x)), _c32(np.atleast_1d(y))
+    out = np.empty(len(x), np.float32 if mode < 2 else np.uint8)
+    lib().orc_scalar_lookup(_p(field), *_field_args(field), _i(mode), _p(x), _p(y),
+                            _l(len(x)), _f(default), _f(reduction), _p(out))
+    return out
+
+
+def center_filter(field, x, y, sigma, mode):
+    rows, n = field.shape
+    item = field.dtype.itemsize
+    if mode == 3:
+        out = np.zeros(n, np.uint8)
+    else:
+        out = np.zeros((rows, n), np.float32)
+    k = lib().orc_center_filter(_p(field), _l(rows), _l(n), _l(field.strides[0] // item),
+                                _l(field.strides[1] // item), _i(mode), _f(x), _f(y),
+                                _f(sigma), _p(out))
+    if mode == 3:
+        return out != 0
+    return out[:, :k]

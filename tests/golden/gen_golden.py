@@ -1,0 +1,332 @@
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE itself.
+
+Run in the build container only (needs /root/reference):
+    python tests/golden/gen_golden.py
+
+The reference decoder is imported from /root/reference with its Cython primitives
+compiled by oracle/build_ref.sh (see oracle/ref_loader.py).  Nothing of the reference is
+copied: the fixtures hold inputs (or the parameters + SHA-256 that regenerate them with
+openpifpaf_amd.synthetic) and the reference's outputs.
+
+Fixtures:
+  primitives.npz       known-answer tests for every openpifpaf.functional primitive
+                       (small fields, full inputs and outputs, strided views, edge cases)
+  errors.json          the reference's ValueError messages at the boundary
+  decode_<case>.npz    per-stage vectors of the full CifCaf decoder: CifHr digest +
+                       per-field sums + windows, full seed list, CafScored counts + digests,
+                       full annotation lists (data, joint_scales, score, decoding_order,
+                       frontier_order)
+  meta.json            NumPy / Cython versions and SIMD dispatch of the generating host
+"""
+import hashlib
+import json
+import os
+import platform
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.abspath(os.path.join(HERE, '..', '..'))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, 'oracle'))
+
+import ref_loader  # noqa: E402  pylint: disable=wrong-import-position
+from openpifpaf_amd import constants, synthetic  # noqa: E402  pylint: disable=wrong-import-position
+from openpifpaf_amd._abi import EVAL_CONFIG, PREDICT_CONFIG  # noqa: E402  pylint: disable=wrong-import-position
+
+MODES = {'eval': EVAL_CONFIG, 'predict': PREDICT_CONFIG}
+
+# (name, generator, H, W, seed, mode, skeleton name, extra)
+CASES = [
+    ('u10_s0_eval', 'uniform', 10, 10, 0, 'eval', 'coco', {}),
+    ('u20_s0_eval', 'uniform', 20, 20, 0, 'eval', 'coco', {}),
+    ('u20_s1_eval', 'uniform', 20, 20, 1, 'eval', 'coco', {}),
+    ('u20_s2_predict', 'uniform', 20, 20, 2, 'predict', 'coco', {}),
+    ('u16x21_s0_eval', 'uniform', 16, 21, 0, 'eval', 'coco', {}),
+    ('p31x41_s0_eval', 'planted', 31, 41, 0, 'eval', 'coco', {'n_people': 3}),
+    ('p40_s0_eval', 'planted', 40, 40, 0, 'eval', 'coco', {}),
+    ('p40_s0_predict', 'planted', 40, 40, 0, 'predict', 'coco', {}),
+    ('p40_s3_max', 'planted', 40, 40, 3, 'eval', 'coco', {'connection_method': 'max'}),
+    ('p40_s4_greedy', 'planted', 40, 40, 4, 'eval', 'coco', {'greedy': True}),
+    ('p80_s0_eval', 'planted', 80, 80, 0, 'eval', 'coco', {}),
+    ('p80_s1_eval', 'planted', 80, 80, 1, 'eval', 'coco', {}),
+    ('p80_s2_eval', 'planted', 80, 80, 2, 'eval', 'coco', {}),
+    ('p80_s3_eval', 'planted', 80, 80, 3, 'eval', 'coco', {}),
+    ('p80_s0_predict', 'planted', 80, 80, 0, 'predict', 'coco', {}),
+    ('p81_s0_eval', 'planted', 81, 81, 0, 'eval', 'coco', {}),
+    ('u80_s0_eval', 'uniform', 80, 80, 0, 'eval', 'coco', {}),
+    ('u80_s0_predict', 'uniform', 80, 80, 0, 'predict', 'coco', {}),
+    ('p160_s0_dense_eval', 'planted', 160, 160, 0, 'eval', 'dense', {'n_people': 16}),
+    ('u160_s0_dense_eval', 'uniform', 160, 160, 0, 'eval', 'dense', {}),
+    ('zero20_eval', 'zero', 20, 20, 0, 'eval', 'coco', {}),
+]
+
+SKELETONS = {'coco': constants.COCO_PERSON_SKELETON, 'dense': constants.DENSE_DECODE_SKELETON}
+
+
+def sha(*arrays):
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def make_inputs(gen, h, w, seed, skeleton, extra):
+    if gen == 'zero':
+        return (np.zeros((17, 5, h, w), np.float32), np.zeros((len(skeleton), 9, h, w), np.float32))
+    if gen == 'uniform':
+        return synthetic.uniform(h, w, n_caf=len(skeleton), seed=seed)
+    return synthetic.planted(h, w, n_people=extra.get('n_people', 8), seed=seed,
+                             skeleton=skeleton)
+
+
+def configure(decoder, mode, extra):
+    c = MODES[mode]
+    decoder.CifHr.v_threshold = 0.1
+    decoder.CifSeeds.threshold = c['seed_threshold']
+    decoder.CafScored.default_score_th = 0.1
+    decoder.CifCaf.force_complete = c['force_complete']
+    decoder.CifCaf.keypoint_threshold = c['keypoint_threshold']
+    decoder.CifCaf.greedy = extra.get('greedy', False)
+    decoder.CifCaf.connection_method = extra.get('connection_method', 'blend')
+    decoder.nms.Keypoints.instance_threshold = c['nms_instance_threshold']
+    decoder.nms.Keypoints.keypoint_threshold = c['nms_keypoint_threshold']
+
+
+def run_case(op, name, gen, h, w, seed, mode, skel_name, extra):
+    from openpifpaf import decoder  # pylint: disable=import-outside-toplevel
+    skeleton = list(SKELETONS[skel_name])
+    configure(decoder, mode, extra)
+    cif, caf = make_inputs(gen, h, w, seed, skeleton, extra)
+    fc = decoder.FieldConfig()
+    hr = decoder.CifHr(fc).fill([cif, caf]).accumulated
+    seeds = decoder.CifSeeds(hr, fc).fill([cif, caf]).get()
+    cs_a = decoder.CafScored(hr, fc, skeleton).fill([cif, caf])
+    cs_b = decoder.CafScored(hr, fc, skeleton, score_th=0.0001).fill([cif, caf])
+    dec = decoder.CifCaf(fc, keypoints=constants.COCO_KEYPOINTS, skeleton=skeleton,
+                         out_skeleton=constants.COCO_PERSON_SKELETON)
+    anns = dec([cif, caf])
+
+    out = {
+        'generator': np.array(gen), 'H': h, 'W': w, 'seed': seed, 'mode': np.array(mode),
+        'skeleton': np.asarray(skeleton, np.int32),
+        'n_people': extra.get('n_people', 8),
+        'connection_method': np.array(extra.get('connection_method', 'blend')),
+        'greedy': int(extra.get('greedy', False)),
+        'input_sha': np.array(sha(cif, caf)),
+        'cifhr_sha': np.array(sha(hr)),
+        'cifhr_field_sums': hr.astype(np.float64).sum(axis=(1, 2)),
+        'seeds': np.array([tuple(float(t) for t in s) for s in seeds], np.float32).reshape(-1, 5),
+    }
+    if h <= 10:
+        out['cifhr'] = hr
+    # windows: top-left corner of each field's 48x48 window at the densest 8x8 cell block
+    wins = []
+    for f in (0, 5, 11, 16):
+        yy = min(hr.shape[1] - 48, hr.shape[1] // 3)
+        xx = min(hr.shape[2] - 48, hr.shape[2] // 3)
+        wins.append(hr[f, max(0, yy):max(0, yy) + 48, max(0, xx):max(0, xx) + 48])
+    out['cifhr_windows'] = np.stack([np.pad(wd, ((0, 48 - wd.shape[0]), (0, 48 - wd.shape[1])))
+                                     for wd in wins])
+    for tag, cs in (('a', cs_a), ('b', cs_b)):
+        out['caf_%s_fwd_counts' % tag] = np.array([f.shape[1] for f in cs.forward], np.int32)
+        out['caf_%s_bwd_counts' % tag] = np.array([b.shape[1] for b in cs.backward], np.int32)
+        out['caf_%s_fwd_sha' % tag] = np.array([sha(f) for f in cs.forward])
+        out['caf_%s_bwd_sha' % tag] = np.array([sha(b) for b in cs.backward])
+        if h <= 10:
+            out['caf_%s_fwd_cat' % tag] = np.concatenate(cs.forward, axis=1)
+            out['caf_%s_bwd_cat' % tag] = np.concatenate(cs.backward, axis=1)
+
+    n = len(anns)
+    out['ann_data'] = np.array([a.data for a in anns], np.float32).reshape(n, 17, 3)
+    out['ann_joint_scales'] = np.array([a.joint_scales for a in anns], np.float32).reshape(n, 17)
+    out['ann_score'] = np.array([a.score() for a in anns], np.float64)
+    dec_pairs = np.full((n, 17, 2), -1, np.int16)
+    dec_xyv = np.zeros((n, 17, 6), np.float32)
+    fr = np.full((n, 4 * len(skeleton), 2), -1, np.int16)
+    for i, a in enumerate(anns):
+        for t, (j1, j2, x1, x2) in enumerate(a.decoding_order):
+            dec_pairs[i, t] = (j1, j2)
+            dec_xyv[i, t, :3] = x1
+            dec_xyv[i, t, 3:] = x2
+        for t, (j1, j2) in enumerate(a.frontier_order):
+            fr[i, t] = (j1, j2)
+    out['ann_decoding_pairs'] = dec_pairs
+    out['ann_decoding_xyv'] = dec_xyv
+    out['ann_frontier_pairs'] = fr
+    np.savez_compressed(os.path.join(HERE, 'decode_%s.npz' % name), **out)
+    print('%-22s seeds %5d  caf_a %6d  caf_b %7d  anns %4d' % (
+        name, len(seeds), out['caf_a_fwd_counts'].sum(), out['caf_b_fwd_counts'].sum(), n))
+
+
+def gen_primitives(op):
+    F = sys.modules['openpifpaf.functional']
+    rng = np.random.default_rng(1234)
+    out = {}
+
+    def points(n, h, w, smin, smax):
+        x = rng.uniform(-4, w + 4, n).astype(np.float32)
+        y = rng.uniform(-4, h + 4, n).astype(np.float32)
+        s = rng.uniform(smin, smax, n).astype(np.float32)
+        v = rng.uniform(0.0, 0.8, n).astype(np.float32)
+        # integer and half-integer centres exercise the nearest-pixel branch
+        x[:6] = np.round(x[:6])
+        y[:6] = np.round(y[:6]) + 0.25
+        return x, y, s, v
+
+    h, w = 24, 32
+    for t, (trunc, maxv) in enumerate([(1.0, 1.0), (2.0, 1.0), (0.5, 0.7), (2.0, 0.3)]):
+        field = rng.uniform(0, 0.9, (h, w)).astype(np.float32)
+        x, y, s, v = points(40, h, w, 0.3, 6.0)
+        out['sqg_max_%d_in' % t] = field.copy()
+        out['sqg_max_%d_pts' % t] = np.stack([x, y, s, v])
+        out['sqg_max_%d_args' % t] = np.array([trunc, maxv], np.float32)
+        F.scalar_square_add_gauss_with_max(field, x, y, s, v, truncate=trunc, max_value=maxv)
+        out['sqg_max_%d_out' % t] = field
+    # strided view + empty point list
+    big = rng.uniform(0, 0.5, (2 * h, 2 * w + 1)).astype(np.float32)
+    out['sqg_max_strided_in'] = big.copy()
+    x, y, s, v = points(25, h, w, 0.5, 4.0)
+    out['sqg_max_strided_pts'] = np.stack([x, y, s, v])
+    F.scalar_square_add_gauss_with_max(big[::2, 1::2], x, y, s, v, truncate=1.0)
+    out['sqg_max_strided_out'] = big
+    field = rng.uniform(0, 0.5, (h, w)).astype(np.float32)
+    out['sqg_max_empty_in'] = field.copy()
+    e = np.zeros(0, np.float32)
+    F.scalar_square_add_gauss_with_max(field, e, e, e, e)
+    out['sqg_max_empty_out'] = field
+
+    for t, trunc in enumerate([2.0, 1.0]):
+        field = rng.uniform(0, 0.5, (h, w)).astype(np.float32)
+        x, y, s, v = points(30, h, w, 0.3, 5.0)
+        out['sqg_%d_in' % t] = field.copy()
+        out['sqg_%d_pts' % t] = np.stack([x, y, s, v])
+        out['sqg_%d_args' % t] = np.array([trunc], np.float32)
+        F.scalar_square_add_gauss(field, x, y, s, v, truncate=trunc)
+        out['sqg_%d_out' % t] = field
+
+    for t, trunc in enumerate([2.0, 1.0]):
+        field = rng.uniform(0, 0.5, (h, w)).astype(np.float32)
+        x, y, s, v = points(30, h, w, 0.3, 5.0)
+        out['sqmax_%d_in' % t] = field.copy()
+        out['sqmax_%d_pts' % t] = np.stack([x, y, s, v])
+        out['sqmax_%d_args' % t] = np.array([trunc], np.float32)
+        F.scalar_square_max_gauss(field, x, y, s, v, truncate=trunc)
+        out['sqmax_%d_out' % t] = field
+
+    field = rng.uniform(0, 0.5, (h, w)).astype(np.float32)
+    x, y, s, v = points(30, h, w, 0.3, 5.0)
+    out['sqc_in'] = field.copy()
+    out['sqc_pts'] = np.stack([x, y, s, v])
+    F.scalar_square_add_constant(field, x, y, s, v)
+    out['sqc_out'] = field
+
+    cuma = rng.uniform(0, 1, (h, w)).astype(np.float32)
+    cumw = rng.uniform(0, 2, (h, w)).astype(np.float32)
+    cumw[:4] = 0.0
+    x, y, s, v = points(30, h, w, 0.3, 5.0)
+    wt = rng.uniform(-0.5, 1.5, 30).astype(np.float32)
+    out['cuma_in'] = np.stack([cuma, cumw])
+    out['cuma_pts'] = np.stack([x, y, s, v, wt])
+    F.cumulative_average(cuma, cumw, x, y, s, v, wt)
+    out['cuma_out'] = np.stack([cuma, cumw])
+
+    for t, n in enumerate([7, 50, 1]):
+        xw = rng.normal(0, 10, (n, 2)).astype(np.float32)
+        y0 = rng.normal(0, 3, 2).astype(np.float32)
+        wts = rng.uniform(0.1, 2.0, n).astype(np.float32)
+        y = y0.copy()
+        _, denom = F.weiszfeld_nd(xw, y, weights=wts)
+        out['weisz_%d_x' % t] = xw
+        out['weisz_%d_y0' % t] = y0
+        out['weisz_%d_w' % t] = wts
+        out['weisz_%d_y' % t] = y
+        out['weisz_%d_denom' % t] = denom
+
+    field = rng.uniform(0, 1, (h, w)).astype(np.float32)
+    px = np.concatenate([rng.uniform(-2, w + 2, 60), [0.0, w - 1.0, w - 0.9, -0.0, 3.9]]).astype(np.float32)
+    py = np.concatenate([rng.uniform(-2, h + 2, 60), [0.0, h - 1.0, 2.0, h - 0.5, 1.0]]).astype(np.float32)
+    out['lookup_field'] = field
+    out['lookup_pts'] = np.stack([px, py])
+    out['scalar_values'] = F.scalar_values(field, px, py)
+    out['scalar_values_d0'] = F.scalar_values(field, px, py, default=0.0)
+    out['scalar_value'] = np.array([F.scalar_value(field, a, b) for a, b in zip(px, py)], np.float32)
+    out['scalar_value_clipped'] = np.array(
+        [F.scalar_value_clipped(field, a, b) for a, b in zip(px, py)], np.float32)
+    occ = rng.integers(0, 3, (h, w)).astype(np.uint8)
+    out['lookup_occ'] = occ
+    out['scalar_nonzero'] = np.array([F.scalar_nonzero(occ, a, b) for a, b in zip(px, py)], np.uint8)
+    out['scalar_nonzero_clipped'] = np.array(
+        [F.scalar_nonzero_clipped(occ, a, b) for a, b in zip(px, py)], np.uint8)
+    out['scalar_nonzero_red'] = np.array(
+        [F.scalar_nonzero_clipped_with_reduction(occ, 2 * a, 2 * b, 2.0) for a, b in zip(px, py)],
+        np.uint8)
+
+    caf = rng.uniform(0, 20, (9, 200)).astype(np.float32)
+    caf[3] = rng.uniform(0.5, 3, 200)
+    out['center_field'] = caf
+    qs = np.array([[10.0, 10.0, 3.0], [5.0, 15.0, 1.5], [0.0, 0.0, 2.0], [12.5, 7.25, 6.0]],
+                  np.float32)
+    out['center_queries'] = qs
+    for t, (qx, qy, qs_) in enumerate(qs):
+        out['caf_center_s_%d' % t] = F.caf_center_s(caf, qx, qy, qs_)
+        out['paf_center_%d' % t] = F.paf_center(caf[:7], qx, qy, qs_)
+        out['paf_center_b_%d' % t] = F.paf_center_b(caf[:7], qx, qy, sigma=qs_ / 3)
+        out['paf_mask_center_%d' % t] = F.paf_mask_center(caf[:7], qx, qy, sigma=qs_ / 3)
+    np.savez_compressed(os.path.join(HERE, 'primitives.npz'), **out)
+    print('primitives: %d arrays' % len(out))
+
+
+def gen_errors():
+    F = sys.modules['openpifpaf.functional']
+    errs = {}
+
+    def capture(name, fn):
+        try:
+            fn()
+            errs[name] = None
+        except Exception as e:  # pylint: disable=broad-except
+            errs[name] = [type(e).__name__, str(e)]
+
+    f32 = np.zeros((4, 4), np.float32)
+    p = np.zeros(2, np.float32)
+    capture('dtype', lambda: F.scalar_square_add_gauss_with_max(np.zeros((4, 4)), p, p, p, p))
+    ro = np.zeros((4, 4), np.float32)
+    ro.setflags(write=False)
+    capture('readonly', lambda: F.scalar_values(ro, p, p))
+    capture('ndim', lambda: F.scalar_values(np.zeros((2, 4, 4), np.float32), p, p))
+    capture('weiszfeld_none', lambda: F.weiszfeld_nd(np.zeros((3, 2), np.float32),
+                                                     np.zeros(2, np.float32)))
+    capture('ndim_points', lambda: F.scalar_values(f32, np.zeros((2, 2), np.float32), p))
+    with open(os.path.join(HERE, 'errors.json'), 'w') as fh:
+        json.dump(errs, fh, indent=1, sort_keys=True)
+    print('errors:', errs)
+
+
+def main():
+    op = ref_loader.load()
+    import Cython  # pylint: disable=import-outside-toplevel
+    meta = {
+        'reference': '/root/reference openpifpaf ' + op.__version__,
+        'numpy': np.__version__,
+        'cython': Cython.__version__,
+        'python': platform.python_version(),
+        'machine': platform.processor() or platform.machine(),
+        'numpy_simd': str(np.lib.introspect.opt_func_info(func_name='exp', signature='float32')
+                          if hasattr(np.lib, 'introspect') else ''),
+        'note': 'outputs of the reference decoder (functional.pyx built by oracle/build_ref.sh)',
+    }
+    with open(os.path.join(HERE, 'meta.json'), 'w') as fh:
+        json.dump(meta, fh, indent=1, sort_keys=True)
+    gen_primitives(op)
+    gen_errors()
+    only = sys.argv[1:]
+    for case in CASES:
+        if only and case[0] not in only:
+            continue
+        run_case(op, *case)
+
+
+if __name__ == '__main__':
+    main()

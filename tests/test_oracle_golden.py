@@ -1,0 +1,131 @@
+"""Pin the oracle (oracle/pp_oracle.c) against the reference's own outputs.
+
+The golden fixtures were produced by running the reference decoder
+(tests/golden/gen_golden.py).  Bit-exact for CifHr, seeds, CafScored and every
+functional primitive; tolerance (golden_util.ATOL/RTOL) for the grow-stage floats.
+"""
+import numpy as np
+import pytest
+
+import golden_util as gu
+import oracle
+
+
+@pytest.fixture(scope='module')
+def prim():
+    return gu.load_primitives()
+
+
+def _pts(p, key):
+    return [np.ascontiguousarray(r) for r in p[key]]
+
+
+@pytest.mark.parametrize('t', range(4))
+def test_add_gauss_with_max(prim, t):
+    field = prim['sqg_max_%d_in' % t].copy()
+    trunc, maxv = prim['sqg_max_%d_args' % t]
+    oracle.scalar_square_add_gauss_with_max(field, *_pts(prim, 'sqg_max_%d_pts' % t),
+                                            truncate=trunc, max_value=maxv)
+    assert np.array_equal(field, prim['sqg_max_%d_out' % t])
+
+
+def test_add_gauss_with_max_strided_and_empty(prim):
+    big = prim['sqg_max_strided_in'].copy()
+    oracle.scalar_square_add_gauss_with_max(big[::2, 1::2], *_pts(prim, 'sqg_max_strided_pts'),
+                                            truncate=1.0)
+    assert np.array_equal(big, prim['sqg_max_strided_out'])
+    field = prim['sqg_max_empty_in'].copy()
+    e = np.zeros(0, np.float32)
+    oracle.scalar_square_add_gauss_with_max(field, e, e, e, e)
+    assert np.array_equal(field, prim['sqg_max_empty_out'])
+
+
+@pytest.mark.parametrize('t', range(2))
+def test_add_gauss(prim, t):
+    field = prim['sqg_%d_in' % t].copy()
+    oracle.scalar_square_add_gauss(field, *_pts(prim, 'sqg_%d_pts' % t),
+                                   truncate=prim['sqg_%d_args' % t][0])
+    assert np.array_equal(field, prim['sqg_%d_out' % t])
+
+
+@pytest.mark.parametrize('t', range(2))
+def test_max_gauss(prim, t):
+    field = prim['sqmax_%d_in' % t].copy()
+    oracle.scalar_square_max_gauss(field, *_pts(prim, 'sqmax_%d_pts' % t),
+                                   truncate=prim['sqmax_%d_args' % t][0])
+    assert np.array_equal(field, prim['sqmax_%d_out' % t])
+
+
+def test_add_constant(prim):
+    field = prim['sqc_in'].copy()
+    oracle.scalar_square_add_constant(field, *_pts(prim, 'sqc_pts'))
+    assert np.array_equal(field, prim['sqc_out'])
+
+
+def test_cumulative_average(prim):
+    cuma, cumw = [a.copy() for a in prim['cuma_in']]
+    oracle.cumulative_average(cuma, cumw, *_pts(prim, 'cuma_pts'))
+    assert np.array_equal(np.stack([cuma, cumw]), prim['cuma_out'])
+
+
+@pytest.mark.parametrize('t', range(3))
+def test_weiszfeld(prim, t):
+    y = prim['weisz_%d_y0' % t].copy()
+    _, denom = oracle.weiszfeld_nd(prim['weisz_%d_x' % t], y, prim['weisz_%d_w' % t])
+    assert np.array_equal(y, prim['weisz_%d_y' % t])
+    assert np.array_equal(denom, prim['weisz_%d_denom' % t])
+
+
+def test_lookups(prim):
+    f = prim['lookup_field']
+    px, py = prim['lookup_pts']
+    assert np.array_equal(oracle.scalar_values(f, px, py), prim['scalar_values'])
+    assert np.array_equal(oracle.scalar_values(f, px, py, 0.0), prim['scalar_values_d0'])
+    assert np.array_equal(oracle.scalar_lookup(f, px, py, 0, -1.0), prim['scalar_value'])
+    assert np.array_equal(oracle.scalar_lookup(f, px, py, 1), prim['scalar_value_clipped'])
+    occ = prim['lookup_occ']
+    assert np.array_equal(oracle.scalar_lookup(occ, px, py, 2, 0), prim['scalar_nonzero'])
+    assert np.array_equal(oracle.scalar_lookup(occ, px, py, 3), prim['scalar_nonzero_clipped'])
+    assert np.array_equal(oracle.scalar_lookup(occ, 2 * px, 2 * py, 4, reduction=2.0),
+                          prim['scalar_nonzero_red'])
+
+
+def test_center_filters(prim):
+    caf = prim['center_field']
+    for t, (qx, qy, qs) in enumerate(prim['center_queries']):
+        assert np.array_equal(oracle.center_filter(caf, qx, qy, qs, 0), prim['caf_center_s_%d' % t])
+        assert np.array_equal(oracle.center_filter(caf[:7], qx, qy, qs, 1), prim['paf_center_%d' % t])
+        assert np.array_equal(oracle.center_filter(caf[:7], qx, qy, np.float32(qs / 3), 2),
+                              prim['paf_center_b_%d' % t])
+        assert np.array_equal(oracle.center_filter(caf[:7], qx, qy, np.float32(qs / 3), 3),
+                              prim['paf_mask_center_%d' % t])
+
+
+CASES = gu.case_names()
+FAST_CASES = [c for c in CASES if not c.startswith('u160')]
+
+
+@pytest.mark.parametrize('name', FAST_CASES)
+def test_stages(name):
+    g = gu.load_case(name)
+    cif, caf, skeleton = gu.case_inputs(g)
+    cfg = gu.case_config(g)
+    hr = oracle.cifhr(cif, cfg)
+    assert gu.sha(hr) == str(g['cifhr_sha'])
+    seeds = oracle.seeds(cif, hr, cfg)
+    assert np.array_equal(gu.seeds_as_rows(seeds), g['seeds'])
+    for tag, th in (('a', 0.1), ('b', 0.0001)):
+        fwd, bwd = oracle.caf_scored(caf, hr, skeleton, th, cfg)
+        assert [f.shape[1] for f in fwd] == list(g['caf_%s_fwd_counts' % tag])
+        assert [b.shape[1] for b in bwd] == list(g['caf_%s_bwd_counts' % tag])
+        assert [gu.sha(f) for f in fwd] == [str(s) for s in g['caf_%s_fwd_sha' % tag]]
+        assert [gu.sha(b) for b in bwd] == [str(s) for s in g['caf_%s_bwd_sha' % tag]]
+
+
+@pytest.mark.parametrize('name', CASES)
+def test_decode(name):
+    g = gu.load_case(name)
+    cif, caf, skeleton = gu.case_inputs(g)
+    recs = oracle.decode(cif, caf, skeleton, gu.case_config(g))
+    errs = gu.compare_annotations(g, recs)
+    assert not errs, errs[:10]
