@@ -1,0 +1,226 @@
+"""Benchmark: batched CIF/CAF decode on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg3|cfg2|cfg5]
+                    [--generator planted|uniform] [--mode eval|predict]
+
+One step = one full decode (CifHr -> seeds -> CafScored -> seed loop / grow ->
+force-complete -> NMS) of the rank's resident batch of synthetic fields, plus the device
+gather of the packed annotation records and their copy to the host; for N > 1 also the
+RCCL all-gather of every rank's records to rank 0 (weak scaling: each rank owns its own
+batch, no data-path collective).  Inputs are generated once and stay in HBM.
+
+Rank 0 prints ONE JSON line.  `roofline` is the CifHr stage (splat compaction + tile
+gather-fold kernels) measured with HIP events on the decode stream: algorithmic bytes =
+4*K*(5*H*W + H'*W') per image over the stage's event time.
+`cpu_baseline` is the oracle (oracle/pp_oracle.c, C restatement of the reference decoder)
+on one host core over a bounded sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+WORKLOADS = {
+    # BASELINE.json configs[2]: synthetic batch=256 at 80x80, full CifCaf, 1 GPU
+    'cfg3': dict(h=80, w=80, batch=256, skeleton='coco', n_people=8),
+    # configs[1]: batch 1, CifHr + seeds only
+    'cfg2': dict(h=80, w=80, batch=1, skeleton='coco', n_people=8, stages=3),
+    # configs[4]: 160x160, dense 44-CAF skeleton, 64 images per GPU
+    'cfg5': dict(h=160, w=160, batch=64, skeleton='dense', n_people=16),
+}
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=20)
+    p.add_argument('--warmup', type=int, default=3)
+    p.add_argument('--workload', default='cfg3', choices=sorted(WORKLOADS))
+    p.add_argument('--generator', default='planted', choices=('planted', 'uniform'))
+    p.add_argument('--mode', default='eval', choices=('eval', 'predict'))
+    p.add_argument('--batch', type=int, default=None, help='images per GPU (override)')
+    p.add_argument('--cpu-seconds', type=float, default=12.0,
+                   help='budget of the oracle CPU baseline sample (rank 0, N=1)')
+    p.add_argument('--no-cpu-baseline', action='store_true')
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device('cuda', local_rank)
+
+    from openpifpaf_amd import build as ppbuild
+    ppbuild.build(verbose=False)
+    from openpifpaf_amd import constants, synthetic
+    from openpifpaf_amd._abi import EVAL_CONFIG, PREDICT_CONFIG, make_config
+    from openpifpaf_amd.engine import (STAGE_CAF, STAGE_CIFHR, STAGE_GROW, STAGE_SEEDS,
+                                       DecodeEngine)
+
+    wl = dict(WORKLOADS[args.workload])
+    batch = args.batch or wl['batch']
+    h, w = wl['h'], wl['w']
+    skeleton = (constants.COCO_PERSON_SKELETON if wl['skeleton'] == 'coco'
+                else constants.DENSE_DECODE_SKELETON)
+    cfg = make_config(**(EVAL_CONFIG if args.mode == 'eval' else PREDICT_CONFIG))
+    gen_kw = {'n_caf': len(skeleton)} if args.generator == 'uniform' else {
+        'skeleton': skeleton, 'n_people': wl['n_people']}
+    cif_h, caf_h = synthetic.batch(args.generator, batch, h, w, first_seed=rank * batch, **gen_kw)
+    cif = torch.from_numpy(cif_h).to(dev)
+    caf = torch.from_numpy(caf_h).to(dev)
+    k = cif.shape[1]
+    stages = wl.get('stages', 15)
+
+    eng = DecodeEngine()
+    stream = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+    stage_ms = np.zeros(4)
+
+    def step(timed):
+        b = None
+        for si, bit in enumerate((STAGE_CIFHR, STAGE_SEEDS, STAGE_CAF, STAGE_GROW)):
+            if timed:
+                ev[si].record(stream)
+            if stages & bit:
+                b = eng.launch(cif, caf, skeleton, cfg, stages=bit)
+        if timed:
+            ev[4].record(stream)
+        recs = None
+        if stages & STAGE_GROW:
+            recs, _ = eng.fetch(b)  # packed records -> host (synchronises)
+            if world > 1:
+                recs = gather_records(recs, dist, dev)
+        if timed:
+            torch.cuda.synchronize()
+            for si in range(4):
+                stage_ms[si] += ev[si].elapsed_time(ev[si + 1])
+        return b, recs
+
+    for _ in range(args.warmup):
+        b, recs = step(False)
+    status = b.status.cpu().numpy()
+    if status.any():
+        raise SystemExit('decode status flags set: {}'.format(status[status != 0][:8]))
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n_anns = 0
+    for _ in range(args.steps):
+        b, recs = step(True)
+        n_anns += 0 if recs is None else len(recs)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    images = batch * world * args.steps
+    value = images / elapsed
+    ms_step = 1e3 * elapsed / args.steps
+    stage_avg = stage_ms / args.steps
+    hh, ww = (h - 1) * 8 + 1, (w - 1) * 8 + 1
+    cifhr_bytes = 4 * k * (5 * h * w + hh * ww) * batch
+    achieved = cifhr_bytes / (stage_avg[0] * 1e-3) / 1e9
+    line = {
+        'metric': 'decoder images/sec + ms/image, 17-CIF/19-CAF @80x80; CifHr HBM GB/s vs '
+                  'roofline',
+        'value': round(value, 1),
+        'unit': 'images/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': round(ms_step, 4),
+        'ms_per_image': round(ms_step / (batch * world), 6),
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'f32',
+        'data': 'synthetic ({} generator, fields resident in HBM)'.format(args.generator),
+        'config': {
+            'workload': '{}: {} images/GPU at {}x{}, 17 CIF / {} CAF, full CifCaf decode, {} '
+                        'defaults'.format(args.workload, batch, h, w, len(skeleton), args.mode),
+            'global_batch': batch * world,
+            'parallelism': 'image-sharded dp{} (RCCL all-gather of annotation records)'.format(
+                world) if world > 1 else 'single GPU',
+        },
+        'stage_ms': {'cifhr': round(stage_avg[0], 4), 'seeds': round(stage_avg[1], 4),
+                     'caf_scored': round(stage_avg[2], 4), 'grow_nms': round(stage_avg[3], 4)},
+        'annotations_per_image': round(n_anns / max(1, args.steps * batch * world), 3)
+        if stages & STAGE_GROW else None,
+        'roofline': {
+            'bound': 'hbm', 'kernel': 'cifhr (cifhr_splats_kernel + splat_tile_kernel)',
+            'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
+            'frac': round(achieved / PEAK_HBM_GBS, 4),
+            'algorithmic_bytes_per_launch': cifhr_bytes, 'traffic': None,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line['cpu_baseline'] = cpu_baseline(cif_h, caf_h, skeleton, cfg, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def gather_records(recs, dist, dev):
+    """All-gather every rank's packed pp_ann records (padded to the largest count)."""
+    import torch
+    from openpifpaf_amd._abi import ANN_DTYPE
+    world = dist.get_world_size()
+    n = torch.tensor([len(recs)], dtype=torch.int64, device=dev)
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(counts, n)
+    counts = [int(c.item()) for c in counts]
+    width = ANN_DTYPE.itemsize
+    cap = max(1, max(counts))
+    buf = torch.zeros((cap, width), dtype=torch.uint8, device=dev)
+    if len(recs):
+        buf[:len(recs)] = torch.from_numpy(recs.view(np.uint8).reshape(-1, width)).to(dev)
+    out = torch.empty((world * cap, width), dtype=torch.uint8, device=dev)
+    dist.all_gather_into_tensor(out, buf)
+    host = out.cpu().numpy()
+    parts = [host[r * cap:r * cap + counts[r]] for r in range(world)]
+    return np.frombuffer(np.concatenate(parts).tobytes(), dtype=ANN_DTYPE)
+
+
+def cpu_baseline(cif, caf, skeleton, cfg, budget_s):
+    """Oracle (C restatement of the reference decoder) on one core, bounded sample."""
+    sys.path.insert(0, os.path.join(REPO, 'oracle'))
+    import oracle  # pylint: disable=import-outside-toplevel
+    oracle.lib()
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        i = n % len(cif)
+        oracle.decode(cif[i], caf[i], skeleton, cfg)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {'value': round(n / dt, 2), 'unit': 'images/s', 'cores': 1, 'kind': 'port',
+            'sample': '{} single-image decodes (cycling over the first {} images of the '
+                      'batch) in {:.1f} s on one host core; oracle/pp_oracle.c'.format(
+                          n, min(n, len(cif)), dt),
+            'host_cpu_count': os.cpu_count()}
+
+
+if __name__ == '__main__':
+    main()

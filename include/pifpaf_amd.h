@@ -165,6 +165,23 @@ int pp_decode_batch(const float *d_cif, const float *d_caf, int32_t n_img, int32
                     int32_t ann_capacity, int32_t *d_counts, int32_t *d_status,
                     void *d_workspace, size_t workspace_bytes, void *stream);
 
+/*
+ * The same decode split into stages for measurement: bit 1 CifHr, 2 CifSeeds,
+ * 4 CafScored (both thresholds), 8 seed loop + grow + complete + NMS.  Stage buffers live
+ * in the workspace, so calling the stages in order with the same workspace equals one
+ * pp_decode_batch call.  pp_decode_batch == pp_decode_stages(..., 15, stream).
+ *
+ * Workspace contract: bytes [pp_decode_workspace_zero_offset(), end) must be zero before
+ * the first call (e.g. hipMemset once at allocation); every call leaves them zero again.
+ */
+int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int32_t K,
+                     int32_t C, int32_t H, int32_t W, const int32_t *skeleton,
+                     const pp_config *cfg, float *d_cifhr, pp_ann *d_anns,
+                     int32_t ann_capacity, int32_t *d_counts, int32_t *d_status,
+                     void *d_workspace, size_t workspace_bytes, uint32_t stages, void *stream);
+size_t pp_decode_workspace_zero_offset(int32_t n_img, int32_t K, int32_t C, int32_t H,
+                                       int32_t W, const pp_config *cfg, int32_t ann_capacity);
+
 /* ---------------------------------------------------------------------------------
  * openpifpaf.functional primitives (functional.pyx).  `field` arguments are
  * (h, w) float32 with row pitch `pitch` (elements).  Point lists are length-n device
@@ -218,6 +235,15 @@ int pp_scalar_lookup(const void *d_field, int64_t h, int64_t w, int64_t pitch, i
 int pp_center_filter(const float *d_field, int64_t rows, int64_t n, int64_t pitch, int32_t mode,
                      float x, float y, float sigma, void *d_out, int64_t out_pitch,
                      int32_t *d_count, void *stream);
+
+/*
+ * CifCaf._grow_connection + _target_with_blend / _target_with_maxscore
+ * (cifcaf.py:124-192; the north star's "grow_connection_blend") for one query point on a
+ * (9, n) column set with row pitch `pitch`.  method 0 blend, 1 max.  d_out = 4 floats
+ * (x, y, scale, score); all zero when no column lies in the 2*xy_scale box.
+ */
+int pp_grow_connection(const float *d_cols, int64_t n, int64_t pitch, float x, float y,
+                       float xy_scale, int32_t method, float *d_out, void *stream);
 
 #ifdef __cplusplus
 }

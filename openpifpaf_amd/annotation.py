@@ -1,0 +1,123 @@
+"""Output record of the decoder: same interface as openpifpaf/annotation.py:9-119."""
+import numpy as np
+
+NOTSET = '__notset__'
+
+
+class Annotation:
+    """One pose.  data (K, 3) float32 [x, y, v], joint_scales (K,) float32."""
+
+    def __init__(self, keypoints, skeleton, *, category_id=1, suppress_score_index=None):
+        self.keypoints = keypoints
+        self.skeleton = skeleton
+        self.category_id = category_id
+        self.suppress_score_index = suppress_score_index
+        k = len(keypoints)
+        self.data = np.zeros((k, 3), dtype=np.float32)
+        self.joint_scales = np.zeros((k,), dtype=np.float32)
+        self.fixed_score = NOTSET
+        self.decoding_order = []
+        self.frontier_order = []
+        self.skeleton_m1 = (np.asarray(skeleton) - 1).tolist()
+        # annotation.py:24-28: weight 3 for the first three joints, normalised in float64
+        w = np.ones((k,))
+        if suppress_score_index:
+            w[-1] = 0.0
+        w[:3] = 3.0
+        self.score_weights = w / np.sum(w)
+
+    @classmethod
+    def from_record(cls, rec, keypoints, skeleton):
+        """Build from one pp_ann record (include/pifpaf_amd.h)."""
+        k = len(keypoints)
+        ann = cls(keypoints, skeleton)
+        ann.data = np.array(rec['data'][:k], dtype=np.float32)
+        ann.joint_scales = np.array(rec['joint_scales'][:k], dtype=np.float32)
+        nd = int(rec['n_decoding'])
+        pairs = rec['decoding_pairs']
+        xyv = rec['decoding_xyv']
+        ann.decoding_order = [(int(pairs[t, 0]), int(pairs[t, 1]), xyv[t, :3].copy(),
+                               xyv[t, 3:].copy()) for t in range(min(nd, len(pairs)))]
+        fr = rec['frontier_pairs']
+        ann.frontier_order = [(int(fr[t, 0]), int(fr[t, 1]))
+                              for t in range(min(int(rec['n_frontier']), len(fr)))]
+        return ann
+
+    def add(self, joint_i, xyv):
+        self.data[joint_i] = xyv
+        return self
+
+    def set(self, data, joint_scales=None, *, fixed_score=NOTSET):
+        self.data = data
+        if joint_scales is not None:
+            self.joint_scales = joint_scales
+        else:
+            self.joint_scales[:] = 0.0
+        self.fixed_score = fixed_score
+        return self
+
+    def rescale(self, scale_factor):
+        self.data[:, 0:2] *= scale_factor
+        if self.joint_scales is not None:
+            self.joint_scales *= scale_factor
+        for _, __, c1, c2 in self.decoding_order:
+            c1[:2] *= scale_factor
+            c2[:2] *= scale_factor
+        return self
+
+    def fill_joint_scales(self, scales, hr_scale=1.0):
+        from .functional import scalar_value_clipped  # pylint: disable=import-outside-toplevel
+        self.joint_scales = np.zeros((self.data.shape[0],))
+        for i, xyv in enumerate(self.data):
+            if xyv[2] == 0.0:
+                continue
+            s = scalar_value_clipped(scales[i], xyv[0] * hr_scale, xyv[1] * hr_scale)
+            self.joint_scales[i] = s / hr_scale
+
+    def score(self):
+        """annotation.py:60-71: weighted sum of the sorted visibilities (float64)."""
+        if self.fixed_score != NOTSET:
+            return self.fixed_score
+        v = self.data[:, 2]
+        if self.suppress_score_index is not None:
+            v = np.copy(v)
+            v[self.suppress_score_index] = 0.0
+        return np.sum(self.score_weights * np.sort(v)[::-1])
+
+    def scale(self, v_th=0.5):
+        m = self.data[:, 2] > v_th
+        if not np.any(m):
+            return 0.0
+        return max(np.max(self.data[m, 0]) - np.min(self.data[m, 0]),
+                   np.max(self.data[m, 1]) - np.min(self.data[m, 1]))
+
+    def json_data(self):
+        """annotation.py:82-104: rounded to 2 decimals, visible keypoints kept >= 0.01."""
+        v_mask = self.data[:, 2] > 0.0
+        keypoints = np.copy(self.data)
+        keypoints[v_mask, 2] = np.maximum(0.01, keypoints[v_mask, 2])
+        keypoints = np.around(keypoints.astype(np.float64), 2)
+        data = {
+            'keypoints': keypoints.reshape(-1).tolist(),
+            'bbox': [round(float(c), 2) for c in self.bbox()],
+            'score': max(0.001, round(self.score(), 3)),
+            'category_id': self.category_id,
+        }
+        id_ = getattr(self, 'id_', None)
+        if id_:
+            data['id_'] = id_
+        return data
+
+    def bbox(self):
+        return self.bbox_from_keypoints(self.data, self.joint_scales)
+
+    @staticmethod
+    def bbox_from_keypoints(kps, joint_scales):
+        m = kps[:, 2] > 0
+        if not np.any(m):
+            return [0, 0, 0, 0]
+        x = np.min(kps[:, 0][m] - joint_scales[m])
+        y = np.min(kps[:, 1][m] - joint_scales[m])
+        w = np.max(kps[:, 0][m] + joint_scales[m]) - x
+        h = np.max(kps[:, 1][m] + joint_scales[m]) - y
+        return [x, y, w, h]

@@ -1,0 +1,168 @@
+// functional.hip — the remaining openpifpaf.functional primitives on gfx950:
+// point lookups (functional.pyx:231-286), the order-preserving column filters
+// caf_center_s / paf_center / paf_center_b / paf_mask_center (functional.pyx:214-228,
+// 289-359) and weiszfeld_nd (functional.pyx:172-211).  None of these is on the timed
+// decoder path in v0.11.6 except through the batched kernels; they exist so the
+// `functional` API is complete and bit-exact on device data.
+#include "pp_common.hpp"
+
+namespace pp {
+
+__global__ __launch_bounds__(256) void scalar_values_kernel(const float *__restrict__ f, int h,
+                                                            int w, int64_t pitch,
+                                                            const float *__restrict__ x,
+                                                            const float *__restrict__ y, int64_t n,
+                                                            float dflt, float *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    out[i] = hr_lookup(f, h, w, pitch, x[i], y[i], dflt);
+}
+
+// mode: 0 scalar_value, 1 scalar_value_clipped, 2 scalar_nonzero, 3 scalar_nonzero_clipped,
+//       4 scalar_nonzero_clipped_with_reduction
+__global__ __launch_bounds__(256) void scalar_lookup_kernel(const void *field, int h, int w,
+                                                            int64_t pitch, int mode,
+                                                            const float *__restrict__ xs,
+                                                            const float *__restrict__ ys,
+                                                            int64_t n, float dflt, float r,
+                                                            void *out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    float x = xs[i], y = ys[i];
+    const float maxx = (float)(w - 1), maxy = (float)(h - 1);
+    if (mode == 0 || mode == 2) {
+        const bool oob = x < 0.0f || y < 0.0f || x > maxx || y > maxy || x != x || y != y;
+        if (mode == 0) {
+            ((float *)out)[i] = oob ? dflt : ((const float *)field)[(int64_t)(int)y * pitch + (int)x];
+        } else {
+            ((uint8_t *)out)[i] =
+                oob ? (uint8_t)(int)dflt : ((const uint8_t *)field)[(int64_t)(int)y * pitch + (int)x];
+        }
+        return;
+    }
+    if (mode == 4) {
+        x = x / r;
+        y = y / r;
+    }
+    x = clip_ref(x, 0.0f, maxx);
+    y = clip_ref(y, 0.0f, maxy);
+    const int64_t at = (int64_t)(int)y * pitch + (int)x;
+    if (mode == 1)
+        ((float *)out)[i] = ((const float *)field)[at];
+    else
+        ((uint8_t *)out)[i] = ((const uint8_t *)field)[at];
+}
+
+// one workgroup, 1024 threads: order-preserving compaction of the kept columns
+__global__ __launch_bounds__(1024) void center_filter_kernel(const float *__restrict__ f, int rows,
+                                                             int64_t n, int64_t pitch, int mode,
+                                                             float x, float y, float sigma,
+                                                             void *out, int64_t out_pitch,
+                                                             int *count) {
+    __shared__ int s_tmp[16];
+    int64_t running = 0;
+    const float lo_x = x - sigma, hi_x = x + sigma, lo_y = y - sigma, hi_y = y + sigma;
+    for (int64_t base = 0; base < n; base += 1024) {
+        const int64_t i = base + threadIdx.x;
+        bool take = false;
+        if (i < n) {
+            const float r1 = f[pitch + i], r2 = f[2 * pitch + i];
+            if (mode == 0 || mode == 1) {
+                take = !(r1 < lo_x) && !(r1 > hi_x) && !(r2 < lo_y) && !(r2 > hi_y);
+            } else {
+                const float r3 = f[3 * pitch + i];
+                take = r1 > x - sigma * r3 && r1 < x + sigma * r3 && r2 > y - sigma * r3 &&
+                       r2 < y + sigma * r3;
+            }
+            if (mode == 3) ((uint8_t *)out)[i] = take ? 1 : 0;
+        }
+        int total;
+        const int slot = block_compact<16>(take, s_tmp, total);
+        if (mode != 3 && take) {
+            float *o = (float *)out;
+            for (int r = 0; r < rows; r++) o[r * out_pitch + running + slot] = f[r * pitch + i];
+        }
+        running += total;
+    }
+    if (threadIdx.x == 0 && count) *count = (int)(mode == 3 ? n : running);
+}
+
+// functional.pyx:172-211, sequential sums in the reference's order (one lane)
+__global__ void weiszfeld_kernel(const float *__restrict__ x, int64_t n, int64_t d, int64_t xp,
+                                 float *y, const float *__restrict__ wts, float eps,
+                                 int64_t max_steps, float *denom) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    float prev0, prev1;
+    for (int64_t s = 0; s < max_steps; s++) {
+        prev0 = y[0];
+        prev1 = y[1];
+        for (int64_t i = 0; i < n; i++) {
+            const float ax = x[i * xp] - prev0, ay = x[i * xp + 1] - prev1;
+            denom[i] = (float)(sqrt((double)(ax * ax + ay * ay)) + (double)eps);
+        }
+        float top0 = 0.0f, top1 = 0.0f, bottom = 0.0f;
+        for (int64_t j = 0; j < n; j++) {
+            const float w = wts[j];
+            top0 += (w * x[j * xp + 0]) / denom[j];  // weights_x[j, 0] / denom[j]
+            top1 += (w * x[j * xp + 1]) / denom[j];
+            bottom = bottom + w / denom[j];
+        }
+        y[0] = top0 / bottom;
+        y[1] = top1 / bottom;
+        if (fabs((double)(y[0] - prev0)) + fabs((double)(y[1] - prev1)) < 1e-2) return;
+    }
+}
+
+}  // namespace pp
+
+using namespace pp;
+
+extern "C" {
+
+int pp_scalar_values(const float *d_field, int64_t h, int64_t w, int64_t pitch, const float *d_x,
+                     const float *d_y, int64_t n, float default_value, float *d_out, void *stream) {
+    if (!d_field || (n > 0 && (!d_x || !d_y || !d_out))) return fail(PP_EINVAL, "pp_scalar_values: NULL argument");
+    if (h < 0 || w < 0 || pitch < w) return fail(PP_ESHAPE, "pp_scalar_values: bad field shape");
+    if (n <= 0) return PP_OK;
+    hipLaunchKernelGGL(scalar_values_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, d_field, (int)h, (int)w, pitch, d_x, d_y, n,
+                       default_value, d_out);
+    return check_launch("pp_scalar_values");
+}
+
+int pp_scalar_lookup(const void *d_field, int64_t h, int64_t w, int64_t pitch, int32_t mode,
+                     const float *d_x, const float *d_y, int64_t n, float default_value,
+                     float reduction, void *d_out, void *stream) {
+    if (!d_field || (n > 0 && (!d_x || !d_y || !d_out))) return fail(PP_EINVAL, "pp_scalar_lookup: NULL argument");
+    if (mode < 0 || mode > 4) return fail(PP_EINVAL, "pp_scalar_lookup: bad mode");
+    if (h <= 0 || w <= 0 || pitch < w) return fail(PP_ESHAPE, "pp_scalar_lookup: bad field shape");
+    if (n <= 0) return PP_OK;
+    hipLaunchKernelGGL(scalar_lookup_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, d_field, (int)h, (int)w, pitch, mode, d_x, d_y, n,
+                       default_value, reduction, d_out);
+    return check_launch("pp_scalar_lookup");
+}
+
+int pp_center_filter(const float *d_field, int64_t rows, int64_t n, int64_t pitch, int32_t mode,
+                     float x, float y, float sigma, void *d_out, int64_t out_pitch,
+                     int32_t *d_count, void *stream) {
+    if (!d_field || !d_out) return fail(PP_EINVAL, "pp_center_filter: NULL argument");
+    if (mode < 0 || mode > 3) return fail(PP_EINVAL, "pp_center_filter: bad mode");
+    if (rows < (mode >= 2 ? 4 : 3) || n < 0 || pitch < n)
+        return fail(PP_ESHAPE, "pp_center_filter: bad field shape");
+    hipLaunchKernelGGL(center_filter_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, d_field,
+                       (int)rows, n, pitch, mode, x, y, sigma, d_out, out_pitch, d_count);
+    return check_launch("pp_center_filter");
+}
+
+int pp_weiszfeld_nd(const float *d_x, int64_t n, int64_t d, int64_t x_pitch, float *d_y,
+                    const float *d_weights, float epsilon, int64_t max_steps, float *d_denom,
+                    void *stream) {
+    if (!d_x || !d_y || !d_weights || !d_denom) return fail(PP_EINVAL, "pp_weiszfeld_nd: NULL argument");
+    if (n < 0 || d < 2 || x_pitch < d) return fail(PP_ESHAPE, "pp_weiszfeld_nd: bad shape");
+    hipLaunchKernelGGL(weiszfeld_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, d_x, n, d,
+                       x_pitch, d_y, d_weights, epsilon, max_steps, d_denom);
+    return check_launch("pp_weiszfeld_nd");
+}
+
+}  // extern "C"

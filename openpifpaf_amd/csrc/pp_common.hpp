@@ -1,0 +1,93 @@
+// pp_common.hpp — shared device helpers for the gfx950 CIF/CAF decoder kernels.
+//
+// Numerics contract: every kernel is compiled with
+// -ffp-contract=off and IEEE-correct f32 division/sqrt (hipcc's default), so each float
+// op below rounds exactly like the reference's compiled Cython / NumPy float32 op.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "pifpaf_amd.h"
+
+namespace pp {
+
+constexpr int kWave = 64;
+
+// -------------------------------------------------------------------------------------
+// host-side error plumbing (thread-local message, pp_status codes)
+// -------------------------------------------------------------------------------------
+void set_error(const std::string &msg);
+int fail(int status, const std::string &msg);
+int check_launch(const char *what);
+
+inline int64_t hr_dim(int64_t n, int stride) { return (n - 1) * stride + 1; }
+
+// -------------------------------------------------------------------------------------
+// device helpers
+// -------------------------------------------------------------------------------------
+
+// functional.pyx:67-68 clip(): fmax(minv, fmin(maxv, v)); the double round trip of the
+// generated C is exact for float inputs, and NaN behaves the same (fmin/fmax drop NaN).
+__device__ __forceinline__ float clip_ref(float v, float minv, float maxv) {
+    return fmaxf(minv, fminf(maxv, v));
+}
+
+// functional.pyx:57-64 approx_exp.  (float)(1.0 + (double)x / 8.0) == fl32(1 + x*0.125f):
+// x/8 is exact and double rounding of a single add is innocuous (53 >= 2*24+2).
+__device__ __forceinline__ float approx_exp_ref(float x) {
+    if (x > 2.0f || x < -2.0f) return 0.0f;
+    x = 1.0f + x * 0.125f;
+    x = x * x;
+    x = x * x;
+    x = x * x;
+    return x;
+}
+
+// functional.pyx:231-244 scalar_values for one point (bounds inclusive of W'-1, truncation)
+__device__ __forceinline__ float hr_lookup(const float *field, int hh, int ww, int64_t pitch,
+                                           float x, float y, float dflt) {
+    const float maxx = (float)ww - 1.0f, maxy = (float)hh - 1.0f;
+    if (x < 0.0f || y < 0.0f || x > maxx || y > maxy) return dflt;
+    if (x != x || y != y) return dflt;  // NaN: the reference indexes with (Py_ssize_t)NaN (UB)
+    return field[(int64_t)(int)y * pitch + (int)x];
+}
+
+// count of set bits of `mask` below this lane (v_mbcnt)
+__device__ __forceinline__ int lane_prefix(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+// Order-preserving block compaction: returns this thread's slot among the flagged threads
+// of the block (threads in threadIdx order) and the block total.  `s_tmp` holds NW ints.
+template <int NW>
+__device__ __forceinline__ int block_compact(bool flag, int *s_tmp, int &total) {
+    const uint64_t m = __ballot(flag);
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) s_tmp[wave] = __popcll(m);
+    __syncthreads();
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        const int c = s_tmp[w];
+        off += (w < wave) ? c : 0;
+        tot += c;
+    }
+    __syncthreads();
+    total = tot;
+    return off + lane_prefix(m);
+}
+
+// XCD-aware remap: blocks b and b+8 land on one XCD (round-robin dispatch, speed only),
+// so consecutive work items of one XCD share its L2.  nblocks must be a multiple of 8.
+__device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nblocks) {
+    const int64_t per = nblocks >> 3;
+    return (b & 7) * per + (b >> 3);
+}
+
+}  // namespace pp

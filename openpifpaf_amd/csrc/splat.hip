@@ -1,0 +1,435 @@
+// splat.hip — CifHr accumulation and the square-splat primitives of functional.pyx on gfx950.
+//
+// Reference semantics: splats are folded into each pixel in
+// ascending splat order with a clamp after every add (functional.pyx:140-141), so float
+// atomics cannot be bit-exact.  The kernels here are a deterministic GATHER:
+//
+//   cifhr_splats_kernel  one workgroup per (image, CIF field): order-preserving ballot
+//                        compaction of the cells with c > v_threshold (cif_hr.py:27) into
+//                        splat records {box, cx, cy, v, sigma^2} (cif_hr.py:31-40).
+//   splat_tile_kernel    one workgroup per 64x64 output tile: gathers the splats whose box
+//                        intersects the tile into LDS (ballot compaction keeps splat
+//                        order), then every lane folds its 16 pixels over the candidate
+//                        list in ascending order in registers, and the tile is written
+//                        ONCE (fused zero-fill) with 16-B stores staged through LDS.
+//
+// Workgroups of one field run on one XCD (xcd_remap) so the field's splat list is served
+// from that XCD's L2.  Template MODE selects the functional.pyx primitive.
+#include "pp_common.hpp"
+
+namespace pp {
+
+struct Splat {
+    int4 box;    // minx, maxx, miny, maxy (functional.pyx:122-125 bounds, end-exclusive)
+    float4 par;  // cx, cy, v, sigma^2   (CUMAVG: cx, cy, v, w)
+};
+
+enum SplatMode { M_GAUSS_MAX = 0, M_GAUSS = 1, M_MAXG = 2, M_CONST = 3, M_CUMAVG = 4 };
+
+constexpr int kTile = 64;     // output tile edge (pixels)
+constexpr int kCand = 512;    // LDS candidate capacity per pass (>= 256 for progress)
+constexpr int kOutPad = 72;   // LDS staging row pitch (conflict-free ds_write_b32 columns)
+
+// Box of one splat.  ext = truncate*sigma (gauss modes) or width (const / cumavg).
+template <int MODE>
+__device__ __forceinline__ int4 splat_box(float cx, float cy, float ext, int h, int w) {
+    int4 b;
+    b.x = (int)clip_ref(cx - ext, 0.0f, (float)(w - 1));
+    float hx = cx + ext;
+    if (MODE == M_GAUSS_MAX) hx = hx + 1.0f;  // functional.pyx:123 `... + 1`
+    b.y = (int)clip_ref(hx, (float)(b.x + 1), (float)w);
+    b.z = (int)clip_ref(cy - ext, 0.0f, (float)(h - 1));
+    float hy = cy + ext;
+    if (MODE == M_GAUSS_MAX) hy = hy + 1.0f;
+    b.w = (int)clip_ref(hy, (float)(b.z + 1), (float)h);
+    return b;
+}
+
+// -------------------------------------------------------------------------------------
+// K1: CIF cells -> splat records (cif_hr.py:26-40)
+// -------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void cifhr_splats_kernel(const float *__restrict__ cif, int H,
+                                                           int W, int hh, int ww, float stride,
+                                                           float v_th, float neighbors,
+                                                           Splat *__restrict__ splats,
+                                                           int *__restrict__ counts) {
+    __shared__ int s_tmp[4];
+    const int64_t fld = blockIdx.x;  // image * K + field
+    const int hw = H * W;
+    const float *p = cif + fld * 5 * (int64_t)hw;
+    Splat *out = splats + fld * (int64_t)hw;
+    int running = 0;
+    for (int base = 0; base < hw; base += 256) {
+        const int cell = base + threadIdx.x;
+        float c = 0.0f;
+        if (cell < hw) c = p[cell];
+        const bool keep = (cell < hw) && (c > v_th);
+        int total;
+        const int slot = block_compact<4>(keep, s_tmp, total);
+        if (keep) {
+            const float x = p[hw + cell] * stride;
+            const float y = p[2 * hw + cell] * stride;
+            const float sg = (0.5f * p[4 * hw + cell]) * stride;
+            const float sigma = (sg != sg) ? sg : fmaxf(1.0f, sg);  // np.maximum keeps NaN
+            const float v = (c / neighbors) / 1.0f;                 // v / neighbors / len_cifs
+            Splat s;
+            s.box = splat_box<M_GAUSS_MAX>(x, y, 1.0f * sigma, hh, ww);
+            s.par = make_float4(x, y, v, sigma * sigma);
+            out[running + slot] = s;
+        }
+        running += total;
+    }
+    if (threadIdx.x == 0) counts[fld] = running;
+}
+
+// -------------------------------------------------------------------------------------
+// primitive prep: point lists -> splat records (functional.pyx argument order, no filter)
+// -------------------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(256) void prep_splats_kernel(const float *__restrict__ x,
+                                                          const float *__restrict__ y,
+                                                          const float *__restrict__ s,
+                                                          const float *__restrict__ v,
+                                                          const float *__restrict__ wt,
+                                                          int64_t n, int h, int w, float truncate,
+                                                          Splat *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float cx = x[i], cy = y[i], sv = s[i];
+    Splat r;
+    if (MODE == M_CONST || MODE == M_CUMAVG) {
+        r.box = splat_box<MODE>(cx, cy, sv, h, w);
+        float cw = (MODE == M_CUMAVG) ? wt[i] : 0.0f;
+        if (MODE == M_CUMAVG && cw <= 0.0f) r.box = make_int4(0, 0, 0, 0);  // `continue`
+        r.par = make_float4(cx, cy, v[i], cw);
+    } else {
+        r.box = splat_box<MODE>(cx, cy, truncate * sv, h, w);
+        r.par = make_float4(cx, cy, v[i], sv * sv);
+    }
+    out[i] = r;
+}
+
+// -------------------------------------------------------------------------------------
+// K2: tile gather-fold
+// -------------------------------------------------------------------------------------
+struct TileArgs {
+    float *field;           // (n_fields, h, pitch), fields back to back
+    float *field2;          // cumw for M_CUMAVG
+    const Splat *splats;    // n_fields * splat_cap
+    const int *counts;      // per field splat count (NULL: n_splats)
+    int64_t splat_cap;
+    int64_t n_splats;
+    int64_t field_stride;   // elements between fields
+    int h, w, pitch;
+    int tiles_x, tiles;     // tiles per field
+    int64_t n_work;         // n_fields * tiles
+    float t2;               // truncate^2 (M_GAUSS_MAX circle test)
+    float max_value;
+};
+
+template <int MODE>
+__device__ __forceinline__ void fold_pixel(float &acc, float &acc2, bool in, float px, float py,
+                                           const float4 &par, float t2s2, float maxv) {
+    if (MODE == M_CONST) {
+        if (in) acc = acc + par.z;
+        return;
+    }
+    if (MODE == M_CUMAVG) {
+        if (in) {
+            const float cw = par.w, cv = par.z;
+            acc = (cw * cv + acc2 * acc) / (acc2 + cw);  // functional.pyx:53 (cdivision)
+            acc2 = acc2 + cw;
+        }
+        return;
+    }
+    const float dx = px - par.x, dy = py - par.y;
+    const float dx2 = dx * dx, dy2 = dy * dy;  // powf(d, 2.0)
+    const float sum = dx2 + dy2;
+    if (MODE == M_GAUSS_MAX) in = in && !(sum > t2s2);
+    if (!in) return;
+    float vv;
+    if (MODE != M_MAXG && dx2 < 0.25f && dy2 < 0.25f)
+        vv = par.z;  // "closest pixel"
+    else
+        vv = par.z * approx_exp_ref((-0.5f * sum) / par.w);
+    if (MODE == M_GAUSS_MAX) {
+        acc = acc + vv;
+        acc = (acc < maxv) ? acc : maxv;  // min(max_value, f) as emitted by Cython
+    } else if (MODE == M_GAUSS) {
+        acc = acc + vv;
+    } else {
+        acc = fmaxf(acc, vv);  // (float)fmax((double)f, (double)vv)
+    }
+}
+
+template <int MODE, bool ZERO_INIT>
+__global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
+    __shared__ int4 s_box[kCand];
+    __shared__ float4 s_par[kCand];
+    __shared__ int s_tmp[4];
+    __shared__ __attribute__((aligned(16))) float s_out[ZERO_INIT ? kTile * kOutPad : 4];
+
+    const int64_t wid = xcd_remap(blockIdx.x, gridDim.x);
+    if (wid >= a.n_work) return;
+    const int tile = (int)(wid % a.tiles);
+    const int64_t fld = wid / a.tiles;
+    const int tx0 = (tile % a.tiles_x) * kTile;
+    const int ty0 = (tile / a.tiles_x) * kTile;
+    const Splat *sp = a.splats + fld * a.splat_cap;
+    const int64_t ns = a.counts ? (int64_t)a.counts[fld] : a.n_splats;
+    float *out = a.field + fld * a.field_stride;
+    float *out2 = (MODE == M_CUMAVG) ? a.field2 + fld * a.field_stride : nullptr;
+
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int lx = lane & 7, ly = lane >> 3;
+    const int wx0 = tx0, wy0 = ty0 + wave * 16;
+
+    float acc[16], acc2[16];
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        acc[r] = 0.0f;
+        acc2[r] = 0.0f;
+        if (!ZERO_INIT) {
+            const int px = wx0 + (r & 7) * 8 + lx, py = wy0 + (r >> 3) * 8 + ly;
+            if (px < a.w && py < a.h) {
+                acc[r] = out[(int64_t)py * a.pitch + px];
+                if (MODE == M_CUMAVG) acc2[r] = out2[(int64_t)py * a.pitch + px];
+            }
+        }
+    }
+
+    bool any = false;
+    int64_t cursor = 0;
+    while (cursor < ns) {
+        // ---- gather: splats intersecting this tile, in splat order, into LDS ----
+        int n = 0;
+        while (cursor < ns) {
+            const int64_t i = cursor + threadIdx.x;
+            bool hit = false;
+            int4 b = make_int4(0, 0, 0, 0);
+            if (i < ns) {
+                b = sp[i].box;
+                hit = b.y > tx0 && b.x < tx0 + kTile && b.w > ty0 && b.z < ty0 + kTile;
+            }
+            int total;
+            const int slot = block_compact<4>(hit, s_tmp, total);
+            if (n + total > kCand) break;  // block-uniform; chunk re-read next pass
+            if (hit) {
+                s_box[n + slot] = b;
+                s_par[n + slot] = sp[i].par;
+            }
+            n += total;
+            cursor += 256;
+        }
+        __syncthreads();
+        any = any || n > 0;
+        // ---- fold: per pixel, ascending candidate order ----
+        for (int c = 0; c < n; c++) {
+            const int bx0 = __builtin_amdgcn_readfirstlane(s_box[c].x);
+            const int bx1 = __builtin_amdgcn_readfirstlane(s_box[c].y);
+            const int by0 = __builtin_amdgcn_readfirstlane(s_box[c].z);
+            const int by1 = __builtin_amdgcn_readfirstlane(s_box[c].w);
+            if (bx1 <= wx0 || bx0 >= wx0 + kTile || by1 <= wy0 || by0 >= wy0 + 16) continue;
+            const float4 par = s_par[c];
+            const float t2s2 = a.t2 * par.w;
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int rx0 = wx0 + (r & 7) * 8, ry0 = wy0 + (r >> 3) * 8;
+                if (bx1 <= rx0 || bx0 >= rx0 + 8 || by1 <= ry0 || by0 >= ry0 + 8) continue;
+                const int px = rx0 + lx, py = ry0 + ly;
+                const bool in = px >= bx0 && px < bx1 && py >= by0 && py < by1;
+                fold_pixel<MODE>(acc[r], acc2[r], in, (float)px, (float)py, par, t2s2,
+                                 a.max_value);
+            }
+        }
+        __syncthreads();
+    }
+
+    if (ZERO_INIT) {
+        // ---- write the tile once: 16-B stores, rows of 256 B ----
+        if (any) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int row = wave * 16 + (r >> 3) * 8 + ly, col = (r & 7) * 8 + lx;
+                s_out[row * kOutPad + col] = acc[r];
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int q = k * 256 + threadIdx.x;  // float4 index in the tile
+            const int row = q >> 4, c4 = (q & 15) * 4;
+            const int gy = ty0 + row, gx = tx0 + c4;
+            if (gy < a.h && gx < a.pitch) {
+                float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (any) v = *reinterpret_cast<const float4 *>(&s_out[row * kOutPad + c4]);
+                *reinterpret_cast<float4 *>(&out[(int64_t)gy * a.pitch + gx]) = v;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const int px = wx0 + (r & 7) * 8 + lx, py = wy0 + (r >> 3) * 8 + ly;
+            if (px < a.w && py < a.h) {
+                out[(int64_t)py * a.pitch + px] = acc[r];
+                if (MODE == M_CUMAVG) out2[(int64_t)py * a.pitch + px] = acc2[r];
+            }
+        }
+    }
+}
+
+// -------------------------------------------------------------------------------------
+// host launchers
+// -------------------------------------------------------------------------------------
+static inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
+
+template <int MODE, bool ZERO_INIT>
+static void launch_tiles(TileArgs a, hipStream_t stream) {
+    a.tiles_x = (int)((a.pitch + kTile - 1) / kTile);
+    if (!ZERO_INIT) a.tiles_x = (a.w + kTile - 1) / kTile;
+    const int tiles_y = (a.h + kTile - 1) / kTile;
+    a.tiles = a.tiles_x * tiles_y;
+    const int64_t n_fields = a.n_work;  // caller passes the field count here
+    a.n_work = n_fields * a.tiles;
+    const int64_t nblocks = round_up(a.n_work, 8);
+    hipLaunchKernelGGL((splat_tile_kernel<MODE, ZERO_INIT>), dim3((unsigned)nblocks), dim3(256), 0,
+                       stream, a);
+}
+
+}  // namespace pp
+
+using namespace pp;
+
+extern "C" {
+
+int64_t pp_cifhr_pitch(int64_t w_hr) { return round_up(w_hr, 32); }
+
+size_t pp_cifhr_workspace_size(int32_t n_img, int32_t K, int32_t H, int32_t W) {
+    const size_t nf = (size_t)n_img * K;
+    return round_up((int64_t)(nf * (size_t)H * W * sizeof(Splat)), 256) +
+           round_up((int64_t)(nf * sizeof(int)), 256);
+}
+
+int pp_cifhr(const float *d_cif, int32_t n_img, int32_t K, int32_t H, int32_t W,
+             const pp_config *cfg, float *d_cifhr, void *d_workspace, size_t workspace_bytes,
+             void *stream) {
+    if (!d_cif || !cfg || !d_cifhr || !d_workspace) return fail(PP_EINVAL, "pp_cifhr: NULL argument");
+    if (n_img < 0 || K <= 0 || H <= 0 || W <= 0 || cfg->stride <= 0)
+        return fail(PP_ESHAPE, "pp_cifhr: bad shape");
+    if (n_img == 0) return PP_OK;
+    if (workspace_bytes < pp_cifhr_workspace_size(n_img, K, H, W))
+        return fail(PP_ENOMEM, "pp_cifhr: workspace too small");
+    const int hh = (int)hr_dim(H, cfg->stride), ww = (int)hr_dim(W, cfg->stride);
+    const int64_t pitch = pp_cifhr_pitch(ww);
+    const int64_t nf = (int64_t)n_img * K;
+    Splat *splats = (Splat *)d_workspace;
+    int *counts = (int *)((char *)d_workspace +
+                          round_up((int64_t)(nf * (int64_t)H * W * sizeof(Splat)), 256));
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(cifhr_splats_kernel, dim3((unsigned)nf), dim3(256), 0, s, d_cif, H, W, hh,
+                       ww, (float)cfg->stride, cfg->cif_threshold, (float)cfg->cif_neighbors,
+                       splats, counts);
+    TileArgs a{};
+    a.field = d_cifhr;
+    a.splats = splats;
+    a.counts = counts;
+    a.splat_cap = (int64_t)H * W;
+    a.field_stride = (int64_t)hh * pitch;
+    a.h = hh;
+    a.w = ww;
+    a.pitch = (int)pitch;
+    a.n_work = nf;
+    a.t2 = 1.0f;  // truncate = 1.0 (cif_hr.py:40)
+    a.max_value = 1.0f;
+    launch_tiles<M_GAUSS_MAX, true>(a, s);
+    return check_launch("pp_cifhr");
+}
+
+}  // extern "C"
+
+// ---- functional.pyx square-splat primitives (in place on one (h, w) field) ----
+namespace pp {
+
+template <int MODE>
+static int run_square_primitive(float *field, float *field2, int64_t h, int64_t w, int64_t pitch,
+                                const float *x, const float *y, const float *s, const float *v,
+                                const float *wt, int64_t n, float truncate, float max_value,
+                                void *stream, const char *name) {
+    if (!field || (n > 0 && (!x || !y || !s || !v))) return fail(PP_EINVAL, std::string(name) + ": NULL argument");
+    if (h <= 0 || w <= 0 || pitch < w || h > (1 << 30) || w > (1 << 30))
+        return fail(PP_ESHAPE, std::string(name) + ": bad field shape");
+    if (n <= 0) return PP_OK;
+    hipStream_t st = (hipStream_t)stream;
+    Splat *splats = nullptr;
+    if (hipMallocAsync((void **)&splats, (size_t)n * sizeof(Splat), st) != hipSuccess)
+        return fail(PP_EHIP, std::string(name) + ": scratch allocation failed");
+    const int64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL((prep_splats_kernel<MODE>), dim3((unsigned)blocks), dim3(256), 0, st, x, y,
+                       s, v, wt, n, (int)h, (int)w, truncate, splats);
+    TileArgs a{};
+    a.field = field;
+    a.field2 = field2;
+    a.splats = splats;
+    a.counts = nullptr;
+    a.n_splats = n;
+    a.splat_cap = n;
+    a.field_stride = h * pitch;
+    a.h = (int)h;
+    a.w = (int)w;
+    a.pitch = (int)pitch;
+    a.n_work = 1;
+    a.t2 = truncate * truncate;
+    a.max_value = max_value;
+    launch_tiles<MODE, false>(a, st);
+    int rc = check_launch(name);
+    hipFreeAsync(splats, st);
+    return rc;
+}
+
+}  // namespace pp
+
+extern "C" {
+
+int pp_scalar_square_add_gauss_with_max(float *d_field, int64_t h, int64_t w, int64_t pitch,
+                                        const float *d_x, const float *d_y, const float *d_sigma,
+                                        const float *d_v, int64_t n, float truncate,
+                                        float max_value, void *stream) {
+    return run_square_primitive<M_GAUSS_MAX>(d_field, nullptr, h, w, pitch, d_x, d_y, d_sigma, d_v,
+                                             nullptr, n, truncate, max_value, stream,
+                                             "pp_scalar_square_add_gauss_with_max");
+}
+
+int pp_scalar_square_add_gauss(float *d_field, int64_t h, int64_t w, int64_t pitch,
+                               const float *d_x, const float *d_y, const float *d_sigma,
+                               const float *d_v, int64_t n, float truncate, void *stream) {
+    return run_square_primitive<M_GAUSS>(d_field, nullptr, h, w, pitch, d_x, d_y, d_sigma, d_v,
+                                         nullptr, n, truncate, 0.0f, stream,
+                                         "pp_scalar_square_add_gauss");
+}
+
+int pp_scalar_square_max_gauss(float *d_field, int64_t h, int64_t w, int64_t pitch,
+                               const float *d_x, const float *d_y, const float *d_sigma,
+                               const float *d_v, int64_t n, float truncate, void *stream) {
+    return run_square_primitive<M_MAXG>(d_field, nullptr, h, w, pitch, d_x, d_y, d_sigma, d_v,
+                                        nullptr, n, truncate, 0.0f, stream,
+                                        "pp_scalar_square_max_gauss");
+}
+
+int pp_scalar_square_add_constant(float *d_field, int64_t h, int64_t w, int64_t pitch,
+                                  const float *d_x, const float *d_y, const float *d_width,
+                                  const float *d_v, int64_t n, void *stream) {
+    return run_square_primitive<M_CONST>(d_field, nullptr, h, w, pitch, d_x, d_y, d_width, d_v,
+                                         nullptr, n, 0.0f, 0.0f, stream,
+                                         "pp_scalar_square_add_constant");
+}
+
+int pp_cumulative_average(float *d_cuma, float *d_cumw, int64_t h, int64_t w, int64_t pitch,
+                          const float *d_x, const float *d_y, const float *d_width,
+                          const float *d_v, const float *d_w, int64_t n, void *stream) {
+    if (!d_cumw || (n > 0 && !d_w)) return fail(PP_EINVAL, "pp_cumulative_average: NULL argument");
+    return run_square_primitive<M_CUMAVG>(d_cuma, d_cumw, h, w, pitch, d_x, d_y, d_width, d_v, d_w,
+                                          n, 0.0f, 0.0f, stream, "pp_cumulative_average");
+}
+
+}  // extern "C"

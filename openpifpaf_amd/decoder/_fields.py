@@ -1,0 +1,39 @@
+"""Shared plumbing of the single-image stage classes: field tensors and the pitched
+high-resolution CIF layout (n, K, H', pitch) the kernels use."""
+import ctypes
+
+import torch
+
+from .. import _device
+from .._lib import load
+
+
+def hr_geometry(h, w, stride):
+    hh = (h - 1) * stride + 1
+    ww = (w - 1) * stride + 1
+    return hh, ww, int(load().pp_cifhr_pitch(ww))
+
+
+def batch1(field):
+    """(1, ...) contiguous float32 device tensor of one image's field."""
+    return _device.to_device(field)[None]
+
+
+def pitched_hr(cifhr, stride_unused=None):
+    """CifHr map as a (1, K, H', pitch) device tensor.  Views of a decoder-made map are
+    used in place; other arrays are copied into a fresh pitched buffer."""
+    k, hh, ww = cifhr.shape
+    pitch = int(load().pp_cifhr_pitch(ww))
+    if (_device.is_device(cifhr) and cifhr.dtype == torch.float32
+            and tuple(cifhr.stride()) == (hh * pitch, pitch, 1)):
+        base = cifhr.storage_offset()
+        if cifhr.untyped_storage().nbytes() >= 4 * (base + k * hh * pitch):
+            return torch.as_strided(cifhr, (1, k, hh, pitch), (k * hh * pitch, hh * pitch, pitch, 1))
+    dev = _device.require()
+    out = torch.zeros((1, k, hh, pitch), dtype=torch.float32, device=dev)
+    out[0, :, :, :ww] = _device.to_device(cifhr)
+    return out
+
+
+def cfg_ptr(cfg):
+    return ctypes.byref(cfg)

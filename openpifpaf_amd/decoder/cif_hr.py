@@ -1,0 +1,69 @@
+"""CifHr: the high-resolution CIF confidence map (cif_hr.py:14-81) on gfx950.
+
+`fill(fields)` runs pp_cifhr (splat compaction + LDS-tiled gather-fold, bit-exact with
+scalar_square_add_gauss_with_max in ascending splat order).  `.accumulated` is a NumPy
+(K, H', W') array for host inputs, a device tensor view for device inputs.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from .. import _device
+from .._abi import make_config
+from .._lib import call, load
+from ..functional import scalar_square_add_gauss_with_max
+from ._fields import batch1, hr_geometry
+from .field_config import FieldConfig
+
+
+def cifhr_device(cif, stride, v_threshold, neighbors):
+    """cif (n, K, 5, H, W) device tensor -> (n, K, H', pitch) device tensor."""
+    n, k, _, h, w = cif.shape
+    hh, _, pitch = hr_geometry(h, w, stride)
+    lib = load()
+    out = torch.empty((n, k, hh, pitch), dtype=torch.float32, device=cif.device)
+    ws = torch.empty(lib.pp_cifhr_workspace_size(n, k, h, w), dtype=torch.uint8,
+                     device=cif.device)
+    cfg = make_config(cif_threshold=v_threshold, stride=stride, cif_neighbors=neighbors)
+    call('pp_cifhr', _device.ptr(cif), n, k, h, w, ctypes.byref(cfg), _device.ptr(out),
+         _device.ptr(ws), ctypes.c_size_t(ws.numel()), _device.stream())
+    return out
+
+
+class CifHr:
+    neighbors = 16
+    v_threshold = 0.1
+
+    def __init__(self, config: FieldConfig):
+        self.config = config
+        self.accumulated = None
+
+    def accumulate(self, len_cifs, t, p, stride, min_scale):
+        """cif_hr.py:26-40, for one field p (5, H, W) into t (H', W') in place."""
+        p = p[:, p[0] > self.v_threshold]
+        if min_scale:
+            p = p[:, p[4] > min_scale / stride]
+        v, x, y, _, scale = p
+        x = x * stride
+        y = y * stride
+        sigma = np.maximum(1.0, 0.5 * scale * stride)
+        scalar_square_add_gauss_with_max(t, x, y, sigma, v / self.neighbors / len_cifs,
+                                         truncate=1.0)
+
+    def fill_cif(self, cif, stride, min_scale=0.0):
+        if min_scale:
+            raise NotImplementedError('min_scale masks (multi-scale) are not implemented')
+        if self.accumulated is not None:
+            raise NotImplementedError('accumulating several CIF heads (multi-scale) is not '
+                                      'implemented on the device decoder')
+        hr = cifhr_device(batch1(cif), int(stride), self.v_threshold, self.neighbors)
+        ww = (cif.shape[3] - 1) * int(stride) + 1
+        acc = hr[0, :, :, :ww]
+        self.accumulated = acc if _device.is_device(cif) else np.ascontiguousarray(
+            acc.cpu().numpy())
+        return self
+
+    def fill(self, fields):
+        cif_i, _, stride = self.config.single_scale()
+        return self.fill_cif(fields[cif_i], stride)

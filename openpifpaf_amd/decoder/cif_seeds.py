@@ -1,0 +1,51 @@
+"""CifSeeds (cif_seeds.py:13-64) on gfx950: threshold, CifHr rescore, ballot compaction
+and the sorted(seeds, reverse=True) order, all in one kernel per image (pp_seeds)."""
+import numpy as np
+import torch
+
+from .. import _device
+from .._abi import SEED_DTYPE, make_config
+from .._lib import call
+from ._fields import batch1, cfg_ptr, pitched_hr
+from .field_config import FieldConfig
+
+
+class CifSeeds:
+    threshold = None
+    score_scale = 1.0
+
+    def __init__(self, cifhr, config: FieldConfig):
+        self.cifhr = cifhr
+        self.config = config
+        self.seeds = []
+
+    def fill_cif(self, cif, stride, *, min_scale=0.0, seed_mask=None):
+        if self.threshold is None:
+            raise TypeError("'>' not supported between instances of 'numpy.ndarray' and "
+                            "'NoneType' (CifSeeds.threshold is not configured)")
+        if min_scale or seed_mask is not None:
+            raise NotImplementedError('min_scale / seed_mask are not implemented')
+        c = batch1(cif)
+        _, k, _, h, w = c.shape
+        hr = pitched_hr(self.cifhr)
+        cap = k * h * w
+        out = torch.empty(cap * SEED_DTYPE.itemsize, dtype=torch.uint8, device=c.device)
+        count = torch.zeros(1, dtype=torch.int32, device=c.device)
+        cfg = make_config(seed_threshold=self.threshold, seed_score_scale=self.score_scale,
+                          stride=int(stride))
+        call('pp_seeds', _device.ptr(c), _device.ptr(hr), 1, k, h, w, cfg_ptr(cfg),
+             _device.ptr(out), cap, _device.ptr(count), _device.stream())
+        n = int(count.item())
+        recs = np.frombuffer(out[:n * SEED_DTYPE.itemsize].cpu().numpy().tobytes(),
+                             dtype=SEED_DTYPE)
+        self.seeds.extend((v, int(f), x, y, s) for v, f, x, y, s in
+                          zip(recs['v'], recs['field'], recs['x'], recs['y'], recs['s']))
+        return self
+
+    def get(self):
+        """cif_seeds.py:52-54 (the kernel already emits this order)."""
+        return sorted(self.seeds, reverse=True)
+
+    def fill(self, fields):
+        cif_i, _, stride = self.config.single_scale()
+        return self.fill_cif(fields[cif_i], stride, seed_mask=self.config.seed_mask)

@@ -1,0 +1,127 @@
+"""CifCaf greedy pose decoder (decoder/generator/cifcaf.py:24-351) on gfx950.
+
+Same constructor, class attributes and call signature as the reference.  One call runs the
+whole per-image pipeline on the device (engine.DecodeEngine -> pp_decode_stages):
+CifHr -> CifSeeds -> CafScored (both thresholds) -> seed loop with occupancy and the
+frontier grow -> complete_annotations / flood fill -> nms.Keypoints, and returns
+Annotation objects.  `decode_batch` decodes a whole (B, ...) batch of device fields in
+one launch sequence, which is how `batch()` (generator.py:84-101) is served.
+"""
+from collections import defaultdict
+import logging
+import time
+
+import numpy as np
+
+from ... import _device
+from ..._abi import make_config, skeleton_array
+from ...annotation import Annotation
+from ...engine import engine
+from ...functional import grow_connection_blend
+from .. import nms as nms_module
+from ..caf_scored import CafScored
+from ..cif_hr import CifHr
+from ..cif_seeds import CifSeeds
+from ..field_config import FieldConfig
+from .generator import Generator
+
+LOG = logging.getLogger(__name__)
+
+
+class CifCaf(Generator):
+    """Generate CifCaf poses from fields.
+
+    :param: nms: set to None to switch off non-maximum suppression.
+    """
+    connection_method = 'blend'
+    force_complete = False
+    greedy = False
+    keypoint_threshold = 0.0
+
+    def __init__(self, field_config: FieldConfig, *, keypoints, skeleton, out_skeleton=None,
+                 confidence_scales=None, worker_pool=None, nms=True):
+        super().__init__(worker_pool)
+        if nms is True:
+            nms = nms_module.Keypoints()
+        if nms is not None and not isinstance(nms, nms_module.Keypoints):
+            raise NotImplementedError('only nms.Keypoints runs inside the device decode')
+        if confidence_scales is not None:
+            raise NotImplementedError('confidence_scales (dense coupling) is not implemented; '
+                                      'factory_decode never passes it (factory.py:184-211)')
+        self.field_config = field_config
+        self.keypoints = keypoints
+        self.skeleton = skeleton
+        self.skeleton_m1 = np.asarray(skeleton) - 1
+        self.out_skeleton = out_skeleton or skeleton
+        self.confidence_scales = confidence_scales
+        self.nms = nms
+        self.timers = defaultdict(float)
+        # cifcaf.py:57-65 (kept for API parity; the kernel builds the same tables)
+        self.by_target = defaultdict(dict)
+        for caf_i, (j1, j2) in enumerate(self.skeleton_m1):
+            self.by_target[j2][j1] = (caf_i, True)
+            self.by_target[j1][j2] = (caf_i, False)
+        self.by_source = defaultdict(dict)
+        for caf_i, (j1, j2) in enumerate(self.skeleton_m1):
+            self.by_source[j1][j2] = (caf_i, True)
+            self.by_source[j2][j1] = (caf_i, False)
+
+    # -- configuration -------------------------------------------------------------------
+    def config(self):
+        """pp_config from the class attributes decoder.configure() writes (factory.py:64-98)."""
+        _, _, stride = self.field_config.single_scale()
+        if CifSeeds.threshold is None:
+            raise TypeError('CifSeeds.threshold is not configured (decoder.configure sets it)')
+        nms = self.nms
+        return make_config(
+            cif_threshold=CifHr.v_threshold,
+            seed_threshold=CifSeeds.threshold,
+            seed_score_scale=CifSeeds.score_scale,
+            caf_threshold=CafScored.default_score_th,
+            complete_caf_threshold=0.0001,
+            keypoint_threshold=self.keypoint_threshold,
+            nms_keypoint_threshold=nms.keypoint_threshold if nms else 0.0,
+            nms_instance_threshold=nms.instance_threshold if nms else 0.0,
+            nms_suppression=nms.suppression if nms else 0.0,
+            stride=stride,
+            cif_neighbors=CifHr.neighbors,
+            force_complete=self.force_complete,
+            greedy=self.greedy,
+            connection_method=self.connection_method,
+            apply_nms=nms is not None,
+        )
+
+    # -- decoding ------------------------------------------------------------------------
+    def __call__(self, fields, initial_annotations=None):
+        """One image: fields = [cif (K, 5, H, W), caf (C, 9, H, W)] (numpy or device)."""
+        if initial_annotations:
+            raise NotImplementedError('initial_annotations are not implemented on the device')
+        cif_i, caf_i, _ = self.field_config.single_scale()
+        start = time.perf_counter()
+        anns = self.decode_batch(_device.to_device(fields[cif_i])[None],
+                                 _device.to_device(fields[caf_i])[None])[0]
+        LOG.debug('%d annotations, %.3fs', len(anns), time.perf_counter() - start)
+        return anns
+
+    def decode_records(self, cif_batch, caf_batch, keep_cifhr=False):
+        """Device decode of a batch -> (packed pp_ann records, per-image offsets, buffers)."""
+        cif = _device.to_device(cif_batch)
+        caf = _device.to_device(caf_batch)
+        return engine().decode(cif, caf, skeleton_array(self.skeleton), self.config(),
+                               keep_cifhr=keep_cifhr)
+
+    def decode_batch(self, cif_batch, caf_batch):
+        """(B, K, 5, H, W) + (B, C, 9, H, W) -> one list of Annotation per image."""
+        recs, offsets, _ = self.decode_records(cif_batch, caf_batch)
+        out = []
+        for i in range(len(offsets) - 1):
+            out.append([Annotation.from_record(r, self.keypoints, self.out_skeleton)
+                        for r in recs[offsets[i]:offsets[i + 1]]])
+        return out
+
+    # -- reference building blocks, on the device ------------------------------------------
+    def _grow_connection(self, xy, xy_scale, caf_field):
+        assert len(xy) == 2
+        assert caf_field.shape[0] == 9
+        return grow_connection_blend(caf_field, xy[0], xy[1], xy_scale,
+                                     connection_method=self.connection_method)

@@ -1,0 +1,58 @@
+"""Batch driver (decoder/generator/generator.py:14-107).
+
+The reference moves every field batch to the host (`.cpu().numpy()`, generator.py:65) and
+maps images over a multiprocessing.Pool.  Here the fields stay in HBM and the whole batch
+is decoded by one device launch sequence; `worker_pool` is accepted for API compatibility
+and ignored.
+"""
+import logging
+import time
+
+import torch
+
+LOG = logging.getLogger(__name__)
+
+
+class DummyPool():
+    @staticmethod
+    def starmap(f, iterable):
+        return [f(*i) for i in iterable]
+
+
+class Generator:
+    def __init__(self, worker_pool=None):
+        self.worker_pool = DummyPool() if not worker_pool else worker_pool
+        self.last_decoder_time = 0.0
+        self.last_nn_time = 0.0
+
+    def __getstate__(self):
+        return {k: v for k, v in self.__dict__.items() if k not in ('worker_pool',)}
+
+    @staticmethod
+    def fields_batch(model, image_batch, *, device=None):
+        """Network forward; the head outputs stay on the device (no .cpu().numpy())."""
+        start = time.time()
+        with torch.no_grad():
+            if device is not None:
+                image_batch = image_batch.to(device, non_blocking=True)
+            with torch.autograd.profiler.record_function('model'):
+                heads = model(image_batch)
+        LOG.debug('nn processing time: %.3fs', time.time() - start)
+        return heads
+
+    def __call__(self, fields, *, initial_annotations=None):
+        raise NotImplementedError()
+
+    def decode_batch(self, *heads):
+        raise NotImplementedError()
+
+    def batch(self, model, image_batch, *, device=None):
+        """From image batch straight to annotations batch (generator.py:84-101)."""
+        start_nn = time.perf_counter()
+        heads = self.fields_batch(model, image_batch, device=device)
+        self.last_nn_time = time.perf_counter() - start_nn
+        start = time.perf_counter()
+        result = self.decode_batch(*heads)
+        self.last_decoder_time = time.perf_counter() - start
+        LOG.debug('time: nn = %.3fs, dec = %.3fs', self.last_nn_time, self.last_decoder_time)
+        return result

@@ -1,0 +1,132 @@
+"""Batched device decode: fields resident in HBM -> packed annotation records.
+
+The engine owns the per-shape workspace (zeroed once at allocation, see the workspace
+contract in include/pifpaf_amd.h) and drives pp_decode_stages on torch's current stream.
+Records come back as a NumPy structured array (openpifpaf_amd._abi.ANN_DTYPE) packed over
+the whole batch plus per-image offsets; decoder/generator/cifcaf.py turns them into
+Annotation objects.
+"""
+import ctypes
+import logging
+
+import numpy as np
+import torch
+
+from . import _device
+from ._abi import (ANN_DTYPE, PP_ST_ANN_OVERFLOW, PP_ST_DEC_OVERFLOW, PP_ST_NMS_OVERFLOW,
+                   skeleton_array)
+from ._lib import PPError, call, load
+
+LOG = logging.getLogger(__name__)
+
+STAGE_CIFHR, STAGE_SEEDS, STAGE_CAF, STAGE_GROW = 1, 2, 4, 8
+STAGE_ALL = 15
+
+
+def default_ann_capacity(h, w):
+    """Annotations per image the first attempt reserves (doubles on overflow)."""
+    return int(min(8192, max(128, (h * w) // 8)))
+
+
+class DecodeBuffers:
+    """Workspace + outputs for one (batch shape, config) combination."""
+
+    def __init__(self, n, k, c, h, w, cfg, cap, device):
+        lib = load()
+        self.key = (n, k, c, h, w, cap, cfg.force_complete, cfg.stride,
+                    cfg.occupancy_reduction)
+        self.n, self.k, self.c, self.h, self.w, self.cap = n, k, c, h, w, cap
+        size = lib.pp_decode_workspace_size(n, k, c, h, w, ctypes.byref(cfg), cap)
+        zero_off = lib.pp_decode_workspace_zero_offset(n, k, c, h, w, ctypes.byref(cfg), cap)
+        if size == 0:
+            raise PPError('pp_decode_workspace_size rejected the shape')
+        self.ws = torch.empty(size, dtype=torch.uint8, device=device)
+        self.ws[zero_off:].zero_()
+        self.anns = torch.empty(n * cap * ANN_DTYPE.itemsize, dtype=torch.uint8, device=device)
+        self.counts = torch.zeros(n, dtype=torch.int32, device=device)
+        self.status = torch.zeros(n, dtype=torch.int32, device=device)
+        self.hh = (h - 1) * cfg.stride + 1
+        self.ww = (w - 1) * cfg.stride + 1
+        self.pitch = int(lib.pp_cifhr_pitch(self.ww))
+        self.cifhr = None
+
+    def cifhr_buffer(self):
+        if self.cifhr is None:
+            self.cifhr = torch.empty((self.n, self.k, self.hh, self.pitch), dtype=torch.float32,
+                                     device=self.ws.device)
+        return self.cifhr
+
+
+class DecodeEngine:
+    def __init__(self):
+        self._bufs = None
+
+    def buffers(self, n, k, c, h, w, cfg, cap):
+        key = (n, k, c, h, w, cap, cfg.force_complete, cfg.stride, cfg.occupancy_reduction)
+        if self._bufs is None or self._bufs.key != key:
+            self._bufs = None  # free the previous workspace first
+            self._bufs = DecodeBuffers(n, k, c, h, w, cfg, cap, _device.require())
+        return self._bufs
+
+    def launch(self, cif, caf, skeleton, cfg, cap=None, keep_cifhr=False, stages=STAGE_ALL):
+        """Enqueue the decode on the current stream; returns the DecodeBuffers."""
+        if cif.dim() != 5 or caf.dim() != 5 or cif.shape[2] != 5 or caf.shape[2] != 9:
+            raise ValueError('expected cif (B, K, 5, H, W) and caf (B, C, 9, H, W)')
+        n, k, _, h, w = cif.shape
+        c = caf.shape[1]
+        if caf.shape[0] != n or caf.shape[3:] != cif.shape[3:]:
+            raise ValueError('cif and caf batch / spatial shapes differ')
+        skel = skeleton_array(skeleton)
+        if len(skel) != c:
+            raise ValueError('skeleton has {} edges but caf has {} fields'.format(len(skel), c))
+        cap = cap or default_ann_capacity(h, w)
+        b = self.buffers(n, k, c, h, w, cfg, cap)
+        hr = b.cifhr_buffer() if keep_cifhr else None
+        call('pp_decode_stages', _device.ptr(cif), _device.ptr(caf), n, k, c, h, w,
+             skel.ctypes.data_as(ctypes.c_void_p), ctypes.byref(cfg), _device.ptr(hr),
+             _device.ptr(b.anns), cap, _device.ptr(b.counts), _device.ptr(b.status),
+             _device.ptr(b.ws), ctypes.c_size_t(b.ws.numel()), ctypes.c_uint32(stages),
+             _device.stream())
+        return b
+
+    def decode(self, cif, caf, skeleton, cfg, cap=None, keep_cifhr=False):
+        """Full decode with overflow retry.  Returns (records, offsets, buffers)."""
+        n, _, _, h, w = cif.shape
+        cap = cap or default_ann_capacity(h, w)
+        while True:
+            b = self.launch(cif, caf, skeleton, cfg, cap=cap, keep_cifhr=keep_cifhr)
+            status = b.status.cpu().numpy()
+            if not (status & PP_ST_ANN_OVERFLOW).any():
+                break
+            cap *= 2
+            LOG.info('annotation capacity overflow, retrying with %d per image', cap)
+        if (status & PP_ST_NMS_OVERFLOW).any():
+            raise PPError('NMS occupancy grid exceeds the workspace (keypoints far outside '
+                          'the field); status={}'.format(status.tolist()))
+        if (status & PP_ST_DEC_OVERFLOW).any():
+            raise PPError('decoding/frontier order exceeded the record capacity')
+        recs, offsets = self.fetch(b)
+        return recs, offsets, b
+
+    @staticmethod
+    def fetch(b):
+        """Packed records of all images (one gather + one D2H copy) and per-image offsets."""
+        counts = b.counts.cpu().numpy().astype(np.int64)
+        offsets = np.concatenate([[0], np.cumsum(counts)])
+        total = int(offsets[-1])
+        if total == 0:
+            return np.zeros(0, ANN_DTYPE), offsets
+        idx = np.concatenate([i * b.cap + np.arange(c) for i, c in enumerate(counts) if c])
+        rows = b.anns.view(b.n * b.cap, ANN_DTYPE.itemsize)
+        sel = rows.index_select(0, torch.from_numpy(idx).to(rows.device))
+        return np.frombuffer(sel.cpu().numpy().tobytes(), dtype=ANN_DTYPE), offsets
+
+
+_ENGINE = None
+
+
+def engine():
+    global _ENGINE  # pylint: disable=global-statement
+    if _ENGINE is None:
+        _ENGINE = DecodeEngine()
+    return _ENGINE

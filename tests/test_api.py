@@ -1,0 +1,104 @@
+"""Host-side API behaviour that needs no GPU: boundary errors (the reference's Cython
+messages), configuration plumbing, synthetic generators."""
+import argparse
+
+import numpy as np
+import pytest
+
+import golden_util as gu
+from openpifpaf_amd import functional as F
+from openpifpaf_amd import synthetic
+from openpifpaf_amd._abi import make_config
+
+
+def test_error_messages_match_reference():
+    errs = gu.load_errors()
+    p = np.zeros(2, np.float32)
+    with pytest.raises(ValueError) as e:
+        F.scalar_square_add_gauss_with_max(np.zeros((4, 4)), p, p, p, p)
+    assert [type(e.value).__name__, str(e.value)] == errs['dtype']
+    ro = np.zeros((4, 4), np.float32)
+    ro.setflags(write=False)
+    with pytest.raises(ValueError) as e:
+        F.scalar_values(ro, p, p)
+    assert [type(e.value).__name__, str(e.value)] == errs['readonly']
+    with pytest.raises(ValueError) as e:
+        F.scalar_values(np.zeros((2, 4, 4), np.float32), p, p)
+    assert [type(e.value).__name__, str(e.value)] == errs['ndim']
+    with pytest.raises(ValueError) as e:
+        F.weiszfeld_nd(np.zeros((3, 2), np.float32), np.zeros(2, np.float32))
+    assert [type(e.value).__name__, str(e.value)] == errs['weiszfeld_none']
+    with pytest.raises(ValueError) as e:
+        F.scalar_values(np.zeros((4, 4), np.float32), np.zeros((2, 2), np.float32), p)
+    assert [type(e.value).__name__, str(e.value)] == errs['ndim_points']
+
+
+def test_no_cpu_fallback():
+    """Without a HIP device the product path raises instead of computing on the CPU."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip('a GPU is visible')
+    from openpifpaf_amd._lib import PPError
+    f = np.zeros((8, 8), np.float32)
+    p = np.ones(1, np.float32)
+    with pytest.raises(PPError):
+        F.scalar_square_add_gauss_with_max(f, p, p, p, p)
+
+
+def test_configure_writes_class_attributes():
+    from openpifpaf_amd import decoder
+    parser = argparse.ArgumentParser()
+    decoder.cli(parser, force_complete_pose=False, instance_threshold=0.1, seed_threshold=0.5)
+    args = parser.parse_args([])
+    args.debug = False
+    decoder.configure(args)
+    assert decoder.CifSeeds.threshold == 0.5
+    assert decoder.CifCaf.force_complete is False
+    assert decoder.CifCaf.keypoint_threshold == 0.001
+    assert decoder.nms.Keypoints.instance_threshold == 0.1
+    cc = decoder.CifCaf(decoder.FieldConfig(), keypoints=list('abcdefghijklmnopq'),
+                        skeleton=[(1, 2), (2, 3)])
+    cfg = cc.config()
+    assert cfg.seed_threshold == pytest.approx(0.5)
+    assert cfg.force_complete == 0
+    assert cfg.apply_nms == 1
+    args = parser.parse_args(['--force-complete-pose', '--seed-threshold', '0.2',
+                              '--instance-threshold', '0.0', '--keypoint-threshold', '0.0'])
+    args.debug = False
+    decoder.configure(args)
+    assert decoder.CifCaf.force_complete is True
+
+
+def test_by_source_tables_follow_dict_order():
+    from openpifpaf_amd import constants, decoder
+    cc = decoder.CifCaf(decoder.FieldConfig(), keypoints=constants.COCO_KEYPOINTS,
+                        skeleton=constants.COCO_PERSON_SKELETON)
+    # joint 5 (left shoulder, 0-based) appears in edges (6,12), (6,7), (6,8), (4,6)
+    assert list(cc.by_source[5].keys()) == [11, 6, 7, 3]
+
+
+def test_unsupported_configurations_raise():
+    from openpifpaf_amd import decoder
+    fc = decoder.FieldConfig(cif_indices=[0, 3], caf_indices=[1, 4], cif_strides=[8, 16],
+                             caf_strides=[8, 16], cif_min_scales=[0.0, 12.0],
+                             caf_min_distances=[0.0, 36.0], caf_max_distances=[None, None])
+    with pytest.raises(NotImplementedError):
+        fc.single_scale()
+    with pytest.raises(NotImplementedError):
+        decoder.CifCaf(decoder.FieldConfig(), keypoints=['a'], skeleton=[(1, 1)],
+                       confidence_scales=[1.0])
+
+
+def test_generators_deterministic():
+    a = synthetic.planted(40, 40, seed=3)
+    b = synthetic.planted(40, 40, seed=3)
+    assert synthetic.digest(*a) == synthetic.digest(*b)
+    c, f = synthetic.uniform(16, 21, seed=0)
+    assert c.shape == (17, 5, 16, 21) and f.shape == (19, 9, 16, 21)
+    cb, fb = synthetic.batch('uniform', 3, 10, 10, first_seed=5)
+    assert np.array_equal(cb[1], synthetic.uniform(10, 10, seed=6)[0])
+
+
+def test_make_config_rejects_unknown_method():
+    with pytest.raises(Exception):
+        make_config(connection_method='nearest')

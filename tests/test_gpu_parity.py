@@ -1,0 +1,321 @@
+"""HIP path vs the reference (golden fixtures) and vs the oracle, on an MI355X.
+
+Bit-exact: CifHr maps, seed lists, CafScored column sets, every functional primitive.
+Tolerance (golden_util.ATOL/RTOL) only for the grow-stage floats against the reference's
+own outputs (np.exp rounding); against the oracle the device decode must match exactly.
+"""
+import numpy as np
+import pytest
+
+import golden_util as gu
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+CASES = gu.case_names()
+
+
+@pytest.fixture(scope='module')
+def F():
+    from openpifpaf_amd import functional
+    return functional
+
+
+@pytest.fixture(scope='module')
+def dec():
+    from openpifpaf_amd import decoder
+    return decoder
+
+
+@pytest.fixture(scope='module')
+def prim():
+    return gu.load_primitives()
+
+
+def _pts(p, key):
+    return [np.ascontiguousarray(r) for r in p[key]]
+
+
+# ---- functional primitives -------------------------------------------------------------
+
+@pytest.mark.parametrize('t', range(4))
+def test_add_gauss_with_max(F, prim, t):
+    field = prim['sqg_max_%d_in' % t].copy()
+    trunc, maxv = prim['sqg_max_%d_args' % t]
+    F.scalar_square_add_gauss_with_max(field, *_pts(prim, 'sqg_max_%d_pts' % t),
+                                       truncate=trunc, max_value=maxv)
+    assert np.array_equal(field, prim['sqg_max_%d_out' % t])
+
+
+def test_add_gauss_with_max_strided_and_empty(F, prim):
+    big = prim['sqg_max_strided_in'].copy()
+    F.scalar_square_add_gauss_with_max(big[::2, 1::2], *_pts(prim, 'sqg_max_strided_pts'),
+                                       truncate=1.0)
+    assert np.array_equal(big, prim['sqg_max_strided_out'])
+    field = prim['sqg_max_empty_in'].copy()
+    e = np.zeros(0, np.float32)
+    F.scalar_square_add_gauss_with_max(field, e, e, e, e)
+    assert np.array_equal(field, prim['sqg_max_empty_out'])
+
+
+@pytest.mark.parametrize('t', range(2))
+def test_add_gauss(F, prim, t):
+    field = prim['sqg_%d_in' % t].copy()
+    F.scalar_square_add_gauss(field, *_pts(prim, 'sqg_%d_pts' % t),
+                              truncate=prim['sqg_%d_args' % t][0])
+    assert np.array_equal(field, prim['sqg_%d_out' % t])
+
+
+@pytest.mark.parametrize('t', range(2))
+def test_max_gauss(F, prim, t):
+    field = prim['sqmax_%d_in' % t].copy()
+    F.scalar_square_max_gauss(field, *_pts(prim, 'sqmax_%d_pts' % t),
+                              truncate=prim['sqmax_%d_args' % t][0])
+    assert np.array_equal(field, prim['sqmax_%d_out' % t])
+
+
+def test_add_constant(F, prim):
+    field = prim['sqc_in'].copy()
+    F.scalar_square_add_constant(field, *_pts(prim, 'sqc_pts'))
+    assert np.array_equal(field, prim['sqc_out'])
+
+
+def test_cumulative_average(F, prim):
+    cuma, cumw = [a.copy() for a in prim['cuma_in']]
+    F.cumulative_average(cuma, cumw, *_pts(prim, 'cuma_pts'))
+    assert np.array_equal(np.stack([cuma, cumw]), prim['cuma_out'])
+
+
+@pytest.mark.parametrize('t', range(3))
+def test_weiszfeld(F, prim, t):
+    y = prim['weisz_%d_y0' % t].copy()
+    _, denom = F.weiszfeld_nd(prim['weisz_%d_x' % t].copy(), y, weights=prim['weisz_%d_w' % t].copy())
+    assert np.array_equal(y, prim['weisz_%d_y' % t])
+    assert np.array_equal(denom, prim['weisz_%d_denom' % t])
+
+
+def test_lookups(F, prim):
+    f = prim['lookup_field'].copy()
+    px, py = [a.copy() for a in prim['lookup_pts']]
+    assert np.array_equal(F.scalar_values(f, px, py), prim['scalar_values'])
+    assert np.array_equal(F.scalar_values(f, px, py, default=0.0), prim['scalar_values_d0'])
+    got = np.array([F.scalar_value(f, a, b) for a, b in zip(px, py)], np.float32)
+    assert np.array_equal(got, prim['scalar_value'])
+    got = np.array([F.scalar_value_clipped(f, a, b) for a, b in zip(px, py)], np.float32)
+    assert np.array_equal(got, prim['scalar_value_clipped'])
+    occ = prim['lookup_occ'].copy()
+    got = np.array([F.scalar_nonzero(occ, a, b) for a, b in zip(px, py)], np.uint8)
+    assert np.array_equal(got, prim['scalar_nonzero'])
+    got = np.array([F.scalar_nonzero_clipped(occ, a, b) for a, b in zip(px, py)], np.uint8)
+    assert np.array_equal(got, prim['scalar_nonzero_clipped'])
+    got = np.array([F.scalar_nonzero_clipped_with_reduction(occ, 2 * a, 2 * b, 2.0)
+                    for a, b in zip(px, py)], np.uint8)
+    assert np.array_equal(got, prim['scalar_nonzero_red'])
+
+
+def test_center_filters(F, prim):
+    caf = prim['center_field'].copy()
+    for t, (qx, qy, qs) in enumerate(prim['center_queries']):
+        assert np.array_equal(F.caf_center_s(caf, qx, qy, qs), prim['caf_center_s_%d' % t])
+        p7 = np.ascontiguousarray(caf[:7])
+        assert np.array_equal(F.paf_center(p7, qx, qy, qs), prim['paf_center_%d' % t])
+        assert np.array_equal(F.paf_center_b(p7, qx, qy, sigma=qs / 3), prim['paf_center_b_%d' % t])
+        assert np.array_equal(F.paf_mask_center(p7, qx, qy, sigma=qs / 3),
+                              prim['paf_mask_center_%d' % t])
+
+
+def test_grow_connection_blend_matches_oracle_decode(F):
+    """Every grow_connection on a real column set: device == oracle restatement."""
+    g = gu.load_case('p40_s0_eval')
+    cif, caf, skeleton = gu.case_inputs(g)
+    cfg = gu.case_config(g)
+    hr = oracle.cifhr(cif, cfg)
+    fwd, _ = oracle.caf_scored(caf, hr, skeleton, 0.1, cfg)
+    rng = np.random.default_rng(0)
+    checked = 0
+    for cols in fwd:
+        if cols.shape[1] == 0:
+            continue
+        for _ in range(10):
+            i = rng.integers(cols.shape[1])
+            x = np.float32(cols[1, i] + rng.normal(0, 3))
+            y = np.float32(cols[2, i] + rng.normal(0, 3))
+            s = np.float32(rng.uniform(1, 12))
+            got = F.grow_connection_blend(cols.copy(), x, y, s)
+            want = _oracle_grow_connection(cols, x, y, s)
+            assert np.array_equal(np.asarray(got, np.float32), want), (got, want)
+            checked += 1
+    assert checked > 50
+
+
+def _oracle_grow_connection(cols, x, y, s):
+    """Direct restatement of cifcaf.py:124-192 in numpy float32 (small n)."""
+    sb = np.float32(2.0) * s
+    m = ~((cols[1] < x - sb) | (cols[1] > x + sb) | (cols[2] < y - sb) | (cols[2] > y + sb))
+    c = cols[:, m]
+    if c.shape[1] == 0:
+        return np.zeros(4, np.float32)
+    dx = x - c[1]
+    dy = y - c[2]
+    d = np.sqrt(dx * dx + dy * dy)
+    sig = np.float32(0.5) * s
+    q = (np.float32(-0.5) * (d * d)) / (sig * sig)
+    scores = np.exp(q.astype(np.float64)).astype(np.float32) * c[0]
+    order = np.argsort(scores, kind='stable')
+    t = c[5:]
+    if len(scores) == 1:
+        return np.array([t[0, 0], t[1, 0], t[3, 0], scores[0] * np.float32(0.5)], np.float32)
+    i1, i2 = order[-1], order[-2]
+    s1, s2 = scores[i1], scores[i2]
+    if s2 < np.float32(0.01) or s2 < np.float32(0.5) * s1:
+        return np.array([t[0, i1], t[1, i1], t[3, i1], s1 * np.float32(0.5)], np.float32)
+    ex = t[0, i1] - t[0, i2]
+    ey = t[1, i1] - t[1, i2]
+    if np.sqrt(ex * ex + ey * ey) > t[3, i1] / np.float32(2.0):
+        return np.array([t[0, i1], t[1, i1], t[3, i1], s1 * np.float32(0.5)], np.float32)
+    ss = s1 + s2
+    return np.array([(s1 * t[0, i1] + s2 * t[0, i2]) / ss, (s1 * t[1, i1] + s2 * t[1, i2]) / ss,
+                     (s1 * t[3, i1] + s2 * t[3, i2]) / ss, np.float32(0.5) * (s1 + s2)],
+                    np.float32)
+
+
+# ---- decoder stages (single image, reference API) --------------------------------------
+
+def _configure(dec, g):
+    mode = str(g['mode'])
+    dec.CifHr.v_threshold = 0.1
+    dec.CafScored.default_score_th = 0.1
+    dec.CifSeeds.threshold = 0.2 if mode == 'eval' else 0.5
+    dec.CifCaf.force_complete = mode == 'eval'
+    dec.CifCaf.keypoint_threshold = 0.0 if mode == 'eval' else 0.001
+    dec.CifCaf.greedy = bool(int(g['greedy']))
+    dec.CifCaf.connection_method = str(g['connection_method'])
+    dec.nms.Keypoints.instance_threshold = 0.0 if mode == 'eval' else 0.1
+    dec.nms.Keypoints.keypoint_threshold = 0.0 if mode == 'eval' else 0.001
+
+
+@pytest.mark.parametrize('name', CASES)
+def test_stages_bit_exact(dec, name):
+    g = gu.load_case(name)
+    cif, caf, skeleton = gu.case_inputs(g)
+    _configure(dec, g)
+    fc = dec.FieldConfig()
+    hr = dec.CifHr(fc).fill([cif, caf]).accumulated
+    assert gu.sha(hr) == str(g['cifhr_sha'])
+    seeds = dec.CifSeeds(hr, fc).fill([cif, caf]).get()
+    rows = np.array([tuple(float(t) for t in s) for s in seeds], np.float32).reshape(-1, 5)
+    assert np.array_equal(rows, g['seeds'])
+    for tag, th in (('a', None), ('b', 0.0001)):
+        cs = dec.CafScored(hr, fc, skeleton, score_th=th).fill([cif, caf])
+        assert [f.shape[1] for f in cs.forward] == list(g['caf_%s_fwd_counts' % tag])
+        assert [gu.sha(f) for f in cs.forward] == [str(s) for s in g['caf_%s_fwd_sha' % tag]]
+        assert [gu.sha(b) for b in cs.backward] == [str(s) for s in g['caf_%s_bwd_sha' % tag]]
+
+
+@pytest.mark.parametrize('name', CASES)
+def test_cifcaf_vs_reference(dec, name):
+    from openpifpaf_amd import constants
+    g = gu.load_case(name)
+    cif, caf, skeleton = gu.case_inputs(g)
+    _configure(dec, g)
+    cc = dec.CifCaf(dec.FieldConfig(), keypoints=constants.COCO_KEYPOINTS, skeleton=skeleton,
+                    out_skeleton=constants.COCO_PERSON_SKELETON)
+    recs, _, _ = cc.decode_records(cif[None], caf[None])
+    errs = gu.compare_annotations(g, recs)
+    assert not errs, errs[:10]
+    anns = cc([cif, caf])
+    assert len(anns) == len(g['ann_score'])
+    for a, s in zip(anns, g['ann_score']):
+        assert np.isclose(a.score(), s, rtol=gu.RTOL, atol=1e-9)
+
+
+@pytest.mark.parametrize('name', CASES)
+def test_cifcaf_vs_oracle_exact(dec, name):
+    """The device decode and the oracle use the same correctly rounded exp: identical."""
+    from openpifpaf_amd import constants
+    g = gu.load_case(name)
+    cif, caf, skeleton = gu.case_inputs(g)
+    _configure(dec, g)
+    cc = dec.CifCaf(dec.FieldConfig(), keypoints=constants.COCO_KEYPOINTS, skeleton=skeleton)
+    recs, _, _ = cc.decode_records(cif[None], caf[None])
+    ref = oracle.decode(cif, caf, skeleton, gu.case_config(g))
+    assert len(recs) == len(ref)
+    for r, o in zip(recs, ref):
+        for key in ('data', 'joint_scales', 'score', 'n_decoding', 'decoding_pairs',
+                    'decoding_xyv', 'n_frontier', 'frontier_pairs'):
+            assert np.array_equal(r[key], o[key]), key
+
+
+# ---- batches at the BASELINE sizes ---------------------------------------------------------
+
+def _batch_vs_oracle(dec, kind, n, h, n_check, mode='eval'):
+    from openpifpaf_amd import constants, synthetic
+    from openpifpaf_amd._abi import EVAL_CONFIG, PREDICT_CONFIG, make_config
+    g = {'mode': np.array(mode), 'greedy': 0, 'connection_method': np.array('blend')}
+    _configure(dec, g)
+    cif, caf = synthetic.batch(kind, n, h, h)
+    cc = dec.CifCaf(dec.FieldConfig(), keypoints=constants.COCO_KEYPOINTS,
+                    skeleton=constants.COCO_PERSON_SKELETON)
+    recs, offsets, _ = cc.decode_records(cif, caf)
+    cfg = make_config(**(EVAL_CONFIG if mode == 'eval' else PREDICT_CONFIG))
+    step = max(1, n // n_check)
+    for i in range(0, n, step):
+        ref = oracle.decode(cif[i], caf[i], constants.COCO_PERSON_SKELETON, cfg)
+        got = recs[offsets[i]:offsets[i + 1]]
+        assert len(got) == len(ref), i
+        for r, o in zip(got, ref):
+            assert np.array_equal(r['data'], o['data']), i
+            assert np.array_equal(r['decoding_pairs'], o['decoding_pairs']), i
+            assert r['score'] == o['score'], i
+    return offsets
+
+
+def test_batch256_planted_eval(dec):
+    offsets = _batch_vs_oracle(dec, 'planted', 256, 80, 32)
+    assert offsets[-1] > 256 * 6  # ~8 people per image
+
+
+def test_batch_uniform_eval(dec):
+    _batch_vs_oracle(dec, 'uniform', 16, 80, 4)
+
+
+def test_batch_predict(dec):
+    _batch_vs_oracle(dec, 'planted', 64, 80, 16, mode='predict')
+
+
+def test_cifhr_batch_bit_exact():
+    """CifHr over a 256-image batch: every image equals the oracle bit for bit."""
+    import torch
+    from openpifpaf_amd import synthetic
+    from openpifpaf_amd._abi import make_config
+    from openpifpaf_amd.decoder.cif_hr import cifhr_device
+    cif, _ = synthetic.batch('planted', 256, 80, 80)
+    hr = cifhr_device(torch.from_numpy(cif).cuda(), 8, 0.1, 16)
+    ww = 633
+    host = hr[:, :, :, :ww].cpu().numpy()
+    assert not hr[:, :, :, ww:].any().item()  # pitch padding written as zeros
+    cfg = make_config()
+    for i in range(0, 256, 16):
+        assert np.array_equal(host[i], oracle.cifhr(cif[i], cfg)), i
+    ucif, _ = synthetic.batch('uniform', 8, 80, 80)
+    uh = cifhr_device(torch.from_numpy(ucif).cuda(), 8, 0.1, 16)[:, :, :, :ww].cpu().numpy()
+    for i in range(8):
+        assert np.array_equal(uh[i], oracle.cifhr(ucif[i], cfg)), i
+
+
+def test_workspace_left_clean(dec):
+    """The occupancy workspace is zero again after a decode (workspace contract)."""
+    from openpifpaf_amd import constants, engine, synthetic
+    g = {'mode': np.array('eval'), 'greedy': 0, 'connection_method': np.array('blend')}
+    _configure(dec, g)
+    cif, caf = synthetic.batch('uniform', 4, 40, 40)
+    cc = dec.CifCaf(dec.FieldConfig(), keypoints=constants.COCO_KEYPOINTS,
+                    skeleton=constants.COCO_PERSON_SKELETON)
+    _, _, b = cc.decode_records(cif, caf)
+    from openpifpaf_amd._lib import load
+    import ctypes
+    cfg = cc.config()
+    zoff = load().pp_decode_workspace_zero_offset(4, 17, 19, 40, 40, ctypes.byref(cfg), b.cap)
+    occ_bytes = b.ws[zoff:zoff + 4 * 17 * (156 + 64) * (156 + 64)]  # H' = 313 -> 156 rows
+    assert int(occ_bytes.sum().item()) == 0
+    assert engine.engine() is not None
