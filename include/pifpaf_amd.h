@@ -134,8 +134,9 @@ int pp_cifhr(const float *d_cif, int32_t n_img, int32_t K, int32_t H, int32_t W,
 
 /*
  * CifSeeds (cif_seeds.py:23-64): per image, the seeds sorted as
- * sorted(seeds, reverse=True) (cif_seeds.py:54).  d_seeds (n_img, seed_capacity),
- * d_counts (n_img) = true count (may exceed capacity -> PP_ST_SEED_OVERFLOW semantics).
+ * sorted(seeds, reverse=True) (cif_seeds.py:54).  d_seeds (n_img, seed_capacity) with
+ * seed_capacity >= K*H*W (every cell can seed, so no overflow is possible);
+ * d_counts (n_img) = number of seeds.
  */
 int pp_seeds(const float *d_cif, const float *d_cifhr, int32_t n_img, int32_t K, int32_t H,
              int32_t W, const pp_config *cfg, pp_seed *d_seeds, int32_t seed_capacity,

@@ -11,6 +11,8 @@ import threading
 from ._abi import PP_ABI_VERSION, STATUS_NAMES
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libpifpaf_amd.so')
+if os.environ.get('PP_LIB_VARIANT'):  # diagnostic builds (e.g. 'stamps'); never the default
+    LIB_PATH = LIB_PATH.replace('.so', '_{}.so'.format(os.environ['PP_LIB_VARIANT']))
 
 _lock = threading.Lock()
 _lib = None

@@ -33,32 +33,39 @@ def _deps_mtime():
     return max(os.path.getmtime(p) for p in paths)
 
 
-def _compile(src):
-    obj = os.path.join(BUILD, os.path.basename(src)[:-4] + '.o')
+def _compile(src, bdir=BUILD, extra=()):
+    obj = os.path.join(bdir, os.path.basename(src)[:-4] + '.o')
     if os.path.exists(obj) and os.path.getmtime(obj) >= _deps_mtime():
         return obj
-    cmd = [HIPCC] + CFLAGS + ['-c', src, '-o', obj]
+    cmd = [HIPCC] + CFLAGS + list(extra) + ['-c', src, '-o', obj]
     res = subprocess.run(cmd, capture_output=True, text=True, check=False)
     if res.returncode != 0:
         raise RuntimeError('hipcc failed for {}:\n{}\n{}'.format(src, ' '.join(cmd), res.stderr))
     return obj
 
 
-def build(force=False, verbose=True):
-    os.makedirs(BUILD, exist_ok=True)
-    if (not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= _deps_mtime()):
-        return LIB
+def build(force=False, verbose=True, variant=''):
+    """variant '' = the product library; 'stamps' = diagnostic build with in-kernel cycle
+    stamps (-DPP_STAMPS), never loaded unless PP_LIB_VARIANT=stamps."""
+    lib = LIB if not variant else LIB.replace('.so', '_{}.so'.format(variant))
+    bdir = BUILD if not variant else BUILD + '_' + variant
+    os.makedirs(bdir, exist_ok=True)
+    if (not force and os.path.exists(lib) and os.path.getmtime(lib) >= _deps_mtime()):
+        return lib
+    extra = ['-DPP_STAMPS'] if variant == 'stamps' else []
     workers = min(8, len(sources()))
     with concurrent.futures.ThreadPoolExecutor(workers) as ex:
-        objs = list(ex.map(_compile, sources()))
-    cmd = [HIPCC, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', LIB] + objs
+        objs = list(ex.map(lambda src: _compile(src, bdir, extra), sources()))
+    cmd = [HIPCC, '--offload-arch=' + ARCH, '-shared', '-fPIC', '-o', lib] + objs
     res = subprocess.run(cmd, capture_output=True, text=True, check=False)
     if res.returncode != 0:
         raise RuntimeError('link failed:\n{}\n{}'.format(' '.join(cmd), res.stderr))
     if verbose:
-        print('built', LIB, file=sys.stderr)
-    return LIB
+        print('built', lib, file=sys.stderr)
+    return lib
 
 
 if __name__ == '__main__':
     build(force='--force' in sys.argv)
+    if '--stamps' in sys.argv:
+        build(force='--force' in sys.argv, variant='stamps')

@@ -19,6 +19,31 @@
 // correctly rounded through f64.
 #include "pp_common.hpp"
 
+#include <stdio.h>
+#include <stdlib.h>
+
+// Diagnostic build only (-DPP_STAMPS, libpifpaf_amd_stamps.so): per-section shader-cycle
+// sums of the decode kernel, dumped to $PP_STAMPS_OUT.  The product build compiles these
+// to nothing.
+#ifdef PP_STAMPS
+#define STAMP_DECL                                                                          \
+    uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};                              \
+    uint64_t st_t = __builtin_amdgcn_s_memtime();
+#define STAMP(i)                                                                            \
+    do {                                                                                    \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();                                   \
+        st_acc[i] += t_ - st_t;                                                             \
+        st_t = t_;                                                                          \
+    } while (0)
+#define STAMP_FLUSH(ph)                                                                     \
+    if (lane == 0 && g.stamps)                                                              \
+        for (int q_ = 0; q_ < 12; q_++) g.stamps[((int64_t)img * 2 + (ph)-1) * 12 + q_] = st_acc[q_];
+#else
+#define STAMP_DECL
+#define STAMP(i)
+#define STAMP_FLUSH(ph)
+#endif
+
 namespace pp {
 
 constexpr int kKP = PP_MAX_KP;
@@ -49,8 +74,11 @@ struct GrowArgs {
     const pp_seed *seeds;
     const int *seed_counts;
     int seed_cap;
-    const float *cols[2];     // threshold A (caf_threshold), B (complete_caf_threshold)
-    const int *col_counts[2];
+    const float *cols[2];     // bucketed column sets (n_img, C, 2, 10, H*W): set A at
+                              // caf_threshold, set B at complete_caf_threshold
+    const int *offs[2];       // bucket boundaries (n_img, C, 2, nb + 1)
+    int bw, bh, nb;           // bucket grid (see caf_bucketed_kernel)
+    float inv_e;
     int K, C, H, W, hh, ww;
     int64_t hw;
     pp_config cfg;
@@ -65,6 +93,9 @@ struct GrowArgs {
     int *nms_idx;             // (n_img, 2 * ann_cap + ann_np)
     int ann_np;               // next pow2 >= ann_cap
     int ann_cap;
+    uint64_t *stamps;         // diagnostic build: (n_img, 2, 12) cycle sums, else NULL
+    int *n_work;              // (n_img) annotations after the seed loop (phase 1 -> 2)
+    int *need_complete;       // (n_img) 1 if force-complete has work (gates the B columns)
     // outputs
     pp_ann *out;
     int *counts;
@@ -78,6 +109,11 @@ struct GrowLDS {
     uint32_t in_frontier[kKP];
     int bs_n[kKP];
     uint8_t bs_k[kKP][kBS], bs_caf[kKP][kBS], bs_fwd[kKP][kBS];
+    int seg_st[64], seg_pre[64];  // flattened bucket segments of one caf_center_s scan
+    int mark_pre[kKP + 1];        // occupancy boxes of one annotation: area prefix
+    int mark_box[kKP][4];
+    double prod[kKP];             // Annotation.score() terms
+    double score_bc;
     int heap_n;
     int ff_n;
     int log_n;
@@ -193,7 +229,8 @@ __device__ FFEntry ff_pop(GrowLDS &L) {
 // ---------------------------------------------------------------------------------------
 struct Top2 {
     float s1, s2;
-    int i1, i2;
+    int o1, o2;  // column index in the reference's row-major order (tie-breaks)
+    int k1, k2;  // storage slot (where the column's rows are)
 };
 
 // blend: top-2 of a stable ascending argsort (ties -> higher column ranks higher)
@@ -207,15 +244,18 @@ __device__ __forceinline__ bool better(float sa, int ia, float sb, int ib) {
 }
 
 template <bool MAXM>
-__device__ __forceinline__ void top2_insert(Top2 &t, float s, int i) {
-    if (better<MAXM>(s, i, t.s1, t.i1)) {
+__device__ __forceinline__ void top2_insert(Top2 &t, float s, int o, int k) {
+    if (better<MAXM>(s, o, t.s1, t.o1)) {
         t.s2 = t.s1;
-        t.i2 = t.i1;
+        t.o2 = t.o1;
+        t.k2 = t.k1;
         t.s1 = s;
-        t.i1 = i;
-    } else if (better<MAXM>(s, i, t.s2, t.i2)) {
+        t.o1 = o;
+        t.k1 = k;
+    } else if (better<MAXM>(s, o, t.s2, t.o2)) {
         t.s2 = s;
-        t.i2 = i;
+        t.o2 = o;
+        t.k2 = k;
     }
 }
 
@@ -224,9 +264,10 @@ __device__ __forceinline__ void top2_wave_merge(Top2 &t) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         const float os1 = __shfl_xor(t.s1, off), os2 = __shfl_xor(t.s2, off);
-        const int oi1 = __shfl_xor(t.i1, off), oi2 = __shfl_xor(t.i2, off);
-        top2_insert<MAXM>(t, os1, oi1);
-        top2_insert<MAXM>(t, os2, oi2);
+        const int oo1 = __shfl_xor(t.o1, off), oo2 = __shfl_xor(t.o2, off);
+        const int ok1 = __shfl_xor(t.k1, off), ok2 = __shfl_xor(t.k2, off);
+        top2_insert<MAXM>(t, os1, oo1, ok1);
+        top2_insert<MAXM>(t, os2, oo2, ok2);
     }
 }
 
@@ -236,47 +277,52 @@ __device__ __forceinline__ int wave_sum(int v) {
     return v;
 }
 
-// cf: (9, n) column set with row stride hw.  Returns x, y, s, score in out[].
-template <bool MAXM>
-__device__ void grow_connection(const float *__restrict__ cf, int n, int64_t hw, float x, float y,
-                                float xy_scale, float out[4]) {
+__device__ __forceinline__ int wave_incl_scan(int v) {
     const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(v, off);
+        if (lane >= off) v += o;
+    }
+    return v;
+}
+
+struct ColQuery {
+    float x, y, lo_x, hi_x, lo_y, hi_y, sigma2;
+};
+
+__device__ __forceinline__ ColQuery make_query(float x, float y, float xy_scale) {
+    ColQuery q;
     const float sbox = 2.0f * xy_scale;  // caf_center_s(..., sigma=2.0 * xy_scale)
-    const float lo_x = x - sbox, hi_x = x + sbox, lo_y = y - sbox, hi_y = y + sbox;
+    q.x = x;
+    q.y = y;
+    q.lo_x = x - sbox;
+    q.hi_x = x + sbox;
+    q.lo_y = y - sbox;
+    q.hi_y = y + sbox;
     const float sigma = 0.5f * xy_scale;
-    const float sigma2 = sigma * sigma;
-    Top2 t{0.0f, 0.0f, -1, -1};
-    int m = 0;
-    const float *r1 = cf + hw, *r2 = cf + 2 * hw;
-    int i = lane;
-    for (; i + 192 < n; i += 256) {  // 4 independent column loads in flight per lane
-        float c1[4], c2[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            c1[u] = r1[i + 64 * u];
-            c2[u] = r2[i + 64 * u];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            if (c1[u] < lo_x || c1[u] > hi_x || c2[u] < lo_y || c2[u] > hi_y) continue;
-            const float dx = x - c1[u], dy = y - c2[u];
-            const float dd = sqrtf(dx * dx + dy * dy);  // np.linalg.norm(axis=0)
-            const float q = (-0.5f * (dd * dd)) / sigma2;
-            const float score = (float)exp((double)q) * cf[i + 64 * u];
-            m++;
-            top2_insert<MAXM>(t, score, i + 64 * u);
-        }
-    }
-    for (; i < n; i += 64) {
-        const float c1 = r1[i], c2 = r2[i];
-        if (c1 < lo_x || c1 > hi_x || c2 < lo_y || c2 > hi_y) continue;
-        const float dx = x - c1, dy = y - c2;
-        const float dd = sqrtf(dx * dx + dy * dy);
-        const float q = (-0.5f * (dd * dd)) / sigma2;
-        const float score = (float)exp((double)q) * cf[i];
-        m++;
-        top2_insert<MAXM>(t, score, i);
-    }
+    q.sigma2 = sigma * sigma;
+    return q;
+}
+
+// one column: caf_center_s test, then the score (cifcaf.py:134-139)
+template <bool MAXM>
+__device__ __forceinline__ void consider(const float *__restrict__ cf, int64_t hw, const ColQuery &q,
+                                         int k, int o, Top2 &t, int &m) {
+    const float c1 = cf[hw + k], c2 = cf[2 * hw + k];
+    if (c1 < q.lo_x || c1 > q.hi_x || c2 < q.lo_y || c2 > q.hi_y) return;
+    const float dx = q.x - c1, dy = q.y - c2;
+    const float dd = sqrtf(dx * dx + dy * dy);  // np.linalg.norm(axis=0)
+    const float qq = (-0.5f * (dd * dd)) / q.sigma2;
+    const float score = (float)exp((double)qq) * cf[k];  // np.exp, correctly rounded
+    m++;
+    top2_insert<MAXM>(t, score, o, k);
+}
+
+// _target_with_blend / _target_with_maxscore (cifcaf.py:147-192) on the merged top-2
+template <bool MAXM>
+__device__ void finish_connection(const float *__restrict__ cf, int64_t hw, Top2 t, int m,
+                                  float out[4]) {
     m = wave_sum(m);
     if (m == 0) {
         out[0] = out[1] = out[2] = out[3] = 0.0f;
@@ -284,8 +330,8 @@ __device__ void grow_connection(const float *__restrict__ cf, int n, int64_t hw,
     }
     top2_wave_merge<MAXM>(t);
     const float *t0 = cf + 5 * hw, *t1 = cf + 6 * hw, *t3 = cf + 8 * hw;
-    const float x1 = t0[t.i1], y1 = t1[t.i1], sc1 = t3[t.i1];
-    if (MAXM) {  // _target_with_maxscore (cifcaf.py:147-155)
+    const float x1 = t0[t.k1], y1 = t1[t.k1], sc1 = t3[t.k1];
+    if (MAXM) {
         out[0] = x1;
         out[1] = y1;
         out[2] = sc1;
@@ -299,7 +345,7 @@ __device__ void grow_connection(const float *__restrict__ cf, int n, int64_t hw,
         out[3] = t.s1 * 0.5f;
         return;
     }
-    const float x2 = t0[t.i2], y2 = t1[t.i2], sc2 = t3[t.i2];
+    const float x2 = t0[t.k2], y2 = t1[t.k2], sc2 = t3[t.k2];
     const float ex = x1 - x2, ey = y1 - y2;
     const float dist = sqrtf(ex * ex + ey * ey);
     if (dist > sc1 / 2.0f) {
@@ -316,15 +362,91 @@ __device__ void grow_connection(const float *__restrict__ cf, int n, int64_t hw,
     out[3] = 0.5f * (t.s1 + t.s2);
 }
 
+// column set in the reference's order, n columns (the functional API entry point)
+template <bool MAXM>
+__device__ void grow_connection_flat(const float *__restrict__ cf, int n, int64_t hw, float x,
+                                     float y, float xy_scale, float out[4]) {
+    const int lane = threadIdx.x & 63;
+    const ColQuery q = make_query(x, y, xy_scale);
+    Top2 t{0.0f, 0.0f, -1, -1, -1, -1};
+    int m = 0;
+    for (int i = lane; i < n; i += 64) consider<MAXM>(cf, hw, q, i, i, t, m);
+    finish_connection<MAXM>(cf, hw, t, m, out);
+}
+
+// bucketed column set (caf_bucketed_kernel): visit only the buckets the 2*scale box
+// overlaps (+ the NaN-source bucket), flattened over the 64 lanes
+template <bool MAXM>
+__device__ void grow_connection(const GrowArgs &g, GrowLDS &L, const float *__restrict__ cf,
+                                const int *__restrict__ off, float x, float y, float xy_scale,
+                                float out[4]) {
+    const int lane = threadIdx.x & 63;
+    const int64_t hw = g.hw;
+    const ColQuery q = make_query(x, y, xy_scale);
+    Top2 t{0.0f, 0.0f, -1, -1, -1, -1};
+    int m = 0;
+    int bx0, bx1, by0, by1;
+    if (q.lo_x != q.lo_x || q.hi_x != q.hi_x || q.lo_y != q.lo_y || q.hi_y != q.hi_y) {
+        bx0 = 0;  // NaN bounds pass every column (every comparison is false): scan all
+        bx1 = g.bw - 1;
+        by0 = 0;
+        by1 = g.bh - 1;
+    } else {
+        bx0 = (int)fminf(fmaxf(floorf(q.lo_x * g.inv_e), 0.0f), (float)(g.bw - 1));
+        bx1 = (int)fminf(fmaxf(floorf(q.hi_x * g.inv_e), 0.0f), (float)(g.bw - 1));
+        by0 = (int)fminf(fmaxf(floorf(q.lo_y * g.inv_e), 0.0f), (float)(g.bh - 1));
+        by1 = (int)fminf(fmaxf(floorf(q.hi_y * g.inv_e), 0.0f), (float)(g.bh - 1));
+    }
+    const int nseg = (by1 - by0 + 1) + 1;  // bucket rows + the NaN bucket
+    for (int sb = 0; sb < nseg; sb += 64) {
+        const int r = sb + lane;
+        int st = 0, len = 0;
+        if (r < nseg) {
+            int lo, hi;
+            if (r == nseg - 1) {
+                lo = g.nb - 1;
+                hi = g.nb;
+            } else {
+                const int row = by0 + r;
+                lo = row * g.bw + bx0;
+                hi = row * g.bw + bx1 + 1;
+            }
+            st = off[lo];
+            len = off[hi] - st;
+        }
+        const int incl = wave_incl_scan(len);
+        const int total = __shfl(incl, 63);
+        L.seg_st[lane] = st;
+        L.seg_pre[lane] = incl - len;
+        __syncthreads();
+        const int ng = min(64, nseg - sb);
+        for (int tt = lane; tt < total; tt += 64) {
+            int lo = 0, hi = ng - 1;  // largest segment whose start prefix <= tt
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (L.seg_pre[mid] <= tt)
+                    lo = mid;
+                else
+                    hi = mid - 1;
+            }
+            const int k = L.seg_st[lo] + tt - L.seg_pre[lo];
+            consider<MAXM>(cf, hw, q, k, __float_as_int(cf[9 * hw + k]), t, m);
+        }
+        __syncthreads();
+    }
+    finish_connection<MAXM>(cf, hw, t, m, out);
+}
+
 __device__ __forceinline__ float max0(float v) { return (v > 0.0f) ? v : 0.0f; }
 
 __device__ __forceinline__ const float *col_set(const GrowArgs &g, int set, int img, int caf_i,
                                                 int dir) {
-    return g.cols[set] + (((int64_t)img * g.C + caf_i) * 2 + dir) * 9 * g.hw;
+    return g.cols[set] + (((int64_t)img * g.C + caf_i) * 2 + dir) * 10 * g.hw;
 }
 
-__device__ __forceinline__ int col_count(const GrowArgs &g, int set, int img, int caf_i, int dir) {
-    return g.col_counts[set][((int64_t)img * g.C + caf_i) * 2 + dir];
+__device__ __forceinline__ const int *col_offs(const GrowArgs &g, int set, int img, int caf_i,
+                                               int dir) {
+    return g.offs[set] + (((int64_t)img * g.C + caf_i) * 2 + dir) * (int64_t)(g.nb + 1);
 }
 
 // cifcaf.py:194-217
@@ -335,18 +457,17 @@ __device__ void connection_value(const GrowArgs &g, GrowLDS &L, int img, int set
         if (L.bs_k[start_i][t] == end_i) e = t;
     const int caf_i = L.bs_caf[start_i][e];
     const int fwd = L.bs_fwd[start_i][e];
-    const float *cf = col_set(g, set, img, caf_i, fwd ? 1 : 0);
-    const float *cb = col_set(g, set, img, caf_i, fwd ? 0 : 1);
-    const int nf = col_count(g, set, img, caf_i, fwd ? 1 : 0);
-    const int nb = col_count(g, set, img, caf_i, fwd ? 0 : 1);
+    const int df = fwd ? 1 : 0, db = fwd ? 0 : 1;
     const float xv0 = L.a.data[start_i][0], xv1 = L.a.data[start_i][1], xv2 = L.a.data[start_i][2];
     const float xy_scale_s = max0(L.a.joint_scales[start_i]);
     const bool maxm = g.cfg.connection_method == 1;
     float nx[4];
     if (maxm)
-        grow_connection<true>(cf, nf, g.hw, xv0, xv1, xy_scale_s, nx);
+        grow_connection<true>(g, L, col_set(g, set, img, caf_i, df), col_offs(g, set, img, caf_i, df),
+                              xv0, xv1, xy_scale_s, nx);
     else
-        grow_connection<false>(cf, nf, g.hw, xv0, xv1, xy_scale_s, nx);
+        grow_connection<false>(g, L, col_set(g, set, img, caf_i, df),
+                               col_offs(g, set, img, caf_i, df), xv0, xv1, xy_scale_s, nx);
     out[0] = out[1] = out[2] = out[3] = 0.0f;
     const float ks = sqrtf(nx[3] * xv2);  // geometric mean
     if (ks < g.cfg.keypoint_threshold) return;
@@ -355,9 +476,11 @@ __device__ void connection_value(const GrowArgs &g, GrowLDS &L, int img, int set
     if (reverse_match) {
         float rv[4];
         if (maxm)
-            grow_connection<true>(cb, nb, g.hw, nx[0], nx[1], xy_scale_t, rv);
+            grow_connection<true>(g, L, col_set(g, set, img, caf_i, db),
+                                  col_offs(g, set, img, caf_i, db), nx[0], nx[1], xy_scale_t, rv);
         else
-            grow_connection<false>(cb, nb, g.hw, nx[0], nx[1], xy_scale_t, rv);
+            grow_connection<false>(g, L, col_set(g, set, img, caf_i, db),
+                                   col_offs(g, set, img, caf_i, db), nx[0], nx[1], xy_scale_t, rv);
         if (rv[2] == 0.0f) return;  // tests the SCALE (cifcaf.py:212)
         if (fabsf(xv0 - rv[0]) + fabsf(xv1 - rv[1]) > xy_scale_s) return;
     }
@@ -495,54 +618,95 @@ struct OccGrid {
 
 __device__ __forceinline__ long round_half_even(float x) { return (long)rintf(x); }
 
+// Occupancy.get (occupancy.py:41-47): nonzero at floor((x, y) / reduction), clipped
 __device__ bool occ_get(const OccGrid &o, int f, float x, float y, float red) {
     if (f >= o.f) return true;
-    if (o.h <= 0 || o.w <= 0) return false;
+    if (o.h <= 0 || o.w <= 0) return false;  // the reference reads out of bounds here
     x = clip_ref(x / red, 0.0f, (float)(o.w - 1));
     y = clip_ref(y / red, 0.0f, (float)(o.h - 1));
     const int xi = (int)x, yi = (int)y;
-    const uint8_t v = o.p[((int64_t)f * o.h + yi) * o.w + xi];
-    return v != 0;
+    return o.p[((int64_t)f * o.h + yi) * o.w + xi] != 0;
 }
 
-__device__ void occ_set(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccGrid &o, int f,
-                        float x, float y, float sigma) {
-    if (f >= o.f) return;
+// Occupancy.set box (occupancy.py:31-39 + utils.py:61-66) of joint f; false when empty
+__device__ bool occ_box(const GrowArgs &g, const OccGrid &o, int f, float x, float y, float sigma,
+                        int box[4]) {
+    if (f >= o.f) return false;
     const float red = (float)g.cfg.occupancy_reduction;
     const float msr = (float)((double)g.cfg.occupancy_min_scale / g.cfg.occupancy_reduction);
-    const long xi = round_half_even(x / red);
-    const long yi = round_half_even(y / red);
+    const long xi = (long)rintf(x / red);  // round(): half to even
+    const long yi = (long)rintf(y / red);
     const float sr = sigma / red;
-    const long si = round_half_even((sr > msr) ? sr : msr);
+    const long si = (long)rintf((sr > msr) ? sr : msr);  // max(min_scale_reduced, sigma / r)
     const long minx = xi - si > 0 ? xi - si : 0;
     const long miny = yi - si > 0 ? yi - si : 0;
     const long mx = xi + si + 1 < o.w ? xi + si + 1 : o.w;
     const long my = yi + si + 1 < o.h ? yi + si + 1 : o.h;
     long maxx = minx + 1 > mx ? minx + 1 : mx;
     long maxy = miny + 1 > my ? miny + 1 : my;
-    if (maxx > o.w) maxx = o.w;
+    if (maxx > o.w) maxx = o.w;  // numpy slice clipping
     if (maxy > o.h) maxy = o.h;
-    if (minx >= maxx || miny >= maxy) return;
-    const int bw = (int)(maxx - minx), bh = (int)(maxy - miny);
-    uint8_t *base = o.p + (int64_t)f * o.h * o.w;
-    for (int t = threadIdx.x & 63; t < bw * bh; t += 64) {
-        const int yy = (int)miny + t / bw, xx = (int)minx + t % bw;
-        uint8_t *c = &base[(int64_t)yy * o.w + xx];
+    if (minx >= maxx || miny >= maxy) return false;
+    box[0] = (int)minx;
+    box[1] = (int)maxx;
+    box[2] = (int)miny;
+    box[3] = (int)maxy;
+    return true;
+}
+
+// Mark the boxes of every joint j with mark(j) in one pass: joints live on different
+// occupancy planes, so the per-joint `+= 1` boxes are independent and spread over the 64
+// lanes.  Each marked box is logged for occ_clear.  Collective (all 64 lanes).
+template <typename MarkFn>
+__device__ void occ_mark(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccGrid &o,
+                         const float (*xy)[3], const float *scales, int K, MarkFn mark) {
+    const int lane = threadIdx.x & 63;
+    int box[4] = {0, 0, 0, 0};
+    bool has = false;
+    if (lane < K && mark(lane)) has = occ_box(g, o, lane, xy[lane][0], xy[lane][1], scales[lane], box);
+    const int area = has ? (box[1] - box[0]) * (box[3] - box[2]) : 0;
+    const int incl = wave_incl_scan(area);
+    const int total = __shfl(incl, 63);
+    const uint64_t hm = __ballot(has);
+    if (lane < K) {
+        L.mark_pre[lane] = incl - area;
+        L.mark_box[lane][0] = box[0];
+        L.mark_box[lane][1] = box[1];
+        L.mark_box[lane][2] = box[2];
+        L.mark_box[lane][3] = box[3];
+        if (has) {
+            const int li = L.log_n + lane_prefix(hm);
+            if (li < g.log_cap) {
+                OccLog e;
+                e.f = lane;
+                e.x0 = (int16_t)box[0];
+                e.x1 = (int16_t)box[1];
+                e.y0 = (int16_t)box[2];
+                e.y1 = (int16_t)box[3];
+                log[li] = e;
+            }
+        }
+    }
+    __syncthreads();
+    for (int t = lane; t < total; t += 64) {
+        int lo = 0, hi = K - 1;  // largest joint whose area prefix <= t
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (L.mark_pre[mid] <= t)
+                lo = mid;
+            else
+                hi = mid - 1;
+        }
+        const int u = t - L.mark_pre[lo];
+        const int bw = L.mark_box[lo][1] - L.mark_box[lo][0];
+        const int yy = L.mark_box[lo][2] + u / bw, xx = L.mark_box[lo][0] + u % bw;
+        uint8_t *c = &o.p[((int64_t)lo * o.h + yy) * o.w + xx];
         *c = (uint8_t)(*c + 1);
     }
-    const int li = L.log_n;
-    if (li < g.log_cap) {
-        OccLog e;
-        e.f = f;
-        e.x0 = (int16_t)minx;
-        e.x1 = (int16_t)maxx;
-        e.y0 = (int16_t)miny;
-        e.y1 = (int16_t)maxy;
-        if ((threadIdx.x & 63) == 0) log[li] = e;
-    } else {
-        L.status |= PP_ST_NMS_OVERFLOW;
-    }
-    L.log_n = li + 1;
+    const int nm = __popcll(hm);
+    if (L.log_n + nm > g.log_cap) L.status |= PP_ST_NMS_OVERFLOW;
+    __syncthreads();
+    L.log_n = L.log_n + nm;
     __syncthreads();
 }
 
@@ -550,57 +714,67 @@ __device__ void occ_set(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccGri
 __device__ void occ_clear(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccGrid &o) {
     __syncthreads();
     const int n = L.log_n < g.log_cap ? L.log_n : g.log_cap;
-    for (int e = 0; e < n; e++) {
-        const OccLog l = log[e];
-        const int bw = l.x1 - l.x0, bh = l.y1 - l.y0;
-        uint8_t *base = o.p + (int64_t)l.f * o.h * o.w;
-        for (int t = threadIdx.x & 63; t < bw * bh; t += 64) {
-            const int yy = l.y0 + t / bw, xx = l.x0 + t % bw;
-            base[(int64_t)yy * o.w + xx] = 0;
+    const int lane = threadIdx.x & 63;
+    for (int e0 = 0; e0 < n; e0 += 64) {  // 64 boxes per round, one per lane
+        const int e = e0 + lane;
+        OccLog l{0, 0, 0, 0, 0};
+        if (e < n) l = log[e];
+        const int area = (e < n) ? (l.x1 - l.x0) * (l.y1 - l.y0) : 0;
+        for (int t = 0; t < area; t++) {
+            const int bw = l.x1 - l.x0;
+            o.p[((int64_t)l.f * o.h + l.y0 + t / bw) * o.w + l.x0 + t % bw] = 0;
         }
     }
     L.log_n = 0;
     __syncthreads();
 }
 
-// NumPy pairwise summation (n <= 128 path) of a float64 array
-__device__ double pw_sum(const double *a, int n) {
-    if (n < 8) {
-        double res = 0.0;
-        for (int i = 0; i < n; i++) res += a[i];
-        return res;
-    }
-    double r[8];
-    for (int j = 0; j < 8; j++) r[j] = a[j];
-    int i;
-    for (i = 8; i < n - (n % 8); i += 8)
-        for (int j = 0; j < 8; j++) r[j] += a[i + j];
-    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-    for (; i < n; i++) res += a[i];
-    return res;
-}
-
-// Annotation.score() (annotation.py:24-28, 60-71), float64
-__device__ double ann_score(const pp_ann &a, int K) {
-    float v[kKP];
-    double w[kKP], prod[kKP];
-    for (int i = 0; i < K; i++) {
-        v[i] = a.data[i][2];
-        w[i] = (i < 3) ? 3.0 : 1.0;
-    }
-    const double ws = pw_sum(w, K);
-    for (int i = 0; i < K; i++) w[i] /= ws;
-    for (int i = 1; i < K; i++) {  // insertion sort descending
-        const float x = v[i];
-        int j = i - 1;
-        while (j >= 0 && v[j] < x) {
-            v[j + 1] = v[j];
-            j--;
+// Annotation.score() (annotation.py:24-28, 60-71) in float64, collective over the wave:
+// lane j finds the rank of v_j in descending order, the rank-ordered products go to LDS
+// and NumPy's pairwise summation (n <= 128 path) adds them in its fixed order.
+__device__ double ann_score(GrowLDS &L, const float (*data)[3], int K) {
+    const int lane = threadIdx.x & 63;
+    const double ws = (double)(3 * min(K, 3) + (K - min(K, 3)));  // np.sum(weights): exact
+    if (lane < K) {
+        const float vj = data[lane][2];
+        int rank = 0;
+        for (int i = 0; i < K; i++) {
+            const float vi = data[i][2];
+            rank += (vi > vj) || (vi == vj && i < lane);
         }
-        v[j + 1] = x;
+        const double w = (rank < 3 ? 3.0 : 1.0) / ws;
+        L.prod[rank] = w * (double)vj;
     }
-    for (int i = 0; i < K; i++) prod[i] = w[i] * (double)v[i];
-    return pw_sum(prod, K);
+    __syncthreads();
+    if (lane == 0) {
+        const double *a = L.prod;
+        double res;
+        if (K < 8) {
+            res = 0.0;
+            for (int i = 0; i < K; i++) res += a[i];
+        } else {
+            double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6],
+                   r7 = a[7];
+            int i;
+            for (i = 8; i < K - (K % 8); i += 8) {
+                r0 += a[i];
+                r1 += a[i + 1];
+                r2 += a[i + 2];
+                r3 += a[i + 3];
+                r4 += a[i + 4];
+                r5 += a[i + 5];
+                r6 += a[i + 6];
+                r7 += a[i + 7];
+            }
+            res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+            for (; i < K; i++) res += a[i];
+        }
+        L.score_bc = res;
+    }
+    __syncthreads();
+    const double res = L.score_bc;
+    __syncthreads();
+    return res;
 }
 
 __device__ void copy_ann(pp_ann *dst, const pp_ann *src) {
@@ -643,6 +817,7 @@ __device__ void sort_by_score(int *perm, int np, int n, const double *score) {
 // ---------------------------------------------------------------------------------------
 // the per-image decode kernel
 // ---------------------------------------------------------------------------------------
+template <int PHASE>
 __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
     __shared__ GrowLDS L;
     const int img = blockIdx.x;
@@ -666,58 +841,100 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
                 L.bs_fwd[s][pos] = (uint8_t)ins[t][2];
             }
         }
-        L.status = 0;
+        L.status = PHASE == 1 ? 0 : g.status[img];
         L.log_n = 0;
     }
     __syncthreads();
 
+    STAMP_DECL
     uint8_t *occ_base = g.occ + (int64_t)img * g.occ_cap;
     OccLog *log = g.log + (int64_t)img * g.log_cap;
     pp_ann *work = g.work + (int64_t)img * g.ann_cap;
     const float red = (float)g.cfg.occupancy_reduction;
 
-    // ---- seed loop (cifcaf.py:84-108) ----
-    OccGrid occ{occ_base, K, (int)((double)g.hh / g.cfg.occupancy_reduction),
-                (int)((double)g.ww / g.cfg.occupancy_reduction)};
-    const int n_seeds = min(g.seed_counts[img], g.seed_cap);
-    const pp_seed *seeds = g.seeds + (int64_t)img * g.seed_cap;
-    int n_anns = 0;
-    for (int s = 0; s < n_seeds; s++) {
-        const pp_seed sd = seeds[s];
-        if (occ_get(occ, sd.field, sd.x, sd.y, red)) continue;
-        if (n_anns >= g.ann_cap) {
-            L.status |= PP_ST_ANN_OVERFLOW;
-            break;
-        }
-        // Annotation(keypoints, out_skeleton).add(f, (x, y, v)); joint_scales[f] = s
-        {
-            uint32_t *z = reinterpret_cast<uint32_t *>(&L.a);
-            for (int t = lane; t < (int)(sizeof(pp_ann) / 4); t += 64) z[t] = 0u;
+    if (PHASE == 1) {
+        // ---- seed loop (cifcaf.py:84-108) ----
+        // The occupancy grid only changes when an annotation is created, so the occupancy
+        // test of the next 64 seeds runs in parallel (one lane each) and the first free seed
+        // starts the next annotation; the occupied ones before it are skipped exactly as the
+        // sequential loop skips them.
+        OccGrid occ{occ_base, K, (int)((double)g.hh / g.cfg.occupancy_reduction),
+                    (int)((double)g.ww / g.cfg.occupancy_reduction)};
+        const int n_seeds = min(g.seed_counts[img], g.seed_cap);
+        const pp_seed *seeds = g.seeds + (int64_t)img * g.seed_cap;
+        int n_anns = 0;
+        bool need_complete = false;
+        int s = 0;
+        while (s < n_seeds) {
+            const int idx = s + lane;
+            bool is_free = false;
+            if (idx < n_seeds) {
+                const pp_seed c = seeds[idx];
+                is_free = !occ_get(occ, c.field, c.x, c.y, red);
+            }
+            const uint64_t m = __ballot(is_free);
+            STAMP(0);
+            if (m == 0) {
+                s += 64;
+                continue;
+            }
+            const int si = s + __ffsll((unsigned long long)m) - 1;
+            s = si + 1;
+            const pp_seed sd = seeds[si];
+            if (n_anns >= g.ann_cap) {
+                L.status |= PP_ST_ANN_OVERFLOW;
+                break;
+            }
+            // Annotation(keypoints, out_skeleton).add(f, (x, y, v)); joint_scales[f] = s
+            {
+                uint32_t *z = reinterpret_cast<uint32_t *>(&L.a);
+                for (int t = lane; t < (int)(sizeof(pp_ann) / 4); t += 64) z[t] = 0u;
+                __syncthreads();
+            }
+            if (lane == 0) {
+                L.a.n_keypoints = K;
+                L.a.image = img;
+                L.a.data[sd.field][0] = sd.x;
+                L.a.data[sd.field][1] = sd.y;
+                L.a.data[sd.field][2] = sd.v;
+                L.a.joint_scales[sd.field] = sd.s;
+            }
             __syncthreads();
+            STAMP(1);
+            grow(g, L, img, 0, true);
+            __syncthreads();
+            STAMP(2);
+            copy_ann(&work[n_anns], &L.a);
+            n_anns++;
+            STAMP(3);
+            // mark_occupied (cifcaf.py:87-93): every joint with v != 0, in one pass
+            for (int j = 0; j < K; j++) need_complete = need_complete || L.a.data[j][2] == 0.0f;
+            occ_mark(g, L, log, occ, L.a.data, L.a.joint_scales, K,
+                     [&](int j) { return L.a.data[j][2] != 0.0f; });
+            STAMP(4);
         }
+        occ_clear(g, L, log, occ);
+        __syncthreads();
+        STAMP(5);
+        STAMP_FLUSH(1);
         if (lane == 0) {
-            L.a.n_keypoints = K;
-            L.a.image = img;
-            L.a.data[sd.field][0] = sd.x;
-            L.a.data[sd.field][1] = sd.y;
-            L.a.data[sd.field][2] = sd.v;
-            L.a.joint_scales[sd.field] = sd.s;
+            g.n_work[img] = n_anns;
+            g.need_complete[img] = (g.cfg.force_complete && need_complete) ? 1 : 0;
+            g.status[img] = L.status;
         }
-        __syncthreads();
-        grow(g, L, img, 0, true);
-        __syncthreads();
-        copy_ann(&work[n_anns], &L.a);
-        n_anns++;
-        for (int j = 0; j < K; j++) {  // mark_occupied (cifcaf.py:87-93)
-            if (L.a.data[j][2] == 0.0f) continue;
-            occ_set(g, L, log, occ, j, L.a.data[j][0], L.a.data[j][1], L.a.joint_scales[j]);
-        }
+        return;
     }
-    occ_clear(g, L, log, occ);
+    const int n_anns = g.n_work[img];
+    STAMP(0);
 
     // ---- complete_annotations (cifcaf.py:333-351) ----
-    if (g.cfg.force_complete) {
+    // Annotations with every joint set are unchanged by it (their frontier is empty), so
+    // only images flagged by phase 1 run it, and only on annotations with a zero joint.
+    if (g.cfg.force_complete && g.need_complete[img]) {
         for (int i = 0; i < n_anns; i++) {
+            bool has0 = false;
+            for (int j = 0; j < K; j++) has0 = has0 || work[i].data[j][2] == 0.0f;
+            if (!has0) continue;
             copy_ann(&L.a, &work[i]);
             bool unfilled[kKP];
             for (int j = 0; j < K; j++) unfilled[j] = L.a.data[j][2] == 0.0f;
@@ -734,6 +951,7 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
         }
     }
 
+    STAMP(1);
     int n_out = n_anns;
     int *keep = g.nms_idx + (int64_t)img * (2 * g.ann_cap + g.ann_np);  // kept work indices
     int *surv = keep + g.ann_cap;                                          // survivors
@@ -754,7 +972,7 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
                 a.data[lane][2] = 0.0f;
             }
             __syncthreads();
-            const double sc = ann_score(a, K);
+            const double sc = ann_score(L, a.data, K);
             if (sc >= it) {
                 float ax = a.data[0][0], ay = a.data[0][1];
                 for (int j = 1; j < K; j++) {
@@ -771,6 +989,7 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
             }
         }
         __syncthreads();
+        STAMP(2);
         n_out = 0;
         if (m > 0) {
             // Occupancy((K, int(max y + 1), int(max x + 1)), 2, min_scale=4)  (nms.py:27-31)
@@ -783,23 +1002,24 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
                 int np = 1;
                 while (np < m) np <<= 1;
                 sort_by_score(perm, np, m, score);  // nms.py:33 (stable)
-                for (int r = 0; r < m; r++) {       // nms.py:34-45
+                STAMP(3);
+                for (int r = 0; r < m; r++) {  // nms.py:34-45
                     pp_ann &a = work[keep[perm[r]]];
-                    for (int f = 0; f < K; f++) {
-                        const float v = a.data[f][2];
-                        if (v == 0.0f) continue;
-                        const bool occd = occ_get(no, f, a.data[f][0], a.data[f][1], red);
-                        __syncthreads();
-                        if (occd) {
-                            if (lane == 0) a.data[f][2] = v * g.cfg.nms_suppression;
-                            __syncthreads();
-                        } else {
-                            occ_set(g, L, log, no, f, a.data[f][0], a.data[f][1],
-                                    a.joint_scales[f]);
-                        }
-                    }
+                    // joints sit on separate occupancy planes: test all in parallel, then
+                    // suppress the occupied ones and mark the free ones
+                    bool occd = false;
+                    if (lane < K && a.data[lane][2] != 0.0f)
+                        occd = occ_get(no, lane, a.data[lane][0], a.data[lane][1], red);
+                    const uint64_t om = __ballot(occd);
+                    __syncthreads();
+                    if (occd) a.data[lane][2] = a.data[lane][2] * g.cfg.nms_suppression;
+                    occ_mark(g, L, log, no, a.data, a.joint_scales, K, [&](int j) {
+                        return !((om >> j) & 1ull) && a.data[j][2] != 0.0f;
+                    });
                 }
+                STAMP(4);
                 occ_clear(g, L, log, no);
+                STAMP(5);
                 int m2 = 0;
                 for (int r = 0; r < m; r++) {  // nms.py:51-53, in sorted order
                     const int wi = keep[perm[r]];
@@ -810,18 +1030,21 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
                         a.data[lane][2] = 0.0f;
                     }
                     __syncthreads();
-                    const double sc = ann_score(a, K);
+                    const double sc = ann_score(L, a.data, K);
                     if (sc >= it) {
-                        if (lane == 0) surv[m2] = wi;
+                        if (lane == 0) {
+                            surv[m2] = wi;
+                            score[m2] = sc;
+                        }
                         m2++;
                     }
                 }
                 __syncthreads();
-                for (int r = lane; r < m2; r += 64) score[r] = ann_score(work[surv[r]], K);
-                __syncthreads();
+                STAMP(6);
                 int np2 = 1;
                 while (np2 < m2) np2 <<= 1;
                 if (m2 > 0) sort_by_score(perm, np2, m2, score);  // nms.py:54
+                STAMP(7);
                 for (int r = 0; r < m2; r++) {
                     copy_ann(&out[r], &work[surv[perm[r]]]);
                     if (lane == 0) out[r].score = score[perm[r]];
@@ -832,11 +1055,13 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
     } else {
         for (int i = 0; i < n_anns; i++) {
             copy_ann(&out[i], &work[i]);
-            const double sc = ann_score(work[i], K);
+            const double sc = ann_score(L, work[i].data, K);
             if (lane == 0) out[i].score = sc;
         }
     }
     __syncthreads();
+    STAMP(8);
+    STAMP_FLUSH(2);
     if (lane == 0) {
         g.counts[img] = n_out;
         g.status[img] = L.status;
@@ -854,9 +1079,10 @@ int launch_seeds(const float *cif, const float *hr, int n_img, int K, int H, int
                  const pp_config *cfg, pp_seed *seeds, int cap, int *counts, void *scratch,
                  hipStream_t s);
 size_t seeds_scratch_size(int n_img, int cap);
-int launch_caf_scored(const float *caf, const float *hr, int n_img, int K, int C, int H, int W,
-                      const int32_t *skeleton, const pp_config *cfg, int nt, const float *th,
-                      float *const *cols, int *const *counts, hipStream_t s);
+int launch_caf_bucketed(const float *caf, const float *hr, int n_img, int K, int C, int H, int W,
+                        const int32_t *skeleton, const pp_config *cfg, float th, float *cols,
+                        int *offs, const int *gate, hipStream_t s);
+void caf_bucket_grid(int H, int W, int stride, int *bw, int *bh, int *nb, float *inv_e);
 
 static inline size_t align_up(size_t a) { return (a + 255) / 256 * 256; }
 
@@ -864,9 +1090,12 @@ struct DecodeLayout {
     int hh, ww;
     int64_t pitch, hw;
     int seed_cap, ann_cap, ann_np, log_cap;
+    int bw, bh, nb;
+    float inv_e;
     int64_t occ_cap;
     size_t off_cifhr, off_cifhr_ws, off_seeds, off_seed_counts, off_seed_ws, off_cols[2],
-        off_col_counts[2], off_occ, off_log, off_work, off_nms_score, off_nms_idx, total;
+        off_offs[2], off_n_work, off_need, off_occ, off_log, off_work, off_nms_score,
+        off_nms_idx, total;
     size_t cifhr_ws_bytes;
 };
 
@@ -898,11 +1127,14 @@ static DecodeLayout make_layout(int n_img, int K, int C, int H, int W, const pp_
     d.off_seeds = take(n * d.seed_cap * sizeof(pp_seed));
     d.off_seed_counts = take(n * sizeof(int));
     d.off_seed_ws = take(seeds_scratch_size(n_img, d.seed_cap));
+    caf_bucket_grid(H, W, cfg->stride, &d.bw, &d.bh, &d.nb, &d.inv_e);
     for (int t = 0; t < 2; t++) {
         const bool used = t == 0 || cfg->force_complete;
-        d.off_cols[t] = take(used ? n * C * 2 * 9 * d.hw * sizeof(float) : 0);
-        d.off_col_counts[t] = take(used ? n * C * 2 * sizeof(int) : 0);
+        d.off_cols[t] = take(used ? n * C * 2 * 10 * d.hw * sizeof(float) : 0);
+        d.off_offs[t] = take(used ? n * C * 2 * (d.nb + 1) * sizeof(int) : 0);
     }
+    d.off_n_work = take(n * sizeof(int));
+    d.off_need = take(n * sizeof(int));
     d.off_occ = take(n * d.occ_cap);
     d.off_log = take(n * d.log_cap * sizeof(OccLog));
     d.off_work = take(n * ann_cap * sizeof(pp_ann));
@@ -957,7 +1189,7 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
     pp_seed *seeds = (pp_seed *)(ws + d.off_seeds);
     int *seed_counts = (int *)(ws + d.off_seed_counts);
     float *cols[2] = {(float *)(ws + d.off_cols[0]), (float *)(ws + d.off_cols[1])};
-    int *col_counts[2] = {(int *)(ws + d.off_col_counts[0]), (int *)(ws + d.off_col_counts[1])};
+    int *offs[2] = {(int *)(ws + d.off_offs[0]), (int *)(ws + d.off_offs[1])};
     int rc = PP_OK;
     if (stages & 1u) {
         rc = pp_cifhr(d_cif, n_img, K, H, W, cfg, hr, ws + d.off_cifhr_ws, d.cifhr_ws_bytes, s);
@@ -968,10 +1200,9 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
                           ws + d.off_seed_ws, s);
         if (rc) return rc;
     }
-    if (stages & 4u) {
-        const float th[2] = {cfg->caf_threshold, cfg->complete_caf_threshold};
-        rc = launch_caf_scored(d_caf, hr, n_img, K, C, H, W, skeleton, cfg,
-                               cfg->force_complete ? 2 : 1, th, cols, col_counts, s);
+    if (stages & 4u) {  // CafScored at caf_threshold; the force-complete set is lazy
+        rc = launch_caf_bucketed(d_caf, hr, n_img, K, C, H, W, skeleton, cfg, cfg->caf_threshold,
+                                 cols[0], offs[0], nullptr, s);
         if (rc) return rc;
     }
     if (stages & 8u) {
@@ -981,8 +1212,12 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
         g.seed_cap = d.seed_cap;
         g.cols[0] = cols[0];
         g.cols[1] = cols[1];
-        g.col_counts[0] = col_counts[0];
-        g.col_counts[1] = col_counts[1];
+        g.offs[0] = offs[0];
+        g.offs[1] = offs[1];
+        g.bw = d.bw;
+        g.bh = d.bh;
+        g.nb = d.nb;
+        g.inv_e = d.inv_e;
         g.K = K;
         g.C = C;
         g.H = H;
@@ -1001,11 +1236,42 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
         g.nms_idx = (int *)(ws + d.off_nms_idx);
         g.ann_np = d.ann_np;
         g.ann_cap = ann_capacity;
+        g.stamps = nullptr;
+#ifdef PP_STAMPS
+        hipMalloc((void **)&g.stamps, (size_t)n_img * 2 * 12 * sizeof(uint64_t));
+        hipMemsetAsync(g.stamps, 0, (size_t)n_img * 2 * 12 * sizeof(uint64_t), s);
+#endif
+        g.n_work = (int *)(ws + d.off_n_work);
+        g.need_complete = (int *)(ws + d.off_need);
         g.out = d_anns;
         g.counts = d_counts;
         g.status = d_status;
-        hipLaunchKernelGGL(grow_kernel, dim3(n_img), dim3(64), 0, s, g);
-        rc = check_launch("pp_decode_batch(grow)");
+        hipLaunchKernelGGL(grow_kernel<1>, dim3(n_img), dim3(64), 0, s, g);
+        rc = check_launch("pp_decode_batch(seed loop)");
+        if (rc) return rc;
+        if (cfg->force_complete) {
+            // complete_annotations' CafScored(score_th=0.0001) only where phase 1 left work
+            rc = launch_caf_bucketed(d_caf, hr, n_img, K, C, H, W, skeleton, cfg,
+                                     cfg->complete_caf_threshold, cols[1], offs[1],
+                                     g.need_complete, s);
+            if (rc) return rc;
+        }
+        hipLaunchKernelGGL(grow_kernel<2>, dim3(n_img), dim3(64), 0, s, g);
+        rc = check_launch("pp_decode_batch(complete + nms)");
+#ifdef PP_STAMPS
+        hipStreamSynchronize(s);
+        const size_t nst = (size_t)n_img * 2 * 12;
+        uint64_t *h = (uint64_t *)malloc(nst * sizeof(uint64_t));
+        hipMemcpy(h, g.stamps, nst * sizeof(uint64_t), hipMemcpyDeviceToHost);
+        const char *path = getenv("PP_STAMPS_OUT");
+        FILE *fo = fopen(path ? path : "pp_stamps.bin", "ab");
+        if (fo) {
+            fwrite(h, sizeof(uint64_t), nst, fo);
+            fclose(fo);
+        }
+        free(h);
+        hipFree(g.stamps);
+#endif
     }
     return rc;
 }
@@ -1030,7 +1296,7 @@ __global__ __launch_bounds__(64) void grow_connection_kernel(const float *cf, in
                                                              float x, float y, float xy_scale,
                                                              float *out) {
     float r[4];
-    grow_connection<MAXM>(cf, n, pitch, x, y, xy_scale, r);
+    grow_connection_flat<MAXM>(cf, n, pitch, x, y, xy_scale, r);
     if (threadIdx.x < 4) out[threadIdx.x] = r[threadIdx.x];
 }
 }  // namespace pp

@@ -48,12 +48,20 @@ __device__ __forceinline__ int4 splat_box(float cx, float cy, float ext, int h, 
 // -------------------------------------------------------------------------------------
 // K1: CIF cells -> splat records (cif_hr.py:26-40)
 // -------------------------------------------------------------------------------------
+constexpr int kTileBits = 1024;  // per-field tile bitmap capacity (32x32 tiles of 64x64 px)
+
 __global__ __launch_bounds__(256) void cifhr_splats_kernel(const float *__restrict__ cif, int H,
                                                            int W, int hh, int ww, float stride,
                                                            float v_th, float neighbors,
                                                            Splat *__restrict__ splats,
-                                                           int *__restrict__ counts) {
+                                                           int *__restrict__ counts,
+                                                           uint32_t *__restrict__ tile_bits,
+                                                           int tiles_x, int tiles) {
     __shared__ int s_tmp[4];
+    __shared__ uint32_t s_bits[kTileBits / 32];
+    const bool use_bits = tiles <= kTileBits;
+    if (threadIdx.x < kTileBits / 32) s_bits[threadIdx.x] = 0u;
+    __syncthreads();
     const int64_t fld = blockIdx.x;  // image * K + field
     const int hw = H * W;
     const float *p = cif + fld * 5 * (int64_t)hw;
@@ -76,10 +84,20 @@ __global__ __launch_bounds__(256) void cifhr_splats_kernel(const float *__restri
             s.box = splat_box<M_GAUSS_MAX>(x, y, 1.0f * sigma, hh, ww);
             s.par = make_float4(x, y, v, sigma * sigma);
             out[running + slot] = s;
+            if (use_bits) {  // mark the 64x64 output tiles this splat's box touches
+                for (int ty = s.box.z / kTile; ty <= (s.box.w - 1) / kTile; ty++)
+                    for (int tx = s.box.x / kTile; tx <= (s.box.y - 1) / kTile; tx++) {
+                        const int t = ty * tiles_x + tx;
+                        atomicOr(&s_bits[t >> 5], 1u << (t & 31));
+                    }
+            }
         }
         running += total;
     }
     if (threadIdx.x == 0) counts[fld] = running;
+    __syncthreads();
+    if (threadIdx.x < kTileBits / 32)
+        tile_bits[fld * (kTileBits / 32) + threadIdx.x] = use_bits ? s_bits[threadIdx.x] : ~0u;
 }
 
 // -------------------------------------------------------------------------------------
@@ -117,6 +135,7 @@ struct TileArgs {
     float *field2;          // cumw for M_CUMAVG
     const Splat *splats;    // n_fields * splat_cap
     const int *counts;      // per field splat count (NULL: n_splats)
+    const uint32_t *tile_bits;  // per field kTileBits bitmap of non-empty tiles (or NULL)
     int64_t splat_cap;
     int64_t n_splats;
     int64_t field_stride;   // elements between fields
@@ -176,7 +195,10 @@ __global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
     const int tx0 = (tile % a.tiles_x) * kTile;
     const int ty0 = (tile / a.tiles_x) * kTile;
     const Splat *sp = a.splats + fld * a.splat_cap;
-    const int64_t ns = a.counts ? (int64_t)a.counts[fld] : a.n_splats;
+    int64_t ns = a.counts ? (int64_t)a.counts[fld] : a.n_splats;
+    if (ZERO_INIT && a.tile_bits &&
+        !((a.tile_bits[fld * (kTileBits / 32) + (tile >> 5)] >> (tile & 31)) & 1u))
+        ns = 0;  // no splat touches this tile: pure zero fill
     float *out = a.field + fld * a.field_stride;
     float *out2 = (MODE == M_CUMAVG) ? a.field2 + fld * a.field_stride : nullptr;
 
@@ -308,7 +330,8 @@ int64_t pp_cifhr_pitch(int64_t w_hr) { return round_up(w_hr, 32); }
 size_t pp_cifhr_workspace_size(int32_t n_img, int32_t K, int32_t H, int32_t W) {
     const size_t nf = (size_t)n_img * K;
     return round_up((int64_t)(nf * (size_t)H * W * sizeof(Splat)), 256) +
-           round_up((int64_t)(nf * sizeof(int)), 256);
+           round_up((int64_t)(nf * sizeof(int)), 256) +
+           round_up((int64_t)(nf * (kTileBits / 32) * sizeof(uint32_t)), 256);
 }
 
 int pp_cifhr(const float *d_cif, int32_t n_img, int32_t K, int32_t H, int32_t W,
@@ -326,14 +349,18 @@ int pp_cifhr(const float *d_cif, int32_t n_img, int32_t K, int32_t H, int32_t W,
     Splat *splats = (Splat *)d_workspace;
     int *counts = (int *)((char *)d_workspace +
                           round_up((int64_t)(nf * (int64_t)H * W * sizeof(Splat)), 256));
+    uint32_t *bits = (uint32_t *)((char *)counts + round_up((int64_t)(nf * sizeof(int)), 256));
+    const int tiles_x = (int)((pitch + kTile - 1) / kTile);
+    const int tiles = tiles_x * ((hh + kTile - 1) / kTile);
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(cifhr_splats_kernel, dim3((unsigned)nf), dim3(256), 0, s, d_cif, H, W, hh,
                        ww, (float)cfg->stride, cfg->cif_threshold, (float)cfg->cif_neighbors,
-                       splats, counts);
+                       splats, counts, bits, tiles_x, tiles);
     TileArgs a{};
     a.field = d_cifhr;
     a.splats = splats;
     a.counts = counts;
+    a.tile_bits = bits;
     a.splat_cap = (int64_t)H * W;
     a.field_stride = (int64_t)hh * pitch;
     a.h = hh;

@@ -1,10 +1,11 @@
 // stages.hip — CifSeeds and CafScored on gfx950.
 //
-//   seeds_kernel       one workgroup per image: threshold + CifHr rescore + order-preserving
-//                      ballot compaction (cif_seeds.py:23-50), then a bitonic sort that
-//                      reproduces sorted(seeds, reverse=True) (cif_seeds.py:54) including
-//                      its stability (ties broken by emission order).  LDS-resident up to
-//                      kSortLds seeds, global-memory network beyond.
+//   seeds_emit_kernel  one workgroup per (image, CIF field): threshold + CifHr rescore +
+//                      order-preserving ballot compaction (cif_seeds.py:28-47).
+//   seeds_sort_kernel  one workgroup per image: fields concatenated in order, then a
+//                      bitonic sort reproducing sorted(seeds, reverse=True)
+//                      (cif_seeds.py:54) including its stability (ties broken by emission
+//                      order).  LDS-resident up to kSortLds seeds, global network beyond.
 //   caf_scored_kernel  one workgroup per (image, CAF field): threshold, x stride, CifHr
 //                      lookups at both ends, forward/backward column sets in row-major
 //                      cell order (caf_scored.py:32-87), one or two thresholds per pass.
@@ -20,17 +21,20 @@ constexpr int kSortLds = 4096;
 struct SeedKeys {
     const float *v, *x, *y, *s;
     const int *f;
+    const int *loc;  // NULL, or emission index -> storage slot
     int n;
+    __device__ __forceinline__ int at(int a) const { return loc ? loc[a] : a; }
     // true when seed a must come before seed b in sorted(..., reverse=True) order
     __device__ __forceinline__ bool before(int a, int b) const {
         if (a >= n) return false;  // padding sorts last
         if (b >= n) return true;
-        if (v[a] != v[b]) return v[a] > v[b];
-        if (f[a] != f[b]) return f[a] > f[b];
-        if (x[a] != x[b]) return x[a] > x[b];
-        if (y[a] != y[b]) return y[a] > y[b];
-        if (s[a] != s[b]) return s[a] > s[b];
-        return a < b;  // stable
+        const int pa = at(a), pb = at(b);
+        if (v[pa] != v[pb]) return v[pa] > v[pb];
+        if (f[pa] != f[pb]) return f[pa] > f[pb];
+        if (x[pa] != x[pb]) return x[pa] > x[pb];
+        if (y[pa] != y[pb]) return y[pa] > y[pb];
+        if (s[pa] != s[pb]) return s[pa] > s[pb];
+        return a < b;  // stable: emission order
     }
 };
 
@@ -61,75 +65,101 @@ struct SeedArgs {
     int64_t pitch;
     float stride, th, score_scale;
     pp_seed *seeds;     // (n_img, cap) sorted output
-    int cap;
-    int *counts;
-    float *g_keys;      // (n_img, 4, cap) global sort scratch (v, x, y, s)
-    int *g_f;           // (n_img, cap)
+    int cap;            // K * H * W
+    int *counts;        // (n_img) seeds per image
+    float *g_keys;      // (n_img, 4, cap): per-field emission slots (v, x, y, s), field f at f*H*W
+    int *g_f;           // (n_img, cap): field of each slot; reused as slot index (global sort)
+    int *f_counts;      // (n_img, K) seeds per field
     int *g_perm;        // (n_img, np_cap)
     int np_cap;
 };
 
-__global__ __launch_bounds__(256) void seeds_kernel(SeedArgs a) {
+// stage 1: one workgroup per (image, field) — cif_seeds.py:28-47 for that field, in
+// row-major cell order, into the field's slot range
+__global__ __launch_bounds__(256) void seeds_emit_kernel(SeedArgs a) {
     __shared__ int s_tmp[4];
+    const int64_t fld = blockIdx.x;
+    const int img = (int)(fld / a.K), f = (int)(fld % a.K);
+    const int hw = a.H * a.W;
+    const int64_t cap = a.cap;
+    float *gv = a.g_keys + (int64_t)img * 4 * cap + (int64_t)f * hw;
+    float *gx = gv + cap, *gy = gx + cap, *gs = gy + cap;
+    int *gf = a.g_f + (int64_t)img * cap + (int64_t)f * hw;
+    const float *p = a.cif + fld * 5 * hw;
+    const float *t = a.hr + fld * a.hh * a.pitch;
+    int running = 0;
+    for (int base = 0; base < hw; base += 256) {
+        const int cell = base + threadIdx.x;
+        bool keep = false;
+        float v = 0.0f, x = 0.0f, y = 0.0f, sc = 0.0f;
+        if (cell < hw) {
+            const float c = p[cell];
+            if (c > a.th) {  // p[:, p[0] > threshold]
+                x = p[hw + cell] * a.stride;
+                y = p[2 * hw + cell] * a.stride;
+                const float h = hr_lookup(t, a.hh, a.ww, a.pitch, x, y, 0.0f);
+                v = 0.9f * h + 0.1f * c;  // 0.9 * v + 0.1 * c
+                if (a.score_scale != 1.0f) v = v * a.score_scale;
+                keep = v > a.th;
+                sc = p[4 * hw + cell] * a.stride;
+            }
+        }
+        int total;
+        const int slot = block_compact<4>(keep, s_tmp, total);
+        if (keep) {
+            const int pos = running + slot;
+            gv[pos] = v;
+            gx[pos] = x;
+            gy[pos] = y;
+            gs[pos] = sc;
+            gf[pos] = f;
+        }
+        running += total;
+    }
+    if (threadIdx.x == 0) a.f_counts[fld] = running;
+}
+
+// stage 2: one workgroup per image — concatenate the fields in order and sort
+__global__ __launch_bounds__(256) void seeds_sort_kernel(SeedArgs a) {
     __shared__ float s_v[kSortLds], s_x[kSortLds], s_y[kSortLds], s_s[kSortLds];
     __shared__ int s_f[kSortLds];
     __shared__ uint16_t s_perm[kSortLds];
+    __shared__ int s_off[PP_MAX_KP + 1];
     const int img = blockIdx.x;
     const int hw = a.H * a.W;
     const int64_t cap = a.cap;
-    float *gv = a.g_keys + (int64_t)img * 4 * cap, *gx = gv + cap, *gy = gx + cap, *gs = gy + cap;
+    const float *gv = a.g_keys + (int64_t)img * 4 * cap, *gx = gv + cap, *gy = gx + cap,
+                *gs = gy + cap;
     int *gf = a.g_f + (int64_t)img * cap;
-    int running = 0;
-    for (int f = 0; f < a.K; f++) {
-        const float *p = a.cif + ((int64_t)img * a.K + f) * 5 * hw;
-        const float *t = a.hr + ((int64_t)img * a.K + f) * a.hh * a.pitch;
-        for (int base = 0; base < hw; base += 256) {
-            const int cell = base + threadIdx.x;
-            bool keep = false;
-            float v = 0.0f, x = 0.0f, y = 0.0f, sc = 0.0f;
-            if (cell < hw) {
-                const float c = p[cell];
-                if (c > a.th) {  // p[:, p[0] > threshold]
-                    x = p[hw + cell] * a.stride;
-                    y = p[2 * hw + cell] * a.stride;
-                    const float h = hr_lookup(t, a.hh, a.ww, a.pitch, x, y, 0.0f);
-                    v = 0.9f * h + 0.1f * c;
-                    if (a.score_scale != 1.0f) v = v * a.score_scale;
-                    keep = v > a.th;
-                    sc = p[4 * hw + cell] * a.stride;
-                }
-            }
-            int total;
-            const int slot = block_compact<4>(keep, s_tmp, total);
-            const int pos = running + slot;
-            if (keep && pos < a.cap) {
-                if (pos < kSortLds) {
-                    s_v[pos] = v;
-                    s_x[pos] = x;
-                    s_y[pos] = y;
-                    s_s[pos] = sc;
-                    s_f[pos] = f;
-                }
-                gv[pos] = v;
-                gx[pos] = x;
-                gy[pos] = y;
-                gs[pos] = sc;
-                gf[pos] = f;
-            }
-            running += total;
+    if (threadIdx.x == 0) {
+        int o = 0;
+        for (int f = 0; f < a.K; f++) {
+            s_off[f] = o;
+            o += a.f_counts[(int64_t)img * a.K + f];
         }
+        s_off[a.K] = o;
+        a.counts[img] = o;
     }
-    if (threadIdx.x == 0) a.counts[img] = running;
-    if (running > a.cap) return;  // overflow: host re-runs with a larger capacity
-    const int n = running;
+    __syncthreads();
+    const int n = s_off[a.K];
     int np = 1;
     while (np < n) np <<= 1;
     pp_seed *out = a.seeds + (int64_t)img * cap;
-    __syncthreads();
     if (n <= kSortLds) {
+        for (int f = 0; f < a.K; f++) {
+            const int o = s_off[f], c = s_off[f + 1] - o;
+            for (int i = threadIdx.x; i < c; i += blockDim.x) {
+                const int64_t q = (int64_t)f * hw + i;
+                s_v[o + i] = gv[q];
+                s_x[o + i] = gx[q];
+                s_y[o + i] = gy[q];
+                s_s[o + i] = gs[q];
+                s_f[o + i] = f;
+            }
+        }
         for (int i = threadIdx.x; i < np; i += blockDim.x) s_perm[i] = (uint16_t)i;
         __syncthreads();
-        SeedKeys keys{s_v, s_x, s_y, s_s, s_f, n};
+        SeedKeys keys{s_v, s_x, s_y, s_s, s_f, nullptr, n};
         bitonic_sort(s_perm, np, keys);
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
             const int k = s_perm[i];
@@ -142,13 +172,20 @@ __global__ __launch_bounds__(256) void seeds_kernel(SeedArgs a) {
             out[i] = r;
         }
     } else {
+        // large seed sets: network over a permutation in global memory; keys are read
+        // through an emission-index -> slot map
         int *perm = a.g_perm + (int64_t)img * a.np_cap;
+        int *loc = perm + np;  // second half of the permutation buffer
+        for (int f = 0; f < a.K; f++) {
+            const int o = s_off[f], c = s_off[f + 1] - o;
+            for (int i = threadIdx.x; i < c; i += blockDim.x) loc[o + i] = f * hw + i;
+        }
         for (int i = threadIdx.x; i < np; i += blockDim.x) perm[i] = i;
         __syncthreads();
-        SeedKeys keys{gv, gx, gy, gs, gf, n};
+        SeedKeys keys{gv, gx, gy, gs, gf, loc, n};
         bitonic_sort(perm, np, keys);
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            const int k = perm[i];
+            const int k = loc[perm[i]];
             pp_seed r;
             r.v = gv[k];
             r.field = gf[k];
@@ -172,6 +209,7 @@ struct CafArgs {
     float th[2];
     float *cols[2];     // (n_img, C, 2, 9, H*W): dir 0 backward, 1 forward
     int *counts[2];     // (n_img, C, 2)
+    const int *gate;    // (n_img) or NULL: images with gate 0 are skipped (empty sets)
     int j1[kMaxCaf], j2[kMaxCaf];
 };
 
@@ -180,6 +218,10 @@ __global__ __launch_bounds__(256) void caf_scored_kernel(CafArgs a) {
     const int64_t fld = blockIdx.x;  // image * C + caf field
     const int img = (int)(fld / a.C), ci = (int)(fld % a.C);
     const int hw = a.H * a.W;
+    if (a.gate && !a.gate[img]) {
+        if (threadIdx.x < a.nt * 2) a.counts[threadIdx.x >> 1][fld * 2 + (threadIdx.x & 1)] = 0;
+        return;
+    }
     const float *p = a.caf + fld * 9 * hw;
     const int j1i = a.j1[ci], j2i = a.j2[ci];
     const bool use1 = a.cif_floor < 1.0f && j1i < a.K;
@@ -252,11 +294,169 @@ __global__ __launch_bounds__(256) void caf_scored_kernel(CafArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------
+// CafScored for the device decoder: the same column sets, stored bucketed by SOURCE
+// position so that caf_center_s (functional.pyx:338-359) in the grow kernel only visits
+// the buckets its 2*scale box overlaps.  Row 9 keeps each column's index in the
+// reference's row-major order, which is what ties are broken on; `offs` holds the
+// bucket boundaries (bucket grid bw x bh of e x e px, plus one bucket for NaN sources).
+// ------------------------------------------------------------------------------------
+constexpr int kMaxBuckets = 6400 + 1;
+
+struct CafBArgs {
+    const float *caf, *hr;
+    int K, C, H, W, hh, ww;
+    int64_t pitch;
+    float stride, cif_floor, one_minus_floor, th;
+    int bw, bh, nb;     // bucket grid and bucket count (bw * bh + 1)
+    float inv_e;        // 1 / bucket edge (a power of two: exact)
+    float *cols;        // (n_img, C, 2, 10, H*W): dir 0 backward, 1 forward
+    int *offs;          // (n_img, C, 2, nb + 1)
+    const int *gate;    // (n_img) or NULL
+    int j1[kMaxCaf], j2[kMaxCaf];
+};
+
+__device__ __forceinline__ int caf_bucket(float x, float y, int bw, int bh, float inv_e) {
+    if (x != x || y != y) return bw * bh;  // NaN sources pass every box test: own bucket
+    const int bx = (int)fminf(fmaxf(floorf(x * inv_e), 0.0f), (float)(bw - 1));
+    const int by = (int)fminf(fmaxf(floorf(y * inv_e), 0.0f), (float)(bh - 1));
+    return by * bw + bx;
+}
+
+__global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
+    __shared__ int s_tmp[4];
+    __shared__ int s_cnt[2][kMaxBuckets + 1];
+    __shared__ int s_wsum[2][4];
+    const int64_t fld = blockIdx.x;  // image * C + caf field
+    const int img = (int)(fld / a.C), ci = (int)(fld % a.C);
+    const int hw = a.H * a.W;
+    const int nb = a.nb;
+    int *offs_b = a.offs + (fld * 2 + 0) * (int64_t)(nb + 1);
+    int *offs_f = a.offs + (fld * 2 + 1) * (int64_t)(nb + 1);
+    if (a.gate && !a.gate[img]) {
+        for (int i = threadIdx.x; i <= nb; i += 256) {
+            offs_b[i] = 0;
+            offs_f[i] = 0;
+        }
+        return;
+    }
+    const float *p = a.caf + fld * 9 * hw;
+    const int j1i = a.j1[ci], j2i = a.j2[ci];
+    const bool use1 = a.cif_floor < 1.0f && j1i < a.K;
+    const bool use2 = a.cif_floor < 1.0f && j2i < a.K;
+    const float *t1 = a.hr + ((int64_t)img * a.K + (use1 ? j1i : 0)) * a.hh * a.pitch;
+    const float *t2 = a.hr + ((int64_t)img * a.K + (use2 ? j2i : 0)) * a.hh * a.pitch;
+    for (int i = threadIdx.x; i <= nb; i += 256) {
+        s_cnt[0][i] = 0;
+        s_cnt[1][i] = 0;
+    }
+    __syncthreads();
+
+    // one cell of caf_scored.py:42-81 (both directions)
+    auto score_cell = [&](int cell, float nine[9], bool &kb, bool &kf, float &sb, float &sf) {
+        kb = kf = false;
+        if (cell >= hw) return;
+        nine[0] = p[cell];
+        if (!(nine[0] > a.th)) return;  // mask = nine[0] > score_th
+#pragma unroll
+        for (int r = 1; r < 9; r++) nine[r] = p[r * hw + cell] * a.stride;
+        const float score = nine[0];
+        sb = score;
+        sf = score;
+        if (use1)
+            sb = score * (a.cif_floor + a.one_minus_floor *
+                                            hr_lookup(t1, a.hh, a.ww, a.pitch, nine[1], nine[2], 0.0f));
+        if (use2)
+            sf = score * (a.cif_floor + a.one_minus_floor *
+                                            hr_lookup(t2, a.hh, a.ww, a.pitch, nine[5], nine[6], 0.0f));
+        kb = sb > a.th;
+        kf = sf > a.th;
+    };
+
+    // pass 1: bucket histograms (backward sources are (x2, y2), forward (x1, y1))
+    for (int base = 0; base < hw; base += 256) {
+        float nine[9], sb, sf;
+        bool kb, kf;
+        score_cell(base + threadIdx.x, nine, kb, kf, sb, sf);
+        if (kb) atomicAdd(&s_cnt[0][caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e)], 1);
+        if (kf) atomicAdd(&s_cnt[1][caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e)], 1);
+    }
+    __syncthreads();
+    // exclusive prefix over the buckets (thread-contiguous ranges + block scan)
+    const int per = (nb + 255) / 256;
+    const int b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
+    int sum[2] = {0, 0};
+    for (int d = 0; d < 2; d++)
+        for (int i = b0; i < b1; i++) sum[d] += s_cnt[d][i];
+    int incl[2];
+    for (int d = 0; d < 2; d++) {
+        int v = sum[d];
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int o = __shfl_up(v, off);
+            if ((threadIdx.x & 63) >= off) v += o;
+        }
+        incl[d] = v;
+        if ((threadIdx.x & 63) == 63) s_wsum[d][threadIdx.x >> 6] = v;
+    }
+    __syncthreads();
+    for (int d = 0; d < 2; d++) {
+        int base = incl[d] - sum[d];
+        for (int w = 0; w < (int)(threadIdx.x >> 6); w++) base += s_wsum[d][w];
+        int *offs = d == 0 ? offs_b : offs_f;
+        for (int i = b0; i < b1; i++) {
+            const int c = s_cnt[d][i];
+            s_cnt[d][i] = base;  // becomes the bucket cursor
+            offs[i] = base;
+            base += c;
+        }
+        if (threadIdx.x == 255) offs[nb] = s_wsum[d][0] + s_wsum[d][1] + s_wsum[d][2] + s_wsum[d][3];
+    }
+    __syncthreads();
+
+    // pass 2: scatter into buckets, remembering each column's row-major index
+    float *bwd = a.cols + (fld * 2 + 0) * 10 * (int64_t)hw;
+    float *fwd = a.cols + (fld * 2 + 1) * 10 * (int64_t)hw;
+    int run_b = 0, run_f = 0;
+    for (int base = 0; base < hw; base += 256) {
+        float nine[9], sb, sf;
+        bool kb, kf;
+        score_cell(base + threadIdx.x, nine, kb, kf, sb, sf);
+        int tot_b, tot_f;
+        const int ob = run_b + block_compact<4>(kb, s_tmp, tot_b);
+        const int of = run_f + block_compact<4>(kf, s_tmp, tot_f);
+        if (kb) {
+            const int c = atomicAdd(&s_cnt[0][caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e)], 1);
+            bwd[c] = sb;  // rows (0, 5, 6, 7, 8, 1, 2, 3, 4), row 0 = scores_b
+            bwd[1 * hw + c] = nine[5];
+            bwd[2 * hw + c] = nine[6];
+            bwd[3 * hw + c] = nine[7];
+            bwd[4 * hw + c] = nine[8];
+            bwd[5 * hw + c] = nine[1];
+            bwd[6 * hw + c] = nine[2];
+            bwd[7 * hw + c] = nine[3];
+            bwd[8 * hw + c] = nine[4];
+            bwd[9 * hw + c] = __int_as_float(ob);
+        }
+        if (kf) {
+            const int c = atomicAdd(&s_cnt[1][caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e)], 1);
+            fwd[c] = sf;
+#pragma unroll
+            for (int r = 1; r < 9; r++) fwd[r * hw + c] = nine[r];
+            fwd[9 * hw + c] = __int_as_float(of);
+        }
+        run_b += tot_b;
+        run_f += tot_f;
+    }
+}
+
 static inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 
 int launch_seeds(const float *cif, const float *hr, int n_img, int K, int H, int W,
                  const pp_config *cfg, pp_seed *seeds, int cap, int *counts, void *scratch,
                  hipStream_t s) {
+    if (K > PP_MAX_KP) return fail(PP_ESHAPE, "seeds: more than PP_MAX_KP CIF fields");
+    if ((int64_t)cap < (int64_t)K * H * W) return fail(PP_ESHAPE, "seeds: capacity < K*H*W");
     SeedArgs a{};
     a.cif = cif;
     a.hr = hr;
@@ -274,14 +474,17 @@ int launch_seeds(const float *cif, const float *hr, int n_img, int K, int H, int
     a.counts = counts;
     int np = 1;
     while (np < cap) np <<= 1;
-    a.np_cap = np;
+    a.np_cap = 2 * np;
     char *w = (char *)scratch;
     a.g_keys = (float *)w;
     w += round_up((int64_t)n_img * 4 * cap * sizeof(float), 256);
     a.g_f = (int *)w;
     w += round_up((int64_t)n_img * cap * sizeof(int), 256);
+    a.f_counts = (int *)w;
+    w += round_up((int64_t)n_img * K * sizeof(int), 256);
     a.g_perm = (int *)w;
-    hipLaunchKernelGGL(seeds_kernel, dim3(n_img), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(seeds_emit_kernel, dim3((unsigned)((int64_t)n_img * K)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(seeds_sort_kernel, dim3(n_img), dim3(256), 0, s, a);
     return check_launch("pp_seeds");
 }
 
@@ -290,12 +493,13 @@ size_t seeds_scratch_size(int n_img, int cap) {
     while (np < cap) np <<= 1;
     return round_up((int64_t)n_img * 4 * cap * sizeof(float), 256) +
            round_up((int64_t)n_img * cap * sizeof(int), 256) +
-           round_up((int64_t)n_img * np * sizeof(int), 256);
+           round_up((int64_t)n_img * PP_MAX_KP * sizeof(int), 256) +
+           round_up((int64_t)n_img * 2 * np * sizeof(int), 256);
 }
 
 int launch_caf_scored(const float *caf, const float *hr, int n_img, int K, int C, int H, int W,
                       const int32_t *skeleton, const pp_config *cfg, int nt, const float *th,
-                      float *const *cols, int *const *counts, hipStream_t s) {
+                      float *const *cols, int *const *counts, hipStream_t s, const int *gate) {
     if (C > kMaxCaf) return fail(PP_ESHAPE, "caf_scored: more than PP_MAX_EDGES CAF fields");
     CafArgs a{};
     a.caf = caf;
@@ -311,6 +515,7 @@ int launch_caf_scored(const float *caf, const float *hr, int n_img, int K, int C
     a.cif_floor = cfg->cif_floor;
     a.one_minus_floor = (float)(1.0 - (double)cfg->cif_floor);  // (1.0 - self.cif_floor)
     a.nt = nt;
+    a.gate = gate;
     for (int t = 0; t < nt; t++) {
         a.th[t] = th[t];
         a.cols[t] = cols[t];
@@ -323,6 +528,47 @@ int launch_caf_scored(const float *caf, const float *hr, int n_img, int K, int C
     }
     hipLaunchKernelGGL(caf_scored_kernel, dim3((unsigned)((int64_t)n_img * C)), dim3(256), 0, s, a);
     return check_launch("pp_caf_scored");
+}
+
+// bucket geometry for an H x W field: edge e = stride * 2^k px with <= 6400 buckets
+void caf_bucket_grid(int H, int W, int stride, int *bw, int *bh, int *nb, float *inv_e) {
+    const int hh = (int)hr_dim(H, stride), ww = (int)hr_dim(W, stride);
+    int e = stride;
+    while (((hh + e - 1) / e) * ((ww + e - 1) / e) > kMaxBuckets - 1) e *= 2;
+    *bw = (ww + e - 1) / e;
+    *bh = (hh + e - 1) / e;
+    *nb = *bw * *bh + 1;
+    *inv_e = 1.0f / (float)e;
+}
+
+int launch_caf_bucketed(const float *caf, const float *hr, int n_img, int K, int C, int H, int W,
+                        const int32_t *skeleton, const pp_config *cfg, float th, float *cols,
+                        int *offs, const int *gate, hipStream_t s) {
+    if (C > kMaxCaf) return fail(PP_ESHAPE, "caf_scored: more than PP_MAX_EDGES CAF fields");
+    CafBArgs a{};
+    a.caf = caf;
+    a.hr = hr;
+    a.K = K;
+    a.C = C;
+    a.H = H;
+    a.W = W;
+    a.hh = (int)hr_dim(H, cfg->stride);
+    a.ww = (int)hr_dim(W, cfg->stride);
+    a.pitch = pp_cifhr_pitch(a.ww);
+    a.stride = (float)cfg->stride;
+    a.cif_floor = cfg->cif_floor;
+    a.one_minus_floor = (float)(1.0 - (double)cfg->cif_floor);
+    a.th = th;
+    caf_bucket_grid(H, W, cfg->stride, &a.bw, &a.bh, &a.nb, &a.inv_e);
+    a.cols = cols;
+    a.offs = offs;
+    a.gate = gate;
+    for (int i = 0; i < C; i++) {
+        a.j1[i] = skeleton[2 * i] - 1;
+        a.j2[i] = skeleton[2 * i + 1] - 1;
+    }
+    hipLaunchKernelGGL(caf_bucketed_kernel, dim3((unsigned)((int64_t)n_img * C)), dim3(256), 0, s, a);
+    return check_launch("caf_scored(bucketed)");
 }
 
 }  // namespace pp
@@ -358,7 +604,7 @@ int pp_caf_scored(const float *d_caf, const float *d_cifhr, int32_t n_img, int32
     float *cols[1] = {d_cols};
     int *counts[1] = {d_counts};
     return launch_caf_scored(d_caf, d_cifhr, n_img, K, C, H, W, skeleton, cfg, 1, &score_th, cols,
-                             counts, (hipStream_t)stream);
+                             counts, (hipStream_t)stream, nullptr);
 }
 
 }  // extern "C"

@@ -1,0 +1,38 @@
+"""Diagnostic: run the decode with the stamps build and print per-section cycle shares.
+
+    PP_LIB_VARIANT=stamps PP_STAMPS_OUT=gpurun_out/stamps.bin python tools/stamps_run.py
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from openpifpaf_amd import constants, synthetic  # noqa: E402
+from openpifpaf_amd._abi import EVAL_CONFIG, make_config  # noqa: E402
+from openpifpaf_amd.engine import DecodeEngine  # noqa: E402
+
+P1 = ['seed_check', 'ann_init', 'grow', 'copy_ann', 'mark_occ', 'occ_clear']
+P2 = ['load', 'complete', 'nms_filter', 'nms_sort', 'nms_occ', 'nms_clear', 'nms_refilter',
+      'nms_sort2', 'output']
+
+out = os.environ.get('PP_STAMPS_OUT', 'pp_stamps.bin')
+for kind, n, h in (('planted', 256, 80), ('uniform', 32, 80)):
+    if os.path.exists(out):
+        os.remove(out)
+    cif, caf = synthetic.batch(kind, n, h, h)
+    eng = DecodeEngine()
+    cfg = make_config(**EVAL_CONFIG)
+    c, f = torch.from_numpy(cif).cuda(), torch.from_numpy(caf).cuda()
+    for _ in range(2):
+        eng.launch(c, f, constants.COCO_PERSON_SKELETON, cfg)
+    torch.cuda.synchronize()
+    st = np.fromfile(out, dtype=np.uint64).reshape(-1, n, 2, 12)[-1].astype(np.float64)
+    print('== {} n={} (mean shader cycles per image)'.format(kind, n))
+    for ph, names in ((0, P1), (1, P2)):
+        tot = st[:, ph, :len(names)].sum(axis=1).mean()
+        print('  phase {} total {:.3e}'.format(ph + 1, tot))
+        for i, name in enumerate(names):
+            m = st[:, ph, i].mean()
+            print('    {:14s} {:12.0f}  {:5.1f}%'.format(name, m, 100 * m / max(tot, 1)))
