@@ -1,17 +1,20 @@
-// grow.hip — the CifCaf greedy decoder (generator/cifcaf.py) as one gfx950 workgroup per image.
+// grow.hip — the CifCaf greedy decoder (generator/cifcaf.py) as one gfx950 wave per image.
 //
 // The seed loop is sequential by construction (each annotation's occupancy marks decide
 // whether later seeds start annotations, cifcaf.py:100-108), so an image is one wave64
-// workgroup and a batch fills the chip with one workgroup per image.  Inside an image:
+// workgroup and a batch fills the chip with one workgroup per image.  A single wave has no
+// other wave to hide latency behind, so the serial state lives in REGISTERS, not memory:
 //
-//   * the serial control (seed loop, lazy best-first frontier, force-complete, flood fill,
-//     keypoint NMS) runs wave-uniformly with its state in LDS: the current annotation, the
-//     frontier binary heap (cifcaf.py:248 PriorityQueue, same tuple order), the
-//     by_source table (cifcaf.py:62-65, dict insertion order);
-//   * caf_center_s + scoring (functional.pyx:338-359, cifcaf.py:124-145) is the parallel
-//     part: 64 lanes stride the CAF column set with coalesced loads, each lane keeps its
-//     top-2 (score, column) and a 6-step xor-shuffle merge yields the argsort top-2 that
-//     _target_with_blend (cifcaf.py:157-192) needs;
+//   * the annotation being grown: lane j holds joint j's (x, y, v, scale);
+//   * the frontier (cifcaf.py:248 PriorityQueue): at most one entry per directed skeleton
+//     edge is ever live (in_frontier admits (j, k) once; its evaluated re-push replaces
+//     the popped unevaluated entry), so lane d holds the entry of directed edge d (by_source
+//     order, cifcaf.py:62-65) and pop-min is a wave reduction with the reference's tuple
+//     order (-score, None|xysv, j, k);
+//   * caf_center_s + scoring (functional.pyx:338-359, cifcaf.py:124-145): 64 lanes scan the
+//     CAF columns of the buckets the 2*scale box overlaps (caf_bucketed_kernel), loading
+//     each candidate's rows in one round, and a 6-step xor-shuffle merge yields the argsort
+//     top-2 _target_with_blend (cifcaf.py:157-192) needs, targets included;
 //   * occupancy grids (occupancy.py, u8 += 1 with wrap) live in a per-image workspace that
 //     every launch leaves zeroed: each box a launch marks is logged and cleared again.
 //
@@ -36,27 +39,33 @@
         st_t = t_;                                                                          \
     } while (0)
 #define STAMP_FLUSH(ph)                                                                     \
-    if (lane == 0 && g.stamps)                                                              \
-        for (int q_ = 0; q_ < 12; q_++) g.stamps[((int64_t)img * 2 + (ph)-1) * 12 + q_] = st_acc[q_];
+    if (lane == 0 && g.stamps) {                                                            \
+        st_acc[9] = L.fst[0];                                                               \
+        st_acc[10] = L.fst[1];                                                              \
+        st_acc[11] = L.fst[2];                                                              \
+        st_acc[8] = L.fst[3];                                                               \
+        for (int q_ = 0; q_ < 12; q_++)                                                     \
+            atomicAdd((unsigned long long *)&g.stamps[((int64_t)img * 3 + (ph)-1) * 12 + q_], \
+                      (unsigned long long)st_acc[q_]);                                      \
+    }
+#define FSTAMP_BEGIN const uint64_t fst_t0 = __builtin_amdgcn_s_memtime();
+#define FSTAMP_END(L, i)                                                                    \
+    if ((threadIdx.x & 63) == 0) (L).fst[i] += __builtin_amdgcn_s_memtime() - fst_t0;
 #else
 #define STAMP_DECL
 #define STAMP(i)
 #define STAMP_FLUSH(ph)
+#define FSTAMP_BEGIN
+#define FSTAMP_END(L, i)
 #endif
 
 namespace pp {
 
 constexpr int kKP = PP_MAX_KP;
-constexpr int kBS = 2 * PP_MAX_EDGES;       // by_source entries per joint (upper bound)
-constexpr int kHeap = 4 * PP_MAX_EDGES + 8; // frontier entries per _grow call
+constexpr int kSlots = 2 * PP_MAX_EDGES;   // directed edges (two lanes' worth of slots)
+constexpr int kHeap = 4 * PP_MAX_EDGES + 8; // flood-fill heap capacity
 constexpr int kOccMargin = 64;              // NMS occupancy slack beyond the main grid
-
-struct HeapEntry {
-    float neg;   // -score
-    int eval;    // 0: (.., None, j, k)   1: (.., xysv, j, k)
-    float xysv[4];
-    int j, k;
-};
+constexpr int kCompleteWays = 32;           // force-complete workgroups per image
 
 struct FFEntry {  // _flood_fill frontier entry (-v, end_i, start_xyv, s)
     float neg;
@@ -82,7 +91,11 @@ struct GrowArgs {
     int K, C, H, W, hh, ww;
     int64_t hw;
     pp_config cfg;
-    int skel[2 * PP_MAX_EDGES];
+    // directed edges ("slots") in by_source order (cifcaf.py:62-65): joint j's entries
+    // are slots j_off[j] .. j_off[j+1]-1 in dict insertion order
+    int nd;
+    uint8_t j_off[kKP + 1];
+    uint8_t d_j[kSlots], d_k[kSlots], d_caf[kSlots], d_fwd[kSlots];
     // workspace (per image regions)
     uint8_t *occ;
     int64_t occ_cap;          // bytes per image
@@ -93,7 +106,7 @@ struct GrowArgs {
     int *nms_idx;             // (n_img, 2 * ann_cap + ann_np)
     int ann_np;               // next pow2 >= ann_cap
     int ann_cap;
-    uint64_t *stamps;         // diagnostic build: (n_img, 2, 12) cycle sums, else NULL
+    uint64_t *stamps;         // diagnostic build: (n_img, 3, 12) cycle sums, else NULL
     int *n_work;              // (n_img) annotations after the seed loop (phase 1 -> 2)
     int *need_complete;       // (n_img) 1 if force-complete has work (gates the B columns)
     // outputs
@@ -103,76 +116,67 @@ struct GrowArgs {
 };
 
 struct GrowLDS {
-    pp_ann a;                  // current annotation
-    HeapEntry heap[kHeap];
+    pp_ann a;                     // record being built (lists; data synced from registers)
     FFEntry ff[kHeap];
-    uint32_t in_frontier[kKP];
-    int bs_n[kKP];
-    uint8_t bs_k[kKP][kBS], bs_caf[kKP][kBS], bs_fwd[kKP][kBS];
-    int seg_st[64], seg_pre[64];  // flattened bucket segments of one caf_center_s scan
     int mark_pre[kKP + 1];        // occupancy boxes of one annotation: area prefix
     int mark_box[kKP][4];
     double prod[kKP];             // Annotation.score() terms
     double score_bc;
-    int heap_n;
     int ff_n;
     int log_n;
     int status;
+#ifdef PP_STAMPS
+    uint64_t fst[8];  // inside-grow section sums (diagnostic build)
+#endif
 };
 
-// ---------------------------------------------------------------------------------------
-// frontier heap (tuple order of cifcaf.py:261,281,285)
-// ---------------------------------------------------------------------------------------
-__device__ __forceinline__ bool heap_less(const HeapEntry &a, const HeapEntry &b) {
-    if (a.neg != b.neg) return a.neg < b.neg;
-    if (a.eval != b.eval) return a.eval < b.eval;  // reference raises TypeError here
-    if (a.eval) {
-        for (int t = 0; t < 4; t++)
-            if (a.xysv[t] != b.xysv[t]) return a.xysv[t] < b.xysv[t];
-    }
-    if (a.j != b.j) return a.j < b.j;
-    return a.k < b.k;
+__device__ __forceinline__ float rl_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ int rl_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+// Wave reductions on DPP (row-level VALU data movement, no LDS round trip): quad xor 1,
+// quad xor 2, row half-mirror, row mirror, then row_bcast15 / row_bcast31 fold the rows
+// into lane 63.  Each step pairs lanes holding disjoint lane sets, so any associative,
+// commutative merge (sum, min, exact top-2) is correct; lanes outside a step's row mask
+// receive `old` (the identity).
+constexpr int kDppXor1 = 0xB1;        // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;        // quad_perm [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141;
+constexpr int kDppMirror = 0x140;
+constexpr int kDppBcast15 = 0x142;
+constexpr int kDppBcast31 = 0x143;
+
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int dpp_i(int old, int v) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWS, 0xF, false);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_f(float old, float v) {
+    return __int_as_float(
+        __builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL, ROWS, 0xF, false));
 }
 
-__device__ void heap_push(GrowLDS &L, const HeapEntry &x) {
-    int i = L.heap_n;
-    if (i >= kHeap) {
-        L.status |= PP_ST_DEC_OVERFLOW;
-        return;
-    }
-    L.heap_n = i + 1;
-    while (i > 0) {
-        const int p = (i - 1) >> 1;
-        if (!heap_less(x, L.heap[p])) break;
-        L.heap[i] = L.heap[p];
-        i = p;
-    }
-    L.heap[i] = x;
+// sum over the wave, uniform result
+__device__ __forceinline__ int wave_total(int v) {
+    v += dpp_i<kDppXor1, 0xF>(0, v);
+    v += dpp_i<kDppXor2, 0xF>(0, v);
+    v += dpp_i<kDppHalfMirror, 0xF>(0, v);
+    v += dpp_i<kDppMirror, 0xF>(0, v);
+    v += dpp_i<kDppBcast15, 0xA>(0, v);
+    v += dpp_i<kDppBcast31, 0xC>(0, v);
+    return __builtin_amdgcn_readlane(v, 63);
 }
 
-__device__ HeapEntry heap_pop(GrowLDS &L) {
-    const HeapEntry top = L.heap[0];
-    const int n = L.heap_n - 1;
-    L.heap_n = n;
-    if (n > 0) {
-        const HeapEntry x = L.heap[n];
-        int i = 0;
-        for (;;) {
-            const int l = 2 * i + 1, r = l + 1;
-            int m = i;
-            const HeapEntry *mv = &x;
-            if (l < n && heap_less(L.heap[l], *mv)) {
-                m = l;
-                mv = &L.heap[l];
-            }
-            if (r < n && heap_less(L.heap[r], *mv)) m = r;
-            if (m == i) break;
-            L.heap[i] = L.heap[m];
-            i = m;
-        }
-        L.heap[i] = x;
-    }
-    return top;
+// min over the wave (fminf: NaN ignored), uniform result
+__device__ __forceinline__ float wave_fmin(float v) {
+    v = fminf(v, dpp_f<kDppXor1, 0xF>(INFINITY, v));
+    v = fminf(v, dpp_f<kDppXor2, 0xF>(INFINITY, v));
+    v = fminf(v, dpp_f<kDppHalfMirror, 0xF>(INFINITY, v));
+    v = fminf(v, dpp_f<kDppMirror, 0xF>(INFINITY, v));
+    v = fminf(v, dpp_f<kDppBcast15, 0xA>(INFINITY, v));
+    v = fminf(v, dpp_f<kDppBcast31, 0xC>(INFINITY, v));
+    return rl_f(v, 63);
 }
 
 __device__ __forceinline__ bool ff_less(const FFEntry &a, const FFEntry &b) {
@@ -227,64 +231,92 @@ __device__ FFEntry ff_pop(GrowLDS &L) {
 // ---------------------------------------------------------------------------------------
 // _grow_connection: caf_center_s + scores + blend / max (cifcaf.py:124-192)
 // ---------------------------------------------------------------------------------------
+// Candidate columns are ranked by a 64-bit key, larger = better: high word = the score's
+// bits (scores are >= 0, so float order == unsigned order; NaN sorts last in np.argsort,
+// i.e. largest, and its bits are above every finite score), low word = the column's
+// row-major index, so ties follow the reference: blend (stable argsort, last wins) ->
+// higher index; max (np.argmax, first wins) -> lower index.  0 = no candidate.
+template <bool MAXM>
+__device__ __forceinline__ uint64_t cand_key(float score, int o) {
+    const uint32_t hi = (score != score) ? 0xFFFFFFFFu : __float_as_uint(score);
+    const uint32_t lo = MAXM ? (uint32_t)(0x7FFFFFFF - o) : (uint32_t)(o + 1);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ float key_score(uint64_t k) { return __uint_as_float((uint32_t)(k >> 32)); }
+
 struct Top2 {
-    float s1, s2;
-    int o1, o2;  // column index in the reference's row-major order (tie-breaks)
-    int k1, k2;  // storage slot (where the column's rows are)
+    uint64_t k1, k2;   // best and second-best keys of this lane (0 = none)
+    float x1, y1, c1;  // target (x2, y2, s2) rows of the best column
+    float x2, y2, c2;  // ... and of the second best
 };
 
-// blend: top-2 of a stable ascending argsort (ties -> higher column ranks higher)
-// max:   np.argmax (ties -> lower column)
-template <bool MAXM>
-__device__ __forceinline__ bool better(float sa, int ia, float sb, int ib) {
-    if (ia < 0) return false;
-    if (ib < 0) return true;
-    if (sa != sb) return sa > sb;
-    return MAXM ? ia < ib : ia > ib;
+// branch-free on purpose: values feed DPP reductions, which must not run under a
+// partial exec mask
+__device__ __forceinline__ void top2_insert(Top2 &t, uint64_t k, float x, float y, float c) {
+    const bool b1 = k > t.k1;
+    const bool b2 = !b1 & (k > t.k2);
+    t.k2 = b1 ? t.k1 : (b2 ? k : t.k2);
+    t.x2 = b1 ? t.x1 : (b2 ? x : t.x2);
+    t.y2 = b1 ? t.y1 : (b2 ? y : t.y2);
+    t.c2 = b1 ? t.c1 : (b2 ? c : t.c2);
+    t.k1 = b1 ? k : t.k1;
+    t.x1 = b1 ? x : t.x1;
+    t.y1 = b1 ? y : t.y1;
+    t.c1 = b1 ? c : t.c1;
 }
 
-template <bool MAXM>
-__device__ __forceinline__ void top2_insert(Top2 &t, float s, int o, int k) {
-    if (better<MAXM>(s, o, t.s1, t.o1)) {
-        t.s2 = t.s1;
-        t.o2 = t.o1;
-        t.k2 = t.k1;
-        t.s1 = s;
-        t.o1 = o;
-        t.k1 = k;
-    } else if (better<MAXM>(s, o, t.s2, t.o2)) {
-        t.s2 = s;
-        t.o2 = o;
-        t.k2 = k;
-    }
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+    const uint32_t lo = (uint32_t)dpp_i<CTRL, ROWS>(0, (int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)dpp_i<CTRL, ROWS>(0, (int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
 }
 
-template <bool MAXM>
-__device__ __forceinline__ void top2_wave_merge(Top2 &t) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const float os1 = __shfl_xor(t.s1, off), os2 = __shfl_xor(t.s2, off);
-        const int oo1 = __shfl_xor(t.o1, off), oo2 = __shfl_xor(t.o2, off);
-        const int ok1 = __shfl_xor(t.k1, off), ok2 = __shfl_xor(t.k2, off);
-        top2_insert<MAXM>(t, os1, oo1, ok1);
-        top2_insert<MAXM>(t, os2, oo2, ok2);
-    }
+// max of a 64-bit key over the wave, uniform result
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+    uint64_t o;
+    o = dpp_u64<kDppXor1, 0xF>(v);
+    v = o > v ? o : v;
+    o = dpp_u64<kDppXor2, 0xF>(v);
+    v = o > v ? o : v;
+    o = dpp_u64<kDppHalfMirror, 0xF>(v);
+    v = o > v ? o : v;
+    o = dpp_u64<kDppMirror, 0xF>(v);
+    v = o > v ? o : v;
+    o = dpp_u64<kDppBcast15, 0xA>(v);
+    v = o > v ? o : v;
+    o = dpp_u64<kDppBcast31, 0xC>(v);
+    v = o > v ? o : v;
+    const uint32_t lo = (uint32_t)rl_i((int)(uint32_t)v, 63);
+    const uint32_t hi = (uint32_t)rl_i((int)(uint32_t)(v >> 32), 63);
+    return ((uint64_t)hi << 32) | lo;
 }
 
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    return v;
-}
+// exact top-2 over the wave (uniform): the global best K1 by a max reduction, then the
+// best key other than K1 (keys are unique per column); targets from the holding lane
+struct Best2 {
+    uint64_t k1, k2;
+    float x1, y1, c1, x2, y2, c2;
+};
 
-__device__ __forceinline__ int wave_incl_scan(int v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int o = __shfl_up(v, off);
-        if (lane >= off) v += o;
-    }
-    return v;
+__device__ __forceinline__ Best2 top2_wave(const Top2 &t) {
+    Best2 b;
+    b.k1 = wave_max_u64(t.k1);
+    b.k2 = wave_max_u64(t.k1 == b.k1 ? t.k2 : t.k1);
+    const uint64_t m1 = __ballot(t.k1 == b.k1 && b.k1 != 0);
+    const int l1 = m1 ? __ffsll((unsigned long long)m1) - 1 : 0;
+    b.x1 = rl_f(t.x1, l1);
+    b.y1 = rl_f(t.y1, l1);
+    b.c1 = rl_f(t.c1, l1);
+    const uint64_t m2a = __ballot(t.k1 == b.k2 && b.k2 != 0);
+    const uint64_t m2b = __ballot(t.k2 == b.k2 && b.k2 != 0);
+    const int l2a = m2a ? __ffsll((unsigned long long)m2a) - 1 : 0;
+    const int l2b = m2b ? __ffsll((unsigned long long)m2b) - 1 : 0;
+    b.x2 = m2a ? rl_f(t.x1, l2a) : rl_f(t.x2, l2b);
+    b.y2 = m2a ? rl_f(t.y1, l2a) : rl_f(t.y2, l2b);
+    b.c2 = m2a ? rl_f(t.c1, l2a) : rl_f(t.c2, l2b);
+    return b;
 }
 
 struct ColQuery {
@@ -305,61 +337,67 @@ __device__ __forceinline__ ColQuery make_query(float x, float y, float xy_scale)
     return q;
 }
 
-// one column: caf_center_s test, then the score (cifcaf.py:134-139)
+// column k (all rows loaded in one round): caf_center_s test, score (cifcaf.py:134-139)
 template <bool MAXM>
 __device__ __forceinline__ void consider(const float *__restrict__ cf, int64_t hw, const ColQuery &q,
-                                         int k, int o, Top2 &t, int &m) {
-    const float c1 = cf[hw + k], c2 = cf[2 * hw + k];
+                                         int k, int o_or_neg, Top2 &t, int &m) {
+    const float c1 = cf[hw + k], c2 = cf[2 * hw + k], c0 = cf[k];
+    const float tx = cf[5 * hw + k], ty = cf[6 * hw + k], tc = cf[8 * hw + k];
+    const int o = o_or_neg >= 0 ? o_or_neg : __float_as_int(cf[9 * hw + k]);
     if (c1 < q.lo_x || c1 > q.hi_x || c2 < q.lo_y || c2 > q.hi_y) return;
     const float dx = q.x - c1, dy = q.y - c2;
     const float dd = sqrtf(dx * dx + dy * dy);  // np.linalg.norm(axis=0)
     const float qq = (-0.5f * (dd * dd)) / q.sigma2;
-    const float score = (float)exp((double)qq) * cf[k];  // np.exp, correctly rounded
+    const float score = (float)exp((double)qq) * c0;  // np.exp, correctly rounded
     m++;
-    top2_insert<MAXM>(t, score, o, k);
+    top2_insert(t, cand_key<MAXM>(score, o), tx, ty, tc);
 }
 
 // _target_with_blend / _target_with_maxscore (cifcaf.py:147-192) on the merged top-2
 template <bool MAXM>
-__device__ void finish_connection(const float *__restrict__ cf, int64_t hw, Top2 t, int m,
-                                  float out[4]) {
-    m = wave_sum(m);
+__device__ void finish_connection(const Top2 &t, int m, float out[4]) {
+    m = wave_total(m);
     if (m == 0) {
         out[0] = out[1] = out[2] = out[3] = 0.0f;
         return;
     }
-    top2_wave_merge<MAXM>(t);
-    const float *t0 = cf + 5 * hw, *t1 = cf + 6 * hw, *t3 = cf + 8 * hw;
-    const float x1 = t0[t.k1], y1 = t1[t.k1], sc1 = t3[t.k1];
+    const Best2 b = top2_wave(t);
+    const float s1 = key_score(b.k1), s2 = key_score(b.k2);
     if (MAXM) {
-        out[0] = x1;
-        out[1] = y1;
-        out[2] = sc1;
-        out[3] = t.s1;
+        out[0] = b.x1;
+        out[1] = b.y1;
+        out[2] = b.c1;
+        out[3] = s1;
         return;
     }
-    if (m == 1 || t.s2 < 0.01f || t.s2 < 0.5f * t.s1) {
-        out[0] = x1;
-        out[1] = y1;
-        out[2] = sc1;
-        out[3] = t.s1 * 0.5f;
+    if (m == 1 || s2 < 0.01f || s2 < 0.5f * s1) {
+        out[0] = b.x1;
+        out[1] = b.y1;
+        out[2] = b.c1;
+        out[3] = s1 * 0.5f;
         return;
     }
-    const float x2 = t0[t.k2], y2 = t1[t.k2], sc2 = t3[t.k2];
-    const float ex = x1 - x2, ey = y1 - y2;
+    const float ex = b.x1 - b.x2, ey = b.y1 - b.y2;
     const float dist = sqrtf(ex * ex + ey * ey);
-    if (dist > sc1 / 2.0f) {
-        out[0] = x1;
-        out[1] = y1;
-        out[2] = sc1;
-        out[3] = t.s1 * 0.5f;
+    if (dist > b.c1 / 2.0f) {
+        out[0] = b.x1;
+        out[1] = b.y1;
+        out[2] = b.c1;
+        out[3] = s1 * 0.5f;
         return;
     }
-    const float ssum = t.s1 + t.s2;
-    out[0] = (t.s1 * x1 + t.s2 * x2) / ssum;
-    out[1] = (t.s1 * y1 + t.s2 * y2) / ssum;
-    out[2] = (t.s1 * sc1 + t.s2 * sc2) / ssum;
-    out[3] = 0.5f * (t.s1 + t.s2);
+    const float ssum = s1 + s2;
+    out[0] = (s1 * b.x1 + s2 * b.x2) / ssum;
+    out[1] = (s1 * b.y1 + s2 * b.y2) / ssum;
+    out[2] = (s1 * b.c1 + s2 * b.c2) / ssum;
+    out[3] = 0.5f * (s1 + s2);
+}
+
+__device__ __forceinline__ Top2 top2_empty() {
+    Top2 t;
+    t.k1 = t.k2 = 0;
+    t.x1 = t.y1 = t.c1 = t.x2 = t.y2 = t.c2 = 0.0f;
+    return t;
 }
 
 // column set in the reference's order, n columns (the functional API entry point)
@@ -368,22 +406,37 @@ __device__ void grow_connection_flat(const float *__restrict__ cf, int n, int64_
                                      float y, float xy_scale, float out[4]) {
     const int lane = threadIdx.x & 63;
     const ColQuery q = make_query(x, y, xy_scale);
-    Top2 t{0.0f, 0.0f, -1, -1, -1, -1};
+    Top2 t = top2_empty();
     int m = 0;
     for (int i = lane; i < n; i += 64) consider<MAXM>(cf, hw, q, i, i, t, m);
-    finish_connection<MAXM>(cf, hw, t, m, out);
+    finish_connection<MAXM>(t, m, out);
 }
 
+#ifdef PP_STAMPS
+__device__ uint64_t *g_gc_stamps;  // diagnostic: [img][4] section sums of grow_connection
+#define GSTAMP(i)                                                                           \
+    do {                                                                                    \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();                                   \
+        if (lane == 0 && g_gc_stamps) g_gc_stamps[blockIdx.x * 4 + (i)] += t_ - gs_t;        \
+        gs_t = t_;                                                                          \
+    } while (0)
+#else
+#define GSTAMP(i)
+#endif
+
 // bucketed column set (caf_bucketed_kernel): visit only the buckets the 2*scale box
-// overlaps (+ the NaN-source bucket), flattened over the 64 lanes
+// overlaps (+ the NaN-source bucket); segments flattened over the 64 lanes
 template <bool MAXM>
-__device__ void grow_connection(const GrowArgs &g, GrowLDS &L, const float *__restrict__ cf,
+__device__ void grow_connection(const GrowArgs &g, const float *__restrict__ cf,
                                 const int *__restrict__ off, float x, float y, float xy_scale,
                                 float out[4]) {
     const int lane = threadIdx.x & 63;
+#ifdef PP_STAMPS
+    uint64_t gs_t = __builtin_amdgcn_s_memtime();
+#endif
     const int64_t hw = g.hw;
     const ColQuery q = make_query(x, y, xy_scale);
-    Top2 t{0.0f, 0.0f, -1, -1, -1, -1};
+    Top2 t = top2_empty();
     int m = 0;
     int bx0, bx1, by0, by1;
     if (q.lo_x != q.lo_x || q.hi_x != q.hi_x || q.lo_y != q.lo_y || q.hi_y != q.hi_y) {
@@ -414,27 +467,24 @@ __device__ void grow_connection(const GrowArgs &g, GrowLDS &L, const float *__re
             st = off[lo];
             len = off[hi] - st;
         }
-        const int incl = wave_incl_scan(len);
-        const int total = __shfl(incl, 63);
-        L.seg_st[lane] = st;
-        L.seg_pre[lane] = incl - len;
-        __syncthreads();
         const int ng = min(64, nseg - sb);
-        for (int tt = lane; tt < total; tt += 64) {
-            int lo = 0, hi = ng - 1;  // largest segment whose start prefix <= tt
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (L.seg_pre[mid] <= tt)
-                    lo = mid;
-                else
-                    hi = mid - 1;
+        int total = 0;
+        for (int rr = 0; rr < ng; rr++) total += rl_i(len, rr);  // scalar
+        GSTAMP(0);
+        for (int base = 0; base < total; base += 64) {
+            const int tt = base + lane;
+            int k = -1, run = 0;
+            for (int rr = 0; rr < ng; rr++) {  // the segment holding tt (uniform loop)
+                const int l = rl_i(len, rr);
+                if (tt >= run && tt < run + l) k = rl_i(st, rr) + (tt - run);
+                run += l;
             }
-            const int k = L.seg_st[lo] + tt - L.seg_pre[lo];
-            consider<MAXM>(cf, hw, q, k, __float_as_int(cf[9 * hw + k]), t, m);
+            if (k >= 0) consider<MAXM>(cf, hw, q, k, -1, t, m);
         }
-        __syncthreads();
+        GSTAMP(1);
     }
-    finish_connection<MAXM>(cf, hw, t, m, out);
+    finish_connection<MAXM>(t, m, out);
+    GSTAMP(2);
 }
 
 __device__ __forceinline__ float max0(float v) { return (v > 0.0f) ? v : 0.0f; }
@@ -449,40 +499,36 @@ __device__ __forceinline__ const int *col_offs(const GrowArgs &g, int set, int i
     return g.offs[set] + (((int64_t)img * g.C + caf_i) * 2 + dir) * (int64_t)(g.nb + 1);
 }
 
-// cifcaf.py:194-217
-__device__ void connection_value(const GrowArgs &g, GrowLDS &L, int img, int set, int start_i,
-                                 int end_i, bool reverse_match, float out[4]) {
-    int e = 0;
-    for (int t = 0; t < L.bs_n[start_i]; t++)
-        if (L.bs_k[start_i][t] == end_i) e = t;
-    const int caf_i = L.bs_caf[start_i][e];
-    const int fwd = L.bs_fwd[start_i][e];
+// cifcaf.py:194-217 for start joint (jx, jy, jv, js) along CAF caf_i in direction fwd
+__device__ void connection_value(const GrowArgs &g, int img, int set, int caf_i, int fwd,
+                                 float jx, float jy, float jv, float js, bool reverse_match,
+                                 float out[4]) {
     const int df = fwd ? 1 : 0, db = fwd ? 0 : 1;
-    const float xv0 = L.a.data[start_i][0], xv1 = L.a.data[start_i][1], xv2 = L.a.data[start_i][2];
-    const float xy_scale_s = max0(L.a.joint_scales[start_i]);
+    const float xy_scale_s = max0(js);
     const bool maxm = g.cfg.connection_method == 1;
     float nx[4];
     if (maxm)
-        grow_connection<true>(g, L, col_set(g, set, img, caf_i, df), col_offs(g, set, img, caf_i, df),
-                              xv0, xv1, xy_scale_s, nx);
+        grow_connection<true>(g, col_set(g, set, img, caf_i, df), col_offs(g, set, img, caf_i, df),
+                              jx, jy, xy_scale_s, nx);
     else
-        grow_connection<false>(g, L, col_set(g, set, img, caf_i, df),
-                               col_offs(g, set, img, caf_i, df), xv0, xv1, xy_scale_s, nx);
+        grow_connection<false>(g, col_set(g, set, img, caf_i, df),
+                               col_offs(g, set, img, caf_i, df), jx, jy, xy_scale_s, nx);
+
     out[0] = out[1] = out[2] = out[3] = 0.0f;
-    const float ks = sqrtf(nx[3] * xv2);  // geometric mean
+    const float ks = sqrtf(nx[3] * jv);  // geometric mean
     if (ks < g.cfg.keypoint_threshold) return;
     if (nx[3] == 0.0f) return;
     const float xy_scale_t = max0(nx[2]);
     if (reverse_match) {
         float rv[4];
         if (maxm)
-            grow_connection<true>(g, L, col_set(g, set, img, caf_i, db),
+            grow_connection<true>(g, col_set(g, set, img, caf_i, db),
                                   col_offs(g, set, img, caf_i, db), nx[0], nx[1], xy_scale_t, rv);
         else
-            grow_connection<false>(g, L, col_set(g, set, img, caf_i, db),
+            grow_connection<false>(g, col_set(g, set, img, caf_i, db),
                                    col_offs(g, set, img, caf_i, db), nx[0], nx[1], xy_scale_t, rv);
         if (rv[2] == 0.0f) return;  // tests the SCALE (cifcaf.py:212)
-        if (fabsf(xv0 - rv[0]) + fabsf(xv1 - rv[1]) > xy_scale_s) return;
+        if (fabsf(jx - rv[0]) + fabsf(jy - rv[1]) > xy_scale_s) return;
     }
     out[0] = nx[0];
     out[1] = nx[1];
@@ -490,97 +536,250 @@ __device__ void connection_value(const GrowArgs &g, GrowLDS &L, int img, int set
     out[3] = ks;
 }
 
-__device__ void add_to_frontier(GrowLDS &L, int start_i) {
-    for (int e = 0; e < L.bs_n[start_i]; e++) {
-        const int end_i = L.bs_k[start_i][e];
-        if (L.a.data[end_i][2] > 0.0f) continue;
-        if (L.in_frontier[start_i] & (1u << end_i)) continue;
-        HeapEntry x;
-        x.neg = -sqrtf(L.a.data[start_i][2]);
-        x.eval = 0;
-        x.xysv[0] = x.xysv[1] = x.xysv[2] = x.xysv[3] = 0.0f;
-        x.j = start_i;
-        x.k = end_i;
-        heap_push(L, x);
-        L.in_frontier[start_i] |= 1u << end_i;
-        const int t = L.a.n_frontier;
-        if (t < PP_MAX_FRONTIER) {
-            L.a.frontier_pairs[t][0] = (uint8_t)start_i;
-            L.a.frontier_pairs[t][1] = (uint8_t)end_i;
-        } else {
-            L.status |= PP_ST_DEC_OVERFLOW;
+// ---------------------------------------------------------------------------------------
+// the frontier in registers: lane l holds directed-edge slots l and l + 64
+// ---------------------------------------------------------------------------------------
+struct Frontier {
+    int st[2];         // 0 empty, 1 (-max_possible, None, j, k), 2 (-score, xysv, j, k)
+    float neg[2];
+    float x[2], y[2], s[2], v[2];
+    int added[2];      // in_frontier (cifcaf.py:249)
+    int sj[2], sk[2], scaf[2], sfwd[2];  // slot constants
+};
+
+struct Entry {
+    int slot, eval, j, k, caf, fwd;
+    float neg, x, y, s, v;
+};
+
+// tuple order of (neg, None | (x, y, s, v), j, k); a None/tuple tie would raise TypeError
+// in the reference (never happens in a successful run): unevaluated first here
+__device__ __forceinline__ bool entry_less(float na, int ea, float xa, float ya, float sa,
+                                           float va, int ja, int ka, float nb, int eb, float xb,
+                                           float yb, float sb, float vb, int jb, int kb) {
+    if (na != nb) return na < nb;
+    if (ea != eb) return ea < eb;
+    if (ea) {
+        if (xa != xb) return xa < xb;
+        if (ya != yb) return ya < yb;
+        if (sa != sb) return sa < sb;
+        if (va != vb) return va < vb;
+    }
+    if (ja != jb) return ja < jb;
+    return ka < kb;
+}
+
+__device__ __forceinline__ bool slot_less(const Frontier &F, int a, int b) {
+    return entry_less(F.neg[a], F.st[a] == 2, F.x[a], F.y[a], F.s[a], F.v[a], F.sj[a], F.sk[a],
+                      F.neg[b], F.st[b] == 2, F.x[b], F.y[b], F.s[b], F.v[b], F.sj[b], F.sk[b]);
+}
+
+// PriorityQueue.get(): remove and return the smallest live entry (false when empty)
+__device__ bool frontier_pop(Frontier &F, Entry &e) {
+    const int lane = threadIdx.x & 63;
+    int lb = -1;
+    if (F.st[0]) lb = 0;
+    if (F.st[1] && (lb < 0 || slot_less(F, 1, 0))) lb = 1;
+    const uint64_t live = __ballot(lb >= 0);
+    if (live == 0) return false;
+    const int w = lb == 1 ? 1 : 0;
+    const float myneg = lb >= 0 ? F.neg[w] : INFINITY;
+    const float mn = wave_fmin(myneg);
+    uint64_t cand = __ballot(lb >= 0 && myneg == mn);
+    if (cand == 0) cand = live;  // only NaN scores left
+    int win = __ffsll((unsigned long long)cand) - 1;
+    const float my_x = F.x[w], my_y = F.y[w], my_s = F.s[w], my_v = F.v[w];
+    const int my_e = F.st[w] == 2, my_j = F.sj[w], my_k = F.sk[w];
+    if (__popcll(cand) > 1) {  // exact score tie: full tuple comparison (rare)
+        uint64_t rest = cand & (cand - 1);
+        while (rest) {
+            const int c = __ffsll((unsigned long long)rest) - 1;
+            rest &= rest - 1;
+            if (entry_less(rl_f(myneg, c), rl_i(my_e, c), rl_f(my_x, c), rl_f(my_y, c),
+                           rl_f(my_s, c), rl_f(my_v, c), rl_i(my_j, c), rl_i(my_k, c),
+                           rl_f(myneg, win), rl_i(my_e, win), rl_f(my_x, win), rl_f(my_y, win),
+                           rl_f(my_s, win), rl_f(my_v, win), rl_i(my_j, win), rl_i(my_k, win)))
+                win = c;
         }
-        L.a.n_frontier = t + 1;
+    }
+    const int wr = rl_i(w, win);
+    e.slot = win + 64 * wr;
+    e.neg = rl_f(myneg, win);
+    e.eval = rl_i(my_e, win);
+    e.x = rl_f(my_x, win);
+    e.y = rl_f(my_y, win);
+    e.s = rl_f(my_s, win);
+    e.v = rl_f(my_v, win);
+    e.j = rl_i(my_j, win);
+    e.k = rl_i(my_k, win);
+    e.caf = rl_i(wr ? F.scaf[1] : F.scaf[0], win);
+    e.fwd = rl_i(wr ? F.sfwd[1] : F.sfwd[0], win);
+    if (lane == win) F.st[wr] = 0;
+    return true;
+}
+
+// add_to_frontier (cifcaf.py:251-263): the start joint's slots in dict order, one pass
+__device__ void add_to_frontier(const GrowArgs &g, GrowLDS &L, Frontier &F, float av, int start,
+                                float start_v, int &nfr) {
+    const int lane = threadIdx.x & 63;
+    const int lo = g.j_off[start], hi = g.j_off[start + 1];
+    const float neg = -sqrtf(start_v);
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const int d = lane + 64 * r;
+        const float tv = __shfl(av, F.sk[r]);  // target joint's v (all lanes shuffle)
+        const bool elig = d >= lo && d < hi && !(tv > 0.0f) && !F.added[r];
+        const uint64_t m = __ballot(elig);
+        if (elig) {
+            F.st[r] = 1;
+            F.neg[r] = neg;
+            F.added[r] = 1;
+            const int t = nfr + lane_prefix(m);
+            if (t < PP_MAX_FRONTIER) {
+                L.a.frontier_pairs[t][0] = (uint8_t)start;
+                L.a.frontier_pairs[t][1] = (uint8_t)F.sk[r];
+            }
+        }
+        nfr += __popcll(m);
     }
 }
 
-// cifcaf.py:247-307
+// _grow (cifcaf.py:247-307) on the record in L.a (joint data mirrored into registers)
 __device__ void grow(const GrowArgs &g, GrowLDS &L, int img, int set, bool reverse_match) {
-    L.heap_n = 0;
-    for (int j = 0; j < kKP; j++) L.in_frontier[j] = 0u;
-    for (int j = 0; j < g.K; j++) {
-        if (L.a.data[j][2] == 0.0f) continue;
-        add_to_frontier(L, j);
+    const int lane = threadIdx.x & 63;
+    const int K = g.K;
+    float ax = 0.0f, ay = 0.0f, av = 0.0f, as = 0.0f;
+    if (lane < K) {
+        ax = L.a.data[lane][0];
+        ay = L.a.data[lane][1];
+        av = L.a.data[lane][2];
+        as = L.a.joint_scales[lane];
+    }
+    int nfr = L.a.n_frontier, ndec = L.a.n_decoding;
+    Frontier F;
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const int d = lane + 64 * r;
+        const bool ok = d < g.nd;
+        F.st[r] = 0;
+        F.added[r] = 0;
+        F.neg[r] = 0.0f;
+        F.x[r] = F.y[r] = F.s[r] = F.v[r] = 0.0f;
+        F.sj[r] = ok ? g.d_j[d] : 0;
+        F.sk[r] = ok ? g.d_k[d] : 0;
+        F.scaf[r] = ok ? g.d_caf[d] : 0;
+        F.sfwd[r] = ok ? g.d_fwd[d] : 0;
+    }
+    for (int j = 0; j < K; j++) {  // seeding the frontier (cifcaf.py:288-291)
+        const float vj = rl_f(av, j);
+        if (vj == 0.0f) continue;
+        add_to_frontier(g, L, F, av, j, vj, nfr);
     }
     for (;;) {
-        HeapEntry got;
+        // frontier_get (cifcaf.py:265-285)
+        Entry got;
         bool have = false;
-        while (L.heap_n > 0) {
-            const HeapEntry en = heap_pop(L);
-            if (en.eval) {
-                got = en;
+        Entry e;
+        for (;;) {
+            bool popped;
+            {
+                FSTAMP_BEGIN
+                popped = frontier_pop(F, e);
+                FSTAMP_END(L, 0)
+            }
+            if (!popped) break;
+            if (e.eval) {
+                got = e;
                 have = true;
                 break;
             }
-            if (L.a.data[en.k][2] > 0.0f) continue;
+            if (rl_f(av, e.k) > 0.0f) continue;
             float nx[4];
-            connection_value(g, L, img, set, en.j, en.k, reverse_match, nx);
+            {
+#ifdef PP_STAMPS
+                if (lane == 0) L.fst[3] += 1;
+#endif
+                FSTAMP_BEGIN
+                connection_value(g, img, set, e.caf, e.fwd, rl_f(ax, e.j), rl_f(ay, e.j),
+                                 rl_f(av, e.j), rl_f(as, e.j), reverse_match, nx);
+                FSTAMP_END(L, 1)
+            }
             if (nx[3] == 0.0f) continue;
-            HeapEntry ev;
-            ev.neg = -nx[3];
-            ev.eval = 1;
-            ev.xysv[0] = nx[0];
-            ev.xysv[1] = nx[1];
-            ev.xysv[2] = nx[2];
-            ev.xysv[3] = nx[3];
-            ev.j = en.j;
-            ev.k = en.k;
+            e.eval = 1;
+            e.neg = -nx[3];
+            e.x = nx[0];
+            e.y = nx[1];
+            e.s = nx[2];
+            e.v = nx[3];
             if (g.cfg.greedy) {
-                got = ev;
+                got = e;
                 have = true;
                 break;
             }
-            heap_push(L, ev);
+            const int sl = e.slot & 63, sr = e.slot >> 6;  // re-push into the edge's slot
+            if (lane == sl) {
+#pragma unroll
+                for (int r = 0; r < 2; r++) {
+                    if (r != sr) continue;
+                    F.st[r] = 2;
+                    F.neg[r] = e.neg;
+                    F.x[r] = e.x;
+                    F.y[r] = e.y;
+                    F.s[r] = e.s;
+                    F.v[r] = e.v;
+                }
+            }
         }
         if (!have) break;
         const int jsi = got.j, jti = got.k;
-        if (L.a.data[jti][2] > 0.0f) continue;
-        L.a.data[jti][0] = got.xysv[0];
-        L.a.data[jti][1] = got.xysv[1];
-        L.a.data[jti][2] = got.xysv[3];
-        L.a.joint_scales[jti] = got.xysv[2];
-        const int t = L.a.n_decoding;
-        if (t < kKP) {
-            L.a.decoding_pairs[t][0] = (uint8_t)jsi;
-            L.a.decoding_pairs[t][1] = (uint8_t)jti;
-            for (int c = 0; c < 3; c++) {
-                L.a.decoding_xyv[t][c] = L.a.data[jsi][c];
-                L.a.decoding_xyv[t][3 + c] = L.a.data[jti][c];
-            }
-        } else {
-            L.status |= PP_ST_DEC_OVERFLOW;
+        if (rl_f(av, jti) > 0.0f) continue;
+        if (lane == jti) {  // ann.data[jti] = (x, y, score); joint_scales[jti] = s
+            ax = got.x;
+            ay = got.y;
+            av = got.v;
+            as = got.s;
         }
-        L.a.n_decoding = t + 1;
-        add_to_frontier(L, jti);
+        if (lane == 0) {
+            if (ndec < kKP) {
+                L.a.decoding_pairs[ndec][0] = (uint8_t)jsi;
+                L.a.decoding_pairs[ndec][1] = (uint8_t)jti;
+                L.a.decoding_xyv[ndec][0] = rl_f(ax, jsi);
+                L.a.decoding_xyv[ndec][1] = rl_f(ay, jsi);
+                L.a.decoding_xyv[ndec][2] = rl_f(av, jsi);
+                L.a.decoding_xyv[ndec][3] = got.x;
+                L.a.decoding_xyv[ndec][4] = got.y;
+                L.a.decoding_xyv[ndec][5] = got.v;
+            } else {
+                L.status |= PP_ST_DEC_OVERFLOW;
+            }
+        }
+        ndec++;
+        {
+            FSTAMP_BEGIN
+            add_to_frontier(g, L, F, av, jti, got.v, nfr);
+            FSTAMP_END(L, 2)
+        }
     }
+    if (nfr > PP_MAX_FRONTIER && lane == 0) L.status |= PP_ST_DEC_OVERFLOW;
+    if (lane < K) {
+        L.a.data[lane][0] = ax;
+        L.a.data[lane][1] = ay;
+        L.a.data[lane][2] = av;
+        L.a.joint_scales[lane] = as;
+    }
+    if (lane == 0) {
+        L.a.n_frontier = nfr;
+        L.a.n_decoding = ndec;
+    }
+    __syncthreads();
 }
 
 // cifcaf.py:309-331 (the key is the ENCLOSING xyv, App. D item 5)
 __device__ void flood_fill(const GrowArgs &g, GrowLDS &L) {
     L.ff_n = 0;
     auto add = [&](int start_i, float key_v) {
-        for (int e = 0; e < L.bs_n[start_i]; e++) {
-            const int end_i = L.bs_k[start_i][e];
+        for (int e = g.j_off[start_i]; e < g.j_off[start_i + 1]; e++) {
+            const int end_i = g.d_k[e];
             if (L.a.data[end_i][2] > 0.0f) continue;
             FFEntry x;
             x.neg = -key_v;
@@ -665,11 +864,15 @@ __device__ void occ_mark(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccGr
     bool has = false;
     if (lane < K && mark(lane)) has = occ_box(g, o, lane, xy[lane][0], xy[lane][1], scales[lane], box);
     const int area = has ? (box[1] - box[0]) * (box[3] - box[2]) : 0;
-    const int incl = wave_incl_scan(area);
-    const int total = __shfl(incl, 63);
+    int pre = 0, total = 0;
+    for (int i = 0; i < K; i++) {  // exclusive prefix of the box areas (uniform loop)
+        const int ai = rl_i(area, i);
+        pre += (i < lane) ? ai : 0;
+        total += ai;
+    }
     const uint64_t hm = __ballot(has);
     if (lane < K) {
-        L.mark_pre[lane] = incl - area;
+        L.mark_pre[lane] = pre;
         L.mark_box[lane][0] = box[0];
         L.mark_box[lane][1] = box[1];
         L.mark_box[lane][2] = box[2];
@@ -824,25 +1027,12 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
     const int K = g.K;
     const int lane = threadIdx.x & 63;
 
-    // by_source (cifcaf.py:62-65): dict insertion order, later duplicate keys overwrite
     if (lane == 0) {
-        for (int j = 0; j < kKP; j++) L.bs_n[j] = 0;
-        for (int ci = 0; ci < g.C; ci++) {
-            const int j1 = g.skel[2 * ci] - 1, j2 = g.skel[2 * ci + 1] - 1;
-            const int ins[2][3] = {{j1, j2, 1}, {j2, j1, 0}};
-            for (int t = 0; t < 2; t++) {
-                const int s = ins[t][0];
-                int pos = -1;
-                for (int e = 0; e < L.bs_n[s]; e++)
-                    if (L.bs_k[s][e] == ins[t][1]) pos = e;
-                if (pos < 0) pos = L.bs_n[s]++;
-                L.bs_k[s][pos] = (uint8_t)ins[t][1];
-                L.bs_caf[s][pos] = (uint8_t)ci;
-                L.bs_fwd[s][pos] = (uint8_t)ins[t][2];
-            }
-        }
-        L.status = PHASE == 1 ? 0 : g.status[img];
+        L.status = PHASE == 3 ? g.status[img] : 0;
         L.log_n = 0;
+#ifdef PP_STAMPS
+        for (int q = 0; q < 8; q++) L.fst[q] = 0;
+#endif
     }
     __syncthreads();
 
@@ -927,11 +1117,14 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
     const int n_anns = g.n_work[img];
     STAMP(0);
 
-    // ---- complete_annotations (cifcaf.py:333-351) ----
-    // Annotations with every joint set are unchanged by it (their frontier is empty), so
-    // only images flagged by phase 1 run it, and only on annotations with a zero joint.
-    if (g.cfg.force_complete && g.need_complete[img]) {
-        for (int i = 0; i < n_anns; i++) {
+    if (PHASE == 2) {
+        // ---- complete_annotations (cifcaf.py:333-351) ----
+        // Each annotation is completed from its own joints and the read-only B columns, so
+        // the annotations of an image are spread over kCompleteWays workgroups.  Ones with
+        // every joint set are unchanged by it (their frontier is empty) and are skipped,
+        // and images phase 1 did not flag launch nothing.
+        if (!g.need_complete[img]) return;
+        for (int i = blockIdx.y; i < n_anns; i += gridDim.y) {
             bool has0 = false;
             for (int j = 0; j < K; j++) has0 = has0 || work[i].data[j][2] == 0.0f;
             if (!has0) continue;
@@ -949,6 +1142,10 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
             __syncthreads();
             copy_ann(&work[i], &L.a);
         }
+        STAMP(1);
+        STAMP_FLUSH(2);
+        if (lane == 0 && L.status) atomicOr(&g.status[img], L.status);
+        return;
     }
 
     STAMP(1);
@@ -1061,7 +1258,7 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
     }
     __syncthreads();
     STAMP(8);
-    STAMP_FLUSH(2);
+    STAMP_FLUSH(3);
     if (lane == 0) {
         g.counts[img] = n_out;
         g.status[img] = L.status;
@@ -1226,7 +1423,38 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
         g.ww = d.ww;
         g.hw = d.hw;
         g.cfg = *cfg;
-        for (int i = 0; i < 2 * C; i++) g.skel[i] = skeleton[i];
+        // by_source (cifcaf.py:62-65): dict insertion order, later duplicate keys
+        // overwrite the value in place; flattened into directed-edge slots per start joint
+        {
+            int nbs[kKP] = {0};
+            int bk[kKP][kKP], bc[kKP][kKP], bf[kKP][kKP];
+            for (int ci = 0; ci < C; ci++) {
+                const int j1 = skeleton[2 * ci] - 1, j2 = skeleton[2 * ci + 1] - 1;
+                const int ins[2][3] = {{j1, j2, 1}, {j2, j1, 0}};
+                for (int t = 0; t < 2; t++) {
+                    const int st = ins[t][0];
+                    int pos = -1;
+                    for (int e = 0; e < nbs[st]; e++)
+                        if (bk[st][e] == ins[t][1]) pos = e;
+                    if (pos < 0) pos = nbs[st]++;
+                    bk[st][pos] = ins[t][1];
+                    bc[st][pos] = ci;
+                    bf[st][pos] = ins[t][2];
+                }
+            }
+            int d = 0;
+            for (int j = 0; j < K; j++) {
+                g.j_off[j] = (uint8_t)d;
+                for (int e = 0; e < nbs[j]; e++, d++) {
+                    g.d_j[d] = (uint8_t)j;
+                    g.d_k[d] = (uint8_t)bk[j][e];
+                    g.d_caf[d] = (uint8_t)bc[j][e];
+                    g.d_fwd[d] = (uint8_t)bf[j][e];
+                }
+            }
+            g.j_off[K] = (uint8_t)d;
+            g.nd = d;
+        }
         g.occ = (uint8_t *)(ws + d.off_occ);
         g.occ_cap = d.occ_cap;
         g.log = (OccLog *)(ws + d.off_log);
@@ -1238,8 +1466,13 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
         g.ann_cap = ann_capacity;
         g.stamps = nullptr;
 #ifdef PP_STAMPS
-        hipMalloc((void **)&g.stamps, (size_t)n_img * 2 * 12 * sizeof(uint64_t));
-        hipMemsetAsync(g.stamps, 0, (size_t)n_img * 2 * 12 * sizeof(uint64_t), s);
+        hipMalloc((void **)&g.stamps, (size_t)n_img * 3 * 12 * sizeof(uint64_t));
+        hipMemsetAsync(g.stamps, 0, (size_t)n_img * 3 * 12 * sizeof(uint64_t), s);
+        uint64_t *gcs = nullptr;
+        hipMalloc((void **)&gcs, (size_t)n_img * 4 * sizeof(uint64_t));
+        hipMemsetAsync(gcs, 0, (size_t)n_img * 4 * sizeof(uint64_t), s);
+        hipMemcpyToSymbolAsync(HIP_SYMBOL(g_gc_stamps), &gcs, sizeof(gcs), 0,
+                               hipMemcpyHostToDevice, s);
 #endif
         g.n_work = (int *)(ws + d.off_n_work);
         g.need_complete = (int *)(ws + d.off_need);
@@ -1256,11 +1489,16 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
                                      g.need_complete, s);
             if (rc) return rc;
         }
-        hipLaunchKernelGGL(grow_kernel<2>, dim3(n_img), dim3(64), 0, s, g);
-        rc = check_launch("pp_decode_batch(complete + nms)");
+        if (cfg->force_complete) {
+            hipLaunchKernelGGL(grow_kernel<2>, dim3(n_img, kCompleteWays), dim3(64), 0, s, g);
+            rc = check_launch("pp_decode_batch(force complete)");
+            if (rc) return rc;
+        }
+        hipLaunchKernelGGL(grow_kernel<3>, dim3(n_img), dim3(64), 0, s, g);
+        rc = check_launch("pp_decode_batch(nms)");
 #ifdef PP_STAMPS
         hipStreamSynchronize(s);
-        const size_t nst = (size_t)n_img * 2 * 12;
+        const size_t nst = (size_t)n_img * 3 * 12;
         uint64_t *h = (uint64_t *)malloc(nst * sizeof(uint64_t));
         hipMemcpy(h, g.stamps, nst * sizeof(uint64_t), hipMemcpyDeviceToHost);
         const char *path = getenv("PP_STAMPS_OUT");
@@ -1271,6 +1509,18 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
         }
         free(h);
         hipFree(g.stamps);
+        uint64_t *hg = (uint64_t *)malloc((size_t)n_img * 4 * sizeof(uint64_t));
+        hipMemcpy(hg, gcs, (size_t)n_img * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost);
+        double a0 = 0, a1 = 0, a2 = 0;
+        for (int i = 0; i < n_img; i++) {
+            a0 += hg[4 * i];
+            a1 += hg[4 * i + 1];
+            a2 += hg[4 * i + 2];
+        }
+        fprintf(stderr, "grow_connection sections per image: offsets+scan-setup %.0f  columns %.0f  merge %.0f\n",
+                a0 / n_img, a1 / n_img, a2 / n_img);
+        free(hg);
+        hipFree(gcs);
 #endif
     }
     return rc;
@@ -1315,3 +1565,4 @@ extern "C" int pp_grow_connection(const float *d_cols, int64_t n, int64_t pitch,
                            pitch, x, y, xy_scale, d_out);
     return check_launch("pp_grow_connection");
 }
+

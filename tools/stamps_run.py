@@ -14,7 +14,8 @@ from openpifpaf_amd._abi import EVAL_CONFIG, make_config  # noqa: E402
 from openpifpaf_amd.engine import DecodeEngine  # noqa: E402
 
 P1 = ['seed_check', 'ann_init', 'grow', 'copy_ann', 'mark_occ', 'occ_clear']
-P2 = ['load', 'complete', 'nms_filter', 'nms_sort', 'nms_occ', 'nms_clear', 'nms_refilter',
+P2 = ['load', 'complete']  # summed over the image's kCompleteWays workgroups
+P3 = ['load', '-', 'nms_filter', 'nms_sort', 'nms_occ', 'nms_clear', 'nms_refilter',
       'nms_sort2', 'output']
 
 out = os.environ.get('PP_STAMPS_OUT', 'pp_stamps.bin')
@@ -28,11 +29,14 @@ for kind, n, h in (('planted', 256, 80), ('uniform', 32, 80)):
     for _ in range(2):
         eng.launch(c, f, constants.COCO_PERSON_SKELETON, cfg)
     torch.cuda.synchronize()
-    st = np.fromfile(out, dtype=np.uint64).reshape(-1, n, 2, 12)[-1].astype(np.float64)
+    st = np.fromfile(out, dtype=np.uint64).reshape(-1, n, 3, 12)[-1].astype(np.float64)
     print('== {} n={} (mean shader cycles per image)'.format(kind, n))
-    for ph, names in ((0, P1), (1, P2)):
+    for ph, names in ((0, P1), (1, P2), (2, P3)):
         tot = st[:, ph, :len(names)].sum(axis=1).mean()
         print('  phase {} total {:.3e}'.format(ph + 1, tot))
         for i, name in enumerate(names):
             m = st[:, ph, i].mean()
             print('    {:14s} {:12.0f}  {:5.1f}%'.format(name, m, 100 * m / max(tot, 1)))
+        for i, name in ((8, 'n connection'), (9, 'in-grow pop'), (10, 'in-grow connection'),
+                        (11, 'in-grow add')):
+            print('    {:14s} {:12.0f}'.format(name, st[:, ph, i].mean()))
