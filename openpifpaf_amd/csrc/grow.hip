@@ -108,7 +108,8 @@ struct GrowArgs {
     int ann_cap;
     uint64_t *stamps;         // diagnostic build: (n_img, 3, 12) cycle sums, else NULL
     int *n_work;              // (n_img) annotations after the seed loop (phase 1 -> 2)
-    int *need_complete;       // (n_img) 1 if force-complete has work (gates the B columns)
+    int *need_complete;       // (n_img) bitmask of joints left unset by the seed loop in any
+                              // annotation (force-complete has work iff != 0; gates the B sets)
     // outputs
     pp_ann *out;
     int *counts;
@@ -810,10 +811,16 @@ __device__ void flood_fill(const GrowArgs &g, GrowLDS &L) {
 // ---------------------------------------------------------------------------------------
 // occupancy (occupancy.py:10-47, decoder/utils.py:61-66)
 // ---------------------------------------------------------------------------------------
+// u8 planes (f, h, w) stored with a row pitch of round_up(w, 16) bytes, so that no two
+// rows (and no two planes) share a 16-byte chunk: marking updates whole chunks.
 struct OccGrid {
     uint8_t *p;
-    int f, h, w;
+    int f, h, w, pitch;
 };
+
+__device__ __forceinline__ OccGrid occ_grid(uint8_t *p, int f, int h, int w) {
+    return OccGrid{p, f, h, w, (w + 15) & ~15};
+}
 
 __device__ __forceinline__ long round_half_even(float x) { return (long)rintf(x); }
 
@@ -824,7 +831,7 @@ __device__ bool occ_get(const OccGrid &o, int f, float x, float y, float red) {
     x = clip_ref(x / red, 0.0f, (float)(o.w - 1));
     y = clip_ref(y / red, 0.0f, (float)(o.h - 1));
     const int xi = (int)x, yi = (int)y;
-    return o.p[((int64_t)f * o.h + yi) * o.w + xi] != 0;
+    return o.p[((int64_t)f * o.h + yi) * o.pitch + xi] != 0;
 }
 
 // Occupancy.set box (occupancy.py:31-39 + utils.py:61-66) of joint f; false when empty
@@ -863,7 +870,8 @@ __device__ void occ_mark(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccGr
     int box[4] = {0, 0, 0, 0};
     bool has = false;
     if (lane < K && mark(lane)) has = occ_box(g, o, lane, xy[lane][0], xy[lane][1], scales[lane], box);
-    const int area = has ? (box[1] - box[0]) * (box[3] - box[2]) : 0;
+    // work items: (row, 16-byte chunk) pairs of the box
+    const int area = has ? (box[3] - box[2]) * (((box[1] - 1) >> 4) - (box[0] >> 4) + 1) : 0;
     int pre = 0, total = 0;
     for (int i = 0; i < K; i++) {  // exclusive prefix of the box areas (uniform loop)
         const int ai = rl_i(area, i);
@@ -891,20 +899,57 @@ __device__ void occ_mark(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccGr
         }
     }
     __syncthreads();
-    for (int t = lane; t < total; t += 64) {
-        int lo = 0, hi = K - 1;  // largest joint whose area prefix <= t
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (L.mark_pre[mid] <= t)
-                lo = mid;
-            else
-                hi = mid - 1;
+    // Within one call every chunk is updated by one lane only (one box per joint plane,
+    // rows padded to whole chunks), so a batch of chunks is loaded before any is stored.
+    // u8 += 1 with wrap on the bytes inside the box: ((v & 0x7f..) + inc) ^ (v & 0x80..).
+    constexpr int kB = 4;
+    for (int t0 = 0; t0 < total; t0 += 64 * kB) {
+        uint4 *cell[kB];
+        uint4 inc[kB], val[kB];
+#pragma unroll
+        for (int u = 0; u < kB; u++) {
+            const int t = t0 + u * 64 + lane;
+            cell[u] = nullptr;
+            inc[u] = make_uint4(0, 0, 0, 0);
+            if (t < total) {
+                int lo = 0, hi = K - 1;  // largest joint whose item prefix <= t
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (L.mark_pre[mid] <= t)
+                        lo = mid;
+                    else
+                        hi = mid - 1;
+                }
+                const int r = t - L.mark_pre[lo];
+                const int x0 = L.mark_box[lo][0], x1 = L.mark_box[lo][1];
+                const int c0 = x0 >> 4, nch = ((x1 - 1) >> 4) - c0 + 1;
+                const int yy = L.mark_box[lo][2] + r / nch, cx = (c0 + r % nch) << 4;
+                cell[u] = reinterpret_cast<uint4 *>(&o.p[((int64_t)lo * o.h + yy) * o.pitch + cx]);
+                uint32_t w4[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    uint32_t m = 0;
+#pragma unroll
+                    for (int bq = 0; bq < 4; bq++) {
+                        const int x = cx + 4 * q + bq;
+                        m |= (x >= x0 && x < x1) ? (1u << (8 * bq)) : 0u;
+                    }
+                    w4[q] = m;
+                }
+                inc[u] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+            }
         }
-        const int u = t - L.mark_pre[lo];
-        const int bw = L.mark_box[lo][1] - L.mark_box[lo][0];
-        const int yy = L.mark_box[lo][2] + u / bw, xx = L.mark_box[lo][0] + u % bw;
-        uint8_t *c = &o.p[((int64_t)lo * o.h + yy) * o.w + xx];
-        *c = (uint8_t)(*c + 1);
+#pragma unroll
+        for (int u = 0; u < kB; u++) val[u] = cell[u] ? *cell[u] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < kB; u++) {
+            if (!cell[u]) continue;
+            const uint4 v = val[u], m = inc[u];
+            *cell[u] = make_uint4(((v.x & 0x7F7F7F7Fu) + m.x) ^ (v.x & 0x80808080u),
+                                  ((v.y & 0x7F7F7F7Fu) + m.y) ^ (v.y & 0x80808080u),
+                                  ((v.z & 0x7F7F7F7Fu) + m.z) ^ (v.z & 0x80808080u),
+                                  ((v.w & 0x7F7F7F7Fu) + m.w) ^ (v.w & 0x80808080u));
+        }
     }
     const int nm = __popcll(hm);
     if (L.log_n + nm > g.log_cap) L.status |= PP_ST_NMS_OVERFLOW;
@@ -922,10 +967,12 @@ __device__ void occ_clear(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccG
         const int e = e0 + lane;
         OccLog l{0, 0, 0, 0, 0};
         if (e < n) l = log[e];
-        const int area = (e < n) ? (l.x1 - l.x0) * (l.y1 - l.y0) : 0;
-        for (int t = 0; t < area; t++) {
-            const int bw = l.x1 - l.x0;
-            o.p[((int64_t)l.f * o.h + l.y0 + t / bw) * o.w + l.x0 + t % bw] = 0;
+        // bytes outside the marked boxes are zero already: clear whole chunks
+        const int c0 = l.x0 >> 4, nch = (e < n) ? ((l.x1 - 1) >> 4) - c0 + 1 : 0;
+        const int items = (e < n) ? nch * (l.y1 - l.y0) : 0;
+        for (int t = 0; t < items; t++) {
+            uint8_t *c = &o.p[((int64_t)l.f * o.h + l.y0 + t / nch) * o.pitch + ((c0 + t % nch) << 4)];
+            *reinterpret_cast<uint4 *>(c) = make_uint4(0, 0, 0, 0);
         }
     }
     L.log_n = 0;
@@ -1048,12 +1095,12 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
         // test of the next 64 seeds runs in parallel (one lane each) and the first free seed
         // starts the next annotation; the occupied ones before it are skipped exactly as the
         // sequential loop skips them.
-        OccGrid occ{occ_base, K, (int)((double)g.hh / g.cfg.occupancy_reduction),
-                    (int)((double)g.ww / g.cfg.occupancy_reduction)};
+        const OccGrid occ = occ_grid(occ_base, K, (int)((double)g.hh / g.cfg.occupancy_reduction),
+                                     (int)((double)g.ww / g.cfg.occupancy_reduction));
         const int n_seeds = min(g.seed_counts[img], g.seed_cap);
         const pp_seed *seeds = g.seeds + (int64_t)img * g.seed_cap;
         int n_anns = 0;
-        bool need_complete = false;
+        uint32_t unset_mask = 0;
         int s = 0;
         while (s < n_seeds) {
             const int idx = s + lane;
@@ -1098,7 +1145,8 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
             n_anns++;
             STAMP(3);
             // mark_occupied (cifcaf.py:87-93): every joint with v != 0, in one pass
-            for (int j = 0; j < K; j++) need_complete = need_complete || L.a.data[j][2] == 0.0f;
+            for (int j = 0; j < K; j++)
+                unset_mask |= (L.a.data[j][2] > 0.0f) ? 0u : (1u << j);
             occ_mark(g, L, log, occ, L.a.data, L.a.joint_scales, K,
                      [&](int j) { return L.a.data[j][2] != 0.0f; });
             STAMP(4);
@@ -1109,7 +1157,7 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
         STAMP_FLUSH(1);
         if (lane == 0) {
             g.n_work[img] = n_anns;
-            g.need_complete[img] = (g.cfg.force_complete && need_complete) ? 1 : 0;
+            g.need_complete[img] = g.cfg.force_complete ? (int)unset_mask : 0;
             g.status[img] = L.status;
         }
         return;
@@ -1192,8 +1240,8 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
             // Occupancy((K, int(max y + 1), int(max x + 1)), 2, min_scale=4)  (nms.py:27-31)
             const long oh = (long)((double)(long)(my + 1.0f) / g.cfg.occupancy_reduction);
             const long ow = (long)((double)(long)(mx + 1.0f) / g.cfg.occupancy_reduction);
-            OccGrid no{occ_base, K, (int)(oh > 0 ? oh : 0), (int)(ow > 0 ? ow : 0)};
-            if ((int64_t)K * no.h * no.w > g.occ_cap) {
+            const OccGrid no = occ_grid(occ_base, K, (int)(oh > 0 ? oh : 0), (int)(ow > 0 ? ow : 0));
+            if ((int64_t)K * no.h * no.pitch > g.occ_cap) {
                 L.status |= PP_ST_NMS_OVERFLOW;
             } else {
                 int np = 1;
@@ -1310,7 +1358,7 @@ static DecodeLayout make_layout(int n_img, int K, int C, int H, int W, const pp_
     d.log_cap = K * ann_cap;
     const int64_t oh = (int64_t)((double)d.hh / cfg->occupancy_reduction);
     const int64_t ow = (int64_t)((double)d.ww / cfg->occupancy_reduction);
-    d.occ_cap = (int64_t)align_up((size_t)(K * (oh + kOccMargin) * (ow + kOccMargin)));
+    d.occ_cap = (int64_t)align_up((size_t)(K * (oh + kOccMargin) * ((ow + kOccMargin + 15) & ~15)));
     size_t o = 0;
     auto take = [&](size_t bytes) {
         const size_t at = o;

@@ -312,7 +312,10 @@ struct CafBArgs {
     float inv_e;        // 1 / bucket edge (a power of two: exact)
     float *cols;        // (n_img, C, 2, 10, H*W): dir 0 backward, 1 forward
     int *offs;          // (n_img, C, 2, nb + 1)
-    const int *gate;    // (n_img) or NULL
+    // (n_img) or NULL: bitmask of the joints force-complete may still set.  Completion
+    // only evaluates connections INTO unset joints (cifcaf.py:253, 272), so a direction
+    // whose target joint is set everywhere is never read and its set is left empty.
+    const int *gate;
     int j1[kMaxCaf], j2[kMaxCaf];
 };
 
@@ -333,7 +336,11 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
     const int nb = a.nb;
     int *offs_b = a.offs + (fld * 2 + 0) * (int64_t)(nb + 1);
     int *offs_f = a.offs + (fld * 2 + 1) * (int64_t)(nb + 1);
-    if (a.gate && !a.gate[img]) {
+    const int j1i = a.j1[ci], j2i = a.j2[ci];
+    // backward columns end at j1, forward ones at j2
+    const bool need_b = !a.gate || ((a.gate[img] >> j1i) & 1);
+    const bool need_f = !a.gate || ((a.gate[img] >> j2i) & 1);
+    if (!need_b && !need_f) {
         for (int i = threadIdx.x; i <= nb; i += 256) {
             offs_b[i] = 0;
             offs_f[i] = 0;
@@ -341,9 +348,8 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
         return;
     }
     const float *p = a.caf + fld * 9 * hw;
-    const int j1i = a.j1[ci], j2i = a.j2[ci];
-    const bool use1 = a.cif_floor < 1.0f && j1i < a.K;
-    const bool use2 = a.cif_floor < 1.0f && j2i < a.K;
+    const bool use1 = need_b && a.cif_floor < 1.0f && j1i < a.K;
+    const bool use2 = need_f && a.cif_floor < 1.0f && j2i < a.K;
     const float *t1 = a.hr + ((int64_t)img * a.K + (use1 ? j1i : 0)) * a.hh * a.pitch;
     const float *t2 = a.hr + ((int64_t)img * a.K + (use2 ? j2i : 0)) * a.hh * a.pitch;
     for (int i = threadIdx.x; i <= nb; i += 256) {
@@ -369,8 +375,8 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
         if (use2)
             sf = score * (a.cif_floor + a.one_minus_floor *
                                             hr_lookup(t2, a.hh, a.ww, a.pitch, nine[5], nine[6], 0.0f));
-        kb = sb > a.th;
-        kf = sf > a.th;
+        kb = need_b && sb > a.th;
+        kf = need_f && sf > a.th;
     };
 
     // pass 1: bucket histograms (backward sources are (x2, y2), forward (x1, y1))
