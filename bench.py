@@ -68,6 +68,7 @@ def main():
     from openpifpaf_amd import build as ppbuild
     ppbuild.build(verbose=False)
     from openpifpaf_amd import constants, synthetic
+    from openpifpaf_amd.distributed import gather_records
     from openpifpaf_amd._abi import EVAL_CONFIG, PREDICT_CONFIG, make_config
     from openpifpaf_amd.engine import (STAGE_CAF, STAGE_CIFHR, STAGE_GROW, STAGE_SEEDS,
                                        DecodeEngine)
@@ -102,9 +103,9 @@ def main():
             ev[4].record(stream)
         recs = None
         if stages & STAGE_GROW:
-            recs, _ = eng.fetch(b)  # packed records -> host (synchronises)
+            recs, offsets = eng.fetch(b)  # packed records -> host (synchronises)
             if world > 1:
-                recs = gather_records(recs, dist, dev)
+                recs, _ = gather_records(recs, offsets, dist, dev)
         if timed:
             torch.cuda.synchronize()
             for si in range(4):
@@ -174,6 +175,10 @@ def main():
             'algorithmic_bytes_per_launch': cifhr_bytes, 'traffic': None,
         },
     }
+    default_run = (args.workload == 'cfg3' and args.generator == 'planted' and
+                   args.mode == 'eval' and batch == WORKLOADS['cfg3']['batch'])
+    if default_run:
+        line['roofline'].update(committed_traffic())
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line['cpu_baseline'] = cpu_baseline(cif_h, caf_h, skeleton, cfg, args.cpu_seconds)
     if rank == 0:
@@ -182,25 +187,19 @@ def main():
         dist.destroy_process_group()
 
 
-def gather_records(recs, dist, dev):
-    """All-gather every rank's packed pp_ann records (padded to the largest count)."""
-    import torch
-    from openpifpaf_amd._abi import ANN_DTYPE
-    world = dist.get_world_size()
-    n = torch.tensor([len(recs)], dtype=torch.int64, device=dev)
-    counts = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(counts, n)
-    counts = [int(c.item()) for c in counts]
-    width = ANN_DTYPE.itemsize
-    cap = max(1, max(counts))
-    buf = torch.zeros((cap, width), dtype=torch.uint8, device=dev)
-    if len(recs):
-        buf[:len(recs)] = torch.from_numpy(recs.view(np.uint8).reshape(-1, width)).to(dev)
-    out = torch.empty((world * cap, width), dtype=torch.uint8, device=dev)
-    dist.all_gather_into_tensor(out, buf)
-    host = out.cpu().numpy()
-    parts = [host[r * cap:r * cap + counts[r]] for r in range(world)]
-    return np.frombuffer(np.concatenate(parts).tobytes(), dtype=ANN_DTYPE)
+def committed_traffic():
+    """HBM bytes per CifHr launch from the newest committed PMC profile of this same
+    workload (profiles/<tag>_summary.json, written by tools/prof_summary.py from the
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of tools/gpu_profile.sh; counters cannot be
+    read from inside the timed process)."""
+    import glob
+    paths = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_summary.json')))
+    if not paths:
+        return {}
+    with open(paths[-1]) as f:
+        summ = json.load(f)
+    return {'traffic': summ['cifhr_traffic_bytes'],
+            'traffic_source': 'profiles/' + os.path.basename(paths[-1])}
 
 
 def cpu_baseline(cif, caf, skeleton, cfg, budget_s):

@@ -119,7 +119,12 @@ class DecodeEngine:
         idx = np.concatenate([i * b.cap + np.arange(c) for i, c in enumerate(counts) if c])
         rows = b.anns.view(b.n * b.cap, ANN_DTYPE.itemsize)
         sel = rows.index_select(0, torch.from_numpy(idx).to(rows.device))
-        return np.frombuffer(sel.cpu().numpy().tobytes(), dtype=ANN_DTYPE), offsets
+        # pinned destination from torch's caching host allocator: full-rate D2H, and the
+        # returned array owns the block (released to the cache when the caller drops it)
+        host = torch.empty(sel.shape, dtype=torch.uint8, pin_memory=True)
+        host.copy_(sel, non_blocking=True)
+        torch.cuda.current_stream(rows.device).synchronize()
+        return host.numpy().reshape(-1).view(ANN_DTYPE), offsets
 
 
 _ENGINE = None
