@@ -168,7 +168,8 @@ int pp_decode_batch(const float *d_cif, const float *d_caf, int32_t n_img, int32
 
 /*
  * The same decode split into stages for measurement: bit 1 CifHr, 2 CifSeeds,
- * 4 CafScored (both thresholds), 8 seed loop + grow + complete + NMS.  Stage buffers live
+ * 4 CafScored at caf_threshold, 8 seed loop + grow + complete + NMS (stage 8 also builds
+ * the complete_caf_threshold column sets, only where force-complete needs them).  Stage buffers live
  * in the workspace, so calling the stages in order with the same workspace equals one
  * pp_decode_batch call.  pp_decode_batch == pp_decode_stages(..., 15, stream).
  *
