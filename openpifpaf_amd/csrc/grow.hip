@@ -83,7 +83,7 @@ struct GrowArgs {
     const pp_seed *seeds;
     const int *seed_counts;
     int seed_cap;
-    const float *cols[2];     // bucketed column sets (n_img, C, 2, 10, H*W): set A at
+    const float *cols[2];     // bucketed column sets (n_img, C, 2, kColRows, H*W): set A at
                               // caf_threshold, set B at complete_caf_threshold
     const int *offs[2];       // bucket boundaries (n_img, C, 2, nb + 1)
     int bw, bh, nb;           // bucket grid (see caf_bucketed_kernel)
@@ -102,6 +102,8 @@ struct GrowArgs {
     OccLog *log;
     int log_cap;              // entries per image
     pp_ann *work;             // working annotations
+    pp_ann *spec;             // (n_img, kSpecCache) speculatively grown annotations
+    float spec_far;           // seed-loop speculation distance, in joint scales
     double *nms_score;        // (n_img, ann_cap)
     int *nms_idx;             // (n_img, 2 * ann_cap + ann_np)
     int ann_np;               // next pow2 >= ann_cap
@@ -130,6 +132,15 @@ struct GrowLDS {
     uint64_t fst[8];  // inside-grow section sums (diagnostic build)
 #endif
 };
+
+// Orders this wave's LDS / global accesses the way __syncthreads() does (workgroup-scope
+// fence: outstanding stores complete before later loads) without the s_barrier, so the
+// helpers below can run in ONE wave of a multi-wave workgroup (the seed loop's committer)
+// as well as in single-wave workgroups.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
 
 __device__ __forceinline__ float rl_f(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
@@ -338,13 +349,16 @@ __device__ __forceinline__ ColQuery make_query(float x, float y, float xy_scale)
     return q;
 }
 
-// column k (all rows loaded in one round): caf_center_s test, score (cifcaf.py:134-139)
-template <bool MAXM>
+// column k (all rows loaded in one round): caf_center_s test, score (cifcaf.py:134-139).
+// PACKED: the decoder's kColRows layout (index in row 6); else the reference's 9 rows
+// with the column's position k as its index.
+template <bool MAXM, bool PACKED>
 __device__ __forceinline__ void consider(const float *__restrict__ cf, int64_t hw, const ColQuery &q,
-                                         int k, int o_or_neg, Top2 &t, int &m) {
+                                         int k, Top2 &t, int &m) {
     const float c1 = cf[hw + k], c2 = cf[2 * hw + k], c0 = cf[k];
-    const float tx = cf[5 * hw + k], ty = cf[6 * hw + k], tc = cf[8 * hw + k];
-    const int o = o_or_neg >= 0 ? o_or_neg : __float_as_int(cf[9 * hw + k]);
+    const float tx = cf[(PACKED ? 3 : 5) * hw + k], ty = cf[(PACKED ? 4 : 6) * hw + k];
+    const float tc = cf[(PACKED ? 5 : 8) * hw + k];
+    const int o = PACKED ? __float_as_int(cf[6 * hw + k]) : k;
     if (c1 < q.lo_x || c1 > q.hi_x || c2 < q.lo_y || c2 > q.hi_y) return;
     const float dx = q.x - c1, dy = q.y - c2;
     const float dd = sqrtf(dx * dx + dy * dy);  // np.linalg.norm(axis=0)
@@ -409,7 +423,7 @@ __device__ void grow_connection_flat(const float *__restrict__ cf, int n, int64_
     const ColQuery q = make_query(x, y, xy_scale);
     Top2 t = top2_empty();
     int m = 0;
-    for (int i = lane; i < n; i += 64) consider<MAXM>(cf, hw, q, i, i, t, m);
+    for (int i = lane; i < n; i += 64) consider<MAXM, false>(cf, hw, q, i, t, m);
     finish_connection<MAXM>(t, m, out);
 }
 
@@ -418,7 +432,7 @@ __device__ uint64_t *g_gc_stamps;  // diagnostic: [img][4] section sums of grow_
 #define GSTAMP(i)                                                                           \
     do {                                                                                    \
         const uint64_t t_ = __builtin_amdgcn_s_memtime();                                   \
-        if (lane == 0 && g_gc_stamps) g_gc_stamps[blockIdx.x * 4 + (i)] += t_ - gs_t;        \
+        if (lane == 0 && g_gc_stamps) atomicAdd((unsigned long long *)&g_gc_stamps[blockIdx.x * 4 + (i)], (unsigned long long)(t_ - gs_t));        \
         gs_t = t_;                                                                          \
     } while (0)
 #else
@@ -480,7 +494,7 @@ __device__ void grow_connection(const GrowArgs &g, const float *__restrict__ cf,
                 if (tt >= run && tt < run + l) k = rl_i(st, rr) + (tt - run);
                 run += l;
             }
-            if (k >= 0) consider<MAXM>(cf, hw, q, k, -1, t, m);
+            if (k >= 0) consider<MAXM, true>(cf, hw, q, k, t, m);
         }
         GSTAMP(1);
     }
@@ -492,7 +506,7 @@ __device__ __forceinline__ float max0(float v) { return (v > 0.0f) ? v : 0.0f; }
 
 __device__ __forceinline__ const float *col_set(const GrowArgs &g, int set, int img, int caf_i,
                                                 int dir) {
-    return g.cols[set] + (((int64_t)img * g.C + caf_i) * 2 + dir) * 10 * g.hw;
+    return g.cols[set] + (((int64_t)img * g.C + caf_i) * 2 + dir) * kColRows * g.hw;
 }
 
 __device__ __forceinline__ const int *col_offs(const GrowArgs &g, int set, int img, int caf_i,
@@ -583,14 +597,16 @@ __device__ bool frontier_pop(Frontier &F, Entry &e) {
     if (F.st[1] && (lb < 0 || slot_less(F, 1, 0))) lb = 1;
     const uint64_t live = __ballot(lb >= 0);
     if (live == 0) return false;
-    const int w = lb == 1 ? 1 : 0;
-    const float myneg = lb >= 0 ? F.neg[w] : INFINITY;
+    const bool w1 = lb == 1;  // selects, not F.x[w]: a dynamic index sends F to scratch
+    const float myneg = lb >= 0 ? (w1 ? F.neg[1] : F.neg[0]) : INFINITY;
     const float mn = wave_fmin(myneg);
     uint64_t cand = __ballot(lb >= 0 && myneg == mn);
     if (cand == 0) cand = live;  // only NaN scores left
     int win = __ffsll((unsigned long long)cand) - 1;
-    const float my_x = F.x[w], my_y = F.y[w], my_s = F.s[w], my_v = F.v[w];
-    const int my_e = F.st[w] == 2, my_j = F.sj[w], my_k = F.sk[w];
+    const float my_x = w1 ? F.x[1] : F.x[0], my_y = w1 ? F.y[1] : F.y[0];
+    const float my_s = w1 ? F.s[1] : F.s[0], my_v = w1 ? F.v[1] : F.v[0];
+    const int my_e = (w1 ? F.st[1] : F.st[0]) == 2, my_j = w1 ? F.sj[1] : F.sj[0];
+    const int my_k = w1 ? F.sk[1] : F.sk[0];
     if (__popcll(cand) > 1) {  // exact score tie: full tuple comparison (rare)
         uint64_t rest = cand & (cand - 1);
         while (rest) {
@@ -603,7 +619,7 @@ __device__ bool frontier_pop(Frontier &F, Entry &e) {
                 win = c;
         }
     }
-    const int wr = rl_i(w, win);
+    const int wr = rl_i(w1 ? 1 : 0, win);
     e.slot = win + 64 * wr;
     e.neg = rl_f(myneg, win);
     e.eval = rl_i(my_e, win);
@@ -615,7 +631,12 @@ __device__ bool frontier_pop(Frontier &F, Entry &e) {
     e.k = rl_i(my_k, win);
     e.caf = rl_i(wr ? F.scaf[1] : F.scaf[0], win);
     e.fwd = rl_i(wr ? F.sfwd[1] : F.sfwd[0], win);
-    if (lane == win) F.st[wr] = 0;
+    if (lane == win) {
+        if (wr)
+            F.st[1] = 0;
+        else
+            F.st[0] = 0;
+    }
     return true;
 }
 
@@ -772,7 +793,7 @@ __device__ void grow(const GrowArgs &g, GrowLDS &L, int img, int set, bool rever
         L.a.n_frontier = nfr;
         L.a.n_decoding = ndec;
     }
-    __syncthreads();
+    wave_sync();
 }
 
 // cifcaf.py:309-331 (the key is the ENCLOSING xyv, App. D item 5)
@@ -898,7 +919,7 @@ __device__ void occ_mark(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccGr
             }
         }
     }
-    __syncthreads();
+    wave_sync();
     // Within one call every chunk is updated by one lane only (one box per joint plane,
     // rows padded to whole chunks), so a batch of chunks is loaded before any is stored.
     // u8 += 1 with wrap on the bytes inside the box: ((v & 0x7f..) + inc) ^ (v & 0x80..).
@@ -953,14 +974,14 @@ __device__ void occ_mark(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccGr
     }
     const int nm = __popcll(hm);
     if (L.log_n + nm > g.log_cap) L.status |= PP_ST_NMS_OVERFLOW;
-    __syncthreads();
+    wave_sync();
     L.log_n = L.log_n + nm;
-    __syncthreads();
+    wave_sync();
 }
 
 // zero every box the launch marked, so the next launch starts from a clean grid
 __device__ void occ_clear(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccGrid &o) {
-    __syncthreads();
+    wave_sync();
     const int n = L.log_n < g.log_cap ? L.log_n : g.log_cap;
     const int lane = threadIdx.x & 63;
     for (int e0 = 0; e0 < n; e0 += 64) {  // 64 boxes per round, one per lane
@@ -976,7 +997,7 @@ __device__ void occ_clear(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccG
         }
     }
     L.log_n = 0;
-    __syncthreads();
+    wave_sync();
 }
 
 // Annotation.score() (annotation.py:24-28, 60-71) in float64, collective over the wave:
@@ -995,7 +1016,7 @@ __device__ double ann_score(GrowLDS &L, const float (*data)[3], int K) {
         const double w = (rank < 3 ? 3.0 : 1.0) / ws;
         L.prod[rank] = w * (double)vj;
     }
-    __syncthreads();
+    wave_sync();
     if (lane == 0) {
         const double *a = L.prod;
         double res;
@@ -1021,9 +1042,9 @@ __device__ double ann_score(GrowLDS &L, const float (*data)[3], int K) {
         }
         L.score_bc = res;
     }
-    __syncthreads();
+    wave_sync();
     const double res = L.score_bc;
-    __syncthreads();
+    wave_sync();
     return res;
 }
 
@@ -1032,13 +1053,13 @@ __device__ void copy_ann(pp_ann *dst, const pp_ann *src) {
     uint32_t *d = reinterpret_cast<uint32_t *>(dst);
     constexpr int nw = sizeof(pp_ann) / 4;
     for (int t = threadIdx.x & 63; t < nw; t += 64) d[t] = s[t];
-    __syncthreads();
+    wave_sync();
 }
 
 // stable sort of idx[0..n) by descending score (sorted(anns, key=lambda a: -a.score()))
 __device__ void sort_by_score(int *perm, int np, int n, const double *score) {
     for (int i = threadIdx.x & 63; i < np; i += 64) perm[i] = i;
-    __syncthreads();
+    wave_sync();
     for (int k = 2; k <= np; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
             for (int i = threadIdx.x & 63; i < np; i += 64) {
@@ -1059,7 +1080,262 @@ __device__ void sort_by_score(int *perm, int np, int n, const double *score) {
                     }
                 }
             }
-            __syncthreads();
+            wave_sync();
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// seed loop (cifcaf.py:84-108): one workgroup of kSeedWaves waves per image
+// ---------------------------------------------------------------------------------------
+// The loop is sequential: whether a seed starts an annotation depends on the occupancy
+// marks of every annotation before it.  But _grow from a seed is a pure function of the
+// seed and the CAF columns, so helper waves grow seeds the loop is LIKELY to reach next
+// while wave 0 grows the one it needs now; wave 0 then commits strictly in the reference
+// order (the next free seed, cifcaf.py:100-104) and takes a seed's annotation from the
+// cache when a helper grew it already.  Speculation only changes WHEN an annotation is
+// computed, never which seeds start one or what they contain.
+//
+// Helpers pick free seeds after the committed one that lie far (kSpecFar joint scales,
+// Chebyshev) from it, from each other and from the cached ones, since seeds near an
+// annotation's joints are the ones its occupancy marks will cover.
+constexpr int kSeedWaves = 8;
+constexpr int kSpecCache = 16;     // speculative annotations kept per image
+constexpr int kSpecScan = 128;     // seeds after the committed one examined per round
+// distance (joint scales) a helper's seed keeps from the committed one and from the
+// round's other picks; cached annotations are excluded by their exact occupancy boxes.
+// Throughput is flat for 0-4 (both generators) and drops beyond 8.
+constexpr float kSpecFar = 4.0f;
+
+struct SeedLoopShared {
+    int task[kSeedWaves];          // seed each wave grows this round (-1 idle)
+    int task_slot[kSeedWaves];     // cache slot a helper's annotation goes to
+    int cache_seed[kSpecCache];    // seed index held by a cache slot (< current: dead)
+    float cache_x[kSpecCache], cache_y[kSpecCache], cache_s[kSpecCache];  // seed position
+    int cache_ready[kSpecCache];   // the slot's annotation is grown (joints below valid)
+    float4 cache_j[kSpecCache][kKP];  // its joints (x, y, v, scale)
+    int done;
+};
+
+__device__ __forceinline__ bool spec_far(float far, float xa, float ya, float sa, float xb,
+                                         float yb, float sb) {
+    const float r = far * fmaxf(fmaxf(sa, sb), 1.0f);
+    return fabsf(xa - xb) > r || fabsf(ya - yb) > r;
+}
+
+// Annotation(keypoints, out_skeleton).add(f, (x, y, v)); joint_scales[f] = s
+__device__ void ann_from_seed(GrowLDS &L, const pp_seed &sd, int K, int img) {
+    const int lane = threadIdx.x & 63;
+    uint32_t *z = reinterpret_cast<uint32_t *>(&L.a);
+    for (int t = lane; t < (int)(sizeof(pp_ann) / 4); t += 64) z[t] = 0u;
+    wave_sync();
+    if (lane == 0) {
+        L.a.n_keypoints = K;
+        L.a.image = img;
+        L.a.data[sd.field][0] = sd.x;
+        L.a.data[sd.field][1] = sd.y;
+        L.a.data[sd.field][2] = sd.v;
+        L.a.joint_scales[sd.field] = sd.s;
+    }
+    wave_sync();
+}
+
+__global__ __launch_bounds__(64 * kSeedWaves) void seed_loop_kernel(GrowArgs g) {
+    __shared__ GrowLDS Ls[kSeedWaves];
+    __shared__ SeedLoopShared S;
+    const int img = blockIdx.x;
+    const int K = g.K;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    GrowLDS &L = Ls[wave];
+    if (lane == 0) {
+        L.status = 0;
+        L.log_n = 0;
+#ifdef PP_STAMPS
+        for (int q = 0; q < 8; q++) L.fst[q] = 0;
+#endif
+    }
+    if (threadIdx.x < kSpecCache) {
+        S.cache_seed[threadIdx.x] = -1;
+        S.cache_ready[threadIdx.x] = 0;
+    }
+    if (threadIdx.x == 0) S.done = 0;
+    __syncthreads();
+
+    STAMP_DECL
+    uint8_t *occ_base = g.occ + (int64_t)img * g.occ_cap;
+    OccLog *log = g.log + (int64_t)img * g.log_cap;
+    pp_ann *work = g.work + (int64_t)img * g.ann_cap;
+    pp_ann *cache = g.spec + (int64_t)img * kSpecCache;
+    const float red = (float)g.cfg.occupancy_reduction;
+    const OccGrid occ = occ_grid(occ_base, K, (int)((double)g.hh / g.cfg.occupancy_reduction),
+                                 (int)((double)g.ww / g.cfg.occupancy_reduction));
+    const int n_seeds = min(g.seed_counts[img], g.seed_cap);
+    const pp_seed *seeds = g.seeds + (int64_t)img * g.seed_cap;
+
+    // committer state (wave 0)
+    int n_anns = 0, s = 0;
+    uint32_t unset_mask = 0;
+#ifdef PP_STAMPS
+    int n_rounds = 0, n_hits = 0;
+#endif
+
+    // append one finished annotation and mark_occupied (cifcaf.py:87-93): wave 0 only
+    auto commit = [&](const pp_ann *src) {
+        copy_ann(&work[n_anns], src);
+        n_anns++;
+        for (int j = 0; j < K; j++) unset_mask |= (src->data[j][2] > 0.0f) ? 0u : (1u << j);
+        occ_mark(g, L, log, occ, src->data, src->joint_scales, K,
+                 [&](int j) { return src->data[j][2] != 0.0f; });
+    };
+
+    for (;;) {
+        if (wave == 0) {
+            for (;;) {
+                // the next free seed (cifcaf.py:100-104): 64 occupancy tests per step
+                int t = -1;
+                while (s < n_seeds) {
+                    const int idx = s + lane;
+                    bool is_free = false;
+                    if (idx < n_seeds) {
+                        const pp_seed c = seeds[idx];
+                        is_free = !occ_get(occ, c.field, c.x, c.y, red);
+                    }
+                    const uint64_t m = __ballot(is_free);
+                    if (m == 0) {
+                        s += 64;
+                        continue;
+                    }
+                    t = s + __ffsll((unsigned long long)m) - 1;
+                    break;
+                }
+                STAMP(0);
+                if (t < 0 || n_anns >= g.ann_cap) {
+                    if (lane == 0) {
+                        if (t >= 0) L.status |= PP_ST_ANN_OVERFLOW;
+                        S.done = 1;
+                    }
+                    break;
+                }
+                const int cs = lane < kSpecCache ? S.cache_seed[lane] : -1;
+                const uint64_t hit = __ballot(lane < kSpecCache && cs == t);
+                if (hit) {  // a helper grew it already
+                    const int slot = __ffsll((unsigned long long)hit) - 1;
+                    commit(&cache[slot]);
+                    s = t + 1;
+#ifdef PP_STAMPS
+                    n_hits++;
+#endif
+                    STAMP(4);
+                    continue;
+                }
+                // plan a round: t on wave 0, far-away free seeds on the helpers
+                const pp_seed st = seeds[t];
+                int nsp = 0;
+                const int scan_end = min(n_seeds, t + 1 + kSpecScan);
+                for (int base = t + 1; base < scan_end && nsp < kSeedWaves - 1; base += 64) {
+                    const int idx = base + lane;
+                    bool ok = idx < scan_end;
+                    pp_seed c{};
+                    if (ok) {
+                        c = seeds[idx];
+                        ok = spec_far(g.spec_far, c.x, c.y, c.s, st.x, st.y, st.s) &&
+                             !occ_get(occ, c.field, c.x, c.y, red);
+                    }
+                    // live cache entries (uniform loop): skip seeds they hold or that their
+                    // annotation's occupancy boxes will cover once committed
+                    const int cxi = (int)clip_ref(c.x / red, 0.0f, (float)(occ.w - 1));
+                    const int cyi = (int)clip_ref(c.y / red, 0.0f, (float)(occ.h - 1));
+                    for (int q = 0; q < kSpecCache; q++) {
+                        const int sq = S.cache_seed[q];
+                        if (sq <= t) continue;
+                        if (sq == idx) ok = false;
+                        if (!ok || !S.cache_ready[q]) continue;  // this round's picks: below
+                        const float4 jq = S.cache_j[q][c.field];
+                        int box[4];
+                        if (jq.z != 0.0f && occ_box(g, occ, c.field, jq.x, jq.y, jq.w, box) &&
+                            cxi >= box[0] && cxi < box[1] && cyi >= box[2] && cyi < box[3])
+                            ok = false;
+                    }
+                    uint64_t m = __ballot(ok);
+                    while (m && nsp < kSeedWaves - 1) {
+                        const int l = __ffsll((unsigned long long)m) - 1;
+                        m &= m - 1;
+                        const float cx = rl_f(c.x, l), cy = rl_f(c.y, l), csc = rl_f(c.s, l);
+                        bool far = true;
+                        for (int r = 0; r < nsp; r++) {
+                            const int q = S.task_slot[1 + r];
+                            far = far && spec_far(g.spec_far, cx, cy, csc, S.cache_x[q],
+                                                  S.cache_y[q], S.cache_s[q]);
+                        }
+                        if (!far) continue;
+                        const int cq = lane < kSpecCache ? S.cache_seed[lane] : 0;
+                        const uint64_t freeq = __ballot(lane < kSpecCache && cq < t);
+                        if (!freeq) {
+                            m = 0;
+                            break;
+                        }
+                        const int q = __ffsll((unsigned long long)freeq) - 1;
+                        if (lane == 0) {
+                            S.task[1 + nsp] = base + l;
+                            S.task_slot[1 + nsp] = q;
+                            S.cache_seed[q] = base + l;
+                            S.cache_x[q] = cx;
+                            S.cache_y[q] = cy;
+                            S.cache_s[q] = csc;
+                            S.cache_ready[q] = 0;
+                        }
+                        wave_sync();
+                        nsp++;
+                    }
+                }
+                if (lane == 0) {
+                    S.task[0] = t;
+                    for (int r = 1 + nsp; r < kSeedWaves; r++) S.task[r] = -1;
+                }
+#ifdef PP_STAMPS
+                n_rounds++;
+#endif
+                STAMP(1);
+                break;
+            }
+        }
+        __syncthreads();
+        if (S.done) break;
+        const int my = S.task[wave];
+        if (my >= 0) {
+            ann_from_seed(L, seeds[my], K, img);
+            grow(g, L, img, 0, true);
+            if (wave > 0) {
+                const int q = S.task_slot[wave];
+                copy_ann(&cache[q], &L.a);
+                if (lane < kKP)
+                    S.cache_j[q][lane] = make_float4(L.a.data[lane][0], L.a.data[lane][1],
+                                                     L.a.data[lane][2], L.a.joint_scales[lane]);
+                if (lane == 0) S.cache_ready[q] = 1;
+            }
+        }
+        __syncthreads();
+        STAMP(2);
+        if (wave == 0) {
+            commit(&L.a);
+            s = S.task[0] + 1;
+            STAMP(3);
+        }
+    }
+    if (wave == 0) {
+        occ_clear(g, L, log, occ);
+        STAMP(5);
+#ifdef PP_STAMPS
+        st_acc[6] = n_rounds;
+        st_acc[7] = n_hits;
+#endif
+        STAMP_FLUSH(1);
+        if (lane == 0) {
+            int st = 0;
+            for (int w = 0; w < kSeedWaves; w++) st |= Ls[w].status;
+            g.n_work[img] = n_anns;
+            g.need_complete[img] = g.cfg.force_complete ? (int)unset_mask : 0;
+            g.status[img] = st;
         }
     }
 }
@@ -1081,7 +1357,7 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
         for (int q = 0; q < 8; q++) L.fst[q] = 0;
 #endif
     }
-    __syncthreads();
+    wave_sync();
 
     STAMP_DECL
     uint8_t *occ_base = g.occ + (int64_t)img * g.occ_cap;
@@ -1089,79 +1365,6 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
     pp_ann *work = g.work + (int64_t)img * g.ann_cap;
     const float red = (float)g.cfg.occupancy_reduction;
 
-    if (PHASE == 1) {
-        // ---- seed loop (cifcaf.py:84-108) ----
-        // The occupancy grid only changes when an annotation is created, so the occupancy
-        // test of the next 64 seeds runs in parallel (one lane each) and the first free seed
-        // starts the next annotation; the occupied ones before it are skipped exactly as the
-        // sequential loop skips them.
-        const OccGrid occ = occ_grid(occ_base, K, (int)((double)g.hh / g.cfg.occupancy_reduction),
-                                     (int)((double)g.ww / g.cfg.occupancy_reduction));
-        const int n_seeds = min(g.seed_counts[img], g.seed_cap);
-        const pp_seed *seeds = g.seeds + (int64_t)img * g.seed_cap;
-        int n_anns = 0;
-        uint32_t unset_mask = 0;
-        int s = 0;
-        while (s < n_seeds) {
-            const int idx = s + lane;
-            bool is_free = false;
-            if (idx < n_seeds) {
-                const pp_seed c = seeds[idx];
-                is_free = !occ_get(occ, c.field, c.x, c.y, red);
-            }
-            const uint64_t m = __ballot(is_free);
-            STAMP(0);
-            if (m == 0) {
-                s += 64;
-                continue;
-            }
-            const int si = s + __ffsll((unsigned long long)m) - 1;
-            s = si + 1;
-            const pp_seed sd = seeds[si];
-            if (n_anns >= g.ann_cap) {
-                L.status |= PP_ST_ANN_OVERFLOW;
-                break;
-            }
-            // Annotation(keypoints, out_skeleton).add(f, (x, y, v)); joint_scales[f] = s
-            {
-                uint32_t *z = reinterpret_cast<uint32_t *>(&L.a);
-                for (int t = lane; t < (int)(sizeof(pp_ann) / 4); t += 64) z[t] = 0u;
-                __syncthreads();
-            }
-            if (lane == 0) {
-                L.a.n_keypoints = K;
-                L.a.image = img;
-                L.a.data[sd.field][0] = sd.x;
-                L.a.data[sd.field][1] = sd.y;
-                L.a.data[sd.field][2] = sd.v;
-                L.a.joint_scales[sd.field] = sd.s;
-            }
-            __syncthreads();
-            STAMP(1);
-            grow(g, L, img, 0, true);
-            __syncthreads();
-            STAMP(2);
-            copy_ann(&work[n_anns], &L.a);
-            n_anns++;
-            STAMP(3);
-            // mark_occupied (cifcaf.py:87-93): every joint with v != 0, in one pass
-            for (int j = 0; j < K; j++)
-                unset_mask |= (L.a.data[j][2] > 0.0f) ? 0u : (1u << j);
-            occ_mark(g, L, log, occ, L.a.data, L.a.joint_scales, K,
-                     [&](int j) { return L.a.data[j][2] != 0.0f; });
-            STAMP(4);
-        }
-        occ_clear(g, L, log, occ);
-        __syncthreads();
-        STAMP(5);
-        STAMP_FLUSH(1);
-        if (lane == 0) {
-            g.n_work[img] = n_anns;
-            g.need_complete[img] = g.cfg.force_complete ? (int)unset_mask : 0;
-            g.status[img] = L.status;
-        }
-        return;
-    }
     const int n_anns = g.n_work[img];
     STAMP(0);
 
@@ -1177,17 +1380,17 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
             for (int j = 0; j < K; j++) has0 = has0 || work[i].data[j][2] == 0.0f;
             if (!has0) continue;
             copy_ann(&L.a, &work[i]);
-            bool unfilled[kKP];
-            for (int j = 0; j < K; j++) unfilled[j] = L.a.data[j][2] == 0.0f;
+            uint32_t unfilled = 0;
+            for (int j = 0; j < K; j++) unfilled |= (L.a.data[j][2] == 0.0f) ? (1u << j) : 0u;
             grow(g, L, img, 1, false);
             bool any0 = false;
             for (int j = 0; j < K; j++) {
                 float &v = L.a.data[j][2];
-                if (unfilled[j] && v > 0.0f) v = (0.001f < v) ? 0.001f : v;  // np.minimum
+                if (((unfilled >> j) & 1u) && v > 0.0f) v = (0.001f < v) ? 0.001f : v;  // np.minimum
                 any0 = any0 || v == 0.0f;
             }
             if (any0) flood_fill(g, L);
-            __syncthreads();
+            wave_sync();
             copy_ann(&work[i], &L.a);
         }
         STAMP(1);
@@ -1216,7 +1419,7 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
                 a.data[lane][1] = 0.0f;
                 a.data[lane][2] = 0.0f;
             }
-            __syncthreads();
+            wave_sync();
             const double sc = ann_score(L, a.data, K);
             if (sc >= it) {
                 float ax = a.data[0][0], ay = a.data[0][1];
@@ -1233,7 +1436,7 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
                 m++;
             }
         }
-        __syncthreads();
+        wave_sync();
         STAMP(2);
         n_out = 0;
         if (m > 0) {
@@ -1256,7 +1459,7 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
                     if (lane < K && a.data[lane][2] != 0.0f)
                         occd = occ_get(no, lane, a.data[lane][0], a.data[lane][1], red);
                     const uint64_t om = __ballot(occd);
-                    __syncthreads();
+                    wave_sync();
                     if (occd) a.data[lane][2] = a.data[lane][2] * g.cfg.nms_suppression;
                     occ_mark(g, L, log, no, a.data, a.joint_scales, K, [&](int j) {
                         return !((om >> j) & 1ull) && a.data[j][2] != 0.0f;
@@ -1274,7 +1477,7 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
                         a.data[lane][1] = 0.0f;
                         a.data[lane][2] = 0.0f;
                     }
-                    __syncthreads();
+                    wave_sync();
                     const double sc = ann_score(L, a.data, K);
                     if (sc >= it) {
                         if (lane == 0) {
@@ -1284,7 +1487,7 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
                         m2++;
                     }
                 }
-                __syncthreads();
+                wave_sync();
                 STAMP(6);
                 int np2 = 1;
                 while (np2 < m2) np2 <<= 1;
@@ -1304,7 +1507,7 @@ __global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
             if (lane == 0) out[i].score = sc;
         }
     }
-    __syncthreads();
+    wave_sync();
     STAMP(8);
     STAMP_FLUSH(3);
     if (lane == 0) {
@@ -1339,7 +1542,7 @@ struct DecodeLayout {
     float inv_e;
     int64_t occ_cap;
     size_t off_cifhr, off_cifhr_ws, off_seeds, off_seed_counts, off_seed_ws, off_cols[2],
-        off_offs[2], off_n_work, off_need, off_occ, off_log, off_work, off_nms_score,
+        off_offs[2], off_n_work, off_need, off_occ, off_log, off_work, off_spec, off_nms_score,
         off_nms_idx, total;
     size_t cifhr_ws_bytes;
 };
@@ -1375,7 +1578,7 @@ static DecodeLayout make_layout(int n_img, int K, int C, int H, int W, const pp_
     caf_bucket_grid(H, W, cfg->stride, &d.bw, &d.bh, &d.nb, &d.inv_e);
     for (int t = 0; t < 2; t++) {
         const bool used = t == 0 || cfg->force_complete;
-        d.off_cols[t] = take(used ? n * C * 2 * 10 * d.hw * sizeof(float) : 0);
+        d.off_cols[t] = take(used ? n * C * 2 * kColRows * d.hw * sizeof(float) : 0);
         d.off_offs[t] = take(used ? n * C * 2 * (d.nb + 1) * sizeof(int) : 0);
     }
     d.off_n_work = take(n * sizeof(int));
@@ -1383,6 +1586,7 @@ static DecodeLayout make_layout(int n_img, int K, int C, int H, int W, const pp_
     d.off_occ = take(n * d.occ_cap);
     d.off_log = take(n * d.log_cap * sizeof(OccLog));
     d.off_work = take(n * ann_cap * sizeof(pp_ann));
+    d.off_spec = take(n * kSpecCache * sizeof(pp_ann));
     d.off_nms_score = take(n * ann_cap * sizeof(double));
     d.off_nms_idx = take(n * (2 * ann_cap + d.ann_np) * sizeof(int));
     d.total = o;
@@ -1508,6 +1712,8 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
         g.log = (OccLog *)(ws + d.off_log);
         g.log_cap = d.log_cap;
         g.work = (pp_ann *)(ws + d.off_work);
+        g.spec = (pp_ann *)(ws + d.off_spec);
+        g.spec_far = kSpecFar;
         g.nms_score = (double *)(ws + d.off_nms_score);
         g.nms_idx = (int *)(ws + d.off_nms_idx);
         g.ann_np = d.ann_np;
@@ -1527,7 +1733,7 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
         g.out = d_anns;
         g.counts = d_counts;
         g.status = d_status;
-        hipLaunchKernelGGL(grow_kernel<1>, dim3(n_img), dim3(64), 0, s, g);
+        hipLaunchKernelGGL(seed_loop_kernel, dim3(n_img), dim3(64 * kSeedWaves), 0, s, g);
         rc = check_launch("pp_decode_batch(seed loop)");
         if (rc) return rc;
         if (cfg->force_complete) {

@@ -90,4 +90,8 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nblocks) {
     return (b & 7) * per + (b >> 3);
 }
 
+// rows of one column of the decoder's bucketed CAF sets (caf_bucketed_kernel): score,
+// source x, y, target x, y, target scale, row-major index (as float bits)
+constexpr int kColRows = 7;
+
 }  // namespace pp

@@ -183,10 +183,15 @@ __device__ __forceinline__ void fold_pixel(float &acc, float &acc2, bool in, flo
 
 template <int MODE, bool ZERO_INIT>
 __global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
-    __shared__ int4 s_box[kCand];
-    __shared__ float4 s_par[kCand];
+    // candidates (gather / fold) and the output staging tile (store) are live in disjoint
+    // phases: one LDS buffer, ~18 KB, so 8 workgroups fit a CU while the tiles stream out
+    constexpr int kCandBytes = kCand * (int)(sizeof(int4) + sizeof(float4));
+    constexpr int kOutBytes = ZERO_INIT ? kTile * kOutPad * (int)sizeof(float) : 0;
+    __shared__ __attribute__((aligned(16))) char s_mem[kCandBytes > kOutBytes ? kCandBytes : kOutBytes];
     __shared__ int s_tmp[4];
-    __shared__ __attribute__((aligned(16))) float s_out[ZERO_INIT ? kTile * kOutPad : 4];
+    int4 *s_box = reinterpret_cast<int4 *>(s_mem);
+    float4 *s_par = reinterpret_cast<float4 *>(s_mem + kCand * sizeof(int4));
+    float *s_out = reinterpret_cast<float *>(s_mem);
 
     const int64_t wid = xcd_remap(blockIdx.x, gridDim.x);
     if (wid >= a.n_work) return;
@@ -284,9 +289,11 @@ __global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
             const int row = q >> 4, c4 = (q & 15) * 4;
             const int gy = ty0 + row, gx = tx0 + c4;
             if (gy < a.h && gx < a.pitch) {
-                float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                if (any) v = *reinterpret_cast<const float4 *>(&s_out[row * kOutPad + c4]);
-                *reinterpret_cast<float4 *>(&out[(int64_t)gy * a.pitch + gx]) = v;
+                typedef float v4f __attribute__((ext_vector_type(4)));
+                v4f v = {0.0f, 0.0f, 0.0f, 0.0f};
+                if (any) v = *reinterpret_cast<const v4f *>(&s_out[row * kOutPad + c4]);
+                // written once, read back only by sparse lookups: streaming (nt) store
+                __builtin_nontemporal_store(v, reinterpret_cast<v4f *>(&out[(int64_t)gy * a.pitch + gx]));
             }
         }
     } else {

@@ -310,7 +310,7 @@ struct CafBArgs {
     float stride, cif_floor, one_minus_floor, th;
     int bw, bh, nb;     // bucket grid and bucket count (bw * bh + 1)
     float inv_e;        // 1 / bucket edge (a power of two: exact)
-    float *cols;        // (n_img, C, 2, 10, H*W): dir 0 backward, 1 forward
+    float *cols;        // (n_img, C, 2, kColRows, H*W): dir 0 backward, 1 forward
     int *offs;          // (n_img, C, 2, nb + 1)
     // (n_img) or NULL: bitmask of the joints force-complete may still set.  Completion
     // only evaluates connections INTO unset joints (cifcaf.py:253, 272), so a direction
@@ -365,7 +365,8 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
         nine[0] = p[cell];
         if (!(nine[0] > a.th)) return;  // mask = nine[0] > score_th
 #pragma unroll
-        for (int r = 1; r < 9; r++) nine[r] = p[r * hw + cell] * a.stride;
+        for (int r = 1; r < 9; r++)  // b1, b2 (rows 3, 7) are never read by the decoder
+            nine[r] = (r == 3 || r == 7) ? 0.0f : p[r * hw + cell] * a.stride;
         const float score = nine[0];
         sb = score;
         sf = score;
@@ -421,8 +422,8 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
     __syncthreads();
 
     // pass 2: scatter into buckets, remembering each column's row-major index
-    float *bwd = a.cols + (fld * 2 + 0) * 10 * (int64_t)hw;
-    float *fwd = a.cols + (fld * 2 + 1) * 10 * (int64_t)hw;
+    float *bwd = a.cols + (fld * 2 + 0) * kColRows * (int64_t)hw;
+    float *fwd = a.cols + (fld * 2 + 1) * kColRows * (int64_t)hw;
     int run_b = 0, run_f = 0;
     for (int base = 0; base < hw; base += 256) {
         float nine[9], sb, sf;
@@ -431,25 +432,28 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
         int tot_b, tot_f;
         const int ob = run_b + block_compact<4>(kb, s_tmp, tot_b);
         const int of = run_f + block_compact<4>(kf, s_tmp, tot_f);
+        // the kColRows rows the grow kernel reads: score, source x, y, target x, y, target
+        // scale, index.  Backward sets are the reference's rows (0, 5, 6, 7, 8, 1, 2, 3, 4)
+        // with row 0 = scores_b, so their source is (x2, y2) and their target (x1, y1, s1).
         if (kb) {
             const int c = atomicAdd(&s_cnt[0][caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e)], 1);
-            bwd[c] = sb;  // rows (0, 5, 6, 7, 8, 1, 2, 3, 4), row 0 = scores_b
+            bwd[c] = sb;
             bwd[1 * hw + c] = nine[5];
             bwd[2 * hw + c] = nine[6];
-            bwd[3 * hw + c] = nine[7];
-            bwd[4 * hw + c] = nine[8];
-            bwd[5 * hw + c] = nine[1];
-            bwd[6 * hw + c] = nine[2];
-            bwd[7 * hw + c] = nine[3];
-            bwd[8 * hw + c] = nine[4];
-            bwd[9 * hw + c] = __int_as_float(ob);
+            bwd[3 * hw + c] = nine[1];
+            bwd[4 * hw + c] = nine[2];
+            bwd[5 * hw + c] = nine[4];
+            bwd[6 * hw + c] = __int_as_float(ob);
         }
         if (kf) {
             const int c = atomicAdd(&s_cnt[1][caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e)], 1);
             fwd[c] = sf;
-#pragma unroll
-            for (int r = 1; r < 9; r++) fwd[r * hw + c] = nine[r];
-            fwd[9 * hw + c] = __int_as_float(of);
+            fwd[1 * hw + c] = nine[1];
+            fwd[2 * hw + c] = nine[2];
+            fwd[3 * hw + c] = nine[5];
+            fwd[4 * hw + c] = nine[6];
+            fwd[5 * hw + c] = nine[8];
+            fwd[6 * hw + c] = __int_as_float(of);
         }
         run_b += tot_b;
         run_f += tot_f;

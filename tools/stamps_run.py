@@ -13,7 +13,8 @@ from openpifpaf_amd import constants, synthetic  # noqa: E402
 from openpifpaf_amd._abi import EVAL_CONFIG, make_config  # noqa: E402
 from openpifpaf_amd.engine import DecodeEngine  # noqa: E402
 
-P1 = ['seed_check', 'ann_init', 'grow', 'copy_ann', 'mark_occ', 'occ_clear']
+P1 = ['seed_scan', 'plan', 'round_grow', 'commit+mark', 'cache_commit', 'occ_clear']
+# phase 1 slots 6 / 7: rounds (grows on wave 0) and annotations taken from the cache
 P2 = ['load', 'complete']  # summed over the image's kCompleteWays workgroups
 P3 = ['load', '-', 'nms_filter', 'nms_sort', 'nms_occ', 'nms_clear', 'nms_refilter',
       'nms_sort2', 'output']
@@ -32,11 +33,13 @@ for kind, n, h in (('planted', 256, 80), ('uniform', 32, 80)):
     st = np.fromfile(out, dtype=np.uint64).reshape(-1, n, 3, 12)[-1].astype(np.float64)
     print('== {} n={} (mean shader cycles per image)'.format(kind, n))
     for ph, names in ((0, P1), (1, P2), (2, P3)):
-        tot = st[:, ph, :len(names)].sum(axis=1).mean()
+        tot = st[:, ph, :min(len(names), 6 if ph == 0 else 8)].sum(axis=1).mean()
         print('  phase {} total {:.3e}'.format(ph + 1, tot))
         for i, name in enumerate(names):
             m = st[:, ph, i].mean()
             print('    {:14s} {:12.0f}  {:5.1f}%'.format(name, m, 100 * m / max(tot, 1)))
+        if ph == 0:
+            print('    rounds {:.1f}  cache hits {:.1f}'.format(st[:, 0, 6].mean(), st[:, 0, 7].mean()))
         for i, name in ((8, 'n connection'), (9, 'in-grow pop'), (10, 'in-grow connection'),
                         (11, 'in-grow add')):
             print('    {:14s} {:12.0f}'.format(name, st[:, ph, i].mean()))
