@@ -86,6 +86,13 @@ struct GrowArgs {
     const float *cols[2];     // bucketed column sets (n_img, C, 2, kColRows, H*W): set A at
                               // caf_threshold, set B at complete_caf_threshold
     const int *offs[2];       // bucket boundaries (n_img, C, 2, nb + 1)
+    // set B (force-complete, complete_caf_threshold) holds only cell indices (n_img, C, 2,
+    // H*W); its queries read the raw CAF and rescore with CifHr (consider_raw)
+    const float *caf;         // (n_img, C, 9, H, W) input
+    const float *hr;          // (n_img, K, hh, hr_pitch) CifHr
+    int64_t hr_pitch;
+    float stride_f, cif_floor, one_minus_floor, th_b;
+    uint8_t caf_j1[PP_MAX_EDGES], caf_j2[PP_MAX_EDGES];  // 0-based joints of each CAF
     int bw, bh, nb;           // bucket grid (see caf_bucketed_kernel)
     float inv_e;
     int K, C, H, W, hh, ww;
@@ -368,6 +375,38 @@ __device__ __forceinline__ void consider(const float *__restrict__ cf, int64_t h
     top2_insert(t, cand_key<MAXM>(score, o), tx, ty, tc);
 }
 
+// a set-B column: cell index -> raw CAF values (caf_scored.py:58-81 for this one column:
+// rows * stride, CifHr rescoring at the target, the second threshold), then as consider
+struct RawSet {
+    const int *idx;      // bucketed cell indices
+    const float *caf9;   // the field's 9 raw rows
+    const float *hrt;    // CifHr plane of the direction's target joint (rescore), or NULL
+    int src, tgt, tsc;   // raw rows of source x, target x, target scale (y = x + 1)
+};
+
+template <bool MAXM>
+__device__ __forceinline__ void consider_raw(const GrowArgs &g, const RawSet &r, int64_t hw,
+                                             const ColQuery &q, int k, Top2 &t, int &m) {
+    const int cell = r.idx[k];
+    const float c = r.caf9[cell];
+    const float c1 = r.caf9[r.src * hw + cell] * g.stride_f;
+    const float c2 = r.caf9[(r.src + 1) * hw + cell] * g.stride_f;
+    const float tx = r.caf9[r.tgt * hw + cell] * g.stride_f;
+    const float ty = r.caf9[(r.tgt + 1) * hw + cell] * g.stride_f;
+    const float tc = r.caf9[r.tsc * hw + cell] * g.stride_f;
+    if (c1 < q.lo_x || c1 > q.hi_x || c2 < q.lo_y || c2 > q.hi_y) return;
+    float c0 = c;
+    if (r.hrt)
+        c0 = c * (g.cif_floor + g.one_minus_floor * hr_lookup(r.hrt, g.hh, g.ww, g.hr_pitch, tx, ty, 0.0f));
+    if (!(c0 > g.th_b)) return;
+    const float dx = q.x - c1, dy = q.y - c2;
+    const float dd = sqrtf(dx * dx + dy * dy);
+    const float qq = (-0.5f * (dd * dd)) / q.sigma2;
+    const float score = (float)exp((double)qq) * c0;
+    m++;
+    top2_insert(t, cand_key<MAXM>(score, cell), tx, ty, tc);
+}
+
 // _target_with_blend / _target_with_maxscore (cifcaf.py:147-192) on the merged top-2
 template <bool MAXM>
 __device__ void finish_connection(const Top2 &t, int m, float out[4]) {
@@ -441,8 +480,8 @@ __device__ uint64_t *g_gc_stamps;  // diagnostic: [img][4] section sums of grow_
 
 // bucketed column set (caf_bucketed_kernel): visit only the buckets the 2*scale box
 // overlaps (+ the NaN-source bucket); segments flattened over the 64 lanes
-template <bool MAXM>
-__device__ void grow_connection(const GrowArgs &g, const float *__restrict__ cf,
+template <bool MAXM, bool RAW>
+__device__ void grow_connection(const GrowArgs &g, const float *__restrict__ cf, const RawSet &raw,
                                 const int *__restrict__ off, float x, float y, float xy_scale,
                                 float out[4]) {
     const int lane = threadIdx.x & 63;
@@ -494,7 +533,12 @@ __device__ void grow_connection(const GrowArgs &g, const float *__restrict__ cf,
                 if (tt >= run && tt < run + l) k = rl_i(st, rr) + (tt - run);
                 run += l;
             }
-            if (k >= 0) consider<MAXM, true>(cf, hw, q, k, t, m);
+            if (k >= 0) {
+                if (RAW)
+                    consider_raw<MAXM>(g, raw, hw, q, k, t, m);
+                else
+                    consider<MAXM, true>(cf, hw, q, k, t, m);
+            }
         }
         GSTAMP(1);
     }
@@ -506,7 +550,22 @@ __device__ __forceinline__ float max0(float v) { return (v > 0.0f) ? v : 0.0f; }
 
 __device__ __forceinline__ const float *col_set(const GrowArgs &g, int set, int img, int caf_i,
                                                 int dir) {
-    return g.cols[set] + (((int64_t)img * g.C + caf_i) * 2 + dir) * kColRows * g.hw;
+    return g.cols[set] + (((int64_t)img * g.C + caf_i) * 2 + dir) * (set ? 1 : kColRows) * g.hw;
+}
+
+// set B of (image, CAF, direction): dir 1 forward (x1, y1) -> (x2, y2, s2), rescored at
+// joint j2; dir 0 backward (x2, y2) -> (x1, y1, s1), rescored at j1 (caf_scored.py:58-81)
+__device__ __forceinline__ RawSet raw_set(const GrowArgs &g, int img, int caf_i, int dir) {
+    RawSet r;
+    r.idx = reinterpret_cast<const int *>(col_set(g, 1, img, caf_i, dir));
+    r.caf9 = g.caf + ((int64_t)img * g.C + caf_i) * 9 * g.hw;
+    const int tj = dir ? g.caf_j2[caf_i] : g.caf_j1[caf_i];
+    r.hrt = (g.cif_floor < 1.0f && tj < g.K) ? g.hr + ((int64_t)img * g.K + tj) * g.hh * g.hr_pitch
+                                              : nullptr;
+    r.src = dir ? 1 : 5;
+    r.tgt = dir ? 5 : 1;
+    r.tsc = dir ? 8 : 4;
+    return r;
 }
 
 __device__ __forceinline__ const int *col_offs(const GrowArgs &g, int set, int img, int caf_i,
@@ -521,13 +580,26 @@ __device__ void connection_value(const GrowArgs &g, int img, int set, int caf_i,
     const int df = fwd ? 1 : 0, db = fwd ? 0 : 1;
     const float xy_scale_s = max0(js);
     const bool maxm = g.cfg.connection_method == 1;
+    // one query along direction `dir` from (qx, qy, qs)
+    auto query = [&](int dir, float qx, float qy, float qs, float r[4]) {
+        const float *cf = col_set(g, set, img, caf_i, dir);
+        const int *off = col_offs(g, set, img, caf_i, dir);
+        if (set) {
+            const RawSet raw = raw_set(g, img, caf_i, dir);
+            if (maxm)
+                grow_connection<true, true>(g, cf, raw, off, qx, qy, qs, r);
+            else
+                grow_connection<false, true>(g, cf, raw, off, qx, qy, qs, r);
+        } else {
+            const RawSet none{};
+            if (maxm)
+                grow_connection<true, false>(g, cf, none, off, qx, qy, qs, r);
+            else
+                grow_connection<false, false>(g, cf, none, off, qx, qy, qs, r);
+        }
+    };
     float nx[4];
-    if (maxm)
-        grow_connection<true>(g, col_set(g, set, img, caf_i, df), col_offs(g, set, img, caf_i, df),
-                              jx, jy, xy_scale_s, nx);
-    else
-        grow_connection<false>(g, col_set(g, set, img, caf_i, df),
-                               col_offs(g, set, img, caf_i, df), jx, jy, xy_scale_s, nx);
+    query(df, jx, jy, xy_scale_s, nx);
 
     out[0] = out[1] = out[2] = out[3] = 0.0f;
     const float ks = sqrtf(nx[3] * jv);  // geometric mean
@@ -536,12 +608,7 @@ __device__ void connection_value(const GrowArgs &g, int img, int set, int caf_i,
     const float xy_scale_t = max0(nx[2]);
     if (reverse_match) {
         float rv[4];
-        if (maxm)
-            grow_connection<true>(g, col_set(g, set, img, caf_i, db),
-                                  col_offs(g, set, img, caf_i, db), nx[0], nx[1], xy_scale_t, rv);
-        else
-            grow_connection<false>(g, col_set(g, set, img, caf_i, db),
-                                   col_offs(g, set, img, caf_i, db), nx[0], nx[1], xy_scale_t, rv);
+        query(db, nx[0], nx[1], xy_scale_t, rv);
         if (rv[2] == 0.0f) return;  // tests the SCALE (cifcaf.py:212)
         if (fabsf(jx - rv[0]) + fabsf(jy - rv[1]) > xy_scale_s) return;
     }
@@ -1529,7 +1596,7 @@ int launch_seeds(const float *cif, const float *hr, int n_img, int K, int H, int
 size_t seeds_scratch_size(int n_img, int cap);
 int launch_caf_bucketed(const float *caf, const float *hr, int n_img, int K, int C, int H, int W,
                         const int32_t *skeleton, const pp_config *cfg, float th, float *cols,
-                        int *offs, const int *gate, hipStream_t s);
+                        int *offs, const int *gate, bool index_only, hipStream_t s);
 void caf_bucket_grid(int H, int W, int stride, int *bw, int *bh, int *nb, float *inv_e);
 
 static inline size_t align_up(size_t a) { return (a + 255) / 256 * 256; }
@@ -1578,7 +1645,7 @@ static DecodeLayout make_layout(int n_img, int K, int C, int H, int W, const pp_
     caf_bucket_grid(H, W, cfg->stride, &d.bw, &d.bh, &d.nb, &d.inv_e);
     for (int t = 0; t < 2; t++) {
         const bool used = t == 0 || cfg->force_complete;
-        d.off_cols[t] = take(used ? n * C * 2 * kColRows * d.hw * sizeof(float) : 0);
+        d.off_cols[t] = take(used ? n * C * 2 * (t ? 1 : kColRows) * d.hw * sizeof(float) : 0);
         d.off_offs[t] = take(used ? n * C * 2 * (d.nb + 1) * sizeof(int) : 0);
     }
     d.off_n_work = take(n * sizeof(int));
@@ -1651,7 +1718,7 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
     }
     if (stages & 4u) {  // CafScored at caf_threshold; the force-complete set is lazy
         rc = launch_caf_bucketed(d_caf, hr, n_img, K, C, H, W, skeleton, cfg, cfg->caf_threshold,
-                                 cols[0], offs[0], nullptr, s);
+                                 cols[0], offs[0], nullptr, false, s);
         if (rc) return rc;
     }
     if (stages & 8u) {
@@ -1675,6 +1742,17 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
         g.ww = d.ww;
         g.hw = d.hw;
         g.cfg = *cfg;
+        g.caf = d_caf;
+        g.hr = hr;
+        g.hr_pitch = d.pitch;
+        g.stride_f = (float)cfg->stride;
+        g.cif_floor = cfg->cif_floor;
+        g.one_minus_floor = (float)(1.0 - (double)cfg->cif_floor);  // (1.0 - self.cif_floor)
+        g.th_b = cfg->complete_caf_threshold;
+        for (int ci = 0; ci < C; ci++) {
+            g.caf_j1[ci] = (uint8_t)(skeleton[2 * ci] - 1);
+            g.caf_j2[ci] = (uint8_t)(skeleton[2 * ci + 1] - 1);
+        }
         // by_source (cifcaf.py:62-65): dict insertion order, later duplicate keys
         // overwrite the value in place; flattened into directed-edge slots per start joint
         {
@@ -1740,7 +1818,7 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
             // complete_annotations' CafScored(score_th=0.0001) only where phase 1 left work
             rc = launch_caf_bucketed(d_caf, hr, n_img, K, C, H, W, skeleton, cfg,
                                      cfg->complete_caf_threshold, cols[1], offs[1],
-                                     g.need_complete, s);
+                                     g.need_complete, true, s);
             if (rc) return rc;
         }
         if (cfg->force_complete) {

@@ -119,11 +119,23 @@ __global__ __launch_bounds__(256) void seeds_emit_kernel(SeedArgs a) {
     if (threadIdx.x == 0) a.f_counts[fld] = running;
 }
 
+// Seeds with v > threshold > 0 sort as 64-bit keys, descending: v's bits (positive
+// floats order like integers), then the field, then the INVERTED emission index, so equal
+// (v, field) stay in emission order.  The reference breaks (v, field) ties on x, y, s
+// before emission order (tuple comparison, cif_seeds.py:54); such runs are rare and get
+// re-sorted with the full comparator afterwards.
+constexpr uint32_t kEmitMask = (1u << 27) - 1;
+
+__device__ __forceinline__ uint64_t seed_key(float v, int f, int e) {
+    return ((uint64_t)__float_as_uint(v) << 32) | ((uint32_t)f << 27) | (kEmitMask - (uint32_t)e);
+}
+
+__device__ __forceinline__ int key_emit(uint64_t k) { return (int)(kEmitMask - ((uint32_t)k & kEmitMask)); }
+
 // stage 2: one workgroup per image — concatenate the fields in order and sort
-__global__ __launch_bounds__(256) void seeds_sort_kernel(SeedArgs a) {
-    __shared__ float s_v[kSortLds], s_x[kSortLds], s_y[kSortLds], s_s[kSortLds];
-    __shared__ int s_f[kSortLds];
-    __shared__ uint16_t s_perm[kSortLds];
+__global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
+    __shared__ uint64_t s_key[kSortLds];
+    __shared__ float s_x[kSortLds], s_y[kSortLds], s_s[kSortLds];
     __shared__ int s_off[PP_MAX_KP + 1];
     const int img = blockIdx.x;
     const int hw = a.H * a.W;
@@ -150,25 +162,65 @@ __global__ __launch_bounds__(256) void seeds_sort_kernel(SeedArgs a) {
             const int o = s_off[f], c = s_off[f + 1] - o;
             for (int i = threadIdx.x; i < c; i += blockDim.x) {
                 const int64_t q = (int64_t)f * hw + i;
-                s_v[o + i] = gv[q];
+                s_key[o + i] = seed_key(gv[q], f, o + i);
                 s_x[o + i] = gx[q];
                 s_y[o + i] = gy[q];
                 s_s[o + i] = gs[q];
-                s_f[o + i] = f;
             }
         }
-        for (int i = threadIdx.x; i < np; i += blockDim.x) s_perm[i] = (uint16_t)i;
+        for (int i = n + threadIdx.x; i < np; i += blockDim.x) s_key[i] = 0;  // sorts last
         __syncthreads();
-        SeedKeys keys{s_v, s_x, s_y, s_s, s_f, nullptr, n};
-        bitonic_sort(s_perm, np, keys);
+        for (int k = 2; k <= np; k <<= 1) {  // bitonic network, descending
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = threadIdx.x; i < np; i += blockDim.x) {
+                    const int ixj = i ^ j;
+                    if (ixj > i) {
+                        const uint64_t ka = s_key[i], kb = s_key[ixj];
+                        const bool desc = (i & k) == 0;
+                        if (desc ? ka < kb : ka > kb) {
+                            s_key[i] = kb;
+                            s_key[ixj] = ka;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        // runs of equal (v, field): insertion sort by (x, y, s) descending, then emission
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            const int k = s_perm[i];
+            const uint64_t ki = s_key[i] >> 27;
+            const bool tie_prev = i > 0 && (s_key[i - 1] >> 27) == ki;
+            const bool tie_next = i + 1 < n && (s_key[i + 1] >> 27) == ki;
+            if (tie_prev || !tie_next) continue;
+            int end = i + 1;
+            while (end < n && (s_key[end] >> 27) == ki) end++;
+            auto before = [&](uint64_t p, uint64_t q) {  // p must precede q
+                const int ep = key_emit(p), eq = key_emit(q);
+                if (s_x[ep] != s_x[eq]) return s_x[ep] > s_x[eq];
+                if (s_y[ep] != s_y[eq]) return s_y[ep] > s_y[eq];
+                if (s_s[ep] != s_s[eq]) return s_s[ep] > s_s[eq];
+                return ep < eq;
+            };
+            for (int u = i + 1; u < end; u++) {
+                const uint64_t cur = s_key[u];
+                int w = u;
+                while (w > i && before(cur, s_key[w - 1])) {
+                    s_key[w] = s_key[w - 1];
+                    w--;
+                }
+                s_key[w] = cur;
+            }
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const uint64_t k = s_key[i];
+            const int e = key_emit(k);
             pp_seed r;
-            r.v = s_v[k];
-            r.field = s_f[k];
-            r.x = s_x[k];
-            r.y = s_y[k];
-            r.s = s_s[k];
+            r.v = __uint_as_float((uint32_t)(k >> 32));
+            r.field = (int)((k >> 27) & 31u);
+            r.x = s_x[e];
+            r.y = s_y[e];
+            r.s = s_s[e];
             out[i] = r;
         }
     } else {
@@ -301,7 +353,7 @@ __global__ __launch_bounds__(256) void caf_scored_kernel(CafArgs a) {
 // reference's row-major order, which is what ties are broken on; `offs` holds the
 // bucket boundaries (bucket grid bw x bh of e x e px, plus one bucket for NaN sources).
 // ------------------------------------------------------------------------------------
-constexpr int kMaxBuckets = 6400 + 1;
+constexpr int kMaxBuckets = 1600 + 1;
 
 struct CafBArgs {
     const float *caf, *hr;
@@ -326,8 +378,13 @@ __device__ __forceinline__ int caf_bucket(float x, float y, int bw, int bh, floa
     return by * bw + bx;
 }
 
+// INDEX_ONLY (the force-complete set): bucket the cell index of every cell with c > th by
+// its source position and store nothing else.  The rescoring by CifHr and the second
+// threshold (caf_scored.py:63-81) are applied by the query (grow.hip, consider_raw) to the
+// few columns in its box; both filters commute with the bucketing and the tie-break key is
+// the cell index either way.
+template <bool INDEX_ONLY>
 __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
-    __shared__ int s_tmp[4];
     __shared__ int s_cnt[2][kMaxBuckets + 1];
     __shared__ int s_wsum[2][4];
     const int64_t fld = blockIdx.x;  // image * C + caf field
@@ -361,9 +418,21 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
     // one cell of caf_scored.py:42-81 (both directions)
     auto score_cell = [&](int cell, float nine[9], bool &kb, bool &kf, float &sb, float &sf) {
         kb = kf = false;
-        if (cell >= hw) return;
         nine[0] = p[cell];
         if (!(nine[0] > a.th)) return;  // mask = nine[0] > score_th
+        if (INDEX_ONLY) {  // source positions only: forward (x1, y1), backward (x2, y2)
+            if (need_f) {
+                nine[1] = p[1 * hw + cell] * a.stride;
+                nine[2] = p[2 * hw + cell] * a.stride;
+            }
+            if (need_b) {
+                nine[5] = p[5 * hw + cell] * a.stride;
+                nine[6] = p[6 * hw + cell] * a.stride;
+            }
+            kb = need_b;
+            kf = need_f;
+            return;
+        }
 #pragma unroll
         for (int r = 1; r < 9; r++)  // b1, b2 (rows 3, 7) are never read by the decoder
             nine[r] = (r == 3 || r == 7) ? 0.0f : p[r * hw + cell] * a.stride;
@@ -380,11 +449,12 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
         kf = need_f && sf > a.th;
     };
 
-    // pass 1: bucket histograms (backward sources are (x2, y2), forward (x1, y1))
-    for (int base = 0; base < hw; base += 256) {
+    // pass 1: bucket histograms (backward sources are (x2, y2), forward (x1, y1)); no
+    // barrier inside the loop, so the cells' loads overlap freely
+    for (int cell = threadIdx.x; cell < hw; cell += 256) {
         float nine[9], sb, sf;
         bool kb, kf;
-        score_cell(base + threadIdx.x, nine, kb, kf, sb, sf);
+        score_cell(cell, nine, kb, kf, sb, sf);
         if (kb) atomicAdd(&s_cnt[0][caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e)], 1);
         if (kf) atomicAdd(&s_cnt[1][caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e)], 1);
     }
@@ -421,17 +491,25 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
     }
     __syncthreads();
 
-    // pass 2: scatter into buckets, remembering each column's row-major index
-    float *bwd = a.cols + (fld * 2 + 0) * kColRows * (int64_t)hw;
-    float *fwd = a.cols + (fld * 2 + 1) * kColRows * (int64_t)hw;
-    int run_b = 0, run_f = 0;
-    for (int base = 0; base < hw; base += 256) {
+    // pass 2: scatter into buckets.  A column's tie-break key is its cell's row-major index:
+    // it orders the kept columns exactly as their rank in the reference's compacted array
+    // does, and the grow kernel's merge is independent of the order inside a bucket.
+    const int rows = INDEX_ONLY ? 1 : kColRows;
+    float *bwd = a.cols + (fld * 2 + 0) * rows * (int64_t)hw;
+    float *fwd = a.cols + (fld * 2 + 1) * rows * (int64_t)hw;
+    for (int cell = threadIdx.x; cell < hw; cell += 256) {
         float nine[9], sb, sf;
         bool kb, kf;
-        score_cell(base + threadIdx.x, nine, kb, kf, sb, sf);
-        int tot_b, tot_f;
-        const int ob = run_b + block_compact<4>(kb, s_tmp, tot_b);
-        const int of = run_f + block_compact<4>(kf, s_tmp, tot_f);
+        score_cell(cell, nine, kb, kf, sb, sf);
+        if (INDEX_ONLY) {
+            if (kb)
+                reinterpret_cast<int *>(bwd)[atomicAdd(
+                    &s_cnt[0][caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e)], 1)] = cell;
+            if (kf)
+                reinterpret_cast<int *>(fwd)[atomicAdd(
+                    &s_cnt[1][caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e)], 1)] = cell;
+            continue;
+        }
         // the kColRows rows the grow kernel reads: score, source x, y, target x, y, target
         // scale, index.  Backward sets are the reference's rows (0, 5, 6, 7, 8, 1, 2, 3, 4)
         // with row 0 = scores_b, so their source is (x2, y2) and their target (x1, y1, s1).
@@ -443,7 +521,7 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
             bwd[3 * hw + c] = nine[1];
             bwd[4 * hw + c] = nine[2];
             bwd[5 * hw + c] = nine[4];
-            bwd[6 * hw + c] = __int_as_float(ob);
+            bwd[6 * hw + c] = __int_as_float(cell);
         }
         if (kf) {
             const int c = atomicAdd(&s_cnt[1][caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e)], 1);
@@ -453,10 +531,8 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
             fwd[3 * hw + c] = nine[5];
             fwd[4 * hw + c] = nine[6];
             fwd[5 * hw + c] = nine[8];
-            fwd[6 * hw + c] = __int_as_float(of);
+            fwd[6 * hw + c] = __int_as_float(cell);
         }
-        run_b += tot_b;
-        run_f += tot_f;
     }
 }
 
@@ -494,7 +570,7 @@ int launch_seeds(const float *cif, const float *hr, int n_img, int K, int H, int
     w += round_up((int64_t)n_img * K * sizeof(int), 256);
     a.g_perm = (int *)w;
     hipLaunchKernelGGL(seeds_emit_kernel, dim3((unsigned)((int64_t)n_img * K)), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(seeds_sort_kernel, dim3(n_img), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(seeds_sort_kernel, dim3(n_img), dim3(1024), 0, s, a);
     return check_launch("pp_seeds");
 }
 
@@ -540,7 +616,7 @@ int launch_caf_scored(const float *caf, const float *hr, int n_img, int K, int C
     return check_launch("pp_caf_scored");
 }
 
-// bucket geometry for an H x W field: edge e = stride * 2^k px with <= 6400 buckets
+// bucket geometry for an H x W field: edge e = stride * 2^k px with <= 1600 buckets
 void caf_bucket_grid(int H, int W, int stride, int *bw, int *bh, int *nb, float *inv_e) {
     const int hh = (int)hr_dim(H, stride), ww = (int)hr_dim(W, stride);
     int e = stride;
@@ -553,7 +629,7 @@ void caf_bucket_grid(int H, int W, int stride, int *bw, int *bh, int *nb, float 
 
 int launch_caf_bucketed(const float *caf, const float *hr, int n_img, int K, int C, int H, int W,
                         const int32_t *skeleton, const pp_config *cfg, float th, float *cols,
-                        int *offs, const int *gate, hipStream_t s) {
+                        int *offs, const int *gate, bool index_only, hipStream_t s) {
     if (C > kMaxCaf) return fail(PP_ESHAPE, "caf_scored: more than PP_MAX_EDGES CAF fields");
     CafBArgs a{};
     a.caf = caf;
@@ -577,7 +653,12 @@ int launch_caf_bucketed(const float *caf, const float *hr, int n_img, int K, int
         a.j1[i] = skeleton[2 * i] - 1;
         a.j2[i] = skeleton[2 * i + 1] - 1;
     }
-    hipLaunchKernelGGL(caf_bucketed_kernel, dim3((unsigned)((int64_t)n_img * C)), dim3(256), 0, s, a);
+    if (index_only)
+        hipLaunchKernelGGL(caf_bucketed_kernel<true>, dim3((unsigned)((int64_t)n_img * C)),
+                           dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(caf_bucketed_kernel<false>, dim3((unsigned)((int64_t)n_img * C)),
+                           dim3(256), 0, s, a);
     return check_launch("caf_scored(bucketed)");
 }
 

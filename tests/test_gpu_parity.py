@@ -303,6 +303,34 @@ def test_cifhr_batch_bit_exact():
         assert np.array_equal(uh[i], oracle.cifhr(ucif[i], cfg)), i
 
 
+@pytest.mark.parametrize('hw', [12, 20])  # 17*144 seeds sort in LDS, 17*400 globally
+def test_seed_ties(dec, hw):
+    """Saturated CifHr gives equal v within a field: the sort must fall back to the full
+    tuple order (x, y, s descending, then emission order), cif_seeds.py:54."""
+    g = {'mode': np.array('eval'), 'greedy': 0, 'connection_method': np.array('blend')}
+    _configure(dec, g)
+    rng = np.random.default_rng(3)
+    yy, xx = np.mgrid[0:hw, 0:hw].astype(np.float32)
+    cif = np.zeros((17, 5, hw, hw), np.float32)
+    cif[:, 0] = 0.9
+    cif[:, 1] = np.floor(xx / 2) * 2   # duplicate positions -> ties on (x, y)
+    cif[:, 2] = np.floor(yy / 2) * 2
+    cif[:, 3] = 0.5
+    cif[:, 4] = rng.choice(np.array([1.0, 2.0], np.float32), (17, hw, hw))  # ties on s too
+    cif[5, 0, 3:6, 3:6] = 0.35  # a few distinct v
+    caf = np.zeros((19, 9, hw, hw), np.float32)
+    fc = dec.FieldConfig()
+    hr = dec.CifHr(fc).fill([cif, caf]).accumulated
+    assert np.array_equal(hr, oracle.cifhr(cif))
+    seeds = dec.CifSeeds(hr, fc).fill([cif, caf]).get()
+    got = np.array([tuple(float(t) for t in sd) for sd in seeds], np.float32).reshape(-1, 5)
+    ref = oracle.seeds(cif, hr)
+    exp = np.stack([ref['v'], ref['field'].astype(np.float32), ref['x'], ref['y'], ref['s']], 1)
+    assert len(got) == len(exp) > 17 * hw * hw // 2
+    assert np.array_equal(got, exp)
+    assert (np.diff(exp[:, 0]) == 0).sum() > len(exp) // 2  # the case really has ties
+
+
 def test_workspace_left_clean(dec):
     """The occupancy workspace is zero again after a decode (workspace contract)."""
     from openpifpaf_amd import constants, engine, synthetic
@@ -316,6 +344,7 @@ def test_workspace_left_clean(dec):
     import ctypes
     cfg = cc.config()
     zoff = load().pp_decode_workspace_zero_offset(4, 17, 19, 40, 40, ctypes.byref(cfg), b.cap)
-    occ_bytes = b.ws[zoff:zoff + 4 * 17 * (156 + 64) * (156 + 64)]  # H' = 313 -> 156 rows
+    # H' = 313 -> 156 rows; rows padded to 16 bytes: 17 planes of (156 + 64) x 224
+    occ_bytes = b.ws[zoff:zoff + 4 * 17 * (156 + 64) * 224]
     assert int(occ_bytes.sum().item()) == 0
     assert engine.engine() is not None
