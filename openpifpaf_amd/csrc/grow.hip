@@ -111,8 +111,10 @@ struct GrowArgs {
     pp_ann *work;             // working annotations
     pp_ann *spec;             // (n_img, kSpecCache) speculatively grown annotations
     float spec_far;           // seed-loop speculation distance, in joint scales
-    double *nms_score;        // (n_img, ann_cap)
-    int *nms_idx;             // (n_img, 2 * ann_cap + ann_np)
+    double *nms_score;        // (n_img, 2 * ann_cap)
+    int *nms_idx;             // (n_img, 4 * ann_cap + ann_np)
+    float *nms_f;             // (n_img, 2 * ann_cap) per-annotation max x, max y
+    int2 *nms_box;            // (n_img, kNmsWaves, ann_cap) plane box lists beyond LDS
     int ann_np;               // next pow2 >= ann_cap
     int ann_cap;
     uint64_t *stamps;         // diagnostic build: (n_img, 3, 12) cycle sums, else NULL
@@ -130,8 +132,6 @@ struct GrowLDS {
     FFEntry ff[kHeap];
     int mark_pre[kKP + 1];        // occupancy boxes of one annotation: area prefix
     int mark_box[kKP][4];
-    double prod[kKP];             // Annotation.score() terms
-    double score_bc;
     int ff_n;
     int log_n;
     int status;
@@ -1067,51 +1067,28 @@ __device__ void occ_clear(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccG
     wave_sync();
 }
 
-// Annotation.score() (annotation.py:24-28, 60-71) in float64, collective over the wave:
-// lane j finds the rank of v_j in descending order, the rank-ordered products go to LDS
-// and NumPy's pairwise summation (n <= 128 path) adds them in its fixed order.
-__device__ double ann_score(GrowLDS &L, const float (*data)[3], int K) {
-    const int lane = threadIdx.x & 63;
-    const double ws = (double)(3 * min(K, 3) + (K - min(K, 3)));  // np.sum(weights): exact
-    if (lane < K) {
-        const float vj = data[lane][2];
-        int rank = 0;
-        for (int i = 0; i < K; i++) {
-            const float vi = data[i][2];
-            rank += (vi > vj) || (vi == vj && i < lane);
-        }
-        const double w = (rank < 3 ? 3.0 : 1.0) / ws;
-        L.prod[rank] = w * (double)vj;
+// np.sum of K float64 terms in NumPy's pairwise order (n <= 128: eight accumulators over
+// blocks of 8, combined as ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)), then the tail)
+__device__ double pw_sum(const double *a, int K) {
+    if (K < 8) {
+        double res = 0.0;
+        for (int i = 0; i < K; i++) res += a[i];
+        return res;
     }
-    wave_sync();
-    if (lane == 0) {
-        const double *a = L.prod;
-        double res;
-        if (K < 8) {
-            res = 0.0;
-            for (int i = 0; i < K; i++) res += a[i];
-        } else {
-            double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6],
-                   r7 = a[7];
-            int i;
-            for (i = 8; i < K - (K % 8); i += 8) {
-                r0 += a[i];
-                r1 += a[i + 1];
-                r2 += a[i + 2];
-                r3 += a[i + 3];
-                r4 += a[i + 4];
-                r5 += a[i + 5];
-                r6 += a[i + 6];
-                r7 += a[i + 7];
-            }
-            res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-            for (; i < K; i++) res += a[i];
-        }
-        L.score_bc = res;
+    double r0 = a[0], r1 = a[1], r2 = a[2], r3 = a[3], r4 = a[4], r5 = a[5], r6 = a[6], r7 = a[7];
+    int i;
+    for (i = 8; i < K - (K % 8); i += 8) {
+        r0 += a[i];
+        r1 += a[i + 1];
+        r2 += a[i + 2];
+        r3 += a[i + 3];
+        r4 += a[i + 4];
+        r5 += a[i + 5];
+        r6 += a[i + 6];
+        r7 += a[i + 7];
     }
-    wave_sync();
-    const double res = L.score_bc;
-    wave_sync();
+    double res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+    for (; i < K; i++) res += a[i];
     return res;
 }
 
@@ -1410,176 +1387,333 @@ __global__ __launch_bounds__(64 * kSeedWaves) void seed_loop_kernel(GrowArgs g) 
 // ---------------------------------------------------------------------------------------
 // the per-image decode kernel
 // ---------------------------------------------------------------------------------------
-template <int PHASE>
-__global__ __launch_bounds__(64) void grow_kernel(GrowArgs g) {
+// ---- complete_annotations (cifcaf.py:333-351) ----
+// Each annotation is completed from its own joints and the read-only set-B columns, so the
+// annotations of an image are spread over kCompleteWays workgroups.  Ones with every joint
+// set are unchanged by it (their frontier is empty) and are skipped, and images the seed
+// loop did not flag return at once.
+__global__ __launch_bounds__(64) void complete_kernel(GrowArgs g) {
     __shared__ GrowLDS L;
     const int img = blockIdx.x;
     const int K = g.K;
     const int lane = threadIdx.x & 63;
-
     if (lane == 0) {
-        L.status = PHASE == 3 ? g.status[img] : 0;
+        L.status = 0;
         L.log_n = 0;
 #ifdef PP_STAMPS
         for (int q = 0; q < 8; q++) L.fst[q] = 0;
 #endif
     }
     wave_sync();
-
     STAMP_DECL
-    uint8_t *occ_base = g.occ + (int64_t)img * g.occ_cap;
-    OccLog *log = g.log + (int64_t)img * g.log_cap;
     pp_ann *work = g.work + (int64_t)img * g.ann_cap;
-    const float red = (float)g.cfg.occupancy_reduction;
-
     const int n_anns = g.n_work[img];
     STAMP(0);
-
-    if (PHASE == 2) {
-        // ---- complete_annotations (cifcaf.py:333-351) ----
-        // Each annotation is completed from its own joints and the read-only B columns, so
-        // the annotations of an image are spread over kCompleteWays workgroups.  Ones with
-        // every joint set are unchanged by it (their frontier is empty) and are skipped,
-        // and images phase 1 did not flag launch nothing.
-        if (!g.need_complete[img]) return;
-        for (int i = blockIdx.y; i < n_anns; i += gridDim.y) {
-            bool has0 = false;
-            for (int j = 0; j < K; j++) has0 = has0 || work[i].data[j][2] == 0.0f;
-            if (!has0) continue;
-            copy_ann(&L.a, &work[i]);
-            uint32_t unfilled = 0;
-            for (int j = 0; j < K; j++) unfilled |= (L.a.data[j][2] == 0.0f) ? (1u << j) : 0u;
-            grow(g, L, img, 1, false);
-            bool any0 = false;
-            for (int j = 0; j < K; j++) {
-                float &v = L.a.data[j][2];
-                if (((unfilled >> j) & 1u) && v > 0.0f) v = (0.001f < v) ? 0.001f : v;  // np.minimum
-                any0 = any0 || v == 0.0f;
-            }
-            if (any0) flood_fill(g, L);
-            wave_sync();
-            copy_ann(&work[i], &L.a);
+    if (!g.need_complete[img]) return;
+    for (int i = blockIdx.y; i < n_anns; i += gridDim.y) {
+        bool has0 = false;
+        for (int j = 0; j < K; j++) has0 = has0 || work[i].data[j][2] == 0.0f;
+        if (!has0) continue;
+        copy_ann(&L.a, &work[i]);
+        uint32_t unfilled = 0;
+        for (int j = 0; j < K; j++) unfilled |= (L.a.data[j][2] == 0.0f) ? (1u << j) : 0u;
+        grow(g, L, img, 1, false);
+        bool any0 = false;
+        for (int j = 0; j < K; j++) {
+            float &v = L.a.data[j][2];
+            if (((unfilled >> j) & 1u) && v > 0.0f) v = (0.001f < v) ? 0.001f : v;  // np.minimum
+            any0 = any0 || v == 0.0f;
         }
-        STAMP(1);
-        STAMP_FLUSH(2);
-        if (lane == 0 && L.status) atomicOr(&g.status[img], L.status);
+        if (any0) flood_fill(g, L);
+        wave_sync();
+        copy_ann(&work[i], &L.a);
+    }
+    STAMP(1);
+    STAMP_FLUSH(2);
+    if (lane == 0 && L.status) atomicOr(&g.status[img], L.status);
+}
+
+// ---- nms.Keypoints.annotations (nms.py:17-57) + output, one workgroup per image ----
+// The score filters are per annotation: spread over the waves.  The suppression pass
+// (nms.py:34-45) is sequential over the sorted annotations, but each joint lives on its
+// own occupancy plane, so the planes are independent: wave w walks planes w, w + 8, ...
+// and keeps the plane's marked boxes in a list instead of a u8 grid.  A joint is
+// "occupied" iff the number of earlier marked boxes covering its cell is non-zero mod 256
+// (the grid's u8 += 1 wraps), which is exactly what the grid lookup returns.
+constexpr int kNmsWaves = 8;
+constexpr int kNmsBoxLds = 1024;  // boxes per plane kept in LDS (global scratch beyond)
+
+struct ScoreLDS {
+    double prod[kKP];
+    double score_bc;
+#ifdef PP_STAMPS
+    uint64_t fst[8];  // unused here; keeps STAMP_FLUSH uniform
+#endif
+};
+
+// Annotation.score() (annotation.py:24-28, 60-71) in float64, collective over one wave:
+// lane j finds the rank of v_j in descending order, the rank-ordered products go to LDS
+// and lane 0 adds them in NumPy's pairwise order
+__device__ double ann_score_w(ScoreLDS &L, const float (*data)[3], int K) {
+    const int lane = threadIdx.x & 63;
+    const double ws = (double)(3 * min(K, 3) + (K - min(K, 3)));
+    if (lane < K) {
+        const float vj = data[lane][2];
+        int rank = 0;
+        for (int i = 0; i < K; i++) {
+            const float vi = data[i][2];
+            rank += (vi > vj) || (vi == vj && i < lane);
+        }
+        L.prod[rank] = ((rank < 3 ? 3.0 : 1.0) / ws) * (double)vj;
+    }
+    wave_sync();
+    if (lane == 0) L.score_bc = pw_sum(L.prod, K);
+    wave_sync();
+    const double res = L.score_bc;
+    wave_sync();
+    return res;
+}
+
+// the grid cell occ_get reads: 1 = occupied whatever the grid holds (f beyond the planes),
+// 0 = free whatever it holds (empty grid), -1 = look at (xi, yi)
+__device__ __forceinline__ int occ_cell(const OccGrid &o, int f, float x, float y, float red,
+                                        int &xi, int &yi) {
+    if (f >= o.f) return 1;
+    if (o.h <= 0 || o.w <= 0) return 0;
+    xi = (int)clip_ref(x / red, 0.0f, (float)(o.w - 1));
+    yi = (int)clip_ref(y / red, 0.0f, (float)(o.h - 1));
+    return -1;
+}
+
+__global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
+    __shared__ ScoreLDS Ls[kNmsWaves];
+    __shared__ int2 s_box[kNmsWaves][kNmsBoxLds];
+    __shared__ int s_m, s_m2, s_status;
+    __shared__ float s_mx, s_my;
+    const int img = blockIdx.x;
+    const int K = g.K;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    ScoreLDS &L = Ls[wave];
+    pp_ann *work = g.work + (int64_t)img * g.ann_cap;
+    pp_ann *out = g.out + (int64_t)img * g.ann_cap;
+    const int n_anns = g.n_work[img];
+    const int cap = g.ann_cap;
+    int *keep = g.nms_idx + (int64_t)img * (4 * cap + g.ann_np);  // kept work indices
+    int *surv = keep + cap;                                           // survivors
+    int *flag = surv + cap;                                           // per-index pass flags
+    int *perm2 = flag + cap;                                          // (unused pad)
+    int *perm = perm2 + cap;                                          // sort permutation
+    double *score = g.nms_score + (int64_t)img * 2 * cap;             // by work index
+    double *kscore = score + cap;                                     // by kept / survivor rank
+    float *amax = g.nms_f + (int64_t)img * 2 * cap;                   // per-ann max x, max y
+    int2 *gbox = g.nms_box + ((int64_t)img * kNmsWaves + wave) * cap;
+    const float red = (float)g.cfg.occupancy_reduction;
+    const float kt = g.cfg.nms_keypoint_threshold;
+    const double it = (double)g.cfg.nms_instance_threshold;
+    if (threadIdx.x == 0) s_status = g.status[img];
+#ifdef PP_STAMPS
+    if (lane == 0)
+        for (int q = 0; q < 8; q++) L.fst[q] = 0;
+#endif
+    __syncthreads();
+    STAMP_DECL
+
+    if (!g.cfg.apply_nms) {
+        for (int i = wave; i < n_anns; i += kNmsWaves) {
+            copy_ann(&out[i], &work[i]);
+            const double sc = ann_score_w(L, work[i].data, K);
+            if (lane == 0) out[i].score = sc;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            g.counts[img] = n_anns;
+            g.status[img] = s_status;
+        }
         return;
     }
 
-    STAMP(1);
-    int n_out = n_anns;
-    int *keep = g.nms_idx + (int64_t)img * (2 * g.ann_cap + g.ann_np);  // kept work indices
-    int *surv = keep + g.ann_cap;                                          // survivors
-    int *perm = surv + g.ann_cap;                                          // sort permutation
-    double *score = g.nms_score + (int64_t)img * g.ann_cap;
-    pp_ann *out = g.out + (int64_t)img * g.ann_cap;
-    if (g.cfg.apply_nms && n_anns > 0) {
-        // ---- nms.Keypoints.annotations (nms.py:17-57) ----
-        const float kt = g.cfg.nms_keypoint_threshold;
-        const double it = (double)g.cfg.nms_instance_threshold;
+    // nms.py:20-22: zero joints below keypoint_threshold, drop low scores (per annotation)
+    for (int i = wave; i < n_anns; i += kNmsWaves) {
+        pp_ann &a = work[i];
+        if (lane < K && a.data[lane][2] < kt) {
+            a.data[lane][0] = 0.0f;
+            a.data[lane][1] = 0.0f;
+            a.data[lane][2] = 0.0f;
+        }
+        wave_sync();
+        const double sc = ann_score_w(L, a.data, K);
+        if (lane == 0) {
+            float ax = a.data[0][0], ay = a.data[0][1];
+            for (int j = 1; j < K; j++) {
+                ax = a.data[j][0] > ax ? a.data[j][0] : ax;
+                ay = a.data[j][1] > ay ? a.data[j][1] : ay;
+            }
+            score[i] = sc;
+            flag[i] = sc >= it;
+            amax[i] = ax;
+            amax[cap + i] = ay;
+        }
+    }
+    __syncthreads();
+    STAMP(2);
+    // keep list in work order + the occupancy shape (nms.py:27-31), then the stable sort
+    if (wave == 0) {
         int m = 0;
         float mx = 0.0f, my = 0.0f;
-        for (int i = 0; i < n_anns; i++) {  // nms.py:20-22
-            pp_ann &a = work[i];
+        for (int i0 = 0; i0 < n_anns; i0 += 64) {
+            const int i = i0 + lane;
+            const bool k = i < n_anns && flag[i];
+            float ax = 0.0f, ay = 0.0f;
+            double sc = 0.0;
+            if (k) {
+                ax = amax[i];
+                ay = amax[cap + i];
+                sc = score[i];
+            }
+            const uint64_t km = __ballot(k);
+            if (k) {
+                const int r = m + lane_prefix(km);
+                keep[r] = i;
+                kscore[r] = sc;
+            }
+            uint64_t rest = km;
+            while (rest) {  // max over the kept annotations, in order (NaN behaviour)
+                const int l = __ffsll((unsigned long long)rest) - 1;
+                rest &= rest - 1;
+                const float lx = rl_f(ax, l), ly = rl_f(ay, l);
+                if (m == 0 || lx > mx) mx = lx;
+                if (m == 0 || ly > my) my = ly;
+                m++;
+            }
+        }
+        wave_sync();
+        if (m > 0) {
+            int np = 1;
+            while (np < m) np <<= 1;
+            sort_by_score(perm, np, m, kscore);  // nms.py:33 (stable)
+        }
+        if (lane == 0) {
+            s_m = m;
+            s_mx = mx;
+            s_my = my;
+        }
+    }
+    __syncthreads();
+    STAMP(3);
+    const int m = s_m;
+    int n_out = 0;
+    if (m > 0) {
+        // Occupancy((K, int(max y + 1), int(max x + 1)), 2, min_scale=4)
+        const long oh = (long)((double)(long)(s_my + 1.0f) / g.cfg.occupancy_reduction);
+        const long ow = (long)((double)(long)(s_mx + 1.0f) / g.cfg.occupancy_reduction);
+        const OccGrid no = occ_grid(nullptr, K, (int)(oh > 0 ? oh : 0), (int)(ow > 0 ? ow : 0));
+        int2 *boxes = m <= kNmsBoxLds ? s_box[wave] : gbox;
+        for (int f = wave; f < K; f += kNmsWaves) {  // nms.py:34-45, one plane per pass
+            int nbox = 0;
+            for (int r0 = 0; r0 < m; r0 += 64) {
+                const int r = r0 + lane;
+                int wi = 0;
+                float jx = 0.0f, jy = 0.0f, jv = 0.0f, js = 0.0f;
+                if (r < m) {
+                    wi = keep[perm[r]];
+                    jx = work[wi].data[f][0];
+                    jy = work[wi].data[f][1];
+                    jv = work[wi].data[f][2];
+                    js = work[wi].joint_scales[f];
+                }
+                const int nr = min(64, m - r0);
+                for (int l = 0; l < nr; l++) {
+                    const float v = rl_f(jv, l);
+                    if (v == 0.0f) continue;
+                    const float x = rl_f(jx, l), y = rl_f(jy, l);
+                    int xi = 0, yi = 0;
+                    const int fixed = occ_cell(no, f, x, y, red, xi, yi);
+                    int cnt = 0;
+                    if (fixed < 0) {
+                        for (int q = lane; q < nbox; q += 64) {
+                            const int2 b = boxes[q];
+                            cnt += (xi >= (b.x & 0xFFFF) && xi < (b.x >> 16) &&
+                                    yi >= (b.y & 0xFFFF) && yi < (b.y >> 16));
+                        }
+                        cnt = wave_total(cnt);
+                    }
+                    const bool occupied = fixed < 0 ? (cnt & 255) != 0 : fixed == 1;
+                    if (occupied) {
+                        if (lane == 0) work[rl_i(wi, l)].data[f][2] = v * g.cfg.nms_suppression;
+                    } else {
+                        int box[4];
+                        if (occ_box(g, no, f, x, y, rl_f(js, l), box)) {
+                            if (lane == 0)
+                                boxes[nbox] = make_int2(box[0] | (box[1] << 16), box[2] | (box[3] << 16));
+                            nbox++;
+                            wave_sync();
+                        }
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        STAMP(4);
+        // nms.py:51-53 in sorted order: zero low joints, drop low scores
+        for (int r = wave; r < m; r += kNmsWaves) {
+            pp_ann &a = work[keep[perm[r]]];
             if (lane < K && a.data[lane][2] < kt) {
                 a.data[lane][0] = 0.0f;
                 a.data[lane][1] = 0.0f;
                 a.data[lane][2] = 0.0f;
             }
             wave_sync();
-            const double sc = ann_score(L, a.data, K);
-            if (sc >= it) {
-                float ax = a.data[0][0], ay = a.data[0][1];
-                for (int j = 1; j < K; j++) {
-                    ax = a.data[j][0] > ax ? a.data[j][0] : ax;
-                    ay = a.data[j][1] > ay ? a.data[j][1] : ay;
-                }
-                if (m == 0 || ax > mx) mx = ax;
-                if (m == 0 || ay > my) my = ay;
-                if (lane == 0) {
-                    keep[m] = i;
-                    score[m] = sc;
-                }
-                m++;
+            const double sc = ann_score_w(L, a.data, K);
+            if (lane == 0) {
+                flag[r] = sc >= it;
+                score[r] = sc;  // by sorted rank now (the work-index scores are consumed)
             }
         }
-        wave_sync();
-        STAMP(2);
-        n_out = 0;
-        if (m > 0) {
-            // Occupancy((K, int(max y + 1), int(max x + 1)), 2, min_scale=4)  (nms.py:27-31)
-            const long oh = (long)((double)(long)(my + 1.0f) / g.cfg.occupancy_reduction);
-            const long ow = (long)((double)(long)(mx + 1.0f) / g.cfg.occupancy_reduction);
-            const OccGrid no = occ_grid(occ_base, K, (int)(oh > 0 ? oh : 0), (int)(ow > 0 ? ow : 0));
-            if ((int64_t)K * no.h * no.pitch > g.occ_cap) {
-                L.status |= PP_ST_NMS_OVERFLOW;
-            } else {
-                int np = 1;
-                while (np < m) np <<= 1;
-                sort_by_score(perm, np, m, score);  // nms.py:33 (stable)
-                STAMP(3);
-                for (int r = 0; r < m; r++) {  // nms.py:34-45
-                    pp_ann &a = work[keep[perm[r]]];
-                    // joints sit on separate occupancy planes: test all in parallel, then
-                    // suppress the occupied ones and mark the free ones
-                    bool occd = false;
-                    if (lane < K && a.data[lane][2] != 0.0f)
-                        occd = occ_get(no, lane, a.data[lane][0], a.data[lane][1], red);
-                    const uint64_t om = __ballot(occd);
-                    wave_sync();
-                    if (occd) a.data[lane][2] = a.data[lane][2] * g.cfg.nms_suppression;
-                    occ_mark(g, L, log, no, a.data, a.joint_scales, K, [&](int j) {
-                        return !((om >> j) & 1ull) && a.data[j][2] != 0.0f;
-                    });
+        __syncthreads();
+        STAMP(6);
+        if (wave == 0) {
+            int m2 = 0;
+            for (int r0 = 0; r0 < m; r0 += 64) {
+                const int r = r0 + lane;
+                const bool k = r < m && flag[r];
+                int wi = 0;
+                double sc = 0.0;
+                if (k) {
+                    wi = keep[perm[r]];
+                    sc = score[r];
                 }
-                STAMP(4);
-                occ_clear(g, L, log, no);
-                STAMP(5);
-                int m2 = 0;
-                for (int r = 0; r < m; r++) {  // nms.py:51-53, in sorted order
-                    const int wi = keep[perm[r]];
-                    pp_ann &a = work[wi];
-                    if (lane < K && a.data[lane][2] < kt) {
-                        a.data[lane][0] = 0.0f;
-                        a.data[lane][1] = 0.0f;
-                        a.data[lane][2] = 0.0f;
-                    }
-                    wave_sync();
-                    const double sc = ann_score(L, a.data, K);
-                    if (sc >= it) {
-                        if (lane == 0) {
-                            surv[m2] = wi;
-                            score[m2] = sc;
-                        }
-                        m2++;
-                    }
+                const uint64_t km = __ballot(k);
+                if (k) {
+                    const int q = m2 + lane_prefix(km);
+                    surv[q] = wi;
+                    kscore[q] = sc;
                 }
-                wave_sync();
-                STAMP(6);
+                m2 += __popcll(km);
+            }
+            wave_sync();
+            if (m2 > 0) {
                 int np2 = 1;
                 while (np2 < m2) np2 <<= 1;
-                if (m2 > 0) sort_by_score(perm, np2, m2, score);  // nms.py:54
-                STAMP(7);
-                for (int r = 0; r < m2; r++) {
-                    copy_ann(&out[r], &work[surv[perm[r]]]);
-                    if (lane == 0) out[r].score = score[perm[r]];
-                }
-                n_out = m2;
+                sort_by_score(perm, np2, m2, kscore);  // nms.py:54
             }
+            if (lane == 0) s_m2 = m2;
         }
-    } else {
-        for (int i = 0; i < n_anns; i++) {
-            copy_ann(&out[i], &work[i]);
-            const double sc = ann_score(L, work[i].data, K);
-            if (lane == 0) out[i].score = sc;
+        __syncthreads();
+        STAMP(7);
+        n_out = s_m2;
+        for (int r = wave; r < n_out; r += kNmsWaves) {
+            copy_ann(&out[r], &work[surv[perm[r]]]);
+            if (lane == 0) out[r].score = kscore[perm[r]];
         }
     }
-    wave_sync();
+    __syncthreads();
     STAMP(8);
-    STAMP_FLUSH(3);
-    if (lane == 0) {
+    if (wave == 0) {
+        STAMP_FLUSH(3);
+    }
+    if (threadIdx.x == 0) {
         g.counts[img] = n_out;
-        g.status[img] = L.status;
+        g.status[img] = s_status;
     }
 }
 
@@ -1610,7 +1744,7 @@ struct DecodeLayout {
     int64_t occ_cap;
     size_t off_cifhr, off_cifhr_ws, off_seeds, off_seed_counts, off_seed_ws, off_cols[2],
         off_offs[2], off_n_work, off_need, off_occ, off_log, off_work, off_spec, off_nms_score,
-        off_nms_idx, total;
+        off_nms_idx, off_nms_f, off_nms_box, total;
     size_t cifhr_ws_bytes;
 };
 
@@ -1654,8 +1788,10 @@ static DecodeLayout make_layout(int n_img, int K, int C, int H, int W, const pp_
     d.off_log = take(n * d.log_cap * sizeof(OccLog));
     d.off_work = take(n * ann_cap * sizeof(pp_ann));
     d.off_spec = take(n * kSpecCache * sizeof(pp_ann));
-    d.off_nms_score = take(n * ann_cap * sizeof(double));
-    d.off_nms_idx = take(n * (2 * ann_cap + d.ann_np) * sizeof(int));
+    d.off_nms_score = take(n * 2 * ann_cap * sizeof(double));
+    d.off_nms_idx = take(n * (4 * ann_cap + d.ann_np) * sizeof(int));
+    d.off_nms_f = take(n * 2 * ann_cap * sizeof(float));
+    d.off_nms_box = take(n * kNmsWaves * ann_cap * sizeof(int2));
     d.total = o;
     return d;
 }
@@ -1794,6 +1930,8 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
         g.spec_far = kSpecFar;
         g.nms_score = (double *)(ws + d.off_nms_score);
         g.nms_idx = (int *)(ws + d.off_nms_idx);
+        g.nms_f = (float *)(ws + d.off_nms_f);
+        g.nms_box = (int2 *)(ws + d.off_nms_box);
         g.ann_np = d.ann_np;
         g.ann_cap = ann_capacity;
         g.stamps = nullptr;
@@ -1822,11 +1960,11 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
             if (rc) return rc;
         }
         if (cfg->force_complete) {
-            hipLaunchKernelGGL(grow_kernel<2>, dim3(n_img, kCompleteWays), dim3(64), 0, s, g);
+            hipLaunchKernelGGL(complete_kernel, dim3(n_img, kCompleteWays), dim3(64), 0, s, g);
             rc = check_launch("pp_decode_batch(force complete)");
             if (rc) return rc;
         }
-        hipLaunchKernelGGL(grow_kernel<3>, dim3(n_img), dim3(64), 0, s, g);
+        hipLaunchKernelGGL(nms_kernel, dim3(n_img), dim3(64 * kNmsWaves), 0, s, g);
         rc = check_launch("pp_decode_batch(nms)");
 #ifdef PP_STAMPS
         hipStreamSynchronize(s);

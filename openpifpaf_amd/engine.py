@@ -116,7 +116,9 @@ class DecodeEngine:
         total = int(offsets[-1])
         if total == 0:
             return np.zeros(0, ANN_DTYPE), offsets
-        idx = np.concatenate([i * b.cap + np.arange(c) for i, c in enumerate(counts) if c])
+        # row of record r of image i is i * cap + r: one vectorised gather index
+        idx = np.arange(total, dtype=np.int64) + np.repeat(
+            np.arange(len(counts), dtype=np.int64) * b.cap - offsets[:-1], counts)
         rows = b.anns.view(b.n * b.cap, ANN_DTYPE.itemsize)
         sel = rows.index_select(0, torch.from_numpy(idx).to(rows.device))
         # pinned destination from torch's caching host allocator: full-rate D2H, and the
