@@ -21,6 +21,8 @@ CALIB_BYTES = 1 << 30
 
 
 def short(name):
+    """Kernel name without return type, namespace, template and parameter lists (the
+    caf_bucketed_kernel<false> / <true> stages therefore share one row)."""
     name = name.split('(')[0]
     for pre in ('void ', 'pp::'):
         name = name.replace(pre, '')
