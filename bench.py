@@ -49,6 +49,8 @@ def parse():
     p.add_argument('--cpu-seconds', type=float, default=12.0,
                    help='budget of the oracle CPU baseline sample (rank 0, N=1)')
     p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--stage-breakdown', action='store_true',
+                   help='one library call per stage (per-stage times)')
     return p.parse_args()
 
 
@@ -89,18 +91,24 @@ def main():
 
     eng = DecodeEngine()
     stream = torch.cuda.current_stream()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
-    stage_ms = np.zeros(4)
+    # default: CifHr alone (its events give the roofline), then the other stages in one
+    # call; --stage-breakdown: one call per stage
+    groups = ((STAGE_CIFHR, STAGE_SEEDS, STAGE_CAF, STAGE_GROW) if args.stage_breakdown else
+              (STAGE_CIFHR, STAGE_SEEDS | STAGE_CAF | STAGE_GROW))
+    names = (('cifhr', 'seeds', 'caf_scored', 'grow_nms') if args.stage_breakdown else
+             ('cifhr', 'seeds+caf+grow+nms'))
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(groups) + 1)]
+    stage_ms = np.zeros(len(groups))
 
     def step(timed):
         b = None
-        for si, bit in enumerate((STAGE_CIFHR, STAGE_SEEDS, STAGE_CAF, STAGE_GROW)):
+        for si, bits in enumerate(groups):
             if timed:
                 ev[si].record(stream)
-            if stages & bit:
-                b = eng.launch(cif, caf, skeleton, cfg, stages=bit)
+            if stages & bits:
+                b = eng.launch(cif, caf, skeleton, cfg, stages=stages & bits)
         if timed:
-            ev[4].record(stream)
+            ev[len(groups)].record(stream)
         recs = None
         if stages & STAGE_GROW:
             recs, offsets = eng.fetch(b)  # packed records -> host (synchronises)
@@ -108,7 +116,7 @@ def main():
                 recs, _ = gather_records(recs, offsets, dist, dev)
         if timed:
             torch.cuda.synchronize()
-            for si in range(4):
+            for si in range(len(groups)):
                 stage_ms[si] += ev[si].elapsed_time(ev[si + 1])
         return b, recs
 
@@ -164,8 +172,7 @@ def main():
             'parallelism': 'image-sharded dp{} (RCCL all-gather of annotation records)'.format(
                 world) if world > 1 else 'single GPU',
         },
-        'stage_ms': {'cifhr': round(stage_avg[0], 4), 'seeds': round(stage_avg[1], 4),
-                     'caf_scored': round(stage_avg[2], 4), 'grow_nms': round(stage_avg[3], 4)},
+        'stage_ms': {n: round(float(v), 4) for n, v in zip(names, stage_avg)},
         'annotations_per_image': round(n_anns / max(1, args.steps * batch * world), 3)
         if stages & STAGE_GROW else None,
         'roofline': {

@@ -331,6 +331,27 @@ def test_seed_ties(dec, hw):
     assert (np.diff(exp[:, 0]) == 0).sum() > len(exp) // 2  # the case really has ties
 
 
+def test_stage_calls_equal_full_decode(dec):
+    """pp_decode_stages called stage by stage, or with several stages per call, gives the
+    same records as pp_decode_batch (the stage contract of include/pifpaf_amd.h)."""
+    import torch
+    from openpifpaf_amd import constants, engine, synthetic
+    from openpifpaf_amd._abi import EVAL_CONFIG, make_config
+    cif, caf = synthetic.batch('planted', 32, 80, 80, first_seed=900)
+    c, f = torch.from_numpy(cif).cuda(), torch.from_numpy(caf).cuda()
+    cfg = make_config(**EVAL_CONFIG)
+    sk = constants.COCO_PERSON_SKELETON
+    eng = engine.DecodeEngine()
+    ref, ref_off = eng.fetch(eng.launch(c, f, sk, cfg))
+    ref = ref.copy()
+    for groups in ((1, 2, 4, 8), (1, 14), (15,)):
+        for bits in groups:
+            b = eng.launch(c, f, sk, cfg, stages=bits)
+        got, off = eng.fetch(b)
+        assert np.array_equal(off, ref_off), groups
+        assert got.tobytes() == ref.tobytes(), groups
+
+
 def test_workspace_left_clean(dec):
     """The occupancy workspace is zero again after a decode (workspace contract)."""
     from openpifpaf_amd import constants, engine, synthetic
