@@ -65,7 +65,7 @@ constexpr int kKP = PP_MAX_KP;
 constexpr int kSlots = 2 * PP_MAX_EDGES;   // directed edges (two lanes' worth of slots)
 constexpr int kHeap = 4 * PP_MAX_EDGES + 8; // flood-fill heap capacity
 constexpr int kOccMargin = 64;              // NMS occupancy slack beyond the main grid
-constexpr int kCompleteWays = 32;           // force-complete workgroups per image
+constexpr int kCompleteWays = 64;           // force-complete workgroups per image
 
 struct FFEntry {  // _flood_fill frontier entry (-v, end_i, start_xyv, s)
     float neg;
@@ -119,6 +119,8 @@ struct GrowArgs {
     int ann_cap;
     uint64_t *stamps;         // diagnostic build: (n_img, 3, 12) cycle sums, else NULL
     int *n_work;              // (n_img) annotations after the seed loop (phase 1 -> 2)
+    int *complete_next;       // (n_img) force-complete work counters (zero region; the NMS
+                              // kernel, ordered after completion, resets them)
     int *need_complete;       // (n_img) bitmask of joints left unset by the seed loop in any
                               // annotation (force-complete has work iff != 0; gates the B sets)
     // outputs
@@ -206,7 +208,7 @@ __device__ __forceinline__ bool ff_less(const FFEntry &a, const FFEntry &b) {
     return a.s < b.s;
 }
 
-__device__ void ff_push(GrowLDS &L, const FFEntry &x) {
+__device__ __forceinline__ void ff_push(GrowLDS &L, const FFEntry &x) {
     int i = L.ff_n;
     if (i >= kHeap) {
         L.status |= PP_ST_DEC_OVERFLOW;
@@ -222,7 +224,7 @@ __device__ void ff_push(GrowLDS &L, const FFEntry &x) {
     L.ff[i] = x;
 }
 
-__device__ FFEntry ff_pop(GrowLDS &L) {
+__device__ __forceinline__ FFEntry ff_pop(GrowLDS &L) {
     const FFEntry top = L.ff[0];
     const int n = L.ff_n - 1;
     L.ff_n = n;
@@ -232,12 +234,8 @@ __device__ FFEntry ff_pop(GrowLDS &L) {
         for (;;) {
             const int l = 2 * i + 1, r = l + 1;
             int m = i;
-            const FFEntry *mv = &x;
-            if (l < n && ff_less(L.ff[l], *mv)) {
-                m = l;
-                mv = &L.ff[l];
-            }
-            if (r < n && ff_less(L.ff[r], *mv)) m = r;
+            if (l < n && ff_less(L.ff[l], x)) m = l;
+            if (r < n && ff_less(L.ff[r], m == i ? x : L.ff[l])) m = r;
             if (m == i) break;
             L.ff[i] = L.ff[m];
             i = m;
@@ -1410,7 +1408,12 @@ __global__ __launch_bounds__(64) void complete_kernel(GrowArgs g) {
     const int n_anns = g.n_work[img];
     STAMP(0);
     if (!g.need_complete[img]) return;
-    for (int i = blockIdx.y; i < n_anns; i += gridDim.y) {
+    // annotations are handed out one at a time (their completion costs differ widely)
+    for (;;) {
+        int i = 0;
+        if (lane == 0) i = atomicAdd(&g.complete_next[img], 1);
+        i = __builtin_amdgcn_readfirstlane(i);
+        if (i >= n_anns) break;
         bool has0 = false;
         for (int j = 0; j < K; j++) has0 = has0 || work[i].data[j][2] == 0.0f;
         if (!has0) continue;
@@ -1510,7 +1513,10 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
     const float red = (float)g.cfg.occupancy_reduction;
     const float kt = g.cfg.nms_keypoint_threshold;
     const double it = (double)g.cfg.nms_instance_threshold;
-    if (threadIdx.x == 0) s_status = g.status[img];
+    if (threadIdx.x == 0) {
+        s_status = g.status[img];
+        g.complete_next[img] = 0;  // workspace contract: left zero
+    }
 #ifdef PP_STAMPS
     if (lane == 0)
         for (int q = 0; q < 8; q++) L.fst[q] = 0;
@@ -1743,7 +1749,7 @@ struct DecodeLayout {
     float inv_e;
     int64_t occ_cap;
     size_t off_cifhr, off_cifhr_ws, off_seeds, off_seed_counts, off_seed_ws, off_cols[2],
-        off_offs[2], off_n_work, off_need, off_occ, off_log, off_work, off_spec, off_nms_score,
+        off_offs[2], off_n_work, off_need, off_occ, off_wq, off_log, off_work, off_spec, off_nms_score,
         off_nms_idx, off_nms_f, off_nms_box, total;
     size_t cifhr_ws_bytes;
 };
@@ -1784,7 +1790,8 @@ static DecodeLayout make_layout(int n_img, int K, int C, int H, int W, const pp_
     }
     d.off_n_work = take(n * sizeof(int));
     d.off_need = take(n * sizeof(int));
-    d.off_occ = take(n * d.occ_cap);
+    d.off_occ = take(n * d.occ_cap);  // zero region from here (pp_decode_workspace_zero_offset)
+    d.off_wq = take(n * sizeof(int));
     d.off_log = take(n * d.log_cap * sizeof(OccLog));
     d.off_work = take(n * ann_cap * sizeof(pp_ann));
     d.off_spec = take(n * kSpecCache * sizeof(pp_ann));
@@ -1946,6 +1953,7 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
 #endif
         g.n_work = (int *)(ws + d.off_n_work);
         g.need_complete = (int *)(ws + d.off_need);
+        g.complete_next = (int *)(ws + d.off_wq);
         g.out = d_anns;
         g.counts = d_counts;
         g.status = d_status;
