@@ -167,6 +167,22 @@ int pp_decode_batch(const float *d_cif, const float *d_caf, int32_t n_img, int32
                     void *d_workspace, size_t workspace_bytes, void *stream);
 
 /*
+ * nms.Keypoints.annotations (nms.py:17-57) over caller records, n_img independent groups:
+ * d_anns (n_img, ann_capacity) with d_counts[i] records in group i (modified in place as
+ * the reference modifies its Annotation objects: joints below keypoint_threshold zeroed,
+ * suppressed joints' v scaled by nms_suppression).  Survivors sorted by -score go to
+ * d_out (n_img, ann_capacity) with their score set, d_out_counts (n_img), and optionally
+ * d_out_index (n_img, ann_capacity) = the input index of each survivor.  Uses cfg's
+ * nms_* thresholds and occupancy_reduction / occupancy_min_scale.  Scores are the
+ * default Annotation.score() (no fixed_score, no suppress_score_index).
+ */
+size_t pp_nms_workspace_size(int32_t n_img, int32_t ann_capacity);
+int pp_nms_keypoints(pp_ann *d_anns, const int32_t *d_counts, int32_t n_img, int32_t K,
+                     int32_t ann_capacity, const pp_config *cfg, pp_ann *d_out,
+                     int32_t *d_out_counts, int32_t *d_out_index, void *d_workspace,
+                     size_t workspace_bytes, void *stream);
+
+/*
  * The same decode split into stages for measurement: bit 1 CifHr, 2 CifSeeds,
  * 4 CafScored at caf_threshold, 8 seed loop + grow + complete + NMS (stage 8 also builds
  * the complete_caf_threshold column sets, only where force-complete needs them).  Stage buffers live

@@ -55,6 +55,9 @@ _SIGNATURES = {
     'pp_scalar_lookup': ([_vp, _i64, _i64, _i64, _i32, _vp, _vp, _i64, _f, _f, _vp, _vp],
                          ctypes.c_int),
     'pp_grow_connection': ([_vp, _i64, _i64, _f, _f, _f, _i32, _vp, _vp], ctypes.c_int),
+    'pp_nms_workspace_size': ([_i32, _i32], _sz),
+    'pp_nms_keypoints': ([_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _sz, _vp],
+                         ctypes.c_int),
     'pp_center_filter': ([_vp, _i64, _i64, _i64, _i32, _f, _f, _f, _vp, _i64, _vp, _vp],
                          ctypes.c_int),
 }

@@ -124,6 +124,7 @@ struct GrowArgs {
     int *need_complete;       // (n_img) bitmask of joints left unset by the seed loop in any
                               // annotation (force-complete has work iff != 0; gates the B sets)
     // outputs
+    int *out_idx;             // optional (n_img, ann_cap): input index of each output record
     pp_ann *out;
     int *counts;
     int *status;
@@ -1499,7 +1500,7 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
     ScoreLDS &L = Ls[wave];
     pp_ann *work = g.work + (int64_t)img * g.ann_cap;
     pp_ann *out = g.out + (int64_t)img * g.ann_cap;
-    const int n_anns = g.n_work[img];
+    const int n_anns = max(0, min(g.n_work[img], g.ann_cap));
     const int cap = g.ann_cap;
     int *keep = g.nms_idx + (int64_t)img * (4 * cap + g.ann_np);  // kept work indices
     int *surv = keep + cap;                                           // survivors
@@ -1528,7 +1529,10 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
         for (int i = wave; i < n_anns; i += kNmsWaves) {
             copy_ann(&out[i], &work[i]);
             const double sc = ann_score_w(L, work[i].data, K);
-            if (lane == 0) out[i].score = sc;
+            if (lane == 0) {
+                out[i].score = sc;
+                if (g.out_idx) g.out_idx[(int64_t)img * cap + i] = i;
+            }
         }
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -1709,7 +1713,10 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
         n_out = s_m2;
         for (int r = wave; r < n_out; r += kNmsWaves) {
             copy_ann(&out[r], &work[surv[perm[r]]]);
-            if (lane == 0) out[r].score = kscore[perm[r]];
+            if (lane == 0) {
+                out[r].score = kscore[perm[r]];
+                if (g.out_idx) g.out_idx[(int64_t)img * cap + r] = surv[perm[r]];
+            }
         }
     }
     __syncthreads();
@@ -2002,6 +2009,75 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
 #endif
     }
     return rc;
+}
+
+// ---- standalone nms.Keypoints.annotations (nms.py:17-57) over caller records ----------
+namespace {
+struct NmsLayout {
+    size_t off_status, off_wq, off_score, off_idx, off_f, off_box, total;
+    int ann_np;
+};
+NmsLayout nms_layout(int n_img, int cap) {
+    NmsLayout l{};
+    l.ann_np = 1;
+    while (l.ann_np < cap) l.ann_np <<= 1;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t at = o;
+        o += align_up(bytes);
+        return at;
+    };
+    const size_t n = (size_t)n_img;
+    l.off_status = take(n * sizeof(int));
+    l.off_wq = take(n * sizeof(int));
+    l.off_score = take(n * 2 * cap * sizeof(double));
+    l.off_idx = take(n * (4 * (size_t)cap + l.ann_np) * sizeof(int));
+    l.off_f = take(n * 2 * cap * sizeof(float));
+    l.off_box = take(n * kNmsWaves * (size_t)cap * sizeof(int2));
+    l.total = o;
+    return l;
+}
+}  // namespace
+
+size_t pp_nms_workspace_size(int32_t n_img, int32_t ann_capacity) {
+    if (n_img < 0 || ann_capacity <= 0) return 0;
+    return nms_layout(n_img, ann_capacity).total;
+}
+
+int pp_nms_keypoints(pp_ann *d_anns, const int32_t *d_counts, int32_t n_img, int32_t K,
+                     int32_t ann_capacity, const pp_config *cfg, pp_ann *d_out,
+                     int32_t *d_out_counts, int32_t *d_out_index, void *d_workspace,
+                     size_t workspace_bytes, void *stream) {
+    if (!d_anns || !d_counts || !cfg || !d_out || !d_out_counts || !d_workspace)
+        return fail(PP_EINVAL, "pp_nms_keypoints: NULL argument");
+    if (n_img < 0 || K <= 0 || K > PP_MAX_KP || ann_capacity <= 0 || cfg->occupancy_reduction <= 0)
+        return fail(PP_ESHAPE, "pp_nms_keypoints: shape outside the supported envelope");
+    if (n_img == 0) return PP_OK;
+    const NmsLayout l = nms_layout(n_img, ann_capacity);
+    if (workspace_bytes < l.total) return fail(PP_ENOMEM, "pp_nms_keypoints: workspace too small");
+    char *ws = (char *)d_workspace;
+    hipStream_t s = (hipStream_t)stream;
+    GrowArgs g{};
+    g.K = K;
+    g.cfg = *cfg;
+    g.cfg.apply_nms = 1;
+    g.work = d_anns;
+    g.n_work = const_cast<int *>(d_counts);
+    g.ann_cap = ann_capacity;
+    g.ann_np = l.ann_np;
+    g.status = (int *)(ws + l.off_status);
+    g.complete_next = (int *)(ws + l.off_wq);
+    g.nms_score = (double *)(ws + l.off_score);
+    g.nms_idx = (int *)(ws + l.off_idx);
+    g.nms_f = (float *)(ws + l.off_f);
+    g.nms_box = (int2 *)(ws + l.off_box);
+    g.out = d_out;
+    g.counts = d_out_counts;
+    g.out_idx = d_out_index;
+    if (hipMemsetAsync(g.status, 0, (size_t)n_img * sizeof(int), s) != hipSuccess)
+        return fail(PP_EHIP, "pp_nms_keypoints: memset failed");
+    hipLaunchKernelGGL(nms_kernel, dim3(n_img), dim3(64 * kNmsWaves), 0, s, g);
+    return check_launch("pp_nms_keypoints");
 }
 
 int pp_decode_batch(const float *d_cif, const float *d_caf, int32_t n_img, int32_t K, int32_t C,

@@ -38,6 +38,7 @@ def lib():
         _LIB.orc_weiszfeld_nd.restype = ctypes.c_long
         _LIB.orc_center_filter.restype = ctypes.c_long
         _LIB.orc_ann_score.restype = ctypes.c_double
+        _LIB.orc_nms_keypoints.restype = ctypes.c_long
         assert _LIB.orc_sizeof_ann() == ANN_DTYPE.itemsize
     return _LIB
 
@@ -113,8 +114,24 @@ def decode(cif, caf, skeleton, cfg=None):
         cap = int(n)
 
 
+def nms_keypoints(data, scales, keypoint_threshold, instance_threshold, suppression):
+    """nms.Keypoints().annotations on n annotations (data (n, K, 3), scales (n, K)).
+    Returns (order: survivors' input indices, survivor records)."""
+    n, k, _ = data.shape
+    recs = np.zeros(n, ANN_DTYPE)
+    recs['data'][:, :k] = data
+    recs['joint_scales'][:, :k] = scales
+    recs['n_keypoints'] = k
+    recs['image'] = np.arange(n)
+    cfg = make_config(nms_keypoint_threshold=keypoint_threshold,
+                      nms_instance_threshold=instance_threshold, nms_suppression=suppression)
+    m = lib().orc_nms_keypoints(recs.ctypes.data_as(_vp), _l(n), _i(k), ctypes.byref(cfg))
+    return recs['image'][:m].astype(np.int64), recs[:m]
+
+
 def ann_score(v):
-    v = _c32(np.stack([np.zeros_like(v), np.zeros_like(v), v], axis=1))
+    """Annotation.score() of joint confidences v (K,) (orc_ann_score reads v with stride 3)."""
+    v = _c32(np.stack([v, np.zeros_like(v), np.zeros_like(v)], axis=1))
     return lib().orc_ann_score(_p(v.reshape(-1)), _i(len(v)))
 
 

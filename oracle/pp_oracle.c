@@ -988,6 +988,18 @@ static int nms_keypoints(const dec_t *d, pp_ann *anns, int n) {
     return k;
 }
 
+/* nms.Keypoints().annotations (nms.py:17-57) on caller records; survivors written to
+ * anns[0..k) in output order (carry an input index in pp_ann.image to track them) */
+EXPORT long orc_nms_keypoints(pp_ann *anns, long n, int K, const pp_config *cfg) {
+    if (K <= 0 || K > PP_MAX_KP || n < 0) return -1;
+    if (n == 0) return 0;
+    dec_t d;
+    memset(&d, 0, sizeof(d));
+    d.K = K;
+    d.cfg = cfg;
+    return nms_keypoints(&d, anns, (int)n);
+}
+
 static void ann_init(pp_ann *a, int K) {
     memset(a, 0, sizeof(*a));
     a->n_keypoints = K;

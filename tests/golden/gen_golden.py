@@ -12,6 +12,8 @@ Fixtures:
   primitives.npz       known-answer tests for every openpifpaf.functional primitive
                        (small fields, full inputs and outputs, strided views, edge cases)
   errors.json          the reference's ValueError messages at the boundary
+  nms.npz              nms.Keypoints().annotations on random overlapping Annotation lists
+                       (inputs, output order as input indices, mutated data), per config
   decode_<case>.npz    per-stage vectors of the full CifCaf decoder: CifHr digest +
                        per-field sums + windows, full seed list, CafScored counts + digests,
                        full annotation lists (data, joint_scales, score, decoding_order,
@@ -304,6 +306,49 @@ def gen_errors():
     print('errors:', errs)
 
 
+NMS_CASES = [  # (name, n annotations, spread px, seed, keypoint_th, instance_th, suppression)
+    ('eval', 60, 160.0, 0, 0.0, 0.0, 0.0),
+    ('predict', 60, 160.0, 1, 0.001, 0.1, 0.0),
+    ('supp', 80, 120.0, 2, 0.0, 0.0, 0.5),
+    ('dense', 300, 200.0, 3, 0.001, 0.1, 0.0),
+    ('zeros', 20, 80.0, 4, 0.3, 0.2, 0.0),
+]
+
+
+def gen_nms(op):
+    """Random overlapping poses through the reference nms.Keypoints (nms.py:17-57)."""
+    from openpifpaf.annotation import Annotation  # pylint: disable=import-outside-toplevel
+    from openpifpaf.decoder import nms  # pylint: disable=import-outside-toplevel
+    out = {}
+    kps, skel = constants.COCO_KEYPOINTS, constants.COCO_PERSON_SKELETON
+    for name, n, spread, seed, kt, it, sup in NMS_CASES:
+        rng = np.random.default_rng(100 + seed)
+        base = rng.uniform(10.0, spread, (n, 1, 2)).astype(np.float32)
+        xy = (base + rng.normal(0.0, 12.0, (n, 17, 2))).astype(np.float32)
+        v = rng.uniform(0.0, 1.0, (n, 17)).astype(np.float32)
+        v[rng.uniform(0.0, 1.0, (n, 17)) < 0.2] = 0.0
+        data = np.concatenate([xy, v[:, :, None]], axis=2).astype(np.float32)
+        scales = rng.uniform(0.5, 24.0, (n, 17)).astype(np.float32)
+        anns = []
+        for i in range(n):
+            a = Annotation(kps, skel)
+            a.data = data[i].copy()
+            a.joint_scales = scales[i].copy()
+            anns.append(a)
+        k = nms.Keypoints()
+        k.keypoint_threshold, k.instance_threshold, k.suppression = kt, it, sup
+        ids = {id(a): i for i, a in enumerate(anns)}
+        res = k.annotations(list(anns))
+        out[name + '_data_in'] = data
+        out[name + '_scales'] = scales
+        out[name + '_cfg'] = np.array([kt, it, sup], np.float32)
+        out[name + '_order'] = np.array([ids[id(a)] for a in res], np.int64)
+        out[name + '_data_out'] = np.stack([a.data for a in anns]).astype(np.float32)
+        out[name + '_score'] = np.array([a.score() for a in res], np.float64)
+        print('nms', name, n, '->', len(res))
+    np.savez_compressed(os.path.join(HERE, 'nms.npz'), **out)
+
+
 def main():
     op = ref_loader.load()
     import Cython  # pylint: disable=import-outside-toplevel
@@ -319,9 +364,13 @@ def main():
     }
     with open(os.path.join(HERE, 'meta.json'), 'w') as fh:
         json.dump(meta, fh, indent=1, sort_keys=True)
+    only = sys.argv[1:]
+    if only == ['nms']:
+        gen_nms(op)
+        return
     gen_primitives(op)
     gen_errors()
-    only = sys.argv[1:]
+    gen_nms(op)
     for case in CASES:
         if only and case[0] not in only:
             continue

@@ -4,6 +4,8 @@ Bit-exact: CifHr maps, seed lists, CafScored column sets, every functional primi
 Tolerance (golden_util.ATOL/RTOL) only for the grow-stage floats against the reference's
 own outputs (np.exp rounding); against the oracle the device decode must match exactly.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -369,3 +371,49 @@ def test_workspace_left_clean(dec):
     occ_bytes = b.ws[zoff:zoff + 4 * 17 * (156 + 64) * 224]
     assert int(occ_bytes.sum().item()) == 0
     assert engine.engine() is not None
+
+
+# ---- standalone nms.Keypoints (nms.py:17-57) ------------------------------------------------
+
+def _nms_anns(data, scales):
+    from openpifpaf_amd import constants
+    from openpifpaf_amd.annotation import Annotation
+    anns = []
+    for d, sc in zip(data, scales):
+        a = Annotation(constants.COCO_KEYPOINTS, constants.COCO_PERSON_SKELETON)
+        a.data = d.copy()
+        a.joint_scales = sc.copy()
+        anns.append(a)
+    return anns
+
+
+@pytest.mark.parametrize('name', ['eval', 'predict', 'supp', 'dense', 'zeros'])
+def test_nms_keypoints_vs_reference(dec, name):
+    """Device NMS over host Annotation lists: the reference's order, in-place edits, scores."""
+    g = np.load(os.path.join(gu.GOLDEN, 'nms.npz'))
+    kt, it, sup = (float(t) for t in g[name + '_cfg'])
+    anns = _nms_anns(g[name + '_data_in'], g[name + '_scales'])
+    k = dec.nms.Keypoints()
+    k.keypoint_threshold, k.instance_threshold, k.suppression = kt, it, sup
+    res = k.annotations(list(anns))
+    ids = {id(a): i for i, a in enumerate(anns)}
+    assert [ids[id(a)] for a in res] == g[name + '_order'].tolist()
+    assert np.array_equal(np.stack([a.data for a in anns]), g[name + '_data_out'])
+    assert np.array_equal(np.array([a.score() for a in res]), g[name + '_score'])
+
+
+def test_nms_keypoints_many_vs_oracle(dec):
+    """More kept annotations than the LDS box lists hold (global-memory path)."""
+    rng = np.random.default_rng(7)
+    n = 1500
+    xy = rng.uniform(0.0, 2000.0, (n, 17, 2)).astype(np.float32)
+    v = rng.uniform(0.05, 1.0, (n, 17)).astype(np.float32)
+    data = np.concatenate([xy, v[:, :, None]], axis=2)
+    scales = rng.uniform(0.5, 6.0, (n, 17)).astype(np.float32)
+    order, recs = oracle.nms_keypoints(data, scales, 0.0, 0.0, 0.0)
+    assert len(order) > 1100
+    anns = _nms_anns(data, scales)
+    res = dec.nms.Keypoints().annotations(list(anns))
+    ids = {id(a): i for i, a in enumerate(anns)}
+    assert [ids[id(a)] for a in res] == order.tolist()
+    assert np.array_equal(np.stack([a.data for a in res]), recs['data'][:, :17])

@@ -4,6 +4,8 @@ The golden fixtures were produced by running the reference decoder
 (tests/golden/gen_golden.py).  Bit-exact for CifHr, seeds, CafScored and every
 functional primitive; tolerance (golden_util.ATOL/RTOL) for the grow-stage floats.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -129,3 +131,20 @@ def test_decode(name):
     recs = oracle.decode(cif, caf, skeleton, gu.case_config(g))
     errs = gu.compare_annotations(g, recs)
     assert not errs, errs[:10]
+
+
+# ---- standalone keypoint NMS (nms.py:17-57) ----------------------------------------------
+
+NMS_NAMES = ('eval', 'predict', 'supp', 'dense', 'zeros')
+
+
+@pytest.mark.parametrize('name', NMS_NAMES)
+def test_oracle_nms_vs_reference(name):
+    g = np.load(os.path.join(gu.GOLDEN, 'nms.npz'))
+    kt, it, sup = (float(t) for t in g[name + '_cfg'])
+    order, recs = oracle.nms_keypoints(g[name + '_data_in'], g[name + '_scales'], kt, it, sup)
+    assert order.tolist() == g[name + '_order'].tolist()
+    exp = g[name + '_data_out'][order]
+    assert np.array_equal(recs['data'][:, :17], exp)
+    scores = np.array([oracle.ann_score(d[:, 2]) for d in exp])
+    assert np.array_equal(scores, g[name + '_score'])
