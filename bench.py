@@ -49,6 +49,8 @@ def parse():
     p.add_argument('--cpu-seconds', type=float, default=12.0,
                    help='budget of the oracle CPU baseline sample (rank 0, N=1)')
     p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--no-uniform', action='store_true',
+                   help='skip the uniform-generator line added to the default run')
     p.add_argument('--stage-breakdown', action='store_true',
                    help='one library call per stage (per-stage times)')
     return p.parse_args()
@@ -98,55 +100,62 @@ def main():
     names = (('cifhr', 'seeds', 'caf_scored', 'grow_nms') if args.stage_breakdown else
              ('cifhr', 'seeds+caf+grow+nms'))
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(groups) + 1)]
-    stage_ms = np.zeros(len(groups))
 
-    def step(timed):
-        b = None
-        for si, bits in enumerate(groups):
+    def timed_run(cif, caf, steps, warmup):
+        """warmup + `steps` timed decode steps of one resident batch: (elapsed s over all
+        ranks, per-group event ms per step, annotations decoded)."""
+        stage_ms = np.zeros(len(groups))
+
+        def step(timed):
+            b = None
+            for si, bits in enumerate(groups):
+                if timed:
+                    ev[si].record(stream)
+                if stages & bits:
+                    b = eng.launch(cif, caf, skeleton, cfg, stages=stages & bits)
             if timed:
-                ev[si].record(stream)
-            if stages & bits:
-                b = eng.launch(cif, caf, skeleton, cfg, stages=stages & bits)
-        if timed:
-            ev[len(groups)].record(stream)
-        recs = None
-        if stages & STAGE_GROW:
-            recs, offsets = eng.fetch(b)  # packed records -> host (synchronises)
-            if world > 1:
-                recs, _ = gather_records(recs, offsets, dist, dev)
-        if timed:
-            torch.cuda.synchronize()
-            for si in range(len(groups)):
-                stage_ms[si] += ev[si].elapsed_time(ev[si + 1])
-        return b, recs
+                ev[len(groups)].record(stream)
+            recs = None
+            if stages & STAGE_GROW:
+                recs, offsets = eng.fetch(b)  # packed records -> host (synchronises)
+                if world > 1:
+                    recs, _ = gather_records(recs, offsets, dist, dev)
+            if timed:
+                torch.cuda.synchronize()
+                for si in range(len(groups)):
+                    stage_ms[si] += ev[si].elapsed_time(ev[si + 1])
+            return b, recs
 
-    for _ in range(args.warmup):
-        b, recs = step(False)
-    status = b.status.cpu().numpy()
-    if status.any():
-        raise SystemExit('decode status flags set: {}'.format(status[status != 0][:8]))
+        for _ in range(warmup):
+            b, recs = step(False)
+            recs = None
+        status = b.status.cpu().numpy()
+        if status.any():
+            raise SystemExit('decode status flags set: {}'.format(status[status != 0][:8]))
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n_anns = 0
+        for _ in range(steps):
+            b, recs = step(True)
+            n_anns += 0 if recs is None else len(recs)
+            recs = None  # the caller owns records; release them so pinned blocks recycle
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return elapsed, stage_ms / steps, n_anns
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    n_anns = 0
-    for _ in range(args.steps):
-        b, recs = step(True)
-        n_anns += 0 if recs is None else len(recs)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, stage_avg, n_anns = timed_run(cif, caf, args.steps, args.warmup)
 
     images = batch * world * args.steps
     value = images / elapsed
     ms_step = 1e3 * elapsed / args.steps
-    stage_avg = stage_ms / args.steps
     hh, ww = (h - 1) * 8 + 1, (w - 1) * 8 + 1
     cifhr_bytes = 4 * k * (5 * h * w + hh * ww) * batch
     achieved = cifhr_bytes / (stage_avg[0] * 1e-3) / 1e9
@@ -186,6 +195,20 @@ def main():
                    args.mode == 'eval' and batch == WORKLOADS['cfg3']['batch'])
     if default_run:
         line['roofline'].update(committed_traffic())
+    if default_run and world == 1 and not args.no_uniform:
+        # the same workload on the uniform generator (SURVEY.md §8d cfg3 names both):
+        # dense random fields, ~400 annotations per image
+        del cif, caf
+        ucif, ucaf = synthetic.batch('uniform', batch, h, w, n_caf=len(skeleton))
+        ucif, ucaf = torch.from_numpy(ucif).to(dev), torch.from_numpy(ucaf).to(dev)
+        u_steps = max(3, args.steps // 2)
+        u_el, u_stage, u_anns = timed_run(ucif, ucaf, u_steps, 2)
+        line['uniform'] = {
+            'value': round(batch * u_steps / u_el, 1), 'unit': 'images/s',
+            'ms_per_step': round(1e3 * u_el / u_steps, 4),
+            'stage_ms': {n: round(float(v), 4) for n, v in zip(names, u_stage)},
+            'annotations_per_image': round(u_anns / (u_steps * batch), 3),
+        }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line['cpu_baseline'] = cpu_baseline(cif_h, caf_h, skeleton, cfg, args.cpu_seconds)
     if rank == 0:

@@ -167,6 +167,21 @@ int pp_decode_batch(const float *d_cif, const float *d_caf, int32_t n_img, int32
                     void *d_workspace, size_t workspace_bytes, void *stream);
 
 /*
+ * Field ingestion: the raw output of a CompositeFieldFused head's conv (network/heads.py:
+ * 406-455, eval mode) -> the decoder's field layout, as CifCafCollector /
+ * CifdetCollector.forward (heads.py:65-88, 127-144) produce it: `quad` PixelShuffle(2)
+ * dequads with the last row / column cropped, sigmoid on confidences, exp on scales, the
+ * index grid added to the vector components and the channel reorder, in one pass.
+ *   d_conv  (n_img, F * 4^quad, h, w) with F = n_fields * (5 | 9 | 7) for layout
+ *           0 CIF (IntensityMeta), 1 CAF (AssociationMeta), 2 CifDet (DetectionMeta)
+ *   d_out   (n_img, n_fields, 5 | 9 | 7, H, W) with H = pp_fields_dim(h, quad)
+ * Floats: sigmoid / exp are evaluated in f64 and rounded (within 1 ulp of torch's).
+ */
+int64_t pp_fields_dim(int64_t n, int32_t quad);
+int pp_fields_from_conv(const float *d_conv, int32_t n_img, int32_t n_fields, int32_t layout,
+                        int32_t h, int32_t w, int32_t quad, float *d_out, void *stream);
+
+/*
  * nms.Keypoints.annotations (nms.py:17-57) over caller records, n_img independent groups:
  * d_anns (n_img, ann_capacity) with d_counts[i] records in group i (modified in place as
  * the reference modifies its Annotation objects: joints below keypoint_threshold zeroed,

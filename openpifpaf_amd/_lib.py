@@ -56,6 +56,8 @@ _SIGNATURES = {
                          ctypes.c_int),
     'pp_grow_connection': ([_vp, _i64, _i64, _f, _f, _f, _i32, _vp, _vp], ctypes.c_int),
     'pp_nms_workspace_size': ([_i32, _i32], _sz),
+    'pp_fields_dim': ([_i64, _i32], _i64),
+    'pp_fields_from_conv': ([_vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp], ctypes.c_int),
     'pp_nms_keypoints': ([_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _sz, _vp],
                          ctypes.c_int),
     'pp_center_filter': ([_vp, _i64, _i64, _i64, _i32, _f, _f, _f, _vp, _i64, _vp, _vp],

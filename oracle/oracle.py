@@ -217,3 +217,39 @@ def center_filter(field, x, y, sigma, mode):
     if mode == 3:
         return out != 0
     return out[:, :k]
+
+
+# ---- network/heads.py field ingestion (numpy restatement, test infrastructure) -------------
+
+_INGEST = {  # (n_conf, n_vec, n_scales), output channel -> concatenated channel
+    'cif': ((1, 1, 1), (0, 1, 2, 3, 4)),
+    'caf': ((1, 2, 2), (0, 1, 2, 5, 7, 3, 4, 6, 8)),        # heads.py:87
+    'cifdet': ((1, 2, 0), (0, 1, 2, 5, 3, 4, 6)),           # heads.py:142
+}
+
+
+def fields_from_conv(conv, n_fields, kind, quad):
+    """CompositeFieldFused.forward (eval, heads.py:406-455) after its conv, then the
+    collector (heads.py:65-88 / 127-144).  sigmoid / exp in float64, rounded to float32."""
+    (nc, nv, ns), perm = _INGEST[kind]
+    x = np.asarray(conv, np.float32)
+    for _ in range(quad):  # PixelShuffle(2), then [:, :, :-1, :-1]
+        b, c, h, w = x.shape
+        x = x.reshape(b, c // 4, 2, 2, h, w).transpose(0, 1, 4, 2, 5, 3).reshape(
+            b, c // 4, 2 * h, 2 * w)[:, :, :-1, :-1]
+    b, _, h, w = x.shape
+    f0, f1, f2 = nc * n_fields, (nc + 2 * nv) * n_fields, (nc + 3 * nv) * n_fields
+    conf = 1.0 / (1.0 + np.exp(-x[:, :f0].astype(np.float64)))
+    parts = [conf.astype(np.float32).reshape(b, n_fields, nc, h, w),
+             x[:, f0:f1].reshape(b, n_fields, 2 * nv, h, w),
+             x[:, f1:f2].reshape(b, n_fields, nv, h, w)]
+    if ns:
+        parts.append(np.exp(x[:, f2:].astype(np.float64)).astype(np.float32).reshape(
+            b, n_fields, ns, h, w))
+    cat = np.concatenate(parts, axis=2)
+    yy, xx = np.indices((h, w), dtype=np.float32)
+    vec_pairs = 1 if kind == 'cifdet' else nv
+    for v in range(vec_pairs):  # index_field_torch added to the vector components
+        cat[:, :, 1 + 2 * v] += xx
+        cat[:, :, 2 + 2 * v] += yy
+    return np.ascontiguousarray(cat[:, :, list(perm)])

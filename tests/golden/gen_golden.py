@@ -12,6 +12,8 @@ Fixtures:
   primitives.npz       known-answer tests for every openpifpaf.functional primitive
                        (small fields, full inputs and outputs, strided views, edge cases)
   errors.json          the reference's ValueError messages at the boundary
+  heads.npz            CompositeFieldFused (conv replaced by identity, eval mode) +
+                       CifCafCollector / CifdetCollector on random conv outputs, quad 0-2
   nms.npz              nms.Keypoints().annotations on random overlapping Annotation lists
                        (inputs, output order as input indices, mutated data), per config
   decode_<case>.npz    per-stage vectors of the full CifCaf decoder: CifHr digest +
@@ -349,6 +351,43 @@ def gen_nms(op):
     np.savez_compressed(os.path.join(HERE, 'nms.npz'), **out)
 
 
+def gen_heads(op):
+    """Raw head conv output -> decoder fields through the reference modules."""
+    import torch  # pylint: disable=import-outside-toplevel
+    from openpifpaf.network import heads  # pylint: disable=import-outside-toplevel
+    kps, skel = constants.COCO_KEYPOINTS, constants.COCO_PERSON_SKELETON
+    metas = {
+        'cif': heads.IntensityMeta('cif', kps, [0.05] * 17, None),
+        'caf': heads.AssociationMeta('caf', kps, [0.05] * 17, None, skel),
+        'cifdet': heads.DetectionMeta('cifdet', ['a', 'b', 'c']),
+    }
+    out = {}
+    rng = np.random.default_rng(11)
+    for quad in (0, 1, 2):
+        heads.CompositeFieldFused.quad = quad
+        res = {}
+        for kind, meta in metas.items():
+            head = heads.CompositeFieldFused(meta, 4)
+            head.conv = torch.nn.Identity()
+            head.eval()
+            per = {'cif': 5, 'caf': 9, 'cifdet': 7}[kind]
+            h, w = 3, 4
+            x = (2.0 * rng.standard_normal((1, meta.n_fields * per * 4 ** quad, h, w))).astype(
+                np.float32)
+            with torch.no_grad():
+                res[kind] = head(torch.from_numpy(x))
+            out['q%d_%s_conv' % (quad, kind)] = x
+        with torch.no_grad():
+            cif, caf = heads.CifCafCollector([0], [1])([res['cif'], res['caf']])
+            (det,) = heads.CifdetCollector([0])([res['cifdet']])
+        out['q%d_cif' % quad] = cif.numpy()
+        out['q%d_caf' % quad] = caf.numpy()
+        out['q%d_cifdet' % quad] = det.numpy()
+        print('heads quad', quad, cif.shape, caf.shape, det.shape)
+    heads.CompositeFieldFused.quad = 1
+    np.savez_compressed(os.path.join(HERE, 'heads.npz'), **out)
+
+
 def main():
     op = ref_loader.load()
     import Cython  # pylint: disable=import-outside-toplevel
@@ -368,9 +407,13 @@ def main():
     if only == ['nms']:
         gen_nms(op)
         return
+    if only == ['heads']:
+        gen_heads(op)
+        return
     gen_primitives(op)
     gen_errors()
     gen_nms(op)
+    gen_heads(op)
     for case in CASES:
         if only and case[0] not in only:
             continue

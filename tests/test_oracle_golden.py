@@ -148,3 +148,19 @@ def test_oracle_nms_vs_reference(name):
     assert np.array_equal(recs['data'][:, :17], exp)
     scores = np.array([oracle.ann_score(d[:, 2]) for d in exp])
     assert np.array_equal(scores, g[name + '_score'])
+
+
+# ---- head conv output -> decoder fields (network/heads.py) ----------------------------------
+
+@pytest.mark.parametrize('quad', [0, 1, 2])
+@pytest.mark.parametrize('kind,n_fields', [('cif', 17), ('caf', 19), ('cifdet', 3)])
+def test_oracle_ingest_vs_reference(kind, n_fields, quad):
+    g = np.load(os.path.join(gu.GOLDEN, 'heads.npz'))
+    got = oracle.fields_from_conv(g['q%d_%s_conv' % (quad, kind)], n_fields, kind, quad)
+    exp = g['q%d_%s' % (quad, kind)]
+    assert got.shape == exp.shape
+    # torch's float32 sigmoid / exp vs f64-rounded: 1e-6 relative; everything else exact
+    np.testing.assert_allclose(got, exp, rtol=1e-6, atol=1e-7)
+    exact = [o for o in range(exp.shape[2]) if not (o == 0 or (kind == 'cif' and o == 4) or
+                                                   (kind == 'caf' and o in (4, 8)))]
+    assert np.array_equal(got[:, :, exact], exp[:, :, exact])
