@@ -100,6 +100,25 @@ typedef struct pp_seed {
     float s;
 } pp_seed;
 
+/* One detection: AnnotationDet (annotation.py:122-137) with its image */
+typedef struct pp_det {
+    int32_t field;       /* category index (field_i)                                     */
+    float score;
+    float bbox[4];       /* x, y, w, h                                                   */
+    int32_t image;
+    int32_t pad_;
+} pp_det;
+
+/* nms.Detection class attributes (nms.py:60-65) */
+typedef struct pp_det_nms {
+    float suppression;        /* 0.1 */
+    float suppression_soft;   /* 0.3 */
+    float instance_threshold; /* 0.1 */
+    float iou_threshold;      /* 0.7 */
+    float iou_threshold_soft; /* 0.5 */
+    int32_t apply;            /* 1 */
+} pp_det_nms;
+
 /* per-image status bits written by pp_decode_batch (d_status) */
 #define PP_ST_ANN_OVERFLOW 1   /* more annotations than ann_capacity               */
 #define PP_ST_NMS_OVERFLOW 2   /* NMS occupancy larger than the occupancy workspace */

@@ -50,6 +50,9 @@ __device__ __forceinline__ int4 splat_box(float cx, float cy, float ext, int h, 
 // -------------------------------------------------------------------------------------
 constexpr int kTileBits = 1024;  // per-field tile bitmap capacity (32x32 tiles of 64x64 px)
 
+// DET: CifDetHr.accumulate (cif_hr.py:84-100) on 7-channel fields [c, x, y, b, w, h, b2],
+// sigma = max(1, 0.1 * min(w, h) * stride); else CifHr (cif_hr.py:26-40), 5 channels.
+template <bool DET>
 __global__ __launch_bounds__(256) void cifhr_splats_kernel(const float *__restrict__ cif, int H,
                                                            int W, int hh, int ww, float stride,
                                                            float v_th, float neighbors,
@@ -64,7 +67,7 @@ __global__ __launch_bounds__(256) void cifhr_splats_kernel(const float *__restri
     __syncthreads();
     const int64_t fld = blockIdx.x;  // image * K + field
     const int hw = H * W;
-    const float *p = cif + fld * 5 * (int64_t)hw;
+    const float *p = cif + fld * (DET ? 7 : 5) * (int64_t)hw;
     Splat *out = splats + fld * (int64_t)hw;
     int running = 0;
     for (int base = 0; base < hw; base += 256) {
@@ -77,7 +80,14 @@ __global__ __launch_bounds__(256) void cifhr_splats_kernel(const float *__restri
         if (keep) {
             const float x = p[hw + cell] * stride;
             const float y = p[2 * hw + cell] * stride;
-            const float sg = (0.5f * p[4 * hw + cell]) * stride;
+            float sg;
+            if (DET) {  // np.minimum / np.maximum propagate NaN
+                const float w = p[4 * hw + cell], h = p[5 * hw + cell];
+                const float m = (w != w) ? w : ((h != h) ? h : (h < w ? h : w));
+                sg = (0.1f * m) * stride;
+            } else {
+                sg = (0.5f * p[4 * hw + cell]) * stride;
+            }
             const float sigma = (sg != sg) ? sg : fmaxf(1.0f, sg);  // np.maximum keeps NaN
             const float v = (c / neighbors) / 1.0f;                 // v / neighbors / len_cifs
             Splat s;
@@ -341,9 +351,13 @@ size_t pp_cifhr_workspace_size(int32_t n_img, int32_t K, int32_t H, int32_t W) {
            round_up((int64_t)(nf * (kTileBits / 32) * sizeof(uint32_t)), 256);
 }
 
-int pp_cifhr(const float *d_cif, int32_t n_img, int32_t K, int32_t H, int32_t W,
-             const pp_config *cfg, float *d_cifhr, void *d_workspace, size_t workspace_bytes,
-             void *stream) {
+}  // extern "C"
+
+namespace pp {
+template <bool DET>
+static int cifhr_launch(const float *d_cif, int32_t n_img, int32_t K, int32_t H, int32_t W,
+                        const pp_config *cfg, float *d_cifhr, void *d_workspace,
+                        size_t workspace_bytes, void *stream) {
     if (!d_cif || !cfg || !d_cifhr || !d_workspace) return fail(PP_EINVAL, "pp_cifhr: NULL argument");
     if (n_img < 0 || K <= 0 || H <= 0 || W <= 0 || cfg->stride <= 0)
         return fail(PP_ESHAPE, "pp_cifhr: bad shape");
@@ -360,7 +374,7 @@ int pp_cifhr(const float *d_cif, int32_t n_img, int32_t K, int32_t H, int32_t W,
     const int tiles_x = (int)((pitch + kTile - 1) / kTile);
     const int tiles = tiles_x * ((hh + kTile - 1) / kTile);
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(cifhr_splats_kernel, dim3((unsigned)nf), dim3(256), 0, s, d_cif, H, W, hh,
+    hipLaunchKernelGGL(cifhr_splats_kernel<DET>, dim3((unsigned)nf), dim3(256), 0, s, d_cif, H, W, hh,
                        ww, (float)cfg->stride, cfg->cif_threshold, (float)cfg->cif_neighbors,
                        splats, counts, bits, tiles_x, tiles);
     TileArgs a{};
@@ -377,7 +391,24 @@ int pp_cifhr(const float *d_cif, int32_t n_img, int32_t K, int32_t H, int32_t W,
     a.t2 = 1.0f;  // truncate = 1.0 (cif_hr.py:40)
     a.max_value = 1.0f;
     launch_tiles<M_GAUSS_MAX, true>(a, s);
-    return check_launch("pp_cifhr");
+    return check_launch(DET ? "pp_cifdet_hr" : "pp_cifhr");
+}
+}  // namespace pp
+
+extern "C" {
+
+int pp_cifhr(const float *d_cif, int32_t n_img, int32_t K, int32_t H, int32_t W,
+             const pp_config *cfg, float *d_cifhr, void *d_workspace, size_t workspace_bytes,
+             void *stream) {
+    return cifhr_launch<false>(d_cif, n_img, K, H, W, cfg, d_cifhr, d_workspace, workspace_bytes,
+                               stream);
+}
+
+int pp_cifdet_hr(const float *d_det, int32_t n_img, int32_t K, int32_t H, int32_t W,
+                 const pp_config *cfg, float *d_cifhr, void *d_workspace, size_t workspace_bytes,
+                 void *stream) {
+    return cifhr_launch<true>(d_det, n_img, K, H, W, cfg, d_cifhr, d_workspace, workspace_bytes,
+                              stream);
 }
 
 }  // extern "C"

@@ -10,6 +10,9 @@ synthetic fields with the reference's field layout (network/heads.py:65-88):
 * planted(...)  - realistic input: a low-confidence background plus n people whose joints
                   get 4x4 CIF patches (encoder/cif.py:118-145 places 4x4 patches) and whose
                   limbs get one 4x4 CAF patch at the limb midpoint pointing joint1 -> joint2.
+* det_planted / det_uniform(...) - CifDet fields (n_categories, 7, H, W), channels
+                  [c, x, y, b, w, h, b2] (CifdetCollector, heads.py:127-144): boxes whose
+                  centre cells carry the box centre and size, or random fields.
 
 Both are deterministic functions of their arguments (numpy PCG64 streams).  The golden
 fixtures record a SHA-256 of the generated inputs so a change here is caught by the tests.
@@ -117,6 +120,48 @@ def planted(h, w, n_people=8, seed=0, skeleton=None, noise=0.08):
             sub[8][m] = scale
 
     return cif, caf
+
+
+def det_uniform(h, w, n_categories=3, seed=0):
+    rng = np.random.default_rng(seed)
+    det = rng.random((n_categories, 7, h, w), dtype=np.float32)
+    det[:, 0] **= 4
+    det[:, 1:3] += _grid(h, w) - 0.5
+    det[:, 4:6] = 0.5 + 8.0 * det[:, 4:6]
+    return det
+
+
+def det_planted(h, w, n_categories=3, n_objects=10, seed=0, noise=0.08):
+    """Objects of random category, centre and size (field cells); the 4x4 patch of cells
+    around each centre predicts it."""
+    rng = np.random.default_rng(seed)
+    g = _grid(h, w)
+    det = np.zeros((n_categories, 7, h, w), dtype=np.float32)
+    det[:, 0] = rng.uniform(0.0, noise, (n_categories, h, w))
+    det[:, 1:3] = g + rng.uniform(-0.5, 0.5, (n_categories, 2, h, w))
+    det[:, 3] = 0.5
+    det[:, 4:6] = rng.uniform(0.5, 3.0, (n_categories, 2, h, w))
+    det[:, 6] = 0.5
+    for _ in range(n_objects):
+        f = int(rng.integers(n_categories))
+        cx, cy = rng.uniform(2.0, w - 2.0), rng.uniform(2.0, h - 2.0)
+        bw, bh = rng.uniform(2.0, w / 2.0), rng.uniform(2.0, h / 2.0)
+        xs, ys = _patch_cells(cx, cy, h, w)
+        conf = rng.uniform(0.7, 1.0, (len(ys), len(xs))).astype(np.float32)
+        sub = det[f, :, ys[0]:ys[-1] + 1, xs[0]:xs[-1] + 1]
+        m = conf > sub[0]
+        sub[0][m] = conf[m]
+        sub[1][m] = cx + rng.normal(0.0, 0.1, m.sum())
+        sub[2][m] = cy + rng.normal(0.0, 0.1, m.sum())
+        sub[4][m] = bw
+        sub[5][m] = bh
+    return det
+
+
+def det_batch(kind, n, h, w, first_seed=0, **kwargs):
+    """(n, n_categories, 7, H, W) CifDet fields, image i from seed first_seed + i."""
+    fn = {'planted': det_planted, 'uniform': det_uniform}[kind]
+    return np.stack([fn(h, w, seed=first_seed + i, **kwargs) for i in range(n)])
 
 
 def generate(kind, h, w, seed, n_caf=19, skeleton=None, n_people=8):

@@ -39,6 +39,8 @@ def lib():
         _LIB.orc_center_filter.restype = ctypes.c_long
         _LIB.orc_ann_score.restype = ctypes.c_double
         _LIB.orc_nms_keypoints.restype = ctypes.c_long
+        _LIB.orc_cifdet_seeds.restype = ctypes.c_long
+        _LIB.orc_cifdet_decode.restype = ctypes.c_long
         assert _LIB.orc_sizeof_ann() == ANN_DTYPE.itemsize
     return _LIB
 
@@ -253,3 +255,54 @@ def fields_from_conv(conv, n_fields, kind, quad):
         cat[:, :, 1 + 2 * v] += xx
         cat[:, :, 2 + 2 * v] += yy
     return np.ascontiguousarray(cat[:, :, list(perm)])
+
+
+# ---- CifDet (decoder/generator/cifdet.py) --------------------------------------------------
+
+DET_DTYPE = np.dtype([('field', '<i4'), ('score', '<f4'), ('bbox', '<f4', (4,)), ('image', '<i4'),
+                      ('pad_', '<i4')])
+
+
+class DetNms(ctypes.Structure):
+    """pp_det_nms: nms.Detection class attributes (nms.py:60-65)."""
+    _fields_ = [('suppression', ctypes.c_float), ('suppression_soft', ctypes.c_float),
+                ('instance_threshold', ctypes.c_float), ('iou_threshold', ctypes.c_float),
+                ('iou_threshold_soft', ctypes.c_float), ('apply', ctypes.c_int32)]
+
+
+def det_nms_defaults():
+    return DetNms(0.1, 0.3, 0.1, 0.7, 0.5, 1)
+
+
+def cifdet_hr(det, cfg=None):
+    cfg = cfg or make_config()
+    det = _c32(det)
+    k, _, h, w = det.shape
+    hh, ww = hr_shape(h, w, cfg.stride)
+    out = np.empty((k, hh, ww), np.float32)
+    lib().orc_cifdet_hr(_p(det), _i(k), _i(h), _i(w), ctypes.byref(cfg), _p(out))
+    return out
+
+
+def cifdet_seeds(det, hr, cfg=None):
+    """(n, 7): v, field, x, y, w, h, emission index; sorted as the reference."""
+    cfg = cfg or make_config()
+    det, hr = _c32(det), _c32(hr)
+    k, _, h, w = det.shape
+    cap = k * h * w
+    out = np.empty((cap, 7), np.float32)
+    n = lib().orc_cifdet_seeds(_p(det), _p(hr), _l(hr.shape[-1]), _i(k), _i(h), _i(w),
+                               ctypes.byref(cfg), _p(out), _l(cap))
+    return out[:n]
+
+
+def cifdet_decode(det, cfg=None, nms=None):
+    cfg = cfg or make_config()
+    nms = nms or det_nms_defaults()
+    det = _c32(det)
+    k, _, h, w = det.shape
+    cap = k * h * w
+    out = np.zeros(cap, DET_DTYPE)
+    n = lib().orc_cifdet_decode(_p(det), _i(k), _i(h), _i(w), ctypes.byref(cfg),
+                                ctypes.byref(nms), out.ctypes.data_as(_vp), _l(cap))
+    return out[:n]

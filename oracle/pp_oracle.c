@@ -1083,4 +1083,192 @@ EXPORT long orc_decode(const float *cif, const float *caf, int K, int C, int H, 
     return n;
 }
 
+/* ---- CifDet (decoder/generator/cifdet.py:27-52) ---------------------------------------- */
+
+/* cif_hr.py:84-100 on (K, 7, H, W) fields [c, x, y, b, w, h, b2]; out (K, H', W') */
+EXPORT void orc_cifdet_hr(const float *det, int K, int H, int W, const pp_config *cfg, float *out) {
+    long hh = hr_dim(H, cfg->stride), ww = hr_dim(W, cfg->stride);
+    long hw = (long)H * W;
+    float *xs = (float *)malloc(sizeof(float) * 4 * (size_t)hw);
+    float *ys = xs + hw, *ss = ys + hw, *vs = ss + hw;
+    memset(out, 0, sizeof(float) * (size_t)K * hh * ww);
+    float stride = (float)cfg->stride;
+    for (int f = 0; f < K; f++) {
+        const float *p = det + (size_t)f * 7 * hw;
+        long n = 0;
+        for (long c = 0; c < hw; c++) {
+            if (!(p[c] > cfg->cif_threshold)) continue;
+            xs[n] = p[1 * hw + c] * stride;
+            ys[n] = p[2 * hw + c] * stride;
+            float w = p[4 * hw + c], h = p[5 * hw + c];
+            float m = (w != w) ? w : ((h != h) ? h : (h < w ? h : w)); /* np.minimum */
+            float sg = (0.1f * m) * stride;
+            ss[n] = (sg != sg) ? sg : fmaxf(1.0f, sg); /* np.maximum(1.0, .) */
+            vs[n] = (p[c] / (float)cfg->cif_neighbors) / 1.0f;
+            n++;
+        }
+        orc_scalar_square_add_gauss_with_max(out + (size_t)f * hh * ww, hh, ww, ww, 1, xs, ys, ss,
+                                             vs, n, 1.0f, 1.0f);
+    }
+    free(xs);
+}
+
+static int det_seed_cmp_desc(const void *pa, const void *pb) {
+    /* sorted(seeds, reverse=True) on (v, f, x, y, w, h); stable -> emission ascending */
+    const float *a = (const float *)pa, *b = (const float *)pb; /* v f x y w h idx */
+    for (int i = 0; i < 6; i++) {
+        if (a[i] == b[i]) continue;
+        return (a[i] > b[i]) ? -1 : 1;
+    }
+    return (a[6] < b[6]) ? -1 : (a[6] > b[6]);
+}
+
+/* cif_seeds.py:67-90.  out (cap, 7): v, f, x, y, w, h, emission index */
+EXPORT long orc_cifdet_seeds(const float *det, const float *hr, long hr_pitch, int K, int H, int W,
+                             const pp_config *cfg, float *out, long cap) {
+    long hh = hr_dim(H, cfg->stride), ww = hr_dim(W, cfg->stride);
+    long hw = (long)H * W;
+    float stride = (float)cfg->stride;
+    float *tmp = (float *)malloc(sizeof(float) * 7 * (size_t)(K * hw + 1));
+    long n = 0;
+    for (int f = 0; f < K; f++) {
+        const float *p = det + (size_t)f * 7 * hw;
+        const float *t = hr + (size_t)f * hh * hr_pitch;
+        for (long c = 0; c < hw; c++) {
+            float conf = p[c];
+            if (!(conf > cfg->seed_threshold)) continue;
+            float x = p[1 * hw + c], y = p[2 * hw + c];
+            float xs = x * stride, ys = y * stride, v;
+            orc_scalar_values(t, hh, ww, hr_pitch, 1, &xs, &ys, 1, 0.0f, &v);
+            v = 0.9f * v + 0.1f * conf;
+            if (cfg->seed_score_scale != 1.0f) v = v * cfg->seed_score_scale;
+            if (!(v > cfg->seed_threshold)) continue;
+            float *r = tmp + 7 * n;
+            r[0] = v;
+            r[1] = (float)f;
+            r[2] = xs;
+            r[3] = ys;
+            r[4] = p[4 * hw + c] * stride;
+            r[5] = p[5 * hw + c] * stride;
+            r[6] = (float)n;
+            n++;
+        }
+    }
+    qsort(tmp, (size_t)n, sizeof(float) * 7, det_seed_cmp_desc);
+    for (long i = 0; i < n && i < cap; i++) memcpy(out + 7 * i, tmp + 7 * i, sizeof(float) * 7);
+    free(tmp);
+    return n;
+}
+
+static inline float np_max(float a, float b) { return (a != a || b != b) ? NAN : (a > b ? a : b); }
+static inline float np_min(float a, float b) { return (a != a || b != b) ? NAN : (a < b ? a : b); }
+
+/* nms.Detection.bbox_iou (nms.py:67-77) for one pair, float32 as NumPy evaluates it */
+static float det_iou(const float *b, const float *o) {
+    float x1 = np_max(b[0], o[0]), y1 = np_max(b[1], o[1]);
+    float x2 = np_min(b[0] + b[2], o[0] + o[2]), y2 = np_min(b[1] + b[3], o[1] + o[3]);
+    float inter = np_max(0.0f, x2 - x1) * np_max(0.0f, y2 - y1);
+    float ba = b[2] * b[3], oa = o[2] * o[3];
+    return inter / (((ba + oa) - inter) + 1e-5f);
+}
+
+typedef struct {
+    float score;
+    int idx;
+} det_si;
+
+static int det_si_cmp(const void *pa, const void *pb) { /* sorted(key=-score), stable */
+    const det_si *a = (const det_si *)pa, *b = (const det_si *)pb;
+    float ka = -a->score, kb = -b->score;
+    if (ka < kb) return -1;
+    if (ka > kb) return 1;
+    return (a->idx < b->idx) ? -1 : (a->idx > b->idx);
+}
+
+/* nms.py:79-102 in place on d[0..n); returns the new count */
+static long det_nms(pp_det *d, long n, const pp_det_nms *p) {
+    det_si *si = (det_si *)malloc(sizeof(det_si) * (size_t)(n + 1));
+    pp_det *tmp = (pp_det *)malloc(sizeof(pp_det) * (size_t)(n + 1));
+    long m = 0;
+    for (long i = 0; i < n; i++)
+        if (d[i].score >= p->instance_threshold) tmp[m++] = d[i];
+    if (m == 0) {
+        free(si);
+        free(tmp);
+        return 0;
+    }
+    for (long i = 0; i < m; i++) {
+        si[i].score = tmp[i].score;
+        si[i].idx = (int)i;
+    }
+    qsort(si, (size_t)m, sizeof(det_si), det_si_cmp);
+    for (long i = 0; i < m; i++) d[i] = tmp[si[i].idx];
+    for (long i = 1; i < m; i++) {
+        float mx = -INFINITY; /* np.max over the masked IoUs: NaN if any is NaN */
+        int nan = 0;
+        for (long j = 0; j < i; j++) {
+            if (!(d[j].score >= p->instance_threshold)) continue;
+            float iou = det_iou(d[i].bbox, d[j].bbox);
+            if (iou != iou)
+                nan = 1;
+            else if (iou > mx)
+                mx = iou;
+        }
+        if (nan) mx = NAN;
+        if (mx > p->iou_threshold)
+            d[i].score *= p->suppression;
+        else if (mx > p->iou_threshold_soft)
+            d[i].score *= p->suppression_soft;
+    }
+    long k = 0;
+    for (long i = 0; i < m; i++)
+        if (d[i].score >= p->instance_threshold) tmp[k++] = d[i];
+    for (long i = 0; i < k; i++) {
+        si[i].score = tmp[i].score;
+        si[i].idx = (int)i;
+    }
+    qsort(si, (size_t)k, sizeof(det_si), det_si_cmp);
+    for (long i = 0; i < k; i++) d[i] = tmp[si[i].idx];
+    free(si);
+    free(tmp);
+    return k;
+}
+
+/* CifDet.__call__ for one image; returns the number of detections (written when <= cap) */
+EXPORT long orc_cifdet_decode(const float *det, int K, int H, int W, const pp_config *cfg,
+                              const pp_det_nms *nms, pp_det *out, long cap) {
+    long hh = hr_dim(H, cfg->stride), ww = hr_dim(W, cfg->stride);
+    float *hr = (float *)malloc(sizeof(float) * (size_t)K * hh * ww);
+    orc_cifdet_hr(det, K, H, W, cfg, hr);
+    long hw = (long)H * W;
+    float *seeds = (float *)malloc(sizeof(float) * 7 * (size_t)(K * hw + 1));
+    long ns = orc_cifdet_seeds(det, hr, ww, K, H, W, cfg, seeds, K * hw);
+    occ_t o;
+    occ_init(&o, K, hh, ww, 2, 2); /* Occupancy(cifhr.shape, 2, min_scale=2.0) */
+    pp_det *d = (pp_det *)calloc((size_t)(ns + 1), sizeof(pp_det));
+    long n = 0;
+    for (long i = 0; i < ns; i++) {
+        const float *r = seeds + 7 * i;
+        int f = (int)r[1];
+        float x = r[2], y = r[3], w = r[4], h = r[5];
+        if (occ_get(&o, f, x, y)) continue;
+        d[n].field = f;
+        d[n].score = r[0];
+        d[n].bbox[0] = x - w / 2.0f;
+        d[n].bbox[1] = y - h / 2.0f;
+        d[n].bbox[2] = w;
+        d[n].bbox[3] = h;
+        n++;
+        float mwh = (h < w) ? h : w; /* builtin min(w, h) */
+        occ_set(&o, f, x, y, 0.1f * mwh);
+    }
+    if (nms->apply) n = det_nms(d, n, nms);
+    for (long i = 0; i < n && i < cap; i++) out[i] = d[i];
+    free(o.occ);
+    free(d);
+    free(seeds);
+    free(hr);
+    return n;
+}
+
 EXPORT int orc_sizeof_ann(void) { return (int)sizeof(pp_ann); }

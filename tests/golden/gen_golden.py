@@ -12,6 +12,8 @@ Fixtures:
   primitives.npz       known-answer tests for every openpifpaf.functional primitive
                        (small fields, full inputs and outputs, strided views, edge cases)
   errors.json          the reference's ValueError messages at the boundary
+  det_<case>.npz       CifDet decoder (cifdet.py:27-52): CifDetHr digest + sums, the seed
+                       list, and the AnnotationDet list (field, score, bbox)
   heads.npz            CompositeFieldFused (conv replaced by identity, eval mode) +
                        CifCafCollector / CifdetCollector on random conv outputs, quad 0-2
   nms.npz              nms.Keypoints().annotations on random overlapping Annotation lists
@@ -388,6 +390,42 @@ def gen_heads(op):
     np.savez_compressed(os.path.join(HERE, 'heads.npz'), **out)
 
 
+# (name, generator, H, W, seed, seed threshold, n_categories)
+DET_CASES = [
+    ('dp40_s0', 'planted', 40, 40, 0, 0.5, 3),
+    ('dp40_s1', 'planted', 40, 40, 1, 0.2, 3),
+    ('dp80_s2', 'planted', 80, 80, 2, 0.5, 3),
+    ('dp40_c1', 'planted', 40, 40, 3, 0.5, 1),
+    ('du20_s0', 'uniform', 20, 20, 0, 0.05, 3),
+    ('du40_s1', 'uniform', 40, 40, 1, 0.1, 2),
+]
+
+
+def gen_det(op):
+    """The reference CifDet decoder on synthetic detection fields."""
+    from openpifpaf.decoder import CifDet, CifDetHr, FieldConfig  # pylint: disable=import-outside-toplevel
+    from openpifpaf.decoder.cif_seeds import CifDetSeeds, CifSeeds  # pylint: disable=import-outside-toplevel
+    for name, gen, h, w, seed, th, n_cat in DET_CASES:
+        det = synthetic.det_batch(gen, 1, h, w, first_seed=seed, n_categories=n_cat)[0]
+        CifSeeds.threshold = th
+        fc = FieldConfig()
+        hr = CifDetHr(fc).fill([det]).accumulated
+        seeds = CifDetSeeds(hr, fc).fill([det]).get()
+        anns = CifDet(fc, ['c%d' % i for i in range(n_cat)])([det])
+        out = {
+            'gen': np.array(gen), 'h': h, 'w': w, 'seed': seed, 'seed_threshold': th,
+            'n_categories': n_cat, 'input_sha': np.array(sha(det)),
+            'cifhr_sha': np.array(sha(hr)), 'cifhr_sums': hr.sum(axis=(1, 2), dtype=np.float64),
+            'seeds': np.array([[float(t) for t in sd] for sd in seeds], np.float32).reshape(-1, 6),
+            'ann_field': np.array([a.field_i for a in anns], np.int64),
+            'ann_score': np.array([a.score for a in anns], np.float32),
+            'ann_bbox': np.array([a.bbox for a in anns], np.float32).reshape(-1, 4),
+        }
+        np.savez_compressed(os.path.join(HERE, 'det_%s.npz' % name), **out)
+        print('det', name, 'seeds', len(seeds), 'anns', len(anns))
+    CifSeeds.threshold = None
+
+
 def main():
     op = ref_loader.load()
     import Cython  # pylint: disable=import-outside-toplevel
@@ -410,10 +448,14 @@ def main():
     if only == ['heads']:
         gen_heads(op)
         return
+    if only == ['det']:
+        gen_det(op)
+        return
     gen_primitives(op)
     gen_errors()
     gen_nms(op)
     gen_heads(op)
+    gen_det(op)
     for case in CASES:
         if only and case[0] not in only:
             continue
