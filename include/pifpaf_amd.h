@@ -186,6 +186,41 @@ int pp_decode_batch(const float *d_cif, const float *d_caf, int32_t n_img, int32
                     void *d_workspace, size_t workspace_bytes, void *stream);
 
 /*
+ * CifDet detection decoder (decoder/generator/cifdet.py:27-52), batched:
+ *   d_det     (n_img, K, 7, H, W) CifDet fields [c, x, y, b, w, h, b2] (heads.py:127-144)
+ *   d_cifhr   optional (n_img, K, H', pitch) output of CifDetHr (NULL: scratch)
+ *   d_out     (n_img, det_capacity) pp_det, d_counts (n_img), d_status (n_img) PP_ST_* bits
+ * Uses cfg's cif_threshold (CifHr.v_threshold), seed_threshold (>= 0), seed_score_scale,
+ * stride and cif_neighbors; the occupancy is the reference's fixed Occupancy(cifhr.shape,
+ * 2, min_scale=2.0); nms.Detection runs with *nms (pp_default_det_nms) when nms->apply.
+ * pp_cifdet_hr is the CifDetHr stage alone (cif_hr.py:84-100), workspace as pp_cifhr.
+ */
+void pp_default_det_nms(pp_det_nms *nms);
+int pp_cifdet_hr(const float *d_det, int32_t n_img, int32_t K, int32_t H, int32_t W,
+                 const pp_config *cfg, float *d_cifhr, void *d_workspace, size_t workspace_bytes,
+                 void *stream);
+/* nms.Detection.annotations (nms.py:79-102) over caller records: n_img groups, d_in
+ * (n_img, capacity) with d_counts[i] records (field, score, bbox) in list order.  Output
+ * as pp_cifdet_decode; d_out_index (optional) = input index of each output record. */
+size_t pp_nms_detection_workspace_size(int32_t n_img, int32_t capacity);
+int pp_nms_detection(const pp_det *d_in, const int32_t *d_counts, int32_t n_img, int32_t capacity,
+                     const pp_det_nms *nms, pp_det *d_out, int32_t *d_out_counts,
+                     int32_t *d_out_index, void *d_workspace, size_t workspace_bytes,
+                     void *stream);
+/* CifDetSeeds.fill_cif (cif_seeds.py:67-90) per (image, field), in cell order:
+ * d_seg (n_img, K, 5, H*W) = v, x, y, w, h of the first d_seg_counts[i, f] entries;
+ * d_cifhr (n_img, K, H', pitch).  get() = sorted((v, f, x, y, w, h), reverse=True). */
+int pp_cifdet_seeds(const float *d_det, const float *d_cifhr, int32_t n_img, int32_t K, int32_t H,
+                    int32_t W, const pp_config *cfg, float *d_seg, int32_t *d_seg_counts,
+                    void *stream);
+size_t pp_cifdet_workspace_size(int32_t n_img, int32_t K, int32_t H, int32_t W,
+                                const pp_config *cfg, int32_t det_capacity);
+int pp_cifdet_decode(const float *d_det, int32_t n_img, int32_t K, int32_t H, int32_t W,
+                     const pp_config *cfg, const pp_det_nms *nms, float *d_cifhr, pp_det *d_out,
+                     int32_t det_capacity, int32_t *d_counts, int32_t *d_status,
+                     void *d_workspace, size_t workspace_bytes, void *stream);
+
+/*
  * Field ingestion: the raw output of a CompositeFieldFused head's conv (network/heads.py:
  * 406-455, eval mode) -> the decoder's field layout, as CifCafCollector /
  * CifdetCollector.forward (heads.py:65-88, 127-144) produce it: `quad` PixelShuffle(2)

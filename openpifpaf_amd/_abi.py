@@ -88,3 +88,16 @@ PREDICT_CONFIG = dict(seed_threshold=0.5, force_complete=False, keypoint_thresho
 
 def skeleton_array(skeleton):
     return np.ascontiguousarray(np.asarray(skeleton, dtype=np.int32).reshape(-1, 2))
+
+
+# pp_det: one AnnotationDet (annotation.py:122-137) with its image
+DET_DTYPE = np.dtype([('field', '<i4'), ('score', '<f4'), ('bbox', '<f4', (4,)), ('image', '<i4'),
+                      ('pad_', '<i4')])
+assert DET_DTYPE.itemsize == 32
+
+
+class DetNms(ctypes.Structure):
+    """pp_det_nms: nms.Detection class attributes (nms.py:60-65)."""
+    _fields_ = [('suppression', ctypes.c_float), ('suppression_soft', ctypes.c_float),
+                ('instance_threshold', ctypes.c_float), ('iou_threshold', ctypes.c_float),
+                ('iou_threshold_soft', ctypes.c_float), ('apply', ctypes.c_int32)]

@@ -121,3 +121,38 @@ class Annotation:
         w = np.max(kps[:, 0][m] + joint_scales[m]) - x
         h = np.max(kps[:, 1][m] + joint_scales[m]) - y
         return [x, y, w, h]
+
+
+class AnnotationDet:
+    """One detection (annotation.py:122-145): category field_i, score, bbox (x, y, w, h)."""
+
+    def __init__(self, categories):
+        self.categories = categories
+        self.field_i = None
+        self.score = None
+        self.bbox = None
+
+    def set(self, field_i, score, bbox):
+        """Set score to None for a ground truth annotation."""
+        self.field_i = field_i
+        self.score = score
+        self.bbox = np.asarray(bbox)
+        return self
+
+    @classmethod
+    def from_record(cls, rec, categories):
+        """Build from one pp_det record (include/pifpaf_amd.h)."""
+        return cls(categories).set(int(rec['field']), np.float32(rec['score']),
+                                   np.array(rec['bbox'], dtype=np.float32))
+
+    @property
+    def category(self):
+        return self.categories[self.field_i]
+
+    def json_data(self):
+        return {
+            'category_id': self.field_i + 1,
+            'category': self.category,
+            'score': max(0.001, round(float(self.score), 3)),
+            'bbox': [round(float(c), 2) for c in self.bbox],
+        }

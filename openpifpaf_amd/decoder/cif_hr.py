@@ -31,6 +31,20 @@ def cifhr_device(cif, stride, v_threshold, neighbors):
     return out
 
 
+def cifdet_hr_device(det, stride, v_threshold, neighbors):
+    """det (n, K, 7, H, W) device tensor -> (n, K, H', pitch) device tensor (pp_cifdet_hr)."""
+    n, k, _, h, w = det.shape
+    hh, _, pitch = hr_geometry(h, w, stride)
+    lib = load()
+    out = torch.empty((n, k, hh, pitch), dtype=torch.float32, device=det.device)
+    ws = torch.empty(lib.pp_cifhr_workspace_size(n, k, h, w), dtype=torch.uint8,
+                     device=det.device)
+    cfg = make_config(cif_threshold=v_threshold, stride=stride, cif_neighbors=neighbors)
+    call('pp_cifdet_hr', _device.ptr(det), n, k, h, w, ctypes.byref(cfg), _device.ptr(out),
+         _device.ptr(ws), ctypes.c_size_t(ws.numel()), _device.stream())
+    return out
+
+
 class CifHr:
     neighbors = 16
     v_threshold = 0.1
@@ -67,3 +81,31 @@ class CifHr:
     def fill(self, fields):
         cif_i, _, stride = self.config.single_scale()
         return self.fill_cif(fields[cif_i], stride)
+
+
+class CifDetHr(CifHr):
+    """cif_hr.py:84-100: detection fields (K, 7, H, W), sigma = max(1, 0.1 min(w, h) stride)."""
+
+    def accumulate(self, len_cifs, t, p, stride, min_scale):
+        p = p[:, p[0] > self.v_threshold]
+        if min_scale:
+            p = p[:, p[4] > min_scale / stride]
+            p = p[:, p[5] > min_scale / stride]
+        v, x, y, _, w, h, _ = p
+        x = x * stride
+        y = y * stride
+        sigma = np.maximum(1.0, 0.1 * np.minimum(w, h) * stride)
+        scalar_square_add_gauss_with_max(t, x, y, sigma, v / self.neighbors / len_cifs,
+                                         truncate=1.0)
+
+    def fill_cif(self, cif, stride, min_scale=0.0):
+        if min_scale:
+            raise NotImplementedError('min_scale masks (multi-scale) are not implemented')
+        if self.accumulated is not None:
+            raise NotImplementedError('accumulating several CifDet heads is not implemented')
+        hr = cifdet_hr_device(batch1(cif), int(stride), self.v_threshold, self.neighbors)
+        ww = (cif.shape[3] - 1) * int(stride) + 1
+        acc = hr[0, :, :, :ww]
+        self.accumulated = acc if _device.is_device(cif) else np.ascontiguousarray(
+            acc.cpu().numpy())
+        return self

@@ -49,3 +49,28 @@ class CifSeeds:
     def fill(self, fields):
         cif_i, _, stride = self.config.single_scale()
         return self.fill_cif(fields[cif_i], stride, seed_mask=self.config.seed_mask)
+
+
+class CifDetSeeds(CifSeeds):
+    """cif_seeds.py:67-90: (v, field, x, y, w, h) seeds of detection fields."""
+
+    def fill_cif(self, cif, stride, *, min_scale=0.0, seed_mask=None):
+        if self.threshold is None:
+            raise TypeError("'>' not supported between instances of 'float' and 'NoneType' "
+                            "(CifSeeds.threshold is not configured)")
+        if min_scale or seed_mask is not None:
+            raise NotImplementedError('min_scale / seed_mask are not implemented')
+        c = batch1(cif)
+        _, k, _, h, w = c.shape
+        hr = pitched_hr(self.cifhr)
+        seg = torch.empty((k, 5, h * w), dtype=torch.float32, device=c.device)
+        counts = torch.zeros(k, dtype=torch.int32, device=c.device)
+        cfg = make_config(seed_threshold=self.threshold, seed_score_scale=self.score_scale,
+                          stride=int(stride))
+        call('pp_cifdet_seeds', _device.ptr(c), _device.ptr(hr), 1, k, h, w, cfg_ptr(cfg),
+             _device.ptr(seg), _device.ptr(counts), _device.stream())
+        seg, counts = seg.cpu().numpy(), counts.cpu().numpy()
+        for f in range(k):  # emission order: fields in order, cells in row-major order
+            n = int(counts[f])
+            self.seeds.extend((v, f, x, y, ww, hh) for v, x, y, ww, hh in zip(*seg[f, :, :n]))
+        return self

@@ -1,0 +1,89 @@
+"""CifDet (decoder/generator/cifdet.py:17-52) on gfx950.
+
+Same constructor and call signature as the reference.  One call runs CifDetHr, CifDetSeeds,
+the occupancy loop and nms.Detection on the device for one image (`__call__`) or a whole
+batch (`decode_batch`), configured from the CifHr / CifSeeds / nms.Detection class
+attributes as the reference's decoder.configure() sets them.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from ... import _device
+from ..._abi import DET_DTYPE, DetNms, make_config
+from ..._lib import PPError, call, load
+from ...annotation import AnnotationDet
+from .. import nms
+from ..cif_hr import CifHr
+from ..cif_seeds import CifSeeds
+from ..field_config import FieldConfig
+from .generator import Generator
+
+PP_ST_ANN_OVERFLOW = 1
+
+
+def det_nms_config(cls=None):
+    cls = cls or nms.Detection
+    return DetNms(cls.suppression, cls.suppression_soft, cls.instance_threshold,
+                  cls.iou_threshold, cls.iou_threshold_soft, 1)
+
+
+class CifDet(Generator):
+    occupancy_visualizer = None
+
+    def __init__(self, field_config: FieldConfig, categories, *, worker_pool=None):
+        super().__init__(worker_pool)
+        self.field_config = field_config
+        self.categories = categories
+        self._ws = None
+
+    def config(self):
+        if CifSeeds.threshold is None:
+            raise TypeError("'>' not supported between instances of 'float' and 'NoneType' "
+                            "(CifSeeds.threshold is not configured)")
+        _, _, stride = self.field_config.single_scale()
+        return make_config(cif_threshold=CifHr.v_threshold, seed_threshold=CifSeeds.threshold,
+                           seed_score_scale=CifSeeds.score_scale, stride=int(stride),
+                           cif_neighbors=CifHr.neighbors)
+
+    def decode_records(self, det_batch, cap=None):
+        """det_batch (B, K, 7, H, W) -> (pp_det records, per-image offsets)."""
+        det = _device.to_device(det_batch)
+        if det.dim() != 5 or det.shape[2] != 7:
+            raise ValueError('expected CifDet fields (B, K, 7, H, W)')
+        b, k, _, h, w = det.shape
+        cfg = self.config()
+        z = det_nms_config()
+        cap = cap or max(64, h * w)
+        while True:
+            size = int(load().pp_cifdet_workspace_size(b, k, h, w, ctypes.byref(cfg), cap))
+            if self._ws is None or self._ws.numel() < size:
+                self._ws = torch.empty(size, dtype=torch.uint8, device=det.device)
+            out = torch.empty((b, cap, DET_DTYPE.itemsize), dtype=torch.uint8, device=det.device)
+            counts = torch.empty(b, dtype=torch.int32, device=det.device)
+            status = torch.empty(b, dtype=torch.int32, device=det.device)
+            call('pp_cifdet_decode', _device.ptr(det), b, k, h, w, ctypes.byref(cfg),
+                 ctypes.byref(z), _device.ptr(None), _device.ptr(out), cap, _device.ptr(counts),
+                 _device.ptr(status), _device.ptr(self._ws), ctypes.c_size_t(self._ws.numel()),
+                 _device.stream())
+            st = status.cpu().numpy()
+            if not (st & PP_ST_ANN_OVERFLOW).any():
+                break
+            if cap >= k * h * w:
+                raise PPError('CifDet: detection capacity overflow')
+            cap = min(k * h * w, 2 * cap)
+        counts = counts.cpu().numpy().astype(np.int64)
+        offsets = np.concatenate([[0], np.cumsum(counts)])
+        host = out.cpu().numpy()
+        recs = np.concatenate([host[i, :counts[i]].reshape(-1) for i in range(b)])
+        return np.frombuffer(recs.tobytes(), dtype=DET_DTYPE), offsets
+
+    def decode_batch(self, det_batch):
+        recs, offsets = self.decode_records(det_batch)
+        return [[AnnotationDet.from_record(r, self.categories)
+                 for r in recs[offsets[i]:offsets[i + 1]]] for i in range(len(offsets) - 1)]
+
+    def __call__(self, fields):
+        cif_i, _, _ = self.field_config.single_scale()
+        return self.decode_batch(_device.to_device(fields[cif_i])[None])[0]

@@ -1,4 +1,4 @@
-"""Keypoint NMS (nms.py:11-57).
+"""Keypoint and detection NMS (nms.py:11-102).
 
 Inside the device decode the suppression runs after the seed loop and force-complete
 (csrc/grow.hip, nms_kernel), configured from these class attributes exactly as the
@@ -12,7 +12,7 @@ import numpy as np
 import torch
 
 from .. import _device
-from .._abi import ANN_DTYPE, make_config
+from .._abi import ANN_DTYPE, DET_DTYPE, DetNms, make_config
 from .._lib import call, load
 from ..annotation import NOTSET
 
@@ -64,4 +64,64 @@ class Keypoints:
         order = d_out_index[:m].cpu().numpy()
         for i, ann in enumerate(anns):  # the reference edits ann.data in place
             ann.data[:] = mutated['data'][i, :k]
+        return [anns[int(i)] for i in order]
+
+
+class Detection:
+    """nms.py:60-102.  `annotations(anns)` runs pp_nms_detection on a host list of
+    AnnotationDet (scores and order as the reference; scores edited in place)."""
+    suppression = 0.1
+    suppression_soft = 0.3
+    instance_threshold = 0.1
+    iou_threshold = 0.7
+    iou_threshold_soft = 0.5
+
+    @staticmethod
+    def bbox_iou(box, other_boxes):
+        """nms.py:67-77 (host arrays, as the reference)."""
+        box = np.expand_dims(box, 0)
+        x1 = np.maximum(box[:, 0], other_boxes[:, 0])
+        y1 = np.maximum(box[:, 1], other_boxes[:, 1])
+        x2 = np.minimum(box[:, 0] + box[:, 2], other_boxes[:, 0] + other_boxes[:, 2])
+        y2 = np.minimum(box[:, 1] + box[:, 3], other_boxes[:, 1] + other_boxes[:, 3])
+        inter_area = np.maximum(0.0, x2 - x1) * np.maximum(0.0, y2 - y1)
+        box_area = box[:, 2] * box[:, 3]
+        other_areas = other_boxes[:, 2] * other_boxes[:, 3]
+        return inter_area / (box_area + other_areas - inter_area + 1e-5)
+
+    def config(self):
+        return DetNms(self.suppression, self.suppression_soft, self.instance_threshold,
+                      self.iou_threshold, self.iou_threshold_soft, 1)
+
+    def annotations(self, anns):
+        if not anns:
+            return anns
+        n = len(anns)
+        recs = np.zeros(n, DET_DTYPE)
+        for i, a in enumerate(anns):
+            recs[i]['field'] = a.field_i
+            recs[i]['score'] = a.score
+            recs[i]['bbox'] = np.asarray(a.bbox, dtype=np.float32)
+        dev = _device.require()
+        w = DET_DTYPE.itemsize
+        d_in = torch.from_numpy(recs.view(np.uint8).reshape(n, w)).to(dev)
+        d_out = torch.empty_like(d_in)
+        d_counts = torch.tensor([n], dtype=torch.int32, device=dev)
+        d_out_counts = torch.empty(1, dtype=torch.int32, device=dev)
+        d_out_index = torch.empty(n, dtype=torch.int32, device=dev)
+        ws = torch.empty(int(load().pp_nms_detection_workspace_size(1, n)), dtype=torch.uint8,
+                         device=dev)
+        z = self.config()
+        call('pp_nms_detection', _device.ptr(d_in), _device.ptr(d_counts), 1, n,
+             ctypes.byref(z), _device.ptr(d_out), _device.ptr(d_out_counts),
+             _device.ptr(d_out_index), _device.ptr(ws), ctypes.c_size_t(ws.numel()),
+             _device.stream())
+        m = int(d_out_counts.cpu().item())
+        order = d_out_index[:m].cpu().numpy()
+        # the reference edits every annotation's score in place: the kernel's candidate
+        # scratch (workspace head, 10 floats per input, score at 7) holds them all
+        scores = ws[:n * 40].view(torch.float32).reshape(n, 10)[:, 7].cpu().numpy()
+        for ann, sc in zip(anns, scores):
+            if ann.score >= self.instance_threshold:
+                ann.score = np.float32(sc)
         return [anns[int(i)] for i in order]

@@ -401,6 +401,35 @@ DET_CASES = [
 ]
 
 
+def gen_det_nms(op):
+    """nms.Detection().annotations on random overlapping boxes (nms.py:79-102)."""
+    from openpifpaf.annotation import AnnotationDet  # pylint: disable=import-outside-toplevel
+    from openpifpaf.decoder import nms  # pylint: disable=import-outside-toplevel
+    out = {}
+    for name, n, spread, seed in (('few', 12, 40.0, 0), ('many', 400, 300.0, 1),
+                                  ('ties', 60, 20.0, 2)):
+        rng = np.random.default_rng(200 + seed)
+        xy = rng.uniform(0.0, spread, (n, 2)).astype(np.float32)
+        wh = rng.uniform(4.0, 60.0, (n, 2)).astype(np.float32)
+        scores = rng.uniform(0.0, 1.0, n).astype(np.float32)
+        if name == 'ties':
+            scores = np.round(scores * 4) / 4  # many equal scores: stable-sort ties
+            scores = scores.astype(np.float32)
+        fields = rng.integers(0, 3, n)
+        anns = [AnnotationDet(['a', 'b', 'c']).set(int(f), np.float32(s),
+                                                   (xy[i, 0], xy[i, 1], wh[i, 0], wh[i, 1]))
+                for i, (f, s) in enumerate(zip(fields, scores))]
+        ids = {id(a): i for i, a in enumerate(anns)}
+        res = nms.Detection().annotations(list(anns))
+        out[name + '_field'] = fields.astype(np.int64)
+        out[name + '_score_in'] = scores
+        out[name + '_bbox'] = np.concatenate([xy, wh], axis=1)
+        out[name + '_order'] = np.array([ids[id(a)] for a in res], np.int64)
+        out[name + '_score_out'] = np.array([a.score for a in anns], np.float32)
+        print('det nms', name, n, '->', len(res))
+    np.savez_compressed(os.path.join(HERE, 'det_nms.npz'), **out)
+
+
 def gen_det(op):
     """The reference CifDet decoder on synthetic detection fields."""
     from openpifpaf.decoder import CifDet, CifDetHr, FieldConfig  # pylint: disable=import-outside-toplevel
@@ -450,12 +479,14 @@ def main():
         return
     if only == ['det']:
         gen_det(op)
+        gen_det_nms(op)
         return
     gen_primitives(op)
     gen_errors()
     gen_nms(op)
     gen_heads(op)
     gen_det(op)
+    gen_det_nms(op)
     for case in CASES:
         if only and case[0] not in only:
             continue

@@ -99,3 +99,24 @@ def test_no_oracle_in_product():
             if f.endswith(('.py', '.hip', '.hpp', '.cpp')):
                 text = open(os.path.join(root, f)).read()
                 assert 'oracle' not in text.replace('Oracle', '').lower() or f == 'build.py', f
+
+
+def test_det_struct_layout_matches_header(tmp_path):
+    src = tmp_path / 'det_layout.c'
+    src.write_text('''
+#include <stdio.h>
+#include <stddef.h>
+#include "pifpaf_amd.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(pp_det), offsetof(pp_det, score),
+         offsetof(pp_det, bbox), offsetof(pp_det, image), sizeof(pp_det_nms),
+         offsetof(pp_det_nms, apply));
+  return 0;
+}
+''')
+    exe = tmp_path / 'det_layout'
+    subprocess.check_call(['gcc', '-I', os.path.dirname(HEADER), str(src), '-o', str(exe)])
+    vals = [int(v) for v in subprocess.check_output([str(exe)]).split()]
+    d = _abi.DET_DTYPE
+    assert vals == [d.itemsize, d.fields['score'][1], d.fields['bbox'][1], d.fields['image'][1],
+                    ctypes.sizeof(_abi.DetNms), _abi.DetNms.apply.offset]

@@ -448,3 +448,74 @@ def test_ingest_large_batch():
     assert got.shape == (8, 17, 5, 81, 81)
     ulp = np.abs(got.view(np.int32).astype(np.int64) - ref.view(np.int32).astype(np.int64))
     assert ulp.max() <= 1
+
+
+# ---- CifDet (decoder/generator/cifdet.py) -----------------------------------------------------
+
+DET_NAMES = sorted(os.path.basename(p)[4:-4] for p in
+                   __import__('glob').glob(os.path.join(gu.GOLDEN, 'det_*.npz'))
+                   if not p.endswith('det_nms.npz'))
+
+
+def _det_case(dec, name):
+    from openpifpaf_amd import synthetic
+    g = np.load(os.path.join(gu.GOLDEN, 'det_%s.npz' % name))
+    det = synthetic.det_batch(str(g['gen']), 1, int(g['h']), int(g['w']), first_seed=int(g['seed']),
+                              n_categories=int(g['n_categories']))[0]
+    assert gu.sha(det) == str(g['input_sha'])
+    dec.CifHr.v_threshold = 0.1
+    dec.CifSeeds.threshold = float(g['seed_threshold'])
+    return g, det
+
+
+@pytest.mark.parametrize('name', DET_NAMES)
+def test_cifdet_stages_vs_reference(dec, name):
+    g, det = _det_case(dec, name)
+    fc = dec.FieldConfig()
+    hr = dec.CifDetHr(fc).fill([det]).accumulated
+    assert gu.sha(hr) == str(g['cifhr_sha'])
+    seeds = dec.CifDetSeeds(hr, fc).fill([det]).get()
+    rows = np.array([[float(t) for t in sd] for sd in seeds], np.float32).reshape(-1, 6)
+    assert np.array_equal(rows, g['seeds'])
+
+
+@pytest.mark.parametrize('name', DET_NAMES)
+def test_cifdet_vs_reference(dec, name):
+    g, det = _det_case(dec, name)
+    k = int(g['n_categories'])
+    anns = dec.CifDet(dec.FieldConfig(), ['c%d' % i for i in range(k)])([det])
+    assert [a.field_i for a in anns] == g['ann_field'].tolist()
+    assert np.array_equal(np.array([a.score for a in anns], np.float32), g['ann_score'])
+    assert np.array_equal(np.array([a.bbox for a in anns], np.float32).reshape(-1, 4),
+                          g['ann_bbox'])
+
+
+@pytest.mark.parametrize('kind', ['planted', 'uniform'])
+def test_cifdet_batch_vs_oracle(dec, kind):
+    from openpifpaf_amd import synthetic
+    from openpifpaf_amd._abi import make_config
+    dec.CifHr.v_threshold = 0.1
+    dec.CifSeeds.threshold = 0.3 if kind == 'planted' else 0.1
+    det = synthetic.det_batch(kind, 24, 48, 40, first_seed=50, n_categories=4)
+    cd = dec.CifDet(dec.FieldConfig(), ['a', 'b', 'c', 'd'])
+    recs, offsets = cd.decode_records(det)
+    cfg = make_config(seed_threshold=dec.CifSeeds.threshold)
+    for i in range(len(det)):
+        ref = oracle.cifdet_decode(det[i], cfg)
+        got = recs[offsets[i]:offsets[i + 1]]
+        assert len(got) == len(ref), i
+        assert np.array_equal(got['field'], ref['field']), i
+        assert np.array_equal(got['score'], ref['score']), i
+        assert np.array_equal(got['bbox'], ref['bbox']), i
+
+
+@pytest.mark.parametrize('name', ['few', 'many', 'ties'])
+def test_nms_detection_vs_reference(dec, name):
+    from openpifpaf_amd.annotation import AnnotationDet
+    g = np.load(os.path.join(gu.GOLDEN, 'det_nms.npz'))
+    anns = [AnnotationDet(['a', 'b', 'c']).set(int(f), np.float32(s), b)
+            for f, s, b in zip(g[name + '_field'], g[name + '_score_in'], g[name + '_bbox'])]
+    ids = {id(a): i for i, a in enumerate(anns)}
+    res = dec.nms.Detection().annotations(list(anns))
+    assert [ids[id(a)] for a in res] == g[name + '_order'].tolist()
+    assert np.array_equal(np.array([a.score for a in anns], np.float32), g[name + '_score_out'])
