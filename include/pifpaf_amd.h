@@ -119,6 +119,20 @@ typedef struct pp_det_nms {
     int32_t apply;            /* 1 */
 } pp_det_nms;
 
+/* The meta of one image that Preprocess.annotations_inverse reads
+ * (transforms/annotations.py:39-44): offset and scale float64, width_height[0], hflip,
+ * rotation angle / width / height */
+typedef struct pp_inverse_meta {
+    double offset[2];
+    double scale[2];
+    double rotation_angle;
+    double rotation_width;
+    double rotation_height;
+    double width;
+    int32_t hflip;
+    int32_t pad_;
+} pp_inverse_meta;
+
 /* per-image status bits written by pp_decode_batch (d_status) */
 #define PP_ST_ANN_OVERFLOW 1   /* more annotations than ann_capacity               */
 #define PP_ST_NMS_OVERFLOW 2   /* NMS occupancy larger than the occupancy workspace */
@@ -219,6 +233,21 @@ int pp_cifdet_decode(const float *d_det, int32_t n_img, int32_t K, int32_t H, in
                      const pp_config *cfg, const pp_det_nms *nms, float *d_cifhr, pp_det *d_out,
                      int32_t det_capacity, int32_t *d_counts, int32_t *d_status,
                      void *d_workspace, size_t workspace_bytes, void *stream);
+
+/*
+ * Preprocess.annotations_inverse (transforms/preprocess.py:35-95) on device records, one
+ * meta per image (d_metas (n_img) device array):
+ *   pp_annotations_inverse  poses: rotation, offset, scale (data, joint_scales,
+ *                           decoding_order), hflip with the optional horizontal swap
+ *                           d_hswap (K) = target row of each source row (hflip.py:17-29);
+ *                           d_nan_flags[i] |= 1 where the reference's NaN assert fires
+ *   pp_dets_inverse         boxes: rotate_box (transforms/utils.py:5-28), offset, scale
+ */
+int pp_annotations_inverse(pp_ann *d_anns, const int32_t *d_counts, int32_t n_img,
+                           int32_t capacity, int32_t K, const pp_inverse_meta *d_metas,
+                           const int32_t *d_hswap, int32_t *d_nan_flags, void *stream);
+int pp_dets_inverse(pp_det *d_dets, const int32_t *d_counts, int32_t n_img, int32_t capacity,
+                    const pp_inverse_meta *d_metas, void *stream);
 
 /*
  * Field ingestion: the raw output of a CompositeFieldFused head's conv (network/heads.py:

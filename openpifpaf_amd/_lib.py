@@ -58,6 +58,8 @@ _SIGNATURES = {
     'pp_nms_workspace_size': ([_i32, _i32], _sz),
     'pp_fields_dim': ([_i64, _i32], _i64),
     'pp_default_det_nms': ([_vp], None),
+    'pp_annotations_inverse': ([_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp], ctypes.c_int),
+    'pp_dets_inverse': ([_vp, _vp, _i32, _i32, _vp, _vp], ctypes.c_int),
     'pp_cifdet_hr': ([_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _sz, _vp], ctypes.c_int),
     'pp_cifdet_seeds': ([_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp], ctypes.c_int),
     'pp_nms_detection_workspace_size': ([_i32, _i32], _sz),

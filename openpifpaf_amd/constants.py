@@ -50,3 +50,16 @@ COCO_UPRIGHT_POSE = np.array([
     [1.75, 4.2], [-1.26, 4.0], [1.26, 4.0], [-1.4, 2.0], [1.4, 2.1],
     [-1.4, 0.0], [1.4, 0.1],
 ], dtype=np.float64)
+
+
+# datasets/constants.py: left / right keypoint pairs swapped by a horizontal flip
+HFLIP = {
+    'left_eye': 'right_eye', 'right_eye': 'left_eye',
+    'left_ear': 'right_ear', 'right_ear': 'left_ear',
+    'left_shoulder': 'right_shoulder', 'right_shoulder': 'left_shoulder',
+    'left_elbow': 'right_elbow', 'right_elbow': 'left_elbow',
+    'left_wrist': 'right_wrist', 'right_wrist': 'left_wrist',
+    'left_hip': 'right_hip', 'right_hip': 'left_hip',
+    'left_knee': 'right_knee', 'right_knee': 'left_knee',
+    'left_ankle': 'right_ankle', 'right_ankle': 'left_ankle',
+}

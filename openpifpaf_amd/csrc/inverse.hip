@@ -1,0 +1,153 @@
+// inverse.hip — Preprocess.annotations_inverse (transforms/preprocess.py:35-95) on decoded
+// records: image-space poses and boxes from network-input coordinates, one thread per
+// record, batched over images (each image has its own meta).
+//
+// NumPy semantics, step by step: the meta's offset / scale are float64 arrays and
+// width_height an int64 array (transforms/annotations.py:39-44), so those in-place steps
+// on the float32 records compute in float64 and round to float32; the rotation mixes
+// float32 arrays with Python floats, so it runs in float32 with the constants rounded.
+#include "pp_common.hpp"
+
+#include <math.h>
+
+namespace pp {
+
+__device__ __forceinline__ float npmin3(float a, float b) { return (a != a || b != b) ? NAN : (a < b ? a : b); }
+__device__ __forceinline__ float npmax3(float a, float b) { return (a != a || b != b) ? NAN : (a > b ? a : b); }
+
+__global__ __launch_bounds__(256) void ann_inverse_kernel(pp_ann *anns, const int *counts, int cap,
+                                                          int K, const pp_inverse_meta *metas,
+                                                          const int *hswap, int *nan_flags) {
+    const int img = blockIdx.y;
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= min(counts[img], cap)) return;
+    pp_ann &a = anns[(int64_t)img * cap + r];
+    const pp_inverse_meta m = metas[img];
+    const double angle = -m.rotation_angle;
+    if (angle != 0.0) {  // preprocess.py:51-56, float32 with the Python floats rounded
+        const float c = (float)cos(angle / 180.0 * M_PI), s = (float)sin(angle / 180.0 * M_PI);
+        const float hw = (float)((m.rotation_width - 1.0) / 2.0);
+        const float hh = (float)((m.rotation_height - 1.0) / 2.0);
+        for (int j = 0; j < K; j++) {
+            const float xo = a.data[j][0] - hw, yo = a.data[j][1] - hh;
+            a.data[j][0] = (hw + c * xo) + s * yo;
+            a.data[j][1] = (hh - s * xo) + c * yo;
+        }
+    }
+    bool nan = false;
+    for (int j = 0; j < K; j++) {  // offset, then scale (float64, rounded to float32)
+        float x = (float)((double)a.data[j][0] + m.offset[0]);
+        float y = (float)((double)a.data[j][1] + m.offset[1]);
+        x = (float)((double)x / m.scale[0]);
+        y = (float)((double)y / m.scale[1]);
+        a.data[j][0] = x;
+        a.data[j][1] = y;
+        a.joint_scales[j] = (float)((double)a.joint_scales[j] / m.scale[0]);
+        nan = nan || x != x || y != y || a.data[j][2] != a.data[j][2];
+    }
+    if (nan) atomicOr(&nan_flags[img], 1);  // the reference asserts here (preprocess.py:67)
+    if (m.hflip) {
+        for (int j = 0; j < K; j++)
+            a.data[j][0] = (float)(-(double)a.data[j][0] + (m.width - 1.0));
+        if (hswap) {  // _HorizontalSwap (hflip.py:17-29): target rows, last writer wins
+            float t[PP_MAX_KP][3];
+            for (int j = 0; j < K; j++) t[j][0] = t[j][1] = t[j][2] = 0.0f;
+            for (int sj = 0; sj < K; sj++) {
+                const int tj = hswap[sj];
+                t[tj][0] = a.data[sj][0];
+                t[tj][1] = a.data[sj][1];
+                t[tj][2] = a.data[sj][2];
+            }
+            for (int j = 0; j < K; j++) {
+                a.data[j][0] = t[j][0];
+                a.data[j][1] = t[j][1];
+                a.data[j][2] = t[j][2];
+            }
+        }
+    }
+    const int nd = min(a.n_decoding, PP_MAX_KP);
+    for (int d = 0; d < nd; d++) {  // decoding_order: offset and scale only (preprocess.py:76-81)
+        for (int c = 0; c < 2; c++) {
+            for (int h = 0; h < 2; h++) {
+                float v = (float)((double)a.decoding_xyv[d][3 * h + c] + m.offset[c]);
+                a.decoding_xyv[d][3 * h + c] = (float)((double)v / m.scale[c]);
+            }
+        }
+    }
+}
+
+// anndet_inverse (preprocess.py:84-95) with utils.rotate_box (transforms/utils.py:5-28)
+__global__ __launch_bounds__(256) void det_inverse_kernel(pp_det *dets, const int *counts, int cap,
+                                                          const pp_inverse_meta *metas) {
+    const int img = blockIdx.y;
+    const int r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= min(counts[img], cap)) return;
+    pp_det &d = dets[(int64_t)img * cap + r];
+    const pp_inverse_meta m = metas[img];
+    const double angle = -m.rotation_angle;
+    float b[4] = {d.bbox[0], d.bbox[1], d.bbox[2], d.bbox[3]};
+    if (angle != 0.0) {
+        const float c = (float)cos(angle / 180.0 * M_PI), s = (float)sin(angle / 180.0 * M_PI);
+        const float w2 = (float)((m.rotation_width - 1.0) / 2.0);
+        const float h2 = (float)((m.rotation_height - 1.0) / 2.0);
+        const float cx[4] = {b[0], b[0] + b[2], b[0], b[0] + b[2]};
+        const float cy[4] = {b[1], b[1], b[1] + b[3], b[1] + b[3]};
+        float rx[4], ry[4];
+        for (int i = 0; i < 4; i++) {
+            const float xo = cx[i] - w2, yo = cy[i] - h2;
+            rx[i] = (w2 + c * xo) + s * yo;
+            ry[i] = (h2 - s * xo) + c * yo;
+        }
+        float x = rx[0], y = ry[0], xm = rx[0], ym = ry[0];
+        for (int i = 1; i < 4; i++) {
+            x = npmin3(x, rx[i]);
+            y = npmin3(y, ry[i]);
+            xm = npmax3(xm, rx[i]);
+            ym = npmax3(ym, ry[i]);
+        }
+        b[0] = x;
+        b[1] = y;
+        b[2] = xm - x;
+        b[3] = ym - y;
+    }
+    b[0] = (float)((double)b[0] + m.offset[0]);
+    b[1] = (float)((double)b[1] + m.offset[1]);
+    b[0] = (float)((double)b[0] / m.scale[0]);
+    b[1] = (float)((double)b[1] / m.scale[1]);
+    b[2] = (float)((double)b[2] / m.scale[0]);
+    b[3] = (float)((double)b[3] / m.scale[1]);
+    for (int i = 0; i < 4; i++) d.bbox[i] = b[i];
+}
+
+}  // namespace pp
+
+using namespace pp;
+
+extern "C" {
+
+int pp_annotations_inverse(pp_ann *d_anns, const int32_t *d_counts, int32_t n_img,
+                           int32_t capacity, int32_t K, const pp_inverse_meta *d_metas,
+                           const int32_t *d_hswap, int32_t *d_nan_flags, void *stream) {
+    if (!d_anns || !d_counts || !d_metas || !d_nan_flags)
+        return fail(PP_EINVAL, "pp_annotations_inverse: NULL argument");
+    if (n_img < 0 || capacity <= 0 || K <= 0 || K > PP_MAX_KP)
+        return fail(PP_ESHAPE, "pp_annotations_inverse: bad shape");
+    if (n_img == 0) return PP_OK;
+    const dim3 grid((unsigned)((capacity + 255) / 256), (unsigned)n_img);
+    hipLaunchKernelGGL(ann_inverse_kernel, grid, dim3(256), 0, (hipStream_t)stream, d_anns,
+                       d_counts, capacity, K, d_metas, d_hswap, d_nan_flags);
+    return check_launch("pp_annotations_inverse");
+}
+
+int pp_dets_inverse(pp_det *d_dets, const int32_t *d_counts, int32_t n_img, int32_t capacity,
+                    const pp_inverse_meta *d_metas, void *stream) {
+    if (!d_dets || !d_counts || !d_metas) return fail(PP_EINVAL, "pp_dets_inverse: NULL argument");
+    if (n_img < 0 || capacity <= 0) return fail(PP_ESHAPE, "pp_dets_inverse: bad shape");
+    if (n_img == 0) return PP_OK;
+    const dim3 grid((unsigned)((capacity + 255) / 256), (unsigned)n_img);
+    hipLaunchKernelGGL(det_inverse_kernel, grid, dim3(256), 0, (hipStream_t)stream, d_dets,
+                       d_counts, capacity, d_metas);
+    return check_launch("pp_dets_inverse");
+}
+
+}  // extern "C"

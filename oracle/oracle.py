@@ -306,3 +306,40 @@ def cifdet_decode(det, cfg=None, nms=None):
     n = lib().orc_cifdet_decode(_p(det), _i(k), _i(h), _i(w), ctypes.byref(cfg),
                                 ctypes.byref(nms), out.ctypes.data_as(_vp), _l(cap))
     return out[:n]
+
+
+# ---- Preprocess.annotations_inverse (transforms/preprocess.py:35-95), numpy restatement ----
+
+def annotations_inverse(data, scales, dxyv, nd, meta, hswap=None):
+    """Poses (n, K, 3) / (n, K) / decoding xyv (n, T, 6) with nd[i] valid rows."""
+    data, scales, dxyv = data.copy(), scales.copy(), dxyv.copy()
+    off = np.asarray(meta['offset'], np.float64)
+    sc = np.asarray(meta['scale'], np.float64)
+    angle = -meta['rotation']['angle']
+    if angle != 0.0:
+        rw, rh = meta['rotation']['width'], meta['rotation']['height']
+        c = np.float32(np.cos(angle / 180.0 * np.pi))
+        s = np.float32(np.sin(angle / 180.0 * np.pi))
+        hw, hh = np.float32((rw - 1) / 2), np.float32((rh - 1) / 2)
+        xo, yo = data[:, :, 0] - hw, data[:, :, 1] - hh
+        data[:, :, 0] = (hw + c * xo) + s * yo
+        data[:, :, 1] = (hh - s * xo) + c * yo
+    data[:, :, 0] = (data[:, :, 0].astype(np.float64) + off[0]).astype(np.float32)
+    data[:, :, 1] = (data[:, :, 1].astype(np.float64) + off[1]).astype(np.float32)
+    data[:, :, 0] = (data[:, :, 0].astype(np.float64) / sc[0]).astype(np.float32)
+    data[:, :, 1] = (data[:, :, 1].astype(np.float64) / sc[1]).astype(np.float32)
+    scales = (scales.astype(np.float64) / sc[0]).astype(np.float32)
+    if meta['hflip']:
+        w = float(meta['width_height'][0])
+        data[:, :, 0] = (-data[:, :, 0].astype(np.float64) + (w - 1)).astype(np.float32)
+        if hswap is not None:
+            t = np.zeros_like(data)
+            for src, dst in enumerate(hswap):
+                t[:, dst] = data[:, src]
+            data = t
+    for i in range(len(dxyv)):
+        for col in (0, 1, 3, 4):
+            v = dxyv[i, :nd[i], col].astype(np.float64) + off[col % 3]
+            v = v.astype(np.float32).astype(np.float64) / sc[col % 3]
+            dxyv[i, :nd[i], col] = v.astype(np.float32)
+    return data, scales, dxyv

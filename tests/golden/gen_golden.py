@@ -14,6 +14,8 @@ Fixtures:
   errors.json          the reference's ValueError messages at the boundary
   det_<case>.npz       CifDet decoder (cifdet.py:27-52): CifDetHr digest + sums, the seed
                        list, and the AnnotationDet list (field, score, bbox)
+  inverse.npz          Preprocess.annotations_inverse + json_data on reference-decoded poses
+                       and detections under offset / scale, hflip + swap, rotation metas
   heads.npz            CompositeFieldFused (conv replaced by identity, eval mode) +
                        CifCafCollector / CifdetCollector on random conv outputs, quad 0-2
   nms.npz              nms.Keypoints().annotations on random overlapping Annotation lists
@@ -401,6 +403,67 @@ DET_CASES = [
 ]
 
 
+def inverse_metas(hswap):
+    base = {'offset': np.array((3.5, -2.25)), 'scale': np.array((0.5, 0.75)),
+            'rotation': {'angle': 0.0, 'width': None, 'height': None}, 'hflip': False,
+            'width_height': np.array((641, 427)), 'image_id': 7}
+    flip = dict(base, hflip=True, horizontal_swap=hswap)
+    rot = dict(base, rotation={'angle': 12.5, 'width': 481, 'height': 361},
+               offset=np.array((-1.0, 4.5)), scale=np.array((1.25, 0.8)))
+    return {'shift': base, 'flip': flip, 'rot': rot}
+
+
+def gen_inverse(op):
+    """Preprocess.annotations_inverse (preprocess.py:35-95) + json_data on decoded output."""
+    import json  # pylint: disable=import-outside-toplevel
+    from openpifpaf import transforms  # pylint: disable=import-outside-toplevel
+    from openpifpaf.decoder import CifCaf, CifDet, FieldConfig  # pylint: disable=import-outside-toplevel
+    from openpifpaf.decoder.cif_seeds import CifSeeds  # pylint: disable=import-outside-toplevel
+    from openpifpaf.datasets import constants as dc  # pylint: disable=import-outside-toplevel
+    from openpifpaf.transforms.hflip import _HorizontalSwap  # pylint: disable=import-outside-toplevel
+    kps, skel = constants.COCO_KEYPOINTS, constants.COCO_PERSON_SKELETON
+    metas = inverse_metas(_HorizontalSwap(kps, dc.HFLIP))
+    out = {}
+    cif, caf = make_inputs('planted', 40, 40, 0, skel, {})
+    decoder = __import__('openpifpaf').decoder
+    configure(decoder, 'eval', {})
+    anns = CifCaf(FieldConfig(), keypoints=kps, skeleton=skel)([cif, caf])
+    nd = max(len(a.decoding_order) for a in anns)
+    out['pose_data'] = np.stack([a.data for a in anns]).astype(np.float32)
+    out['pose_scales'] = np.stack([a.joint_scales for a in anns]).astype(np.float32)
+    dxyv = np.zeros((len(anns), nd, 6), np.float32)
+    dpairs = np.zeros((len(anns), nd, 2), np.int64)
+    for i, a in enumerate(anns):
+        for t, (j1, j2, c1, c2) in enumerate(a.decoding_order):
+            dxyv[i, t, :3], dxyv[i, t, 3:] = c1[:3], c2[:3]
+            dpairs[i, t] = (j1, j2)
+    out['pose_dxyv'] = dxyv
+    out['pose_dpairs'] = dpairs
+    out['pose_nd'] = np.array([len(a.decoding_order) for a in anns], np.int64)
+    CifSeeds.threshold = 0.5
+    det = synthetic.det_batch('planted', 1, 40, 40, first_seed=0, n_categories=3)[0]
+    dets = CifDet(FieldConfig(), ['c0', 'c1', 'c2'])([det])
+    CifSeeds.threshold = None
+    out['det_field'] = np.array([a.field_i for a in dets], np.int64)
+    out['det_score'] = np.array([a.score for a in dets], np.float32)
+    out['det_bbox'] = np.stack([a.bbox for a in dets]).astype(np.float32)
+    for name, meta in metas.items():
+        inv = transforms.Preprocess.annotations_inverse(anns, meta)
+        out[name + '_pose_data'] = np.stack([a.data for a in inv]).astype(np.float32)
+        out[name + '_pose_scales'] = np.stack([a.joint_scales for a in inv]).astype(np.float32)
+        o = np.zeros_like(dxyv)
+        for i, a in enumerate(inv):
+            for t, (_, __, c1, c2) in enumerate(a.decoding_order):
+                o[i, t, :3], o[i, t, 3:] = c1[:3], c2[:3]
+        out[name + '_pose_dxyv'] = o
+        out[name + '_pose_json'] = np.array(json.dumps([a.json_data() for a in inv]))
+        dinv = transforms.Preprocess.annotations_inverse(dets, meta)
+        out[name + '_det_bbox'] = np.stack([a.bbox for a in dinv]).astype(np.float32)
+        out[name + '_det_json'] = np.array(json.dumps([a.json_data() for a in dinv]))
+        print('inverse', name, len(inv), len(dinv))
+    np.savez_compressed(os.path.join(HERE, 'inverse.npz'), **out)
+
+
 def gen_det_nms(op):
     """nms.Detection().annotations on random overlapping boxes (nms.py:79-102)."""
     from openpifpaf.annotation import AnnotationDet  # pylint: disable=import-outside-toplevel
@@ -477,6 +540,9 @@ def main():
     if only == ['heads']:
         gen_heads(op)
         return
+    if only == ['inverse']:
+        gen_inverse(op)
+        return
     if only == ['det']:
         gen_det(op)
         gen_det_nms(op)
@@ -487,6 +553,7 @@ def main():
     gen_heads(op)
     gen_det(op)
     gen_det_nms(op)
+    gen_inverse(op)
     for case in CASES:
         if only and case[0] not in only:
             continue

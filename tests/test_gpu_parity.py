@@ -519,3 +519,42 @@ def test_nms_detection_vs_reference(dec, name):
     res = dec.nms.Detection().annotations(list(anns))
     assert [ids[id(a)] for a in res] == g[name + '_order'].tolist()
     assert np.array_equal(np.array([a.score for a in anns], np.float32), g[name + '_score_out'])
+
+
+
+# ---- Preprocess.annotations_inverse + json_data (transforms/preprocess.py, annotation.py) ----
+
+@pytest.mark.parametrize('name', ['shift', 'flip', 'rot'])
+def test_annotations_inverse_vs_reference(name):
+    import json
+    from test_oracle_golden import inverse_metas
+    from openpifpaf_amd import constants, eval_coco, transforms
+    from openpifpaf_amd.annotation import Annotation, AnnotationDet
+    g = np.load(os.path.join(gu.GOLDEN, 'inverse.npz'))
+    meta = inverse_metas()[name]
+    anns = []
+    for i in range(len(g['pose_data'])):
+        a = Annotation(constants.COCO_KEYPOINTS, constants.COCO_PERSON_SKELETON)
+        a.data = g['pose_data'][i].copy()
+        a.joint_scales = g['pose_scales'][i].copy()
+        a.decoding_order = [(int(j1), int(j2), g['pose_dxyv'][i, t, :3].copy(),
+                             g['pose_dxyv'][i, t, 3:].copy())
+                            for t, (j1, j2) in enumerate(g['pose_dpairs'][i][:g['pose_nd'][i]])]
+        anns.append(a)
+    inv = transforms.Preprocess.annotations_inverse(anns, meta)
+    assert np.array_equal(np.stack([a.data for a in inv]), g[name + '_pose_data'])
+    assert np.array_equal(np.stack([a.joint_scales for a in inv]), g[name + '_pose_scales'])
+    o = np.zeros_like(g['pose_dxyv'])
+    for i, a in enumerate(inv):
+        for t, (_, __, c1, c2) in enumerate(a.decoding_order):
+            o[i, t, :3], o[i, t, 3:] = c1[:3], c2[:3]
+    assert np.array_equal(o, g[name + '_pose_dxyv'])
+    assert json.dumps([a.json_data() for a in inv]) == str(g[name + '_pose_json'])
+    assert np.array_equal(np.stack([a.data for a in anns]), g['pose_data'])  # inputs untouched
+    dets = [AnnotationDet(['c0', 'c1', 'c2']).set(int(f), np.float32(sc), b)
+            for f, sc, b in zip(g['det_field'], g['det_score'], g['det_bbox'])]
+    dinv = transforms.Preprocess.annotations_inverse(dets, meta)
+    assert np.array_equal(np.stack([a.bbox for a in dinv]), g[name + '_det_bbox'])
+    assert json.dumps([a.json_data() for a in dinv]) == str(g[name + '_det_json'])
+    recs = eval_coco.coco_predictions(anns, meta)
+    assert [r['image_id'] for r in recs] == [7] * len(anns)

@@ -195,3 +195,31 @@ def test_oracle_cifdet_vs_reference(name):
     assert anns['field'].tolist() == g['ann_field'].tolist()
     assert np.array_equal(anns['score'], g['ann_score'])
     assert np.array_equal(anns['bbox'], g['ann_bbox'])
+
+
+# ---- Preprocess.annotations_inverse ----------------------------------------------------------
+
+def inverse_metas():
+    from openpifpaf_amd import constants, transforms
+    base = {'offset': np.array((3.5, -2.25)), 'scale': np.array((0.5, 0.75)),
+            'rotation': {'angle': 0.0, 'width': None, 'height': None}, 'hflip': False,
+            'width_height': np.array((641, 427)), 'image_id': 7}
+    flip = dict(base, hflip=True,
+                horizontal_swap=transforms._HorizontalSwap(constants.COCO_KEYPOINTS,
+                                                           constants.HFLIP))
+    rot = dict(base, rotation={'angle': 12.5, 'width': 481, 'height': 361},
+               offset=np.array((-1.0, 4.5)), scale=np.array((1.25, 0.8)))
+    return {'shift': base, 'flip': flip, 'rot': rot}
+
+
+@pytest.mark.parametrize('name', ['shift', 'flip', 'rot'])
+def test_oracle_inverse_vs_reference(name):
+    from openpifpaf_amd import transforms
+    g = np.load(os.path.join(gu.GOLDEN, 'inverse.npz'))
+    meta = inverse_metas()[name]
+    hswap = transforms.swap_table(meta['horizontal_swap'], 17) if meta['hflip'] else None
+    data, scales, dxyv = oracle.annotations_inverse(g['pose_data'], g['pose_scales'],
+                                                    g['pose_dxyv'], g['pose_nd'], meta, hswap)
+    assert np.array_equal(data, g[name + '_pose_data'])
+    assert np.array_equal(scales, g[name + '_pose_scales'])
+    assert np.array_equal(dxyv, g[name + '_pose_dxyv'])
