@@ -133,6 +133,18 @@ typedef struct pp_inverse_meta {
     int32_t pad_;
 } pp_inverse_meta;
 
+/* One scale of a multi-scale decode: the FieldConfig entries of one CIF / CAF head
+ * (field_config.py:7-13, factory.py:153-180).  0 for a min scale / distance means unused
+ * (the reference tests them for truthiness). */
+typedef struct pp_scale {
+    const float *cif;        /* (n_img, K, 5, H, W) */
+    const float *caf;        /* (n_img, C, 9, H, W) */
+    int32_t H, W, stride;
+    float cif_min_scale;     /* cif_min_scales[i] */
+    float caf_min_distance;  /* caf_min_distances[i] */
+    float caf_max_distance;  /* caf_max_distances[i] (None -> 0) */
+} pp_scale;
+
 /* per-image status bits written by pp_decode_batch (d_status) */
 #define PP_ST_ANN_OVERFLOW 1   /* more annotations than ann_capacity               */
 #define PP_ST_NMS_OVERFLOW 2   /* NMS occupancy larger than the occupancy workspace */

@@ -101,3 +101,12 @@ class DetNms(ctypes.Structure):
     _fields_ = [('suppression', ctypes.c_float), ('suppression_soft', ctypes.c_float),
                 ('instance_threshold', ctypes.c_float), ('iou_threshold', ctypes.c_float),
                 ('iou_threshold_soft', ctypes.c_float), ('apply', ctypes.c_int32)]
+
+
+class Scale(ctypes.Structure):
+    """pp_scale: one CIF / CAF head of a multi-scale FieldConfig (field_config.py:7-13).
+    0.0 for a min scale / distance means unused (the reference tests them for truthiness)."""
+    _fields_ = [('cif', ctypes.c_void_p), ('caf', ctypes.c_void_p), ('H', ctypes.c_int32),
+                ('W', ctypes.c_int32), ('stride', ctypes.c_int32),
+                ('cif_min_scale', ctypes.c_float), ('caf_min_distance', ctypes.c_float),
+                ('caf_max_distance', ctypes.c_float)]

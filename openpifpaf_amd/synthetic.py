@@ -54,6 +54,109 @@ def _patch_cells(px, py, h, w):
     return xs, ys
 
 
+def _plant_person(cif, caf, kps, scale, skeleton, rng):
+    """4x4 CIF patches at the joints kps (17, 2) and one 4x4 CAF patch per limb midpoint
+    (field-cell units), confidences 0.7-1.0."""
+    h, w = cif.shape[2:]
+    for j in range(17):
+        xs, ys = _patch_cells(kps[j, 0], kps[j, 1], h, w)
+        conf = rng.uniform(0.7, 1.0, (len(ys), len(xs))).astype(np.float32)
+        if conf.size == 0:
+            continue
+        sub = cif[j, :, ys[0]:ys[-1] + 1, xs[0]:xs[-1] + 1]
+        m = conf > sub[0]
+        sub[0][m] = conf[m]
+        sub[1][m] = kps[j, 0]
+        sub[2][m] = kps[j, 1]
+        sub[3][m] = 0.5
+        sub[4][m] = scale
+
+    for e, (j1, j2) in enumerate(skeleton):
+        a = kps[j1 - 1]
+        b = kps[j2 - 1]
+        mid = 0.5 * (a + b)
+        xs, ys = _patch_cells(mid[0], mid[1], h, w)
+        conf = rng.uniform(0.7, 1.0, (len(ys), len(xs))).astype(np.float32)
+        if conf.size == 0:
+            continue
+        sub = caf[e, :, ys[0]:ys[-1] + 1, xs[0]:xs[-1] + 1]
+        m = conf > sub[0]
+        sub[0][m] = conf[m]
+        sub[1][m] = a[0]
+        sub[2][m] = a[1]
+        sub[3][m] = 0.5
+        sub[4][m] = scale
+        sub[5][m] = b[0]
+        sub[6][m] = b[1]
+        sub[7][m] = 0.5
+        sub[8][m] = scale
+
+
+def _background(h, w, n_caf, rng, noise):
+    g = _grid(h, w)
+    cif = np.zeros((17, 5, h, w), dtype=np.float32)
+    cif[:, 0] = rng.uniform(0.0, noise, (17, h, w))
+    cif[:, 1:3] = g + rng.uniform(-0.5, 0.5, (17, 2, h, w))
+    cif[:, 3] = 0.5
+    cif[:, 4] = 1.0
+    caf = np.zeros((n_caf, 9, h, w), dtype=np.float32)
+    caf[:, 0] = rng.uniform(0.0, noise, (n_caf, h, w))
+    caf[:, 1:3] = g
+    caf[:, 5:7] = g + 4.0 * rng.uniform(-0.5, 0.5, (n_caf, 2, h, w))
+    caf[:, 3] = 0.5
+    caf[:, 4] = 1.0
+    caf[:, 7] = 0.5
+    caf[:, 8] = 1.0
+    return cif, caf
+
+
+def planted_multi(h_px, w_px, strides, n_people=4, seed=0, skeleton=None, noise=0.08):
+    """The same people seen at several strides (multi-scale heads): a list of (cif, caf),
+    one per stride, with fields of (h_px - 1) // stride + 1 rows."""
+    if skeleton is None:
+        skeleton = COCO_PERSON_SKELETON
+    rng = np.random.default_rng(seed)
+    people = []
+    for _ in range(n_people):
+        u = rng.uniform(8.0, 28.0)  # pixels per pose unit
+        cx = rng.uniform(0.15 * w_px, 0.85 * w_px)
+        cy = rng.uniform(0.15 * h_px, 0.85 * h_px)
+        kps = np.stack([cx + u * COCO_UPRIGHT_POSE[:, 0],
+                        cy - u * (COCO_UPRIGHT_POSE[:, 1] - 5.0)], axis=1)
+        people.append((kps + rng.normal(0.0, 2.0, (17, 2)), 3.2 * u))
+    out = []
+    for si, stride in enumerate(strides):
+        h, w = (h_px - 1) // stride + 1, (w_px - 1) // stride + 1
+        srng = np.random.default_rng(seed * 1000 + si)
+        cif, caf = _background(h, w, len(skeleton), srng, noise)
+        for kps, scale_px in people:
+            _plant_person(cif, caf, kps / stride, scale_px / stride, skeleton, srng)
+        out.append((cif, caf))
+    return out
+
+
+# multi-scale FieldConfigs (factory.py:153-180): strides per head, cif min scales,
+# caf min / max distances.  'ms10' has 10 heads: CifHr pairs i with i + 5 (cif_hr.py:63).
+MULTI_CASES = {
+    'ms2': ([8, 16], [0.0, 12.0], [0.0, 36.0], [160.0, None]),
+    'ms10': ([8, 16, 8, 16, 8] * 2, [0.0, 12.0, 16.0, 24.0, 40.0] * 2,
+             [0.0, 36.0, 48.0, 72.0, 120.0] * 2, [160.0, 240.0, 320.0, 480.0, None] * 2),
+}
+
+
+def multi_case(name, seed=0, h_px=321, w_px=321, n_people=4):
+    """fields list [cif_0, caf_0, cif_1, caf_1, ...] and the FieldConfig kwargs of a case."""
+    strides, mins, dmin, dmax = MULTI_CASES[name]
+    fields = []
+    for cif, caf in planted_multi(h_px, w_px, strides, n_people=n_people, seed=seed):
+        fields += [cif, caf]
+    n = len(strides)
+    kw = dict(cif_indices=[2 * i for i in range(n)], caf_indices=[2 * i + 1 for i in range(n)],
+              cif_strides=list(strides), caf_strides=list(strides), cif_min_scales=list(mins),
+              caf_min_distances=list(dmin), caf_max_distances=list(dmax))
+    return fields, kw
+
+
 def planted(h, w, n_people=8, seed=0, skeleton=None, noise=0.08):
     if skeleton is None:
         skeleton = COCO_PERSON_SKELETON
@@ -84,40 +187,7 @@ def planted(h, w, n_people=8, seed=0, skeleton=None, noise=0.08):
             cx + u * COCO_UPRIGHT_POSE[:, 0],
             cy - u * (COCO_UPRIGHT_POSE[:, 1] - 5.0),
         ], axis=1) + rng.normal(0.0, 0.3, (17, 2))
-        scale = 0.4 * u
-
-        for j in range(17):
-            xs, ys = _patch_cells(kps[j, 0], kps[j, 1], h, w)
-            conf = rng.uniform(0.7, 1.0, (len(ys), len(xs))).astype(np.float32)
-            if conf.size == 0:
-                continue
-            sub = cif[j, :, ys[0]:ys[-1] + 1, xs[0]:xs[-1] + 1]
-            m = conf > sub[0]
-            sub[0][m] = conf[m]
-            sub[1][m] = kps[j, 0]
-            sub[2][m] = kps[j, 1]
-            sub[3][m] = 0.5
-            sub[4][m] = scale
-
-        for e, (j1, j2) in enumerate(skeleton):
-            a = kps[j1 - 1]
-            b = kps[j2 - 1]
-            mid = 0.5 * (a + b)
-            xs, ys = _patch_cells(mid[0], mid[1], h, w)
-            conf = rng.uniform(0.7, 1.0, (len(ys), len(xs))).astype(np.float32)
-            if conf.size == 0:
-                continue
-            sub = caf[e, :, ys[0]:ys[-1] + 1, xs[0]:xs[-1] + 1]
-            m = conf > sub[0]
-            sub[0][m] = conf[m]
-            sub[1][m] = a[0]
-            sub[2][m] = a[1]
-            sub[3][m] = 0.5
-            sub[4][m] = scale
-            sub[5][m] = b[0]
-            sub[6][m] = b[1]
-            sub[7][m] = 0.5
-            sub[8][m] = scale
+        _plant_person(cif, caf, kps, 0.4 * u, skeleton, rng)
 
     return cif, caf
 

@@ -10,7 +10,7 @@ import subprocess
 
 import numpy as np
 
-from openpifpaf_amd._abi import ANN_DTYPE, SEED_DTYPE, make_config, skeleton_array
+from openpifpaf_amd._abi import ANN_DTYPE, SEED_DTYPE, Scale, make_config, skeleton_array
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
@@ -41,6 +41,8 @@ def lib():
         _LIB.orc_nms_keypoints.restype = ctypes.c_long
         _LIB.orc_cifdet_seeds.restype = ctypes.c_long
         _LIB.orc_cifdet_decode.restype = ctypes.c_long
+        _LIB.orc_seeds_multi.restype = ctypes.c_long
+        _LIB.orc_decode_multi.restype = ctypes.c_long
         assert _LIB.orc_sizeof_ann() == ANN_DTYPE.itemsize
     return _LIB
 
@@ -109,6 +111,86 @@ def decode(cif, caf, skeleton, cfg=None):
         out = np.zeros(cap, ANN_DTYPE)
         n = lib().orc_decode(_p(cif), _p(caf), _i(k), _i(c), _i(h), _i(w), _p(skel),
                              ctypes.byref(cfg), _p(out), _l(cap))
+        if n < 0:
+            raise ValueError('oracle decode rejected the shapes')
+        if n <= cap:
+            return out[:n]
+        cap = int(n)
+
+
+class Members:
+    """The heads of a multi-scale FieldConfig for the oracle: fields list + FieldConfig
+    lists (cif_indices, caf_indices, strides, cif_min_scales, caf min / max distances)."""
+
+    def __init__(self, fields, *, cif_indices, caf_indices, cif_strides, cif_min_scales=None,
+                 caf_min_distances=None, caf_max_distances=None, **_):
+        n = len(cif_indices)
+        assert len(caf_indices) == n
+        self.cifs = [_c32(fields[i]) for i in cif_indices]
+        self.cafs = [_c32(fields[i]) for i in caf_indices]
+        self.arr = (Scale * n)()
+        for m in range(n):
+            cif, caf = self.cifs[m], self.cafs[m]
+            assert cif.shape[-2:] == caf.shape[-2:]
+            self.arr[m] = Scale(cif.ctypes.data, caf.ctypes.data, cif.shape[-2], cif.shape[-1],
+                                int(cif_strides[m]),
+                                float((cif_min_scales or [0.0] * n)[m] or 0.0),
+                                float((caf_min_distances or [0.0] * n)[m] or 0.0),
+                                float((caf_max_distances or [None] * n)[m] or 0.0))
+        self.n = n
+        self.pairs = int(n == 10)  # cif_hr.py:63
+        self.k = self.cifs[0].shape[0]
+        self.c = self.cafs[0].shape[0]
+        self.hr_shape = (self.k,) + hr_shape(self.cifs[0].shape[-2], self.cifs[0].shape[-1],
+                                             int(cif_strides[0]))
+
+
+def cifhr_multi(members, cfg=None):
+    cfg = cfg or make_config()
+    out = np.empty(members.hr_shape, np.float32)
+    lib().orc_cifhr_multi(members.arr, _i(members.n), _i(members.pairs), _i(members.k),
+                          ctypes.byref(cfg), _p(out))
+    return out
+
+
+def seeds_multi(members, hr, cfg=None):
+    cfg = cfg or make_config()
+    hr = _c32(hr)
+    cap = sum(c.shape[0] * c.shape[2] * c.shape[3] for c in members.cifs)
+    out = np.empty(max(cap, 1), SEED_DTYPE)
+    n = lib().orc_seeds_multi(members.arr, _i(members.n), _i(members.k), _p(hr),
+                              _l(hr.shape[1]), _l(hr.shape[2]), ctypes.byref(cfg), _p(out),
+                              _l(cap))
+    return out[:n]
+
+
+def caf_scored_multi(members, hr, skeleton, score_th, cfg=None):
+    """(forward, backward) lists of (9, N_i) arrays, every head's columns concatenated."""
+    cfg = cfg or make_config()
+    hr = _c32(hr)
+    skel = skeleton_array(skeleton)
+    cap = sum(c.shape[2] * c.shape[3] for c in members.cafs)
+    c = members.c
+    cols = np.zeros((c, 2, 9, cap), np.float32)
+    counts = np.zeros((c, 2), np.int32)
+    lib().orc_caf_scored_multi(members.arr, _i(members.n), _i(hr.shape[0]), _i(c), _p(hr),
+                               _l(hr.shape[1]), _l(hr.shape[2]), _p(skel), _f(score_th),
+                               ctypes.byref(cfg), _p(cols), _l(cap), _p(counts))
+    forward = [cols[i, 1, :, :counts[i, 1]].copy() for i in range(c)]
+    backward = [cols[i, 0, :, :counts[i, 0]].copy() for i in range(c)]
+    return forward, backward
+
+
+def decode_multi(members, skeleton, cfg=None):
+    """One image, CifCaf.__call__ over a multi-scale FieldConfig -> pp_ann records."""
+    cfg = cfg or make_config()
+    skel = skeleton_array(skeleton)
+    cap = 64
+    while True:
+        out = np.zeros(cap, ANN_DTYPE)
+        n = lib().orc_decode_multi(members.arr, _i(members.n), _i(members.pairs),
+                                   _i(members.k), _i(members.c), _p(skel), ctypes.byref(cfg),
+                                   _p(out), _l(cap))
         if n < 0:
             raise ValueError('oracle decode rejected the shapes')
         if n <= cap:

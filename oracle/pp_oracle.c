@@ -1000,6 +1000,9 @@ EXPORT long orc_nms_keypoints(pp_ann *anns, long n, int K, const pp_config *cfg)
     return nms_keypoints(&d, anns, (int)n);
 }
 
+EXPORT long orc_decode_multi(const pp_scale *sc, int n, int pairs, int K, int C,
+                             const int32_t *skel, const pp_config *cfg, pp_ann *out, long cap);
+
 static void ann_init(pp_ann *a, int K) {
     memset(a, 0, sizeof(*a));
     a->n_keypoints = K;
@@ -1009,40 +1012,221 @@ static void ann_init(pp_ann *a, int K) {
  * <= cap). */
 EXPORT long orc_decode(const float *cif, const float *caf, int K, int C, int H, int W,
                        const int32_t *skel, const pp_config *cfg, pp_ann *out, long cap) {
-    if (K > PP_MAX_KP || C > PP_MAX_EDGES || K <= 0 || C <= 0 || H <= 0 || W <= 0) return -1;
-    long hh = hr_dim(H, cfg->stride), ww = hr_dim(W, cfg->stride);
-    long hw = (long)H * W;
+    pp_scale sc;
+    memset(&sc, 0, sizeof(sc));
+    sc.cif = cif;
+    sc.caf = caf;
+    sc.H = H;
+    sc.W = W;
+    sc.stride = cfg->stride;
+    return orc_decode_multi(&sc, 1, 0, K, C, skel, cfg, out, cap);
+}
+
+/* ---- multi-scale (cif_hr.py:42-73, cif_seeds.py:56-64, caf_scored.py:32-98) ----------- */
+
+/* CifHr.fill: with pairs (10 CIF heads) heads i and i + 5 accumulate into one map with
+ * len_cifs = 2 at head i's stride / min scale; otherwise every head on its own.  Maps
+ * combine by np.maximum in order.  out (K, H', W') from head 0's field size and stride. */
+EXPORT void orc_cifhr_multi(const pp_scale *sc, int n, int pairs, int K, const pp_config *cfg,
+                            float *out) {
+    long hh = hr_dim(sc[0].H, sc[0].stride), ww = hr_dim(sc[0].W, sc[0].stride);
+    size_t plane = (size_t)hh * ww;
+    float *ta = (float *)malloc(sizeof(float) * K * plane);
+    int n_groups = pairs ? n / 2 : n;
+    for (int gi = 0; gi < n_groups; gi++) {
+        int members[2] = {gi, pairs ? gi + n / 2 : -1};
+        int len = pairs ? 2 : 1;
+        float stride = (float)sc[gi].stride;
+        float min_scale = sc[gi].cif_min_scale;
+        memset(ta, 0, sizeof(float) * K * plane);
+        for (int mi = 0; mi < len; mi++) {
+            const pp_scale *m = &sc[members[mi]];
+            long hw = (long)m->H * m->W;
+            float *xs = (float *)malloc(sizeof(float) * 4 * (size_t)(hw + 1));
+            float *ys = xs + hw, *ss = ys + hw, *vs = ss + hw;
+            for (int f = 0; f < K; f++) {
+                const float *p = m->cif + (size_t)f * 5 * hw;
+                long k = 0;
+                for (long c = 0; c < hw; c++) {
+                    if (!(p[c] > cfg->cif_threshold)) continue;
+                    if (min_scale != 0.0f && !(p[4 * hw + c] > (float)((double)min_scale / stride)))
+                        continue;
+                    xs[k] = p[1 * hw + c] * stride;
+                    ys[k] = p[2 * hw + c] * stride;
+                    float sg = (0.5f * p[4 * hw + c]) * stride;
+                    ss[k] = (sg != sg) ? sg : fmaxf(1.0f, sg);
+                    vs[k] = (p[c] / (float)cfg->cif_neighbors) / (float)len;
+                    k++;
+                }
+                orc_scalar_square_add_gauss_with_max(ta + f * plane, hh, ww, ww, 1, xs, ys, ss,
+                                                     vs, k, 1.0f, 1.0f);
+            }
+            free(xs);
+        }
+        if (gi == 0) {
+            memcpy(out, ta, sizeof(float) * K * plane);
+        } else {
+            for (size_t i = 0; i < K * plane; i++) { /* np.maximum(ta, accumulated) */
+                float a = ta[i], b = out[i];
+                out[i] = (a != a || b != b) ? NAN : (a > b ? a : b);
+            }
+        }
+    }
+    free(ta);
+}
+
+/* CifSeeds.fill over every CIF head in order; sorted as get() */
+EXPORT long orc_seeds_multi(const pp_scale *sc, int n, int K, const float *hr, long hh, long ww,
+                            const pp_config *cfg, pp_seed *out, long cap) {
+    long total = 0;
+    for (int m = 0; m < n; m++) total += (long)K * sc[m].H * sc[m].W;
+    float *tmp = (float *)malloc(sizeof(float) * 6 * (size_t)(total + 1));
+    long k = 0;
+    for (int m = 0; m < n; m++) {
+        long hw = (long)sc[m].H * sc[m].W;
+        float stride = (float)sc[m].stride;
+        for (int f = 0; f < K; f++) {
+            const float *p = sc[m].cif + (size_t)f * 5 * hw;
+            const float *t = hr + (size_t)f * hh * ww;
+            for (long c = 0; c < hw; c++) {
+                float conf = p[c];
+                if (!(conf > cfg->seed_threshold)) continue;
+                if (sc[m].cif_min_scale != 0.0f &&
+                    !(p[4 * hw + c] > (float)((double)sc[m].cif_min_scale / sc[m].stride)))
+                    continue;
+                float x = p[1 * hw + c] * stride, y = p[2 * hw + c] * stride, v;
+                orc_scalar_values(t, hh, ww, ww, 1, &x, &y, 1, 0.0f, &v);
+                v = 0.9f * v + 0.1f * conf;
+                if (cfg->seed_score_scale != 1.0f) v = v * cfg->seed_score_scale;
+                if (!(v > cfg->seed_threshold)) continue;
+                float *r = tmp + 6 * k;
+                r[0] = v;
+                r[1] = (float)f;
+                r[2] = x;
+                r[3] = y;
+                r[4] = p[4 * hw + c] * stride;
+                r[5] = (float)k;
+                k++;
+            }
+        }
+    }
+    qsort(tmp, (size_t)k, sizeof(float) * 6, seed_cmp_desc);
+    for (long i = 0; i < k && i < cap; i++) {
+        float *r = tmp + 6 * i;
+        out[i].v = r[0];
+        out[i].field = (int32_t)r[1];
+        out[i].x = r[2];
+        out[i].y = r[3];
+        out[i].s = r[4];
+    }
+    free(tmp);
+    return k;
+}
+
+/* CafScored.fill over every CAF head in order: per field the heads' columns concatenated.
+ * cols (C, 2, 9, cap) with cap >= sum of H*W over the heads */
+EXPORT void orc_caf_scored_multi(const pp_scale *sc, int n, int K, int C, const float *hr, long hh,
+                                 long ww, const int32_t *skel, float score_th, const pp_config *cfg,
+                                 float *cols, long cap, int32_t *counts) {
+    float floor_ = cfg->cif_floor;
+    float one_minus = (float)(1.0 - (double)cfg->cif_floor);
+    for (int i = 0; i < C; i++) {
+        float *bwd = cols + ((size_t)i * 2 + 0) * 9 * cap;
+        float *fwd = cols + ((size_t)i * 2 + 1) * 9 * cap;
+        int j1i = skel[2 * i] - 1, j2i = skel[2 * i + 1] - 1;
+        long nb = 0, nf = 0;
+        for (int m = 0; m < n; m++) {
+            long hw = (long)sc[m].H * sc[m].W;
+            float stride = (float)sc[m].stride;
+            const float *p = sc[m].caf + (size_t)i * 9 * hw;
+            float dmin = sc[m].caf_min_distance, dmax = sc[m].caf_max_distance;
+            float tmin = (float)((double)dmin / sc[m].stride), tmax = (float)((double)dmax / sc[m].stride);
+            for (long c = 0; c < hw; c++) {
+                float nine[9];
+                nine[0] = p[c];
+                if (!(nine[0] > score_th)) continue;
+                if (dmin != 0.0f || dmax != 0.0f) { /* np.linalg.norm(nine[1:3] - nine[5:7]) */
+                    float dx = p[1 * hw + c] - p[5 * hw + c], dy = p[2 * hw + c] - p[6 * hw + c];
+                    float dist = sqrtf(dx * dx + dy * dy);
+                    if (dmin != 0.0f && !(dist > tmin)) continue;
+                    if (dmax != 0.0f && !(dist < tmax)) continue;
+                }
+                for (int r = 1; r < 9; r++) nine[r] = p[r * hw + c] * stride;
+                float score = nine[0], sb = score, sf = score;
+                if (floor_ < 1.0f && j1i < K) {
+                    float h1;
+                    orc_scalar_values(hr + (size_t)j1i * hh * ww, hh, ww, ww, 1, &nine[1], &nine[2],
+                                      1, 0.0f, &h1);
+                    sb = score * (floor_ + one_minus * h1);
+                }
+                if (sb > score_th) {
+                    static const int order_b[9] = {0, 5, 6, 7, 8, 1, 2, 3, 4};
+                    for (int r = 0; r < 9; r++) bwd[r * cap + nb] = nine[order_b[r]];
+                    bwd[nb] = sb;
+                    nb++;
+                }
+                if (floor_ < 1.0f && j2i < K) {
+                    float h2;
+                    orc_scalar_values(hr + (size_t)j2i * hh * ww, hh, ww, ww, 1, &nine[5], &nine[6],
+                                      1, 0.0f, &h2);
+                    sf = score * (floor_ + one_minus * h2);
+                }
+                if (sf > score_th) {
+                    for (int r = 0; r < 9; r++) fwd[r * cap + nf] = nine[r];
+                    fwd[nf] = sf;
+                    nf++;
+                }
+            }
+        }
+        counts[2 * i + 0] = (int32_t)nb;
+        counts[2 * i + 1] = (int32_t)nf;
+    }
+}
+
+/* cifcaf.py:67-122 over a FieldConfig of n CIF / CAF heads (one image): CifHr, CifSeeds and
+ * CafScored fill from every head (the functions above), the rest as one scale. */
+EXPORT long orc_decode_multi(const pp_scale *sc, int n, int pairs, int K, int C,
+                             const int32_t *skel, const pp_config *cfg, pp_ann *out, long cap) {
+    if (K > PP_MAX_KP || C > PP_MAX_EDGES || K <= 0 || C <= 0 || n <= 0) return -1;
+    if (pairs && n != 10) return -1;
+    long total_hw = 0;
+    for (int m = 0; m < n; m++) {
+        if (sc[m].H <= 0 || sc[m].W <= 0 || sc[m].stride <= 0) return -1;
+        total_hw += (long)sc[m].H * sc[m].W;
+    }
+    long hh = hr_dim(sc[0].H, sc[0].stride), ww = hr_dim(sc[0].W, sc[0].stride);
     float *hr = (float *)malloc(sizeof(float) * (size_t)K * hh * ww);
-    orc_cifhr(cif, K, H, W, cfg, hr);
-    pp_seed *seeds = (pp_seed *)malloc(sizeof(pp_seed) * (size_t)(K * hw + 1));
-    long n_seeds = orc_seeds(cif, hr, ww, K, H, W, cfg, seeds, K * hw);
+    orc_cifhr_multi(sc, n, pairs, K, cfg, hr);
+    pp_seed *seeds = (pp_seed *)malloc(sizeof(pp_seed) * (size_t)(K * total_hw + 1));
+    long n_seeds = orc_seeds_multi(sc, n, K, hr, hh, ww, cfg, seeds, K * total_hw);
 
     dec_t d;
     d.K = K;
     d.C = C;
-    d.H = H;
-    d.W = W;
-    d.hw = hw;
+    d.H = sc[0].H;
+    d.W = sc[0].W;
+    d.hw = total_hw; /* column capacity of every (connection, direction) set */
     d.cfg = cfg;
     build_by_source(&d, skel);
-    float *cols = (float *)malloc(sizeof(float) * (size_t)C * 2 * 9 * hw);
+    float *cols = (float *)malloc(sizeof(float) * (size_t)C * 2 * 9 * total_hw);
     int32_t *counts = (int32_t *)malloc(sizeof(int32_t) * (size_t)C * 2);
-    orc_caf_scored(caf, hr, ww, K, C, H, W, skel, cfg->caf_threshold, cfg, cols, counts);
+    orc_caf_scored_multi(sc, n, K, C, hr, hh, ww, skel, cfg->caf_threshold, cfg, cols, total_hw,
+                         counts);
     d.cols = cols;
     d.counts = counts;
 
     occ_t o;
     occ_init(&o, K, hh, ww, cfg->occupancy_reduction, cfg->occupancy_min_scale);
-    long acap = 64, n = 0;
+    long acap = 64, na = 0;
     pp_ann *anns = (pp_ann *)malloc(sizeof(pp_ann) * (size_t)acap);
     for (long s = 0; s < n_seeds; s++) {
         const pp_seed *sd = &seeds[s];
         if (occ_get(&o, sd->field, sd->x, sd->y)) continue;
-        if (n == acap) {
+        if (na == acap) {
             acap *= 2;
             anns = (pp_ann *)realloc(anns, sizeof(pp_ann) * (size_t)acap);
         }
-        pp_ann *a = &anns[n++];
+        pp_ann *a = &anns[na++];
         ann_init(a, K);
         a->data[sd->field][0] = sd->x;
         a->data[sd->field][1] = sd->y;
@@ -1055,9 +1239,9 @@ EXPORT long orc_decode(const float *cif, const float *caf, int K, int C, int H, 
 
     if (cfg->force_complete) {
         /* cifcaf.py:333-351 */
-        orc_caf_scored(caf, hr, ww, K, C, H, W, skel, cfg->complete_caf_threshold, cfg, cols,
-                       counts);
-        for (long i = 0; i < n; i++) {
+        orc_caf_scored_multi(sc, n, K, C, hr, hh, ww, skel, cfg->complete_caf_threshold, cfg, cols,
+                             total_hw, counts);
+        for (long i = 0; i < na; i++) {
             pp_ann *a = &anns[i];
             int unfilled[PP_MAX_KP];
             for (int j = 0; j < K; j++) unfilled[j] = a->data[j][2] == 0.0f;
@@ -1070,8 +1254,8 @@ EXPORT long orc_decode(const float *cif, const float *caf, int K, int C, int H, 
             if (any0) flood_fill(&d, a);
         }
     }
-    if (cfg->apply_nms) n = nms_keypoints(&d, anns, (int)n);
-    for (long i = 0; i < n; i++) {
+    if (cfg->apply_nms) na = nms_keypoints(&d, anns, (int)na);
+    for (long i = 0; i < na; i++) {
         anns[i].score = ann_score(&anns[i], K);
         if (i < cap) out[i] = anns[i];
     }
@@ -1080,7 +1264,7 @@ EXPORT long orc_decode(const float *cif, const float *caf, int K, int C, int H, 
     free(counts);
     free(seeds);
     free(hr);
-    return n;
+    return na;
 }
 
 /* ---- CifDet (decoder/generator/cifdet.py:27-52) ---------------------------------------- */

@@ -16,6 +16,8 @@ Fixtures:
                        list, and the AnnotationDet list (field, score, bbox)
   inverse.npz          Preprocess.annotations_inverse + json_data on reference-decoded poses
                        and detections under offset / scale, hflip + swap, rotation metas
+  multi_<case>.npz     multi-scale FieldConfig decodes (cif_hr.py:59-73 pairs / maxima,
+                       per-scale seeds, CafScored masks and concatenation) on planted_multi
   heads.npz            CompositeFieldFused (conv replaced by identity, eval mode) +
                        CifCafCollector / CifdetCollector on random conv outputs, quad 0-2
   nms.npz              nms.Keypoints().annotations on random overlapping Annotation lists
@@ -102,6 +104,29 @@ def configure(decoder, mode, extra):
     decoder.nms.Keypoints.keypoint_threshold = c['nms_keypoint_threshold']
 
 
+def ann_arrays(anns, n_caf):
+    """Annotation list -> data, scales, score, decoding / frontier order arrays."""
+    out = {}
+    n = len(anns)
+    out['ann_data'] = np.array([a.data for a in anns], np.float32).reshape(n, 17, 3)
+    out['ann_joint_scales'] = np.array([a.joint_scales for a in anns], np.float32).reshape(n, 17)
+    out['ann_score'] = np.array([a.score() for a in anns], np.float64)
+    dec_pairs = np.full((n, 17, 2), -1, np.int16)
+    dec_xyv = np.zeros((n, 17, 6), np.float32)
+    fr = np.full((n, 4 * n_caf, 2), -1, np.int16)
+    for i, a in enumerate(anns):
+        for t, (j1, j2, x1, x2) in enumerate(a.decoding_order):
+            dec_pairs[i, t] = (j1, j2)
+            dec_xyv[i, t, :3] = x1
+            dec_xyv[i, t, 3:] = x2
+        for t, (j1, j2) in enumerate(a.frontier_order):
+            fr[i, t] = (j1, j2)
+    out['ann_decoding_pairs'] = dec_pairs
+    out['ann_decoding_xyv'] = dec_xyv
+    out['ann_frontier_pairs'] = fr
+    return out
+
+
 def run_case(op, name, gen, h, w, seed, mode, skel_name, extra):
     from openpifpaf import decoder  # pylint: disable=import-outside-toplevel
     skeleton = list(SKELETONS[skel_name])
@@ -146,23 +171,7 @@ def run_case(op, name, gen, h, w, seed, mode, skel_name, extra):
             out['caf_%s_fwd_cat' % tag] = np.concatenate(cs.forward, axis=1)
             out['caf_%s_bwd_cat' % tag] = np.concatenate(cs.backward, axis=1)
 
-    n = len(anns)
-    out['ann_data'] = np.array([a.data for a in anns], np.float32).reshape(n, 17, 3)
-    out['ann_joint_scales'] = np.array([a.joint_scales for a in anns], np.float32).reshape(n, 17)
-    out['ann_score'] = np.array([a.score() for a in anns], np.float64)
-    dec_pairs = np.full((n, 17, 2), -1, np.int16)
-    dec_xyv = np.zeros((n, 17, 6), np.float32)
-    fr = np.full((n, 4 * len(skeleton), 2), -1, np.int16)
-    for i, a in enumerate(anns):
-        for t, (j1, j2, x1, x2) in enumerate(a.decoding_order):
-            dec_pairs[i, t] = (j1, j2)
-            dec_xyv[i, t, :3] = x1
-            dec_xyv[i, t, 3:] = x2
-        for t, (j1, j2) in enumerate(a.frontier_order):
-            fr[i, t] = (j1, j2)
-    out['ann_decoding_pairs'] = dec_pairs
-    out['ann_decoding_xyv'] = dec_xyv
-    out['ann_frontier_pairs'] = fr
+    out.update(ann_arrays(anns, len(skeleton)))
     np.savez_compressed(os.path.join(HERE, 'decode_%s.npz' % name), **out)
     print('%-22s seeds %5d  caf_a %6d  caf_b %7d  anns %4d' % (
         name, len(seeds), out['caf_a_fwd_counts'].sum(), out['caf_b_fwd_counts'].sum(), n))
@@ -464,6 +473,38 @@ def gen_inverse(op):
     np.savez_compressed(os.path.join(HERE, 'inverse.npz'), **out)
 
 
+def gen_multi(op):
+    """Multi-scale decodes through the reference (factory.py:153-180 FieldConfig)."""
+    decoder = __import__('openpifpaf').decoder
+    from openpifpaf.decoder import CafScored, CifCaf, CifHr, CifSeeds, FieldConfig  # pylint: disable=import-outside-toplevel
+    kps, skel = constants.COCO_KEYPOINTS, constants.COCO_PERSON_SKELETON
+    for name in synthetic.MULTI_CASES:
+        for mode in ('eval', 'predict'):
+            fields, kw = synthetic.multi_case(name)
+            configure(decoder, mode, {})
+            fc = FieldConfig(**kw)
+            hr = CifHr(fc).fill(fields).accumulated
+            seeds = CifSeeds(hr, fc).fill(fields).get()
+            anns = CifCaf(fc, keypoints=kps, skeleton=skel)(fields)
+            out = {
+                'name': np.array(name), 'mode': np.array(mode),
+                'connection_method': np.array('blend'), 'greedy': 0,
+                'input_sha': np.array(sha(*fields)),
+                'cifhr_sha': np.array(sha(hr)), 'cifhr_shape': np.array(hr.shape),
+                'seeds': np.array([[float(t) for t in sd] for sd in seeds],
+                                  np.float32).reshape(-1, 5),
+            }
+            for tag, th in (('a', None), ('b', 0.0001)):
+                cs = CafScored(hr, fc, skel, score_th=th).fill(fields)
+                out['caf_%s_fwd_counts' % tag] = np.array([f.shape[1] for f in cs.forward])
+                out['caf_%s_bwd_counts' % tag] = np.array([b.shape[1] for b in cs.backward])
+                out['caf_%s_fwd_sha' % tag] = np.array([sha(f) for f in cs.forward])
+                out['caf_%s_bwd_sha' % tag] = np.array([sha(b) for b in cs.backward])
+            out.update(ann_arrays(anns, len(skel)))
+            np.savez_compressed(os.path.join(HERE, 'multi_%s_%s.npz' % (name, mode)), **out)
+            print('multi', name, mode, hr.shape, 'seeds', len(seeds), 'anns', len(anns))
+
+
 def gen_det_nms(op):
     """nms.Detection().annotations on random overlapping boxes (nms.py:79-102)."""
     from openpifpaf.annotation import AnnotationDet  # pylint: disable=import-outside-toplevel
@@ -543,6 +584,9 @@ def main():
     if only == ['inverse']:
         gen_inverse(op)
         return
+    if only == ['multi']:
+        gen_multi(op)
+        return
     if only == ['det']:
         gen_det(op)
         gen_det_nms(op)
@@ -554,6 +598,7 @@ def main():
     gen_det(op)
     gen_det_nms(op)
     gen_inverse(op)
+    gen_multi(op)
     for case in CASES:
         if only and case[0] not in only:
             continue
