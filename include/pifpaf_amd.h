@@ -36,6 +36,7 @@ extern "C" {
 #define PP_MAX_KP 24
 #define PP_MAX_EDGES 64
 #define PP_MAX_FRONTIER (4 * PP_MAX_EDGES)
+#define PP_MAX_SCALES 16   /* CIF / CAF heads of one multi-scale decode */
 
 typedef enum pp_status {
     PP_OK = 0,
@@ -133,16 +134,21 @@ typedef struct pp_inverse_meta {
     int32_t pad_;
 } pp_inverse_meta;
 
-/* One scale of a multi-scale decode: the FieldConfig entries of one CIF / CAF head
- * (field_config.py:7-13, factory.py:153-180).  0 for a min scale / distance means unused
- * (the reference tests them for truthiness). */
+/* One head of a multi-scale decode: FieldConfig entries (field_config.py:7-13,
+ * factory.py:153-180).  The entries with the PP_ROLE_CIF bit form the CIF head list
+ * (cif_indices order), those with PP_ROLE_CAF the CAF head list (caf_indices order); role 0
+ * means both (one stride shared by a CIF and a CAF head).  0 for a min scale / distance
+ * means unused (the reference tests them for truthiness). */
+#define PP_ROLE_CIF 1
+#define PP_ROLE_CAF 2
 typedef struct pp_scale {
-    const float *cif;        /* (n_img, K, 5, H, W) */
-    const float *caf;        /* (n_img, C, 9, H, W) */
+    const float *cif;        /* (n_img, K, 5, H, W) when a CIF head */
+    const float *caf;        /* (n_img, C, 9, H, W) when a CAF head */
     int32_t H, W, stride;
     float cif_min_scale;     /* cif_min_scales[i] */
     float caf_min_distance;  /* caf_min_distances[i] */
     float caf_max_distance;  /* caf_max_distances[i] (None -> 0) */
+    int32_t role;            /* PP_ROLE_* bits, 0 = both */
 } pp_scale;
 
 /* per-image status bits written by pp_decode_batch (d_status) */
@@ -210,6 +216,52 @@ int pp_decode_batch(const float *d_cif, const float *d_caf, int32_t n_img, int32
                     const pp_config *cfg, float *d_cifhr, pp_ann *d_anns,
                     int32_t ann_capacity, int32_t *d_counts, int32_t *d_status,
                     void *d_workspace, size_t workspace_bytes, void *stream);
+
+/*
+ * Multi-scale decode: the same stages over a FieldConfig of CIF and CAF heads
+ * (field_config.py:7-13; the heads' scale / min-distance lists of factory.py:153-180) given
+ * as n_scales pp_scale entries (see PP_ROLE_*), device arrays of each head's own size.
+ * cif_pairs != 0 is the reference's 10-head hflip layout (cif_hr.py:63-68): CifHr
+ * accumulates CIF heads g and g + n/2 into one map at head g's stride and min scale; the
+ * reference pairs exactly when len(cif_indices) == 10.  The CifHr map has CIF head 0's
+ * size: (n_img, K, H', pitch) with H' = (H_0 - 1) * stride_0 + 1.  cfg->stride is unused.
+ *   pp_cifhr_multi       CifHr.fill (cif_hr.py:59-73), maps combined by np.maximum
+ *   pp_seeds_multi       CifSeeds.fill over every CIF head (cif_seeds.py:56-64), sorted;
+ *                        seed_capacity >= K * (sum of the CIF heads' H * W)
+ *   pp_caf_scored_multi  CafScored.fill over every CAF head (caf_scored.py:88-98): per field
+ *                        the heads' columns concatenated; d_cols (n_img, C, 2, 9,
+ *                        col_capacity) with col_capacity >= the CAF heads' cells,
+ *                        d_counts (n_img, C, 2); the list must hold the CIF heads too
+ *                        (CIF head 0 gives the CifHr geometry; CIF fields are not read)
+ *   pp_decode_multi      CifCaf.__call__ (cifcaf.py:67-122) over the heads, `stages` as
+ *                        pp_decode_stages (15 = the full decode); outputs and status as
+ *                        pp_decode_batch, workspace contract as pp_decode_stages (zero
+ *                        region from pp_decode_multi_workspace_zero_offset).
+ */
+size_t pp_cifhr_multi_workspace_size(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs,
+                                     int32_t n_img, int32_t K);
+int pp_cifhr_multi(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs, int32_t n_img,
+                   int32_t K, const pp_config *cfg, float *d_cifhr, void *d_workspace,
+                   size_t workspace_bytes, void *stream);
+int pp_seeds_multi(const pp_scale *scales, int32_t n_scales, const float *d_cifhr, int32_t n_img,
+                   int32_t K, const pp_config *cfg, pp_seed *d_seeds, int32_t seed_capacity,
+                   int32_t *d_counts, void *stream);
+int pp_caf_scored_multi(const pp_scale *scales, int32_t n_scales, const float *d_cifhr,
+                        int32_t n_img, int32_t K, int32_t C, const int32_t *skeleton,
+                        float score_th, const pp_config *cfg, float *d_cols,
+                        int64_t col_capacity, int32_t *d_counts, void *stream);
+size_t pp_decode_multi_workspace_size(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs,
+                                      int32_t n_img, int32_t K, int32_t C, const pp_config *cfg,
+                                      int32_t ann_capacity);
+size_t pp_decode_multi_workspace_zero_offset(const pp_scale *scales, int32_t n_scales,
+                                             int32_t cif_pairs, int32_t n_img, int32_t K,
+                                             int32_t C, const pp_config *cfg,
+                                             int32_t ann_capacity);
+int pp_decode_multi(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs, int32_t n_img,
+                    int32_t K, int32_t C, const int32_t *skeleton, const pp_config *cfg,
+                    float *d_cifhr, pp_ann *d_anns, int32_t ann_capacity, int32_t *d_counts,
+                    int32_t *d_status, void *d_workspace, size_t workspace_bytes,
+                    uint32_t stages, void *stream);
 
 /*
  * CifDet detection decoder (decoder/generator/cifdet.py:27-52), batched:

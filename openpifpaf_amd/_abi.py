@@ -103,10 +103,31 @@ class DetNms(ctypes.Structure):
                 ('iou_threshold_soft', ctypes.c_float), ('apply', ctypes.c_int32)]
 
 
+ROLE_CIF, ROLE_CAF = 1, 2
+
+
 class Scale(ctypes.Structure):
-    """pp_scale: one CIF / CAF head of a multi-scale FieldConfig (field_config.py:7-13).
-    0.0 for a min scale / distance means unused (the reference tests them for truthiness)."""
+    """pp_scale: one head of a multi-scale FieldConfig (field_config.py:7-13).  role
+    ROLE_CIF / ROLE_CAF bits say which head list the entry joins (0 = both).  0.0 for a
+    min scale / distance means unused (the reference tests them for truthiness)."""
     _fields_ = [('cif', ctypes.c_void_p), ('caf', ctypes.c_void_p), ('H', ctypes.c_int32),
                 ('W', ctypes.c_int32), ('stride', ctypes.c_int32),
                 ('cif_min_scale', ctypes.c_float), ('caf_min_distance', ctypes.c_float),
-                ('caf_max_distance', ctypes.c_float)]
+                ('caf_max_distance', ctypes.c_float), ('role', ctypes.c_int32)]
+
+
+def scale_list(cifs, cafs, cif_strides, caf_strides, cif_min_scales=None,
+               caf_min_distances=None, caf_max_distances=None):
+    """pp_scale array of a FieldConfig: the CIF heads (role CIF) then the CAF heads (role
+    CAF).  cifs / cafs: (pointer, H, W) per head."""
+    nc, na = len(cifs), len(cafs)
+    arr = (Scale * (nc + na))()
+    for m, (ptr, h, w) in enumerate(cifs):
+        ms = (cif_min_scales or [0.0] * nc)[m] or 0.0
+        arr[m] = Scale(ptr, None, h, w, int(cif_strides[m]), float(ms), 0.0, 0.0, ROLE_CIF)
+    for m, (ptr, h, w) in enumerate(cafs):
+        dmin = (caf_min_distances or [0.0] * na)[m] or 0.0
+        dmax = (caf_max_distances or [None] * na)[m] or 0.0
+        arr[nc + m] = Scale(None, ptr, h, w, int(caf_strides[m]), 0.0, float(dmin),
+                            float(dmax), ROLE_CAF)
+    return arr

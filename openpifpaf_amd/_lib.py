@@ -40,6 +40,16 @@ _SIGNATURES = {
                          _vp, _vp, _sz, _vp], ctypes.c_int),
     'pp_decode_stages': ([_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp,
                           _vp, _vp, _sz, _u32, _vp], ctypes.c_int),
+    'pp_cifhr_multi_workspace_size': ([_vp, _i32, _i32, _i32, _i32], _sz),
+    'pp_cifhr_multi': ([_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _sz, _vp], ctypes.c_int),
+    'pp_seeds_multi': ([_vp, _i32, _vp, _i32, _i32, _vp, _vp, _i32, _vp, _vp], ctypes.c_int),
+    'pp_caf_scored_multi': ([_vp, _i32, _vp, _i32, _i32, _i32, _vp, _f, _vp, _vp, _i64, _vp,
+                             _vp], ctypes.c_int),
+    'pp_decode_multi_workspace_size': ([_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32], _sz),
+    'pp_decode_multi_workspace_zero_offset': ([_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32],
+                                              _sz),
+    'pp_decode_multi': ([_vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _vp,
+                         _vp, _sz, _u32, _vp], ctypes.c_int),
     'pp_scalar_square_add_gauss_with_max': ([_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _f,
                                              _f, _vp], ctypes.c_int),
     'pp_scalar_square_add_gauss': ([_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _f, _vp],

@@ -83,20 +83,21 @@ struct GrowArgs {
     const pp_seed *seeds;
     const int *seed_counts;
     int seed_cap;
-    const float *cols[2];     // bucketed column sets (n_img, C, 2, kColRows, H*W): set A at
-                              // caf_threshold, set B at complete_caf_threshold
+    const float *cols[2];     // bucketed column sets (n_img, C, 2, kColRows, col_cap): set A
+                              // at caf_threshold, set B at complete_caf_threshold
     const int *offs[2];       // bucket boundaries (n_img, C, 2, nb + 1)
-    // set B (force-complete, complete_caf_threshold) holds only cell indices (n_img, C, 2,
-    // H*W); its queries read the raw CAF and rescore with CifHr (consider_raw)
-    const float *caf;         // (n_img, C, 9, H, W) input
+    int64_t col_cap;          // columns per set: the cells of all heads
+    // set B (force-complete, complete_caf_threshold) holds only concatenated cell indices
+    // (n_img, C, 2, col_cap); its queries read the heads' raw CAF and rescore with CifHr
+    // (consider_raw)
+    Heads heads;
     const float *hr;          // (n_img, K, hh, hr_pitch) CifHr
     int64_t hr_pitch;
-    float stride_f, cif_floor, one_minus_floor, th_b;
+    float cif_floor, one_minus_floor, th_b;
     uint8_t caf_j1[PP_MAX_EDGES], caf_j2[PP_MAX_EDGES];  // 0-based joints of each CAF
     int bw, bh, nb;           // bucket grid (see caf_bucketed_kernel)
     float inv_e;
-    int K, C, H, W, hh, ww;
-    int64_t hw;
+    int K, C, hh, ww;
     pp_config cfg;
     // directed edges ("slots") in by_source order (cifcaf.py:62-65): joint j's entries
     // are slots j_off[j] .. j_off[j+1]-1 in dict insertion order
@@ -374,25 +375,35 @@ __device__ __forceinline__ void consider(const float *__restrict__ cf, int64_t h
     top2_insert(t, cand_key<MAXM>(score, o), tx, ty, tc);
 }
 
-// a set-B column: cell index -> raw CAF values (caf_scored.py:58-81 for this one column:
-// rows * stride, CifHr rescoring at the target, the second threshold), then as consider
+// a set-B column: concatenated cell index -> the head's raw CAF values (caf_scored.py:58-81
+// for this one column: rows * stride, CifHr rescoring at the target, the second
+// threshold), then as consider
 struct RawSet {
-    const int *idx;      // bucketed cell indices
-    const float *caf9;   // the field's 9 raw rows
+    const int *idx;      // bucketed concatenated cell indices
+    int64_t fld;         // image * C + CAF field
     const float *hrt;    // CifHr plane of the direction's target joint (rescore), or NULL
     int src, tgt, tsc;   // raw rows of source x, target x, target scale (y = x + 1)
 };
 
 template <bool MAXM>
-__device__ __forceinline__ void consider_raw(const GrowArgs &g, const RawSet &r, int64_t hw,
-                                             const ColQuery &q, int k, Top2 &t, int &m) {
-    const int cell = r.idx[k];
-    const float c = r.caf9[cell];
-    const float c1 = r.caf9[r.src * hw + cell] * g.stride_f;
-    const float c2 = r.caf9[(r.src + 1) * hw + cell] * g.stride_f;
-    const float tx = r.caf9[r.tgt * hw + cell] * g.stride_f;
-    const float ty = r.caf9[(r.tgt + 1) * hw + cell] * g.stride_f;
-    const float tc = r.caf9[r.tsc * hw + cell] * g.stride_f;
+__device__ __forceinline__ void consider_raw(const GrowArgs &g, const RawSet &r, const ColQuery &q,
+                                             int k, Top2 &t, int &m) {
+    const int key = r.idx[k];
+    const Heads &h = g.heads;
+    int hm = 0, cell = key;
+    if (h.n_caf > 1) {
+        hm = h.caf_head_of(key);
+        cell = key - (int)h.caf_off[hm];
+    }
+    const int64_t hw = (int64_t)h.aH[hm] * h.aW[hm];
+    const float stride = (float)h.astride[hm];
+    const float *caf9 = h.caf[hm] + r.fld * 9 * hw;
+    const float c = caf9[cell];
+    const float c1 = caf9[r.src * hw + cell] * stride;
+    const float c2 = caf9[(r.src + 1) * hw + cell] * stride;
+    const float tx = caf9[r.tgt * hw + cell] * stride;
+    const float ty = caf9[(r.tgt + 1) * hw + cell] * stride;
+    const float tc = caf9[r.tsc * hw + cell] * stride;
     if (c1 < q.lo_x || c1 > q.hi_x || c2 < q.lo_y || c2 > q.hi_y) return;
     float c0 = c;
     if (r.hrt)
@@ -403,7 +414,7 @@ __device__ __forceinline__ void consider_raw(const GrowArgs &g, const RawSet &r,
     const float qq = (-0.5f * (dd * dd)) / q.sigma2;
     const float score = (float)exp((double)qq) * c0;
     m++;
-    top2_insert(t, cand_key<MAXM>(score, cell), tx, ty, tc);
+    top2_insert(t, cand_key<MAXM>(score, key), tx, ty, tc);
 }
 
 // _target_with_blend / _target_with_maxscore (cifcaf.py:147-192) on the merged top-2
@@ -487,7 +498,7 @@ __device__ void grow_connection(const GrowArgs &g, const float *__restrict__ cf,
 #ifdef PP_STAMPS
     uint64_t gs_t = __builtin_amdgcn_s_memtime();
 #endif
-    const int64_t hw = g.hw;
+    const int64_t hw = g.col_cap;
     const ColQuery q = make_query(x, y, xy_scale);
     Top2 t = top2_empty();
     int m = 0;
@@ -534,7 +545,7 @@ __device__ void grow_connection(const GrowArgs &g, const float *__restrict__ cf,
             }
             if (k >= 0) {
                 if (RAW)
-                    consider_raw<MAXM>(g, raw, hw, q, k, t, m);
+                    consider_raw<MAXM>(g, raw, q, k, t, m);
                 else
                     consider<MAXM, true>(cf, hw, q, k, t, m);
             }
@@ -549,7 +560,7 @@ __device__ __forceinline__ float max0(float v) { return (v > 0.0f) ? v : 0.0f; }
 
 __device__ __forceinline__ const float *col_set(const GrowArgs &g, int set, int img, int caf_i,
                                                 int dir) {
-    return g.cols[set] + (((int64_t)img * g.C + caf_i) * 2 + dir) * (set ? 1 : kColRows) * g.hw;
+    return g.cols[set] + (((int64_t)img * g.C + caf_i) * 2 + dir) * (set ? 1 : kColRows) * g.col_cap;
 }
 
 // set B of (image, CAF, direction): dir 1 forward (x1, y1) -> (x2, y2, s2), rescored at
@@ -557,7 +568,7 @@ __device__ __forceinline__ const float *col_set(const GrowArgs &g, int set, int 
 __device__ __forceinline__ RawSet raw_set(const GrowArgs &g, int img, int caf_i, int dir) {
     RawSet r;
     r.idx = reinterpret_cast<const int *>(col_set(g, 1, img, caf_i, dir));
-    r.caf9 = g.caf + ((int64_t)img * g.C + caf_i) * 9 * g.hw;
+    r.fld = (int64_t)img * g.C + caf_i;
     const int tj = dir ? g.caf_j2[caf_i] : g.caf_j1[caf_i];
     r.hrt = (g.cif_floor < 1.0f && tj < g.K) ? g.hr + ((int64_t)img * g.K + tj) * g.hh * g.hr_pitch
                                               : nullptr;
@@ -1737,11 +1748,10 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
 // ---------------------------------------------------------------------------------------
 namespace pp {
 
-int launch_seeds(const float *cif, const float *hr, int n_img, int K, int H, int W,
-                 const pp_config *cfg, pp_seed *seeds, int cap, int *counts, void *scratch,
-                 hipStream_t s);
+int launch_seeds(const Heads &h, const float *hr, int n_img, int K, const pp_config *cfg,
+                 pp_seed *seeds, int cap, int *counts, void *scratch, hipStream_t s);
 size_t seeds_scratch_size(int n_img, int cap);
-int launch_caf_bucketed(const float *caf, const float *hr, int n_img, int K, int C, int H, int W,
+int launch_caf_bucketed(const Heads &h, const float *hr, int n_img, int K, int C,
                         const int32_t *skeleton, const pp_config *cfg, float th, float *cols,
                         int *offs, const int *gate, bool index_only, hipStream_t s);
 void caf_bucket_grid(int H, int W, int stride, int *bw, int *bh, int *nb, float *inv_e);
@@ -1761,14 +1771,15 @@ struct DecodeLayout {
     size_t cifhr_ws_bytes;
 };
 
-static DecodeLayout make_layout(int n_img, int K, int C, int H, int W, const pp_config *cfg,
+// CifHr map from head 0 (cif_hr.py:46-51); column sets and seeds over the cells of all heads
+static DecodeLayout make_layout(int n_img, int K, int C, const Heads &h, const pp_config *cfg,
                                 int ann_cap) {
     DecodeLayout d{};
-    d.hh = (int)hr_dim(H, cfg->stride);
-    d.ww = (int)hr_dim(W, cfg->stride);
+    d.hh = (int)hr_dim(h.cH[0], h.cstride[0]);
+    d.ww = (int)hr_dim(h.cW[0], h.cstride[0]);
     d.pitch = pp_cifhr_pitch(d.ww);
-    d.hw = (int64_t)H * W;
-    d.seed_cap = (int)(K * d.hw);  // every cell of every field: no seed overflow possible
+    d.hw = h.caf_cells();
+    d.seed_cap = (int)(K * h.cif_cells());  // every cell of every field: no seed overflow
     d.ann_cap = ann_cap;
     d.ann_np = 1;
     while (d.ann_np < ann_cap) d.ann_np <<= 1;
@@ -1784,12 +1795,12 @@ static DecodeLayout make_layout(int n_img, int K, int C, int H, int W, const pp_
     };
     const size_t n = (size_t)n_img;
     d.off_cifhr = take(n * K * d.hh * d.pitch * sizeof(float));
-    d.cifhr_ws_bytes = pp_cifhr_workspace_size(n_img, K, H, W);
+    d.cifhr_ws_bytes = cifhr_heads_workspace_size(h, n_img, K);
     d.off_cifhr_ws = take(d.cifhr_ws_bytes);
     d.off_seeds = take(n * d.seed_cap * sizeof(pp_seed));
     d.off_seed_counts = take(n * sizeof(int));
     d.off_seed_ws = take(seeds_scratch_size(n_img, d.seed_cap));
-    caf_bucket_grid(H, W, cfg->stride, &d.bw, &d.bh, &d.nb, &d.inv_e);
+    caf_bucket_grid(h.cH[0], h.cW[0], h.cstride[0], &d.bw, &d.bh, &d.nb, &d.inv_e);
     for (int t = 0; t < 2; t++) {
         const bool used = t == 0 || cfg->force_complete;
         d.off_cols[t] = take(used ? n * C * 2 * (t ? 1 : kColRows) * d.hw * sizeof(float) : 0);
@@ -1818,25 +1829,60 @@ extern "C" {
 
 size_t pp_decode_workspace_size(int32_t n_img, int32_t K, int32_t C, int32_t H, int32_t W,
                                 const pp_config *cfg, int32_t ann_capacity) {
-    if (!cfg || n_img < 0 || K <= 0 || C <= 0 || H <= 0 || W <= 0 || ann_capacity <= 0) return 0;
-    return make_layout(n_img, K, C, H, W, cfg, ann_capacity).total;
+    if (!cfg || n_img < 0 || K <= 0 || C <= 0 || H <= 0 || W <= 0 || ann_capacity <= 0 ||
+        cfg->stride <= 0)
+        return 0;
+    return make_layout(n_img, K, C, single_head(nullptr, nullptr, H, W, cfg->stride), cfg,
+                       ann_capacity).total;
 }
 
 size_t pp_decode_workspace_zero_offset(int32_t n_img, int32_t K, int32_t C, int32_t H, int32_t W,
                                        const pp_config *cfg, int32_t ann_capacity) {
-    if (!cfg || n_img <= 0 || K <= 0 || C <= 0 || H <= 0 || W <= 0 || ann_capacity <= 0) return 0;
-    return make_layout(n_img, K, C, H, W, cfg, ann_capacity).off_occ;
+    if (!cfg || n_img <= 0 || K <= 0 || C <= 0 || H <= 0 || W <= 0 || ann_capacity <= 0 ||
+        cfg->stride <= 0)
+        return 0;
+    return make_layout(n_img, K, C, single_head(nullptr, nullptr, H, W, cfg->stride), cfg,
+                       ann_capacity).off_occ;
 }
 
-int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int32_t K, int32_t C,
-                     int32_t H, int32_t W, const int32_t *skeleton, const pp_config *cfg,
-                     float *d_cifhr, pp_ann *d_anns, int32_t ann_capacity, int32_t *d_counts,
-                     int32_t *d_status, void *d_workspace, size_t workspace_bytes,
-                     uint32_t stages, void *stream) {
-    if (!d_cif || !d_caf || !skeleton || !cfg || !d_anns || !d_counts || !d_status || !d_workspace)
+size_t pp_decode_multi_workspace_size(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs,
+                                      int32_t n_img, int32_t K, int32_t C, const pp_config *cfg,
+                                      int32_t ann_capacity) {
+    Heads h;
+    if (!cfg || make_heads(scales, n_scales, cif_pairs, 3, &h, "pp_decode_multi_workspace_size") ||
+        n_img < 0 || K <= 0 || C <= 0 || ann_capacity <= 0)
+        return 0;
+    return make_layout(n_img, K, C, h, cfg, ann_capacity).total;
+}
+
+size_t pp_decode_multi_workspace_zero_offset(const pp_scale *scales, int32_t n_scales,
+                                             int32_t cif_pairs, int32_t n_img, int32_t K,
+                                             int32_t C, const pp_config *cfg,
+                                             int32_t ann_capacity) {
+    Heads h;
+    if (!cfg || make_heads(scales, n_scales, cif_pairs, 3, &h, "pp_decode_multi_workspace_zero_offset") ||
+        n_img <= 0 || K <= 0 || C <= 0 || ann_capacity <= 0)
+        return 0;
+    return make_layout(n_img, K, C, h, cfg, ann_capacity).off_occ;
+}
+
+}  // extern "C"
+
+namespace pp {
+
+static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
+                        const int32_t *skeleton, const pp_config *cfg, float *d_cifhr,
+                        pp_ann *d_anns, int32_t ann_capacity, int32_t *d_counts,
+                        int32_t *d_status, void *d_workspace, size_t workspace_bytes,
+                        uint32_t stages, void *stream) {
+    if (!skeleton || !cfg || !d_anns || !d_counts || !d_status || !d_workspace)
         return fail(PP_EINVAL, "pp_decode_batch: NULL argument");
-    if (n_img < 0 || K <= 0 || K > PP_MAX_KP || C <= 0 || C > PP_MAX_EDGES || H <= 0 || W <= 0 ||
-        ann_capacity <= 0 || cfg->stride <= 0 || cfg->occupancy_reduction <= 0)
+    for (int m = 0; m < h.n_cif; m++)
+        if (!h.cif[m]) return fail(PP_EINVAL, "pp_decode_batch: NULL CIF field");
+    for (int m = 0; m < h.n_caf; m++)
+        if (!h.caf[m]) return fail(PP_EINVAL, "pp_decode_batch: NULL CAF field");
+    if (n_img < 0 || K <= 0 || K > PP_MAX_KP || C <= 0 || C > PP_MAX_EDGES ||
+        ann_capacity <= 0 || cfg->occupancy_reduction <= 0)
         return fail(PP_ESHAPE, "pp_decode_batch: shape outside the supported envelope "
                                "(K <= PP_MAX_KP, C <= PP_MAX_EDGES)");
     if (cfg->connection_method != 0 && cfg->connection_method != 1)
@@ -1844,8 +1890,10 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
     for (int i = 0; i < 2 * C; i++)
         if (skeleton[i] < 1 || skeleton[i] > K)
             return fail(PP_EINVAL, "pp_decode_batch: skeleton joint index out of 1..K");
+    if ((int64_t)K * h.cif_cells() > INT32_MAX || h.caf_cells() > INT32_MAX)
+        return fail(PP_ESHAPE, "pp_decode_batch: fields too large");
     if (n_img == 0) return PP_OK;
-    const DecodeLayout d = make_layout(n_img, K, C, H, W, cfg, ann_capacity);
+    const DecodeLayout d = make_layout(n_img, K, C, h, cfg, ann_capacity);
     if (workspace_bytes < d.total) return fail(PP_ENOMEM, "pp_decode_batch: workspace too small");
     if ((int64_t)d.hh >= 32767 * 2 || (int64_t)d.ww >= 32767 * 2)
         return fail(PP_ESHAPE, "pp_decode_batch: field too large");
@@ -1858,17 +1906,17 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
     int *offs[2] = {(int *)(ws + d.off_offs[0]), (int *)(ws + d.off_offs[1])};
     int rc = PP_OK;
     if (stages & 1u) {
-        rc = pp_cifhr(d_cif, n_img, K, H, W, cfg, hr, ws + d.off_cifhr_ws, d.cifhr_ws_bytes, s);
+        rc = cifhr_heads_launch<false>(h, n_img, K, cfg, hr, ws + d.off_cifhr_ws, d.cifhr_ws_bytes, s,
+                                       "pp_decode_batch(cifhr)");
         if (rc) return rc;
     }
     if (stages & 2u) {
-        rc = launch_seeds(d_cif, hr, n_img, K, H, W, cfg, seeds, d.seed_cap, seed_counts,
-                          ws + d.off_seed_ws, s);
+        rc = launch_seeds(h, hr, n_img, K, cfg, seeds, d.seed_cap, seed_counts, ws + d.off_seed_ws, s);
         if (rc) return rc;
     }
     if (stages & 4u) {  // CafScored at caf_threshold; the force-complete set is lazy
-        rc = launch_caf_bucketed(d_caf, hr, n_img, K, C, H, W, skeleton, cfg, cfg->caf_threshold,
-                                 cols[0], offs[0], nullptr, false, s);
+        rc = launch_caf_bucketed(h, hr, n_img, K, C, skeleton, cfg, cfg->caf_threshold, cols[0],
+                                 offs[0], nullptr, false, s);
         if (rc) return rc;
     }
     if (stages & 8u) {
@@ -1886,16 +1934,13 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
         g.inv_e = d.inv_e;
         g.K = K;
         g.C = C;
-        g.H = H;
-        g.W = W;
         g.hh = d.hh;
         g.ww = d.ww;
-        g.hw = d.hw;
+        g.col_cap = d.hw;
         g.cfg = *cfg;
-        g.caf = d_caf;
+        g.heads = h;
         g.hr = hr;
         g.hr_pitch = d.pitch;
-        g.stride_f = (float)cfg->stride;
         g.cif_floor = cfg->cif_floor;
         g.one_minus_floor = (float)(1.0 - (double)cfg->cif_floor);  // (1.0 - self.cif_floor)
         g.th_b = cfg->complete_caf_threshold;
@@ -1969,9 +2014,8 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
         if (rc) return rc;
         if (cfg->force_complete) {
             // complete_annotations' CafScored(score_th=0.0001) only where phase 1 left work
-            rc = launch_caf_bucketed(d_caf, hr, n_img, K, C, H, W, skeleton, cfg,
-                                     cfg->complete_caf_threshold, cols[1], offs[1],
-                                     g.need_complete, true, s);
+            rc = launch_caf_bucketed(h, hr, n_img, K, C, skeleton, cfg, cfg->complete_caf_threshold,
+                                     cols[1], offs[1], g.need_complete, true, s);
             if (rc) return rc;
         }
         if (cfg->force_complete) {
@@ -2009,6 +2053,34 @@ int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int3
 #endif
     }
     return rc;
+}
+
+}  // namespace pp
+
+extern "C" {
+
+int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int32_t K, int32_t C,
+                     int32_t H, int32_t W, const int32_t *skeleton, const pp_config *cfg,
+                     float *d_cifhr, pp_ann *d_anns, int32_t ann_capacity, int32_t *d_counts,
+                     int32_t *d_status, void *d_workspace, size_t workspace_bytes,
+                     uint32_t stages, void *stream) {
+    if (!d_cif || !d_caf || !cfg) return fail(PP_EINVAL, "pp_decode_batch: NULL argument");
+    if (H <= 0 || W <= 0 || cfg->stride <= 0) return fail(PP_ESHAPE, "pp_decode_batch: bad shape");
+    return decode_heads(single_head(d_cif, d_caf, H, W, cfg->stride), n_img, K, C, skeleton, cfg,
+                        d_cifhr, d_anns, ann_capacity, d_counts, d_status, d_workspace,
+                        workspace_bytes, stages, stream);
+}
+
+int pp_decode_multi(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs, int32_t n_img,
+                    int32_t K, int32_t C, const int32_t *skeleton, const pp_config *cfg,
+                    float *d_cifhr, pp_ann *d_anns, int32_t ann_capacity, int32_t *d_counts,
+                    int32_t *d_status, void *d_workspace, size_t workspace_bytes,
+                    uint32_t stages, void *stream) {
+    Heads h;
+    const int rc = make_heads(scales, n_scales, cif_pairs, 3, &h, "pp_decode_multi");
+    if (rc) return rc;
+    return decode_heads(h, n_img, K, C, skeleton, cfg, d_cifhr, d_anns, ann_capacity, d_counts,
+                        d_status, d_workspace, workspace_bytes, stages, stream);
 }
 
 // ---- standalone nms.Keypoints.annotations (nms.py:17-57) over caller records ----------

@@ -94,4 +94,56 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nblocks) {
 // source x, y, target x, y, target scale, row-major index (as float bits)
 constexpr int kColRows = 7;
 
+// The CIF and CAF heads of one decode (a FieldConfig, field_config.py:7-13); a
+// single-scale decode is one CIF and one CAF head.  Concatenated cell index of CAF head m =
+// caf_off[m] + row-major cell: the order of the reference's concatenated column sets
+// (caf_scored.py:70, 81); seeds concatenate the CIF heads the same way (cif_off).
+constexpr int kMaxHeads = PP_MAX_SCALES;
+
+struct Heads {
+    // CIF heads (cif_indices order)
+    const float *cif[kMaxHeads];  // (n_img, K, 5, H, W)
+    int cH[kMaxHeads], cW[kMaxHeads], cstride[kMaxHeads];
+    int64_t cif_off[kMaxHeads + 1];
+    float ms_th[kMaxHeads];       // fl32(cif_min_scale / stride)  (p[4] > ms_th)
+    uint32_t ms_on;               // heads whose min scale is set (truthy in the reference)
+    int n_cif;
+    int pairs;                    // CifHr groups heads g and g + n/2 (cif_hr.py:63-68)
+    int n_groups;
+    // CAF heads (caf_indices order)
+    const float *caf[kMaxHeads];  // (n_img, C, 9, H, W)
+    int aH[kMaxHeads], aW[kMaxHeads], astride[kMaxHeads];
+    int64_t caf_off[kMaxHeads + 1];
+    float dmin_th[kMaxHeads];     // fl32(caf_min_distance / stride) (dist > dmin_th)
+    float dmax_th[kMaxHeads];     // fl32(caf_max_distance / stride) (dist < dmax_th)
+    uint32_t dmin_on, dmax_on;
+    int n_caf;
+    __host__ __device__ __forceinline__ int64_t cif_hw(int m) const { return (int64_t)cH[m] * cW[m]; }
+    __host__ __device__ __forceinline__ int64_t caf_hw(int m) const { return (int64_t)aH[m] * aW[m]; }
+    __host__ __device__ __forceinline__ int64_t cif_cells() const { return cif_off[n_cif]; }
+    __host__ __device__ __forceinline__ int64_t caf_cells() const { return caf_off[n_caf]; }
+    // CifHr group g: its members; the group uses head g's stride and min scale
+    __host__ __device__ __forceinline__ int group_size() const { return pairs ? 2 : 1; }
+    __host__ __device__ __forceinline__ int member(int g, int i) const { return i ? g + n_cif / 2 : g; }
+    // CAF head of a concatenated cell index (n <= 16: a short scalar scan)
+    __host__ __device__ __forceinline__ int caf_head_of(int64_t idx) const {
+        int m = 0;
+        while (m + 1 < n_caf && idx >= caf_off[m + 1]) m++;
+        return m;
+    }
+};
+
+// validates a pp_scale list into Heads (need: PP_ROLE_* lists that must be non-empty);
+// returns PP_OK or a pp_status
+int make_heads(const pp_scale *sc, int n, int pairs, int need, Heads *h, const char *who);
+// one CIF and one CAF head from the single-scale arguments
+Heads single_head(const float *cif, const float *caf, int H, int W, int stride);
+
+// stage launchers over heads (splat.hip, stages.hip)
+size_t cifhr_heads_workspace_size(const Heads &h, int n_img, int K);
+template <bool DET>
+int cifhr_heads_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config *cfg,
+                       float *d_cifhr, void *d_workspace, size_t workspace_bytes, hipStream_t s,
+                       const char *who);
+
 }  // namespace pp

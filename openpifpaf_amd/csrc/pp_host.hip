@@ -18,6 +18,71 @@ int check_launch(const char *what) {
     return PP_OK;
 }
 
+int make_heads(const pp_scale *sc, int n, int pairs, int need, Heads *h, const char *who) {
+    if (!sc || !h) return fail(PP_EINVAL, std::string(who) + ": NULL scale list");
+    if (n <= 0 || n > 2 * kMaxHeads) return fail(PP_ESHAPE, std::string(who) + ": bad scale count");
+    *h = Heads{};
+    int64_t coff = 0, aoff = 0;
+    for (int i = 0; i < n; i++) {
+        const pp_scale &s = sc[i];
+        const int role = s.role ? s.role : (PP_ROLE_CIF | PP_ROLE_CAF);
+        if (role & ~(PP_ROLE_CIF | PP_ROLE_CAF)) return fail(PP_EINVAL, std::string(who) + ": bad role");
+        if (s.H <= 0 || s.W <= 0 || s.stride <= 0)
+            return fail(PP_ESHAPE, std::string(who) + ": bad head shape / stride");
+        // `if min_scale:` / `if min_distance:` / `if max_distance:` (truthiness); the
+        // thresholds are Python float / int divisions rounded to the f32 comparand
+        if (role & PP_ROLE_CIF) {
+            const int m = h->n_cif++;
+            if (m >= kMaxHeads) return fail(PP_ESHAPE, std::string(who) + ": more than PP_MAX_SCALES CIF heads");
+            h->cif[m] = s.cif;
+            h->cH[m] = s.H;
+            h->cW[m] = s.W;
+            h->cstride[m] = s.stride;
+            h->cif_off[m] = coff;
+            coff += (int64_t)s.H * s.W;
+            if (s.cif_min_scale != 0.0f) h->ms_on |= 1u << m;
+            h->ms_th[m] = (float)((double)s.cif_min_scale / s.stride);
+        }
+        if (role & PP_ROLE_CAF) {
+            const int m = h->n_caf++;
+            if (m >= kMaxHeads) return fail(PP_ESHAPE, std::string(who) + ": more than PP_MAX_SCALES CAF heads");
+            h->caf[m] = s.caf;
+            h->aH[m] = s.H;
+            h->aW[m] = s.W;
+            h->astride[m] = s.stride;
+            h->caf_off[m] = aoff;
+            aoff += (int64_t)s.H * s.W;
+            if (s.caf_min_distance != 0.0f) h->dmin_on |= 1u << m;
+            if (s.caf_max_distance != 0.0f) h->dmax_on |= 1u << m;
+            h->dmin_th[m] = (float)((double)s.caf_min_distance / s.stride);
+            h->dmax_th[m] = (float)((double)s.caf_max_distance / s.stride);
+        }
+    }
+    h->cif_off[h->n_cif] = coff;
+    h->caf_off[h->n_caf] = aoff;
+    if ((need & PP_ROLE_CIF) && h->n_cif == 0) return fail(PP_EINVAL, std::string(who) + ": no CIF head");
+    if ((need & PP_ROLE_CAF) && h->n_caf == 0) return fail(PP_EINVAL, std::string(who) + ": no CAF head");
+    if (pairs && (h->n_cif & 1))
+        return fail(PP_ESHAPE, std::string(who) + ": paired CIF heads need an even count");
+    h->pairs = pairs ? 1 : 0;
+    h->n_groups = pairs ? h->n_cif / 2 : h->n_cif;
+    if (coff * PP_MAX_KP > INT32_MAX || aoff > INT32_MAX)
+        return fail(PP_ESHAPE, std::string(who) + ": too many cells");
+    return PP_OK;
+}
+
+Heads single_head(const float *cif, const float *caf, int H, int W, int stride) {
+    pp_scale s{};
+    s.cif = cif;
+    s.caf = caf;
+    s.H = H;
+    s.W = W;
+    s.stride = stride;
+    Heads h{};
+    make_heads(&s, 1, 0, 0, &h, "single");
+    return h;
+}
+
 }  // namespace pp
 
 extern "C" {

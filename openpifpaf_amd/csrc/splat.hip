@@ -52,62 +52,84 @@ constexpr int kTileBits = 1024;  // per-field tile bitmap capacity (32x32 tiles 
 
 // DET: CifDetHr.accumulate (cif_hr.py:84-100) on 7-channel fields [c, x, y, b, w, h, b2],
 // sigma = max(1, 0.1 * min(w, h) * stride); else CifHr (cif_hr.py:26-40), 5 channels.
+//
+// One workgroup per (image, field, CifHr group).  A group's members (cif_hr.py:42-57
+// fill_multiple: one head, or heads g and g + n/2 with pairs) are compacted one after the
+// other into one list, in the reference's accumulation order, at the group head's stride
+// and min scale with v / neighbors / len_cifs.
+struct HrSplatArgs {
+    Heads h;
+    int K, hh, ww;
+    float v_th, neighbors;
+    Splat *splats;        // (n_img * K, list_cap); group g's list at goff[g]
+    int64_t list_cap;     // cells of all heads
+    int64_t goff[kMaxHeads];
+    int *counts;          // (n_img * K, n_groups)
+    uint32_t *tile_bits;  // (n_img * K, n_groups, kTileBits / 32)
+    int tiles_x, tiles;
+};
+
 template <bool DET>
-__global__ __launch_bounds__(256) void cifhr_splats_kernel(const float *__restrict__ cif, int H,
-                                                           int W, int hh, int ww, float stride,
-                                                           float v_th, float neighbors,
-                                                           Splat *__restrict__ splats,
-                                                           int *__restrict__ counts,
-                                                           uint32_t *__restrict__ tile_bits,
-                                                           int tiles_x, int tiles) {
+__global__ __launch_bounds__(256) void cifhr_splats_kernel(HrSplatArgs a) {
     __shared__ int s_tmp[4];
     __shared__ uint32_t s_bits[kTileBits / 32];
-    const bool use_bits = tiles <= kTileBits;
+    const bool use_bits = a.tiles <= kTileBits;
     if (threadIdx.x < kTileBits / 32) s_bits[threadIdx.x] = 0u;
     __syncthreads();
-    const int64_t fld = blockIdx.x;  // image * K + field
-    const int hw = H * W;
-    const float *p = cif + fld * (DET ? 7 : 5) * (int64_t)hw;
-    Splat *out = splats + fld * (int64_t)hw;
+    const int ng = a.h.n_groups;
+    const int64_t fld = blockIdx.x / ng;  // image * K + field
+    const int g = (int)(blockIdx.x % ng);
+    const float stride = (float)a.h.cstride[g];
+    const bool ms_on = (a.h.ms_on >> g) & 1u;
+    const float ms_th = a.h.ms_th[g];
+    const float len_cifs = (float)a.h.group_size();
+    Splat *out = a.splats + fld * a.list_cap + a.goff[g];
     int running = 0;
-    for (int base = 0; base < hw; base += 256) {
-        const int cell = base + threadIdx.x;
-        float c = 0.0f;
-        if (cell < hw) c = p[cell];
-        const bool keep = (cell < hw) && (c > v_th);
-        int total;
-        const int slot = block_compact<4>(keep, s_tmp, total);
-        if (keep) {
-            const float x = p[hw + cell] * stride;
-            const float y = p[2 * hw + cell] * stride;
-            float sg;
-            if (DET) {  // np.minimum / np.maximum propagate NaN
-                const float w = p[4 * hw + cell], h = p[5 * hw + cell];
-                const float m = (w != w) ? w : ((h != h) ? h : (h < w ? h : w));
-                sg = (0.1f * m) * stride;
-            } else {
-                sg = (0.5f * p[4 * hw + cell]) * stride;
+    for (int i = 0; i < a.h.group_size(); i++) {
+        const int m = a.h.member(g, i);
+        const int hw = a.h.cH[m] * a.h.cW[m];
+        const float *p = a.h.cif[m] + fld * (DET ? 7 : 5) * (int64_t)hw;
+        for (int base = 0; base < hw; base += 256) {
+            const int cell = base + threadIdx.x;
+            float c = 0.0f;
+            if (cell < hw) c = p[cell];
+            bool keep = (cell < hw) && (c > a.v_th);
+            if (keep && !DET && ms_on) keep = p[4 * hw + cell] > ms_th;  // p[4] > min_scale / stride
+            int total;
+            const int slot = block_compact<4>(keep, s_tmp, total);
+            if (keep) {
+                const float x = p[hw + cell] * stride;
+                const float y = p[2 * hw + cell] * stride;
+                float sg;
+                if (DET) {  // np.minimum / np.maximum propagate NaN
+                    const float w = p[4 * hw + cell], h = p[5 * hw + cell];
+                    const float mn = (w != w) ? w : ((h != h) ? h : (h < w ? h : w));
+                    sg = (0.1f * mn) * stride;
+                } else {
+                    sg = (0.5f * p[4 * hw + cell]) * stride;
+                }
+                const float sigma = (sg != sg) ? sg : fmaxf(1.0f, sg);  // np.maximum keeps NaN
+                const float v = (c / a.neighbors) / len_cifs;           // v / neighbors / len_cifs
+                Splat s;
+                s.box = splat_box<M_GAUSS_MAX>(x, y, 1.0f * sigma, a.hh, a.ww);
+                s.par = make_float4(x, y, v, sigma * sigma);
+                out[running + slot] = s;
+                if (use_bits) {  // mark the 64x64 output tiles this splat's box touches
+                    for (int ty = s.box.z / kTile; ty <= (s.box.w - 1) / kTile; ty++)
+                        for (int tx = s.box.x / kTile; tx <= (s.box.y - 1) / kTile; tx++) {
+                            const int t = ty * a.tiles_x + tx;
+                            atomicOr(&s_bits[t >> 5], 1u << (t & 31));
+                        }
+                }
             }
-            const float sigma = (sg != sg) ? sg : fmaxf(1.0f, sg);  // np.maximum keeps NaN
-            const float v = (c / neighbors) / 1.0f;                 // v / neighbors / len_cifs
-            Splat s;
-            s.box = splat_box<M_GAUSS_MAX>(x, y, 1.0f * sigma, hh, ww);
-            s.par = make_float4(x, y, v, sigma * sigma);
-            out[running + slot] = s;
-            if (use_bits) {  // mark the 64x64 output tiles this splat's box touches
-                for (int ty = s.box.z / kTile; ty <= (s.box.w - 1) / kTile; ty++)
-                    for (int tx = s.box.x / kTile; tx <= (s.box.y - 1) / kTile; tx++) {
-                        const int t = ty * tiles_x + tx;
-                        atomicOr(&s_bits[t >> 5], 1u << (t & 31));
-                    }
-            }
+            running += total;
         }
-        running += total;
     }
-    if (threadIdx.x == 0) counts[fld] = running;
+    if (threadIdx.x == 0) a.counts[blockIdx.x] = running;
     __syncthreads();
     if (threadIdx.x < kTileBits / 32)
-        tile_bits[fld * (kTileBits / 32) + threadIdx.x] = use_bits ? s_bits[threadIdx.x] : ~0u;
+        a.tile_bits[(int64_t)blockIdx.x * (kTileBits / 32) + threadIdx.x] =
+            use_bits ? s_bits[threadIdx.x] : ~0u;
 }
 
 // -------------------------------------------------------------------------------------
@@ -154,6 +176,8 @@ struct TileArgs {
     int64_t n_work;         // n_fields * tiles
     float t2;               // truncate^2 (M_GAUSS_MAX circle test)
     float max_value;
+    int n_groups;           // CifHr groups (MULTI): field fld's group g list at
+    int64_t goff[kMaxHeads];  // splats + fld * splat_cap + goff[g], count fld * n_groups + g
 };
 
 template <int MODE>
@@ -191,7 +215,11 @@ __device__ __forceinline__ void fold_pixel(float &acc, float &acc2, bool in, flo
     }
 }
 
-template <int MODE, bool ZERO_INIT>
+// MULTI (CifHr over several groups, cif_hr.py:59-73): each group's list folds into a zero
+// tile and the groups combine by np.maximum(ta, accumulated), all in registers.  A group
+// with no splat on the tile contributes max(0, acc) = acc (every fold value is >= 0 and
+// the clamp maps NaN to max_value), so it is skipped.
+template <int MODE, bool ZERO_INIT, bool MULTI>
 __global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
     // candidates (gather / fold) and the output staging tile (store) are live in disjoint
     // phases: one LDS buffer, ~18 KB, so 8 workgroups fit a CU while the tiles stream out
@@ -209,11 +237,6 @@ __global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
     const int64_t fld = wid / a.tiles;
     const int tx0 = (tile % a.tiles_x) * kTile;
     const int ty0 = (tile / a.tiles_x) * kTile;
-    const Splat *sp = a.splats + fld * a.splat_cap;
-    int64_t ns = a.counts ? (int64_t)a.counts[fld] : a.n_splats;
-    if (ZERO_INIT && a.tile_bits &&
-        !((a.tile_bits[fld * (kTileBits / 32) + (tile >> 5)] >> (tile & 31)) & 1u))
-        ns = 0;  // no splat touches this tile: pure zero fill
     float *out = a.field + fld * a.field_stride;
     float *out2 = (MODE == M_CUMAVG) ? a.field2 + fld * a.field_stride : nullptr;
 
@@ -222,11 +245,12 @@ __global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
     const int lx = lane & 7, ly = lane >> 3;
     const int wx0 = tx0, wy0 = ty0 + wave * 16;
 
-    float acc[16], acc2[16];
+    float acc[16], acc2[16], res[MULTI ? 16 : 1];
 #pragma unroll
     for (int r = 0; r < 16; r++) {
         acc[r] = 0.0f;
         acc2[r] = 0.0f;
+        if (MULTI) res[r] = 0.0f;
         if (!ZERO_INIT) {
             const int px = wx0 + (r & 7) * 8 + lx, py = wy0 + (r >> 3) * 8 + ly;
             if (px < a.w && py < a.h) {
@@ -237,50 +261,75 @@ __global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
     }
 
     bool any = false;
-    int64_t cursor = 0;
-    while (cursor < ns) {
-        // ---- gather: splats intersecting this tile, in splat order, into LDS ----
-        int n = 0;
-        while (cursor < ns) {
-            const int64_t i = cursor + threadIdx.x;
-            bool hit = false;
-            int4 b = make_int4(0, 0, 0, 0);
-            if (i < ns) {
-                b = sp[i].box;
-                hit = b.y > tx0 && b.x < tx0 + kTile && b.w > ty0 && b.z < ty0 + kTile;
-            }
-            int total;
-            const int slot = block_compact<4>(hit, s_tmp, total);
-            if (n + total > kCand) break;  // block-uniform; chunk re-read next pass
-            if (hit) {
-                s_box[n + slot] = b;
-                s_par[n + slot] = sp[i].par;
-            }
-            n += total;
-            cursor += 256;
-        }
-        __syncthreads();
-        any = any || n > 0;
-        // ---- fold: per pixel, ascending candidate order ----
-        for (int c = 0; c < n; c++) {
-            const int bx0 = __builtin_amdgcn_readfirstlane(s_box[c].x);
-            const int bx1 = __builtin_amdgcn_readfirstlane(s_box[c].y);
-            const int by0 = __builtin_amdgcn_readfirstlane(s_box[c].z);
-            const int by1 = __builtin_amdgcn_readfirstlane(s_box[c].w);
-            if (bx1 <= wx0 || bx0 >= wx0 + kTile || by1 <= wy0 || by0 >= wy0 + 16) continue;
-            const float4 par = s_par[c];
-            const float t2s2 = a.t2 * par.w;
+    const int ng = MULTI ? a.n_groups : 1;
+    for (int g = 0; g < ng; g++) {
+        const int64_t lst = MULTI ? fld * a.n_groups + g : fld;
+        const Splat *sp = a.splats + fld * a.splat_cap + (MULTI ? a.goff[g] : 0);
+        int64_t ns = a.counts ? (int64_t)a.counts[lst] : a.n_splats;
+        if (ZERO_INIT && a.tile_bits &&
+            !((a.tile_bits[lst * (kTileBits / 32) + (tile >> 5)] >> (tile & 31)) & 1u))
+            ns = 0;  // no splat of this list touches this tile
+        if (MULTI && ns == 0) continue;
+        if (MULTI) {
 #pragma unroll
-            for (int r = 0; r < 16; r++) {
-                const int rx0 = wx0 + (r & 7) * 8, ry0 = wy0 + (r >> 3) * 8;
-                if (bx1 <= rx0 || bx0 >= rx0 + 8 || by1 <= ry0 || by0 >= ry0 + 8) continue;
-                const int px = rx0 + lx, py = ry0 + ly;
-                const bool in = px >= bx0 && px < bx1 && py >= by0 && py < by1;
-                fold_pixel<MODE>(acc[r], acc2[r], in, (float)px, (float)py, par, t2s2,
-                                 a.max_value);
-            }
+            for (int r = 0; r < 16; r++) acc[r] = 0.0f;
         }
-        __syncthreads();
+        bool hit_any = false;
+        int64_t cursor = 0;
+        while (cursor < ns) {
+            // ---- gather: splats intersecting this tile, in splat order, into LDS ----
+            int n = 0;
+            while (cursor < ns) {
+                const int64_t i = cursor + threadIdx.x;
+                bool hit = false;
+                int4 b = make_int4(0, 0, 0, 0);
+                if (i < ns) {
+                    b = sp[i].box;
+                    hit = b.y > tx0 && b.x < tx0 + kTile && b.w > ty0 && b.z < ty0 + kTile;
+                }
+                int total;
+                const int slot = block_compact<4>(hit, s_tmp, total);
+                if (n + total > kCand) break;  // block-uniform; chunk re-read next pass
+                if (hit) {
+                    s_box[n + slot] = b;
+                    s_par[n + slot] = sp[i].par;
+                }
+                n += total;
+                cursor += 256;
+            }
+            __syncthreads();
+            hit_any = hit_any || n > 0;
+            // ---- fold: per pixel, ascending candidate order ----
+            for (int c = 0; c < n; c++) {
+                const int bx0 = __builtin_amdgcn_readfirstlane(s_box[c].x);
+                const int bx1 = __builtin_amdgcn_readfirstlane(s_box[c].y);
+                const int by0 = __builtin_amdgcn_readfirstlane(s_box[c].z);
+                const int by1 = __builtin_amdgcn_readfirstlane(s_box[c].w);
+                if (bx1 <= wx0 || bx0 >= wx0 + kTile || by1 <= wy0 || by0 >= wy0 + 16) continue;
+                const float4 par = s_par[c];
+                const float t2s2 = a.t2 * par.w;
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int rx0 = wx0 + (r & 7) * 8, ry0 = wy0 + (r >> 3) * 8;
+                    if (bx1 <= rx0 || bx0 >= rx0 + 8 || by1 <= ry0 || by0 >= ry0 + 8) continue;
+                    const int px = rx0 + lx, py = ry0 + ly;
+                    const bool in = px >= bx0 && px < bx1 && py >= by0 && py < by1;
+                    fold_pixel<MODE>(acc[r], acc2[r], in, (float)px, (float)py, par, t2s2,
+                                     a.max_value);
+                }
+            }
+            __syncthreads();
+        }
+        any = any || hit_any;
+        if (MULTI && hit_any) {
+#pragma unroll
+            for (int r = 0; r < 16; r++)  // np.maximum(ta, accumulated)
+                res[r] = (acc[r] != acc[r] || res[r] != res[r]) ? NAN : (acc[r] > res[r] ? acc[r] : res[r]);
+        }
+    }
+    if (MULTI) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) acc[r] = res[r];
     }
 
     if (ZERO_INIT) {
@@ -323,7 +372,7 @@ __global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
 // -------------------------------------------------------------------------------------
 static inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 
-template <int MODE, bool ZERO_INIT>
+template <int MODE, bool ZERO_INIT, bool MULTI = false>
 static void launch_tiles(TileArgs a, hipStream_t stream) {
     a.tiles_x = (int)((a.pitch + kTile - 1) / kTile);
     if (!ZERO_INIT) a.tiles_x = (a.w + kTile - 1) / kTile;
@@ -332,8 +381,8 @@ static void launch_tiles(TileArgs a, hipStream_t stream) {
     const int64_t n_fields = a.n_work;  // caller passes the field count here
     a.n_work = n_fields * a.tiles;
     const int64_t nblocks = round_up(a.n_work, 8);
-    hipLaunchKernelGGL((splat_tile_kernel<MODE, ZERO_INIT>), dim3((unsigned)nblocks), dim3(256), 0,
-                       stream, a);
+    hipLaunchKernelGGL((splat_tile_kernel<MODE, ZERO_INIT, MULTI>), dim3((unsigned)nblocks), dim3(256),
+                       0, stream, a);
 }
 
 }  // namespace pp
@@ -345,44 +394,60 @@ extern "C" {
 int64_t pp_cifhr_pitch(int64_t w_hr) { return round_up(w_hr, 32); }
 
 size_t pp_cifhr_workspace_size(int32_t n_img, int32_t K, int32_t H, int32_t W) {
-    const size_t nf = (size_t)n_img * K;
-    return round_up((int64_t)(nf * (size_t)H * W * sizeof(Splat)), 256) +
-           round_up((int64_t)(nf * sizeof(int)), 256) +
-           round_up((int64_t)(nf * (kTileBits / 32) * sizeof(uint32_t)), 256);
+    return pp::cifhr_heads_workspace_size(pp::single_head(nullptr, nullptr, H, W, 1), n_img, K);
 }
 
 }  // extern "C"
 
 namespace pp {
+
+size_t cifhr_heads_workspace_size(const Heads &h, int n_img, int K) {
+    const size_t nf = (size_t)n_img * K;
+    return round_up((int64_t)(nf * (size_t)h.cif_cells() * sizeof(Splat)), 256) +
+           round_up((int64_t)(nf * h.n_groups * sizeof(int)), 256) +
+           round_up((int64_t)(nf * h.n_groups * (kTileBits / 32) * sizeof(uint32_t)), 256);
+}
+
+// CifHr.fill (cif_hr.py:59-73) over the heads: the map has head 0's field size and stride
 template <bool DET>
-static int cifhr_launch(const float *d_cif, int32_t n_img, int32_t K, int32_t H, int32_t W,
-                        const pp_config *cfg, float *d_cifhr, void *d_workspace,
-                        size_t workspace_bytes, void *stream) {
-    if (!d_cif || !cfg || !d_cifhr || !d_workspace) return fail(PP_EINVAL, "pp_cifhr: NULL argument");
-    if (n_img < 0 || K <= 0 || H <= 0 || W <= 0 || cfg->stride <= 0)
-        return fail(PP_ESHAPE, "pp_cifhr: bad shape");
+int cifhr_heads_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config *cfg,
+                       float *d_cifhr, void *d_workspace, size_t workspace_bytes,
+                       hipStream_t s, const char *who) {
+    if (!cfg || !d_cifhr || !d_workspace) return fail(PP_EINVAL, std::string(who) + ": NULL argument");
+    for (int m = 0; m < h.n_cif; m++)
+        if (!h.cif[m]) return fail(PP_EINVAL, std::string(who) + ": NULL field");
+    if (n_img < 0 || K <= 0) return fail(PP_ESHAPE, std::string(who) + ": bad shape");
     if (n_img == 0) return PP_OK;
-    if (workspace_bytes < pp_cifhr_workspace_size(n_img, K, H, W))
-        return fail(PP_ENOMEM, "pp_cifhr: workspace too small");
-    const int hh = (int)hr_dim(H, cfg->stride), ww = (int)hr_dim(W, cfg->stride);
+    if (workspace_bytes < cifhr_heads_workspace_size(h, n_img, K))
+        return fail(PP_ENOMEM, std::string(who) + ": workspace too small");
+    const int hh = (int)hr_dim(h.cH[0], h.cstride[0]), ww = (int)hr_dim(h.cW[0], h.cstride[0]);
     const int64_t pitch = pp_cifhr_pitch(ww);
     const int64_t nf = (int64_t)n_img * K;
-    Splat *splats = (Splat *)d_workspace;
-    int *counts = (int *)((char *)d_workspace +
-                          round_up((int64_t)(nf * (int64_t)H * W * sizeof(Splat)), 256));
-    uint32_t *bits = (uint32_t *)((char *)counts + round_up((int64_t)(nf * sizeof(int)), 256));
-    const int tiles_x = (int)((pitch + kTile - 1) / kTile);
-    const int tiles = tiles_x * ((hh + kTile - 1) / kTile);
-    hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(cifhr_splats_kernel<DET>, dim3((unsigned)nf), dim3(256), 0, s, d_cif, H, W, hh,
-                       ww, (float)cfg->stride, cfg->cif_threshold, (float)cfg->cif_neighbors,
-                       splats, counts, bits, tiles_x, tiles);
+    HrSplatArgs sa{};
+    sa.h = h;
+    sa.K = K;
+    sa.hh = hh;
+    sa.ww = ww;
+    sa.v_th = cfg->cif_threshold;
+    sa.neighbors = (float)cfg->cif_neighbors;
+    sa.splats = (Splat *)d_workspace;
+    sa.list_cap = h.cif_cells();
+    int64_t o = 0;
+    for (int g = 0; g < h.n_groups; g++) {
+        sa.goff[g] = o;
+        for (int i = 0; i < h.group_size(); i++) o += h.cif_hw(h.member(g, i));
+    }
+    sa.counts = (int *)((char *)d_workspace + round_up((int64_t)(nf * sa.list_cap * sizeof(Splat)), 256));
+    sa.tile_bits = (uint32_t *)((char *)sa.counts + round_up((int64_t)(nf * h.n_groups * sizeof(int)), 256));
+    sa.tiles_x = (int)((pitch + kTile - 1) / kTile);
+    sa.tiles = sa.tiles_x * ((hh + kTile - 1) / kTile);
+    hipLaunchKernelGGL(cifhr_splats_kernel<DET>, dim3((unsigned)(nf * h.n_groups)), dim3(256), 0, s, sa);
     TileArgs a{};
     a.field = d_cifhr;
-    a.splats = splats;
-    a.counts = counts;
-    a.tile_bits = bits;
-    a.splat_cap = (int64_t)H * W;
+    a.splats = sa.splats;
+    a.counts = sa.counts;
+    a.tile_bits = sa.tile_bits;
+    a.splat_cap = sa.list_cap;
     a.field_stride = (int64_t)hh * pitch;
     a.h = hh;
     a.w = ww;
@@ -390,9 +455,18 @@ static int cifhr_launch(const float *d_cif, int32_t n_img, int32_t K, int32_t H,
     a.n_work = nf;
     a.t2 = 1.0f;  // truncate = 1.0 (cif_hr.py:40)
     a.max_value = 1.0f;
-    launch_tiles<M_GAUSS_MAX, true>(a, s);
-    return check_launch(DET ? "pp_cifdet_hr" : "pp_cifhr");
+    a.n_groups = h.n_groups;
+    for (int g = 0; g < h.n_groups; g++) a.goff[g] = sa.goff[g];
+    if (h.n_groups > 1)
+        launch_tiles<M_GAUSS_MAX, true, true>(a, s);
+    else
+        launch_tiles<M_GAUSS_MAX, true, false>(a, s);
+    return check_launch(who);
 }
+
+template int cifhr_heads_launch<false>(const Heads &, int32_t, int32_t, const pp_config *, float *,
+                                       void *, size_t, hipStream_t, const char *);
+
 }  // namespace pp
 
 extern "C" {
@@ -400,15 +474,40 @@ extern "C" {
 int pp_cifhr(const float *d_cif, int32_t n_img, int32_t K, int32_t H, int32_t W,
              const pp_config *cfg, float *d_cifhr, void *d_workspace, size_t workspace_bytes,
              void *stream) {
-    return cifhr_launch<false>(d_cif, n_img, K, H, W, cfg, d_cifhr, d_workspace, workspace_bytes,
-                               stream);
+    if (!d_cif || !cfg) return fail(PP_EINVAL, "pp_cifhr: NULL argument");
+    if (H <= 0 || W <= 0 || cfg->stride <= 0) return fail(PP_ESHAPE, "pp_cifhr: bad shape");
+    return cifhr_heads_launch<false>(single_head(d_cif, nullptr, H, W, cfg->stride), n_img, K, cfg,
+                                     d_cifhr, d_workspace, workspace_bytes, (hipStream_t)stream,
+                                     "pp_cifhr");
 }
 
 int pp_cifdet_hr(const float *d_det, int32_t n_img, int32_t K, int32_t H, int32_t W,
                  const pp_config *cfg, float *d_cifhr, void *d_workspace, size_t workspace_bytes,
                  void *stream) {
-    return cifhr_launch<true>(d_det, n_img, K, H, W, cfg, d_cifhr, d_workspace, workspace_bytes,
-                              stream);
+    if (!d_det || !cfg) return fail(PP_EINVAL, "pp_cifdet_hr: NULL argument");
+    if (H <= 0 || W <= 0 || cfg->stride <= 0) return fail(PP_ESHAPE, "pp_cifdet_hr: bad shape");
+    return cifhr_heads_launch<true>(single_head(d_det, nullptr, H, W, cfg->stride), n_img, K, cfg,
+                                    d_cifhr, d_workspace, workspace_bytes, (hipStream_t)stream,
+                                    "pp_cifdet_hr");
+}
+
+size_t pp_cifhr_multi_workspace_size(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs,
+                                     int32_t n_img, int32_t K) {
+    Heads h;
+    if (make_heads(scales, n_scales, cif_pairs, PP_ROLE_CIF, &h, "pp_cifhr_multi_workspace_size") ||
+        n_img < 0 || K <= 0)
+        return 0;
+    return cifhr_heads_workspace_size(h, n_img, K);
+}
+
+int pp_cifhr_multi(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs, int32_t n_img,
+                   int32_t K, const pp_config *cfg, float *d_cifhr, void *d_workspace,
+                   size_t workspace_bytes, void *stream) {
+    Heads h;
+    const int rc = make_heads(scales, n_scales, cif_pairs, PP_ROLE_CIF, &h, "pp_cifhr_multi");
+    if (rc) return rc;
+    return cifhr_heads_launch<false>(h, n_img, K, cfg, d_cifhr, d_workspace, workspace_bytes,
+                                     (hipStream_t)stream, "pp_cifhr_multi");
 }
 
 }  // extern "C"

@@ -60,33 +60,42 @@ __device__ void bitonic_sort(Perm *p, int np, const SeedKeys &keys) {
 }
 
 struct SeedArgs {
-    const float *cif, *hr;
-    int K, H, W, hh, ww;
+    Heads h;            // CifSeeds.fill visits the heads in order (cif_seeds.py:56-64)
+    const float *hr;
+    int K, hh, ww;
     int64_t pitch;
-    float stride, th, score_scale;
+    float th, score_scale;
     pp_seed *seeds;     // (n_img, cap) sorted output
-    int cap;            // K * H * W
+    int cap;            // K * sum of the heads' H * W
     int *counts;        // (n_img) seeds per image
-    float *g_keys;      // (n_img, 4, cap): per-field emission slots (v, x, y, s), field f at f*H*W
-    int *g_f;           // (n_img, cap): field of each slot; reused as slot index (global sort)
-    int *f_counts;      // (n_img, K) seeds per field
+    float *g_keys;      // (n_img, 4, cap): per-segment emission slots (v, x, y, s)
+    int *g_f;           // (n_img, cap): field of each slot
+    int *f_counts;      // (n_img, n_heads * K) seeds per segment (head, field)
     int *g_perm;        // (n_img, np_cap)
     int np_cap;
+    // first slot of segment (CIF head m, field f): K * cif_off[m] + f * H_m * W_m
+    __device__ __forceinline__ int64_t seg_base(int m, int f) const {
+        return (int64_t)K * h.cif_off[m] + (int64_t)f * h.cif_hw(m);
+    }
 };
 
-// stage 1: one workgroup per (image, field) — cif_seeds.py:28-47 for that field, in
-// row-major cell order, into the field's slot range
+// stage 1: one workgroup per (image, head, field) — cif_seeds.py:28-47 for that field, in
+// row-major cell order, into the segment's slot range
 __global__ __launch_bounds__(256) void seeds_emit_kernel(SeedArgs a) {
     __shared__ int s_tmp[4];
-    const int64_t fld = blockIdx.x;
-    const int img = (int)(fld / a.K), f = (int)(fld % a.K);
-    const int hw = a.H * a.W;
+    const int nseg = a.h.n_cif * a.K;
+    const int img = (int)(blockIdx.x / nseg), seg = (int)(blockIdx.x % nseg);
+    const int m = seg / a.K, f = seg % a.K;
+    const int hw = a.h.cH[m] * a.h.cW[m];
+    const float stride = (float)a.h.cstride[m];
+    const bool ms_on = (a.h.ms_on >> m) & 1u;
+    const float ms_th = a.h.ms_th[m];
     const int64_t cap = a.cap;
-    float *gv = a.g_keys + (int64_t)img * 4 * cap + (int64_t)f * hw;
+    float *gv = a.g_keys + (int64_t)img * 4 * cap + a.seg_base(m, f);
     float *gx = gv + cap, *gy = gx + cap, *gs = gy + cap;
-    int *gf = a.g_f + (int64_t)img * cap + (int64_t)f * hw;
-    const float *p = a.cif + fld * 5 * hw;
-    const float *t = a.hr + fld * a.hh * a.pitch;
+    int *gf = a.g_f + (int64_t)img * cap + a.seg_base(m, f);
+    const float *p = a.h.cif[m] + ((int64_t)img * a.K + f) * 5 * hw;
+    const float *t = a.hr + ((int64_t)img * a.K + f) * a.hh * a.pitch;
     int running = 0;
     for (int base = 0; base < hw; base += 256) {
         const int cell = base + threadIdx.x;
@@ -94,14 +103,15 @@ __global__ __launch_bounds__(256) void seeds_emit_kernel(SeedArgs a) {
         float v = 0.0f, x = 0.0f, y = 0.0f, sc = 0.0f;
         if (cell < hw) {
             const float c = p[cell];
-            if (c > a.th) {  // p[:, p[0] > threshold]
-                x = p[hw + cell] * a.stride;
-                y = p[2 * hw + cell] * a.stride;
-                const float h = hr_lookup(t, a.hh, a.ww, a.pitch, x, y, 0.0f);
-                v = 0.9f * h + 0.1f * c;  // 0.9 * v + 0.1 * c
+            // p[:, p[0] > threshold], then p[:, p[4] > min_scale / stride]
+            if (c > a.th && (!ms_on || p[4 * hw + cell] > ms_th)) {
+                x = p[hw + cell] * stride;
+                y = p[2 * hw + cell] * stride;
+                const float hv = hr_lookup(t, a.hh, a.ww, a.pitch, x, y, 0.0f);
+                v = 0.9f * hv + 0.1f * c;  // 0.9 * v + 0.1 * c
                 if (a.score_scale != 1.0f) v = v * a.score_scale;
                 keep = v > a.th;
-                sc = p[4 * hw + cell] * a.stride;
+                sc = p[4 * hw + cell] * stride;
             }
         }
         int total;
@@ -116,7 +126,7 @@ __global__ __launch_bounds__(256) void seeds_emit_kernel(SeedArgs a) {
         }
         running += total;
     }
-    if (threadIdx.x == 0) a.f_counts[fld] = running;
+    if (threadIdx.x == 0) a.f_counts[blockIdx.x] = running;
 }
 
 // Seeds with v > threshold > 0 sort as 64-bit keys, descending: v's bits (positive
@@ -132,40 +142,42 @@ __device__ __forceinline__ uint64_t seed_key(float v, int f, int e) {
 
 __device__ __forceinline__ int key_emit(uint64_t k) { return (int)(kEmitMask - ((uint32_t)k & kEmitMask)); }
 
-// stage 2: one workgroup per image — concatenate the fields in order and sort
+// stage 2: one workgroup per image — concatenate the segments in order and sort
 __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
     __shared__ uint64_t s_key[kSortLds];
     __shared__ float s_x[kSortLds], s_y[kSortLds], s_s[kSortLds];
-    __shared__ int s_off[PP_MAX_KP + 1];
+    __shared__ int s_off[kMaxHeads * PP_MAX_KP + 1];
     const int img = blockIdx.x;
-    const int hw = a.H * a.W;
+    const int nseg = a.h.n_cif * a.K;
     const int64_t cap = a.cap;
     const float *gv = a.g_keys + (int64_t)img * 4 * cap, *gx = gv + cap, *gy = gx + cap,
                 *gs = gy + cap;
     int *gf = a.g_f + (int64_t)img * cap;
     if (threadIdx.x == 0) {
         int o = 0;
-        for (int f = 0; f < a.K; f++) {
-            s_off[f] = o;
-            o += a.f_counts[(int64_t)img * a.K + f];
+        for (int q = 0; q < nseg; q++) {
+            s_off[q] = o;
+            o += a.f_counts[(int64_t)img * nseg + q];
         }
-        s_off[a.K] = o;
+        s_off[nseg] = o;
         a.counts[img] = o;
     }
     __syncthreads();
-    const int n = s_off[a.K];
+    const int n = s_off[nseg];
     int np = 1;
     while (np < n) np <<= 1;
     pp_seed *out = a.seeds + (int64_t)img * cap;
     if (n <= kSortLds) {
-        for (int f = 0; f < a.K; f++) {
-            const int o = s_off[f], c = s_off[f + 1] - o;
+        for (int q = 0; q < nseg; q++) {
+            const int o = s_off[q], c = s_off[q + 1] - o;
+            const int f = q % a.K;
+            const int64_t sb = a.seg_base(q / a.K, f);
             for (int i = threadIdx.x; i < c; i += blockDim.x) {
-                const int64_t q = (int64_t)f * hw + i;
-                s_key[o + i] = seed_key(gv[q], f, o + i);
-                s_x[o + i] = gx[q];
-                s_y[o + i] = gy[q];
-                s_s[o + i] = gs[q];
+                const int64_t k = sb + i;
+                s_key[o + i] = seed_key(gv[k], f, o + i);
+                s_x[o + i] = gx[k];
+                s_y[o + i] = gy[k];
+                s_s[o + i] = gs[k];
             }
         }
         for (int i = n + threadIdx.x; i < np; i += blockDim.x) s_key[i] = 0;  // sorts last
@@ -228,9 +240,10 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
         // through an emission-index -> slot map
         int *perm = a.g_perm + (int64_t)img * a.np_cap;
         int *loc = perm + np;  // second half of the permutation buffer
-        for (int f = 0; f < a.K; f++) {
-            const int o = s_off[f], c = s_off[f + 1] - o;
-            for (int i = threadIdx.x; i < c; i += blockDim.x) loc[o + i] = f * hw + i;
+        for (int q = 0; q < nseg; q++) {
+            const int o = s_off[q], c = s_off[q + 1] - o;
+            const int64_t sb = a.seg_base(q / a.K, q % a.K);
+            for (int i = threadIdx.x; i < c; i += blockDim.x) loc[o + i] = (int)(sb + i);
         }
         for (int i = threadIdx.x; i < np; i += blockDim.x) perm[i] = i;
         __syncthreads();
@@ -253,89 +266,107 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
 constexpr int kMaxCaf = PP_MAX_EDGES;
 
 struct CafArgs {
-    const float *caf, *hr;
-    int K, C, H, W, hh, ww;
+    Heads h;            // CafScored.fill visits the heads in order (caf_scored.py:88-98)
+    const float *hr;
+    int K, C, hh, ww;
     int64_t pitch;
-    float stride, cif_floor, one_minus_floor;
+    int64_t col_cap;    // columns per set (>= cells of all heads)
+    float cif_floor, one_minus_floor;
     int nt;             // number of thresholds (1 or 2)
     float th[2];
-    float *cols[2];     // (n_img, C, 2, 9, H*W): dir 0 backward, 1 forward
+    float *cols[2];     // (n_img, C, 2, 9, col_cap): dir 0 backward, 1 forward
     int *counts[2];     // (n_img, C, 2)
     const int *gate;    // (n_img) or NULL: images with gate 0 are skipped (empty sets)
     int j1[kMaxCaf], j2[kMaxCaf];
 };
 
+// caf_scored.py:46-56: the min / max distance masks of head m on the raw (unstrided) vectors
+__device__ __forceinline__ bool caf_distance_ok(const Heads &h, int m, const float *p, int64_t hw,
+                                                int64_t cell) {
+    const bool on_min = (h.dmin_on >> m) & 1u, on_max = (h.dmax_on >> m) & 1u;
+    if (!on_min && !on_max) return true;
+    const float dx = p[1 * hw + cell] - p[5 * hw + cell], dy = p[2 * hw + cell] - p[6 * hw + cell];
+    const float dist = sqrtf(dx * dx + dy * dy);  // np.linalg.norm(nine[1:3] - nine[5:7], axis=0)
+    if (on_min && !(dist > h.dmin_th[m])) return false;
+    if (on_max && !(dist < h.dmax_th[m])) return false;
+    return true;
+}
+
 __global__ __launch_bounds__(256) void caf_scored_kernel(CafArgs a) {
     __shared__ int s_tmp[4];
     const int64_t fld = blockIdx.x;  // image * C + caf field
     const int img = (int)(fld / a.C), ci = (int)(fld % a.C);
-    const int hw = a.H * a.W;
     if (a.gate && !a.gate[img]) {
         if (threadIdx.x < a.nt * 2) a.counts[threadIdx.x >> 1][fld * 2 + (threadIdx.x & 1)] = 0;
         return;
     }
-    const float *p = a.caf + fld * 9 * hw;
     const int j1i = a.j1[ci], j2i = a.j2[ci];
     const bool use1 = a.cif_floor < 1.0f && j1i < a.K;
     const bool use2 = a.cif_floor < 1.0f && j2i < a.K;
     const float *t1 = a.hr + ((int64_t)img * a.K + (use1 ? j1i : 0)) * a.hh * a.pitch;
     const float *t2 = a.hr + ((int64_t)img * a.K + (use2 ? j2i : 0)) * a.hh * a.pitch;
+    const int64_t cc = a.col_cap;
     int run_b[2] = {0, 0}, run_f[2] = {0, 0};
     const float th_min = a.nt == 2 ? fminf(a.th[0], a.th[1]) : a.th[0];
-    for (int base = 0; base < hw; base += 256) {
-        const int cell = base + threadIdx.x;
-        float nine[9];
-        float sb = 0.0f, sf = 0.0f;
-        bool any = false;
-        if (cell < hw) {
-            nine[0] = p[cell];
-            any = nine[0] > th_min;
-            if (any) {
+    for (int m = 0; m < a.h.n_caf; m++) {
+        const int hw = a.h.aH[m] * a.h.aW[m];
+        const float stride = (float)a.h.astride[m];
+        const float *p = a.h.caf[m] + fld * 9 * hw;
+        for (int base = 0; base < hw; base += 256) {
+            const int cell = base + threadIdx.x;
+            float nine[9];
+            float sb = 0.0f, sf = 0.0f;
+            bool any = false;
+            if (cell < hw) {
+                nine[0] = p[cell];
+                any = nine[0] > th_min && caf_distance_ok(a.h, m, p, hw, cell);
+                if (any) {
 #pragma unroll
-                for (int r = 1; r < 9; r++) nine[r] = p[r * hw + cell] * a.stride;
-                const float score = nine[0];
-                sb = score;
-                sf = score;
-                if (use1)
-                    sb = score * (a.cif_floor +
-                                  a.one_minus_floor *
-                                      hr_lookup(t1, a.hh, a.ww, a.pitch, nine[1], nine[2], 0.0f));
-                if (use2)
-                    sf = score * (a.cif_floor +
-                                  a.one_minus_floor *
-                                      hr_lookup(t2, a.hh, a.ww, a.pitch, nine[5], nine[6], 0.0f));
+                    for (int r = 1; r < 9; r++) nine[r] = p[r * hw + cell] * stride;
+                    const float score = nine[0];
+                    sb = score;
+                    sf = score;
+                    if (use1)
+                        sb = score * (a.cif_floor +
+                                      a.one_minus_floor *
+                                          hr_lookup(t1, a.hh, a.ww, a.pitch, nine[1], nine[2], 0.0f));
+                    if (use2)
+                        sf = score * (a.cif_floor +
+                                      a.one_minus_floor *
+                                          hr_lookup(t2, a.hh, a.ww, a.pitch, nine[5], nine[6], 0.0f));
+                }
             }
-        }
-        for (int t = 0; t < a.nt; t++) {
-            const float th = a.th[t];
-            const bool pass = any && nine[0] > th;  // mask = nine[0] > score_th
-            const bool kb = pass && sb > th, kf = pass && sf > th;
-            int tot_b, tot_f;
-            const int slot_b = block_compact<4>(kb, s_tmp, tot_b);
-            const int slot_f = block_compact<4>(kf, s_tmp, tot_f);
-            float *bwd = a.cols[t] + (fld * 2 + 0) * 9 * (int64_t)hw;
-            float *fwd = a.cols[t] + (fld * 2 + 1) * 9 * (int64_t)hw;
-            if (kb) {
-                // backward rows (0, 5, 6, 7, 8, 1, 2, 3, 4) with row 0 = scores_b
-                const int c = run_b[t] + slot_b;
-                bwd[c] = sb;
-                bwd[1 * hw + c] = nine[5];
-                bwd[2 * hw + c] = nine[6];
-                bwd[3 * hw + c] = nine[7];
-                bwd[4 * hw + c] = nine[8];
-                bwd[5 * hw + c] = nine[1];
-                bwd[6 * hw + c] = nine[2];
-                bwd[7 * hw + c] = nine[3];
-                bwd[8 * hw + c] = nine[4];
-            }
-            if (kf) {
-                const int c = run_f[t] + slot_f;
-                fwd[c] = sf;
+            for (int t = 0; t < a.nt; t++) {
+                const float th = a.th[t];
+                const bool pass = any && nine[0] > th;  // mask = nine[0] > score_th
+                const bool kb = pass && sb > th, kf = pass && sf > th;
+                int tot_b, tot_f;
+                const int slot_b = block_compact<4>(kb, s_tmp, tot_b);
+                const int slot_f = block_compact<4>(kf, s_tmp, tot_f);
+                float *bwd = a.cols[t] + (fld * 2 + 0) * 9 * cc;
+                float *fwd = a.cols[t] + (fld * 2 + 1) * 9 * cc;
+                if (kb) {
+                    // backward rows (0, 5, 6, 7, 8, 1, 2, 3, 4) with row 0 = scores_b
+                    const int64_t c = run_b[t] + slot_b;
+                    bwd[c] = sb;
+                    bwd[1 * cc + c] = nine[5];
+                    bwd[2 * cc + c] = nine[6];
+                    bwd[3 * cc + c] = nine[7];
+                    bwd[4 * cc + c] = nine[8];
+                    bwd[5 * cc + c] = nine[1];
+                    bwd[6 * cc + c] = nine[2];
+                    bwd[7 * cc + c] = nine[3];
+                    bwd[8 * cc + c] = nine[4];
+                }
+                if (kf) {
+                    const int64_t c = run_f[t] + slot_f;
+                    fwd[c] = sf;
 #pragma unroll
-                for (int r = 1; r < 9; r++) fwd[r * hw + c] = nine[r];
+                    for (int r = 1; r < 9; r++) fwd[r * cc + c] = nine[r];
+                }
+                run_b[t] += tot_b;
+                run_f[t] += tot_f;
             }
-            run_b[t] += tot_b;
-            run_f[t] += tot_f;
         }
     }
     if (threadIdx.x == 0) {
@@ -356,13 +387,15 @@ __global__ __launch_bounds__(256) void caf_scored_kernel(CafArgs a) {
 constexpr int kMaxBuckets = 1600 + 1;
 
 struct CafBArgs {
-    const float *caf, *hr;
-    int K, C, H, W, hh, ww;
+    Heads h;
+    const float *hr;
+    int K, C, hh, ww;
     int64_t pitch;
-    float stride, cif_floor, one_minus_floor, th;
+    int64_t col_cap;    // columns per set: cells of all heads
+    float cif_floor, one_minus_floor, th;
     int bw, bh, nb;     // bucket grid and bucket count (bw * bh + 1)
     float inv_e;        // 1 / bucket edge (a power of two: exact)
-    float *cols;        // (n_img, C, 2, kColRows, H*W): dir 0 backward, 1 forward
+    float *cols;        // (n_img, C, 2, kColRows, col_cap): dir 0 backward, 1 forward
     int *offs;          // (n_img, C, 2, nb + 1)
     // (n_img) or NULL: bitmask of the joints force-complete may still set.  Completion
     // only evaluates connections INTO unset joints (cifcaf.py:253, 272), so a direction
@@ -389,7 +422,6 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
     __shared__ int s_wsum[2][4];
     const int64_t fld = blockIdx.x;  // image * C + caf field
     const int img = (int)(fld / a.C), ci = (int)(fld % a.C);
-    const int hw = a.H * a.W;
     const int nb = a.nb;
     int *offs_b = a.offs + (fld * 2 + 0) * (int64_t)(nb + 1);
     int *offs_f = a.offs + (fld * 2 + 1) * (int64_t)(nb + 1);
@@ -404,7 +436,6 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
         }
         return;
     }
-    const float *p = a.caf + fld * 9 * hw;
     const bool use1 = need_b && a.cif_floor < 1.0f && j1i < a.K;
     const bool use2 = need_f && a.cif_floor < 1.0f && j2i < a.K;
     const float *t1 = a.hr + ((int64_t)img * a.K + (use1 ? j1i : 0)) * a.hh * a.pitch;
@@ -415,19 +446,21 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
     }
     __syncthreads();
 
-    // one cell of caf_scored.py:42-81 (both directions)
-    auto score_cell = [&](int cell, float nine[9], bool &kb, bool &kf, float &sb, float &sf) {
+    // one cell of caf_scored.py:42-81 (both directions) of head m
+    auto score_cell = [&](const float *p, int64_t hw, float stride, int m, int cell, float nine[9],
+                          bool &kb, bool &kf, float &sb, float &sf) {
         kb = kf = false;
         nine[0] = p[cell];
         if (!(nine[0] > a.th)) return;  // mask = nine[0] > score_th
+        if (!caf_distance_ok(a.h, m, p, hw, cell)) return;
         if (INDEX_ONLY) {  // source positions only: forward (x1, y1), backward (x2, y2)
             if (need_f) {
-                nine[1] = p[1 * hw + cell] * a.stride;
-                nine[2] = p[2 * hw + cell] * a.stride;
+                nine[1] = p[1 * hw + cell] * stride;
+                nine[2] = p[2 * hw + cell] * stride;
             }
             if (need_b) {
-                nine[5] = p[5 * hw + cell] * a.stride;
-                nine[6] = p[6 * hw + cell] * a.stride;
+                nine[5] = p[5 * hw + cell] * stride;
+                nine[6] = p[6 * hw + cell] * stride;
             }
             kb = need_b;
             kf = need_f;
@@ -435,7 +468,7 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
         }
 #pragma unroll
         for (int r = 1; r < 9; r++)  // b1, b2 (rows 3, 7) are never read by the decoder
-            nine[r] = (r == 3 || r == 7) ? 0.0f : p[r * hw + cell] * a.stride;
+            nine[r] = (r == 3 || r == 7) ? 0.0f : p[r * hw + cell] * stride;
         const float score = nine[0];
         sb = score;
         sf = score;
@@ -451,12 +484,17 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
 
     // pass 1: bucket histograms (backward sources are (x2, y2), forward (x1, y1)); no
     // barrier inside the loop, so the cells' loads overlap freely
-    for (int cell = threadIdx.x; cell < hw; cell += 256) {
-        float nine[9], sb, sf;
-        bool kb, kf;
-        score_cell(cell, nine, kb, kf, sb, sf);
-        if (kb) atomicAdd(&s_cnt[0][caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e)], 1);
-        if (kf) atomicAdd(&s_cnt[1][caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e)], 1);
+    for (int m = 0; m < a.h.n_caf; m++) {
+        const int hw = a.h.aH[m] * a.h.aW[m];
+        const float stride = (float)a.h.astride[m];
+        const float *p = a.h.caf[m] + fld * 9 * hw;
+        for (int cell = threadIdx.x; cell < hw; cell += 256) {
+            float nine[9], sb, sf;
+            bool kb, kf;
+            score_cell(p, hw, stride, m, cell, nine, kb, kf, sb, sf);
+            if (kb) atomicAdd(&s_cnt[0][caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e)], 1);
+            if (kf) atomicAdd(&s_cnt[1][caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e)], 1);
+        }
     }
     __syncthreads();
     // exclusive prefix over the buckets (thread-contiguous ranges + block scan)
@@ -491,68 +529,74 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
     }
     __syncthreads();
 
-    // pass 2: scatter into buckets.  A column's tie-break key is its cell's row-major index:
-    // it orders the kept columns exactly as their rank in the reference's compacted array
-    // does, and the grow kernel's merge is independent of the order inside a bucket.
+    // pass 2: scatter into buckets.  A column's tie-break key is its concatenated cell index
+    // (cell_off[m] + row-major cell): it orders the kept columns exactly as their rank in the
+    // reference's concatenated array does, and the grow kernel's merge is independent of the
+    // order inside a bucket.
     const int rows = INDEX_ONLY ? 1 : kColRows;
-    float *bwd = a.cols + (fld * 2 + 0) * rows * (int64_t)hw;
-    float *fwd = a.cols + (fld * 2 + 1) * rows * (int64_t)hw;
-    for (int cell = threadIdx.x; cell < hw; cell += 256) {
-        float nine[9], sb, sf;
-        bool kb, kf;
-        score_cell(cell, nine, kb, kf, sb, sf);
-        if (INDEX_ONLY) {
-            if (kb)
-                reinterpret_cast<int *>(bwd)[atomicAdd(
-                    &s_cnt[0][caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e)], 1)] = cell;
-            if (kf)
-                reinterpret_cast<int *>(fwd)[atomicAdd(
-                    &s_cnt[1][caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e)], 1)] = cell;
-            continue;
-        }
-        // the kColRows rows the grow kernel reads: score, source x, y, target x, y, target
-        // scale, index.  Backward sets are the reference's rows (0, 5, 6, 7, 8, 1, 2, 3, 4)
-        // with row 0 = scores_b, so their source is (x2, y2) and their target (x1, y1, s1).
-        if (kb) {
-            const int c = atomicAdd(&s_cnt[0][caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e)], 1);
-            bwd[c] = sb;
-            bwd[1 * hw + c] = nine[5];
-            bwd[2 * hw + c] = nine[6];
-            bwd[3 * hw + c] = nine[1];
-            bwd[4 * hw + c] = nine[2];
-            bwd[5 * hw + c] = nine[4];
-            bwd[6 * hw + c] = __int_as_float(cell);
-        }
-        if (kf) {
-            const int c = atomicAdd(&s_cnt[1][caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e)], 1);
-            fwd[c] = sf;
-            fwd[1 * hw + c] = nine[1];
-            fwd[2 * hw + c] = nine[2];
-            fwd[3 * hw + c] = nine[5];
-            fwd[4 * hw + c] = nine[6];
-            fwd[5 * hw + c] = nine[8];
-            fwd[6 * hw + c] = __int_as_float(cell);
+    const int64_t cc = a.col_cap;
+    float *bwd = a.cols + (fld * 2 + 0) * rows * cc;
+    float *fwd = a.cols + (fld * 2 + 1) * rows * cc;
+    for (int m = 0; m < a.h.n_caf; m++) {
+        const int hw = a.h.aH[m] * a.h.aW[m];
+        const float stride = (float)a.h.astride[m];
+        const float *p = a.h.caf[m] + fld * 9 * hw;
+        const int coff = (int)a.h.caf_off[m];
+        for (int cell = threadIdx.x; cell < hw; cell += 256) {
+            float nine[9], sb, sf;
+            bool kb, kf;
+            score_cell(p, hw, stride, m, cell, nine, kb, kf, sb, sf);
+            const int key = coff + cell;
+            if (INDEX_ONLY) {
+                if (kb)
+                    reinterpret_cast<int *>(bwd)[atomicAdd(
+                        &s_cnt[0][caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e)], 1)] = key;
+                if (kf)
+                    reinterpret_cast<int *>(fwd)[atomicAdd(
+                        &s_cnt[1][caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e)], 1)] = key;
+                continue;
+            }
+            // the kColRows rows the grow kernel reads: score, source x, y, target x, y, target
+            // scale, index.  Backward sets are the reference's rows (0, 5, 6, 7, 8, 1, 2, 3, 4)
+            // with row 0 = scores_b, so their source is (x2, y2) and their target (x1, y1, s1).
+            if (kb) {
+                const int64_t c = atomicAdd(&s_cnt[0][caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e)], 1);
+                bwd[c] = sb;
+                bwd[1 * cc + c] = nine[5];
+                bwd[2 * cc + c] = nine[6];
+                bwd[3 * cc + c] = nine[1];
+                bwd[4 * cc + c] = nine[2];
+                bwd[5 * cc + c] = nine[4];
+                bwd[6 * cc + c] = __int_as_float(key);
+            }
+            if (kf) {
+                const int64_t c = atomicAdd(&s_cnt[1][caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e)], 1);
+                fwd[c] = sf;
+                fwd[1 * cc + c] = nine[1];
+                fwd[2 * cc + c] = nine[2];
+                fwd[3 * cc + c] = nine[5];
+                fwd[4 * cc + c] = nine[6];
+                fwd[5 * cc + c] = nine[8];
+                fwd[6 * cc + c] = __int_as_float(key);
+            }
         }
     }
 }
 
 static inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 
-int launch_seeds(const float *cif, const float *hr, int n_img, int K, int H, int W,
-                 const pp_config *cfg, pp_seed *seeds, int cap, int *counts, void *scratch,
-                 hipStream_t s) {
+int launch_seeds(const Heads &h, const float *hr, int n_img, int K, const pp_config *cfg,
+                 pp_seed *seeds, int cap, int *counts, void *scratch, hipStream_t s) {
     if (K > PP_MAX_KP) return fail(PP_ESHAPE, "seeds: more than PP_MAX_KP CIF fields");
-    if ((int64_t)cap < (int64_t)K * H * W) return fail(PP_ESHAPE, "seeds: capacity < K*H*W");
+    if ((int64_t)cap < (int64_t)K * h.cif_cells())
+        return fail(PP_ESHAPE, "seeds: capacity < K * cells");
     SeedArgs a{};
-    a.cif = cif;
+    a.h = h;
     a.hr = hr;
     a.K = K;
-    a.H = H;
-    a.W = W;
-    a.hh = (int)hr_dim(H, cfg->stride);
-    a.ww = (int)hr_dim(W, cfg->stride);
+    a.hh = (int)hr_dim(h.cH[0], h.cstride[0]);
+    a.ww = (int)hr_dim(h.cW[0], h.cstride[0]);
     a.pitch = pp_cifhr_pitch(a.ww);
-    a.stride = (float)cfg->stride;
     a.th = cfg->seed_threshold;
     a.score_scale = cfg->seed_score_scale;
     a.seeds = seeds;
@@ -567,9 +611,9 @@ int launch_seeds(const float *cif, const float *hr, int n_img, int K, int H, int
     a.g_f = (int *)w;
     w += round_up((int64_t)n_img * cap * sizeof(int), 256);
     a.f_counts = (int *)w;
-    w += round_up((int64_t)n_img * K * sizeof(int), 256);
+    w += round_up((int64_t)n_img * kMaxHeads * PP_MAX_KP * sizeof(int), 256);
     a.g_perm = (int *)w;
-    hipLaunchKernelGGL(seeds_emit_kernel, dim3((unsigned)((int64_t)n_img * K)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(seeds_emit_kernel, dim3((unsigned)((int64_t)n_img * h.n_cif * K)), dim3(256), 0, s, a);
     hipLaunchKernelGGL(seeds_sort_kernel, dim3(n_img), dim3(1024), 0, s, a);
     return check_launch("pp_seeds");
 }
@@ -579,25 +623,25 @@ size_t seeds_scratch_size(int n_img, int cap) {
     while (np < cap) np <<= 1;
     return round_up((int64_t)n_img * 4 * cap * sizeof(float), 256) +
            round_up((int64_t)n_img * cap * sizeof(int), 256) +
-           round_up((int64_t)n_img * PP_MAX_KP * sizeof(int), 256) +
+           round_up((int64_t)n_img * kMaxHeads * PP_MAX_KP * sizeof(int), 256) +
            round_up((int64_t)n_img * 2 * np * sizeof(int), 256);
 }
 
-int launch_caf_scored(const float *caf, const float *hr, int n_img, int K, int C, int H, int W,
+int launch_caf_scored(const Heads &h, const float *hr, int n_img, int K, int C,
                       const int32_t *skeleton, const pp_config *cfg, int nt, const float *th,
-                      float *const *cols, int *const *counts, hipStream_t s, const int *gate) {
+                      float *const *cols, int64_t col_cap, int *const *counts, hipStream_t s,
+                      const int *gate) {
     if (C > kMaxCaf) return fail(PP_ESHAPE, "caf_scored: more than PP_MAX_EDGES CAF fields");
+    if (col_cap < h.caf_cells()) return fail(PP_ESHAPE, "caf_scored: column capacity < cells");
     CafArgs a{};
-    a.caf = caf;
+    a.h = h;
     a.hr = hr;
     a.K = K;
     a.C = C;
-    a.H = H;
-    a.W = W;
-    a.hh = (int)hr_dim(H, cfg->stride);
-    a.ww = (int)hr_dim(W, cfg->stride);
+    a.hh = (int)hr_dim(h.cH[0], h.cstride[0]);
+    a.ww = (int)hr_dim(h.cW[0], h.cstride[0]);
     a.pitch = pp_cifhr_pitch(a.ww);
-    a.stride = (float)cfg->stride;
+    a.col_cap = col_cap;
     a.cif_floor = cfg->cif_floor;
     a.one_minus_floor = (float)(1.0 - (double)cfg->cif_floor);  // (1.0 - self.cif_floor)
     a.nt = nt;
@@ -616,7 +660,7 @@ int launch_caf_scored(const float *caf, const float *hr, int n_img, int K, int C
     return check_launch("pp_caf_scored");
 }
 
-// bucket geometry for an H x W field: edge e = stride * 2^k px with <= 1600 buckets
+// bucket geometry for the CifHr map (head 0): edge e = stride * 2^k px with <= 1600 buckets
 void caf_bucket_grid(int H, int W, int stride, int *bw, int *bh, int *nb, float *inv_e) {
     const int hh = (int)hr_dim(H, stride), ww = (int)hr_dim(W, stride);
     int e = stride;
@@ -627,25 +671,23 @@ void caf_bucket_grid(int H, int W, int stride, int *bw, int *bh, int *nb, float 
     *inv_e = 1.0f / (float)e;
 }
 
-int launch_caf_bucketed(const float *caf, const float *hr, int n_img, int K, int C, int H, int W,
+int launch_caf_bucketed(const Heads &h, const float *hr, int n_img, int K, int C,
                         const int32_t *skeleton, const pp_config *cfg, float th, float *cols,
                         int *offs, const int *gate, bool index_only, hipStream_t s) {
     if (C > kMaxCaf) return fail(PP_ESHAPE, "caf_scored: more than PP_MAX_EDGES CAF fields");
     CafBArgs a{};
-    a.caf = caf;
+    a.h = h;
     a.hr = hr;
     a.K = K;
     a.C = C;
-    a.H = H;
-    a.W = W;
-    a.hh = (int)hr_dim(H, cfg->stride);
-    a.ww = (int)hr_dim(W, cfg->stride);
+    a.hh = (int)hr_dim(h.cH[0], h.cstride[0]);
+    a.ww = (int)hr_dim(h.cW[0], h.cstride[0]);
     a.pitch = pp_cifhr_pitch(a.ww);
-    a.stride = (float)cfg->stride;
+    a.col_cap = h.caf_cells();
     a.cif_floor = cfg->cif_floor;
     a.one_minus_floor = (float)(1.0 - (double)cfg->cif_floor);
     a.th = th;
-    caf_bucket_grid(H, W, cfg->stride, &a.bw, &a.bh, &a.nb, &a.inv_e);
+    caf_bucket_grid(h.cH[0], h.cW[0], h.cstride[0], &a.bw, &a.bh, &a.nb, &a.inv_e);
     a.cols = cols;
     a.offs = offs;
     a.gate = gate;
@@ -668,21 +710,39 @@ using namespace pp;
 
 extern "C" {
 
-int pp_seeds(const float *d_cif, const float *d_cifhr, int32_t n_img, int32_t K, int32_t H,
-             int32_t W, const pp_config *cfg, pp_seed *d_seeds, int32_t seed_capacity,
-             int32_t *d_counts, void *stream) {
-    if (!d_cif || !d_cifhr || !cfg || !d_seeds || !d_counts) return fail(PP_EINVAL, "pp_seeds: NULL argument");
-    if (n_img < 0 || K <= 0 || H <= 0 || W <= 0 || seed_capacity <= 0)
-        return fail(PP_ESHAPE, "pp_seeds: bad shape");
+static int seeds_entry(const Heads &h, const float *d_cifhr, int32_t n_img, int32_t K,
+                       const pp_config *cfg, pp_seed *d_seeds, int32_t seed_capacity,
+                       int32_t *d_counts, void *stream) {
+    if (!d_cifhr || !cfg || !d_seeds || !d_counts) return fail(PP_EINVAL, "pp_seeds: NULL argument");
+    if (n_img < 0 || K <= 0 || seed_capacity <= 0) return fail(PP_ESHAPE, "pp_seeds: bad shape");
     if (n_img == 0) return PP_OK;
     void *scratch = nullptr;
     hipStream_t s = (hipStream_t)stream;
     if (hipMallocAsync(&scratch, seeds_scratch_size(n_img, seed_capacity), s) != hipSuccess)
         return fail(PP_EHIP, "pp_seeds: scratch allocation failed");
-    int rc = launch_seeds(d_cif, d_cifhr, n_img, K, H, W, cfg, d_seeds, seed_capacity, d_counts,
-                          scratch, s);
+    int rc = launch_seeds(h, d_cifhr, n_img, K, cfg, d_seeds, seed_capacity, d_counts, scratch, s);
     hipFreeAsync(scratch, s);
     return rc;
+}
+
+int pp_seeds(const float *d_cif, const float *d_cifhr, int32_t n_img, int32_t K, int32_t H,
+             int32_t W, const pp_config *cfg, pp_seed *d_seeds, int32_t seed_capacity,
+             int32_t *d_counts, void *stream) {
+    if (!d_cif || !cfg) return fail(PP_EINVAL, "pp_seeds: NULL argument");
+    if (H <= 0 || W <= 0 || cfg->stride <= 0) return fail(PP_ESHAPE, "pp_seeds: bad shape");
+    return seeds_entry(single_head(d_cif, nullptr, H, W, cfg->stride), d_cifhr, n_img, K, cfg,
+                       d_seeds, seed_capacity, d_counts, stream);
+}
+
+int pp_seeds_multi(const pp_scale *scales, int32_t n_scales, const float *d_cifhr, int32_t n_img,
+                   int32_t K, const pp_config *cfg, pp_seed *d_seeds, int32_t seed_capacity,
+                   int32_t *d_counts, void *stream) {
+    Heads h;
+    const int rc = make_heads(scales, n_scales, 0, PP_ROLE_CIF, &h, "pp_seeds_multi");
+    if (rc) return rc;
+    for (int m = 0; m < h.n_cif; m++)
+        if (!h.cif[m]) return fail(PP_EINVAL, "pp_seeds_multi: NULL field");
+    return seeds_entry(h, d_cifhr, n_img, K, cfg, d_seeds, seed_capacity, d_counts, stream);
 }
 
 int pp_caf_scored(const float *d_caf, const float *d_cifhr, int32_t n_img, int32_t K, int32_t C,
@@ -690,12 +750,34 @@ int pp_caf_scored(const float *d_caf, const float *d_cifhr, int32_t n_img, int32
                   const pp_config *cfg, float *d_cols, int32_t *d_counts, void *stream) {
     if (!d_caf || !d_cifhr || !skeleton || !cfg || !d_cols || !d_counts)
         return fail(PP_EINVAL, "pp_caf_scored: NULL argument");
-    if (n_img < 0 || K <= 0 || C <= 0 || H <= 0 || W <= 0) return fail(PP_ESHAPE, "pp_caf_scored: bad shape");
+    if (n_img < 0 || K <= 0 || C <= 0 || H <= 0 || W <= 0 || cfg->stride <= 0)
+        return fail(PP_ESHAPE, "pp_caf_scored: bad shape");
     if (n_img == 0) return PP_OK;
     float *cols[1] = {d_cols};
     int *counts[1] = {d_counts};
-    return launch_caf_scored(d_caf, d_cifhr, n_img, K, C, H, W, skeleton, cfg, 1, &score_th, cols,
-                             counts, (hipStream_t)stream, nullptr);
+    return launch_caf_scored(single_head(nullptr, d_caf, H, W, cfg->stride), d_cifhr, n_img, K, C,
+                             skeleton, cfg, 1, &score_th, cols, (int64_t)H * W, counts,
+                             (hipStream_t)stream, nullptr);
+}
+
+int pp_caf_scored_multi(const pp_scale *scales, int32_t n_scales, const float *d_cifhr,
+                        int32_t n_img, int32_t K, int32_t C, const int32_t *skeleton,
+                        float score_th, const pp_config *cfg, float *d_cols,
+                        int64_t col_capacity, int32_t *d_counts, void *stream) {
+    Heads h;
+    // the CIF heads give the CifHr map's geometry (CIF head 0); their fields are not read
+    const int rc = make_heads(scales, n_scales, 0, PP_ROLE_CIF | PP_ROLE_CAF, &h, "pp_caf_scored_multi");
+    if (rc) return rc;
+    if (!d_cifhr || !skeleton || !cfg || !d_cols || !d_counts)
+        return fail(PP_EINVAL, "pp_caf_scored_multi: NULL argument");
+    for (int m = 0; m < h.n_caf; m++)
+        if (!h.caf[m]) return fail(PP_EINVAL, "pp_caf_scored_multi: NULL field");
+    if (n_img < 0 || K <= 0 || C <= 0) return fail(PP_ESHAPE, "pp_caf_scored_multi: bad shape");
+    if (n_img == 0) return PP_OK;
+    float *cols[1] = {d_cols};
+    int *counts[1] = {d_counts};
+    return launch_caf_scored(h, d_cifhr, n_img, K, C, skeleton, cfg, 1, &score_th, cols,
+                             col_capacity, counts, (hipStream_t)stream, nullptr);
 }
 
 }  // extern "C"

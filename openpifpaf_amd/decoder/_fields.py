@@ -37,3 +37,21 @@ def pitched_hr(cifhr, stride_unused=None):
 
 def cfg_ptr(cfg):
     return ctypes.byref(cfg)
+
+
+def head_scales(fields, config, role):
+    """pp_scale list of a FieldConfig's heads for one image: (array, the batch-1 device
+    tensors it points into).  role 'cif' lists the CIF heads; 'caf' the CAF heads after the
+    CIF heads' shapes (CIF head 0 gives the CifHr geometry; their fields are not read)."""
+    from .._abi import scale_list  # pylint: disable=import-outside-toplevel
+    if role == 'cif':
+        ts = [batch1(fields[i]) for i in config.cif_indices]
+        arr = scale_list([(t.data_ptr(), t.shape[3], t.shape[4]) for t in ts], [],
+                         config.cif_strides, [], config.cif_min_scales)
+        return arr, ts
+    ts = [batch1(fields[i]) for i in config.caf_indices]
+    geo = [(None, fields[i].shape[-2], fields[i].shape[-1]) for i in config.cif_indices]
+    arr = scale_list(geo, [(t.data_ptr(), t.shape[3], t.shape[4]) for t in ts],
+                     config.cif_strides, config.caf_strides, None, config.caf_min_distances,
+                     config.caf_max_distances)
+    return arr, ts

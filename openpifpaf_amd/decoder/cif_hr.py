@@ -13,7 +13,7 @@ from .. import _device
 from .._abi import make_config
 from .._lib import call, load
 from ..functional import scalar_square_add_gauss_with_max
-from ._fields import batch1, hr_geometry
+from ._fields import batch1, head_scales, hr_geometry
 from .field_config import FieldConfig
 
 
@@ -78,9 +78,42 @@ class CifHr:
             acc.cpu().numpy())
         return self
 
+    def fill_multiple(self, cifs, stride, min_scale=0.0):
+        """cif_hr.py:42-57 for the first group (1 or 2 heads at one stride)."""
+        if self.accumulated is not None:
+            raise NotImplementedError('accumulating into an existing map: use fill()')
+        if len(cifs) == 1 and not min_scale:
+            return self.fill_cif(cifs[0], stride)
+        if len(cifs) > 2:
+            raise NotImplementedError('fill_multiple over more than two heads')
+        n = len(cifs)
+        fc = FieldConfig(cif_indices=list(range(n)), cif_strides=[stride] * n,
+                         cif_min_scales=[min_scale] * n)
+        return self._fill_heads(cifs, fc, pairs=int(n == 2))
+
     def fill(self, fields):
-        cif_i, _, stride = self.config.single_scale()
-        return self.fill_cif(fields[cif_i], stride)
+        """cif_hr.py:59-73: every CIF head of the FieldConfig, pairs when there are 10."""
+        if self.config.is_single_scale():
+            cif_i, _, stride = self.config.single_scale()
+            return self.fill_cif(fields[cif_i], stride)
+        return self._fill_heads(fields, self.config, pairs=int(len(self.config.cif_indices) == 10))
+
+    def _fill_heads(self, fields, config, pairs):
+        arr, ts = head_scales(fields, config, 'cif')
+        _, k, _, h, w = ts[0].shape
+        stride = int(config.cif_strides[0])
+        hh, ww, pitch = hr_geometry(h, w, stride)
+        lib = load()
+        out = torch.empty((1, k, hh, pitch), dtype=torch.float32, device=ts[0].device)
+        ws = torch.empty(int(lib.pp_cifhr_multi_workspace_size(arr, len(arr), pairs, 1, k)),
+                         dtype=torch.uint8, device=ts[0].device)
+        cfg = make_config(cif_threshold=self.v_threshold, cif_neighbors=self.neighbors)
+        call('pp_cifhr_multi', arr, len(arr), pairs, 1, k, ctypes.byref(cfg), _device.ptr(out),
+             _device.ptr(ws), ctypes.c_size_t(ws.numel()), _device.stream())
+        acc = out[0, :, :, :ww]
+        host = not any(_device.is_device(fields[i]) for i in config.cif_indices)
+        self.accumulated = np.ascontiguousarray(acc.cpu().numpy()) if host else acc
+        return self
 
 
 class CifDetHr(CifHr):

@@ -6,7 +6,7 @@ import torch
 from .. import _device
 from .._abi import SEED_DTYPE, make_config
 from .._lib import call
-from ._fields import batch1, cfg_ptr, pitched_hr
+from ._fields import batch1, cfg_ptr, head_scales, pitched_hr
 from .field_config import FieldConfig
 
 
@@ -47,8 +47,30 @@ class CifSeeds:
         return sorted(self.seeds, reverse=True)
 
     def fill(self, fields):
-        cif_i, _, stride = self.config.single_scale()
-        return self.fill_cif(fields[cif_i], stride, seed_mask=self.config.seed_mask)
+        """cif_seeds.py:56-64: every CIF head of the FieldConfig, in order."""
+        if self.config.is_single_scale():
+            cif_i, _, stride = self.config.single_scale()
+            return self.fill_cif(fields[cif_i], stride, seed_mask=self.config.seed_mask)
+        if self.threshold is None:
+            raise TypeError("'>' not supported between instances of 'numpy.ndarray' and "
+                            "'NoneType' (CifSeeds.threshold is not configured)")
+        if self.config.seed_mask is not None:
+            raise NotImplementedError('seed_mask is not implemented')
+        arr, ts = head_scales(fields, self.config, 'cif')
+        k = ts[0].shape[1]
+        cap = k * sum(t.shape[3] * t.shape[4] for t in ts)
+        hr = pitched_hr(self.cifhr)
+        out = torch.empty(cap * SEED_DTYPE.itemsize, dtype=torch.uint8, device=ts[0].device)
+        count = torch.zeros(1, dtype=torch.int32, device=ts[0].device)
+        cfg = make_config(seed_threshold=self.threshold, seed_score_scale=self.score_scale)
+        call('pp_seeds_multi', arr, len(arr), _device.ptr(hr), 1, k, cfg_ptr(cfg),
+             _device.ptr(out), cap, _device.ptr(count), _device.stream())
+        n = int(count.item())
+        recs = np.frombuffer(out[:n * SEED_DTYPE.itemsize].cpu().numpy().tobytes(),
+                             dtype=SEED_DTYPE)
+        self.seeds.extend((v, int(f), x, y, s) for v, f, x, y, s in
+                          zip(recs['v'], recs['field'], recs['x'], recs['y'], recs['s']))
+        return self
 
 
 class CifDetSeeds(CifSeeds):

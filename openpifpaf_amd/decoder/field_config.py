@@ -24,15 +24,16 @@ class FieldConfig:
         assert len(self.caf_strides) == len(self.caf_min_distances)
         assert len(self.caf_strides) == len(self.caf_max_distances)
 
+    def is_single_scale(self):
+        """One CIF and one CAF head at one stride without min-scale / distance masks: the
+        pp_decode_stages path.  Everything else runs pp_decode_multi."""
+        return (len(self.cif_indices) == 1 and len(self.caf_indices) == 1
+                and not any(self.cif_min_scales) and not any(self.caf_min_distances)
+                and all(d is None or not d for d in self.caf_max_distances)
+                and self.cif_strides[0] == self.caf_strides[0])
+
     def single_scale(self):
-        """The device decoder covers the single-scale configuration (one CIF, one CAF
-        head, no min-scale / distance masks).  Multi-scale fusion (factory.py:153-180) is
-        the next row of SURVEY.md §8(f)."""
-        if (len(self.cif_indices) != 1 or len(self.caf_indices) != 1
-                or any(self.cif_min_scales) or any(self.caf_min_distances)
-                or any(d is not None for d in self.caf_max_distances)):
-            raise NotImplementedError('multi-scale field configurations are not implemented '
-                                      'on the device decoder yet')
-        if self.cif_strides[0] != self.caf_strides[0]:
-            raise NotImplementedError('CIF and CAF strides must match')
+        """(cif index, caf index, stride) of a single-scale configuration."""
+        if not self.is_single_scale():
+            raise NotImplementedError('not a single-scale field configuration')
         return self.cif_indices[0], self.caf_indices[0], int(self.cif_strides[0])

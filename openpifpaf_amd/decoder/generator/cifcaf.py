@@ -16,7 +16,7 @@ import numpy as np
 from ... import _device
 from ..._abi import make_config, skeleton_array
 from ...annotation import Annotation
-from ...engine import engine
+from ...engine import HeadSet, engine
 from ...functional import grow_connection_blend
 from .. import nms as nms_module
 from ..caf_scored import CafScored
@@ -69,7 +69,7 @@ class CifCaf(Generator):
     # -- configuration -------------------------------------------------------------------
     def config(self):
         """pp_config from the class attributes decoder.configure() writes (factory.py:64-98)."""
-        _, _, stride = self.field_config.single_scale()
+        stride = int(self.field_config.cif_strides[0])  # multi-scale heads carry their own
         if CifSeeds.threshold is None:
             raise TypeError('CifSeeds.threshold is not configured (decoder.configure sets it)')
         nms = self.nms
@@ -93,13 +93,20 @@ class CifCaf(Generator):
 
     # -- decoding ------------------------------------------------------------------------
     def __call__(self, fields, initial_annotations=None):
-        """One image: fields = [cif (K, 5, H, W), caf (C, 9, H, W)] (numpy or device)."""
+        """One image: fields = the head outputs [cif (K, 5, H, W), caf (C, 9, H, W), ...]
+        (numpy or device), read through the FieldConfig (single- or multi-scale)."""
         if initial_annotations:
             raise NotImplementedError('initial_annotations are not implemented on the device')
-        cif_i, caf_i, _ = self.field_config.single_scale()
         start = time.perf_counter()
-        anns = self.decode_batch(_device.to_device(fields[cif_i])[None],
-                                 _device.to_device(fields[caf_i])[None])[0]
+        if self.field_config.is_single_scale():
+            cif_i, caf_i, _ = self.field_config.single_scale()
+            anns = self.decode_batch(_device.to_device(fields[cif_i])[None],
+                                     _device.to_device(fields[caf_i])[None])[0]
+        else:
+            used = set(self.field_config.cif_indices) | set(self.field_config.caf_indices)
+            batched = [_device.to_device(f)[None] if i in used else None
+                       for i, f in enumerate(fields)]
+            anns = self.decode_fields_batch(batched)[0]
         LOG.debug('%d annotations, %.3fs', len(anns), time.perf_counter() - start)
         return anns
 
@@ -110,14 +117,30 @@ class CifCaf(Generator):
         return engine().decode(cif, caf, skeleton_array(self.skeleton), self.config(),
                                keep_cifhr=keep_cifhr)
 
-    def decode_batch(self, cif_batch, caf_batch):
-        """(B, K, 5, H, W) + (B, C, 9, H, W) -> one list of Annotation per image."""
-        recs, offsets, _ = self.decode_records(cif_batch, caf_batch)
+    def decode_fields_records(self, fields_batch, keep_cifhr=False):
+        """Multi-scale device decode (pp_decode_multi): fields_batch is the head output list
+        with a batch dimension, indexed by the FieldConfig (factory.py:153-180)."""
+        heads = HeadSet([None if f is None else _device.to_device(f) for f in fields_batch],
+                        self.field_config)
+        return engine().decode(None, None, skeleton_array(self.skeleton), self.config(),
+                               keep_cifhr=keep_cifhr, heads=heads)
+
+    def _annotations(self, recs, offsets):
         out = []
         for i in range(len(offsets) - 1):
             out.append([Annotation.from_record(r, self.keypoints, self.out_skeleton)
                         for r in recs[offsets[i]:offsets[i + 1]]])
         return out
+
+    def decode_batch(self, cif_batch, caf_batch):
+        """(B, K, 5, H, W) + (B, C, 9, H, W) -> one list of Annotation per image."""
+        recs, offsets, _ = self.decode_records(cif_batch, caf_batch)
+        return self._annotations(recs, offsets)
+
+    def decode_fields_batch(self, fields_batch):
+        """Batched head outputs of any FieldConfig -> one list of Annotation per image."""
+        recs, offsets, _ = self.decode_fields_records(fields_batch)
+        return self._annotations(recs, offsets)
 
     # -- reference building blocks, on the device ------------------------------------------
     def _grow_connection(self, xy, xy_scale, caf_field):

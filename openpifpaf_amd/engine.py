@@ -14,7 +14,7 @@ import torch
 
 from . import _device
 from ._abi import (ANN_DTYPE, PP_ST_ANN_OVERFLOW, PP_ST_DEC_OVERFLOW, PP_ST_NMS_OVERFLOW,
-                   skeleton_array)
+                   scale_list, skeleton_array)
 from ._lib import PPError, call, load
 
 LOG = logging.getLogger(__name__)
@@ -29,24 +29,32 @@ def default_ann_capacity(h, w):
 
 
 class DecodeBuffers:
-    """Workspace + outputs for one (batch shape, config) combination."""
+    """Workspace + outputs for one (batch shape, config) combination.  `heads` (a HeadSet)
+    selects the multi-scale entry points."""
 
-    def __init__(self, n, k, c, h, w, cfg, cap, device):
+    def __init__(self, key, n, k, c, h, w, cfg, cap, device, heads=None):
         lib = load()
-        self.key = (n, k, c, h, w, cap, cfg.force_complete, cfg.stride,
-                    cfg.occupancy_reduction)
-        self.n, self.k, self.c, self.h, self.w, self.cap = n, k, c, h, w, cap
-        size = lib.pp_decode_workspace_size(n, k, c, h, w, ctypes.byref(cfg), cap)
-        zero_off = lib.pp_decode_workspace_zero_offset(n, k, c, h, w, ctypes.byref(cfg), cap)
+        self.key = key
+        self.n, self.k, self.c, self.cap = n, k, c, cap
+        if heads is None:
+            size = lib.pp_decode_workspace_size(n, k, c, h, w, ctypes.byref(cfg), cap)
+            zero_off = lib.pp_decode_workspace_zero_offset(n, k, c, h, w, ctypes.byref(cfg), cap)
+            stride = cfg.stride
+        else:
+            args = (heads.arr, len(heads.arr), heads.pairs, n, k, c, ctypes.byref(cfg), cap)
+            size = lib.pp_decode_multi_workspace_size(*args)
+            zero_off = lib.pp_decode_multi_workspace_zero_offset(*args)
+            stride = heads.stride0
         if size == 0:
-            raise PPError('pp_decode_workspace_size rejected the shape')
+            raise PPError('pp_decode_workspace_size rejected the shape: ' +
+                          lib.pp_last_error().decode())
         self.ws = torch.empty(size, dtype=torch.uint8, device=device)
         self.ws[zero_off:].zero_()
         self.anns = torch.empty(n * cap * ANN_DTYPE.itemsize, dtype=torch.uint8, device=device)
         self.counts = torch.zeros(n, dtype=torch.int32, device=device)
         self.status = torch.zeros(n, dtype=torch.int32, device=device)
-        self.hh = (h - 1) * cfg.stride + 1
-        self.ww = (w - 1) * cfg.stride + 1
+        self.hh = (h - 1) * stride + 1
+        self.ww = (w - 1) * stride + 1
         self.pitch = int(lib.pp_cifhr_pitch(self.ww))
         self.cifhr = None
 
@@ -57,15 +65,53 @@ class DecodeBuffers:
         return self.cifhr
 
 
+class HeadSet:
+    """The CIF and CAF heads of a FieldConfig for one batch of device fields
+    (field_config.py:7-13): `fields` is the head-network output list with a leading batch
+    dimension on every tensor.  Builds the pp_scale list of pp_decode_multi."""
+
+    def __init__(self, fields, fc):
+        self.cifs = [fields[i] for i in fc.cif_indices]
+        self.cafs = [fields[i] for i in fc.caf_indices]
+        for t in self.cifs + self.cafs:
+            if not _device.is_device(t) or t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError('multi-scale fields must be contiguous float32 device tensors')
+            if t.dim() != 5:
+                raise ValueError('expected batched fields (B, n_fields, channels, H, W)')
+        if any(t.shape[2] != 5 for t in self.cifs) or any(t.shape[2] != 9 for t in self.cafs):
+            raise ValueError('expected CIF heads (B, K, 5, H, W) and CAF heads (B, C, 9, H, W)')
+        self.n = self.cifs[0].shape[0]
+        self.k = self.cifs[0].shape[1]
+        self.c = self.cafs[0].shape[1]
+        if any(t.shape[0] != self.n for t in self.cifs + self.cafs):
+            raise ValueError('heads have different batch sizes')
+        if any(t.shape[1] != self.k for t in self.cifs) or any(t.shape[1] != self.c for t in self.cafs):
+            raise ValueError('heads have different field counts')
+        self.h, self.w = self.cifs[0].shape[3], self.cifs[0].shape[4]
+        self.stride0 = int(fc.cif_strides[0])
+        self.pairs = int(len(fc.cif_indices) == 10)  # cif_hr.py:63
+        self.arr = scale_list([(t.data_ptr(), t.shape[3], t.shape[4]) for t in self.cifs],
+                              [(t.data_ptr(), t.shape[3], t.shape[4]) for t in self.cafs],
+                              fc.cif_strides, fc.caf_strides, fc.cif_min_scales,
+                              fc.caf_min_distances, fc.caf_max_distances)
+        self.shape_key = (self.pairs,) + tuple(
+            (s.H, s.W, s.stride, s.role) for s in self.arr)
+
+
+def _buffer_key(n, k, c, shape, cap, cfg):
+    return (n, k, c, shape, cap, cfg.force_complete, cfg.stride, cfg.occupancy_reduction)
+
+
 class DecodeEngine:
     def __init__(self):
         self._bufs = None
 
-    def buffers(self, n, k, c, h, w, cfg, cap):
-        key = (n, k, c, h, w, cap, cfg.force_complete, cfg.stride, cfg.occupancy_reduction)
+    def buffers(self, n, k, c, h, w, cfg, cap, heads=None):
+        shape = (h, w) if heads is None else heads.shape_key
+        key = _buffer_key(n, k, c, shape, cap, cfg)
         if self._bufs is None or self._bufs.key != key:
             self._bufs = None  # free the previous workspace first
-            self._bufs = DecodeBuffers(n, k, c, h, w, cfg, cap, _device.require())
+            self._bufs = DecodeBuffers(key, n, k, c, h, w, cfg, cap, _device.require(), heads)
         return self._bufs
 
     def launch(self, cif, caf, skeleton, cfg, cap=None, keep_cifhr=False, stages=STAGE_ALL):
@@ -89,12 +135,32 @@ class DecodeEngine:
              _device.stream())
         return b
 
-    def decode(self, cif, caf, skeleton, cfg, cap=None, keep_cifhr=False):
-        """Full decode with overflow retry.  Returns (records, offsets, buffers)."""
-        n, _, _, h, w = cif.shape
+    def launch_multi(self, heads, skeleton, cfg, cap=None, keep_cifhr=False, stages=STAGE_ALL):
+        """pp_decode_multi over a HeadSet; returns the DecodeBuffers."""
+        skel = skeleton_array(skeleton)
+        if len(skel) != heads.c:
+            raise ValueError('skeleton has {} edges but caf has {} fields'.format(len(skel),
+                                                                                  heads.c))
+        cap = cap or default_ann_capacity(heads.h, heads.w)
+        b = self.buffers(heads.n, heads.k, heads.c, heads.h, heads.w, cfg, cap, heads)
+        hr = b.cifhr_buffer() if keep_cifhr else None
+        call('pp_decode_multi', heads.arr, len(heads.arr), heads.pairs, heads.n, heads.k,
+             heads.c, skel.ctypes.data_as(ctypes.c_void_p), ctypes.byref(cfg), _device.ptr(hr),
+             _device.ptr(b.anns), cap, _device.ptr(b.counts), _device.ptr(b.status),
+             _device.ptr(b.ws), ctypes.c_size_t(b.ws.numel()), ctypes.c_uint32(stages),
+             _device.stream())
+        return b
+
+    def decode(self, cif, caf, skeleton, cfg, cap=None, keep_cifhr=False, heads=None):
+        """Full decode with overflow retry.  Returns (records, offsets, buffers).  With a
+        HeadSet `heads`, cif / caf are ignored and the multi-scale decode runs."""
+        h, w = (cif.shape[3], cif.shape[4]) if heads is None else (heads.h, heads.w)
         cap = cap or default_ann_capacity(h, w)
         while True:
-            b = self.launch(cif, caf, skeleton, cfg, cap=cap, keep_cifhr=keep_cifhr)
+            if heads is None:
+                b = self.launch(cif, caf, skeleton, cfg, cap=cap, keep_cifhr=keep_cifhr)
+            else:
+                b = self.launch_multi(heads, skeleton, cfg, cap=cap, keep_cifhr=keep_cifhr)
             status = b.status.cpu().numpy()
             if not (status & PP_ST_ANN_OVERFLOW).any():
                 break

@@ -10,7 +10,7 @@ import subprocess
 
 import numpy as np
 
-from openpifpaf_amd._abi import ANN_DTYPE, SEED_DTYPE, Scale, make_config, skeleton_array
+from openpifpaf_amd._abi import ANN_DTYPE, SEED_DTYPE, make_config, scale_list, skeleton_array
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
@@ -122,23 +122,16 @@ class Members:
     """The heads of a multi-scale FieldConfig for the oracle: fields list + FieldConfig
     lists (cif_indices, caf_indices, strides, cif_min_scales, caf min / max distances)."""
 
-    def __init__(self, fields, *, cif_indices, caf_indices, cif_strides, cif_min_scales=None,
-                 caf_min_distances=None, caf_max_distances=None, **_):
-        n = len(cif_indices)
-        assert len(caf_indices) == n
+    def __init__(self, fields, *, cif_indices, caf_indices, cif_strides, caf_strides,
+                 cif_min_scales=None, caf_min_distances=None, caf_max_distances=None, **_):
         self.cifs = [_c32(fields[i]) for i in cif_indices]
         self.cafs = [_c32(fields[i]) for i in caf_indices]
-        self.arr = (Scale * n)()
-        for m in range(n):
-            cif, caf = self.cifs[m], self.cafs[m]
-            assert cif.shape[-2:] == caf.shape[-2:]
-            self.arr[m] = Scale(cif.ctypes.data, caf.ctypes.data, cif.shape[-2], cif.shape[-1],
-                                int(cif_strides[m]),
-                                float((cif_min_scales or [0.0] * n)[m] or 0.0),
-                                float((caf_min_distances or [0.0] * n)[m] or 0.0),
-                                float((caf_max_distances or [None] * n)[m] or 0.0))
-        self.n = n
-        self.pairs = int(n == 10)  # cif_hr.py:63
+        self.arr = scale_list([(c.ctypes.data, c.shape[-2], c.shape[-1]) for c in self.cifs],
+                              [(c.ctypes.data, c.shape[-2], c.shape[-1]) for c in self.cafs],
+                              cif_strides, caf_strides, cif_min_scales, caf_min_distances,
+                              caf_max_distances)
+        self.n = len(self.arr)
+        self.pairs = int(len(cif_indices) == 10)  # cif_hr.py:63
         self.k = self.cifs[0].shape[0]
         self.c = self.cafs[0].shape[0]
         self.hr_shape = (self.k,) + hr_shape(self.cifs[0].shape[-2], self.cifs[0].shape[-1],

@@ -1024,23 +1024,33 @@ EXPORT long orc_decode(const float *cif, const float *caf, int K, int C, int H, 
 
 /* ---- multi-scale (cif_hr.py:42-73, cif_seeds.py:56-64, caf_scored.py:32-98) ----------- */
 
+/* the CIF (role bit 1) or CAF (role bit 2) heads of a pp_scale list, in order */
+static int role_list(const pp_scale *sc, int n, int bit, const pp_scale **out) {
+    int k = 0;
+    for (int i = 0; i < n; i++)
+        if ((sc[i].role ? sc[i].role : 3) & bit) out[k++] = &sc[i];
+    return k;
+}
+
 /* CifHr.fill: with pairs (10 CIF heads) heads i and i + 5 accumulate into one map with
  * len_cifs = 2 at head i's stride / min scale; otherwise every head on its own.  Maps
  * combine by np.maximum in order.  out (K, H', W') from head 0's field size and stride. */
-EXPORT void orc_cifhr_multi(const pp_scale *sc, int n, int pairs, int K, const pp_config *cfg,
+EXPORT void orc_cifhr_multi(const pp_scale *all, int n_all, int pairs, int K, const pp_config *cfg,
                             float *out) {
-    long hh = hr_dim(sc[0].H, sc[0].stride), ww = hr_dim(sc[0].W, sc[0].stride);
+    const pp_scale *cl[2 * PP_MAX_SCALES];
+    int n = role_list(all, n_all, 1, cl);
+    long hh = hr_dim(cl[0]->H, cl[0]->stride), ww = hr_dim(cl[0]->W, cl[0]->stride);
     size_t plane = (size_t)hh * ww;
     float *ta = (float *)malloc(sizeof(float) * K * plane);
     int n_groups = pairs ? n / 2 : n;
     for (int gi = 0; gi < n_groups; gi++) {
         int members[2] = {gi, pairs ? gi + n / 2 : -1};
         int len = pairs ? 2 : 1;
-        float stride = (float)sc[gi].stride;
-        float min_scale = sc[gi].cif_min_scale;
+        float stride = (float)cl[gi]->stride;
+        float min_scale = cl[gi]->cif_min_scale;
         memset(ta, 0, sizeof(float) * K * plane);
         for (int mi = 0; mi < len; mi++) {
-            const pp_scale *m = &sc[members[mi]];
+            const pp_scale *m = cl[members[mi]];
             long hw = (long)m->H * m->W;
             float *xs = (float *)malloc(sizeof(float) * 4 * (size_t)(hw + 1));
             float *ys = xs + hw, *ss = ys + hw, *vs = ss + hw;
@@ -1076,23 +1086,25 @@ EXPORT void orc_cifhr_multi(const pp_scale *sc, int n, int pairs, int K, const p
 }
 
 /* CifSeeds.fill over every CIF head in order; sorted as get() */
-EXPORT long orc_seeds_multi(const pp_scale *sc, int n, int K, const float *hr, long hh, long ww,
-                            const pp_config *cfg, pp_seed *out, long cap) {
+EXPORT long orc_seeds_multi(const pp_scale *all, int n_all, int K, const float *hr, long hh,
+                            long ww, const pp_config *cfg, pp_seed *out, long cap) {
+    const pp_scale *cl[2 * PP_MAX_SCALES];
+    int n = role_list(all, n_all, 1, cl);
     long total = 0;
-    for (int m = 0; m < n; m++) total += (long)K * sc[m].H * sc[m].W;
+    for (int m = 0; m < n; m++) total += (long)K * cl[m]->H * cl[m]->W;
     float *tmp = (float *)malloc(sizeof(float) * 6 * (size_t)(total + 1));
     long k = 0;
     for (int m = 0; m < n; m++) {
-        long hw = (long)sc[m].H * sc[m].W;
-        float stride = (float)sc[m].stride;
+        long hw = (long)cl[m]->H * cl[m]->W;
+        float stride = (float)cl[m]->stride;
         for (int f = 0; f < K; f++) {
-            const float *p = sc[m].cif + (size_t)f * 5 * hw;
+            const float *p = cl[m]->cif + (size_t)f * 5 * hw;
             const float *t = hr + (size_t)f * hh * ww;
             for (long c = 0; c < hw; c++) {
                 float conf = p[c];
                 if (!(conf > cfg->seed_threshold)) continue;
-                if (sc[m].cif_min_scale != 0.0f &&
-                    !(p[4 * hw + c] > (float)((double)sc[m].cif_min_scale / sc[m].stride)))
+                if (cl[m]->cif_min_scale != 0.0f &&
+                    !(p[4 * hw + c] > (float)((double)cl[m]->cif_min_scale / cl[m]->stride)))
                     continue;
                 float x = p[1 * hw + c] * stride, y = p[2 * hw + c] * stride, v;
                 orc_scalar_values(t, hh, ww, ww, 1, &x, &y, 1, 0.0f, &v);
@@ -1125,9 +1137,11 @@ EXPORT long orc_seeds_multi(const pp_scale *sc, int n, int K, const float *hr, l
 
 /* CafScored.fill over every CAF head in order: per field the heads' columns concatenated.
  * cols (C, 2, 9, cap) with cap >= sum of H*W over the heads */
-EXPORT void orc_caf_scored_multi(const pp_scale *sc, int n, int K, int C, const float *hr, long hh,
-                                 long ww, const int32_t *skel, float score_th, const pp_config *cfg,
-                                 float *cols, long cap, int32_t *counts) {
+EXPORT void orc_caf_scored_multi(const pp_scale *all, int n_all, int K, int C, const float *hr,
+                                 long hh, long ww, const int32_t *skel, float score_th,
+                                 const pp_config *cfg, float *cols, long cap, int32_t *counts) {
+    const pp_scale *al[2 * PP_MAX_SCALES];
+    int n = role_list(all, n_all, 2, al);
     float floor_ = cfg->cif_floor;
     float one_minus = (float)(1.0 - (double)cfg->cif_floor);
     for (int i = 0; i < C; i++) {
@@ -1136,11 +1150,11 @@ EXPORT void orc_caf_scored_multi(const pp_scale *sc, int n, int K, int C, const 
         int j1i = skel[2 * i] - 1, j2i = skel[2 * i + 1] - 1;
         long nb = 0, nf = 0;
         for (int m = 0; m < n; m++) {
-            long hw = (long)sc[m].H * sc[m].W;
-            float stride = (float)sc[m].stride;
-            const float *p = sc[m].caf + (size_t)i * 9 * hw;
-            float dmin = sc[m].caf_min_distance, dmax = sc[m].caf_max_distance;
-            float tmin = (float)((double)dmin / sc[m].stride), tmax = (float)((double)dmax / sc[m].stride);
+            long hw = (long)al[m]->H * al[m]->W;
+            float stride = (float)al[m]->stride;
+            const float *p = al[m]->caf + (size_t)i * 9 * hw;
+            float dmin = al[m]->caf_min_distance, dmax = al[m]->caf_max_distance;
+            float tmin = (float)((double)dmin / al[m]->stride), tmax = (float)((double)dmax / al[m]->stride);
             for (long c = 0; c < hw; c++) {
                 float nine[9];
                 nine[0] = p[c];
@@ -1188,23 +1202,25 @@ EXPORT void orc_caf_scored_multi(const pp_scale *sc, int n, int K, int C, const 
 EXPORT long orc_decode_multi(const pp_scale *sc, int n, int pairs, int K, int C,
                              const int32_t *skel, const pp_config *cfg, pp_ann *out, long cap) {
     if (K > PP_MAX_KP || C > PP_MAX_EDGES || K <= 0 || C <= 0 || n <= 0) return -1;
-    if (pairs && n != 10) return -1;
-    long total_hw = 0;
-    for (int m = 0; m < n; m++) {
+    const pp_scale *cl[2 * PP_MAX_SCALES], *al[2 * PP_MAX_SCALES];
+    int n_cif = role_list(sc, n, 1, cl), n_caf = role_list(sc, n, 2, al);
+    if (n_cif == 0 || n_caf == 0 || (pairs && (n_cif & 1))) return -1;
+    long total_hw = 0, cif_hw = 0;
+    for (int m = 0; m < n; m++)
         if (sc[m].H <= 0 || sc[m].W <= 0 || sc[m].stride <= 0) return -1;
-        total_hw += (long)sc[m].H * sc[m].W;
-    }
-    long hh = hr_dim(sc[0].H, sc[0].stride), ww = hr_dim(sc[0].W, sc[0].stride);
+    for (int m = 0; m < n_cif; m++) cif_hw += (long)cl[m]->H * cl[m]->W;
+    for (int m = 0; m < n_caf; m++) total_hw += (long)al[m]->H * al[m]->W;
+    long hh = hr_dim(cl[0]->H, cl[0]->stride), ww = hr_dim(cl[0]->W, cl[0]->stride);
     float *hr = (float *)malloc(sizeof(float) * (size_t)K * hh * ww);
     orc_cifhr_multi(sc, n, pairs, K, cfg, hr);
-    pp_seed *seeds = (pp_seed *)malloc(sizeof(pp_seed) * (size_t)(K * total_hw + 1));
-    long n_seeds = orc_seeds_multi(sc, n, K, hr, hh, ww, cfg, seeds, K * total_hw);
+    pp_seed *seeds = (pp_seed *)malloc(sizeof(pp_seed) * (size_t)(K * cif_hw + 1));
+    long n_seeds = orc_seeds_multi(sc, n, K, hr, hh, ww, cfg, seeds, K * cif_hw);
 
     dec_t d;
     d.K = K;
     d.C = C;
-    d.H = sc[0].H;
-    d.W = sc[0].W;
+    d.H = cl[0]->H;
+    d.W = cl[0]->W;
     d.hw = total_hw; /* column capacity of every (connection, direction) set */
     d.cfg = cfg;
     build_by_source(&d, skel);

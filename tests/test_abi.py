@@ -120,3 +120,29 @@ int main(void) {
     d = _abi.DET_DTYPE
     assert vals == [d.itemsize, d.fields['score'][1], d.fields['bbox'][1], d.fields['image'][1],
                     ctypes.sizeof(_abi.DetNms), _abi.DetNms.apply.offset]
+
+
+def test_scale_struct_and_multi_workspace():
+    """pp_scale layout and the host-only multi-scale sizing entry points (no GPU needed)."""
+    import ctypes
+    from openpifpaf_amd._abi import ROLE_CAF, ROLE_CIF, Scale, make_config, scale_list
+    from openpifpaf_amd._lib import load
+    assert ctypes.sizeof(Scale) == 48
+    lib = load()
+    cfg = make_config()
+    arr = scale_list([(0, 41, 41), (0, 21, 21)], [(0, 41, 41), (0, 21, 21)], [8, 16], [8, 16],
+                     [0.0, 12.0], [0.0, 36.0], [160.0, None])
+    assert [s.role for s in arr] == [ROLE_CIF, ROLE_CIF, ROLE_CAF, ROLE_CAF]
+    size = lib.pp_decode_multi_workspace_size(arr, 4, 0, 2, 17, 19, ctypes.byref(cfg), 128)
+    zero = lib.pp_decode_multi_workspace_zero_offset(arr, 4, 0, 2, 17, 19, ctypes.byref(cfg), 128)
+    assert 0 < zero < size
+    # one CIF + one CAF head of the single-scale shape sizes like pp_decode_workspace_size
+    one = scale_list([(0, 41, 41)], [(0, 41, 41)], [8], [8])
+    assert (lib.pp_decode_multi_workspace_size(one, 2, 0, 2, 17, 19, ctypes.byref(cfg), 128)
+            == lib.pp_decode_workspace_size(2, 17, 19, 41, 41, ctypes.byref(cfg), 128))
+    # pairs need an even CIF head count; no CAF head is rejected
+    odd = scale_list([(0, 41, 41)] * 3, [(0, 41, 41)], [8] * 3, [8])
+    assert lib.pp_decode_multi_workspace_size(odd, 4, 1, 1, 17, 19, ctypes.byref(cfg), 128) == 0
+    cif_only = scale_list([(0, 41, 41)], [], [8], [])
+    assert lib.pp_decode_multi_workspace_size(cif_only, 1, 0, 1, 17, 19, ctypes.byref(cfg), 128) == 0
+    assert lib.pp_cifhr_multi_workspace_size(cif_only, 1, 0, 1, 17) > 0

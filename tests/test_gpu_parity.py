@@ -558,3 +558,132 @@ def test_annotations_inverse_vs_reference(name):
     assert json.dumps([a.json_data() for a in dinv]) == str(g[name + '_det_json'])
     recs = eval_coco.coco_predictions(anns, meta)
     assert [r['image_id'] for r in recs] == [7] * len(anns)
+
+
+# ---- multi-scale FieldConfig (cif_hr.py:59-73, cif_seeds.py:56-64, caf_scored.py:88-98) ----
+
+MULTI_NAMES = [(c, m) for c in ('ms2', 'ms10') for m in ('eval', 'predict')]
+REC_KEYS = ('data', 'joint_scales', 'score', 'n_keypoints', 'n_decoding', 'decoding_pairs',
+            'decoding_xyv', 'n_frontier', 'frontier_pairs')
+
+
+def _same_records(got, ref):
+    assert len(got) == len(ref)
+    for r, o in zip(got, ref):
+        for key in REC_KEYS:
+            assert np.array_equal(r[key], o[key]), key
+
+
+def _multi_case(dec, name, mode):
+    from openpifpaf_amd import synthetic
+    g = np.load(os.path.join(gu.GOLDEN, 'multi_%s_%s.npz' % (name, mode)))
+    fields, kw = synthetic.multi_case(name)
+    assert gu.sha(*fields) == str(g['input_sha'])
+    _configure(dec, g)
+    return g, fields, kw
+
+
+@pytest.mark.parametrize('name,mode', MULTI_NAMES)
+def test_multi_stages_vs_reference(dec, name, mode):
+    """CifHr (pairs / maxima), seeds and both CafScored sets of a multi-scale FieldConfig
+    through the reference API, bit-exact against the reference's fixtures."""
+    from openpifpaf_amd import constants
+    g, fields, kw = _multi_case(dec, name, mode)
+    fc = dec.FieldConfig(**kw)
+    hr = dec.CifHr(fc).fill(fields).accumulated
+    assert list(hr.shape) == list(g['cifhr_shape'])
+    assert gu.sha(hr) == str(g['cifhr_sha'])
+    seeds = dec.CifSeeds(hr, fc).fill(fields).get()
+    rows = np.array([tuple(float(t) for t in s) for s in seeds], np.float32).reshape(-1, 5)
+    assert np.array_equal(rows, g['seeds'])
+    skel = constants.COCO_PERSON_SKELETON
+    for tag, th in (('a', None), ('b', 0.0001)):
+        cs = dec.CafScored(hr, fc, skel, score_th=th).fill(fields)
+        assert [f.shape[1] for f in cs.forward] == list(g['caf_%s_fwd_counts' % tag])
+        assert [gu.sha(f) for f in cs.forward] == [str(s) for s in g['caf_%s_fwd_sha' % tag]]
+        assert [gu.sha(b) for b in cs.backward] == [str(s) for s in g['caf_%s_bwd_sha' % tag]]
+
+
+@pytest.mark.parametrize('name,mode', MULTI_NAMES)
+def test_multi_cifcaf_vs_reference(dec, name, mode):
+    from openpifpaf_amd import constants
+    g, fields, kw = _multi_case(dec, name, mode)
+    cc = dec.CifCaf(dec.FieldConfig(**kw), keypoints=constants.COCO_KEYPOINTS,
+                    skeleton=constants.COCO_PERSON_SKELETON)
+    recs, _, _ = cc.decode_fields_records([f[None] for f in fields])
+    errs = gu.compare_annotations(g, recs)
+    assert not errs, errs[:10]
+    oracle_recs = oracle.decode_multi(oracle.Members(fields, **kw),
+                                      constants.COCO_PERSON_SKELETON, gu.case_config(g))
+    _same_records(recs, oracle_recs)
+    anns = cc(fields)
+    assert len(anns) == len(g['ann_score'])
+    for a, s in zip(anns, g['ann_score']):
+        assert np.isclose(a.score(), s, rtol=gu.RTOL, atol=1e-9)
+
+
+def _multi_batch(name, n, first_seed=100, n_people=4):
+    from openpifpaf_amd import synthetic
+    per = [synthetic.multi_case(name, seed=first_seed + i, n_people=n_people) for i in range(n)]
+    kw = per[0][1]
+    fields = [np.stack([p[0][j] for p in per]) for j in range(len(per[0][0]))]
+    return fields, kw
+
+
+@pytest.mark.parametrize('name', ['ms2', 'ms10'])
+def test_multi_batch_vs_oracle(dec, name):
+    """A batch of multi-scale images in one pp_decode_multi call equals the oracle per image
+    (records compared byte for byte)."""
+    from openpifpaf_amd import constants
+    from openpifpaf_amd._abi import EVAL_CONFIG, make_config
+    g = {'mode': np.array('eval'), 'greedy': 0, 'connection_method': np.array('blend')}
+    _configure(dec, g)
+    fields, kw = _multi_batch(name, 12, n_people=6)
+    cc = dec.CifCaf(dec.FieldConfig(**kw), keypoints=constants.COCO_KEYPOINTS,
+                    skeleton=constants.COCO_PERSON_SKELETON)
+    recs, offsets, _ = cc.decode_fields_records(fields)
+    cfg = make_config(**EVAL_CONFIG)
+    for i in range(len(offsets) - 1):
+        ref = oracle.decode_multi(oracle.Members([f[i] for f in fields], **kw),
+                                  constants.COCO_PERSON_SKELETON, cfg)
+        _same_records(recs[offsets[i]:offsets[i + 1]], ref)
+    assert offsets[-1] > 12 * 3
+
+
+def test_multi_unequal_heads_vs_oracle(dec):
+    """Two CIF heads and one CAF head at another stride (FieldConfig lists of different
+    lengths): the CIF / CAF head lists are independent."""
+    from openpifpaf_amd import constants, synthetic
+    from openpifpaf_amd._abi import EVAL_CONFIG, make_config
+    g = {'mode': np.array('eval'), 'greedy': 0, 'connection_method': np.array('blend')}
+    _configure(dec, g)
+    heads = synthetic.planted_multi(321, 321, [8, 16], n_people=5, seed=7)
+    fields = [heads[0][0], heads[1][0], heads[1][1]]  # cif s8, cif s16, caf s16
+    kw = dict(cif_indices=[0, 1], caf_indices=[2], cif_strides=[8, 16], caf_strides=[16],
+              cif_min_scales=[0.0, 8.0], caf_min_distances=[12.0], caf_max_distances=[None])
+    cc = dec.CifCaf(dec.FieldConfig(**kw), keypoints=constants.COCO_KEYPOINTS,
+                    skeleton=constants.COCO_PERSON_SKELETON)
+    recs, _, _ = cc.decode_fields_records([f[None] for f in fields])
+    ref = oracle.decode_multi(oracle.Members(fields, **kw), constants.COCO_PERSON_SKELETON,
+                              make_config(**EVAL_CONFIG))
+    assert len(ref) > 2
+    _same_records(recs, ref)
+
+
+def test_multi_stage_calls_equal_full_decode(dec):
+    """pp_decode_multi stage by stage == one call (stage contract)."""
+    import torch
+    from openpifpaf_amd import constants, engine
+    from openpifpaf_amd._abi import EVAL_CONFIG, make_config
+    fields, kw = _multi_batch('ms10', 4)
+    heads = engine.HeadSet([torch.from_numpy(f).cuda() for f in fields], dec.FieldConfig(**kw))
+    cfg = make_config(**EVAL_CONFIG)
+    sk = constants.COCO_PERSON_SKELETON
+    eng = engine.DecodeEngine()
+    ref, ref_off = eng.fetch(eng.launch_multi(heads, sk, cfg))
+    ref = ref.copy()
+    for bits in (1, 2, 4, 8):
+        b = eng.launch_multi(heads, sk, cfg, stages=bits)
+    got, off = eng.fetch(b)
+    assert np.array_equal(off, ref_off)
+    assert got.tobytes() == ref.tobytes()
