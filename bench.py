@@ -51,6 +51,8 @@ def parse():
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--no-uniform', action='store_true',
                    help='skip the uniform-generator line added to the default run')
+    p.add_argument('--no-multi', action='store_true',
+                   help='skip the multi-scale (pp_decode_multi) lines added to the default run')
     p.add_argument('--stage-breakdown', action='store_true',
                    help='one library call per stage (per-stage times)')
     return p.parse_args()
@@ -101,9 +103,10 @@ def main():
              ('cifhr', 'seeds+caf+grow+nms'))
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(groups) + 1)]
 
-    def timed_run(cif, caf, steps, warmup):
-        """warmup + `steps` timed decode steps of one resident batch: (elapsed s over all
-        ranks, per-group event ms per step, annotations decoded)."""
+    def timed_run(cif, caf, steps, warmup, heads=None):
+        """warmup + `steps` timed decode steps of one resident batch (cif / caf, or a
+        multi-scale HeadSet): (elapsed s over all ranks, per-group event ms per step,
+        annotations decoded)."""
         stage_ms = np.zeros(len(groups))
 
         def step(timed):
@@ -111,7 +114,9 @@ def main():
             for si, bits in enumerate(groups):
                 if timed:
                     ev[si].record(stream)
-                if stages & bits:
+                if stages & bits and heads is not None:
+                    b = eng.launch_multi(heads, skeleton, cfg, stages=stages & bits)
+                elif stages & bits:
                     b = eng.launch(cif, caf, skeleton, cfg, stages=stages & bits)
             if timed:
                 ev[len(groups)].record(stream)
@@ -209,6 +214,31 @@ def main():
             'stage_ms': {n: round(float(v), 4) for n, v in zip(names, u_stage)},
             'annotations_per_image': round(u_anns / (u_steps * batch), 3),
         }
+    if default_run and world == 1 and not args.no_multi:
+        # multi-scale FieldConfigs (factory.py:153-180) on pp_decode_multi: the same people
+        # seen by several heads; 'ms2' = stride 8 + 16 heads, 'ms10' = the reference's
+        # 10-head hflip-pair layout (cif_hr.py:63-68)
+        from openpifpaf_amd.decoder import FieldConfig
+        from openpifpaf_amd.engine import HeadSet
+        line['multi'] = {}
+        px = (h - 1) * 8 + 1
+        for name, n_img in (('ms2', batch), ('ms10', batch // 4)):
+            per = [synthetic.multi_case(name, seed=i, h_px=px, w_px=px, n_people=wl['n_people'])
+                   for i in range(n_img)]
+            fields = [torch.from_numpy(np.stack([p[0][j] for p in per])).to(dev)
+                      for j in range(len(per[0][0]))]
+            heads = HeadSet(fields, FieldConfig(**per[0][1]))
+            del per
+            m_steps = max(3, args.steps // 2)
+            m_el, m_stage, m_anns = timed_run(None, None, m_steps, 2, heads=heads)
+            line['multi'][name] = {
+                'value': round(n_img * m_steps / m_el, 1), 'unit': 'images/s',
+                'images': n_img, 'image_px': px, 'heads': len(heads.cifs),
+                'ms_per_step': round(1e3 * m_el / m_steps, 4),
+                'stage_ms': {n: round(float(v), 4) for n, v in zip(names, m_stage)},
+                'annotations_per_image': round(m_anns / (m_steps * n_img), 3),
+            }
+            del heads, fields
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line['cpu_baseline'] = cpu_baseline(cif_h, caf_h, skeleton, cfg, args.cpu_seconds)
     if rank == 0:

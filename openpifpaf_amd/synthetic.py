@@ -123,7 +123,9 @@ def planted_multi(h_px, w_px, strides, n_people=4, seed=0, skeleton=None, noise=
         cy = rng.uniform(0.15 * h_px, 0.85 * h_px)
         kps = np.stack([cx + u * COCO_UPRIGHT_POSE[:, 0],
                         cy - u * (COCO_UPRIGHT_POSE[:, 1] - 5.0)], axis=1)
-        people.append((kps + rng.normal(0.0, 2.0, (17, 2)), 3.2 * u))
+        # joint scale in pixels: ~0.4 u as planted() (0.4 pose units), spread over people so
+        # that the heads' min-scale masks keep some joints and drop others
+        people.append((kps + rng.normal(0.0, 2.0, (17, 2)), u * rng.uniform(0.3, 1.2)))
     out = []
     for si, stride in enumerate(strides):
         h, w = (h_px - 1) // stride + 1, (w_px - 1) // stride + 1
