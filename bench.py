@@ -162,7 +162,7 @@ def main():
     value = images / elapsed
     ms_step = 1e3 * elapsed / args.steps
     hh, ww = (h - 1) * 8 + 1, (w - 1) * 8 + 1
-    cifhr_bytes = 4 * k * (5 * h * w + hh * ww) * batch
+    cifhr_bytes, hr_tiles = cifhr_stage_bytes(cif_h, 8, cfg.cif_threshold)
     achieved = cifhr_bytes / (stage_avg[0] * 1e-3) / 1e9
     line = {
         'metric': 'decoder images/sec + ms/image, 17-CIF/19-CAF @80x80; CifHr HBM GB/s vs '
@@ -194,6 +194,7 @@ def main():
             'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
             'frac': round(achieved / PEAK_HBM_GBS, 4),
             'algorithmic_bytes_per_launch': cifhr_bytes, 'traffic': None,
+            'written_tile_frac': round(hr_tiles, 4),
         },
     }
     default_run = (args.workload == 'cfg3' and args.generator == 'planted' and
@@ -245,6 +246,44 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def cifhr_stage_bytes(cif, stride, v_th, tile=64):
+    """Algorithmic HBM bytes of the decoder's CifHr stage over a batch (n, K, 5, H, W):
+    the confidence plane of every cell, the x / y / scale rows of passing cells, each
+    splat record written and read once (32 B), and the tile-major scratch map's touched
+    64x64 tiles (16 KB each, exactly the tiles the splats' boxes intersect — the same
+    box arithmetic as splat_box in csrc/splat.hip) plus one flag byte per tile.
+    Returns (bytes, fraction of tiles written)."""
+    n, k, _, h, w = cif.shape
+    hh, ww = (h - 1) * stride + 1, (w - 1) * stride + 1
+    tiles_x = (-(-ww // 32) * 32 + tile - 1) // tile
+    tiles_y = (hh + tile - 1) // tile
+    c = cif[:, :, 0]
+    img, fld, cy_i, cx_i = np.nonzero(c > np.float32(v_th))
+    x = cif[img, fld, 1, cy_i, cx_i] * np.float32(stride)
+    y = cif[img, fld, 2, cy_i, cx_i] * np.float32(stride)
+    sg = (np.float32(0.5) * cif[img, fld, 4, cy_i, cx_i]) * np.float32(stride)
+    sigma = np.where(np.isnan(sg), sg, np.maximum(np.float32(1.0), sg))
+
+    def span(cen, size):
+        lo = np.fmax(np.float32(0), np.fmin(np.float32(size - 1), cen - sigma))
+        lo = np.nan_to_num(lo).astype(np.int64)
+        hi = np.fmax((lo + 1).astype(np.float32), np.fmin(np.float32(size), (cen + sigma) + np.float32(1)))
+        hi = np.nan_to_num(hi, nan=size).astype(np.int64)
+        return lo // tile, (hi - 1) // tile
+
+    tx0, tx1 = span(x, ww)
+    ty0, ty1 = span(y, hh)
+    touched = np.zeros((n, k, tiles_y, tiles_x), bool)
+    for dy in range(int((ty1 - ty0).max(initial=0)) + 1):
+        for dx in range(int((tx1 - tx0).max(initial=0)) + 1):
+            m = (ty0 + dy <= ty1) & (tx0 + dx <= tx1)
+            touched[img[m], fld[m], ty0[m] + dy, tx0[m] + dx] = True
+    n_tiles = int(touched.sum())
+    nbytes = (4 * n * k * h * w + 12 * len(img) + 64 * len(img) +
+              n_tiles * 4 * tile * tile + n * k * tiles_x * tiles_y)
+    return nbytes, n_tiles / touched.size
 
 
 def committed_traffic():

@@ -91,8 +91,7 @@ struct GrowArgs {
     // (n_img, C, 2, col_cap); its queries read the heads' raw CAF and rescore with CifHr
     // (consider_raw)
     Heads heads;
-    const float *hr;          // (n_img, K, hh, hr_pitch) CifHr
-    int64_t hr_pitch;
+    HrMap hr;                 // CifHr (dense, or the tile-major scratch layout)
     float cif_floor, one_minus_floor, th_b;
     uint8_t caf_j1[PP_MAX_EDGES], caf_j2[PP_MAX_EDGES];  // 0-based joints of each CAF
     int bw, bh, nb;           // bucket grid (see caf_bucketed_kernel)
@@ -144,14 +143,6 @@ struct GrowLDS {
 #endif
 };
 
-// Orders this wave's LDS / global accesses the way __syncthreads() does (workgroup-scope
-// fence: outstanding stores complete before later loads) without the s_barrier, so the
-// helpers below can run in ONE wave of a multi-wave workgroup (the seed loop's committer)
-// as well as in single-wave workgroups.
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-}
 
 __device__ __forceinline__ float rl_f(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
@@ -381,7 +372,7 @@ __device__ __forceinline__ void consider(const float *__restrict__ cf, int64_t h
 struct RawSet {
     const int *idx;      // bucketed concatenated cell indices
     int64_t fld;         // image * C + CAF field
-    const float *hrt;    // CifHr plane of the direction's target joint (rescore), or NULL
+    int64_t hrt;         // CifHr plane of the direction's target joint (rescore), or -1
     int src, tgt, tsc;   // raw rows of source x, target x, target scale (y = x + 1)
 };
 
@@ -406,8 +397,7 @@ __device__ __forceinline__ void consider_raw(const GrowArgs &g, const RawSet &r,
     const float tc = caf9[r.tsc * hw + cell] * stride;
     if (c1 < q.lo_x || c1 > q.hi_x || c2 < q.lo_y || c2 > q.hi_y) return;
     float c0 = c;
-    if (r.hrt)
-        c0 = c * (g.cif_floor + g.one_minus_floor * hr_lookup(r.hrt, g.hh, g.ww, g.hr_pitch, tx, ty, 0.0f));
+    if (r.hrt >= 0) c0 = c * (g.cif_floor + g.one_minus_floor * g.hr.at(r.hrt, tx, ty, 0.0f));
     if (!(c0 > g.th_b)) return;
     const float dx = q.x - c1, dy = q.y - c2;
     const float dd = sqrtf(dx * dx + dy * dy);
@@ -570,8 +560,7 @@ __device__ __forceinline__ RawSet raw_set(const GrowArgs &g, int img, int caf_i,
     r.idx = reinterpret_cast<const int *>(col_set(g, 1, img, caf_i, dir));
     r.fld = (int64_t)img * g.C + caf_i;
     const int tj = dir ? g.caf_j2[caf_i] : g.caf_j1[caf_i];
-    r.hrt = (g.cif_floor < 1.0f && tj < g.K) ? g.hr + ((int64_t)img * g.K + tj) * g.hh * g.hr_pitch
-                                              : nullptr;
+    r.hrt = (g.cif_floor < 1.0f && tj < g.K) ? (int64_t)img * g.K + tj : -1;
     r.src = dir ? 1 : 5;
     r.tgt = dir ? 5 : 1;
     r.tsc = dir ? 8 : 4;
@@ -1748,10 +1737,10 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
 // ---------------------------------------------------------------------------------------
 namespace pp {
 
-int launch_seeds(const Heads &h, const float *hr, int n_img, int K, const pp_config *cfg,
+int launch_seeds(const Heads &h, const HrMap &hr, int n_img, int K, const pp_config *cfg,
                  pp_seed *seeds, int cap, int *counts, void *scratch, hipStream_t s);
 size_t seeds_scratch_size(int n_img, int cap);
-int launch_caf_bucketed(const Heads &h, const float *hr, int n_img, int K, int C,
+int launch_caf_bucketed(const Heads &h, const HrMap &hr, int n_img, int K, int C,
                         const int32_t *skeleton, const pp_config *cfg, float th, float *cols,
                         int *offs, const int *gate, bool index_only, hipStream_t s);
 void caf_bucket_grid(int H, int W, int stride, int *bw, int *bh, int *nb, float *inv_e);
@@ -1765,7 +1754,7 @@ struct DecodeLayout {
     int bw, bh, nb;
     float inv_e;
     int64_t occ_cap;
-    size_t off_cifhr, off_cifhr_ws, off_seeds, off_seed_counts, off_seed_ws, off_cols[2],
+    size_t off_cifhr, off_hr_flags, off_cifhr_ws, off_seeds, off_seed_counts, off_seed_ws, off_cols[2],
         off_offs[2], off_n_work, off_need, off_occ, off_wq, off_log, off_work, off_spec, off_nms_score,
         off_nms_idx, off_nms_f, off_nms_box, total;
     size_t cifhr_ws_bytes;
@@ -1794,7 +1783,10 @@ static DecodeLayout make_layout(int n_img, int K, int C, const Heads &h, const p
         return at;
     };
     const size_t n = (size_t)n_img;
-    d.off_cifhr = take(n * K * d.hh * d.pitch * sizeof(float));
+    // scratch CifHr in the tile-major layout (HrMap): one 64x64 tile per flag
+    const HrMap geo = dense_hr(nullptr, d.hh, d.ww);
+    d.off_cifhr = take(n * K * (size_t)geo.tiles * kHrTile * kHrTile * sizeof(float));
+    d.off_hr_flags = take(n * K * (size_t)geo.tiles);
     d.cifhr_ws_bytes = cifhr_heads_workspace_size(h, n_img, K);
     d.off_cifhr_ws = take(d.cifhr_ws_bytes);
     d.off_seeds = take(n * d.seed_cap * sizeof(pp_seed));
@@ -1899,14 +1891,20 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
         return fail(PP_ESHAPE, "pp_decode_batch: field too large");
     char *ws = (char *)d_workspace;
     hipStream_t s = (hipStream_t)stream;
-    float *hr = d_cifhr ? d_cifhr : (float *)(ws + d.off_cifhr);
+    // the caller's d_cifhr gets the dense map; otherwise the decoder keeps the tile-major
+    // scratch map, written only where splats land
+    float *hr_base = d_cifhr ? d_cifhr : (float *)(ws + d.off_cifhr);
+    uint8_t *hr_flags = d_cifhr ? nullptr : (uint8_t *)(ws + d.off_hr_flags);
+    HrMap hr = dense_hr(hr_base, d.hh, d.ww);
+    hr.flags = hr_flags;
     pp_seed *seeds = (pp_seed *)(ws + d.off_seeds);
     int *seed_counts = (int *)(ws + d.off_seed_counts);
     float *cols[2] = {(float *)(ws + d.off_cols[0]), (float *)(ws + d.off_cols[1])};
     int *offs[2] = {(int *)(ws + d.off_offs[0]), (int *)(ws + d.off_offs[1])};
     int rc = PP_OK;
     if (stages & 1u) {
-        rc = cifhr_heads_launch<false>(h, n_img, K, cfg, hr, ws + d.off_cifhr_ws, d.cifhr_ws_bytes, s,
+        rc = cifhr_heads_launch<false>(h, n_img, K, cfg, hr_base, hr_flags, ws + d.off_cifhr_ws,
+                                       d.cifhr_ws_bytes, s,
                                        "pp_decode_batch(cifhr)");
         if (rc) return rc;
     }
@@ -1940,7 +1938,6 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
         g.cfg = *cfg;
         g.heads = h;
         g.hr = hr;
-        g.hr_pitch = d.pitch;
         g.cif_floor = cfg->cif_floor;
         g.one_minus_floor = (float)(1.0 - (double)cfg->cif_floor);  // (1.0 - self.cif_floor)
         g.th_b = cfg->complete_caf_threshold;

@@ -55,6 +55,77 @@ __device__ __forceinline__ float hr_lookup(const float *field, int hh, int ww, i
     return field[(int64_t)(int)y * pitch + (int)x];
 }
 
+// The CifHr map as the decode stages read it: dense row-major (n_img * K, hh, pitch) — the
+// caller-visible layout — or, for the decoder's scratch map, tile-major (n_img * K, tiles,
+// 64 * 64) with a per-tile flag: the tile kernel writes only tiles some splat touched, and
+// an unwritten tile reads as its true value 0.
+constexpr int kHrTile = 64;
+
+struct HrMap {
+    const float *base;
+    const uint8_t *flags;  // tiled: (n_img * K, tiles) 1 = tile written; NULL: dense
+    int hh, ww;
+    int64_t pitch;         // dense row pitch
+    int tiles_x, tiles;    // tile grid (tiles_x = pitch / 64 rounded up)
+    // functional.pyx:231-244 scalar_values on plane `plane` (= image * K + field)
+    __device__ __forceinline__ float at(int64_t plane, float x, float y, float dflt) const {
+        const float maxx = (float)ww - 1.0f, maxy = (float)hh - 1.0f;
+        if (x < 0.0f || y < 0.0f || x > maxx || y > maxy) return dflt;
+        if (x != x || y != y) return dflt;
+        const int ix = (int)x, iy = (int)y;
+        if (!flags) return base[(plane * hh + iy) * pitch + ix];
+        const int64_t t = plane * tiles + (iy >> 6) * tiles_x + (ix >> 6);
+        if (!flags[t]) return 0.0f;
+        return base[t * (kHrTile * kHrTile) + (iy & 63) * kHrTile + (ix & 63)];
+    }
+};
+
+// dense map view of a caller's (n_img * K, hh, pitch) buffer
+inline HrMap dense_hr(const float *base, int hh, int ww) {
+    HrMap m{};
+    m.base = base;
+    m.hh = hh;
+    m.ww = ww;
+    m.pitch = (ww + 31) / 32 * 32;  // pp_cifhr_pitch
+    m.tiles_x = (int)((m.pitch + kHrTile - 1) / kHrTile);
+    m.tiles = m.tiles_x * ((hh + kHrTile - 1) / kHrTile);
+    return m;
+}
+
+// Orders this wave's LDS / global accesses the way __syncthreads() does (workgroup-scope
+// fence: outstanding stores complete before later loads) without the s_barrier, so code
+// can run in ONE wave of a multi-wave workgroup (the seed loop's committer, a CifHr tile
+// stripe) as well as in single-wave workgroups.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Correctly rounded n / d with a reciprocal refined once per divisor: the compiler's IEEE
+// f32 division (v_div_scale, v_rcp, Newton step, two fma corrections, v_div_fmas,
+// v_div_fixup) minus the scaling and special-case steps, which are the identity when
+// d is in [1, 2^100] and n is finite or NaN with |n| <= 2^100 (no operand scaling is
+// needed there; vcc = 0 makes v_div_fmas a plain fma).  Bit-identical to `n / d` on that
+// domain (tests/hip/div_check.hip checks it exhaustively over sampled ranges); callers
+// keep `n / d` for divisors outside it.
+struct Recip {
+    float d, r;
+};
+__device__ __forceinline__ Recip recip_of(float d) {
+    float r = __builtin_amdgcn_rcpf(d);
+    const float e = __builtin_fmaf(-d, r, 1.0f);
+    r = __builtin_fmaf(e, r, r);
+    return {d, r};
+}
+__device__ __forceinline__ bool recip_ok(float d) { return d >= 1.0f && d <= 0x1p100f; }
+__device__ __forceinline__ float div_refined(float n, const Recip &R) {
+    float q = n * R.r;
+    float rem = __builtin_fmaf(-R.d, q, n);
+    q = __builtin_fmaf(rem, R.r, q);
+    rem = __builtin_fmaf(-R.d, q, n);
+    return __builtin_fmaf(rem, R.r, q);
+}
+
 // count of set bits of `mask` below this lane (v_mbcnt)
 __device__ __forceinline__ int lane_prefix(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
@@ -141,9 +212,10 @@ Heads single_head(const float *cif, const float *caf, int H, int W, int stride);
 
 // stage launchers over heads (splat.hip, stages.hip)
 size_t cifhr_heads_workspace_size(const Heads &h, int n_img, int K);
+// d_flags non-NULL: write the tile-major scratch layout of HrMap (only touched tiles)
 template <bool DET>
 int cifhr_heads_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config *cfg,
-                       float *d_cifhr, void *d_workspace, size_t workspace_bytes, hipStream_t s,
-                       const char *who);
+                       float *d_cifhr, uint8_t *d_flags, void *d_workspace,
+                       size_t workspace_bytes, hipStream_t s, const char *who);
 
 }  // namespace pp

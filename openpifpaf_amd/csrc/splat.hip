@@ -166,8 +166,6 @@ struct TileArgs {
     float *field;           // (n_fields, h, pitch), fields back to back
     float *field2;          // cumw for M_CUMAVG
     const Splat *splats;    // n_fields * splat_cap
-    const int *counts;      // per field splat count (NULL: n_splats)
-    const uint32_t *tile_bits;  // per field kTileBits bitmap of non-empty tiles (or NULL)
     int64_t splat_cap;
     int64_t n_splats;
     int64_t field_stride;   // elements between fields
@@ -176,8 +174,6 @@ struct TileArgs {
     int64_t n_work;         // n_fields * tiles
     float t2;               // truncate^2 (M_GAUSS_MAX circle test)
     float max_value;
-    int n_groups;           // CifHr groups (MULTI): field fld's group g list at
-    int64_t goff[kMaxHeads];  // splats + fld * splat_cap + goff[g], count fld * n_groups + g
 };
 
 template <int MODE>
@@ -215,21 +211,13 @@ __device__ __forceinline__ void fold_pixel(float &acc, float &acc2, bool in, flo
     }
 }
 
-// MULTI (CifHr over several groups, cif_hr.py:59-73): each group's list folds into a zero
-// tile and the groups combine by np.maximum(ta, accumulated), all in registers.  A group
-// with no splat on the tile contributes max(0, acc) = acc (every fold value is >= 0 and
-// the clamp maps NaN to max_value), so it is skipped.
-template <int MODE, bool ZERO_INIT, bool MULTI>
+// The functional.pyx primitives in place on one field: one workgroup per 64x64 tile reads
+// the tile, folds the candidate splats in ascending order and writes it back.
+template <int MODE>
 __global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
-    // candidates (gather / fold) and the output staging tile (store) are live in disjoint
-    // phases: one LDS buffer, ~18 KB, so 8 workgroups fit a CU while the tiles stream out
-    constexpr int kCandBytes = kCand * (int)(sizeof(int4) + sizeof(float4));
-    constexpr int kOutBytes = ZERO_INIT ? kTile * kOutPad * (int)sizeof(float) : 0;
-    __shared__ __attribute__((aligned(16))) char s_mem[kCandBytes > kOutBytes ? kCandBytes : kOutBytes];
+    __shared__ int4 s_box[kCand];
+    __shared__ float4 s_par[kCand];
     __shared__ int s_tmp[4];
-    int4 *s_box = reinterpret_cast<int4 *>(s_mem);
-    float4 *s_par = reinterpret_cast<float4 *>(s_mem + kCand * sizeof(int4));
-    float *s_out = reinterpret_cast<float *>(s_mem);
 
     const int64_t wid = xcd_remap(blockIdx.x, gridDim.x);
     if (wid >= a.n_work) return;
@@ -237,6 +225,8 @@ __global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
     const int64_t fld = wid / a.tiles;
     const int tx0 = (tile % a.tiles_x) * kTile;
     const int ty0 = (tile / a.tiles_x) * kTile;
+    const Splat *sp = a.splats + fld * a.splat_cap;
+    const int64_t ns = a.n_splats;
     float *out = a.field + fld * a.field_stride;
     float *out2 = (MODE == M_CUMAVG) ? a.field2 + fld * a.field_stride : nullptr;
 
@@ -245,125 +235,297 @@ __global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
     const int lx = lane & 7, ly = lane >> 3;
     const int wx0 = tx0, wy0 = ty0 + wave * 16;
 
-    float acc[16], acc2[16], res[MULTI ? 16 : 1];
+    float acc[16], acc2[16];
 #pragma unroll
     for (int r = 0; r < 16; r++) {
         acc[r] = 0.0f;
         acc2[r] = 0.0f;
-        if (MULTI) res[r] = 0.0f;
-        if (!ZERO_INIT) {
-            const int px = wx0 + (r & 7) * 8 + lx, py = wy0 + (r >> 3) * 8 + ly;
-            if (px < a.w && py < a.h) {
-                acc[r] = out[(int64_t)py * a.pitch + px];
-                if (MODE == M_CUMAVG) acc2[r] = out2[(int64_t)py * a.pitch + px];
-            }
+        const int px = wx0 + (r & 7) * 8 + lx, py = wy0 + (r >> 3) * 8 + ly;
+        if (px < a.w && py < a.h) {
+            acc[r] = out[(int64_t)py * a.pitch + px];
+            if (MODE == M_CUMAVG) acc2[r] = out2[(int64_t)py * a.pitch + px];
         }
     }
 
-    bool any = false;
-    const int ng = MULTI ? a.n_groups : 1;
-    for (int g = 0; g < ng; g++) {
-        const int64_t lst = MULTI ? fld * a.n_groups + g : fld;
-        const Splat *sp = a.splats + fld * a.splat_cap + (MULTI ? a.goff[g] : 0);
-        int64_t ns = a.counts ? (int64_t)a.counts[lst] : a.n_splats;
-        if (ZERO_INIT && a.tile_bits &&
-            !((a.tile_bits[lst * (kTileBits / 32) + (tile >> 5)] >> (tile & 31)) & 1u))
-            ns = 0;  // no splat of this list touches this tile
-        if (MULTI && ns == 0) continue;
-        if (MULTI) {
-#pragma unroll
-            for (int r = 0; r < 16; r++) acc[r] = 0.0f;
-        }
-        bool hit_any = false;
-        int64_t cursor = 0;
+    int64_t cursor = 0;
+    while (cursor < ns) {
+        // ---- gather: splats intersecting this tile, in splat order, into LDS ----
+        int n = 0;
         while (cursor < ns) {
-            // ---- gather: splats intersecting this tile, in splat order, into LDS ----
-            int n = 0;
-            while (cursor < ns) {
-                const int64_t i = cursor + threadIdx.x;
-                bool hit = false;
-                int4 b = make_int4(0, 0, 0, 0);
-                if (i < ns) {
-                    b = sp[i].box;
-                    hit = b.y > tx0 && b.x < tx0 + kTile && b.w > ty0 && b.z < ty0 + kTile;
-                }
-                int total;
-                const int slot = block_compact<4>(hit, s_tmp, total);
-                if (n + total > kCand) break;  // block-uniform; chunk re-read next pass
-                if (hit) {
-                    s_box[n + slot] = b;
-                    s_par[n + slot] = sp[i].par;
-                }
-                n += total;
-                cursor += 256;
+            const int64_t i = cursor + threadIdx.x;
+            bool hit = false;
+            int4 b = make_int4(0, 0, 0, 0);
+            if (i < ns) {
+                b = sp[i].box;
+                hit = b.y > tx0 && b.x < tx0 + kTile && b.w > ty0 && b.z < ty0 + kTile;
             }
-            __syncthreads();
-            hit_any = hit_any || n > 0;
-            // ---- fold: per pixel, ascending candidate order ----
-            for (int c = 0; c < n; c++) {
-                const int bx0 = __builtin_amdgcn_readfirstlane(s_box[c].x);
-                const int bx1 = __builtin_amdgcn_readfirstlane(s_box[c].y);
-                const int by0 = __builtin_amdgcn_readfirstlane(s_box[c].z);
-                const int by1 = __builtin_amdgcn_readfirstlane(s_box[c].w);
-                if (bx1 <= wx0 || bx0 >= wx0 + kTile || by1 <= wy0 || by0 >= wy0 + 16) continue;
-                const float4 par = s_par[c];
-                const float t2s2 = a.t2 * par.w;
-#pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    const int rx0 = wx0 + (r & 7) * 8, ry0 = wy0 + (r >> 3) * 8;
-                    if (bx1 <= rx0 || bx0 >= rx0 + 8 || by1 <= ry0 || by0 >= ry0 + 8) continue;
-                    const int px = rx0 + lx, py = ry0 + ly;
-                    const bool in = px >= bx0 && px < bx1 && py >= by0 && py < by1;
-                    fold_pixel<MODE>(acc[r], acc2[r], in, (float)px, (float)py, par, t2s2,
-                                     a.max_value);
-                }
+            int total;
+            const int slot = block_compact<4>(hit, s_tmp, total);
+            if (n + total > kCand) break;  // block-uniform; chunk re-read next pass
+            if (hit) {
+                s_box[n + slot] = b;
+                s_par[n + slot] = sp[i].par;
             }
-            __syncthreads();
+            n += total;
+            cursor += 256;
         }
-        any = any || hit_any;
-        if (MULTI && hit_any) {
-#pragma unroll
-            for (int r = 0; r < 16; r++)  // np.maximum(ta, accumulated)
-                res[r] = (acc[r] != acc[r] || res[r] != res[r]) ? NAN : (acc[r] > res[r] ? acc[r] : res[r]);
-        }
-    }
-    if (MULTI) {
-#pragma unroll
-        for (int r = 0; r < 16; r++) acc[r] = res[r];
-    }
-
-    if (ZERO_INIT) {
-        // ---- write the tile once: 16-B stores, rows of 256 B ----
-        if (any) {
+        __syncthreads();
+        // ---- fold: per pixel, ascending candidate order ----
+        for (int c = 0; c < n; c++) {
+            const int bx0 = __builtin_amdgcn_readfirstlane(s_box[c].x);
+            const int bx1 = __builtin_amdgcn_readfirstlane(s_box[c].y);
+            const int by0 = __builtin_amdgcn_readfirstlane(s_box[c].z);
+            const int by1 = __builtin_amdgcn_readfirstlane(s_box[c].w);
+            if (bx1 <= wx0 || bx0 >= wx0 + kTile || by1 <= wy0 || by0 >= wy0 + 16) continue;
+            const float4 par = s_par[c];
+            const float t2s2 = a.t2 * par.w;
 #pragma unroll
             for (int r = 0; r < 16; r++) {
-                const int row = wave * 16 + (r >> 3) * 8 + ly, col = (r & 7) * 8 + lx;
-                s_out[row * kOutPad + col] = acc[r];
+                const int rx0 = wx0 + (r & 7) * 8, ry0 = wy0 + (r >> 3) * 8;
+                if (bx1 <= rx0 || bx0 >= rx0 + 8 || by1 <= ry0 || by0 >= ry0 + 8) continue;
+                const int px = rx0 + lx, py = ry0 + ly;
+                const bool in = px >= bx0 && px < bx1 && py >= by0 && py < by1;
+                fold_pixel<MODE>(acc[r], acc2[r], in, (float)px, (float)py, par, t2s2,
+                                 a.max_value);
             }
-            __syncthreads();
         }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int px = wx0 + (r & 7) * 8 + lx, py = wy0 + (r >> 3) * 8 + ly;
+        if (px < a.w && py < a.h) {
+            out[(int64_t)py * a.pitch + px] = acc[r];
+            if (MODE == M_CUMAVG) out2[(int64_t)py * a.pitch + px] = acc2[r];
+        }
+    }
+}
+
+// -------------------------------------------------------------------------------------
+// K2 for CifHr: one workgroup per (field, chunk of 32 tiles = one tile-bitmap word)
+// -------------------------------------------------------------------------------------
+// The chunk's bitmap words say which tiles any splat box touches.  Untouched tiles cost a
+// flag (tile-major scratch map) or a zero-fill (dense map); the field's splat lists are
+// loaded into LDS once when they fit (kCand entries over all groups), and each touched
+// tile selects its candidates from LDS by ballot compaction, keeping splat order.  Bigger
+// lists gather per tile from global memory in kCand chunks.
+//
+// MULTI (CifHr over several groups, cif_hr.py:59-73): each group's list folds into a zero
+// tile and the groups combine by np.maximum(ta, accumulated), all in registers.  A group
+// with no splat on the tile contributes max(0, acc) = acc (every fold value is >= 0 and
+// the clamp maps NaN to max_value), so it is skipped.
+constexpr int kChunkTiles = 32;
+constexpr int kHrCand = 256;  // LDS list / candidate capacity (>= 256 for progress)
+constexpr int kHrPad = 68;    // accumulator row pitch: ~26 KB of LDS per workgroup
+
+struct HrTileArgs {
+    float *field;           // dense (n_fields, h, pitch) or tile-major (n_fields, tiles, 64*64)
+    uint8_t *flags;         // tile-major: (n_fields, tiles) written flags; NULL = dense
+    const Splat *splats;    // field fld's group g list at splats + fld * splat_cap + goff[g]
+    const int *counts;      // (n_fields, n_groups)
+    const uint32_t *tile_bits;  // (n_fields, n_groups, kTileBits / 32)
+    int64_t splat_cap;
+    int64_t field_stride;
+    int h, w, pitch;
+    int tiles_x, tiles, chunks;  // chunks per field
+    int64_t n_work;         // n_fields * chunks
+    int n_groups;
+    int64_t goff[kMaxHeads];
+};
+
+template <bool MULTI>
+__global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
+    __shared__ int4 s_box[kHrCand];
+    __shared__ float4 s_par[kHrCand];
+    __shared__ uint16_t s_idx[kHrCand];
+    __shared__ __attribute__((aligned(16))) float s_out[kTile * kHrPad];
+    __shared__ int s_tmp[4];
+    __shared__ int s_ns[kMaxHeads], s_loff[kMaxHeads];  // per group: list size, LDS offset
+
+    const int64_t wid = xcd_remap(blockIdx.x, gridDim.x);
+    if (wid >= a.n_work) return;
+    const int chunk = (int)(wid % a.chunks);
+    const int64_t fld = wid / a.chunks;
+    const int t0 = chunk * kChunkTiles, t1 = min(a.tiles, t0 + kChunkTiles);
+    const int ng = MULTI ? a.n_groups : 1;
+
+    // touched tiles of the chunk (over all groups) and the lists' sizes (scalar loads)
+    uint32_t live = 0;
+    int total = 0;
+    for (int g = 0; g < ng; g++) {
+        const int64_t lst = fld * ng + g;
+        const int ns = a.counts[lst];
+        if (threadIdx.x == 0) {
+            s_ns[g] = ns;
+            s_loff[g] = total;
+        }
+        total += ns;
+        if (ns > 0) live |= a.tile_bits[lst * (kTileBits / 32) + chunk];
+    }
+    live &= (t1 - t0 == 32) ? ~0u : ((1u << (t1 - t0)) - 1u);
+    float *out = a.field + fld * a.field_stride;
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    if (a.flags) {
+        if ((int)threadIdx.x < t1 - t0) a.flags[fld * a.tiles + t0 + threadIdx.x] = (live >> threadIdx.x) & 1u;
+    } else {  // dense map: untouched tiles are zero-filled, 16-B nontemporal stores
+        const v4f z = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (int t = t0; t < t1; t++) {
+            if ((live >> (t - t0)) & 1u) continue;
+            const int tx0 = (t % a.tiles_x) * kTile, ty0 = (t / a.tiles_x) * kTile;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int q = k * 256 + threadIdx.x;
+                const int gy = ty0 + (q >> 4), gx = tx0 + (q & 15) * 4;
+                if (gy < a.h && gx < a.pitch)
+                    __builtin_nontemporal_store(z, reinterpret_cast<v4f *>(&out[(int64_t)gy * a.pitch + gx]));
+            }
+        }
+    }
+    if (!live) return;
+
+    // the field's lists in LDS when they fit (one round trip for the whole chunk)
+    const bool pre = total <= kHrCand;
+    __syncthreads();  // s_ns / s_loff
+    if (pre) {
+        for (int g = 0; g < ng; g++) {
+            const Splat *sp = a.splats + fld * a.splat_cap + (MULTI ? a.goff[g] : 0);
+            const int o = s_loff[g], ns = s_ns[g];
+            for (int i = threadIdx.x; i < ns; i += 256) {
+                s_box[o + i] = sp[i].box;
+                s_par[o + i] = sp[i].par;
+            }
+        }
+        __syncthreads();
+    }
+
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int lx = lane & 7, ly = lane >> 3;
+    float *s_acc = s_out + wave * 16 * kHrPad;  // this wave's 64 x 16 stripe
+    for (uint32_t rest = live; rest; rest &= rest - 1) {
+        const int tile = t0 + __builtin_ctz(rest);
+        const int tx0 = (tile % a.tiles_x) * kTile;
+        const int ty0 = (tile / a.tiles_x) * kTile;
+        const int wy0 = ty0 + wave * 16;  // stripe rows [wy0, wy0 + 16)
+        float res[MULTI ? 16 : 1];
+        if (MULTI) {
+#pragma unroll
+            for (int r = 0; r < 16; r++) res[r] = 0.0f;
+        }
+        for (int g = 0; g < ng; g++) {
+            const int64_t lst = fld * ng + g;
+            const int64_t ns = s_ns[g];
+            const int loff = s_loff[g];
+            if (ns == 0 || !((a.tile_bits[lst * (kTileBits / 32) + chunk] >> (tile - t0)) & 1u)) continue;
+            // zero the stripe accumulator (wave-private rows)
+#pragma unroll
+            for (int r = 0; r < 16; r++) s_acc[(r >> 3) * 8 * kHrPad + ly * kHrPad + (r & 7) * 8 + lx] = 0.0f;
+            wave_sync();
+            const Splat *sp = a.splats + fld * a.splat_cap + (MULTI ? a.goff[g] : 0);
+            int64_t cursor = 0;
+            bool hit_any = false;
+            while (cursor < ns) {
+                // ---- gather: this tile's candidates in splat order ----
+                int n = 0;
+                while (cursor < ns) {
+                    const int64_t i = cursor + threadIdx.x;
+                    bool hit = false;
+                    int4 b = make_int4(0, 0, 0, 0);
+                    if (i < ns) {
+                        b = pre ? s_box[loff + i] : sp[i].box;
+                        hit = b.y > tx0 && b.x < tx0 + kTile && b.w > ty0 && b.z < ty0 + kTile;
+                    }
+                    int tot;
+                    const int slot = block_compact<4>(hit, s_tmp, tot);
+                    if (!pre && n + tot > kHrCand) break;  // block-uniform; re-read next pass
+                    if (hit) {
+                        if (pre) {
+                            s_idx[n + slot] = (uint16_t)(loff + i);
+                        } else {
+                            s_box[n + slot] = b;
+                            s_par[n + slot] = sp[i].par;
+                        }
+                    }
+                    n += tot;
+                    cursor += 256;
+                }
+                __syncthreads();
+                hit_any = hit_any || n > 0;
+                // ---- fold, splat-major: for each candidate in ascending order, the wave's
+                // lanes cover the candidate's box clipped to the stripe; each pixel is
+                // read-modified-written in LDS by one lane, in candidate order (a wave's LDS
+                // operations execute in issue order)
+                for (int c = 0; c < n; c++) {
+                    const int e = pre ? (int)s_idx[c] : c;
+                    const int bx0 = max(__builtin_amdgcn_readfirstlane(s_box[e].x), tx0);
+                    const int bx1 = min(__builtin_amdgcn_readfirstlane(s_box[e].y), tx0 + kTile);
+                    const int by0 = max(__builtin_amdgcn_readfirstlane(s_box[e].z), wy0);
+                    const int by1 = min(__builtin_amdgcn_readfirstlane(s_box[e].w), wy0 + 16);
+                    if (bx1 <= bx0 || by1 <= by0) continue;  // wave-uniform
+                    const float4 par = s_par[e];
+                    const float t2s2 = 1.0f * par.w;  // truncate = 1 (cif_hr.py:40)
+                    const int bw = bx1 - bx0, area = bw * (by1 - by0);
+                    const float inv_bw = 1.0f / (float)bw;
+                    const bool fast = recip_ok(par.w);  // wave-uniform
+                    const Recip R = recip_of(par.w);
+                    for (int base = 0; base < area; base += 64) {
+                        const int i = base + lane;
+                        if (i >= area) break;
+                        const int yo = (int)(((float)i + 0.5f) * inv_bw);  // exact: i < 1024
+                        const int px = bx0 + (i - yo * bw), py = by0 + yo;
+                        // fold_pixel<M_GAUSS_MAX> for an in-box pixel (functional.pyx:127-141)
+                        const float dx = (float)px - par.x, dy = (float)py - par.y;
+                        const float dx2 = dx * dx, dy2 = dy * dy;
+                        const float sum = dx2 + dy2;
+                        if (sum > t2s2) continue;
+                        float vv;
+                        if (dx2 < 0.25f && dy2 < 0.25f) {
+                            vv = par.z;  // "closest pixel"
+                        } else {
+                            const float num = -0.5f * sum;
+                            vv = par.z * approx_exp_ref(fast ? div_refined(num, R) : num / par.w);
+                        }
+                        float *cell = &s_out[(py - ty0) * kHrPad + (px - tx0)];
+                        float v = *cell + vv;
+                        *cell = (v < 1.0f) ? v : 1.0f;  // min(max_value, f)
+                    }
+                }
+                __syncthreads();
+            }
+            if (MULTI) {
+                wave_sync();
+                if (hit_any) {
+#pragma unroll
+                    for (int r = 0; r < 16; r++) {  // np.maximum(ta, accumulated)
+                        const float acc = s_acc[(r >> 3) * 8 * kHrPad + ly * kHrPad + (r & 7) * 8 + lx];
+                        res[r] = (acc != acc || res[r] != res[r]) ? NAN : (acc > res[r] ? acc : res[r]);
+                    }
+                }
+            }
+        }
+        if (MULTI) {
+            wave_sync();
+#pragma unroll
+            for (int r = 0; r < 16; r++) s_acc[(r >> 3) * 8 * kHrPad + ly * kHrPad + (r & 7) * 8 + lx] = res[r];
+        }
+        wave_sync();
+        // ---- write the wave's stripe: 16 rows x 64 floats, 16-B nontemporal stores ----
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            const int q = k * 256 + threadIdx.x;  // float4 index in the tile
+            const int q = k * 64 + lane;  // float4 index in the stripe
             const int row = q >> 4, c4 = (q & 15) * 4;
-            const int gy = ty0 + row, gx = tx0 + c4;
-            if (gy < a.h && gx < a.pitch) {
-                typedef float v4f __attribute__((ext_vector_type(4)));
-                v4f v = {0.0f, 0.0f, 0.0f, 0.0f};
-                if (any) v = *reinterpret_cast<const v4f *>(&s_out[row * kOutPad + c4]);
-                // written once, read back only by sparse lookups: streaming (nt) store
-                __builtin_nontemporal_store(v, reinterpret_cast<v4f *>(&out[(int64_t)gy * a.pitch + gx]));
+            const v4f v = *reinterpret_cast<const v4f *>(&s_acc[row * kHrPad + c4]);
+            const int trow = wave * 16 + row;
+            if (a.flags) {
+                __builtin_nontemporal_store(
+                    v, reinterpret_cast<v4f *>(&out[(int64_t)tile * (kTile * kTile) + trow * kTile + c4]));
+            } else {
+                const int gy = ty0 + trow, gx = tx0 + c4;
+                if (gy < a.h && gx < a.pitch)
+                    __builtin_nontemporal_store(v, reinterpret_cast<v4f *>(&out[(int64_t)gy * a.pitch + gx]));
             }
         }
-    } else {
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const int px = wx0 + (r & 7) * 8 + lx, py = wy0 + (r >> 3) * 8 + ly;
-            if (px < a.w && py < a.h) {
-                out[(int64_t)py * a.pitch + px] = acc[r];
-                if (MODE == M_CUMAVG) out2[(int64_t)py * a.pitch + px] = acc2[r];
-            }
-        }
+        __syncthreads();  // s_out / s_idx reuse by the next tile
     }
 }
 
@@ -372,17 +534,15 @@ __global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
 // -------------------------------------------------------------------------------------
 static inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 
-template <int MODE, bool ZERO_INIT, bool MULTI = false>
+template <int MODE>
 static void launch_tiles(TileArgs a, hipStream_t stream) {
-    a.tiles_x = (int)((a.pitch + kTile - 1) / kTile);
-    if (!ZERO_INIT) a.tiles_x = (a.w + kTile - 1) / kTile;
+    a.tiles_x = (a.w + kTile - 1) / kTile;
     const int tiles_y = (a.h + kTile - 1) / kTile;
     a.tiles = a.tiles_x * tiles_y;
     const int64_t n_fields = a.n_work;  // caller passes the field count here
     a.n_work = n_fields * a.tiles;
     const int64_t nblocks = round_up(a.n_work, 8);
-    hipLaunchKernelGGL((splat_tile_kernel<MODE, ZERO_INIT, MULTI>), dim3((unsigned)nblocks), dim3(256),
-                       0, stream, a);
+    hipLaunchKernelGGL(splat_tile_kernel<MODE>, dim3((unsigned)nblocks), dim3(256), 0, stream, a);
 }
 
 }  // namespace pp
@@ -411,8 +571,8 @@ size_t cifhr_heads_workspace_size(const Heads &h, int n_img, int K) {
 // CifHr.fill (cif_hr.py:59-73) over the heads: the map has head 0's field size and stride
 template <bool DET>
 int cifhr_heads_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config *cfg,
-                       float *d_cifhr, void *d_workspace, size_t workspace_bytes,
-                       hipStream_t s, const char *who) {
+                       float *d_cifhr, uint8_t *d_flags, void *d_workspace,
+                       size_t workspace_bytes, hipStream_t s, const char *who) {
     if (!cfg || !d_cifhr || !d_workspace) return fail(PP_EINVAL, std::string(who) + ": NULL argument");
     for (int m = 0; m < h.n_cif; m++)
         if (!h.cif[m]) return fail(PP_EINVAL, std::string(who) + ": NULL field");
@@ -442,30 +602,34 @@ int cifhr_heads_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config
     sa.tiles_x = (int)((pitch + kTile - 1) / kTile);
     sa.tiles = sa.tiles_x * ((hh + kTile - 1) / kTile);
     hipLaunchKernelGGL(cifhr_splats_kernel<DET>, dim3((unsigned)(nf * h.n_groups)), dim3(256), 0, s, sa);
-    TileArgs a{};
+    HrTileArgs a{};
     a.field = d_cifhr;
+    a.flags = d_flags;
     a.splats = sa.splats;
     a.counts = sa.counts;
     a.tile_bits = sa.tile_bits;
     a.splat_cap = sa.list_cap;
-    a.field_stride = (int64_t)hh * pitch;
     a.h = hh;
     a.w = ww;
     a.pitch = (int)pitch;
-    a.n_work = nf;
-    a.t2 = 1.0f;  // truncate = 1.0 (cif_hr.py:40)
-    a.max_value = 1.0f;
+    a.tiles_x = sa.tiles_x;
+    a.tiles = sa.tiles;
+    a.chunks = (sa.tiles + kChunkTiles - 1) / kChunkTiles;
+    a.field_stride = d_flags ? (int64_t)sa.tiles * kTile * kTile : (int64_t)hh * pitch;
+    a.n_work = nf * a.chunks;
     a.n_groups = h.n_groups;
     for (int g = 0; g < h.n_groups; g++) a.goff[g] = sa.goff[g];
+    if (sa.tiles > kTileBits) return fail(PP_ESHAPE, std::string(who) + ": CifHr map too large");
+    const int64_t nblocks = round_up(a.n_work, 8);
     if (h.n_groups > 1)
-        launch_tiles<M_GAUSS_MAX, true, true>(a, s);
+        hipLaunchKernelGGL(cifhr_tile_kernel<true>, dim3((unsigned)nblocks), dim3(256), 0, s, a);
     else
-        launch_tiles<M_GAUSS_MAX, true, false>(a, s);
+        hipLaunchKernelGGL(cifhr_tile_kernel<false>, dim3((unsigned)nblocks), dim3(256), 0, s, a);
     return check_launch(who);
 }
 
 template int cifhr_heads_launch<false>(const Heads &, int32_t, int32_t, const pp_config *, float *,
-                                       void *, size_t, hipStream_t, const char *);
+                                       uint8_t *, void *, size_t, hipStream_t, const char *);
 
 }  // namespace pp
 
@@ -477,8 +641,8 @@ int pp_cifhr(const float *d_cif, int32_t n_img, int32_t K, int32_t H, int32_t W,
     if (!d_cif || !cfg) return fail(PP_EINVAL, "pp_cifhr: NULL argument");
     if (H <= 0 || W <= 0 || cfg->stride <= 0) return fail(PP_ESHAPE, "pp_cifhr: bad shape");
     return cifhr_heads_launch<false>(single_head(d_cif, nullptr, H, W, cfg->stride), n_img, K, cfg,
-                                     d_cifhr, d_workspace, workspace_bytes, (hipStream_t)stream,
-                                     "pp_cifhr");
+                                     d_cifhr, nullptr, d_workspace, workspace_bytes,
+                                     (hipStream_t)stream, "pp_cifhr");
 }
 
 int pp_cifdet_hr(const float *d_det, int32_t n_img, int32_t K, int32_t H, int32_t W,
@@ -487,8 +651,8 @@ int pp_cifdet_hr(const float *d_det, int32_t n_img, int32_t K, int32_t H, int32_
     if (!d_det || !cfg) return fail(PP_EINVAL, "pp_cifdet_hr: NULL argument");
     if (H <= 0 || W <= 0 || cfg->stride <= 0) return fail(PP_ESHAPE, "pp_cifdet_hr: bad shape");
     return cifhr_heads_launch<true>(single_head(d_det, nullptr, H, W, cfg->stride), n_img, K, cfg,
-                                    d_cifhr, d_workspace, workspace_bytes, (hipStream_t)stream,
-                                    "pp_cifdet_hr");
+                                    d_cifhr, nullptr, d_workspace, workspace_bytes,
+                                    (hipStream_t)stream, "pp_cifdet_hr");
 }
 
 size_t pp_cifhr_multi_workspace_size(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs,
@@ -506,8 +670,8 @@ int pp_cifhr_multi(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs, 
     Heads h;
     const int rc = make_heads(scales, n_scales, cif_pairs, PP_ROLE_CIF, &h, "pp_cifhr_multi");
     if (rc) return rc;
-    return cifhr_heads_launch<false>(h, n_img, K, cfg, d_cifhr, d_workspace, workspace_bytes,
-                                     (hipStream_t)stream, "pp_cifhr_multi");
+    return cifhr_heads_launch<false>(h, n_img, K, cfg, d_cifhr, nullptr, d_workspace,
+                                     workspace_bytes, (hipStream_t)stream, "pp_cifhr_multi");
 }
 
 }  // extern "C"
@@ -535,7 +699,6 @@ static int run_square_primitive(float *field, float *field2, int64_t h, int64_t 
     a.field = field;
     a.field2 = field2;
     a.splats = splats;
-    a.counts = nullptr;
     a.n_splats = n;
     a.splat_cap = n;
     a.field_stride = h * pitch;
@@ -545,7 +708,7 @@ static int run_square_primitive(float *field, float *field2, int64_t h, int64_t 
     a.n_work = 1;
     a.t2 = truncate * truncate;
     a.max_value = max_value;
-    launch_tiles<MODE, false>(a, st);
+    launch_tiles<MODE>(a, st);
     int rc = check_launch(name);
     hipFreeAsync(splats, st);
     return rc;

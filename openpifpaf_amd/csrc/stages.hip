@@ -61,9 +61,8 @@ __device__ void bitonic_sort(Perm *p, int np, const SeedKeys &keys) {
 
 struct SeedArgs {
     Heads h;            // CifSeeds.fill visits the heads in order (cif_seeds.py:56-64)
-    const float *hr;
-    int K, hh, ww;
-    int64_t pitch;
+    HrMap hr;
+    int K;
     float th, score_scale;
     pp_seed *seeds;     // (n_img, cap) sorted output
     int cap;            // K * sum of the heads' H * W
@@ -95,7 +94,7 @@ __global__ __launch_bounds__(256) void seeds_emit_kernel(SeedArgs a) {
     float *gx = gv + cap, *gy = gx + cap, *gs = gy + cap;
     int *gf = a.g_f + (int64_t)img * cap + a.seg_base(m, f);
     const float *p = a.h.cif[m] + ((int64_t)img * a.K + f) * 5 * hw;
-    const float *t = a.hr + ((int64_t)img * a.K + f) * a.hh * a.pitch;
+    const int64_t plane = (int64_t)img * a.K + f;
     int running = 0;
     for (int base = 0; base < hw; base += 256) {
         const int cell = base + threadIdx.x;
@@ -107,7 +106,7 @@ __global__ __launch_bounds__(256) void seeds_emit_kernel(SeedArgs a) {
             if (c > a.th && (!ms_on || p[4 * hw + cell] > ms_th)) {
                 x = p[hw + cell] * stride;
                 y = p[2 * hw + cell] * stride;
-                const float hv = hr_lookup(t, a.hh, a.ww, a.pitch, x, y, 0.0f);
+                const float hv = a.hr.at(plane, x, y, 0.0f);
                 v = 0.9f * hv + 0.1f * c;  // 0.9 * v + 0.1 * c
                 if (a.score_scale != 1.0f) v = v * a.score_scale;
                 keep = v > a.th;
@@ -267,9 +266,8 @@ constexpr int kMaxCaf = PP_MAX_EDGES;
 
 struct CafArgs {
     Heads h;            // CafScored.fill visits the heads in order (caf_scored.py:88-98)
-    const float *hr;
-    int K, C, hh, ww;
-    int64_t pitch;
+    HrMap hr;
+    int K, C;
     int64_t col_cap;    // columns per set (>= cells of all heads)
     float cif_floor, one_minus_floor;
     int nt;             // number of thresholds (1 or 2)
@@ -303,8 +301,8 @@ __global__ __launch_bounds__(256) void caf_scored_kernel(CafArgs a) {
     const int j1i = a.j1[ci], j2i = a.j2[ci];
     const bool use1 = a.cif_floor < 1.0f && j1i < a.K;
     const bool use2 = a.cif_floor < 1.0f && j2i < a.K;
-    const float *t1 = a.hr + ((int64_t)img * a.K + (use1 ? j1i : 0)) * a.hh * a.pitch;
-    const float *t2 = a.hr + ((int64_t)img * a.K + (use2 ? j2i : 0)) * a.hh * a.pitch;
+    const int64_t t1 = (int64_t)img * a.K + (use1 ? j1i : 0);
+    const int64_t t2 = (int64_t)img * a.K + (use2 ? j2i : 0);
     const int64_t cc = a.col_cap;
     int run_b[2] = {0, 0}, run_f[2] = {0, 0};
     const float th_min = a.nt == 2 ? fminf(a.th[0], a.th[1]) : a.th[0];
@@ -328,12 +326,10 @@ __global__ __launch_bounds__(256) void caf_scored_kernel(CafArgs a) {
                     sf = score;
                     if (use1)
                         sb = score * (a.cif_floor +
-                                      a.one_minus_floor *
-                                          hr_lookup(t1, a.hh, a.ww, a.pitch, nine[1], nine[2], 0.0f));
+                                      a.one_minus_floor * a.hr.at(t1, nine[1], nine[2], 0.0f));
                     if (use2)
                         sf = score * (a.cif_floor +
-                                      a.one_minus_floor *
-                                          hr_lookup(t2, a.hh, a.ww, a.pitch, nine[5], nine[6], 0.0f));
+                                      a.one_minus_floor * a.hr.at(t2, nine[5], nine[6], 0.0f));
                 }
             }
             for (int t = 0; t < a.nt; t++) {
@@ -388,9 +384,8 @@ constexpr int kMaxBuckets = 1600 + 1;
 
 struct CafBArgs {
     Heads h;
-    const float *hr;
-    int K, C, hh, ww;
-    int64_t pitch;
+    HrMap hr;
+    int K, C;
     int64_t col_cap;    // columns per set: cells of all heads
     float cif_floor, one_minus_floor, th;
     int bw, bh, nb;     // bucket grid and bucket count (bw * bh + 1)
@@ -438,8 +433,8 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
     }
     const bool use1 = need_b && a.cif_floor < 1.0f && j1i < a.K;
     const bool use2 = need_f && a.cif_floor < 1.0f && j2i < a.K;
-    const float *t1 = a.hr + ((int64_t)img * a.K + (use1 ? j1i : 0)) * a.hh * a.pitch;
-    const float *t2 = a.hr + ((int64_t)img * a.K + (use2 ? j2i : 0)) * a.hh * a.pitch;
+    const int64_t t1 = (int64_t)img * a.K + (use1 ? j1i : 0);
+    const int64_t t2 = (int64_t)img * a.K + (use2 ? j2i : 0);
     for (int i = threadIdx.x; i <= nb; i += 256) {
         s_cnt[0][i] = 0;
         s_cnt[1][i] = 0;
@@ -473,11 +468,9 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
         sb = score;
         sf = score;
         if (use1)
-            sb = score * (a.cif_floor + a.one_minus_floor *
-                                            hr_lookup(t1, a.hh, a.ww, a.pitch, nine[1], nine[2], 0.0f));
+            sb = score * (a.cif_floor + a.one_minus_floor * a.hr.at(t1, nine[1], nine[2], 0.0f));
         if (use2)
-            sf = score * (a.cif_floor + a.one_minus_floor *
-                                            hr_lookup(t2, a.hh, a.ww, a.pitch, nine[5], nine[6], 0.0f));
+            sf = score * (a.cif_floor + a.one_minus_floor * a.hr.at(t2, nine[5], nine[6], 0.0f));
         kb = need_b && sb > a.th;
         kf = need_f && sf > a.th;
     };
@@ -585,7 +578,7 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
 
 static inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 
-int launch_seeds(const Heads &h, const float *hr, int n_img, int K, const pp_config *cfg,
+int launch_seeds(const Heads &h, const HrMap &hr, int n_img, int K, const pp_config *cfg,
                  pp_seed *seeds, int cap, int *counts, void *scratch, hipStream_t s) {
     if (K > PP_MAX_KP) return fail(PP_ESHAPE, "seeds: more than PP_MAX_KP CIF fields");
     if ((int64_t)cap < (int64_t)K * h.cif_cells())
@@ -594,9 +587,6 @@ int launch_seeds(const Heads &h, const float *hr, int n_img, int K, const pp_con
     a.h = h;
     a.hr = hr;
     a.K = K;
-    a.hh = (int)hr_dim(h.cH[0], h.cstride[0]);
-    a.ww = (int)hr_dim(h.cW[0], h.cstride[0]);
-    a.pitch = pp_cifhr_pitch(a.ww);
     a.th = cfg->seed_threshold;
     a.score_scale = cfg->seed_score_scale;
     a.seeds = seeds;
@@ -627,7 +617,7 @@ size_t seeds_scratch_size(int n_img, int cap) {
            round_up((int64_t)n_img * 2 * np * sizeof(int), 256);
 }
 
-int launch_caf_scored(const Heads &h, const float *hr, int n_img, int K, int C,
+int launch_caf_scored(const Heads &h, const HrMap &hr, int n_img, int K, int C,
                       const int32_t *skeleton, const pp_config *cfg, int nt, const float *th,
                       float *const *cols, int64_t col_cap, int *const *counts, hipStream_t s,
                       const int *gate) {
@@ -638,9 +628,6 @@ int launch_caf_scored(const Heads &h, const float *hr, int n_img, int K, int C,
     a.hr = hr;
     a.K = K;
     a.C = C;
-    a.hh = (int)hr_dim(h.cH[0], h.cstride[0]);
-    a.ww = (int)hr_dim(h.cW[0], h.cstride[0]);
-    a.pitch = pp_cifhr_pitch(a.ww);
     a.col_cap = col_cap;
     a.cif_floor = cfg->cif_floor;
     a.one_minus_floor = (float)(1.0 - (double)cfg->cif_floor);  // (1.0 - self.cif_floor)
@@ -671,7 +658,7 @@ void caf_bucket_grid(int H, int W, int stride, int *bw, int *bh, int *nb, float 
     *inv_e = 1.0f / (float)e;
 }
 
-int launch_caf_bucketed(const Heads &h, const float *hr, int n_img, int K, int C,
+int launch_caf_bucketed(const Heads &h, const HrMap &hr, int n_img, int K, int C,
                         const int32_t *skeleton, const pp_config *cfg, float th, float *cols,
                         int *offs, const int *gate, bool index_only, hipStream_t s) {
     if (C > kMaxCaf) return fail(PP_ESHAPE, "caf_scored: more than PP_MAX_EDGES CAF fields");
@@ -680,9 +667,6 @@ int launch_caf_bucketed(const Heads &h, const float *hr, int n_img, int K, int C
     a.hr = hr;
     a.K = K;
     a.C = C;
-    a.hh = (int)hr_dim(h.cH[0], h.cstride[0]);
-    a.ww = (int)hr_dim(h.cW[0], h.cstride[0]);
-    a.pitch = pp_cifhr_pitch(a.ww);
     a.col_cap = h.caf_cells();
     a.cif_floor = cfg->cif_floor;
     a.one_minus_floor = (float)(1.0 - (double)cfg->cif_floor);
@@ -720,7 +704,9 @@ static int seeds_entry(const Heads &h, const float *d_cifhr, int32_t n_img, int3
     hipStream_t s = (hipStream_t)stream;
     if (hipMallocAsync(&scratch, seeds_scratch_size(n_img, seed_capacity), s) != hipSuccess)
         return fail(PP_EHIP, "pp_seeds: scratch allocation failed");
-    int rc = launch_seeds(h, d_cifhr, n_img, K, cfg, d_seeds, seed_capacity, d_counts, scratch, s);
+    const HrMap hr = dense_hr(d_cifhr, (int)hr_dim(h.cH[0], h.cstride[0]),
+                              (int)hr_dim(h.cW[0], h.cstride[0]));
+    int rc = launch_seeds(h, hr, n_img, K, cfg, d_seeds, seed_capacity, d_counts, scratch, s);
     hipFreeAsync(scratch, s);
     return rc;
 }
@@ -755,8 +741,9 @@ int pp_caf_scored(const float *d_caf, const float *d_cifhr, int32_t n_img, int32
     if (n_img == 0) return PP_OK;
     float *cols[1] = {d_cols};
     int *counts[1] = {d_counts};
-    return launch_caf_scored(single_head(nullptr, d_caf, H, W, cfg->stride), d_cifhr, n_img, K, C,
-                             skeleton, cfg, 1, &score_th, cols, (int64_t)H * W, counts,
+    return launch_caf_scored(single_head(nullptr, d_caf, H, W, cfg->stride),
+                             dense_hr(d_cifhr, (int)hr_dim(H, cfg->stride), (int)hr_dim(W, cfg->stride)),
+                             n_img, K, C, skeleton, cfg, 1, &score_th, cols, (int64_t)H * W, counts,
                              (hipStream_t)stream, nullptr);
 }
 
@@ -776,8 +763,11 @@ int pp_caf_scored_multi(const pp_scale *scales, int32_t n_scales, const float *d
     if (n_img == 0) return PP_OK;
     float *cols[1] = {d_cols};
     int *counts[1] = {d_counts};
-    return launch_caf_scored(h, d_cifhr, n_img, K, C, skeleton, cfg, 1, &score_th, cols,
-                             col_capacity, counts, (hipStream_t)stream, nullptr);
+    return launch_caf_scored(h,
+                             dense_hr(d_cifhr, (int)hr_dim(h.cH[0], h.cstride[0]),
+                                      (int)hr_dim(h.cW[0], h.cstride[0])),
+                             n_img, K, C, skeleton, cfg, 1, &score_th, cols, col_capacity, counts,
+                             (hipStream_t)stream, nullptr);
 }
 
 }  // extern "C"

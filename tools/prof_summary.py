@@ -16,7 +16,7 @@ import sys
 from collections import defaultdict
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CIFHR_KERNELS = ('cifhr_splats_kernel', 'splat_tile_kernel')
+CIFHR_KERNELS = ('cifhr_splats_kernel', 'cifhr_tile_kernel')
 CALIB_BYTES = 1 << 30
 
 
@@ -90,9 +90,9 @@ def main():
         'write_ratio_16B': round(calib.get('write16', 0.0), 4),
     }
     # per-kernel correction by the calibrated ratio of the access width each one streams
-    # with: cifhr_splats_kernel reads the fields 4 B per lane, splat_tile_kernel reads the
+    # with: cifhr_splats_kernel reads the fields 4 B per lane, cifhr_tile_kernel reads the
     # 32-B splat records 16 B per lane; both store 16 B per lane
-    read_width = {'cifhr_splats_kernel': 'read4', 'splat_tile_kernel': 'read16'}
+    read_width = {'cifhr_splats_kernel': 'read4', 'cifhr_tile_kernel': 'read16'}
     traffic = 0.0
     for k in CIFHR_KERNELS:
         traffic += (sum(fetch[k]) / len(fetch[k])) / (calib.get(read_width[k]) or 1.0)
