@@ -190,7 +190,7 @@ def main():
         'annotations_per_image': round(n_anns / max(1, args.steps * batch * world), 3)
         if stages & STAGE_GROW else None,
         'roofline': {
-            'bound': 'hbm', 'kernel': 'cifhr (cifhr_splats_kernel + splat_tile_kernel)',
+            'bound': 'hbm', 'kernel': 'cifhr (cifhr_splats_kernel + cifhr_tile_kernel)',
             'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
             'frac': round(achieved / PEAK_HBM_GBS, 4),
             'algorithmic_bytes_per_launch': cifhr_bytes, 'traffic': None,
