@@ -89,40 +89,60 @@ __global__ __launch_bounds__(256) void cifhr_splats_kernel(HrSplatArgs a) {
         const int m = a.h.member(g, i);
         const int hw = a.h.cH[m] * a.h.cW[m];
         const float *p = a.h.cif[m] + fld * (DET ? 7 : 5) * (int64_t)hw;
-        for (int base = 0; base < hw; base += 256) {
-            const int cell = base + threadIdx.x;
-            float c = 0.0f;
-            if (cell < hw) c = p[cell];
-            bool keep = (cell < hw) && (c > a.v_th);
-            if (keep && !DET && ms_on) keep = p[4 * hw + cell] > ms_th;  // p[4] > min_scale / stride
-            int total;
-            const int slot = block_compact<4>(keep, s_tmp, total);
-            if (keep) {
-                const float x = p[hw + cell] * stride;
-                const float y = p[2 * hw + cell] * stride;
-                float sg;
-                if (DET) {  // np.minimum / np.maximum propagate NaN
-                    const float w = p[4 * hw + cell], h = p[5 * hw + cell];
-                    const float mn = (w != w) ? w : ((h != h) ? h : (h < w ? h : w));
-                    sg = (0.1f * mn) * stride;
-                } else {
-                    sg = (0.5f * p[4 * hw + cell]) * stride;
-                }
-                const float sigma = (sg != sg) ? sg : fmaxf(1.0f, sg);  // np.maximum keeps NaN
-                const float v = (c / a.neighbors) / len_cifs;           // v / neighbors / len_cifs
-                Splat s;
-                s.box = splat_box<M_GAUSS_MAX>(x, y, 1.0f * sigma, a.hh, a.ww);
-                s.par = make_float4(x, y, v, sigma * sigma);
-                out[running + slot] = s;
-                if (use_bits) {  // mark the 64x64 output tiles this splat's box touches
-                    for (int ty = s.box.z / kTile; ty <= (s.box.w - 1) / kTile; ty++)
-                        for (int tx = s.box.x / kTile; tx <= (s.box.y - 1) / kTile; tx++) {
-                            const int t = ty * a.tiles_x + tx;
-                            atomicOr(&s_bits[t >> 5], 1u << (t & 31));
-                        }
+        // kU cells per thread per batch (cells base + k * 256 + tid): confidences, then the
+        // rows of passing cells, each issued for the whole batch at once
+        constexpr int kU = 8;
+        for (int base = 0; base < hw; base += 256 * kU) {
+            float c[kU], x[kU], y[kU], s4[kU], s5[kU];
+#pragma unroll
+            for (int k = 0; k < kU; k++) {
+                const int cell = base + k * 256 + (int)threadIdx.x;
+                c[k] = cell < hw ? p[cell] : NAN;  // NaN: never > v_th
+                x[k] = y[k] = s4[k] = s5[k] = 0.0f;
+            }
+#pragma unroll
+            for (int k = 0; k < kU; k++) {
+                const int cell = base + k * 256 + (int)threadIdx.x;
+                if (c[k] > a.v_th) {
+                    x[k] = p[hw + cell];
+                    y[k] = p[2 * hw + cell];
+                    s4[k] = p[4 * hw + cell];
+                    if (DET) s5[k] = p[5 * hw + cell];
                 }
             }
-            running += total;
+#pragma unroll
+            for (int k = 0; k < kU; k++) {
+                bool keep = c[k] > a.v_th;
+                if (keep && !DET && ms_on) keep = s4[k] > ms_th;  // p[4] > min_scale / stride
+                int total;
+                const int slot = block_compact<4>(keep, s_tmp, total);
+                if (keep) {
+                    const float cx = x[k] * stride;
+                    const float cy = y[k] * stride;
+                    float sg;
+                    if (DET) {  // np.minimum / np.maximum propagate NaN
+                        const float w = s4[k], h = s5[k];
+                        const float mn = (w != w) ? w : ((h != h) ? h : (h < w ? h : w));
+                        sg = (0.1f * mn) * stride;
+                    } else {
+                        sg = (0.5f * s4[k]) * stride;
+                    }
+                    const float sigma = (sg != sg) ? sg : fmaxf(1.0f, sg);  // np.maximum keeps NaN
+                    const float v = (c[k] / a.neighbors) / len_cifs;        // v / neighbors / len_cifs
+                    Splat sp;
+                    sp.box = splat_box<M_GAUSS_MAX>(cx, cy, 1.0f * sigma, a.hh, a.ww);
+                    sp.par = make_float4(cx, cy, v, sigma * sigma);
+                    out[running + slot] = sp;
+                    if (use_bits) {  // mark the 64x64 output tiles this splat's box touches
+                        for (int ty = sp.box.z / kTile; ty <= (sp.box.w - 1) / kTile; ty++)
+                            for (int tx = sp.box.x / kTile; tx <= (sp.box.y - 1) / kTile; tx++) {
+                                const int t = ty * a.tiles_x + tx;
+                                atomicOr(&s_bits[t >> 5], 1u << (t & 31));
+                            }
+                    }
+                }
+                running += total;
+            }
         }
     }
     if (threadIdx.x == 0) a.counts[blockIdx.x] = running;

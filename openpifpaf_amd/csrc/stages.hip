@@ -95,35 +95,56 @@ __global__ __launch_bounds__(256) void seeds_emit_kernel(SeedArgs a) {
     int *gf = a.g_f + (int64_t)img * cap + a.seg_base(m, f);
     const float *p = a.h.cif[m] + ((int64_t)img * a.K + f) * 5 * hw;
     const int64_t plane = (int64_t)img * a.K + f;
+    // kU cells per thread per batch (cells base + k * 256 + tid): confidences, then the rows
+    // of passing cells, then the CifHr lookups, each issued for the whole batch at once
+    constexpr int kU = 8;
     int running = 0;
-    for (int base = 0; base < hw; base += 256) {
-        const int cell = base + threadIdx.x;
-        bool keep = false;
-        float v = 0.0f, x = 0.0f, y = 0.0f, sc = 0.0f;
-        if (cell < hw) {
-            const float c = p[cell];
-            // p[:, p[0] > threshold], then p[:, p[4] > min_scale / stride]
-            if (c > a.th && (!ms_on || p[4 * hw + cell] > ms_th)) {
-                x = p[hw + cell] * stride;
-                y = p[2 * hw + cell] * stride;
-                const float hv = a.hr.at(plane, x, y, 0.0f);
-                v = 0.9f * hv + 0.1f * c;  // 0.9 * v + 0.1 * c
-                if (a.score_scale != 1.0f) v = v * a.score_scale;
-                keep = v > a.th;
-                sc = p[4 * hw + cell] * stride;
+    for (int base = 0; base < hw; base += 256 * kU) {
+        float c[kU], x[kU], y[kU], sc[kU], v[kU];
+        bool keep[kU];
+#pragma unroll
+        for (int k = 0; k < kU; k++) {
+            const int cell = base + k * 256 + (int)threadIdx.x;
+            c[k] = cell < hw ? p[cell] : NAN;
+            x[k] = y[k] = sc[k] = v[k] = 0.0f;
+        }
+#pragma unroll
+        for (int k = 0; k < kU; k++) {
+            const int cell = base + k * 256 + (int)threadIdx.x;
+            if (c[k] > a.th) {  // p[:, p[0] > threshold]
+                x[k] = p[hw + cell];
+                y[k] = p[2 * hw + cell];
+                sc[k] = p[4 * hw + cell];
             }
         }
-        int total;
-        const int slot = block_compact<4>(keep, s_tmp, total);
-        if (keep) {
-            const int pos = running + slot;
-            gv[pos] = v;
-            gx[pos] = x;
-            gy[pos] = y;
-            gs[pos] = sc;
-            gf[pos] = f;
+#pragma unroll
+        for (int k = 0; k < kU; k++) {
+            keep[k] = c[k] > a.th && (!ms_on || sc[k] > ms_th);  // then p[4] > min_scale / stride
+            if (keep[k]) {
+                x[k] = x[k] * stride;
+                y[k] = y[k] * stride;
+                const float hv = a.hr.at(plane, x[k], y[k], 0.0f);
+                float vv = 0.9f * hv + 0.1f * c[k];  // 0.9 * v + 0.1 * c
+                if (a.score_scale != 1.0f) vv = vv * a.score_scale;
+                v[k] = vv;
+                keep[k] = vv > a.th;
+                sc[k] = sc[k] * stride;
+            }
         }
-        running += total;
+#pragma unroll
+        for (int k = 0; k < kU; k++) {
+            int total;
+            const int slot = block_compact<4>(keep[k], s_tmp, total);
+            if (keep[k]) {
+                const int pos = running + slot;
+                gv[pos] = v[k];
+                gx[pos] = x[k];
+                gy[pos] = y[k];
+                gs[pos] = sc[k];
+                gf[pos] = f;
+            }
+            running += total;
+        }
     }
     if (threadIdx.x == 0) a.f_counts[blockIdx.x] = running;
 }
@@ -441,38 +462,62 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
     }
     __syncthreads();
 
-    // one cell of caf_scored.py:42-81 (both directions) of head m
-    auto score_cell = [&](const float *p, int64_t hw, float stride, int m, int cell, float nine[9],
-                          bool &kb, bool &kf, float &sb, float &sf) {
-        kb = kf = false;
-        nine[0] = p[cell];
-        if (!(nine[0] > a.th)) return;  // mask = nine[0] > score_th
-        if (!caf_distance_ok(a.h, m, p, hw, cell)) return;
-        if (INDEX_ONLY) {  // source positions only: forward (x1, y1), backward (x2, y2)
-            if (need_f) {
-                nine[1] = p[1 * hw + cell] * stride;
-                nine[2] = p[2 * hw + cell] * stride;
-            }
-            if (need_b) {
-                nine[5] = p[5 * hw + cell] * stride;
-                nine[6] = p[6 * hw + cell] * stride;
-            }
-            kb = need_b;
-            kf = need_f;
-            return;
+    // caf_scored.py:42-81 (both directions) for kU cells per thread of head m at once:
+    // cells base + k * 256 + tid.  The loads of the batch (confidences, then the rows of
+    // passing cells, then the CifHr lookups) are issued together, so one batch costs three
+    // memory round trips instead of three per cell.
+    constexpr int kU = INDEX_ONLY ? 8 : 4;
+    struct Batch {
+        float nine[kU][9];
+        float sb[kU], sf[kU];
+        bool kb[kU], kf[kU];
+    };
+    auto score_batch = [&](const float *p, int hw, float stride, int m, int base, Batch &B) {
+        const bool on_min = (a.h.dmin_on >> m) & 1u, on_max = (a.h.dmax_on >> m) & 1u;
+#pragma unroll
+        for (int k = 0; k < kU; k++) {
+            const int cell = base + k * 256 + (int)threadIdx.x;
+            B.nine[k][0] = cell < hw ? p[cell] : NAN;  // NaN: never > score_th
+            B.kb[k] = B.kf[k] = false;
         }
 #pragma unroll
-        for (int r = 1; r < 9; r++)  // b1, b2 (rows 3, 7) are never read by the decoder
-            nine[r] = (r == 3 || r == 7) ? 0.0f : p[r * hw + cell] * stride;
-        const float score = nine[0];
-        sb = score;
-        sf = score;
-        if (use1)
-            sb = score * (a.cif_floor + a.one_minus_floor * a.hr.at(t1, nine[1], nine[2], 0.0f));
-        if (use2)
-            sf = score * (a.cif_floor + a.one_minus_floor * a.hr.at(t2, nine[5], nine[6], 0.0f));
-        kb = need_b && sb > a.th;
-        kf = need_f && sf > a.th;
+        for (int k = 0; k < kU; k++) {
+            const int cell = base + k * 256 + (int)threadIdx.x;
+            if (!(B.nine[k][0] > a.th)) continue;  // mask = nine[0] > score_th
+#pragma unroll
+            for (int r = 1; r < 9; r++) {
+                const bool need = (r == 1 || r == 2 || r == 5 || r == 6) ||
+                                  (!INDEX_ONLY && (r == 4 || r == 8));
+                B.nine[k][r] = need ? p[r * hw + cell] : 0.0f;  // b1, b2 are never read
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kU; k++) {
+            if (!(B.nine[k][0] > a.th)) continue;
+            if (on_min || on_max) {  // caf_scored.py:46-56 on the raw (unstrided) vectors
+                const float dx = B.nine[k][1] - B.nine[k][5], dy = B.nine[k][2] - B.nine[k][6];
+                const float dist = sqrtf(dx * dx + dy * dy);
+                if ((on_min && !(dist > a.h.dmin_th[m])) || (on_max && !(dist < a.h.dmax_th[m])))
+                    continue;
+            }
+#pragma unroll
+            for (int r = 1; r < 9; r++) B.nine[k][r] = B.nine[k][r] * stride;
+            if (INDEX_ONLY) {  // source positions only: forward (x1, y1), backward (x2, y2)
+                B.kb[k] = need_b;
+                B.kf[k] = need_f;
+                continue;
+            }
+            const float score = B.nine[k][0];
+            float sb = score, sf = score;
+            if (use1)
+                sb = score * (a.cif_floor + a.one_minus_floor * a.hr.at(t1, B.nine[k][1], B.nine[k][2], 0.0f));
+            if (use2)
+                sf = score * (a.cif_floor + a.one_minus_floor * a.hr.at(t2, B.nine[k][5], B.nine[k][6], 0.0f));
+            B.sb[k] = sb;
+            B.sf[k] = sf;
+            B.kb[k] = need_b && sb > a.th;
+            B.kf[k] = need_f && sf > a.th;
+        }
     };
 
     // pass 1: bucket histograms (backward sources are (x2, y2), forward (x1, y1)); no
@@ -481,12 +526,14 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
         const int hw = a.h.aH[m] * a.h.aW[m];
         const float stride = (float)a.h.astride[m];
         const float *p = a.h.caf[m] + fld * 9 * hw;
-        for (int cell = threadIdx.x; cell < hw; cell += 256) {
-            float nine[9], sb, sf;
-            bool kb, kf;
-            score_cell(p, hw, stride, m, cell, nine, kb, kf, sb, sf);
-            if (kb) atomicAdd(&s_cnt[0][caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e)], 1);
-            if (kf) atomicAdd(&s_cnt[1][caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e)], 1);
+        for (int base = 0; base < hw; base += 256 * kU) {
+            Batch B;
+            score_batch(p, hw, stride, m, base, B);
+#pragma unroll
+            for (int k = 0; k < kU; k++) {
+                if (B.kb[k]) atomicAdd(&s_cnt[0][caf_bucket(B.nine[k][5], B.nine[k][6], a.bw, a.bh, a.inv_e)], 1);
+                if (B.kf[k]) atomicAdd(&s_cnt[1][caf_bucket(B.nine[k][1], B.nine[k][2], a.bw, a.bh, a.inv_e)], 1);
+            }
         }
     }
     __syncthreads();
@@ -535,42 +582,46 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
         const float stride = (float)a.h.astride[m];
         const float *p = a.h.caf[m] + fld * 9 * hw;
         const int coff = (int)a.h.caf_off[m];
-        for (int cell = threadIdx.x; cell < hw; cell += 256) {
-            float nine[9], sb, sf;
-            bool kb, kf;
-            score_cell(p, hw, stride, m, cell, nine, kb, kf, sb, sf);
-            const int key = coff + cell;
-            if (INDEX_ONLY) {
-                if (kb)
-                    reinterpret_cast<int *>(bwd)[atomicAdd(
-                        &s_cnt[0][caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e)], 1)] = key;
-                if (kf)
-                    reinterpret_cast<int *>(fwd)[atomicAdd(
-                        &s_cnt[1][caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e)], 1)] = key;
-                continue;
-            }
-            // the kColRows rows the grow kernel reads: score, source x, y, target x, y, target
-            // scale, index.  Backward sets are the reference's rows (0, 5, 6, 7, 8, 1, 2, 3, 4)
-            // with row 0 = scores_b, so their source is (x2, y2) and their target (x1, y1, s1).
-            if (kb) {
-                const int64_t c = atomicAdd(&s_cnt[0][caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e)], 1);
-                bwd[c] = sb;
-                bwd[1 * cc + c] = nine[5];
-                bwd[2 * cc + c] = nine[6];
-                bwd[3 * cc + c] = nine[1];
-                bwd[4 * cc + c] = nine[2];
-                bwd[5 * cc + c] = nine[4];
-                bwd[6 * cc + c] = __int_as_float(key);
-            }
-            if (kf) {
-                const int64_t c = atomicAdd(&s_cnt[1][caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e)], 1);
-                fwd[c] = sf;
-                fwd[1 * cc + c] = nine[1];
-                fwd[2 * cc + c] = nine[2];
-                fwd[3 * cc + c] = nine[5];
-                fwd[4 * cc + c] = nine[6];
-                fwd[5 * cc + c] = nine[8];
-                fwd[6 * cc + c] = __int_as_float(key);
+        for (int base = 0; base < hw; base += 256 * kU) {
+            Batch B;
+            score_batch(p, hw, stride, m, base, B);
+#pragma unroll
+            for (int k = 0; k < kU; k++) {
+                const int key = coff + base + k * 256 + (int)threadIdx.x;
+                const float *nine = B.nine[k];
+                if (INDEX_ONLY) {
+                    if (B.kb[k])
+                        reinterpret_cast<int *>(bwd)[atomicAdd(
+                            &s_cnt[0][caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e)], 1)] = key;
+                    if (B.kf[k])
+                        reinterpret_cast<int *>(fwd)[atomicAdd(
+                            &s_cnt[1][caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e)], 1)] = key;
+                    continue;
+                }
+                // the kColRows rows the grow kernel reads: score, source x, y, target x, y,
+                // target scale, index.  Backward sets are the reference's rows (0, 5, 6, 7, 8,
+                // 1, 2, 3, 4) with row 0 = scores_b, so their source is (x2, y2) and their
+                // target (x1, y1, s1).
+                if (B.kb[k]) {
+                    const int64_t c = atomicAdd(&s_cnt[0][caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e)], 1);
+                    bwd[c] = B.sb[k];
+                    bwd[1 * cc + c] = nine[5];
+                    bwd[2 * cc + c] = nine[6];
+                    bwd[3 * cc + c] = nine[1];
+                    bwd[4 * cc + c] = nine[2];
+                    bwd[5 * cc + c] = nine[4];
+                    bwd[6 * cc + c] = __int_as_float(key);
+                }
+                if (B.kf[k]) {
+                    const int64_t c = atomicAdd(&s_cnt[1][caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e)], 1);
+                    fwd[c] = B.sf[k];
+                    fwd[1 * cc + c] = nine[1];
+                    fwd[2 * cc + c] = nine[2];
+                    fwd[3 * cc + c] = nine[5];
+                    fwd[4 * cc + c] = nine[6];
+                    fwd[5 * cc + c] = nine[8];
+                    fwd[6 * cc + c] = __int_as_float(key);
+                }
             }
         }
     }
