@@ -190,11 +190,11 @@ def main():
         'annotations_per_image': round(n_anns / max(1, args.steps * batch * world), 3)
         if stages & STAGE_GROW else None,
         'roofline': {
-            'bound': 'hbm', 'kernel': 'cifhr (cifhr_splats_kernel + cifhr_tile_kernel)',
+            'bound': 'hbm', 'kernel': 'cifhr_sparse_kernel',
             'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
             'frac': round(achieved / PEAK_HBM_GBS, 4),
             'algorithmic_bytes_per_launch': cifhr_bytes, 'traffic': None,
-            'written_tile_frac': round(hr_tiles, 4),
+            'written_block_frac': round(hr_tiles, 6),
         },
     }
     default_run = (args.workload == 'cfg3' and args.generator == 'planted' and
@@ -248,19 +248,21 @@ def main():
         dist.destroy_process_group()
 
 
-def cifhr_stage_bytes(cif, stride, v_th, tile=64):
-    """Algorithmic HBM bytes of the decoder's CifHr stage over a batch (n, K, 5, H, W):
-    the confidence plane of every cell, the x / y / scale rows of passing cells, each
-    splat record written and read once (32 B), and the tile-major scratch map's touched
-    64x64 tiles (16 KB each, exactly the tiles the splats' boxes intersect — the same
-    box arithmetic as splat_box in csrc/splat.hip) plus one flag byte per tile.
-    Returns (bytes, fraction of tiles written)."""
+def cifhr_stage_bytes(cif, stride, v_th, tile=64, block=8, lds_list=256):
+    """Algorithmic HBM bytes of the decoder's CifHr stage (cifhr_sparse_kernel) over a
+    batch (n, K, 5, H, W): the confidence plane of every cell, the x / y / scale rows of
+    passing cells, the splat records beyond the field's LDS-resident list written and read
+    once (32 B each), the 8x8 blocks of the block-sparse map that splat boxes touch (256 B
+    each, the same box arithmetic as splat_box in csrc/splat.hip) and one u64 block mask per
+    64x64 tile.  Returns (bytes, fraction of the map's blocks written)."""
     n, k, _, h, w = cif.shape
     hh, ww = (h - 1) * stride + 1, (w - 1) * stride + 1
     tiles_x = (-(-ww // 32) * 32 + tile - 1) // tile
     tiles_y = (hh + tile - 1) // tile
     c = cif[:, :, 0]
-    img, fld, cy_i, cx_i = np.nonzero(c > np.float32(v_th))
+    keep = c > np.float32(v_th)
+    per_field = keep.reshape(n * k, -1).sum(axis=1)
+    img, fld, cy_i, cx_i = np.nonzero(keep)
     x = cif[img, fld, 1, cy_i, cx_i] * np.float32(stride)
     y = cif[img, fld, 2, cy_i, cx_i] * np.float32(stride)
     sg = (np.float32(0.5) * cif[img, fld, 4, cy_i, cx_i]) * np.float32(stride)
@@ -271,19 +273,20 @@ def cifhr_stage_bytes(cif, stride, v_th, tile=64):
         lo = np.nan_to_num(lo).astype(np.int64)
         hi = np.fmax((lo + 1).astype(np.float32), np.fmin(np.float32(size), (cen + sigma) + np.float32(1)))
         hi = np.nan_to_num(hi, nan=size).astype(np.int64)
-        return lo // tile, (hi - 1) // tile
+        return lo // block, (hi - 1) // block
 
-    tx0, tx1 = span(x, ww)
-    ty0, ty1 = span(y, hh)
-    touched = np.zeros((n, k, tiles_y, tiles_x), bool)
-    for dy in range(int((ty1 - ty0).max(initial=0)) + 1):
-        for dx in range(int((tx1 - tx0).max(initial=0)) + 1):
-            m = (ty0 + dy <= ty1) & (tx0 + dx <= tx1)
-            touched[img[m], fld[m], ty0[m] + dy, tx0[m] + dx] = True
-    n_tiles = int(touched.sum())
-    nbytes = (4 * n * k * h * w + 12 * len(img) + 64 * len(img) +
-              n_tiles * 4 * tile * tile + n * k * tiles_x * tiles_y)
-    return nbytes, n_tiles / touched.size
+    bx0, bx1 = span(x, ww)
+    by0, by1 = span(y, hh)
+    touched = np.zeros((n, k, tiles_y * tile // block, tiles_x * tile // block), bool)
+    for dy in range(int((by1 - by0).max(initial=0)) + 1):
+        for dx in range(int((bx1 - bx0).max(initial=0)) + 1):
+            m = (by0 + dy <= by1) & (bx0 + dx <= bx1)
+            touched[img[m], fld[m], by0[m] + dy, bx0[m] + dx] = True
+    n_blocks = int(touched.sum())
+    overflow = int(np.maximum(per_field - lds_list, 0).sum())
+    nbytes = (4 * n * k * h * w + 12 * len(img) + 64 * overflow +
+              n_blocks * 4 * block * block + 8 * n * k * tiles_x * tiles_y)
+    return nbytes, n_blocks / touched.size
 
 
 def committed_traffic():
@@ -297,6 +300,8 @@ def committed_traffic():
         return {}
     with open(paths[-1]) as f:
         summ = json.load(f)
+    if summ.get('cifhr_kernels') != ['cifhr_sparse_kernel']:
+        return {}  # profiled before the current CifHr kernel
     return {'traffic': summ['cifhr_traffic_bytes'],
             'traffic_source': 'profiles/' + os.path.basename(paths[-1])}
 

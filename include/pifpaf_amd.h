@@ -184,6 +184,21 @@ int pp_cifhr(const float *d_cif, int32_t n_img, int32_t K, int32_t H, int32_t W,
              void *stream);
 
 /*
+ * The same CifHr as the block-sparse map the decoder keeps (cif_hr.py:14-81, values bit-equal
+ * to pp_cifhr): the (H', pitch) plane is cut into T = pp_cifhr_sparse_tiles(H, W, stride)
+ * 64x64 tiles (row-major, ceil(pitch/64) per row) of 64 8x8 blocks.  d_map
+ * (n_img, K, T, 64 blocks, 64 px): block b = 8*by + bx of a tile holds its 8 rows of 8
+ * pixels back to back; d_masks (n_img, K, T) u64 with bit b set iff block b was written.
+ * Only blocks some splat box touches are written; every other pixel is 0.
+ * d_workspace >= pp_cifhr_sparse_workspace_size(n_img, K, H, W).
+ */
+int32_t pp_cifhr_sparse_tiles(int32_t H, int32_t W, int32_t stride);
+size_t pp_cifhr_sparse_workspace_size(int32_t n_img, int32_t K, int32_t H, int32_t W);
+int pp_cifhr_sparse(const float *d_cif, int32_t n_img, int32_t K, int32_t H, int32_t W,
+                    const pp_config *cfg, float *d_map, uint64_t *d_masks, void *d_workspace,
+                    size_t workspace_bytes, void *stream);
+
+/*
  * CifSeeds (cif_seeds.py:23-64): per image, the seeds sorted as
  * sorted(seeds, reverse=True) (cif_seeds.py:54).  d_seeds (n_img, seed_capacity) with
  * seed_capacity >= K*H*W (every cell can seed, so no overflow is possible);

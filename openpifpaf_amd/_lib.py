@@ -30,7 +30,11 @@ _SIGNATURES = {
     'pp_default_config': ([_vp], None),
     'pp_cifhr_pitch': ([_i64], _i64),
     'pp_cifhr_workspace_size': ([_i32, _i32, _i32, _i32], _sz),
+    'pp_cifhr_sparse_tiles': ([_i32, _i32, _i32], _i32),
+    'pp_cifhr_sparse_workspace_size': ([_i32, _i32, _i32, _i32], _sz),
     'pp_cifhr': ([_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _sz, _vp], ctypes.c_int),
+    'pp_cifhr_sparse': ([_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _sz, _vp],
+                        ctypes.c_int),
     'pp_seeds': ([_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp, _vp], ctypes.c_int),
     'pp_caf_scored': ([_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _f, _vp, _vp, _vp, _vp],
                       ctypes.c_int),

@@ -1754,7 +1754,7 @@ struct DecodeLayout {
     int bw, bh, nb;
     float inv_e;
     int64_t occ_cap;
-    size_t off_cifhr, off_hr_flags, off_cifhr_ws, off_seeds, off_seed_counts, off_seed_ws, off_cols[2],
+    size_t off_cifhr, off_hr_aux, off_hr_masks, off_cifhr_ws, off_seeds, off_seed_counts, off_seed_ws, off_cols[2],
         off_offs[2], off_n_work, off_need, off_occ, off_wq, off_log, off_work, off_spec, off_nms_score,
         off_nms_idx, off_nms_f, off_nms_box, total;
     size_t cifhr_ws_bytes;
@@ -1783,11 +1783,13 @@ static DecodeLayout make_layout(int n_img, int K, int C, const Heads &h, const p
         return at;
     };
     const size_t n = (size_t)n_img;
-    // scratch CifHr in the tile-major layout (HrMap): one 64x64 tile per flag
+    // scratch CifHr, block-sparse (HrMap with masks): 64x64 tiles of 8x8 blocks
     const HrMap geo = dense_hr(nullptr, d.hh, d.ww);
     d.off_cifhr = take(n * K * (size_t)geo.tiles * kHrTile * kHrTile * sizeof(float));
-    d.off_hr_flags = take(n * K * (size_t)geo.tiles);
-    d.cifhr_ws_bytes = cifhr_heads_workspace_size(h, n_img, K);
+    d.off_hr_aux = take(h.n_groups > 1 ? n * K * (size_t)geo.tiles * kHrTile * kHrTile * sizeof(float) : 0);
+    d.off_hr_masks = take(n * K * (size_t)geo.tiles * sizeof(uint64_t));
+    d.cifhr_ws_bytes = std::max(cifhr_heads_workspace_size(h, n_img, K),
+                                cifhr_sparse_workspace_size(h, n_img, K));
     d.off_cifhr_ws = take(d.cifhr_ws_bytes);
     d.off_seeds = take(n * d.seed_cap * sizeof(pp_seed));
     d.off_seed_counts = take(n * sizeof(int));
@@ -1891,21 +1893,25 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
         return fail(PP_ESHAPE, "pp_decode_batch: field too large");
     char *ws = (char *)d_workspace;
     hipStream_t s = (hipStream_t)stream;
-    // the caller's d_cifhr gets the dense map; otherwise the decoder keeps the tile-major
-    // scratch map, written only where splats land
+    // the caller's d_cifhr gets the dense map; otherwise the decoder keeps the block-sparse
+    // scratch map, written only where splat boxes land
     float *hr_base = d_cifhr ? d_cifhr : (float *)(ws + d.off_cifhr);
-    uint8_t *hr_flags = d_cifhr ? nullptr : (uint8_t *)(ws + d.off_hr_flags);
+    uint64_t *hr_masks = d_cifhr ? nullptr : (uint64_t *)(ws + d.off_hr_masks);
     HrMap hr = dense_hr(hr_base, d.hh, d.ww);
-    hr.flags = hr_flags;
+    hr.masks = hr_masks;
     pp_seed *seeds = (pp_seed *)(ws + d.off_seeds);
     int *seed_counts = (int *)(ws + d.off_seed_counts);
     float *cols[2] = {(float *)(ws + d.off_cols[0]), (float *)(ws + d.off_cols[1])};
     int *offs[2] = {(int *)(ws + d.off_offs[0]), (int *)(ws + d.off_offs[1])};
     int rc = PP_OK;
     if (stages & 1u) {
-        rc = cifhr_heads_launch<false>(h, n_img, K, cfg, hr_base, hr_flags, ws + d.off_cifhr_ws,
-                                       d.cifhr_ws_bytes, s,
-                                       "pp_decode_batch(cifhr)");
+        if (d_cifhr)
+            rc = cifhr_heads_launch<false>(h, n_img, K, cfg, d_cifhr, ws + d.off_cifhr_ws,
+                                           d.cifhr_ws_bytes, s, "pp_decode_batch(cifhr)");
+        else
+            rc = cifhr_sparse_launch(h, n_img, K, cfg, hr_base, (float *)(ws + d.off_hr_aux),
+                                     hr_masks, ws + d.off_cifhr_ws, d.cifhr_ws_bytes, s,
+                                     "pp_decode_batch(cifhr)");
         if (rc) return rc;
     }
     if (stages & 2u) {

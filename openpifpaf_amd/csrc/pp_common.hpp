@@ -56,14 +56,15 @@ __device__ __forceinline__ float hr_lookup(const float *field, int hh, int ww, i
 }
 
 // The CifHr map as the decode stages read it: dense row-major (n_img * K, hh, pitch) — the
-// caller-visible layout — or, for the decoder's scratch map, tile-major (n_img * K, tiles,
-// 64 * 64) with a per-tile flag: the tile kernel writes only tiles some splat touched, and
-// an unwritten tile reads as its true value 0.
+// caller-visible layout — or, for the decoder's scratch map, block-sparse: 64x64 tiles of
+// 8x8 blocks, (n_img * K, tiles, 64 blocks, 64 px) block-major, with one u64 per tile whose
+// bit b says block b (= 8 * by + bx) was written.  The sparse kernel writes only blocks
+// some splat box touches; an unwritten block reads as its true value 0.
 constexpr int kHrTile = 64;
 
 struct HrMap {
     const float *base;
-    const uint8_t *flags;  // tiled: (n_img * K, tiles) 1 = tile written; NULL: dense
+    const uint64_t *masks; // block-sparse: (n_img * K, tiles) written-block masks; NULL: dense
     int hh, ww;
     int64_t pitch;         // dense row pitch
     int tiles_x, tiles;    // tile grid (tiles_x = pitch / 64 rounded up)
@@ -73,10 +74,11 @@ struct HrMap {
         if (x < 0.0f || y < 0.0f || x > maxx || y > maxy) return dflt;
         if (x != x || y != y) return dflt;
         const int ix = (int)x, iy = (int)y;
-        if (!flags) return base[(plane * hh + iy) * pitch + ix];
+        if (!masks) return base[(plane * hh + iy) * pitch + ix];
         const int64_t t = plane * tiles + (iy >> 6) * tiles_x + (ix >> 6);
-        if (!flags[t]) return 0.0f;
-        return base[t * (kHrTile * kHrTile) + (iy & 63) * kHrTile + (ix & 63)];
+        const int b = ((iy >> 3) & 7) * 8 + ((ix >> 3) & 7);
+        if (!((masks[t] >> b) & 1ull)) return 0.0f;
+        return base[(t * 64 + b) * 64 + (iy & 7) * 8 + (ix & 7)];
     }
 };
 
@@ -212,10 +214,16 @@ Heads single_head(const float *cif, const float *caf, int H, int W, int stride);
 
 // stage launchers over heads (splat.hip, stages.hip)
 size_t cifhr_heads_workspace_size(const Heads &h, int n_img, int K);
-// d_flags non-NULL: write the tile-major scratch layout of HrMap (only touched tiles)
+// dense (n_img * K, hh, pitch) map, every pixel written
 template <bool DET>
 int cifhr_heads_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config *cfg,
-                       float *d_cifhr, uint8_t *d_flags, void *d_workspace,
-                       size_t workspace_bytes, hipStream_t s, const char *who);
+                       float *d_cifhr, void *d_workspace, size_t workspace_bytes, hipStream_t s,
+                       const char *who);
+// the decoder's block-sparse scratch map (HrMap with masks): d_map (n_img * K, tiles, 64, 64),
+// d_masks (n_img * K, tiles); d_aux (same size as d_map) only when h.n_groups > 1
+size_t cifhr_sparse_workspace_size(const Heads &h, int n_img, int K);
+int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config *cfg,
+                        float *d_map, float *d_aux, uint64_t *d_masks, void *d_workspace,
+                        size_t workspace_bytes, hipStream_t s, const char *who);
 
 }  // namespace pp

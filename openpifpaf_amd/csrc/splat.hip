@@ -325,7 +325,7 @@ __global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
 // K2 for CifHr: one workgroup per (field, chunk of 32 tiles = one tile-bitmap word)
 // -------------------------------------------------------------------------------------
 // The chunk's bitmap words say which tiles any splat box touches.  Untouched tiles cost a
-// flag (tile-major scratch map) or a zero-fill (dense map); the field's splat lists are
+// zero-fill; the field's splat lists are
 // loaded into LDS once when they fit (kCand entries over all groups), and each touched
 // tile selects its candidates from LDS by ballot compaction, keeping splat order.  Bigger
 // lists gather per tile from global memory in kCand chunks.
@@ -339,8 +339,7 @@ constexpr int kHrCand = 256;  // LDS list / candidate capacity (>= 256 for progr
 constexpr int kHrPad = 68;    // accumulator row pitch: ~26 KB of LDS per workgroup
 
 struct HrTileArgs {
-    float *field;           // dense (n_fields, h, pitch) or tile-major (n_fields, tiles, 64*64)
-    uint8_t *flags;         // tile-major: (n_fields, tiles) written flags; NULL = dense
+    float *field;           // dense (n_fields, h, pitch)
     const Splat *splats;    // field fld's group g list at splats + fld * splat_cap + goff[g]
     const int *counts;      // (n_fields, n_groups)
     const uint32_t *tile_bits;  // (n_fields, n_groups, kTileBits / 32)
@@ -385,9 +384,7 @@ __global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
     live &= (t1 - t0 == 32) ? ~0u : ((1u << (t1 - t0)) - 1u);
     float *out = a.field + fld * a.field_stride;
     typedef float v4f __attribute__((ext_vector_type(4)));
-    if (a.flags) {
-        if ((int)threadIdx.x < t1 - t0) a.flags[fld * a.tiles + t0 + threadIdx.x] = (live >> threadIdx.x) & 1u;
-    } else {  // dense map: untouched tiles are zero-filled, 16-B nontemporal stores
+    {  // untouched tiles are zero-filled, 16-B nontemporal stores
         const v4f z = {0.0f, 0.0f, 0.0f, 0.0f};
         for (int t = t0; t < t1; t++) {
             if ((live >> (t - t0)) & 1u) continue;
@@ -536,16 +533,291 @@ __global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
             const int row = q >> 4, c4 = (q & 15) * 4;
             const v4f v = *reinterpret_cast<const v4f *>(&s_acc[row * kHrPad + c4]);
             const int trow = wave * 16 + row;
-            if (a.flags) {
-                __builtin_nontemporal_store(
-                    v, reinterpret_cast<v4f *>(&out[(int64_t)tile * (kTile * kTile) + trow * kTile + c4]));
-            } else {
-                const int gy = ty0 + trow, gx = tx0 + c4;
-                if (gy < a.h && gx < a.pitch)
-                    __builtin_nontemporal_store(v, reinterpret_cast<v4f *>(&out[(int64_t)gy * a.pitch + gx]));
-            }
+            const int gy = ty0 + trow, gx = tx0 + c4;
+            if (gy < a.h && gx < a.pitch)
+                __builtin_nontemporal_store(v, reinterpret_cast<v4f *>(&out[(int64_t)gy * a.pitch + gx]));
         }
         __syncthreads();  // s_out / s_idx reuse by the next tile
+    }
+}
+
+// -------------------------------------------------------------------------------------
+// The decoder's CifHr: block-sparse map (HrMap with masks), one workgroup per field
+// -------------------------------------------------------------------------------------
+// Phase 1 compacts the field's splats (every group, cif_hr.py:26-40, 55-57) in the
+// reference's order: each thread loads kSpU cells per round, one barrier per round
+// orders the (cell batch, wave) counts, the first kSpList entries stay in LDS and the rest
+// go to the field's global list; a bitmap marks the 64x64 tiles the boxes touch.
+//
+// Phase 2: the four waves take the touched tiles round robin, each on its own (no
+// barriers).  Per tile a wave gathers the intersecting splats in order (ballot
+// compaction, kSpCand per pass), lane b builds block b's candidate bitmask (8x8 blocks),
+// and for every block with candidates the 64 lanes fold their pixel over the block's
+// candidates in ascending order in registers (functional.pyx:127-141) and store the
+// block's 256 contiguous bytes.  Blocks no splat box touches are never written: the
+// tile's u64 mask says which blocks hold data, and HrMap::at reads the rest as 0.
+// A tile with more than kSpCand candidates takes several passes; a block touched again
+// reloads its fold state from the map (each lane reads back only the pixel it wrote).
+//
+// MULTI (cif_hr.py:59-73): groups fold into zero separately and combine by np.maximum;
+// candidates carry their group, and a change of group closes the running fold into res.
+// Across passes res stays in the map and the open group's fold in `aux`.
+constexpr int kSpList = 256;  // splat entries of a field kept in LDS
+constexpr int kSpCand = 128;  // candidates per wave pass (two u64 block bitmasks per lane)
+constexpr int kSpU = 8;       // cells per thread per compaction round
+
+struct HrSparseArgs {
+    Heads h;
+    int hh, ww;
+    float v_th, neighbors;
+    Splat *splats;    // (n_img * K, list_cap): the entries >= kSpList of each field's list
+    int64_t list_cap;
+    float *map;       // (n_img * K, tiles, 64 blocks, 64 px)
+    float *aux;       // MULTI: open-group folds between passes, same shape as map
+    uint64_t *masks;  // (n_img * K, tiles) written blocks
+    int tiles_x, tiles;
+};
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ float nan_max(float a, float b) {  // np.maximum
+    return (a != a || b != b) ? NAN : (a > b ? a : b);
+}
+
+template <bool MULTI>
+__global__ __launch_bounds__(256) void cifhr_sparse_kernel(HrSparseArgs a) {
+    __shared__ int4 s_lbox[kSpList];
+    __shared__ float4 s_lpar[kSpList];
+    __shared__ uint32_t s_bits[kTileBits / 32];
+    __shared__ __attribute__((aligned(16))) int s_cnt[2][kSpU][4];
+    __shared__ int s_gbeg[kMaxHeads + 1];
+    __shared__ int4 s_cbox[4][kSpCand];
+    __shared__ float4 s_cpar[4][kSpCand];
+    __shared__ uint8_t s_cg[4][MULTI ? kSpCand : 1];
+    __shared__ int8_t s_bg[4][MULTI ? 64 : 1];
+
+    const int64_t fld = blockIdx.x;  // image * K + field
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (threadIdx.x < kTileBits / 32) s_bits[threadIdx.x] = 0u;
+
+    // ---- phase 1: splat list ----
+    const int ng = MULTI ? a.h.n_groups : 1;
+    Splat *glist = a.splats + fld * a.list_cap;
+    int running = 0, buf = 0;
+    for (int g = 0; g < ng; g++) {
+        if (threadIdx.x == 0) s_gbeg[g] = running;
+        const float stride = (float)a.h.cstride[g];
+        const bool ms_on = (a.h.ms_on >> g) & 1u;
+        const float ms_th = a.h.ms_th[g];
+        const float len_cifs = (float)a.h.group_size();
+        for (int i = 0; i < a.h.group_size(); i++) {
+            const int m = a.h.member(g, i);
+            const int hw = a.h.cH[m] * a.h.cW[m];
+            const float *p = a.h.cif[m] + fld * 5 * (int64_t)hw;
+            for (int base = 0; base < hw; base += 256 * kSpU) {
+                float c[kSpU], x[kSpU], y[kSpU], s4[kSpU];
+#pragma unroll
+                for (int k = 0; k < kSpU; k++) {
+                    const int cell = base + k * 256 + (int)threadIdx.x;
+                    c[k] = cell < hw ? p[cell] : NAN;  // NaN: never > v_th
+                    x[k] = y[k] = s4[k] = 0.0f;
+                }
+#pragma unroll
+                for (int k = 0; k < kSpU; k++) {
+                    const int cell = base + k * 256 + (int)threadIdx.x;
+                    if (c[k] > a.v_th) {
+                        x[k] = p[hw + cell];
+                        y[k] = p[2 * hw + cell];
+                        s4[k] = p[4 * hw + cell];
+                    }
+                }
+                bool keep[kSpU];
+                uint64_t bal[kSpU];
+#pragma unroll
+                for (int k = 0; k < kSpU; k++) {
+                    keep[k] = c[k] > a.v_th;
+                    if (keep[k] && ms_on) keep[k] = s4[k] > ms_th;  // p[4] > min_scale / stride
+                    bal[k] = __ballot(keep[k]);
+                    if (lane == 0) s_cnt[buf][k][wave] = __popcll(bal[k]);
+                }
+                __syncthreads();  // (also orders the s_bits clear before the first atomicOr)
+                int off = running;
+#pragma unroll
+                for (int k = 0; k < kSpU; k++) {
+                    const int4 q = *reinterpret_cast<const int4 *>(&s_cnt[buf][k][0]);
+                    const int mine = off + (wave > 0 ? q.x : 0) + (wave > 1 ? q.y : 0) +
+                                     (wave > 2 ? q.z : 0);
+                    off += q.x + q.y + q.z + q.w;
+                    if (keep[k]) {
+                        const int pos = mine + lane_prefix(bal[k]);
+                        const float cx = x[k] * stride, cy = y[k] * stride;
+                        const float sg = (0.5f * s4[k]) * stride;
+                        const float sigma = (sg != sg) ? sg : fmaxf(1.0f, sg);  // np.maximum keeps NaN
+                        const float v = (c[k] / a.neighbors) / len_cifs;        // v / neighbors / len_cifs
+                        const int4 box = splat_box<M_GAUSS_MAX>(cx, cy, 1.0f * sigma, a.hh, a.ww);
+                        const float4 par = make_float4(cx, cy, v, sigma * sigma);
+                        if (pos < kSpList) {
+                            s_lbox[pos] = box;
+                            s_lpar[pos] = par;
+                        } else {
+                            glist[pos].box = box;
+                            glist[pos].par = par;
+                        }
+                        for (int ty = box.z / kTile; ty <= (box.w - 1) / kTile; ty++)
+                            for (int tx = box.x / kTile; tx <= (box.y - 1) / kTile; tx++) {
+                                const int t = ty * a.tiles_x + tx;
+                                atomicOr(&s_bits[t >> 5], 1u << (t & 31));
+                            }
+                    }
+                }
+                running = off;
+                buf ^= 1;
+            }
+        }
+    }
+    if (threadIdx.x == 0) s_gbeg[ng] = running;
+    __syncthreads();
+    const int total = running;
+    for (int t = threadIdx.x; t < a.tiles; t += 256)  // untouched tiles: no block written
+        if (!((s_bits[t >> 5] >> (t & 31)) & 1u)) a.masks[fld * a.tiles + t] = 0ull;
+
+    // ---- phase 2: touched tiles, one wave each ----
+    int4 *cbox = s_cbox[wave];
+    float4 *cpar = s_cpar[wave];
+    const int lx = lane & 7, ly = lane >> 3;
+    const int nwords = (a.tiles + 31) >> 5;
+    int li = 0;
+    for (int wd = 0; wd < nwords; wd++) {
+        uint32_t bits = __builtin_amdgcn_readfirstlane(s_bits[wd]);
+        for (; bits; bits &= bits - 1) {
+            if (((li++) & 3) != wave) continue;
+            const int t = wd * 32 + __builtin_ctz(bits);
+            const int tx0 = (t % a.tiles_x) * kTile, ty0 = (t / a.tiles_x) * kTile;
+            float *mp = a.map + (fld * a.tiles + t) * (int64_t)(kTile * kTile);
+            float *ap = MULTI ? a.aux + (fld * a.tiles + t) * (int64_t)(kTile * kTile) : nullptr;
+            const int bx = tx0 + 8 * lx, by = ty0 + 8 * ly;  // lane as block: its rectangle
+            uint64_t done = 0;                               // blocks written by earlier passes
+            int cursor = 0;
+            while (true) {
+                // ---- this tile's candidates, in list order ----
+                int n = 0;
+                while (cursor < total) {
+                    const int e = cursor + lane;
+                    bool hit = false;
+                    int4 b = make_int4(0, 0, 0, 0);
+                    if (e < total) {
+                        b = e < kSpList ? s_lbox[e] : glist[e].box;
+                        hit = b.y > tx0 && b.x < tx0 + kTile && b.w > ty0 && b.z < ty0 + kTile;
+                    }
+                    const uint64_t mk = __ballot(hit);
+                    const int cnt = __popcll(mk);
+                    if (n + cnt > kSpCand) break;  // wave-uniform; chunk re-read next pass
+                    if (hit) {
+                        const int pos = n + lane_prefix(mk);
+                        cbox[pos] = b;
+                        cpar[pos] = e < kSpList ? s_lpar[e] : glist[e].par;
+                        if (MULTI) {
+                            int gg = 0;
+                            while (gg + 1 < ng && e >= s_gbeg[gg + 1]) gg++;
+                            s_cg[wave][pos] = (uint8_t)gg;
+                        }
+                    }
+                    n += cnt;
+                    cursor += 64;
+                }
+                const bool last = cursor >= total;
+                wave_sync();
+                // ---- lane = block: which candidates touch it ----
+                uint64_t m0 = 0, m1 = 0;
+                const int n0 = n < 64 ? n : 64;
+                for (int c = 0; c < n0; c++) {
+                    const int4 b = cbox[c];
+                    const bool h = b.y > bx && b.x < bx + 8 && b.w > by && b.z < by + 8;
+                    m0 |= (uint64_t)h << c;
+                }
+                for (int c = 64; c < n; c++) {
+                    const int4 b = cbox[c];
+                    const bool h = b.y > bx && b.x < bx + 8 && b.w > by && b.z < by + 8;
+                    m1 |= (uint64_t)h << (c - 64);
+                }
+                const uint64_t live = __ballot((m0 | m1) != 0);
+                // ---- fold: block by block, lane = pixel, candidates ascending ----
+                for (uint64_t rest = live; rest; rest &= rest - 1) {
+                    const int blk = __builtin_ctzll(rest);
+                    const int px = tx0 + 8 * (blk & 7) + lx, py = ty0 + 8 * (blk >> 3) + ly;
+                    const float fx = (float)px, fy = (float)py;
+                    float acc = 0.0f, res = 0.0f;
+                    int gcur = -1;
+                    if ((done >> blk) & 1ull) {  // state of an earlier pass (own pixel)
+                        if (MULTI) {
+                            res = mp[blk * 64 + lane];
+                            acc = ap[blk * 64 + lane];
+                            gcur = s_bg[wave][blk];
+                        } else {
+                            acc = mp[blk * 64 + lane];
+                        }
+                    }
+                    for (int h = 0; h < 2; h++) {
+                        for (uint64_t q = readlane64(h ? m1 : m0, blk); q; q &= q - 1) {
+                            const int c = __builtin_ctzll(q) + 64 * h;
+                            if (MULTI) {
+                                const int gc = s_cg[wave][c];
+                                if (gc != gcur) {  // np.maximum(ta, accumulated) per group
+                                    res = nan_max(acc, res);
+                                    acc = 0.0f;
+                                    gcur = gc;
+                                }
+                            }
+                            const int4 b = cbox[c];
+                            const float4 par = cpar[c];
+                            // fold_pixel<M_GAUSS_MAX>, truncate 1 (functional.pyx:127-141)
+                            const bool in = px >= b.x && px < b.y && py >= b.z && py < b.w;
+                            const float dx = fx - par.x, dy = fy - par.y;
+                            const float dx2 = dx * dx, dy2 = dy * dy;
+                            const float sum = dx2 + dy2;
+                            if (in && !(sum > 1.0f * par.w)) {
+                                float vv;
+                                if (dx2 < 0.25f && dy2 < 0.25f) {
+                                    vv = par.z;  // "closest pixel"
+                                } else {
+                                    const float num = -0.5f * sum;
+                                    const float qq = recip_ok(par.w) ? div_refined(num, recip_of(par.w))
+                                                                     : num / par.w;
+                                    vv = par.z * approx_exp_ref(qq);
+                                }
+                                const float v = acc + vv;
+                                acc = (v < 1.0f) ? v : 1.0f;  // min(max_value, f)
+                            }
+                        }
+                    }
+                    if (!MULTI) {
+                        mp[blk * 64 + lane] = acc;
+                    } else if (last) {
+                        mp[blk * 64 + lane] = nan_max(acc, res);
+                    } else {
+                        mp[blk * 64 + lane] = res;
+                        ap[blk * 64 + lane] = acc;
+                        if (lane == 0) s_bg[wave][blk] = (int8_t)gcur;
+                    }
+                }
+                done |= live;
+                if (last) {
+                    if (MULTI) {  // blocks of earlier passes the last pass did not touch
+                        for (uint64_t rest = done & ~live; rest; rest &= rest - 1) {
+                            const int blk = __builtin_ctzll(rest);
+                            mp[blk * 64 + lane] = nan_max(ap[blk * 64 + lane], mp[blk * 64 + lane]);
+                        }
+                    }
+                    break;
+                }
+                wave_sync();  // candidate arrays are rewritten by the next pass
+            }
+            if (lane == 0) a.masks[fld * a.tiles + t] = done;
+        }
     }
 }
 
@@ -591,8 +863,8 @@ size_t cifhr_heads_workspace_size(const Heads &h, int n_img, int K) {
 // CifHr.fill (cif_hr.py:59-73) over the heads: the map has head 0's field size and stride
 template <bool DET>
 int cifhr_heads_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config *cfg,
-                       float *d_cifhr, uint8_t *d_flags, void *d_workspace,
-                       size_t workspace_bytes, hipStream_t s, const char *who) {
+                       float *d_cifhr, void *d_workspace, size_t workspace_bytes, hipStream_t s,
+                       const char *who) {
     if (!cfg || !d_cifhr || !d_workspace) return fail(PP_EINVAL, std::string(who) + ": NULL argument");
     for (int m = 0; m < h.n_cif; m++)
         if (!h.cif[m]) return fail(PP_EINVAL, std::string(who) + ": NULL field");
@@ -624,7 +896,6 @@ int cifhr_heads_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config
     hipLaunchKernelGGL(cifhr_splats_kernel<DET>, dim3((unsigned)(nf * h.n_groups)), dim3(256), 0, s, sa);
     HrTileArgs a{};
     a.field = d_cifhr;
-    a.flags = d_flags;
     a.splats = sa.splats;
     a.counts = sa.counts;
     a.tile_bits = sa.tile_bits;
@@ -635,7 +906,7 @@ int cifhr_heads_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config
     a.tiles_x = sa.tiles_x;
     a.tiles = sa.tiles;
     a.chunks = (sa.tiles + kChunkTiles - 1) / kChunkTiles;
-    a.field_stride = d_flags ? (int64_t)sa.tiles * kTile * kTile : (int64_t)hh * pitch;
+    a.field_stride = (int64_t)hh * pitch;
     a.n_work = nf * a.chunks;
     a.n_groups = h.n_groups;
     for (int g = 0; g < h.n_groups; g++) a.goff[g] = sa.goff[g];
@@ -649,7 +920,47 @@ int cifhr_heads_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config
 }
 
 template int cifhr_heads_launch<false>(const Heads &, int32_t, int32_t, const pp_config *, float *,
-                                       uint8_t *, void *, size_t, hipStream_t, const char *);
+                                       void *, size_t, hipStream_t, const char *);
+
+size_t cifhr_sparse_workspace_size(const Heads &h, int n_img, int K) {
+    return round_up((int64_t)((size_t)n_img * K * (size_t)h.cif_cells() * sizeof(Splat)), 256);
+}
+
+int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config *cfg,
+                        float *d_map, float *d_aux, uint64_t *d_masks, void *d_workspace,
+                        size_t workspace_bytes, hipStream_t s, const char *who) {
+    if (!cfg || !d_map || !d_masks || !d_workspace || (h.n_groups > 1 && !d_aux))
+        return fail(PP_EINVAL, std::string(who) + ": NULL argument");
+    for (int m = 0; m < h.n_cif; m++)
+        if (!h.cif[m]) return fail(PP_EINVAL, std::string(who) + ": NULL field");
+    if (n_img < 0 || K <= 0) return fail(PP_ESHAPE, std::string(who) + ": bad shape");
+    if (n_img == 0) return PP_OK;
+    if (workspace_bytes < cifhr_sparse_workspace_size(h, n_img, K))
+        return fail(PP_ENOMEM, std::string(who) + ": workspace too small");
+    const int hh = (int)hr_dim(h.cH[0], h.cstride[0]), ww = (int)hr_dim(h.cW[0], h.cstride[0]);
+    const HrMap geo = dense_hr(nullptr, hh, ww);
+    if (geo.tiles > kTileBits) return fail(PP_ESHAPE, std::string(who) + ": CifHr map too large");
+    if (h.n_groups > 8) return fail(PP_ESHAPE, std::string(who) + ": too many CifHr groups");
+    HrSparseArgs a{};
+    a.h = h;
+    a.hh = hh;
+    a.ww = ww;
+    a.v_th = cfg->cif_threshold;
+    a.neighbors = (float)cfg->cif_neighbors;
+    a.splats = (Splat *)d_workspace;
+    a.list_cap = h.cif_cells();
+    a.map = d_map;
+    a.aux = d_aux;
+    a.masks = d_masks;
+    a.tiles_x = geo.tiles_x;
+    a.tiles = geo.tiles;
+    const unsigned nblocks = (unsigned)((int64_t)n_img * K);
+    if (h.n_groups > 1)
+        hipLaunchKernelGGL(cifhr_sparse_kernel<true>, dim3(nblocks), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(cifhr_sparse_kernel<false>, dim3(nblocks), dim3(256), 0, s, a);
+    return check_launch(who);
+}
 
 }  // namespace pp
 
@@ -661,8 +972,27 @@ int pp_cifhr(const float *d_cif, int32_t n_img, int32_t K, int32_t H, int32_t W,
     if (!d_cif || !cfg) return fail(PP_EINVAL, "pp_cifhr: NULL argument");
     if (H <= 0 || W <= 0 || cfg->stride <= 0) return fail(PP_ESHAPE, "pp_cifhr: bad shape");
     return cifhr_heads_launch<false>(single_head(d_cif, nullptr, H, W, cfg->stride), n_img, K, cfg,
-                                     d_cifhr, nullptr, d_workspace, workspace_bytes,
+                                     d_cifhr, d_workspace, workspace_bytes,
                                      (hipStream_t)stream, "pp_cifhr");
+}
+
+int32_t pp_cifhr_sparse_tiles(int32_t H, int32_t W, int32_t stride) {
+    if (H <= 0 || W <= 0 || stride <= 0) return 0;
+    return dense_hr(nullptr, (int)hr_dim(H, stride), (int)hr_dim(W, stride)).tiles;
+}
+
+size_t pp_cifhr_sparse_workspace_size(int32_t n_img, int32_t K, int32_t H, int32_t W) {
+    return pp::cifhr_sparse_workspace_size(pp::single_head(nullptr, nullptr, H, W, 1), n_img, K);
+}
+
+int pp_cifhr_sparse(const float *d_cif, int32_t n_img, int32_t K, int32_t H, int32_t W,
+                    const pp_config *cfg, float *d_map, uint64_t *d_masks, void *d_workspace,
+                    size_t workspace_bytes, void *stream) {
+    if (!d_cif || !cfg) return fail(PP_EINVAL, "pp_cifhr_sparse: NULL argument");
+    if (H <= 0 || W <= 0 || cfg->stride <= 0) return fail(PP_ESHAPE, "pp_cifhr_sparse: bad shape");
+    return cifhr_sparse_launch(single_head(d_cif, nullptr, H, W, cfg->stride), n_img, K, cfg,
+                               d_map, nullptr, d_masks, d_workspace, workspace_bytes,
+                               (hipStream_t)stream, "pp_cifhr_sparse");
 }
 
 int pp_cifdet_hr(const float *d_det, int32_t n_img, int32_t K, int32_t H, int32_t W,
@@ -671,7 +1001,7 @@ int pp_cifdet_hr(const float *d_det, int32_t n_img, int32_t K, int32_t H, int32_
     if (!d_det || !cfg) return fail(PP_EINVAL, "pp_cifdet_hr: NULL argument");
     if (H <= 0 || W <= 0 || cfg->stride <= 0) return fail(PP_ESHAPE, "pp_cifdet_hr: bad shape");
     return cifhr_heads_launch<true>(single_head(d_det, nullptr, H, W, cfg->stride), n_img, K, cfg,
-                                    d_cifhr, nullptr, d_workspace, workspace_bytes,
+                                    d_cifhr, d_workspace, workspace_bytes,
                                     (hipStream_t)stream, "pp_cifdet_hr");
 }
 
@@ -690,8 +1020,8 @@ int pp_cifhr_multi(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs, 
     Heads h;
     const int rc = make_heads(scales, n_scales, cif_pairs, PP_ROLE_CIF, &h, "pp_cifhr_multi");
     if (rc) return rc;
-    return cifhr_heads_launch<false>(h, n_img, K, cfg, d_cifhr, nullptr, d_workspace,
-                                     workspace_bytes, (hipStream_t)stream, "pp_cifhr_multi");
+    return cifhr_heads_launch<false>(h, n_img, K, cfg, d_cifhr, d_workspace, workspace_bytes,
+                                     (hipStream_t)stream, "pp_cifhr_multi");
 }
 
 }  // extern "C"

@@ -31,6 +31,41 @@ def cifhr_device(cif, stride, v_threshold, neighbors):
     return out
 
 
+def cifhr_sparse_device(cif, stride, v_threshold, neighbors):
+    """cif (n, K, 5, H, W) device tensor -> the decoder's block-sparse CifHr
+    (pp_cifhr_sparse): (map (n, K, T, 64, 64) f32, masks (n, K, T) int64 block bits)."""
+    n, k, _, h, w = cif.shape
+    lib = load()
+    t = int(lib.pp_cifhr_sparse_tiles(h, w, stride))
+    hmap = torch.empty((n, k, t, 64, 64), dtype=torch.float32, device=cif.device)
+    masks = torch.empty((n, k, t), dtype=torch.int64, device=cif.device)
+    ws = torch.empty(max(1, lib.pp_cifhr_sparse_workspace_size(n, k, h, w)), dtype=torch.uint8,
+                     device=cif.device)
+    cfg = make_config(cif_threshold=v_threshold, stride=stride, cif_neighbors=neighbors)
+    call('pp_cifhr_sparse', _device.ptr(cif), n, k, h, w, ctypes.byref(cfg), _device.ptr(hmap),
+         _device.ptr(masks), _device.ptr(ws), ctypes.c_size_t(ws.numel()), _device.stream())
+    return hmap, masks
+
+
+def sparse_to_dense(hmap, masks, hh, ww):
+    """Host (numpy) expansion of a block-sparse CifHr (cifhr_sparse_device) to (..., hh, ww);
+    blocks whose mask bit is clear read as 0, as HrMap::at does."""
+    import numpy as np
+    hmap = np.asarray(hmap)
+    bits = np.asarray(masks).view(np.uint64)
+    lead, t = hmap.shape[:-3], hmap.shape[-3]
+    pitch = -(-ww // 32) * 32
+    tx = -(-pitch // 64)
+    ty = t // tx
+    blk = hmap.reshape(lead + (t, 8, 8, 8, 8))  # (tile, by, bx, py, px)
+    on = ((bits[..., None] >> np.arange(64, dtype=np.uint64)) & np.uint64(1)).astype(bool)
+    blk = np.where(on.reshape(lead + (t, 8, 8, 1, 1)), blk, np.float32(0))
+    full = blk.reshape(lead + (ty, tx, 8, 8, 8, 8)).transpose(
+        tuple(range(len(lead))) + tuple(len(lead) + i for i in (0, 2, 4, 1, 3, 5)))
+    full = full.reshape(lead + (ty * 64, tx * 64))
+    return full[..., :hh, :ww]
+
+
 def cifdet_hr_device(det, stride, v_threshold, neighbors):
     """det (n, K, 7, H, W) device tensor -> (n, K, H', pitch) device tensor (pp_cifdet_hr)."""
     n, k, _, h, w = det.shape

@@ -305,6 +305,33 @@ def test_cifhr_batch_bit_exact():
         assert np.array_equal(uh[i], oracle.cifhr(ucif[i], cfg)), i
 
 
+def test_cifhr_sparse_bit_exact():
+    """The decoder's block-sparse CifHr (pp_cifhr_sparse) expands to the oracle's map bit for
+    bit: planted (short LDS lists), uniform (lists beyond LDS, tiles over 128 candidates)
+    and wide splats (sigma up to 40 px: every tile needs several candidate passes)."""
+    import torch
+    from openpifpaf_amd import synthetic
+    from openpifpaf_amd._abi import make_config
+    from openpifpaf_amd.decoder.cif_hr import cifhr_sparse_device, sparse_to_dense
+    cfg = make_config()
+    pcif, _ = synthetic.batch('planted', 64, 80, 80)
+    ucif, _ = synthetic.batch('uniform', 4, 80, 80)
+    rng = np.random.default_rng(5)
+    wcif = ucif[:2].copy()
+    wcif[:, :, 4] = rng.uniform(0.5, 10.0, wcif[:, :, 4].shape).astype(np.float32)
+    wcif[:, :, 0, 30:50, 30:50] = 0.9  # a dense patch of wide splats
+    for cif, n_check in ((pcif, 16), (ucif, 4), (wcif, 2)):
+        hmap, masks = cifhr_sparse_device(torch.from_numpy(cif).cuda(), 8, 0.1, 16)
+        hmap, masks = hmap.cpu().numpy(), masks.cpu().numpy()
+        step = len(cif) // n_check
+        for i in range(0, len(cif), step):
+            dense = sparse_to_dense(hmap[i], masks[i], 633, 633)
+            assert np.array_equal(dense, oracle.cifhr(cif[i], cfg)), i
+    # planted maps are sparse: most blocks never written
+    on = np.unpackbits(masks.view(np.uint8)).mean()
+    assert 0.0 < on <= 1.0
+
+
 @pytest.mark.parametrize('hw', [12, 20])  # 17*144 seeds sort in LDS, 17*400 globally
 def test_seed_ties(dec, hw):
     """Saturated CifHr gives equal v within a field: the sort must fall back to the full

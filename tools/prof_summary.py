@@ -16,7 +16,7 @@ import sys
 from collections import defaultdict
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CIFHR_KERNELS = ('cifhr_splats_kernel', 'cifhr_tile_kernel')
+CIFHR_KERNELS = ('cifhr_sparse_kernel',)
 CALIB_BYTES = 1 << 30
 
 
@@ -90,13 +90,14 @@ def main():
         'write_ratio_16B': round(calib.get('write16', 0.0), 4),
     }
     # per-kernel correction by the calibrated ratio of the access width each one streams
-    # with: cifhr_splats_kernel reads the fields 4 B per lane, cifhr_tile_kernel reads the
-    # 32-B splat records 16 B per lane; both store 16 B per lane
-    read_width = {'cifhr_splats_kernel': 'read4', 'cifhr_tile_kernel': 'read16'}
+    # with: cifhr_sparse_kernel reads the fields and stores the 8x8 blocks 4 B per lane
+    read_width = {'cifhr_sparse_kernel': 'read4'}
+    write_width = {'cifhr_sparse_kernel': 'write4'}
+    summary['write_ratio_4B'] = round(calib.get('write4', 0.0), 4)
     traffic = 0.0
     for k in CIFHR_KERNELS:
         traffic += (sum(fetch[k]) / len(fetch[k])) / (calib.get(read_width[k]) or 1.0)
-        traffic += (sum(write[k]) / len(write[k])) / (calib.get('write16') or 1.0)
+        traffic += (sum(write[k]) / len(write[k])) / (calib.get(write_width[k]) or 1.0)
     summary['cifhr_traffic_bytes'] = round(traffic)
     with open(os.path.join(dst, tag + '_summary.json'), 'w') as f:
         json.dump(summary, f, indent=1)
