@@ -17,6 +17,13 @@
 // from that XCD's L2.  Template MODE selects the functional.pyx primitive.
 #include "pp_common.hpp"
 
+#ifdef PP_STAMPS
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <vector>
+#endif
+
 namespace pp {
 
 struct Splat {
@@ -588,6 +595,52 @@ __device__ __forceinline__ float nan_max(float a, float b) {  // np.maximum
     return (a != a || b != b) ? NAN : (a > b ? a : b);
 }
 
+// the 8x8 blocks of the 64x64 tile at (tx0, ty0) that box b (end-exclusive, intersecting
+// the tile) covers: bit 8 * by + bx
+__device__ __forceinline__ uint64_t block_rect_mask(int4 b, int tx0, int ty0) {
+    const int bx0 = max(b.x - tx0, 0) >> 3, bx1 = (min(b.y - tx0, kTile) - 1) >> 3;
+    const int by0 = max(b.z - ty0, 0) >> 3, by1 = (min(b.w - ty0, kTile) - 1) >> 3;
+    const uint64_t row = (0xFFull >> (7 - bx1)) & (0xFFull << bx0);
+    const uint64_t rows = (~0ull >> (8 * (7 - by1))) & (~0ull << (8 * by0));
+    return (row * 0x0101010101010101ull) & rows;
+}
+
+// fold_pixel<M_GAUSS_MAX> with truncate 1 (functional.pyx:127-141) as straight-line selects:
+// pixel (px, py) inside box b and the circle adds v (nearest pixel) or v * approx_exp(q),
+// then min(max_value = 1, f)
+__device__ __forceinline__ float fold_gauss_max(float acc, int px, int py, float fx, float fy,
+                                                int4 b, float4 par) {
+    const bool in = (px >= b.x) & (px < b.y) & (py >= b.z) & (py < b.w);
+    const float dx = fx - par.x, dy = fy - par.y;
+    const float dx2 = dx * dx, dy2 = dy * dy;  // powf(d, 2.0)
+    const float sum = dx2 + dy2;
+    const bool take = in & !(sum > 1.0f * par.w);
+    const bool nearest = (dx2 < 0.25f) & (dy2 < 0.25f);
+    const float num = -0.5f * sum;
+    float q;
+    if (recip_ok(par.w)) q = div_refined(num, recip_of(par.w));
+    else q = num / par.w;
+    const float vv = nearest ? par.z : par.z * approx_exp_ref(q);
+    const float v = acc + vv;
+    const float f = (v < 1.0f) ? v : 1.0f;
+    return take ? f : acc;
+}
+
+#ifdef PP_STAMPS
+// diagnostic build: per workgroup [start, phase 1 done, wave 0..3 done, hw_id, xcc_id, splats]
+// in s_memrealtime ticks (100 MHz), dumped to $PP_HR_STAMPS_OUT by cifhr_sparse_launch
+__device__ uint64_t *g_hr_stamps;
+#define HR_STAMP(slot)                                                                      \
+    do {                                                                                    \
+        if (g_hr_stamps && lane == 0)                                                       \
+            g_hr_stamps[blockIdx.x * 9 + (slot)] = __builtin_amdgcn_s_memrealtime();        \
+    } while (0)
+#else
+#define HR_STAMP(slot) \
+    do {               \
+    } while (0)
+#endif
+
 template <bool MULTI>
 __global__ __launch_bounds__(256) void cifhr_sparse_kernel(HrSparseArgs a) {
     __shared__ int4 s_lbox[kSpList];
@@ -599,10 +652,14 @@ __global__ __launch_bounds__(256) void cifhr_sparse_kernel(HrSparseArgs a) {
     __shared__ float4 s_cpar[4][kSpCand];
     __shared__ uint8_t s_cg[4][MULTI ? kSpCand : 1];
     __shared__ int8_t s_bg[4][MULTI ? 64 : 1];
+    __shared__ uint64_t s_live[4];
+    __shared__ int s_next;
 
     const int64_t fld = blockIdx.x;  // image * K + field
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (wave == 0) HR_STAMP(0);
     if (threadIdx.x < kTileBits / 32) s_bits[threadIdx.x] = 0u;
+    if (threadIdx.x == 0) s_next = 0;
 
     // ---- phase 1: splat list ----
     const int ng = MULTI ? a.h.n_groups : 1;
@@ -682,143 +739,169 @@ __global__ __launch_bounds__(256) void cifhr_sparse_kernel(HrSparseArgs a) {
     if (threadIdx.x == 0) s_gbeg[ng] = running;
     __syncthreads();
     const int total = running;
+#ifdef PP_STAMPS
+    if (wave == 0) {
+        HR_STAMP(1);
+        if (g_hr_stamps && lane == 0) {
+            g_hr_stamps[blockIdx.x * 9 + 6] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+            g_hr_stamps[blockIdx.x * 9 + 7] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
+            g_hr_stamps[blockIdx.x * 9 + 8] = total;
+        }
+    }
+#endif
     for (int t = threadIdx.x; t < a.tiles; t += 256)  // untouched tiles: no block written
         if (!((s_bits[t >> 5] >> (t & 31)) & 1u)) a.masks[fld * a.tiles + t] = 0ull;
 
-    // ---- phase 2: touched tiles, one wave each ----
+    // ---- phase 2: touched tiles, one wave each, claimed from an LDS counter ----
     int4 *cbox = s_cbox[wave];
     float4 *cpar = s_cpar[wave];
     const int lx = lane & 7, ly = lane >> 3;
     const int nwords = (a.tiles + 31) >> 5;
-    int li = 0;
-    for (int wd = 0; wd < nwords; wd++) {
-        uint32_t bits = __builtin_amdgcn_readfirstlane(s_bits[wd]);
-        for (; bits; bits &= bits - 1) {
-            if (((li++) & 3) != wave) continue;
-            const int t = wd * 32 + __builtin_ctz(bits);
-            const int tx0 = (t % a.tiles_x) * kTile, ty0 = (t / a.tiles_x) * kTile;
-            float *mp = a.map + (fld * a.tiles + t) * (int64_t)(kTile * kTile);
-            float *ap = MULTI ? a.aux + (fld * a.tiles + t) * (int64_t)(kTile * kTile) : nullptr;
-            const int bx = tx0 + 8 * lx, by = ty0 + 8 * ly;  // lane as block: its rectangle
-            uint64_t done = 0;                               // blocks written by earlier passes
-            int cursor = 0;
-            while (true) {
-                // ---- this tile's candidates, in list order ----
-                int n = 0;
-                while (cursor < total) {
-                    const int e = cursor + lane;
-                    bool hit = false;
-                    int4 b = make_int4(0, 0, 0, 0);
-                    if (e < total) {
-                        b = e < kSpList ? s_lbox[e] : glist[e].box;
+    int wd = 0, li = 0;  // this wave's walk over the set bits (live index li)
+    uint32_t bits = __builtin_amdgcn_readfirstlane(s_bits[0]);
+    while (true) {
+        int claim = 0;
+        if (lane == 0) claim = atomicAdd(&s_next, 1);
+        claim = __builtin_amdgcn_readfirstlane(claim);
+        // advance to the claim-th touched tile (claims grow, so the walk only moves on)
+        int t = -1;
+        while (wd < nwords) {
+            if (!bits) {
+                if (++wd < nwords) bits = __builtin_amdgcn_readfirstlane(s_bits[wd]);
+                continue;
+            }
+            if (li == claim) {
+                t = wd * 32 + __builtin_ctz(bits);
+                break;
+            }
+            bits &= bits - 1;
+            li++;
+        }
+        if (t < 0) break;
+        const int tx0 = (t % a.tiles_x) * kTile, ty0 = (t / a.tiles_x) * kTile;
+        float *mp = a.map + (fld * a.tiles + t) * (int64_t)(kTile * kTile);
+        float *ap = MULTI ? a.aux + (fld * a.tiles + t) * (int64_t)(kTile * kTile) : nullptr;
+        uint64_t done = 0;  // blocks written by earlier passes
+        int cursor = 0;
+        while (true) {
+            // ---- this tile's candidates, in list order ----
+            int n = 0;
+            while (cursor < total) {
+                // chunks never straddle kSpList (a multiple of 64): LDS or global per chunk;
+                // the two paths stay apart so the loads keep their address space (a merged
+                // pointer would become a flat load)
+                const int e = cursor + lane;
+                const bool in_lds = cursor < kSpList;
+                bool hit = false;
+                int4 b = make_int4(0, 0, 0, 0);
+                float4 pr = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                if (e < total) {
+                    if (in_lds) {
+                        b = s_lbox[e];
+                        hit = b.y > tx0 && b.x < tx0 + kTile && b.w > ty0 && b.z < ty0 + kTile;
+                        if (hit) pr = s_lpar[e];
+                    } else {
+                        const Splat sp = glist[e];
+                        b = sp.box;
+                        pr = sp.par;
                         hit = b.y > tx0 && b.x < tx0 + kTile && b.w > ty0 && b.z < ty0 + kTile;
                     }
-                    const uint64_t mk = __ballot(hit);
-                    const int cnt = __popcll(mk);
-                    if (n + cnt > kSpCand) break;  // wave-uniform; chunk re-read next pass
-                    if (hit) {
-                        const int pos = n + lane_prefix(mk);
-                        cbox[pos] = b;
-                        cpar[pos] = e < kSpList ? s_lpar[e] : glist[e].par;
-                        if (MULTI) {
-                            int gg = 0;
-                            while (gg + 1 < ng && e >= s_gbeg[gg + 1]) gg++;
-                            s_cg[wave][pos] = (uint8_t)gg;
-                        }
-                    }
-                    n += cnt;
-                    cursor += 64;
                 }
-                const bool last = cursor >= total;
-                wave_sync();
-                // ---- lane = block: which candidates touch it ----
-                uint64_t m0 = 0, m1 = 0;
-                const int n0 = n < 64 ? n : 64;
-                for (int c = 0; c < n0; c++) {
-                    const int4 b = cbox[c];
-                    const bool h = b.y > bx && b.x < bx + 8 && b.w > by && b.z < by + 8;
-                    m0 |= (uint64_t)h << c;
-                }
-                for (int c = 64; c < n; c++) {
-                    const int4 b = cbox[c];
-                    const bool h = b.y > bx && b.x < bx + 8 && b.w > by && b.z < by + 8;
-                    m1 |= (uint64_t)h << (c - 64);
-                }
-                const uint64_t live = __ballot((m0 | m1) != 0);
-                // ---- fold: block by block, lane = pixel, candidates ascending ----
-                for (uint64_t rest = live; rest; rest &= rest - 1) {
-                    const int blk = __builtin_ctzll(rest);
-                    const int px = tx0 + 8 * (blk & 7) + lx, py = ty0 + 8 * (blk >> 3) + ly;
-                    const float fx = (float)px, fy = (float)py;
-                    float acc = 0.0f, res = 0.0f;
-                    int gcur = -1;
-                    if ((done >> blk) & 1ull) {  // state of an earlier pass (own pixel)
-                        if (MULTI) {
-                            res = mp[blk * 64 + lane];
-                            acc = ap[blk * 64 + lane];
-                            gcur = s_bg[wave][blk];
-                        } else {
-                            acc = mp[blk * 64 + lane];
-                        }
-                    }
-                    for (int h = 0; h < 2; h++) {
-                        for (uint64_t q = readlane64(h ? m1 : m0, blk); q; q &= q - 1) {
-                            const int c = __builtin_ctzll(q) + 64 * h;
-                            if (MULTI) {
-                                const int gc = s_cg[wave][c];
-                                if (gc != gcur) {  // np.maximum(ta, accumulated) per group
-                                    res = nan_max(acc, res);
-                                    acc = 0.0f;
-                                    gcur = gc;
-                                }
-                            }
-                            const int4 b = cbox[c];
-                            const float4 par = cpar[c];
-                            // fold_pixel<M_GAUSS_MAX>, truncate 1 (functional.pyx:127-141)
-                            const bool in = px >= b.x && px < b.y && py >= b.z && py < b.w;
-                            const float dx = fx - par.x, dy = fy - par.y;
-                            const float dx2 = dx * dx, dy2 = dy * dy;
-                            const float sum = dx2 + dy2;
-                            if (in && !(sum > 1.0f * par.w)) {
-                                float vv;
-                                if (dx2 < 0.25f && dy2 < 0.25f) {
-                                    vv = par.z;  // "closest pixel"
-                                } else {
-                                    const float num = -0.5f * sum;
-                                    const float qq = recip_ok(par.w) ? div_refined(num, recip_of(par.w))
-                                                                     : num / par.w;
-                                    vv = par.z * approx_exp_ref(qq);
-                                }
-                                const float v = acc + vv;
-                                acc = (v < 1.0f) ? v : 1.0f;  // min(max_value, f)
-                            }
-                        }
-                    }
-                    if (!MULTI) {
-                        mp[blk * 64 + lane] = acc;
-                    } else if (last) {
-                        mp[blk * 64 + lane] = nan_max(acc, res);
-                    } else {
-                        mp[blk * 64 + lane] = res;
-                        ap[blk * 64 + lane] = acc;
-                        if (lane == 0) s_bg[wave][blk] = (int8_t)gcur;
+                const uint64_t mk = __ballot(hit);
+                const int cnt = __popcll(mk);
+                if (n + cnt > kSpCand) break;  // wave-uniform; chunk re-read next pass
+                if (hit) {
+                    const int pos = n + lane_prefix(mk);
+                    cbox[pos] = b;
+                    cpar[pos] = pr;
+                    if (MULTI) {
+                        int gg = 0;
+                        while (gg + 1 < ng && e >= s_gbeg[gg + 1]) gg++;
+                        s_cg[wave][pos] = (uint8_t)gg;
                     }
                 }
-                done |= live;
-                if (last) {
-                    if (MULTI) {  // blocks of earlier passes the last pass did not touch
-                        for (uint64_t rest = done & ~live; rest; rest &= rest - 1) {
-                            const int blk = __builtin_ctzll(rest);
-                            mp[blk * 64 + lane] = nan_max(ap[blk * 64 + lane], mp[blk * 64 + lane]);
-                        }
-                    }
-                    break;
-                }
-                wave_sync();  // candidate arrays are rewritten by the next pass
+                n += cnt;
+                cursor += 64;
             }
-            if (lane == 0) a.masks[fld * a.tiles + t] = done;
+            const bool last = cursor >= total;
+            if (lane == 0) s_live[wave] = 0ull;
+            wave_sync();
+            // ---- lane = candidate: the tile's 8x8 blocks its box covers ----
+            uint64_t cm0 = 0, cm1 = 0;
+            if (lane < n) cm0 = block_rect_mask(cbox[lane], tx0, ty0);
+            if (lane + 64 < n) cm1 = block_rect_mask(cbox[lane + 64], tx0, ty0);
+            if (cm0 | cm1) atomicOr((unsigned long long *)&s_live[wave], (unsigned long long)(cm0 | cm1));
+            wave_sync();
+            const uint64_t live = __builtin_amdgcn_readfirstlane((uint32_t)s_live[wave]) |
+                                  ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_live[wave] >> 32)) << 32);
+            // ---- fold: block by block, lane = pixel, candidates ascending ----
+            for (uint64_t rest = live; rest; rest &= rest - 1) {
+                const int blk = __builtin_ctzll(rest);
+                const int px = tx0 + 8 * (blk & 7) + lx, py = ty0 + 8 * (blk >> 3) + ly;
+                const float fx = (float)px, fy = (float)py;
+                float acc = 0.0f, res = 0.0f;
+                int gcur = -1;
+                if ((done >> blk) & 1ull) {  // state of an earlier pass (own pixel)
+                    if (MULTI) {
+                        res = mp[blk * 64 + lane];
+                        acc = ap[blk * 64 + lane];
+                        gcur = s_bg[wave][blk];
+                    } else {
+                        acc = mp[blk * 64 + lane];
+                    }
+                }
+                uint64_t qa = __ballot((cm0 >> blk) & 1ull), qb = __ballot((cm1 >> blk) & 1ull);
+                // candidates in ascending order; the next one's LDS reads are issued before
+                // the current one folds
+                int c = qa ? __builtin_ctzll(qa) : 64 + __builtin_ctzll(qb);
+                if (qa) qa &= qa - 1; else qb &= qb - 1;
+                int4 b = cbox[c];
+                float4 par = cpar[c];
+                int gc = MULTI ? s_cg[wave][c] : 0;
+                while (true) {
+                    const bool more = (qa | qb) != 0;
+                    const int cn = !more ? c : (qa ? __builtin_ctzll(qa) : 64 + __builtin_ctzll(qb));
+                    if (qa) qa &= qa - 1; else qb &= qb - 1;
+                    const int4 bn = cbox[cn];
+                    const float4 pn = cpar[cn];
+                    const int gn = MULTI ? s_cg[wave][cn] : 0;
+                    if (MULTI && gc != gcur) {  // np.maximum(ta, accumulated) per group
+                        res = nan_max(acc, res);
+                        acc = 0.0f;
+                        gcur = gc;
+                    }
+                    acc = fold_gauss_max(acc, px, py, fx, fy, b, par);
+                    if (!more) break;
+                    c = cn;
+                    b = bn;
+                    par = pn;
+                    gc = gn;
+                }
+                if (!MULTI) {
+                    mp[blk * 64 + lane] = acc;
+                } else if (last) {
+                    mp[blk * 64 + lane] = nan_max(acc, res);
+                } else {
+                    mp[blk * 64 + lane] = res;
+                    ap[blk * 64 + lane] = acc;
+                    if (lane == 0) s_bg[wave][blk] = (int8_t)gcur;
+                }
+            }
+            done |= live;
+            if (last) {
+                if (MULTI) {  // blocks of earlier passes the last pass did not touch
+                    for (uint64_t rest = done & ~live; rest; rest &= rest - 1) {
+                        const int blk = __builtin_ctzll(rest);
+                        mp[blk * 64 + lane] = nan_max(ap[blk * 64 + lane], mp[blk * 64 + lane]);
+                    }
+                }
+                break;
+            }
+            wave_sync();  // candidate arrays are rewritten by the next pass
         }
+        if (lane == 0) a.masks[fld * a.tiles + t] = done;
     }
+    HR_STAMP(2 + wave);
 }
 
 // -------------------------------------------------------------------------------------
@@ -955,10 +1038,31 @@ int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_confi
     a.tiles_x = geo.tiles_x;
     a.tiles = geo.tiles;
     const unsigned nblocks = (unsigned)((int64_t)n_img * K);
+#ifdef PP_STAMPS
+    uint64_t *st = nullptr;
+    hipMalloc((void **)&st, (size_t)nblocks * 9 * sizeof(uint64_t));
+    hipMemcpyToSymbolAsync(HIP_SYMBOL(g_hr_stamps), &st, sizeof(st), 0, hipMemcpyHostToDevice, s);
+#endif
     if (h.n_groups > 1)
         hipLaunchKernelGGL(cifhr_sparse_kernel<true>, dim3(nblocks), dim3(256), 0, s, a);
     else
         hipLaunchKernelGGL(cifhr_sparse_kernel<false>, dim3(nblocks), dim3(256), 0, s, a);
+#ifdef PP_STAMPS
+    {
+        hipStreamSynchronize(s);
+        std::vector<uint64_t> hbuf((size_t)nblocks * 9);
+        hipMemcpy(hbuf.data(), st, hbuf.size() * sizeof(uint64_t), hipMemcpyDeviceToHost);
+        const char *path = getenv("PP_HR_STAMPS_OUT");
+        FILE *fo = fopen(path ? path : "pp_hr_stamps.bin", "ab");
+        if (fo) {
+            fwrite(hbuf.data(), sizeof(uint64_t), hbuf.size(), fo);
+            fclose(fo);
+        }
+        uint64_t *nul = nullptr;
+        hipMemcpyToSymbol(HIP_SYMBOL(g_hr_stamps), &nul, sizeof(nul));
+        hipFree(st);
+    }
+#endif
     return check_launch(who);
 }
 

@@ -1,0 +1,19 @@
+"""Run the decoder's CifHr (pp_cifhr_sparse) alone on a planted 256-image batch, for
+rocprofv3 counter passes: python tools/hr_run.py [planted|uniform] [n]"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from openpifpaf_amd import synthetic  # noqa: E402
+from openpifpaf_amd.decoder.cif_hr import cifhr_sparse_device  # noqa: E402
+
+kind = sys.argv[1] if len(sys.argv) > 1 else 'planted'
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+cif, _ = synthetic.batch(kind, n, 80, 80)
+c = torch.from_numpy(cif).cuda()
+for _ in range(3):
+    cifhr_sparse_device(c, 8, 0.1, 16)
+torch.cuda.synchronize()
+print('ok')
