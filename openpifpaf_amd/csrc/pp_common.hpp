@@ -77,8 +77,11 @@ struct HrMap {
         if (!masks) return base[(plane * hh + iy) * pitch + ix];
         const int64_t t = plane * tiles + (iy >> 6) * tiles_x + (ix >> 6);
         const int b = ((iy >> 3) & 7) * 8 + ((ix >> 3) & 7);
-        if (!((masks[t] >> b) & 1ull)) return 0.0f;
-        return base[(t * 64 + b) * 64 + (iy & 7) * 8 + (ix & 7)];
+        // a block's slot is fixed, so the value is loaded together with the mask (one
+        // memory round trip) and dropped when the block was not written this launch
+        const uint64_t m = masks[t];
+        const float v = base[(t * 64 + b) * 64 + (iy & 7) * 8 + (ix & 7)];
+        return ((m >> b) & 1ull) ? v : 0.0f;
     }
 };
 

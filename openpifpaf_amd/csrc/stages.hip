@@ -432,10 +432,31 @@ __device__ __forceinline__ int caf_bucket(float x, float y, int bw, int bh, floa
 // threshold (caf_scored.py:63-81) are applied by the query (grow.hip, consider_raw) to the
 // few columns in its box; both filters commute with the bucketing and the tie-break key is
 // the cell index either way.
-template <bool INDEX_ONLY>
-__global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
+//
+// STASH: the fields are read ONCE.  Pass 1 scores the cells, builds the bucket histograms
+// and keeps what pass 2 scatters in LDS: for set A the kept columns themselves (any order:
+// the grow kernel's merge ignores the order inside a bucket), for set B each cell's two
+// bucket ids.  A set-A stash that overflows (more than kStashA kept columns in a direction)
+// makes pass 2 recompute from the fields, as the non-STASH kernel always does.
+constexpr int kStashA = 384;      // kept columns per direction (set A stash)
+constexpr int kStashCells = 8192; // cells of all heads (set B stash: u16 bucket per direction)
+constexpr uint16_t kNoBucket = 0xFFFF;
+
+struct StashCol {
+    float v[7];  // score, source x, y, target x, y, target scale, index bits
+    int bucket;
+};
+
+template <bool INDEX_ONLY, bool STASH>
+__global__ __launch_bounds__(STASH && INDEX_ONLY ? 512 : 256) void caf_bucketed_kernel(CafBArgs a) {
+    constexpr int NT = STASH && INDEX_ONLY ? 512 : 256;
+    constexpr int NW = NT / 64;
     __shared__ int s_cnt[2][kMaxBuckets + 1];
-    __shared__ int s_wsum[2][4];
+    __shared__ int s_wsum[2][NW];
+    __shared__ __attribute__((aligned(16))) char s_stash[STASH ? (INDEX_ONLY ? 2 * kStashCells * 2 : 2 * kStashA * (int)sizeof(StashCol)) : 16];
+    __shared__ int s_sn[2], s_ovf;
+    StashCol *stash_a = reinterpret_cast<StashCol *>(s_stash);       // [2][kStashA]
+    uint16_t *stash_b = reinterpret_cast<uint16_t *>(s_stash);       // [2][kStashCells]
     const int64_t fld = blockIdx.x;  // image * C + caf field
     const int img = (int)(fld / a.C), ci = (int)(fld % a.C);
     const int nb = a.nb;
@@ -446,7 +467,7 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
     const bool need_b = !a.gate || ((a.gate[img] >> j1i) & 1);
     const bool need_f = !a.gate || ((a.gate[img] >> j2i) & 1);
     if (!need_b && !need_f) {
-        for (int i = threadIdx.x; i <= nb; i += 256) {
+        for (int i = threadIdx.x; i <= nb; i += NT) {
             offs_b[i] = 0;
             offs_f[i] = 0;
         }
@@ -456,14 +477,18 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
     const bool use2 = need_f && a.cif_floor < 1.0f && j2i < a.K;
     const int64_t t1 = (int64_t)img * a.K + (use1 ? j1i : 0);
     const int64_t t2 = (int64_t)img * a.K + (use2 ? j2i : 0);
-    for (int i = threadIdx.x; i <= nb; i += 256) {
+    for (int i = threadIdx.x; i <= nb; i += NT) {
         s_cnt[0][i] = 0;
         s_cnt[1][i] = 0;
+    }
+    if (threadIdx.x == 0) {
+        s_sn[0] = s_sn[1] = 0;
+        s_ovf = 0;
     }
     __syncthreads();
 
     // caf_scored.py:42-81 (both directions) for kU cells per thread of head m at once:
-    // cells base + k * 256 + tid.  The loads of the batch (confidences, then the rows of
+    // cells base + k * NT + tid.  The loads of the batch (confidences, then the rows of
     // passing cells, then the CifHr lookups) are issued together, so one batch costs three
     // memory round trips instead of three per cell.
     constexpr int kU = INDEX_ONLY ? 8 : 4;
@@ -476,13 +501,13 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
         const bool on_min = (a.h.dmin_on >> m) & 1u, on_max = (a.h.dmax_on >> m) & 1u;
 #pragma unroll
         for (int k = 0; k < kU; k++) {
-            const int cell = base + k * 256 + (int)threadIdx.x;
+            const int cell = base + k * NT + (int)threadIdx.x;
             B.nine[k][0] = cell < hw ? p[cell] : NAN;  // NaN: never > score_th
             B.kb[k] = B.kf[k] = false;
         }
 #pragma unroll
         for (int k = 0; k < kU; k++) {
-            const int cell = base + k * 256 + (int)threadIdx.x;
+            const int cell = base + k * NT + (int)threadIdx.x;
             if (!(B.nine[k][0] > a.th)) continue;  // mask = nine[0] > score_th
 #pragma unroll
             for (int r = 1; r < 9; r++) {
@@ -526,19 +551,64 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
         const int hw = a.h.aH[m] * a.h.aW[m];
         const float stride = (float)a.h.astride[m];
         const float *p = a.h.caf[m] + fld * 9 * hw;
-        for (int base = 0; base < hw; base += 256 * kU) {
+        const int coff = (int)a.h.caf_off[m];
+        for (int base = 0; base < hw; base += NT * kU) {
             Batch B;
             score_batch(p, hw, stride, m, base, B);
 #pragma unroll
             for (int k = 0; k < kU; k++) {
-                if (B.kb[k]) atomicAdd(&s_cnt[0][caf_bucket(B.nine[k][5], B.nine[k][6], a.bw, a.bh, a.inv_e)], 1);
-                if (B.kf[k]) atomicAdd(&s_cnt[1][caf_bucket(B.nine[k][1], B.nine[k][2], a.bw, a.bh, a.inv_e)], 1);
+                const int cell = base + k * NT + (int)threadIdx.x;
+                const float *nine = B.nine[k];
+                const int bkb = B.kb[k] ? caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e) : -1;
+                const int bkf = B.kf[k] ? caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e) : -1;
+                if (bkb >= 0) atomicAdd(&s_cnt[0][bkb], 1);
+                if (bkf >= 0) atomicAdd(&s_cnt[1][bkf], 1);
+                if (STASH && INDEX_ONLY) {
+                    if (cell < hw) {
+                        stash_b[coff + cell] = bkb >= 0 ? (uint16_t)bkb : kNoBucket;
+                        stash_b[kStashCells + coff + cell] = bkf >= 0 ? (uint16_t)bkf : kNoBucket;
+                    }
+                } else if (STASH) {
+                    const float key = __int_as_float(coff + cell);
+                    if (bkb >= 0) {
+                        const int sl = atomicAdd(&s_sn[0], 1);
+                        if (sl < kStashA) {
+                            StashCol &e = stash_a[sl];
+                            e.v[0] = B.sb[k];
+                            e.v[1] = nine[5];
+                            e.v[2] = nine[6];
+                            e.v[3] = nine[1];
+                            e.v[4] = nine[2];
+                            e.v[5] = nine[4];
+                            e.v[6] = key;
+                            e.bucket = bkb;
+                        } else {
+                            s_ovf = 1;
+                        }
+                    }
+                    if (bkf >= 0) {
+                        const int sl = atomicAdd(&s_sn[1], 1);
+                        if (sl < kStashA) {
+                            StashCol &e = stash_a[kStashA + sl];
+                            e.v[0] = B.sf[k];
+                            e.v[1] = nine[1];
+                            e.v[2] = nine[2];
+                            e.v[3] = nine[5];
+                            e.v[4] = nine[6];
+                            e.v[5] = nine[8];
+                            e.v[6] = key;
+                            e.bucket = bkf;
+                        } else {
+                            s_ovf = 1;
+                        }
+                    }
+                }
             }
         }
     }
     __syncthreads();
     // exclusive prefix over the buckets (thread-contiguous ranges + block scan)
-    const int per = (nb + 255) / 256;
+    const int per = (nb + NT - 1) / NT;
     const int b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
     int sum[2] = {0, 0};
     for (int d = 0; d < 2; d++)
@@ -565,7 +635,11 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
             offs[i] = base;
             base += c;
         }
-        if (threadIdx.x == 255) offs[nb] = s_wsum[d][0] + s_wsum[d][1] + s_wsum[d][2] + s_wsum[d][3];
+        if (threadIdx.x == NT - 1) {
+            int tot = 0;
+            for (int w = 0; w < NW; w++) tot += s_wsum[d][w];
+            offs[nb] = tot;
+        }
     }
     __syncthreads();
 
@@ -577,17 +651,39 @@ __global__ __launch_bounds__(256) void caf_bucketed_kernel(CafBArgs a) {
     const int64_t cc = a.col_cap;
     float *bwd = a.cols + (fld * 2 + 0) * rows * cc;
     float *fwd = a.cols + (fld * 2 + 1) * rows * cc;
+    if (STASH && INDEX_ONLY) {
+        const int ncell = (int)cc;
+        for (int cell = threadIdx.x; cell < ncell; cell += NT) {
+            const uint16_t bb = stash_b[cell], bf = stash_b[kStashCells + cell];
+            if (bb != kNoBucket) reinterpret_cast<int *>(bwd)[atomicAdd(&s_cnt[0][bb], 1)] = cell;
+            if (bf != kNoBucket) reinterpret_cast<int *>(fwd)[atomicAdd(&s_cnt[1][bf], 1)] = cell;
+        }
+        return;
+    }
+    if (STASH && !s_ovf) {
+        for (int d = 0; d < 2; d++) {
+            float *out = d ? fwd : bwd;
+            const int n = s_sn[d];
+            for (int i = threadIdx.x; i < n; i += NT) {
+                const StashCol &e = stash_a[d * kStashA + i];
+                const int64_t c = atomicAdd(&s_cnt[d][e.bucket], 1);
+#pragma unroll
+                for (int r = 0; r < kColRows; r++) out[r * cc + c] = e.v[r];
+            }
+        }
+        return;
+    }
     for (int m = 0; m < a.h.n_caf; m++) {
         const int hw = a.h.aH[m] * a.h.aW[m];
         const float stride = (float)a.h.astride[m];
         const float *p = a.h.caf[m] + fld * 9 * hw;
         const int coff = (int)a.h.caf_off[m];
-        for (int base = 0; base < hw; base += 256 * kU) {
+        for (int base = 0; base < hw; base += NT * kU) {
             Batch B;
             score_batch(p, hw, stride, m, base, B);
 #pragma unroll
             for (int k = 0; k < kU; k++) {
-                const int key = coff + base + k * 256 + (int)threadIdx.x;
+                const int key = coff + base + k * NT + (int)threadIdx.x;
                 const float *nine = B.nine[k];
                 if (INDEX_ONLY) {
                     if (B.kb[k])
@@ -730,12 +826,13 @@ int launch_caf_bucketed(const Heads &h, const HrMap &hr, int n_img, int K, int C
         a.j1[i] = skeleton[2 * i] - 1;
         a.j2[i] = skeleton[2 * i + 1] - 1;
     }
-    if (index_only)
-        hipLaunchKernelGGL(caf_bucketed_kernel<true>, dim3((unsigned)((int64_t)n_img * C)),
-                           dim3(256), 0, s, a);
+    const dim3 grid((unsigned)((int64_t)n_img * C));
+    if (index_only && a.col_cap <= kStashCells)
+        hipLaunchKernelGGL((caf_bucketed_kernel<true, true>), grid, dim3(512), 0, s, a);
+    else if (index_only)
+        hipLaunchKernelGGL((caf_bucketed_kernel<true, false>), grid, dim3(256), 0, s, a);
     else
-        hipLaunchKernelGGL(caf_bucketed_kernel<false>, dim3((unsigned)((int64_t)n_img * C)),
-                           dim3(256), 0, s, a);
+        hipLaunchKernelGGL((caf_bucketed_kernel<false, true>), grid, dim3(256), 0, s, a);
     return check_launch("caf_scored(bucketed)");
 }
 
