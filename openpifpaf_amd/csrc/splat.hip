@@ -641,27 +641,16 @@ __device__ uint64_t *g_hr_stamps;
     } while (0)
 #endif
 
+// Phase 1 of the CifHr kernels: the field's splat list in the reference's order (every
+// group, cif_hr.py:26-40, 55-57).  Each thread loads kSpU cells per round and one barrier
+// per round orders the (cell batch, wave) counts; the first kSpList entries stay in LDS
+// (s_lbox / s_lpar), the rest go to the field's global list; s_bits marks the 64x64 tiles
+// the boxes touch (cleared by the caller before the first barrier).  Returns the list
+// length; s_gbeg[g] = start of group g's entries.  Ends with a barrier.
 template <bool MULTI>
-__global__ __launch_bounds__(256) void cifhr_sparse_kernel(HrSparseArgs a) {
-    __shared__ int4 s_lbox[kSpList];
-    __shared__ float4 s_lpar[kSpList];
-    __shared__ uint32_t s_bits[kTileBits / 32];
-    __shared__ __attribute__((aligned(16))) int s_cnt[2][kSpU][4];
-    __shared__ int s_gbeg[kMaxHeads + 1];
-    __shared__ int4 s_cbox[4][kSpCand];
-    __shared__ float4 s_cpar[4][kSpCand];
-    __shared__ uint8_t s_cg[4][MULTI ? kSpCand : 1];
-    __shared__ int8_t s_bg[4][MULTI ? 64 : 1];
-    __shared__ uint64_t s_live[4];
-    __shared__ int s_next;
-
-    const int64_t fld = blockIdx.x;  // image * K + field
+__device__ int hr_splat_list(const HrSparseArgs &a, int64_t fld, int4 *s_lbox, float4 *s_lpar,
+                             uint32_t *s_bits, int (*s_cnt)[kSpU][4], int *s_gbeg) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (wave == 0) HR_STAMP(0);
-    if (threadIdx.x < kTileBits / 32) s_bits[threadIdx.x] = 0u;
-    if (threadIdx.x == 0) s_next = 0;
-
-    // ---- phase 1: splat list ----
     const int ng = MULTI ? a.h.n_groups : 1;
     Splat *glist = a.splats + fld * a.list_cap;
     int running = 0, buf = 0;
@@ -738,7 +727,32 @@ __global__ __launch_bounds__(256) void cifhr_sparse_kernel(HrSparseArgs a) {
     }
     if (threadIdx.x == 0) s_gbeg[ng] = running;
     __syncthreads();
-    const int total = running;
+    return running;
+}
+
+template <bool MULTI>
+__global__ __launch_bounds__(256) void cifhr_sparse_kernel(HrSparseArgs a) {
+    __shared__ int4 s_lbox[kSpList];
+    __shared__ float4 s_lpar[kSpList];
+    __shared__ uint32_t s_bits[kTileBits / 32];
+    __shared__ __attribute__((aligned(16))) int s_cnt[2][kSpU][4];
+    __shared__ int s_gbeg[kMaxHeads + 1];
+    __shared__ int4 s_cbox[4][kSpCand];
+    __shared__ float4 s_cpar[4][kSpCand];
+    __shared__ uint8_t s_cg[4][MULTI ? kSpCand : 1];
+    __shared__ int8_t s_bg[4][MULTI ? 64 : 1];
+    __shared__ uint64_t s_live[4];
+    __shared__ int s_next;
+
+    const int64_t fld = blockIdx.x;  // image * K + field
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (wave == 0) HR_STAMP(0);
+    if (threadIdx.x < kTileBits / 32) s_bits[threadIdx.x] = 0u;
+    if (threadIdx.x == 0) s_next = 0;
+
+    const int total = hr_splat_list<MULTI>(a, fld, s_lbox, s_lpar, s_bits, s_cnt, s_gbeg);
+    const int ng = MULTI ? a.h.n_groups : 1;
+    Splat *glist = a.splats + fld * a.list_cap;
 #ifdef PP_STAMPS
     if (wave == 0) {
         HR_STAMP(1);
