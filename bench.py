@@ -9,9 +9,11 @@ gather of the packed annotation records and their copy to the host; for N > 1 al
 RCCL all-gather of every rank's records to rank 0 (weak scaling: each rank owns its own
 batch, no data-path collective).  Inputs are generated once and stay in HBM.
 
-Rank 0 prints ONE JSON line.  `roofline` is the CifHr stage (splat compaction + tile
-gather-fold kernels) measured with HIP events on the decode stream: algorithmic bytes =
-4*K*(5*H*W + H'*W') per image over the stage's event time.
+Rank 0 prints ONE JSON line.  `roofline` is the CifHr accumulation of the metric: the
+dense CifHr.accumulated map (pp_cifhr) of the same resident batch, timed with HIP events
+on the launch stream; algorithmic bytes = 4*K*(5*H*W + H'*W') per image
+over its launch time.  `roofline_decoder_cifhr` is the decoder's own block-sparse CifHr
+stage inside `value` (its bytes: bench.cifhr_stage_bytes).
 `cpu_baseline` is the oracle (oracle/pp_oracle.c, C restatement of the reference decoder)
 on one host core over a bounded sample of the same workload.
 """
@@ -164,6 +166,9 @@ def main():
     hh, ww = (h - 1) * 8 + 1, (w - 1) * 8 + 1
     cifhr_bytes, hr_tiles = cifhr_stage_bytes(cif_h, 8, cfg.cif_threshold)
     achieved = cifhr_bytes / (stage_avg[0] * 1e-3) / 1e9
+    dense_ms = dense_cifhr_ms(cif, cfg, stream, args.steps, args.warmup)
+    dense_bytes = 4 * k * (5 * h * w + hh * ww) * batch  # SURVEY.md §8d, per launch
+    dense_gbs = dense_bytes / (dense_ms * 1e-3) / 1e9
     line = {
         'metric': 'decoder images/sec + ms/image, 17-CIF/19-CAF @80x80; CifHr HBM GB/s vs '
                   'roofline',
@@ -189,18 +194,34 @@ def main():
         'stage_ms': {n: round(float(v), 4) for n, v in zip(names, stage_avg)},
         'annotations_per_image': round(n_anns / max(1, args.steps * batch * world), 3)
         if stages & STAGE_GROW else None,
+        # CifHr accumulation (the metric's "CifHr HBM GB/s"): CifHr.accumulated of the
+        # reference API, the dense (K, H', W') map, pp_cifhr = cifhr_splats_kernel +
+        # cifhr_tile_kernel, timed on its own over `steps` launches on the same batch
         'roofline': {
+            'bound': 'hbm', 'kernel': 'cifhr_splats_kernel + cifhr_tile_kernel (pp_cifhr)',
+            'achieved': round(dense_gbs, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
+            'frac': round(dense_gbs / PEAK_HBM_GBS, 4), 'traffic': None,
+            'algorithmic_bytes_per_launch': dense_bytes, 'ms_per_launch': round(dense_ms, 4),
+        },
+        # the decoder's own CifHr (inside `value`): the block-sparse map, written only where
+        # splat boxes land; latency-bound per field, far below the dense byte count
+        'roofline_decoder_cifhr': {
             'bound': 'hbm', 'kernel': 'cifhr_sparse_kernel',
             'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
             'frac': round(achieved / PEAK_HBM_GBS, 4),
             'algorithmic_bytes_per_launch': cifhr_bytes, 'traffic': None,
             'written_block_frac': round(hr_tiles, 6),
+            'us_per_image': round(1e3 * stage_avg[0] / batch, 4),
+            'dense_equivalent_gbs': round(dense_bytes / (stage_avg[0] * 1e-3) / 1e9, 1),
         },
     }
     default_run = (args.workload == 'cfg3' and args.generator == 'planted' and
                    args.mode == 'eval' and batch == WORKLOADS['cfg3']['batch'])
     if default_run:
-        line['roofline'].update(committed_traffic())
+        tr = committed_traffic()
+        for key in ('roofline', 'roofline_decoder_cifhr'):
+            if key in tr:
+                line[key].update(tr[key])
     if default_run and world == 1 and not args.no_uniform:
         # the same workload on the uniform generator (SURVEY.md §8d cfg3 names both):
         # dense random fields, ~400 annotations per image
@@ -289,21 +310,60 @@ def cifhr_stage_bytes(cif, stride, v_th, tile=64, block=8, lds_list=256):
     return nbytes, n_blocks / touched.size
 
 
+def dense_cifhr_ms(cif, cfg, stream, steps, warmup):
+    """Average ms of one pp_cifhr launch (the dense CifHr.accumulated map of the whole
+    resident batch) over `steps` back-to-back launches, HIP events on the launch stream."""
+    import ctypes
+    import torch
+    from openpifpaf_amd import _device
+    from openpifpaf_amd._lib import call, load
+    lib = load()
+    n, k, _, h, w = cif.shape
+    hh, ww = (h - 1) * cfg.stride + 1, (w - 1) * cfg.stride + 1
+    out = torch.empty((n, k, hh, int(lib.pp_cifhr_pitch(ww))), dtype=torch.float32,
+                      device=cif.device)
+    ws = torch.empty(int(lib.pp_cifhr_workspace_size(n, k, h, w)), dtype=torch.uint8,
+                     device=cif.device)
+
+    def launch():
+        call('pp_cifhr', _device.ptr(cif), n, k, h, w, ctypes.byref(cfg), _device.ptr(out),
+             _device.ptr(ws), ctypes.c_size_t(ws.numel()), _device.stream())
+
+    for _ in range(max(1, warmup)):
+        launch()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for _ in range(steps):
+        launch()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    del out, ws
+    return e0.elapsed_time(e1) / steps
+
+
+# roofline key -> the kernels whose PMC bytes it reports (tools/prof_summary.py)
+TRAFFIC_KERNELS = {'roofline': 'cifhr_splats_kernel+cifhr_tile_kernel',
+                   'roofline_decoder_cifhr': 'cifhr_sparse_kernel'}
+
+
 def committed_traffic():
-    """HBM bytes per CifHr launch from the newest committed PMC profile of this same
-    workload (profiles/<tag>_summary.json, written by tools/prof_summary.py from the
-    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of tools/gpu_profile.sh; counters cannot be
-    read from inside the timed process)."""
+    """HBM bytes per launch of the CifHr kernels from the newest committed PMC profile of
+    this same workload (profiles/<tag>_summary.json, written by tools/prof_summary.py from
+    the rocprofv3 FETCH_SIZE / WRITE_SIZE passes of tools/gpu_profile.sh; counters cannot
+    be read from inside the timed process).  {roofline key: {traffic, traffic_source}}."""
     import glob
     paths = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_summary.json')))
     if not paths:
         return {}
     with open(paths[-1]) as f:
         summ = json.load(f)
-    if summ.get('cifhr_kernels') != ['cifhr_sparse_kernel']:
-        return {}  # profiled before the current CifHr kernel
-    return {'traffic': summ['cifhr_traffic_bytes'],
-            'traffic_source': 'profiles/' + os.path.basename(paths[-1])}
+    out = {}
+    for key, kernels in TRAFFIC_KERNELS.items():
+        t = summ.get('traffic_bytes', {}).get(kernels)
+        if t is not None:
+            out[key] = {'traffic': t, 'traffic_source': 'profiles/' + os.path.basename(paths[-1])}
+    return out
 
 
 def cpu_baseline(cif, caf, skeleton, cfg, budget_s):

@@ -350,13 +350,9 @@ __device__ __forceinline__ ColQuery make_query(float x, float y, float xy_scale)
 // column k (all rows loaded in one round): caf_center_s test, score (cifcaf.py:134-139).
 // PACKED: the decoder's kColRows layout (index in row 6); else the reference's 9 rows
 // with the column's position k as its index.
-template <bool MAXM, bool PACKED>
-__device__ __forceinline__ void consider(const float *__restrict__ cf, int64_t hw, const ColQuery &q,
-                                         int k, Top2 &t, int &m) {
-    const float c1 = cf[hw + k], c2 = cf[2 * hw + k], c0 = cf[k];
-    const float tx = cf[(PACKED ? 3 : 5) * hw + k], ty = cf[(PACKED ? 4 : 6) * hw + k];
-    const float tc = cf[(PACKED ? 5 : 8) * hw + k];
-    const int o = PACKED ? __float_as_int(cf[6 * hw + k]) : k;
+template <bool MAXM>
+__device__ __forceinline__ void consider_vals(const ColQuery &q, float c0, float c1, float c2, float tx,
+                                              float ty, float tc, int o, Top2 &t, int &m) {
     if (c1 < q.lo_x || c1 > q.hi_x || c2 < q.lo_y || c2 > q.hi_y) return;
     const float dx = q.x - c1, dy = q.y - c2;
     const float dd = sqrtf(dx * dx + dy * dy);  // np.linalg.norm(axis=0)
@@ -364,6 +360,16 @@ __device__ __forceinline__ void consider(const float *__restrict__ cf, int64_t h
     const float score = (float)exp((double)qq) * c0;  // np.exp, correctly rounded
     m++;
     top2_insert(t, cand_key<MAXM>(score, o), tx, ty, tc);
+}
+
+template <bool MAXM, bool PACKED>
+__device__ __forceinline__ void consider(const float *__restrict__ cf, int64_t hw, const ColQuery &q,
+                                         int k, Top2 &t, int &m) {
+    const float c1 = cf[hw + k], c2 = cf[2 * hw + k], c0 = cf[k];
+    const float tx = cf[(PACKED ? 3 : 5) * hw + k], ty = cf[(PACKED ? 4 : 6) * hw + k];
+    const float tc = cf[(PACKED ? 5 : 8) * hw + k];
+    const int o = PACKED ? __float_as_int(cf[6 * hw + k]) : k;
+    consider_vals<MAXM>(q, c0, c1, c2, tx, ty, tc, o, t, m);
 }
 
 // a set-B column: concatenated cell index -> the head's raw CAF values (caf_scored.py:58-81
@@ -626,11 +632,15 @@ struct Frontier {
     float x[2], y[2], s[2], v[2];
     int added[2];      // in_frontier (cifcaf.py:249)
     int sj[2], sk[2], scaf[2], sfwd[2];  // slot constants
+    // connection_value of an unevaluated entry computed ahead of its pop (eval_ahead)
+    int pc[2];
+    float px[2], py[2], ps[2], pv[2];
 };
 
 struct Entry {
-    int slot, eval, j, k, caf, fwd;
+    int slot, eval, j, k, caf, fwd, pc;
     float neg, x, y, s, v;
+    float px, py, ps, pv;
 };
 
 // tuple order of (neg, None | (x, y, s, v), j, k); a None/tuple tie would raise TypeError
@@ -697,6 +707,11 @@ __device__ bool frontier_pop(Frontier &F, Entry &e) {
     e.k = rl_i(my_k, win);
     e.caf = rl_i(wr ? F.scaf[1] : F.scaf[0], win);
     e.fwd = rl_i(wr ? F.sfwd[1] : F.sfwd[0], win);
+    e.pc = rl_i(wr ? F.pc[1] : F.pc[0], win);
+    e.px = rl_f(wr ? F.px[1] : F.px[0], win);
+    e.py = rl_f(wr ? F.py[1] : F.py[0], win);
+    e.ps = rl_f(wr ? F.ps[1] : F.ps[0], win);
+    e.pv = rl_f(wr ? F.pv[1] : F.pv[0], win);
     if (lane == win) {
         if (wr)
             F.st[1] = 0;
@@ -708,7 +723,7 @@ __device__ bool frontier_pop(Frontier &F, Entry &e) {
 
 // add_to_frontier (cifcaf.py:251-263): the start joint's slots in dict order, one pass
 __device__ void add_to_frontier(const GrowArgs &g, GrowLDS &L, Frontier &F, float av, int start,
-                                float start_v, int &nfr) {
+                                float start_v, int &nfr, uint64_t added[2]) {
     const int lane = threadIdx.x & 63;
     const int lo = g.j_off[start], hi = g.j_off[start + 1];
     const float neg = -sqrtf(start_v);
@@ -729,11 +744,154 @@ __device__ void add_to_frontier(const GrowArgs &g, GrowLDS &L, Frontier &F, floa
             }
         }
         nfr += __popcll(m);
+        added[r] = m;
     }
 }
 
-// _grow (cifcaf.py:247-307) on the record in L.a (joint data mirrored into registers)
-__device__ void grow(const GrowArgs &g, GrowLDS &L, int img, int set, bool reverse_match) {
+// ---------------------------------------------------------------------------------------
+// connection_value ahead of the pop, several edges per memory round trip (seed loop)
+// ---------------------------------------------------------------------------------------
+// An unevaluated frontier entry (j, k) is evaluated when popped (cifcaf.py:275-279), but
+// its connection_value depends only on the CAF columns and on joint j, which never changes
+// once set.  So when joint j enters the frontier, the connections of all its new entries
+// are computed at once: up to kAhead edges, each direction's column rows of all of them
+// loaded in ONE round trip (flat scan of small set-A column sets, <= kFlatCols columns,
+// count from LDS), instead of two dependent round trips (bucket offsets, then columns) per
+// edge and direction.  The pop then takes the stored result; the frontier order, the
+// evaluation results and everything the reference observes are unchanged.  Edges whose
+// sets are larger stay lazy (grow_connection over the buckets).
+constexpr int kAhead = 2;
+constexpr int kFlatPer = 2;
+constexpr int kFlatCols = 64 * kFlatPer;
+
+__device__ __forceinline__ void flat_load(const float *__restrict__ cf, int64_t hw, int n,
+                                          float v[kFlatPer][kColRows]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int p = 0; p < kFlatPer; p++) {
+        const int k = p * 64 + lane;
+#pragma unroll
+        for (int r = 0; r < kColRows; r++) v[p][r] = (k < n) ? cf[r * hw + k] : 0.0f;
+    }
+}
+
+// grow_connection over every column of a flat-loaded set (same columns pass caf_center_s
+// as through the buckets; the merge is independent of visiting order: unique keys)
+template <bool MAXM>
+__device__ __forceinline__ void flat_query(const float v[kFlatPer][kColRows], int n, float x, float y,
+                                           float xy_scale, float out[4]) {
+    const int lane = threadIdx.x & 63;
+    const ColQuery q = make_query(x, y, xy_scale);
+    Top2 t = top2_empty();
+    int m = 0;
+#pragma unroll
+    for (int p = 0; p < kFlatPer; p++)
+        if (p * 64 + lane < n)
+            consider_vals<MAXM>(q, v[p][0], v[p][1], v[p][2], v[p][3], v[p][4], v[p][5],
+                                __float_as_int(v[p][6]), t, m);
+    finish_connection<MAXM>(t, m, out);
+}
+
+// the new entries `added` (slot masks, add_to_frontier) of a start joint: connection_value
+// with reverse_match (cifcaf.py:194-217) for those whose two column sets are small
+template <bool MAXM>
+__device__ void eval_ahead(const GrowArgs &g, Frontier &F, int img, const int *ncol, uint64_t r0,
+                           uint64_t r1, float ax, float ay, float av, float as) {
+    const int lane = threadIdx.x & 63;
+    const int64_t hw = g.col_cap;
+    while (r0 | r1) {
+        int sl[kAhead];
+#pragma unroll
+        for (int b = 0; b < kAhead; b++) {  // the next kAhead slots with small sets
+            sl[b] = -1;
+            while (r0 | r1) {
+                const int d = r0 ? __ffsll((unsigned long long)r0) - 1
+                                 : 64 + __ffsll((unsigned long long)r1) - 1;
+                if (r0)
+                    r0 &= r0 - 1;
+                else
+                    r1 &= r1 - 1;
+                const int caf = g.d_caf[d], df = g.d_fwd[d] ? 1 : 0;
+                if (ncol[caf * 2 + df] <= kFlatCols && ncol[caf * 2 + 1 - df] <= kFlatCols) {
+                    sl[b] = d;
+                    break;
+                }
+            }
+        }
+        if (sl[0] < 0) break;
+        float v[kAhead][kFlatPer][kColRows];
+        float nx[kAhead][4], jx[kAhead], jy[kAhead], jv[kAhead], js[kAhead];
+        // forward queries: all columns of every edge in one round trip
+#pragma unroll
+        for (int b = 0; b < kAhead; b++) {
+            if (sl[b] < 0) continue;
+            const int d = sl[b], caf = g.d_caf[d], df = g.d_fwd[d] ? 1 : 0;
+            flat_load(col_set(g, 0, img, caf, df), hw, ncol[caf * 2 + df], v[b]);
+        }
+#pragma unroll
+        for (int b = 0; b < kAhead; b++) {
+            if (sl[b] < 0) continue;
+            const int d = sl[b], j = g.d_j[d], caf = g.d_caf[d], df = g.d_fwd[d] ? 1 : 0;
+            jx[b] = rl_f(ax, j);
+            jy[b] = rl_f(ay, j);
+            jv[b] = rl_f(av, j);
+            js[b] = rl_f(as, j);
+            flat_query<MAXM>(v[b], ncol[caf * 2 + df], jx[b], jy[b], max0(js[b]), nx[b]);
+        }
+        // reverse queries from the new points (cifcaf.py:210-214), again one round trip
+        bool ok[kAhead];
+#pragma unroll
+        for (int b = 0; b < kAhead; b++) {
+            ok[b] = false;
+            if (sl[b] < 0) continue;
+            const float ks = sqrtf(nx[b][3] * jv[b]);
+            ok[b] = !(ks < g.cfg.keypoint_threshold) && nx[b][3] != 0.0f;
+            if (!ok[b]) continue;
+            const int d = sl[b], caf = g.d_caf[d], db = g.d_fwd[d] ? 0 : 1;
+            flat_load(col_set(g, 0, img, caf, db), hw, ncol[caf * 2 + db], v[b]);
+        }
+#pragma unroll
+        for (int b = 0; b < kAhead; b++) {
+            if (sl[b] < 0) continue;
+            float res[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (ok[b]) {
+                const int d = sl[b], caf = g.d_caf[d], db = g.d_fwd[d] ? 0 : 1;
+                float rv[4];
+                flat_query<MAXM>(v[b], ncol[caf * 2 + db], nx[b][0], nx[b][1], max0(nx[b][2]), rv);
+                const float xy_scale_s = max0(js[b]);
+                if (rv[2] != 0.0f && !(fabsf(jx[b] - rv[0]) + fabsf(jy[b] - rv[1]) > xy_scale_s)) {
+                    res[0] = nx[b][0];
+                    res[1] = nx[b][1];
+                    res[2] = nx[b][2];
+                    res[3] = sqrtf(nx[b][3] * jv[b]);
+                }
+            }
+            const int d = sl[b];
+            if (lane == (d & 63)) {
+                if (d < 64) {
+                    F.pc[0] = 1;
+                    F.px[0] = res[0];
+                    F.py[0] = res[1];
+                    F.ps[0] = res[2];
+                    F.pv[0] = res[3];
+                } else {
+                    F.pc[1] = 1;
+                    F.px[1] = res[0];
+                    F.py[1] = res[1];
+                    F.ps[1] = res[2];
+                    F.pv[1] = res[3];
+                }
+            }
+        }
+    }
+}
+
+// _grow (cifcaf.py:247-307) on the record in L.a (joint data mirrored into registers).
+// AHEAD (seed loop: set A, reverse_match): new entries' connections via eval_ahead, with
+// ncol = the image's set-A column counts per (CAF, direction).
+template <bool AHEAD>
+__device__ void grow(const GrowArgs &g, GrowLDS &L, int img, int set, bool reverse_match,
+                     const int *ncol = nullptr) {
     const int lane = threadIdx.x & 63;
     const int K = g.K;
     float ax = 0.0f, ay = 0.0f, av = 0.0f, as = 0.0f;
@@ -757,11 +915,25 @@ __device__ void grow(const GrowArgs &g, GrowLDS &L, int img, int set, bool rever
         F.sk[r] = ok ? g.d_k[d] : 0;
         F.scaf[r] = ok ? g.d_caf[d] : 0;
         F.sfwd[r] = ok ? g.d_fwd[d] : 0;
+        F.pc[r] = 0;
+        F.px[r] = F.py[r] = F.ps[r] = F.pv[r] = 0.0f;
     }
+    const bool maxm = g.cfg.connection_method == 1;
+    auto ahead = [&](const uint64_t added[2]) {
+        if (!AHEAD || !(added[0] | added[1])) return;
+        FSTAMP_BEGIN
+        if (maxm)
+            eval_ahead<true>(g, F, img, ncol, added[0], added[1], ax, ay, av, as);
+        else
+            eval_ahead<false>(g, F, img, ncol, added[0], added[1], ax, ay, av, as);
+        FSTAMP_END(L, 1)
+    };
     for (int j = 0; j < K; j++) {  // seeding the frontier (cifcaf.py:288-291)
         const float vj = rl_f(av, j);
         if (vj == 0.0f) continue;
-        add_to_frontier(g, L, F, av, j, vj, nfr);
+        uint64_t added[2];
+        add_to_frontier(g, L, F, av, j, vj, nfr, added);
+        ahead(added);
     }
     for (;;) {
         // frontier_get (cifcaf.py:265-285)
@@ -783,7 +955,12 @@ __device__ void grow(const GrowArgs &g, GrowLDS &L, int img, int set, bool rever
             }
             if (rl_f(av, e.k) > 0.0f) continue;
             float nx[4];
-            {
+            if (AHEAD && e.pc) {  // computed by eval_ahead when joint e.j entered
+                nx[0] = e.px;
+                nx[1] = e.py;
+                nx[2] = e.ps;
+                nx[3] = e.pv;
+            } else {
 #ifdef PP_STAMPS
                 if (lane == 0) L.fst[3] += 1;
 #endif
@@ -842,11 +1019,13 @@ __device__ void grow(const GrowArgs &g, GrowLDS &L, int img, int set, bool rever
             }
         }
         ndec++;
+        uint64_t added[2];
         {
             FSTAMP_BEGIN
-            add_to_frontier(g, L, F, av, jti, got.v, nfr);
+            add_to_frontier(g, L, F, av, jti, got.v, nfr, added);
             FSTAMP_END(L, 2)
         }
+        ahead(added);
     }
     if (nfr > PP_MAX_FRONTIER && lane == 0) L.status |= PP_ST_DEC_OVERFLOW;
     if (lane < K) {
@@ -1186,10 +1365,12 @@ __device__ void ann_from_seed(GrowLDS &L, const pp_seed &sd, int K, int img) {
 __global__ __launch_bounds__(64 * kSeedWaves) void seed_loop_kernel(GrowArgs g) {
     __shared__ GrowLDS Ls[kSeedWaves];
     __shared__ SeedLoopShared S;
+    __shared__ int s_ncol[2 * PP_MAX_EDGES];  // set-A column counts per (CAF, direction)
     const int img = blockIdx.x;
     const int K = g.K;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     GrowLDS &L = Ls[wave];
+    for (int q = threadIdx.x; q < 2 * g.C; q += blockDim.x) s_ncol[q] = col_offs(g, 0, img, q >> 1, q & 1)[g.nb];
     if (lane == 0) {
         L.status = 0;
         L.log_n = 0;
@@ -1347,7 +1528,7 @@ __global__ __launch_bounds__(64 * kSeedWaves) void seed_loop_kernel(GrowArgs g) 
         const int my = S.task[wave];
         if (my >= 0) {
             ann_from_seed(L, seeds[my], K, img);
-            grow(g, L, img, 0, true);
+            grow<true>(g, L, img, 0, true, s_ncol);
             if (wave > 0) {
                 const int q = S.task_slot[wave];
                 copy_ann(&cache[q], &L.a);
@@ -1421,7 +1602,7 @@ __global__ __launch_bounds__(64) void complete_kernel(GrowArgs g) {
         copy_ann(&L.a, &work[i]);
         uint32_t unfilled = 0;
         for (int j = 0; j < K; j++) unfilled |= (L.a.data[j][2] == 0.0f) ? (1u << j) : 0u;
-        grow(g, L, img, 1, false);
+        grow<false>(g, L, img, 1, false);
         bool any0 = false;
         for (int j = 0; j < K; j++) {
             float &v = L.a.data[j][2];

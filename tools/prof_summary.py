@@ -5,8 +5,8 @@
 Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, verbatim),
 profiles/<tag>_counters.csv (per kernel: launches, mean FETCH_SIZE / WRITE_SIZE bytes per
 launch from the PMC passes), profiles/<tag>_calibration.csv (counter bytes / true bytes for
-the calibration kernels) and profiles/<tag>_summary.json (CifHr stage duration and HBM
-traffic per launch, as bench.py's roofline reports them).
+the calibration kernels) and profiles/<tag>_summary.json (per CifHr kernel set: duration
+and corrected HBM traffic per launch, as bench.py's roofline objects report them).
 """
 import csv
 import json
@@ -16,7 +16,8 @@ import sys
 from collections import defaultdict
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CIFHR_KERNELS = ('cifhr_sparse_kernel',)
+# kernel sets whose HBM bytes per launch the bench's roofline objects report
+KERNEL_SETS = (('cifhr_splats_kernel', 'cifhr_tile_kernel'), ('cifhr_sparse_kernel',))
 CALIB_BYTES = 1 << 30
 
 
@@ -74,31 +75,35 @@ def main():
             calib[k] = mean / CALIB_BYTES
             w.writerow([k, CALIB_BYTES, cname, round(mean), round(calib[k], 4)])
 
-    # CifHr stage: one launch of each kernel per decode
-    dur = sum(stats[k][1] for k in CIFHR_KERNELS)
-    f_raw = sum(sum(fetch[k]) / len(fetch[k]) for k in CIFHR_KERNELS)
-    w_raw = sum(sum(write[k]) / len(write[k]) for k in CIFHR_KERNELS)
+    # per-kernel correction by the calibrated ratio of the access width each one streams
+    # with (tools/calib_counters.hip): 4 B field reads, 16 B nontemporal dense-map stores,
+    # 4 B block stores of the sparse map
+    read_width = {'cifhr_splats_kernel': 'read4', 'cifhr_tile_kernel': 'read16',
+                  'cifhr_sparse_kernel': 'read4'}
+    write_width = {'cifhr_splats_kernel': 'write16', 'cifhr_tile_kernel': 'write16',
+                   'cifhr_sparse_kernel': 'write4'}
     summary = {
         'tag': tag,
-        'cifhr_kernels': list(CIFHR_KERNELS),
-        'cifhr_avg_ns': round(dur, 1),
-        'cifhr_fetch_bytes_raw': round(f_raw),
-        'cifhr_write_bytes_raw': round(w_raw),
-        # counter bytes / true bytes of the calibration kernels (tools/calib_counters.hip)
         'fetch_ratio_16B': round(calib.get('read16', 0.0), 4),
         'fetch_ratio_4B': round(calib.get('read4', 0.0), 4),
         'write_ratio_16B': round(calib.get('write16', 0.0), 4),
+        'write_ratio_4B': round(calib.get('write4', 0.0), 4),
+        'avg_ns': {}, 'fetch_bytes_raw': {}, 'write_bytes_raw': {}, 'traffic_bytes': {},
     }
-    # per-kernel correction by the calibrated ratio of the access width each one streams
-    # with: cifhr_sparse_kernel reads the fields and stores the 8x8 blocks 4 B per lane
-    read_width = {'cifhr_sparse_kernel': 'read4'}
-    write_width = {'cifhr_sparse_kernel': 'write4'}
-    summary['write_ratio_4B'] = round(calib.get('write4', 0.0), 4)
-    traffic = 0.0
-    for k in CIFHR_KERNELS:
-        traffic += (sum(fetch[k]) / len(fetch[k])) / (calib.get(read_width[k]) or 1.0)
-        traffic += (sum(write[k]) / len(write[k])) / (calib.get(write_width[k]) or 1.0)
-    summary['cifhr_traffic_bytes'] = round(traffic)
+    for ks in KERNEL_SETS:
+        if not all(k in fetch and k in write and k in stats for k in ks):
+            continue
+        name = '+'.join(ks)
+        f_raw = sum(sum(fetch[k]) / len(fetch[k]) for k in ks)
+        w_raw = sum(sum(write[k]) / len(write[k]) for k in ks)
+        traffic = 0.0
+        for k in ks:
+            traffic += (sum(fetch[k]) / len(fetch[k])) / (calib.get(read_width[k]) or 1.0)
+            traffic += (sum(write[k]) / len(write[k])) / (calib.get(write_width[k]) or 1.0)
+        summary['avg_ns'][name] = round(sum(stats[k][1] for k in ks), 1)
+        summary['fetch_bytes_raw'][name] = round(f_raw)
+        summary['write_bytes_raw'][name] = round(w_raw)
+        summary['traffic_bytes'][name] = round(traffic)
     with open(os.path.join(dst, tag + '_summary.json'), 'w') as f:
         json.dump(summary, f, indent=1)
     print(json.dumps(summary, indent=1))
