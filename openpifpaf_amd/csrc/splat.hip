@@ -329,11 +329,12 @@ __global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
 }
 
 // -------------------------------------------------------------------------------------
-// K2 for CifHr: one workgroup per (field, chunk of 32 tiles = one tile-bitmap word)
+// K2 for CifHr: one workgroup per (field, chunk of kChunkTiles tiles within one bitmap word)
 // -------------------------------------------------------------------------------------
-// The chunk's bitmap words say which tiles any splat box touches.  Untouched tiles cost a
-// zero-fill; the field's splat lists are
-// loaded into LDS once when they fit (kCand entries over all groups), and each touched
+// The field's tile bitmap says which tiles any splat box touches.  Untouched tiles cost a
+// zero-fill (one tile per workgroup streams best: many short workgroups keep every CU's
+// store queue full, and a touched tile's fold delays no zero-fill); the field's splat lists
+// are loaded into LDS once when they fit (kHrCand entries over all groups), and each touched
 // tile selects its candidates from LDS by ballot compaction, keeping splat order.  Bigger
 // lists gather per tile from global memory in kCand chunks.
 //
@@ -341,7 +342,7 @@ __global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
 // tile and the groups combine by np.maximum(ta, accumulated), all in registers.  A group
 // with no splat on the tile contributes max(0, acc) = acc (every fold value is >= 0 and
 // the clamp maps NaN to max_value), so it is skipped.
-constexpr int kChunkTiles = 32;
+constexpr int kChunkTiles = 1;  // tiles per workgroup: 1.209 ms vs 1.409 ms at 32 (cfg3)
 constexpr int kHrCand = 256;  // LDS list / candidate capacity (>= 256 for progress)
 constexpr int kHrPad = 68;    // accumulator row pitch: ~26 KB of LDS per workgroup
 
@@ -354,6 +355,7 @@ struct HrTileArgs {
     int64_t field_stride;
     int h, w, pitch;
     int tiles_x, tiles, chunks;  // chunks per field
+    int chunk_tiles;        // tiles per chunk: a power of two <= 32 (chunks never straddle a bitmap word)
     int64_t n_work;         // n_fields * chunks
     int n_groups;
     int64_t goff[kMaxHeads];
@@ -372,7 +374,7 @@ __global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
     if (wid >= a.n_work) return;
     const int chunk = (int)(wid % a.chunks);
     const int64_t fld = wid / a.chunks;
-    const int t0 = chunk * kChunkTiles, t1 = min(a.tiles, t0 + kChunkTiles);
+    const int t0 = chunk * a.chunk_tiles, t1 = min(a.tiles, t0 + a.chunk_tiles);
     const int ng = MULTI ? a.n_groups : 1;
 
     // touched tiles of the chunk (over all groups) and the lists' sizes (scalar loads)
@@ -386,7 +388,7 @@ __global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
             s_loff[g] = total;
         }
         total += ns;
-        if (ns > 0) live |= a.tile_bits[lst * (kTileBits / 32) + chunk];
+        if (ns > 0) live |= a.tile_bits[lst * (kTileBits / 32) + (t0 >> 5)] >> (t0 & 31);
     }
     live &= (t1 - t0 == 32) ? ~0u : ((1u << (t1 - t0)) - 1u);
     float *out = a.field + fld * a.field_stride;
@@ -440,7 +442,7 @@ __global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
             const int64_t lst = fld * ng + g;
             const int64_t ns = s_ns[g];
             const int loff = s_loff[g];
-            if (ns == 0 || !((a.tile_bits[lst * (kTileBits / 32) + chunk] >> (tile - t0)) & 1u)) continue;
+            if (ns == 0 || !((a.tile_bits[lst * (kTileBits / 32) + (tile >> 5)] >> (tile & 31)) & 1u)) continue;
             // zero the stripe accumulator (wave-private rows)
 #pragma unroll
             for (int r = 0; r < 16; r++) s_acc[(r >> 3) * 8 * kHrPad + ly * kHrPad + (r & 7) * 8 + lx] = 0.0f;
@@ -1002,7 +1004,8 @@ int cifhr_heads_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config
     a.pitch = (int)pitch;
     a.tiles_x = sa.tiles_x;
     a.tiles = sa.tiles;
-    a.chunks = (sa.tiles + kChunkTiles - 1) / kChunkTiles;
+    a.chunk_tiles = kChunkTiles;
+    a.chunks = (sa.tiles + a.chunk_tiles - 1) / a.chunk_tiles;
     a.field_stride = (int64_t)hh * pitch;
     a.n_work = nf * a.chunks;
     a.n_groups = h.n_groups;
