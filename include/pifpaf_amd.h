@@ -360,6 +360,20 @@ int pp_nms_keypoints(pp_ann *d_anns, const int32_t *d_counts, int32_t n_img, int
                      size_t workspace_bytes, void *stream);
 
 /*
+ * Packs a decode's records (d_anns (n_img, ann_capacity), d_counts[i] valid in slot row i)
+ * image after image into `out` and copies the counts to out_counts: the flattened
+ * per-image Annotation lists that Generator.batch returns (generator.py:96-97), in one
+ * launch.  `out` / `out_counts` may be device memory or pinned host memory
+ * (hipHostMalloc / hipHostRegister; written zero-copy through its mapped device address,
+ * so one stream synchronisation hands the caller every record).  Records whose packed
+ * index is >= out_capacity are not written; out_counts is always complete, so the caller
+ * can size a retry.
+ */
+int pp_pack_records(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img,
+                    int32_t ann_capacity, pp_ann *out, int64_t out_capacity, int32_t *out_counts,
+                    void *stream);
+
+/*
  * The same decode split into stages for measurement: bit 1 CifHr, 2 CifSeeds,
  * 4 CafScored at caf_threshold, 8 seed loop + grow + complete + NMS (stage 8 also builds
  * the complete_caf_threshold column sets, only where force-complete needs them).  Stage buffers live

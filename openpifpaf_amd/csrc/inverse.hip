@@ -119,6 +119,37 @@ __global__ __launch_bounds__(256) void det_inverse_kernel(pp_det *dets, const in
     for (int i = 0; i < 4; i++) d.bbox[i] = b[i];
 }
 
+// -------------------------------------------------------------------------------------
+// record packing: the per-image record slots of a decode, image after image, into one
+// caller buffer (Generator.batch's list of per-image Annotation lists, generator.py:96-97,
+// flattened); the destination may be mapped pinned host memory (zero-copy)
+// -------------------------------------------------------------------------------------
+// One workgroup per image: the image's offset is the sum of the earlier counts (read by
+// the whole workgroup, n is small), then its records are copied as 8-byte words (a record
+// is 1544 = 8 * 193 bytes).  Records at packed index >= out_cap are not written.
+__global__ __launch_bounds__(256) void pack_records_kernel(const pp_ann *__restrict__ anns,
+                                                           const int *__restrict__ counts, int n,
+                                                           int cap, pp_ann *out, int64_t out_cap,
+                                                           int *out_counts) {
+    __shared__ int s_off;
+    const int img = blockIdx.x;
+    if (threadIdx.x == 0) s_off = 0;
+    __syncthreads();
+    int part = 0;
+    for (int j = threadIdx.x; j < img; j += 256) part += counts[j];
+    if (part) atomicAdd(&s_off, part);
+    __syncthreads();
+    const int64_t off = s_off;
+    const int cnt = counts[img];
+    if (threadIdx.x == 0) out_counts[img] = cnt;
+    const int64_t fit = min((int64_t)cnt, max((int64_t)0, out_cap - off));
+    constexpr int kWords = sizeof(pp_ann) / 8;
+    static_assert(sizeof(pp_ann) % 8 == 0, "pp_ann is copied in 8-byte words");
+    const uint64_t *src = reinterpret_cast<const uint64_t *>(anns + (int64_t)img * cap);
+    uint64_t *dst = reinterpret_cast<uint64_t *>(out + off);
+    for (int64_t i = threadIdx.x; i < fit * kWords; i += 256) dst[i] = src[i];
+}
+
 }  // namespace pp
 
 using namespace pp;
@@ -148,6 +179,33 @@ int pp_dets_inverse(pp_det *d_dets, const int32_t *d_counts, int32_t n_img, int3
     hipLaunchKernelGGL(det_inverse_kernel, grid, dim3(256), 0, (hipStream_t)stream, d_dets,
                        d_counts, capacity, d_metas);
     return check_launch("pp_dets_inverse");
+}
+
+int pp_pack_records(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img,
+                    int32_t ann_capacity, pp_ann *out, int64_t out_capacity, int32_t *out_counts,
+                    void *stream) {
+    if (!d_anns || !d_counts || !out || !out_counts)
+        return fail(PP_EINVAL, "pp_pack_records: NULL argument");
+    if (n_img < 0 || ann_capacity <= 0 || out_capacity < 0)
+        return fail(PP_ESHAPE, "pp_pack_records: bad shape");
+    if (n_img == 0) return PP_OK;
+    // destinations as the device sees them: device memory as is, pinned host memory
+    // (hipHostMalloc / registered) through its mapped device address
+    void *dst[2] = {out, out_counts};
+    for (void *&d : dst) {
+        hipPointerAttribute_t at;
+        if (hipPointerGetAttributes(&at, d) != hipSuccess || !at.devicePointer ||
+            (at.type != hipMemoryTypeDevice && at.type != hipMemoryTypeHost)) {
+            (void)hipGetLastError();
+            return fail(PP_EINVAL, "pp_pack_records: destination is neither device memory nor "
+                                   "pinned host memory");
+        }
+        d = at.devicePointer;
+    }
+    hipLaunchKernelGGL(pack_records_kernel, dim3((unsigned)n_img), dim3(256), 0,
+                       (hipStream_t)stream, d_anns, d_counts, n_img, ann_capacity,
+                       (pp_ann *)dst[0], out_capacity, (int *)dst[1]);
+    return check_launch("pp_pack_records");
 }
 
 }  // extern "C"

@@ -377,19 +377,11 @@ __global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
     const int t0 = chunk * a.chunk_tiles, t1 = min(a.tiles, t0 + a.chunk_tiles);
     const int ng = MULTI ? a.n_groups : 1;
 
-    // touched tiles of the chunk (over all groups) and the lists' sizes (scalar loads)
+    // touched tiles of the chunk over all groups: one round trip of scalar loads (a list's
+    // bitmap is all zero when the list is empty), the lists' sizes only if a tile is touched
     uint32_t live = 0;
-    int total = 0;
-    for (int g = 0; g < ng; g++) {
-        const int64_t lst = fld * ng + g;
-        const int ns = a.counts[lst];
-        if (threadIdx.x == 0) {
-            s_ns[g] = ns;
-            s_loff[g] = total;
-        }
-        total += ns;
-        if (ns > 0) live |= a.tile_bits[lst * (kTileBits / 32) + (t0 >> 5)] >> (t0 & 31);
-    }
+    for (int g = 0; g < ng; g++)
+        live |= a.tile_bits[(fld * ng + g) * (kTileBits / 32) + (t0 >> 5)] >> (t0 & 31);
     live &= (t1 - t0 == 32) ? ~0u : ((1u << (t1 - t0)) - 1u);
     float *out = a.field + fld * a.field_stride;
     typedef float v4f __attribute__((ext_vector_type(4)));
@@ -409,6 +401,15 @@ __global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
     }
     if (!live) return;
 
+    int total = 0;
+    for (int g = 0; g < ng; g++) {
+        const int ns = a.counts[fld * ng + g];
+        if (threadIdx.x == 0) {
+            s_ns[g] = ns;
+            s_loff[g] = total;
+        }
+        total += ns;
+    }
     // the field's lists in LDS when they fit (one round trip for the whole chunk)
     const bool pre = total <= kHrCand;
     __syncthreads();  // s_ns / s_loff

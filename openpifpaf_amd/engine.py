@@ -176,6 +176,31 @@ class DecodeEngine:
 
     @staticmethod
     def fetch(b):
+        """Packed records of all images and per-image offsets, after one stream
+        synchronisation: pp_pack_records writes the counts and the records, image after
+        image, straight into a pinned host block (zero-copy).  The block is sized from the
+        largest batch seen so far; a batch that outgrows it is fetched again by
+        `fetch_gather` (and the next block is larger)."""
+        n, width = b.n, ANN_DTYPE.itemsize
+        est = max(getattr(b, 'pack_cap', 0), 16 * n)
+        head = -(-4 * n // 256) * 256
+        # pinned block from torch's caching host allocator: the returned array owns it
+        # (released to the cache when the caller drops the records)
+        host = torch.empty(head + est * width, dtype=torch.uint8, pin_memory=True)
+        call('pp_pack_records', _device.ptr(b.anns), _device.ptr(b.counts), n, b.cap,
+             ctypes.c_void_p(host.data_ptr() + head), est, ctypes.c_void_p(host.data_ptr()),
+             _device.stream())
+        torch.cuda.current_stream(b.anns.device).synchronize()
+        counts = host[:4 * n].numpy().view(np.int32).astype(np.int64)
+        offsets = np.concatenate([[0], np.cumsum(counts)])
+        total = int(offsets[-1])
+        if total > est:
+            b.pack_cap = 2 * total
+            return DecodeEngine.fetch_gather(b)
+        return host[head:head + total * width].numpy().view(ANN_DTYPE), offsets
+
+    @staticmethod
+    def fetch_gather(b):
         """Packed records of all images (one gather + one D2H copy) and per-image offsets."""
         counts = b.counts.cpu().numpy().astype(np.int64)
         offsets = np.concatenate([[0], np.cumsum(counts)])

@@ -714,3 +714,41 @@ def test_multi_stage_calls_equal_full_decode(dec):
     got, off = eng.fetch(b)
     assert np.array_equal(off, ref_off)
     assert got.tobytes() == ref.tobytes()
+
+
+def test_pack_records_zero_copy():
+    """pp_pack_records (engine.fetch, one synchronisation, pinned host destination) returns
+    exactly the records and offsets of the gather path; a too-small destination gets only
+    its first records but every count; the overflow fallback and a pageable (unpinned)
+    host destination, which the library must refuse."""
+    import ctypes
+    import torch
+    from openpifpaf_amd import _device, constants, engine, synthetic
+    from openpifpaf_amd._abi import ANN_DTYPE, EVAL_CONFIG, make_config
+    from openpifpaf_amd._lib import PPError, call
+    cfg = make_config(**EVAL_CONFIG)
+    sk = constants.COCO_PERSON_SKELETON
+    eng = engine.DecodeEngine()
+    for kind, n in (('planted', 24), ('uniform', 3)):
+        cif, caf = synthetic.batch(kind, n, 48, 48, first_seed=31)
+        b = eng.launch(torch.from_numpy(cif).cuda(), torch.from_numpy(caf).cuda(), sk, cfg)
+        ref, ref_off = eng.fetch_gather(b)
+        ref = ref.copy()
+        got, off = eng.fetch(b)  # uniform: > 16 records per image -> the gather fallback
+        assert np.array_equal(off, ref_off) and got.tobytes() == ref.tobytes(), kind
+        got, off = eng.fetch(b)  # the grown block: zero-copy again
+        assert getattr(b, 'pack_cap', 0) == 0 or b.pack_cap >= len(ref)
+        assert np.array_equal(off, ref_off) and got.tobytes() == ref.tobytes(), kind
+    # device destination smaller than the batch: first records, complete counts
+    cut = max(1, len(ref) // 3)
+    out = torch.zeros(cut * ANN_DTYPE.itemsize, dtype=torch.uint8, device='cuda')
+    cnt = torch.full((b.n,), -1, dtype=torch.int32, device='cuda')
+    call('pp_pack_records', _device.ptr(b.anns), _device.ptr(b.counts), b.n, b.cap,
+         _device.ptr(out), cut, _device.ptr(cnt), _device.stream())
+    torch.cuda.synchronize()
+    assert np.array_equal(np.diff(ref_off), cnt.cpu().numpy())
+    assert out.cpu().numpy().tobytes() == ref[:cut].tobytes()
+    pageable = np.zeros(cut * ANN_DTYPE.itemsize, np.uint8)
+    with pytest.raises(PPError):
+        call('pp_pack_records', _device.ptr(b.anns), _device.ptr(b.counts), b.n, b.cap,
+             ctypes.c_void_p(pageable.ctypes.data), cut, _device.ptr(cnt), _device.stream())
