@@ -147,7 +147,22 @@ __global__ __launch_bounds__(256) void pack_records_kernel(const pp_ann *__restr
     static_assert(sizeof(pp_ann) % 8 == 0, "pp_ann is copied in 8-byte words");
     const uint64_t *src = reinterpret_cast<const uint64_t *>(anns + (int64_t)img * cap);
     uint64_t *dst = reinterpret_cast<uint64_t *>(out + off);
-    for (int64_t i = threadIdx.x; i < fit * kWords; i += 256) dst[i] = src[i];
+    // 16-byte stores (the destination is usually across PCIe, where wide writes pay):
+    // one leading 8-byte word when the destination is 8 mod 16, then word pairs, each
+    // assembled from two 8-byte loads, then a trailing word
+    const int64_t words = fit * kWords;
+    const int64_t lead = (reinterpret_cast<uintptr_t>(dst) & 8) ? min(words, (int64_t)1) : 0;
+    const int64_t pairs = (words - lead) >> 1;
+    if (threadIdx.x == 0 && lead) dst[0] = src[0];
+    typedef uint64_t v2u __attribute__((ext_vector_type(2)));
+    v2u *dst2 = reinterpret_cast<v2u *>(dst + lead);
+    for (int64_t i = threadIdx.x; i < pairs; i += 256) {
+        v2u v;
+        v.x = src[lead + 2 * i];
+        v.y = src[lead + 2 * i + 1];
+        dst2[i] = v;
+    }
+    if (threadIdx.x == 0 && lead + 2 * pairs < words) dst[words - 1] = src[words - 1];
 }
 
 }  // namespace pp

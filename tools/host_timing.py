@@ -28,32 +28,32 @@ for _ in range(3):
     eng.fetch(b)
 torch.cuda.synchronize()
 
-acc = np.zeros(7)
+acc = np.zeros(5)
 reps = 20
+ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+pack_ms = 0.0
 for _ in range(reps):
     t0 = time.perf_counter()
+    ev[0].record()
     b = eng.launch(c, f, sk, cfg)
+    ev[1].record()
     t1 = time.perf_counter()
     torch.cuda.synchronize()
     t2 = time.perf_counter()
-    counts = b.counts.cpu().numpy().astype(np.int64)
+    recs, offs = eng.fetch(b)  # pp_pack_records into pinned memory + one sync
+    ev[2].record()
     t3 = time.perf_counter()
-    offs = np.concatenate([[0], np.cumsum(counts)])
-    idx = np.arange(offs[-1], dtype=np.int64) + np.repeat(
-        np.arange(len(counts), dtype=np.int64) * b.cap - offs[:-1], counts)
-    rows = b.anns.view(b.n * b.cap, ANN_DTYPE.itemsize)
-    sel = rows.index_select(0, torch.from_numpy(idx).to(rows.device))
+    torch.cuda.synchronize()
+    pack_ms += ev[1].elapsed_time(ev[2])
     t4 = time.perf_counter()
-    host = torch.empty(sel.shape, dtype=torch.uint8, pin_memory=True)
-    t5 = time.perf_counter()
-    host.copy_(sel, non_blocking=True)
-    torch.cuda.current_stream().synchronize()
+    recs = None
+    b = eng.launch(c, f, sk, cfg)
+    t5 = time.perf_counter()  # one full bench-like step: launch .. fetch
+    eng.fetch(b)
     t6 = time.perf_counter()
-    _ = host.numpy().reshape(-1).view(ANN_DTYPE)
-    t7 = time.perf_counter()
-    acc += np.diff([t0, t1, t2, t3, t4, t5, t6, t7])
-names = ['launch (host)', 'device wait', 'counts D2H', 'idx + index_select', 'pinned alloc',
-         'records D2H', 'view']
+    acc += np.array([t1 - t0, t2 - t1, t3 - t2, t5 - t4, (t6 - t4)])
+names = ['launch (host)', 'device wait', 'fetch (pack + sync)', 'launch again', 'step']
 for n_, v in zip(names, acc / reps * 1e3):
     print('{:22s} {:8.3f} ms'.format(n_, v))
-print('records per step', int(counts.sum()), 'bytes', int(counts.sum()) * ANN_DTYPE.itemsize)
+print('pack kernel (events)   {:8.3f} ms'.format(pack_ms / reps))
+print('records per step', len(offs) and int(offs[-1]), 'bytes', int(offs[-1]) * ANN_DTYPE.itemsize)
