@@ -849,8 +849,11 @@ __global__ __launch_bounds__(256) void cifhr_sparse_kernel(HrSparseArgs a) {
             if (lane + 64 < n) cm1 = block_rect_mask(cbox[lane + 64], tx0, ty0);
             if (cm0 | cm1) atomicOr((unsigned long long *)&s_live[wave], (unsigned long long)(cm0 | cm1));
             wave_sync();
-            const uint64_t live = __builtin_amdgcn_readfirstlane((uint32_t)s_live[wave]) |
-                                  ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_live[wave] >> 32)) << 32);
+            // readfirstlane returns int: widen through uint32_t, or a low half with bit 31
+            // set sign-extends over the high half (blocks 32-63 live without candidates)
+            const uint64_t live =
+                (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)s_live[wave]) |
+                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_live[wave] >> 32)) << 32);
             // ---- fold: block by block, lane = pixel, candidates ascending ----
             for (uint64_t rest = live; rest; rest &= rest - 1) {
                 const int blk = __builtin_ctzll(rest);

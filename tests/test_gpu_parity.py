@@ -752,3 +752,58 @@ def test_pack_records_zero_copy():
     with pytest.raises(PPError):
         call('pp_pack_records', _device.ptr(b.anns), _device.ptr(b.counts), b.n, b.cap,
              ctypes.c_void_p(pageable.ctypes.data), cut, _device.ptr(cnt), _device.stream())
+
+
+def test_cifhr_sparse_poisoned_buffers():
+    """Block-sparse CifHr on map / mask / workspace buffers poisoned with NaN and junk, after
+    launches that leave wide-splat candidates in LDS: every tile with block 31 live once also
+    marked blocks 32-63 (a sign-extended live mask) and folded a stale candidate into them.
+    Bit-exact against the oracle, and no block marked that no splat box touches."""
+    import ctypes
+    import torch
+    from openpifpaf_amd import _device, synthetic
+    from openpifpaf_amd._abi import make_config
+    from openpifpaf_amd._lib import call, load
+    from openpifpaf_amd.decoder.cif_hr import sparse_to_dense
+    lib = load()
+    cfg = make_config()
+    pcif, _ = synthetic.batch('planted', 8, 80, 80)
+    ucif, _ = synthetic.batch('uniform', 2, 80, 80)
+    rng = np.random.default_rng(5)
+    wide = ucif.copy()
+    wide[:, :, 4] = rng.uniform(0.5, 30.0, wide[:, :, 4].shape).astype(np.float32)
+    wide[:, :, 0, 20:60, 20:60] = 0.9
+    for name, cif in (('wide', wide), ('planted', pcif), ('uniform', ucif)):
+        n, k, _, h, w = cif.shape
+        t = int(lib.pp_cifhr_sparse_tiles(h, w, 8))
+        hmap = torch.full((n, k, t, 64, 64), float('nan'), device='cuda')
+        masks = torch.full((n, k, t), 0x5A5A5A5A, dtype=torch.int64, device='cuda')
+        ws = torch.full((max(1, lib.pp_cifhr_sparse_workspace_size(n, k, h, w)),), 0x7F,
+                        dtype=torch.uint8, device='cuda')
+        dcif = torch.from_numpy(cif).cuda()
+        call('pp_cifhr_sparse', _device.ptr(dcif), n, k, h, w, ctypes.byref(cfg),
+             _device.ptr(hmap), _device.ptr(masks), _device.ptr(ws), ctypes.c_size_t(ws.numel()),
+             _device.stream())
+        hm, mk = hmap.cpu().numpy(), masks.cpu().numpy()
+        assert not (mk.view(np.uint64) == 0x5A5A5A5A).any(), name  # every tile's mask written
+        for i in range(n):
+            ref = oracle.cifhr(cif[i], cfg)
+            dense = sparse_to_dense(hm[i], mk[i], 633, 633)
+            assert np.array_equal(dense, ref), (name, i)
+            # marked blocks lie inside some splat box: a block no box touches is unmarked
+            bits = np.unpackbits(mk[i].view(np.uint8), bitorder='little').reshape(k, t, 64)
+            covered = np.zeros((k, t, 64), bool)
+            keep = cif[i, :, 0] > np.float32(0.1)
+            for f in range(k):
+                cx = cif[i, f, 1][keep[f]] * np.float32(8)
+                cy = cif[i, f, 2][keep[f]] * np.float32(8)
+                sg = np.fmax(np.float32(1), (np.float32(0.5) * cif[i, f, 4][keep[f]]) * np.float32(8))
+                x0 = np.clip(cx - sg, 0, 632).astype(int)
+                x1 = np.clip(cx + sg + 1, x0 + 1, 633).astype(int)
+                y0 = np.clip(cy - sg, 0, 632).astype(int)
+                y1 = np.clip(cy + sg + 1, y0 + 1, 633).astype(int)
+                for a0, a1, b0, b1 in zip(x0, x1, y0, y1):
+                    for by in range(b0 // 8, (b1 - 1) // 8 + 1):
+                        bx = np.arange(a0 // 8, (a1 - 1) // 8 + 1)
+                        covered[f, (by // 8) * 10 + bx // 8, (by % 8) * 8 + bx % 8] = True
+            assert not (bits.astype(bool) & ~covered).any(), (name, i)
