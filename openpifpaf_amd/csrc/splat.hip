@@ -573,7 +573,7 @@ __global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
 // candidates carry their group, and a change of group closes the running fold into res.
 // Across passes res stays in the map and the open group's fold in `aux`.
 constexpr int kSpList = 256;  // splat entries of a field kept in LDS
-constexpr int kSpCand = 128;  // candidates per wave pass (two u64 block bitmasks per lane)
+constexpr int kSpCand = 64;   // candidates per wave pass (one u64 block bitmask per lane)
 constexpr int kSpU = 8;       // cells per thread per compaction round
 
 struct HrSparseArgs {
