@@ -22,6 +22,10 @@
 // correctly rounded through f64.
 #include "pp_common.hpp"
 
+#include <stdlib.h>
+
+#include <mutex>
+
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -2045,6 +2049,40 @@ size_t pp_decode_multi_workspace_zero_offset(const pp_scale *scales, int32_t n_s
 
 namespace pp {
 
+// One non-blocking side stream (+ fork / join events) per device, created on first use;
+// the mutex keeps concurrent host threads' fork / join pairs from interleaving.  PP_SIDE=0
+// turns the overlap off (diagnostics).
+struct SideStream {
+    hipStream_t stream;
+    hipEvent_t fork, join;
+    mutable std::mutex mu;
+};
+
+static const SideStream *side_stream() {
+    static std::mutex create_mu;
+    static SideStream *per_dev[64] = {};
+    static const bool off = [] {
+        const char *e = getenv("PP_SIDE");
+        return e && e[0] == '0';
+    }();
+    if (off) return nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lock(create_mu);
+    if (!per_dev[dev]) {
+        SideStream *ss = new SideStream();
+        if (hipStreamCreateWithFlags(&ss->stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&ss->fork, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ss->join, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            delete ss;
+            return nullptr;
+        }
+        per_dev[dev] = ss;
+    }
+    return per_dev[dev];
+}
+
 static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
                         const int32_t *skeleton, const pp_config *cfg, float *d_cifhr,
                         pp_ann *d_anns, int32_t ann_capacity, int32_t *d_counts,
@@ -2095,14 +2133,35 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
                                      "pp_decode_batch(cifhr)");
         if (rc) return rc;
     }
-    if (stages & 2u) {
-        rc = launch_seeds(h, hr, n_img, K, cfg, seeds, d.seed_cap, seed_counts, ws + d.off_seed_ws, s);
-        if (rc) return rc;
-    }
-    if (stages & 4u) {  // CafScored at caf_threshold; the force-complete set is lazy
+    // CifSeeds and CafScored both read only the fields and the CifHr map: with both stages
+    // requested, CafScored runs on a side stream beside the seeds (fork / join events)
+    const SideStream *side = (stages & 6u) == 6u ? side_stream() : nullptr;
+    if (side) {
+        std::lock_guard<std::mutex> lock(side->mu);
+        if (hipEventRecord(side->fork, s) != hipSuccess ||
+            hipStreamWaitEvent(side->stream, side->fork, 0) != hipSuccess)
+            return fail(PP_EHIP, "pp_decode_batch: side-stream fork failed");
         rc = launch_caf_bucketed(h, hr, n_img, K, C, skeleton, cfg, cfg->caf_threshold, cols[0],
-                                 offs[0], nullptr, false, s);
+                                 offs[0], nullptr, false, side->stream);
+        if (!rc)
+            rc = launch_seeds(h, hr, n_img, K, cfg, seeds, d.seed_cap, seed_counts,
+                              ws + d.off_seed_ws, s);
+        // join even after a failed launch, so the caller's stream never runs ahead
+        if (hipEventRecord(side->join, side->stream) != hipSuccess ||
+            hipStreamWaitEvent(s, side->join, 0) != hipSuccess)
+            return fail(PP_EHIP, "pp_decode_batch: side-stream join failed");
         if (rc) return rc;
+    } else {
+        if (stages & 2u) {
+            rc = launch_seeds(h, hr, n_img, K, cfg, seeds, d.seed_cap, seed_counts,
+                              ws + d.off_seed_ws, s);
+            if (rc) return rc;
+        }
+        if (stages & 4u) {  // CafScored at caf_threshold; the force-complete set is lazy
+            rc = launch_caf_bucketed(h, hr, n_img, K, C, skeleton, cfg, cfg->caf_threshold,
+                                     cols[0], offs[0], nullptr, false, s);
+            if (rc) return rc;
+        }
     }
     if (stages & 8u) {
         GrowArgs g{};
