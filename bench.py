@@ -4,8 +4,9 @@
                     [--generator planted|uniform] [--mode eval|predict]
 
 One step = one full decode (CifHr -> seeds -> CafScored -> seed loop / grow ->
-force-complete -> NMS) of the rank's resident batch of synthetic fields, plus the device
-gather of the packed annotation records and their copy to the host; for N > 1 also the
+force-complete -> NMS) of the rank's resident batch of synthetic fields, plus the packing
+of its annotation records into pinned host memory (steps are pipelined two deep: step k + 1
+is enqueued before step k's records are waited for); for N > 1 also the
 RCCL all-gather of every rank's records to rank 0 (weak scaling: each rank owns its own
 batch, no data-path collective).  Inputs are generated once and stay in HBM.
 
@@ -103,7 +104,10 @@ def main():
               (STAGE_CIFHR, STAGE_SEEDS | STAGE_CAF | STAGE_GROW))
     names = (('cifhr', 'seeds', 'caf_scored', 'grow_nms') if args.stage_breakdown else
              ('cifhr', 'seeds+caf+grow+nms'))
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(len(groups) + 1)]
+    # two event sets: with the two-deep pipeline, step k's events are read after step k + 1
+    # has recorded its own
+    ev_sets = [[torch.cuda.Event(enable_timing=True) for _ in range(len(groups) + 1)]
+               for _ in range(2)]
 
     def timed_run(cif, caf, steps, warmup, heads=None):
         """warmup + `steps` timed decode steps of one resident batch (cif / caf, or a
@@ -111,7 +115,10 @@ def main():
         annotations decoded)."""
         stage_ms = np.zeros(len(groups))
 
-        def step(timed):
+        def step(timed, k=0):
+            """Enqueue one decode and its record fetch; returns (buffers, (PendingRecords,
+            its event set))."""
+            ev = ev_sets[k % 2]
             b = None
             for si, bits in enumerate(groups):
                 if timed:
@@ -122,20 +129,29 @@ def main():
                     b = eng.launch(cif, caf, skeleton, cfg, stages=stages & bits)
             if timed:
                 ev[len(groups)].record(stream)
-            recs = None
-            if stages & STAGE_GROW:
-                recs, offsets = eng.fetch(b)  # packed records -> host (synchronises)
+            # packed records -> pinned host memory, enqueued behind the decode
+            return b, ((eng.fetch_async(b) if stages & STAGE_GROW else None), ev)
+
+        def finish(step_out, timed):
+            """Wait for one step's records (and, for N > 1, gather them to rank 0)."""
+            pending, ev = step_out
+            n_recs = 0
+            if pending is None:
+                torch.cuda.synchronize()
+            else:
+                recs, offsets = pending.result()
                 if world > 1:
                     recs, _ = gather_records(recs, offsets, dist, dev)
+                n_recs = len(recs)
             if timed:
-                torch.cuda.synchronize()
+                ev[len(groups)].synchronize()
                 for si in range(len(groups)):
                     stage_ms[si] += ev[si].elapsed_time(ev[si + 1])
-            return b, recs
+            return n_recs
 
         for _ in range(warmup):
-            b, recs = step(False)
-            recs = None
+            b, p = step(False)
+            finish(p, False)
         status = b.status.cpu().numpy()
         if status.any():
             raise SystemExit('decode status flags set: {}'.format(status[status != 0][:8]))
@@ -144,10 +160,17 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         n_anns = 0
-        for _ in range(steps):
-            b, recs = step(True)
-            n_anns += 0 if recs is None else len(recs)
-            recs = None  # the caller owns records; release them so pinned blocks recycle
+        # two-deep pipeline: step k + 1 is enqueued before step k's records are waited for
+        # (decode outputs are double-buffered, engine.DecodeBuffers), so the host's record
+        # handling and next launches overlap the device work; every step's records are on
+        # the host before the clock stops
+        pending = None
+        for k in range(steps):
+            b, p = step(True, k)
+            if pending is not None:
+                n_anns += finish(pending, True)
+            pending = p
+        n_anns += finish(pending, True)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()

@@ -50,13 +50,24 @@ class DecodeBuffers:
                           lib.pp_last_error().decode())
         self.ws = torch.empty(size, dtype=torch.uint8, device=device)
         self.ws[zero_off:].zero_()
-        self.anns = torch.empty(n * cap * ANN_DTYPE.itemsize, dtype=torch.uint8, device=device)
-        self.counts = torch.zeros(n, dtype=torch.int32, device=device)
-        self.status = torch.zeros(n, dtype=torch.int32, device=device)
+        # two output slots (records, counts, status): a decode with the grow stage writes the
+        # slot after the previous one, so records of decode i can still be packed / fetched
+        # while decode i + 1 runs (DecodeEngine.fetch_async)
+        self._slots = [(torch.empty(n * cap * ANN_DTYPE.itemsize, dtype=torch.uint8, device=device),
+                        torch.zeros(n, dtype=torch.int32, device=device),
+                        torch.zeros(n, dtype=torch.int32, device=device)) for _ in range(2)]
+        self._cur = 0
         self.hh = (h - 1) * stride + 1
         self.ww = (w - 1) * stride + 1
         self.pitch = int(lib.pp_cifhr_pitch(self.ww))
         self.cifhr = None
+
+    anns = property(lambda self: self._slots[self._cur][0])
+    counts = property(lambda self: self._slots[self._cur][1])
+    status = property(lambda self: self._slots[self._cur][2])
+
+    def next_slot(self):
+        self._cur ^= 1
 
     def cifhr_buffer(self):
         if self.cifhr is None:
@@ -127,6 +138,8 @@ class DecodeEngine:
             raise ValueError('skeleton has {} edges but caf has {} fields'.format(len(skel), c))
         cap = cap or default_ann_capacity(h, w)
         b = self.buffers(n, k, c, h, w, cfg, cap)
+        if stages & STAGE_GROW:
+            b.next_slot()
         hr = b.cifhr_buffer() if keep_cifhr else None
         call('pp_decode_stages', _device.ptr(cif), _device.ptr(caf), n, k, c, h, w,
              skel.ctypes.data_as(ctypes.c_void_p), ctypes.byref(cfg), _device.ptr(hr),
@@ -143,6 +156,8 @@ class DecodeEngine:
                                                                                   heads.c))
         cap = cap or default_ann_capacity(heads.h, heads.w)
         b = self.buffers(heads.n, heads.k, heads.c, heads.h, heads.w, cfg, cap, heads)
+        if stages & STAGE_GROW:
+            b.next_slot()
         hr = b.cifhr_buffer() if keep_cifhr else None
         call('pp_decode_multi', heads.arr, len(heads.arr), heads.pairs, heads.n, heads.k,
              heads.c, skel.ctypes.data_as(ctypes.c_void_p), ctypes.byref(cfg), _device.ptr(hr),
@@ -176,33 +191,38 @@ class DecodeEngine:
 
     @staticmethod
     def fetch(b):
-        """Packed records of all images and per-image offsets, after one stream
-        synchronisation: pp_pack_records writes the counts and the records, image after
-        image, straight into a pinned host block (zero-copy).  The block is sized from the
-        largest batch seen so far; a batch that outgrows it is fetched again by
-        `fetch_gather` (and the next block is larger)."""
+        """Packed records of all images and per-image offsets of the last decode into `b`
+        (fetch_async(b).result())."""
+        return DecodeEngine.fetch_async(b).result()
+
+    @staticmethod
+    def fetch_async(b):
+        """Enqueue the record fetch of the last decode into `b` on the current stream and
+        return a PendingRecords; its result() waits for it.  pp_pack_records writes the
+        counts and the records, image after image, straight into a pinned host block
+        (zero-copy), so one synchronisation hands over everything.  The block is sized from
+        the largest batch seen so far; a batch that outgrows it is fetched again from the
+        device records by the gather path.  The slot stays valid until the second decode
+        after this one, so a caller may launch the next decode before calling result()."""
         n, width = b.n, ANN_DTYPE.itemsize
         est = max(getattr(b, 'pack_cap', 0), 16 * n)
         head = -(-4 * n // 256) * 256
-        # pinned block from torch's caching host allocator: the returned array owns it
-        # (released to the cache when the caller drops the records)
+        # pinned block from torch's caching host allocator: the returned records own it
+        # (released to the cache when the caller drops them)
         host = torch.empty(head + est * width, dtype=torch.uint8, pin_memory=True)
         call('pp_pack_records', _device.ptr(b.anns), _device.ptr(b.counts), n, b.cap,
              ctypes.c_void_p(host.data_ptr() + head), est, ctypes.c_void_p(host.data_ptr()),
              _device.stream())
-        torch.cuda.current_stream(b.anns.device).synchronize()
-        counts = host[:4 * n].numpy().view(np.int32).astype(np.int64)
-        offsets = np.concatenate([[0], np.cumsum(counts)])
-        total = int(offsets[-1])
-        if total > est:
-            b.pack_cap = 2 * total
-            return DecodeEngine.fetch_gather(b)
-        return host[head:head + total * width].numpy().view(ANN_DTYPE), offsets
+        done = torch.cuda.Event()
+        done.record()
+        return PendingRecords(b, b.anns, b.counts, host, head, est, done)
 
     @staticmethod
-    def fetch_gather(b):
-        """Packed records of all images (one gather + one D2H copy) and per-image offsets."""
-        counts = b.counts.cpu().numpy().astype(np.int64)
+    def fetch_gather(b, anns=None, counts=None):
+        """Packed records of all images (one gather + one D2H copy) and per-image offsets;
+        `anns` / `counts` select an output slot (default: the last decode's)."""
+        anns = b.anns if anns is None else anns
+        counts = (b.counts if counts is None else counts).cpu().numpy().astype(np.int64)
         offsets = np.concatenate([[0], np.cumsum(counts)])
         total = int(offsets[-1])
         if total == 0:
@@ -210,7 +230,7 @@ class DecodeEngine:
         # row of record r of image i is i * cap + r: one vectorised gather index
         idx = np.arange(total, dtype=np.int64) + np.repeat(
             np.arange(len(counts), dtype=np.int64) * b.cap - offsets[:-1], counts)
-        rows = b.anns.view(b.n * b.cap, ANN_DTYPE.itemsize)
+        rows = anns.view(b.n * b.cap, ANN_DTYPE.itemsize)
         sel = rows.index_select(0, torch.from_numpy(idx).to(rows.device))
         # pinned destination from torch's caching host allocator: full-rate D2H, and the
         # returned array owns the block (released to the cache when the caller drops it)
@@ -218,6 +238,27 @@ class DecodeEngine:
         host.copy_(sel, non_blocking=True)
         torch.cuda.current_stream(rows.device).synchronize()
         return host.numpy().reshape(-1).view(ANN_DTYPE), offsets
+
+
+class PendingRecords:
+    """A record fetch enqueued by DecodeEngine.fetch_async."""
+
+    def __init__(self, b, anns, counts, host, head, est, done):
+        self._b, self._anns, self._counts = b, anns, counts
+        self._host, self._head, self._est, self._done = host, head, est, done
+
+    def result(self):
+        """(records, offsets) once the fetch has completed (waits for it)."""
+        b, n, width = self._b, self._b.n, ANN_DTYPE.itemsize
+        self._done.synchronize()
+        counts = self._host[:4 * n].numpy().view(np.int32).astype(np.int64)
+        offsets = np.concatenate([[0], np.cumsum(counts)])
+        total = int(offsets[-1])
+        if total > self._est:
+            b.pack_cap = 2 * total
+            return DecodeEngine.fetch_gather(b, self._anns, self._counts)
+        return (self._host[self._head:self._head + total * width].numpy().view(ANN_DTYPE),
+                offsets)
 
 
 _ENGINE = None

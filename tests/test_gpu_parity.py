@@ -807,3 +807,35 @@ def test_cifhr_sparse_poisoned_buffers():
                         bx = np.arange(a0 // 8, (a1 - 1) // 8 + 1)
                         covered[f, (by // 8) * 10 + bx // 8, (by % 8) * 8 + bx % 8] = True
             assert not (bits.astype(bool) & ~covered).any(), (name, i)
+
+
+def test_fetch_async_two_deep():
+    """Decode i + 1 launched before decode i's records are fetched (the bench's two-deep
+    pipeline): each PendingRecords returns exactly its own decode's records, including the
+    gather fallback when the pinned block is too small (uniform: > 16 records per image)."""
+    import torch
+    from openpifpaf_amd import constants, engine, synthetic
+    from openpifpaf_amd._abi import EVAL_CONFIG, make_config
+    cfg = make_config(**EVAL_CONFIG)
+    sk = constants.COCO_PERSON_SKELETON
+    batches = [synthetic.batch('planted', 6, 48, 48, first_seed=s) for s in (0, 50)]
+    batches += [synthetic.batch('uniform', 6, 48, 48, first_seed=s) for s in (3, 9)]
+    dev = [(torch.from_numpy(c).cuda(), torch.from_numpy(f).cuda()) for c, f in batches]
+    ref = []
+    for c, f in dev:
+        r, off = engine.DecodeEngine().decode(c, f, sk, cfg)[:2]
+        ref.append((r.copy(), off))
+    eng = engine.DecodeEngine()
+    for order in ((0, 1, 0, 1), (2, 3, 2, 3)):
+        pending = None
+        for i in order:
+            b = eng.launch(*dev[i], sk, cfg)
+            p = (i, eng.fetch_async(b))
+            if pending is not None:
+                j, q = pending
+                got, off = q.result()
+                assert np.array_equal(off, ref[j][1]) and got.tobytes() == ref[j][0].tobytes(), j
+            pending = p
+        j, q = pending
+        got, off = q.result()
+        assert np.array_equal(off, ref[j][1]) and got.tobytes() == ref[j][0].tobytes(), j
