@@ -57,6 +57,7 @@ class DecodeBuffers:
                         torch.zeros(n, dtype=torch.int32, device=device),
                         torch.zeros(n, dtype=torch.int32, device=device)) for _ in range(2)]
         self._cur = 0
+        self._free = [None, None]  # per slot: event after which its records were packed
         self.hh = (h - 1) * stride + 1
         self.ww = (w - 1) * stride + 1
         self.pitch = int(lib.pp_cifhr_pitch(self.ww))
@@ -67,7 +68,12 @@ class DecodeBuffers:
     status = property(lambda self: self._slots[self._cur][2])
 
     def next_slot(self):
+        """Switch to the other output slot; the current stream waits until that slot's
+        previous records have been packed (fetch_async packs on a side stream)."""
         self._cur ^= 1
+        if self._free[self._cur] is not None:
+            torch.cuda.current_stream().wait_event(self._free[self._cur])
+            self._free[self._cur] = None
 
     def cifhr_buffer(self):
         if self.cifhr is None:
@@ -210,12 +216,28 @@ class DecodeEngine:
         # pinned block from torch's caching host allocator: the returned records own it
         # (released to the cache when the caller drops them)
         host = torch.empty(head + est * width, dtype=torch.uint8, pin_memory=True)
-        call('pp_pack_records', _device.ptr(b.anns), _device.ptr(b.counts), n, b.cap,
-             ctypes.c_void_p(host.data_ptr() + head), est, ctypes.c_void_p(host.data_ptr()),
-             _device.stream())
-        done = torch.cuda.Event()
-        done.record()
+        # the pack runs on a side stream after the decode, so its PCIe writes overlap the
+        # next decode; the slot is not rewritten before it is done (DecodeBuffers.next_slot)
+        decoded = torch.cuda.Event()
+        decoded.record()
+        side = DecodeEngine._pack_stream(b.anns.device)
+        side.wait_event(decoded)
+        with torch.cuda.stream(side):
+            call('pp_pack_records', _device.ptr(b.anns), _device.ptr(b.counts), n, b.cap,
+                 ctypes.c_void_p(host.data_ptr() + head), est, ctypes.c_void_p(host.data_ptr()),
+                 _device.stream())
+            done = torch.cuda.Event()
+            done.record()
+        b._free[b._cur] = done
         return PendingRecords(b, b.anns, b.counts, host, head, est, done)
+
+    _pack_streams = {}
+
+    @staticmethod
+    def _pack_stream(device):
+        if device not in DecodeEngine._pack_streams:
+            DecodeEngine._pack_streams[device] = torch.cuda.Stream(device=device)
+        return DecodeEngine._pack_streams[device]
 
     @staticmethod
     def fetch_gather(b, anns=None, counts=None):
