@@ -438,7 +438,7 @@ __device__ __forceinline__ int caf_bucket(float x, float y, int bw, int bh, floa
 // the grow kernel's merge ignores the order inside a bucket), for set B each cell's two
 // bucket ids.  A set-A stash that overflows (more than kStashA kept columns in a direction)
 // makes pass 2 recompute from the fields, as the non-STASH kernel always does.
-constexpr int kStashA = 384;      // kept columns per direction (set A stash)
+constexpr int kStashA = 256;      // kept columns per direction (set A stash): 29 KB of LDS, 5 workgroups per CU
 constexpr int kStashCells = 8192; // cells of all heads (set B stash: u16 bucket per direction)
 constexpr uint16_t kNoBucket = 0xFFFF;
 
