@@ -25,7 +25,8 @@ def gather_records(recs, offsets, dist, device):
 
     `recs` is this rank's ANN_DTYPE array, `offsets` its per-image offsets (len n + 1).
     Returns (records, offsets) of all ranks in rank order (images of rank 0 first), on every
-    rank.  Records travel as one padded uint8 tensor per rank.
+    rank.  Records and offsets travel as one padded uint8 tensor per rank (one all-gather
+    after the (count, images) exchange).
     """
     world = dist.get_world_size()
     width = ANN_DTYPE.itemsize
@@ -35,24 +36,26 @@ def gather_records(recs, offsets, dist, device):
     dist.all_gather(metas, meta)
     counts = [int(m[0].item()) for m in metas]
     n_imgs = [int(m[1].item()) for m in metas]
-    cap = max(1, max(counts))
-    buf = torch.zeros((cap, width), dtype=torch.uint8, device=device)
+    # one padded uint8 buffer per rank: the records, then the offsets (int64) in the rows
+    # after them, so the data travels in a single all-gather
+    cap = max(counts)
+    off_rows = -(-8 * (max(n_imgs) + 1) // width)
+    buf = torch.zeros((cap + off_rows, width), dtype=torch.uint8, device=device)
     if len(recs):
         buf[:len(recs)] = torch.from_numpy(
             np.ascontiguousarray(recs).view(np.uint8).reshape(-1, width)).to(device)
+    offs = np.zeros(off_rows * width // 8, dtype=np.int64)
+    offs[:n_img + 1] = np.asarray(offsets, dtype=np.int64)
+    buf[cap:] = torch.from_numpy(offs.view(np.uint8).reshape(off_rows, width)).to(device)
     parts = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(parts, buf)
-    offs = torch.zeros(max(n_imgs) + 1, dtype=torch.int64, device=device)
-    offs[:n_img + 1] = torch.from_numpy(np.asarray(offsets, dtype=np.int64)).to(device)
-    all_offs = [torch.empty_like(offs) for _ in range(world)]
-    dist.all_gather(all_offs, offs)
 
     out_recs, out_offs, base = [], [0], 0
     for r in range(world):
-        host = parts[r][:counts[r]].cpu().numpy()
-        out_recs.append(host.reshape(-1).view(ANN_DTYPE) if counts[r] else
+        host = parts[r].cpu().numpy()
+        out_recs.append(host[:counts[r]].reshape(-1).view(ANN_DTYPE) if counts[r] else
                         np.zeros(0, ANN_DTYPE))
-        o = all_offs[r][:n_imgs[r] + 1].cpu().numpy()
+        o = np.ascontiguousarray(host[cap:]).reshape(-1).view(np.int64)[:n_imgs[r] + 1]
         out_offs.extend((base + o[1:]).tolist())
         base += counts[r]
     return np.concatenate(out_recs), np.asarray(out_offs, dtype=np.int64)
