@@ -1,14 +1,18 @@
 """Benchmark: batched CIF/CAF decode on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg3|cfg2|cfg5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg3|cfg4|cfg5|cfg2]
                     [--generator planted|uniform] [--mode eval|predict]
 
 One step = one full decode (CifHr -> seeds -> CafScored -> seed loop / grow ->
 force-complete -> NMS) of the rank's resident batch of synthetic fields, plus the packing
-of its annotation records into pinned host memory (steps are pipelined two deep: step k + 1
-is enqueued before step k's records are waited for); for N > 1 also the
-RCCL all-gather of every rank's records to rank 0 (weak scaling: each rank owns its own
-batch, no data-path collective).  Inputs are generated once and stay in HBM.
+of its compact annotation records (pp_pack_compact) into pinned host memory (steps are
+pipelined two deep: step k + 1 is enqueued before step k's records are waited for).  For
+N > 1 each rank decodes its own batch (weak scaling, no data-path collective) and the
+records of every rank are gathered to rank 0 over RCCL inside the step (the other ranks
+pack into device memory and send from there).  Inputs are generated once and stay in HBM.
+
+`--gpus N` without a torchrun environment starts the N rank processes itself (before any
+GPU call in this process) and exits with their status.
 
 Rank 0 prints ONE JSON line.  `roofline` is the CifHr accumulation of the metric: the
 dense CifHr.accumulated map (pp_cifhr) of the same resident batch, timed with HIP events
@@ -32,9 +36,11 @@ sys.path.insert(0, REPO)
 WORKLOADS = {
     # BASELINE.json configs[2]: synthetic batch=256 at 80x80, full CifCaf, 1 GPU
     'cfg3': dict(h=80, w=80, batch=256, skeleton='coco', n_people=8),
+    # configs[3]: batch 2048 at 80x80 over 8 GPUs = 256 per GPU, records gathered to rank 0
+    'cfg4': dict(h=80, w=80, batch=256, skeleton='coco', n_people=8),
     # configs[1]: batch 1, CifHr + seeds only
     'cfg2': dict(h=80, w=80, batch=1, skeleton='coco', n_people=8, stages=3),
-    # configs[4]: 160x160, dense 44-CAF skeleton, 64 images per GPU
+    # configs[4]: 160x160, dense 44-CAF skeleton, batch 512 over 8 GPUs = 64 per GPU
     'cfg5': dict(h=160, w=160, batch=64, skeleton='dense', n_people=16),
 }
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
@@ -45,7 +51,8 @@ def parse():
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=20)
     p.add_argument('--warmup', type=int, default=3)
-    p.add_argument('--workload', default='cfg3', choices=sorted(WORKLOADS))
+    p.add_argument('--workload', default=None, choices=sorted(WORKLOADS),
+                   help='default: cfg3 on one GPU, cfg4 on several')
     p.add_argument('--generator', default='planted', choices=('planted', 'uniform'))
     p.add_argument('--mode', default='eval', choices=('eval', 'predict'))
     p.add_argument('--batch', type=int, default=None, help='images per GPU (override)')
@@ -56,29 +63,79 @@ def parse():
                    help='skip the uniform-generator line added to the default run')
     p.add_argument('--no-multi', action='store_true',
                    help='skip the multi-scale (pp_decode_multi) lines added to the default run')
+    p.add_argument('--backend', default='nccl', choices=('nccl', 'gloo'),
+                   help='process group of N > 1 (gloo: rehearsal with several ranks on one '
+                        'GPU, records staged through host memory)')
+    p.add_argument('--no-configs', action='store_true',
+                   help='skip the cfg2 / cfg5 lines added to the default run')
     p.add_argument('--stage-breakdown', action='store_true',
                    help='one library call per stage (per-stage times)')
     return p.parse_args()
 
 
+def spawn_ranks(n):
+    """Start bench.py once per GPU with the torchrun environment (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_*) and wait for all of them; returns the worst exit status.  This
+    process makes no GPU call (children are fresh processes, not re-execs)."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    status = 0
+    while procs:
+        for p in list(procs):
+            rc = p.poll()
+            if rc is None:
+                continue
+            procs.remove(p)
+            if rc != 0:
+                status = status or rc
+                for q in procs:  # one rank failed: the others would wait in a collective
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return status if status >= 0 else 128 - status
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        raise SystemExit('--gpus {} but WORLD_SIZE {}'.format(args.gpus, world))
+    # gloo rehearsal: ranks may share a GPU (nccl needs one GPU per rank)
+    dev = torch.device('cuda', local_rank % max(1, torch.cuda.device_count())
+                       if args.backend == 'gloo' else local_rank)
+    torch.cuda.set_device(dev)
+    comm_dev = dev if args.backend == 'nccl' else torch.device('cpu')
     if world > 1:
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local_rank))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device('cuda', local_rank)
+        if args.backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group('gloo')
+        assert dist.get_world_size() == args.gpus
+    if args.workload is None:
+        args.workload = 'cfg3' if world == 1 else 'cfg4'
 
     from openpifpaf_amd import build as ppbuild
     ppbuild.build(verbose=False)
     from openpifpaf_amd import constants, synthetic
-    from openpifpaf_amd.distributed import gather_records
-    from openpifpaf_amd._abi import EVAL_CONFIG, PREDICT_CONFIG, make_config
+    from openpifpaf_amd.distributed import gather_packed
+    from openpifpaf_amd._abi import (ANN_DTYPE, EVAL_CONFIG, PACK_ALL, PREDICT_CONFIG, make_config,
+                                     packed_dtype)
     from openpifpaf_amd.engine import (STAGE_CAF, STAGE_CIFHR, STAGE_GROW, STAGE_SEEDS,
                                        DecodeEngine)
 
@@ -109,40 +166,62 @@ def main():
     ev_sets = [[torch.cuda.Event(enable_timing=True) for _ in range(len(groups) + 1)]
                for _ in range(2)]
 
-    def timed_run(cif, caf, steps, warmup, heads=None):
+    comm = torch.cuda.Stream(device=dev) if world > 1 and args.backend == 'nccl' else None
+    counters = {'refetch_steps': 0, 'pack_bytes': 0}
+
+    def timed_run(cif, caf, steps, warmup, heads=None, skel=None, n_stages=None):
         """warmup + `steps` timed decode steps of one resident batch (cif / caf, or a
-        multi-scale HeadSet): (elapsed s over all ranks, per-group event ms per step,
-        annotations decoded)."""
+        multi-scale HeadSet): (elapsed s, max over ranks; per-group event ms per step;
+        annotations decoded, on rank 0 those of all ranks)."""
+        skel = skeleton if skel is None else skel
+        n_stages = stages if n_stages is None else n_stages
+        k_img = heads.k if heads is not None else cif.shape[1]
+        n_img = heads.n if heads is not None else cif.shape[0]
+        compact = (k_img, len(skel), PACK_ALL)
         stage_ms = np.zeros(len(groups))
 
         def step(timed, k=0):
-            """Enqueue one decode and its record fetch; returns (buffers, (PendingRecords,
-            its event set))."""
+            """Enqueue one decode and its record fetch; returns (PendingRecords, events)."""
             ev = ev_sets[k % 2]
             b = None
             for si, bits in enumerate(groups):
                 if timed:
                     ev[si].record(stream)
-                if stages & bits and heads is not None:
-                    b = eng.launch_multi(heads, skeleton, cfg, stages=stages & bits)
-                elif stages & bits:
-                    b = eng.launch(cif, caf, skeleton, cfg, stages=stages & bits)
+                if n_stages & bits and heads is not None:
+                    b = eng.launch_multi(heads, skel, cfg, stages=n_stages & bits)
+                elif n_stages & bits:
+                    b = eng.launch(cif, caf, skel, cfg, stages=n_stages & bits)
             if timed:
                 ev[len(groups)].record(stream)
-            # packed records -> pinned host memory, enqueued behind the decode
-            return b, ((eng.fetch_async(b) if stages & STAGE_GROW else None), ev)
+            # compact records -> pinned host memory (rank 0) or device memory (ranks that
+            # send them to rank 0), enqueued behind the decode on a side stream
+            pending = (eng.fetch_async(b, compact, device_out=world > 1 and rank != 0)
+                       if n_stages & STAGE_GROW else None)
+            return b, (pending, ev)
 
-        def finish(step_out, timed):
-            """Wait for one step's records (and, for N > 1, gather them to rank 0)."""
+        def finish(step_out, timed, local=False):
+            """Wait for one step's records (for N > 1: gathered to rank 0 over RCCL on the
+            comm stream, which waits only for this step's pack)."""
             pending, ev = step_out
             n_recs = 0
             if pending is None:
                 torch.cuda.synchronize()
-            else:
-                recs, offsets = pending.result()
-                if world > 1:
-                    recs, _ = gather_records(recs, offsets, dist, dev)
+            elif world == 1 or local:
+                recs, _ = pending.result()
+                counters['refetch_steps'] += int(recs.dtype == ANN_DTYPE)
+                counters['pack_bytes'] = len(recs) * recs.dtype.itemsize
                 n_recs = len(recs)
+            else:
+                counts = pending.wait()
+                if not pending.fits(int(counts.sum())):
+                    raise SystemExit('record block too small after warmup')
+                comm.wait_event(pending.done_event)
+                src = pending.device_records if rank != 0 else pending.host_records()
+                if comm_dev.type == 'cpu':
+                    src = src[:int(counts.sum()) * pending.dtype.itemsize].cpu()
+                recs, _ = gather_packed(src, counts, dist, n_max=n_img, dtype=pending.dtype,
+                                        device=comm_dev, stream=comm)
+                n_recs = len(recs) if recs is not None else 0
             if timed:
                 ev[len(groups)].synchronize()
                 for si in range(len(groups)):
@@ -151,11 +230,13 @@ def main():
 
         for _ in range(warmup):
             b, p = step(False)
-            finish(p, False)
+            finish(p, False, local=True)  # sizes the record block (pack_cap)
         status = b.status.cpu().numpy()
         if status.any():
             raise SystemExit('decode status flags set: {}'.format(status[status != 0][:8]))
         if world > 1:
+            b, p = step(False)
+            finish(p, False)  # one gathered step before the clock (RCCL communicators)
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -163,7 +244,7 @@ def main():
         # two-deep pipeline: step k + 1 is enqueued before step k's records are waited for
         # (decode outputs are double-buffered, engine.DecodeBuffers), so the host's record
         # handling and next launches overlap the device work; every step's records are on
-        # the host before the clock stops
+        # rank 0's host before the clock stops
         pending = None
         for k in range(steps):
             b, p = step(True, k)
@@ -176,7 +257,7 @@ def main():
             dist.barrier()
         elapsed = time.perf_counter() - t0
         if world > 1:
-            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            t = torch.tensor([elapsed], dtype=torch.float64, device=comm_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
         return elapsed, stage_ms / steps, n_anns
@@ -211,8 +292,15 @@ def main():
             'workload': '{}: {} images/GPU at {}x{}, 17 CIF / {} CAF, full CifCaf decode, {} '
                         'defaults'.format(args.workload, batch, h, w, len(skeleton), args.mode),
             'global_batch': batch * world,
-            'parallelism': 'image-sharded dp{} (RCCL all-gather of annotation records)'.format(
-                world) if world > 1 else 'single GPU',
+            'parallelism': 'image-sharded dp{} (compact records gathered to rank 0, RCCL '
+                           'send/recv)'.format(world) if world > 1 else 'single GPU',
+        },
+        # the hand-over format: compact records (pp_pack_compact) instead of 1544-byte pp_ann
+        'records': {
+            'record_bytes': packed_dtype(k, len(skeleton), PACK_ALL).itemsize,
+            'full_record_bytes': ANN_DTYPE.itemsize,
+            'bytes_per_step_rank0': counters['pack_bytes'],
+            'refetch_steps': counters['refetch_steps'],
         },
         'stage_ms': {n: round(float(v), 4) for n, v in zip(names, stage_avg)},
         'annotations_per_image': round(n_anns / max(1, args.steps * batch * world), 3)
@@ -238,7 +326,7 @@ def main():
             'dense_equivalent_gbs': round(dense_bytes / (stage_avg[0] * 1e-3) / 1e9, 1),
         },
     }
-    default_run = (args.workload == 'cfg3' and args.generator == 'planted' and
+    default_run = (args.workload in ('cfg3', 'cfg4') and args.generator == 'planted' and
                    args.mode == 'eval' and batch == WORKLOADS['cfg3']['batch'])
     if default_run:
         tr = committed_traffic()
@@ -284,6 +372,29 @@ def main():
                 'annotations_per_image': round(m_anns / (m_steps * n_img), 3),
             }
             del heads, fields
+    if default_run and world == 1 and not args.no_configs:
+        # configs[1] (cfg2): batch-1 CifHr + seeds latency, host wall clock per call
+        # (launch overhead + one synchronisation) and device time
+        line['cfg2'] = {g: cfg2_latency(g, cfg, dev) for g in ('planted', 'uniform')}
+        # configs[4] (cfg5): 160x160, dense 44-CAF skeleton, 64 images per GPU
+        w5 = WORKLOADS['cfg5']
+        line['cfg5'] = {}
+        for g in ('planted', 'uniform'):
+            kw5 = ({'n_caf': len(constants.DENSE_DECODE_SKELETON)} if g == 'uniform' else
+                   {'skeleton': constants.DENSE_DECODE_SKELETON, 'n_people': w5['n_people']})
+            c5, a5 = synthetic.batch(g, w5['batch'], w5['h'], w5['w'], **kw5)
+            c5, a5 = torch.from_numpy(c5).to(dev), torch.from_numpy(a5).to(dev)
+            s5 = max(3, args.steps // (2 if g == 'planted' else 4))
+            el5, st5, an5 = timed_run(c5, a5, s5, 1, skel=constants.DENSE_DECODE_SKELETON)
+            line['cfg5'][g] = {
+                'value': round(w5['batch'] * s5 / el5, 1), 'unit': 'images/s',
+                'images': w5['batch'], 'field': '{}x{}'.format(w5['h'], w5['w']),
+                'caf_fields': len(constants.DENSE_DECODE_SKELETON),
+                'ms_per_step': round(1e3 * el5 / s5, 4),
+                'stage_ms': {n: round(float(v), 4) for n, v in zip(names, st5)},
+                'annotations_per_image': round(an5 / (s5 * w5['batch']), 3),
+            }
+            del c5, a5
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line['cpu_baseline'] = cpu_baseline(cif_h, caf_h, skeleton, cfg, args.cpu_seconds)
     if rank == 0:
@@ -389,23 +500,91 @@ def committed_traffic():
     return out
 
 
+def cfg2_latency(gen, cfg, dev, calls=200):
+    """BASELINE.json configs[1]: one 80x80 image, CifHr + seeds only (pp_decode_stages with
+    stages 1 | 2).  Host: median wall clock of launch + synchronise per call; device: HIP
+    events over `calls` back-to-back calls."""
+    import torch
+    from openpifpaf_amd import synthetic
+    from openpifpaf_amd.engine import STAGE_CIFHR, STAGE_SEEDS, DecodeEngine
+    from openpifpaf_amd import constants
+    cif, caf = synthetic.batch(gen, 1, 80, 80)
+    cif, caf = torch.from_numpy(cif).to(dev), torch.from_numpy(caf).to(dev)
+    eng = DecodeEngine()
+    skel = constants.COCO_PERSON_SKELETON
+
+    def run():
+        eng.launch(cif, caf, skel, cfg, stages=STAGE_CIFHR | STAGE_SEEDS)
+
+    for _ in range(5):
+        run()
+    torch.cuda.synchronize()
+    host = []
+    for _ in range(calls):
+        t0 = time.perf_counter()
+        run()
+        torch.cuda.synchronize()
+        host.append(time.perf_counter() - t0)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(calls):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    return {'us_per_call_host': round(1e6 * float(np.median(host)), 2),
+            'us_per_call_device': round(1e3 * e0.elapsed_time(e1) / calls, 2),
+            'calls': calls}
+
+
 def cpu_baseline(cif, caf, skeleton, cfg, budget_s):
-    """Oracle (C restatement of the reference decoder) on one core, bounded sample."""
+    """The oracle (C restatement of the reference decoder) on the host cores, over a bounded
+    sample of the same images: one thread, then one thread per core of this job's CPU share
+    (ctypes releases the GIL for the C decode; the oracle has no global state).  The
+    reference's own Cython decoder cannot travel to the GPU box; profiles/cpu_ratio.json
+    (tools/cpu_ratio.py, measured in the build container on the same images) gives the
+    reference/oracle time ratio, so `reference_equivalent` = oracle rate / ratio."""
+    import concurrent.futures
     sys.path.insert(0, os.path.join(REPO, 'oracle'))
     import oracle  # pylint: disable=import-outside-toplevel
     oracle.lib()
-    n = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < budget_s:
-        i = n % len(cif)
-        oracle.decode(cif[i], caf[i], skeleton, cfg)
-        n += 1
-    dt = time.perf_counter() - t0
-    return {'value': round(n / dt, 2), 'unit': 'images/s', 'cores': 1, 'kind': 'port',
-            'sample': '{} single-image decodes (cycling over the first {} images of the '
-                      'batch) in {:.1f} s on one host core; oracle/pp_oracle.c'.format(
-                          n, min(n, len(cif)), dt),
-            'host_cpu_count': os.cpu_count()}
+
+    def worker(first, budget):
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget:
+            i = (first + n) % len(cif)
+            oracle.decode(cif[i], caf[i], skeleton, cfg)
+            n += 1
+        return n, time.perf_counter() - t0
+
+    n1, dt1 = worker(0, budget_s / 2)
+    one = n1 / dt1
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count()
+    cores = max(1, min(share, int(os.environ.get('OMP_NUM_THREADS', '16') or 16)))
+    with concurrent.futures.ThreadPoolExecutor(cores) as ex:
+        res = list(ex.map(lambda t: worker(17 * t, budget_s / 2), range(cores)))
+    allc = sum(n for n, _ in res) / max(dt for _, dt in res)
+    out = {'value': round(allc, 2), 'unit': 'images/s', 'cores': cores, 'kind': 'port',
+           'single_core': round(one, 2),
+           'sample': '{} single-image decodes on one core in {:.1f} s, then {} on {} threads in '
+                     '{:.1f} s, cycling over the batch; oracle/pp_oracle.c'.format(
+                         n1, dt1, sum(n for n, _ in res), cores, max(dt for _, dt in res)),
+           'host_cpu_count': os.cpu_count()}
+    try:
+        with open(os.path.join(REPO, 'profiles', 'cpu_ratio.json')) as f:
+            ratio = json.load(f)['cases']['planted']
+        out['reference_over_oracle_time'] = ratio['ratio']
+        out['reference_equivalent'] = {
+            'single_core': round(one / ratio['ratio'], 2),
+            'all_cores': round(allc / ratio['ratio'], 2),
+            'source': 'profiles/cpu_ratio.json (reference {} ms vs oracle {} ms per planted '
+                      '80x80 eval image, one thread, build container)'.format(
+                          ratio['reference_ms_per_image'], ratio['oracle_ms_per_image'])}
+    except (OSError, KeyError, ValueError):
+        pass
+    return out
 
 
 if __name__ == '__main__':

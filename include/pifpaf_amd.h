@@ -374,6 +374,32 @@ int pp_pack_records(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img
                     void *stream);
 
 /*
+ * The same hand-over with COMPACT records (the wire format of the host fetch and the
+ * multi-GPU gather): a pp_ann cut to K keypoints, pp_packed_record_size(K, C, flags) bytes
+ * (a multiple of 16), little-endian:
+ *   0   f64 score                       Annotation.score()        annotation.py:60-71
+ *   8   i32 image
+ *   12  u16 n_decoding | PP_PACK_REFETCH (bit 15), 14 u16 n_frontier
+ *   16  f32 data[K][3], f32 joint_scales[K]                       annotation.py:17-18
+ *   PP_PACK_DECODING: u8 decoding_pairs[K][2] (padded to 4 B), f32 decoding_v[K][2]: the
+ *       (jsi, jti) pairs of decoding_order (cifcaf.py:305-306) and v of xyv_jsi / xyv_jti;
+ *       their x / y are data[jsi][0:2] / data[jti][0:2] (checked on the device)
+ *   PP_PACK_FRONTIER: u8 frontier_pairs[F][2] (padded to 4 B), F = min(PP_MAX_FRONTIER, 4*C)
+ * A record whose decoding entries do not satisfy the x / y identity, or whose orders exceed
+ * K / F entries, carries PP_PACK_REFETCH: fetch that decode's full pp_ann records instead.
+ * `out` (16-byte aligned) holds out_capacity records; device or pinned host memory as for
+ * pp_pack_records.  Reference consumer: Generator.batch's per-image lists
+ * (generator.py:96-97).
+ */
+#define PP_PACK_DECODING 1u
+#define PP_PACK_FRONTIER 2u
+#define PP_PACK_REFETCH 0x8000u
+int64_t pp_packed_record_size(int32_t K, int32_t C, uint32_t flags);
+int pp_pack_compact(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img,
+                    int32_t ann_capacity, int32_t K, int32_t C, uint32_t flags, void *out,
+                    int64_t out_capacity, int32_t *out_counts, void *stream);
+
+/*
  * The same decode split into stages for measurement: bit 1 CifHr, 2 CifSeeds,
  * 4 CafScored at caf_threshold, 8 seed loop + grow + complete + NMS (stage 8 also builds
  * the complete_caf_threshold column sets, only where force-complete needs them).  Stage buffers live

@@ -32,6 +32,38 @@ ANN_DTYPE = np.dtype([
 ], align=True)
 assert ANN_DTYPE.itemsize == 1544, ANN_DTYPE.itemsize
 
+PP_PACK_DECODING = 1
+PP_PACK_FRONTIER = 2
+PP_PACK_REFETCH = 0x8000
+PACK_ALL = PP_PACK_DECODING | PP_PACK_FRONTIER
+
+
+def _up(n, m):
+    return -(-n // m) * m
+
+
+def packed_dtype(k, c, flags=PACK_ALL):
+    """Compact record of pp_pack_compact (include/pifpaf_amd.h) for K keypoints and C
+    skeleton edges; the layout pp_packed_record_size(K, C, flags) sizes."""
+    f = min(PP_MAX_FRONTIER, 4 * c)
+    names = ['score', 'image', 'n_decoding', 'n_frontier', 'data', 'joint_scales']
+    formats = ['<f8', '<i4', '<u2', '<u2', ('<f4', (k, 3)), ('<f4', (k,))]
+    offsets = [0, 8, 12, 14, 16, 16 + 12 * k]
+    o = 16 + 16 * k
+    if flags & PP_PACK_DECODING:
+        names += ['decoding_pairs', 'decoding_v']
+        formats += [('u1', (k, 2)), ('<f4', (k, 2))]
+        offsets += [o, o + _up(2 * k, 4)]
+        o += _up(2 * k, 4) + 8 * k
+    if flags & PP_PACK_FRONTIER:
+        names.append('frontier_pairs')
+        formats.append(('u1', (f, 2)))
+        offsets.append(o)
+        o += _up(2 * f, 4)
+    return np.dtype({'names': names, 'formats': formats, 'offsets': offsets,
+                     'itemsize': _up(o, 16)})
+
+
 SEED_DTYPE = np.dtype([
     ('v', np.float32), ('field', np.int32), ('x', np.float32), ('y', np.float32),
     ('s', np.float32),

@@ -43,6 +43,39 @@ class Annotation:
                               for t in range(min(int(rec['n_frontier']), len(fr)))]
         return ann
 
+    @classmethod
+    def from_packed(cls, rec, keypoints, skeleton):
+        """Build from one compact record (pp_pack_compact, include/pifpaf_amd.h): the
+        decoding_order coordinates are the data rows of the entry's joints, its v values
+        come with the record."""
+        k = len(keypoints)
+        ann = cls(keypoints, skeleton)
+        ann.data = np.array(rec['data'][:k], dtype=np.float32)
+        ann.joint_scales = np.array(rec['joint_scales'][:k], dtype=np.float32)
+        names = rec.dtype.names
+        if 'decoding_pairs' in names:
+            nd = int(rec['n_decoding']) & 0x7fff
+            pairs, dv = rec['decoding_pairs'], rec['decoding_v']
+            order = []
+            for t in range(nd):
+                js, jt = int(pairs[t, 0]), int(pairs[t, 1])
+                a, b = ann.data[js].copy(), ann.data[jt].copy()
+                a[2], b[2] = dv[t, 0], dv[t, 1]
+                order.append((js, jt, a, b))
+            ann.decoding_order = order
+        if 'frontier_pairs' in names:
+            fr = rec['frontier_pairs']
+            ann.frontier_order = [(int(fr[t, 0]), int(fr[t, 1]))
+                                  for t in range(int(rec['n_frontier']))]
+        return ann
+
+    @classmethod
+    def from_any(cls, rec, keypoints, skeleton):
+        """Full pp_ann record or compact record."""
+        if 'decoding_xyv' in rec.dtype.names:
+            return cls.from_record(rec, keypoints, skeleton)
+        return cls.from_packed(rec, keypoints, skeleton)
+
     def add(self, joint_i, xyv):
         self.data[joint_i] = xyv
         return self

@@ -165,6 +165,123 @@ __global__ __launch_bounds__(256) void pack_records_kernel(const pp_ann *__restr
     if (threadIdx.x == 0 && lead + 2 * pairs < words) dst[words - 1] = src[words - 1];
 }
 
+// -------------------------------------------------------------------------------------
+// compact records (pp_pack_compact): a pp_ann cut to K keypoints and the skeleton's frontier
+// bound, for the PCIe hand-over and the multi-GPU gather.  decoding_order keeps the pairs
+// and the two v of each entry; x / y of an entry equal the final data rows of its joints
+// (set once by _grow, cifcaf.py:300-306, and moved together by every later transform),
+// which the kernel checks bit for bit.  A record where that does not hold, or whose
+// orders exceed the compact bounds, is flagged PP_PACK_REFETCH for a full-record fetch.
+// -------------------------------------------------------------------------------------
+struct PackLayout {
+    int K, F, dec, front;
+    int off_data, off_scales, off_pairs, off_decv, off_front, size;
+};
+
+__host__ __device__ inline PackLayout pack_layout(int K, int C, uint32_t flags) {
+    PackLayout L{};
+    L.K = K;
+    L.F = min(PP_MAX_FRONTIER, 4 * C);  // frontier_order: <= 2C edges per _grow, grow + complete
+    L.dec = (flags & PP_PACK_DECODING) != 0;
+    L.front = (flags & PP_PACK_FRONTIER) != 0;
+    int o = 16;
+    L.off_data = o;
+    o += 12 * K;
+    L.off_scales = o;
+    o += 4 * K;
+    L.off_pairs = o;
+    if (L.dec) o += (2 * K + 3) / 4 * 4;
+    L.off_decv = o;
+    if (L.dec) o += 8 * K;
+    L.off_front = o;
+    if (L.front) o += (2 * L.F + 3) / 4 * 4;
+    L.size = (o + 15) / 16 * 16;
+    return L;
+}
+
+// 4-byte word i of the compact record of `a` (w3 = the count word)
+__device__ __forceinline__ uint32_t packed_word(const pp_ann &a, const PackLayout &L, int i,
+                                                uint32_t w3) {
+    const uint32_t *s = reinterpret_cast<const uint32_t *>(&a);
+    const int b = 4 * i;
+    if (i < 2) return s[offsetof(pp_ann, score) / 4 + i];
+    if (i == 2) return (uint32_t)a.image;
+    if (i == 3) return w3;
+    if (b < L.off_scales) return s[offsetof(pp_ann, data) / 4 + (b - L.off_data) / 4];
+    if (b < L.off_pairs) return s[offsetof(pp_ann, joint_scales) / 4 + (b - L.off_scales) / 4];
+    const int nd = min(a.n_decoding, L.K), nf = min(a.n_frontier, L.F);
+    if (b < L.off_decv) {  // pairs bytes [q, q + 4) of the first nd entries
+        const int q = b - L.off_pairs;
+        uint32_t w = s[offsetof(pp_ann, decoding_pairs) / 4 + q / 4];
+        const int keep = min(max(2 * nd - q, 0), 4);
+        return keep == 4 ? w : (w & ((1u << (8 * keep)) - 1u));
+    }
+    if (b < L.off_front) {  // (v of the source joint, v of the target joint) per entry
+        const int t = (b - L.off_decv) / 4, e = t >> 1;
+        return e < nd ? __float_as_uint(a.decoding_xyv[e][2 + 3 * (t & 1)]) : 0u;
+    }
+    if (b < L.off_front + (2 * L.F + 3) / 4 * 4 && L.front) {
+        const int q = b - L.off_front;
+        uint32_t w = s[offsetof(pp_ann, frontier_pairs) / 4 + q / 4];
+        const int keep = min(max(2 * nf - q, 0), 4);
+        return keep == 4 ? w : (w & ((1u << (8 * keep)) - 1u));
+    }
+    return 0u;
+}
+
+// One workgroup per image (offset = the sum of the earlier counts), one wave per record,
+// lane = one 16-byte chunk of the compact record (16-byte stores; the destination is
+// usually mapped host memory across PCIe).
+__global__ __launch_bounds__(256) void pack_compact_kernel(const pp_ann *__restrict__ anns,
+                                                           const int *__restrict__ counts, int n,
+                                                           int cap, PackLayout L, char *out,
+                                                           int64_t out_cap, int *out_counts) {
+    __shared__ int s_off;
+    const int img = blockIdx.x;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (threadIdx.x == 0) s_off = 0;
+    __syncthreads();
+    int part = 0;
+    for (int j = threadIdx.x; j < img; j += 256) part += counts[j];
+    if (part) atomicAdd(&s_off, part);
+    __syncthreads();
+    const int64_t off = s_off;
+    const int cnt = counts[img];
+    if (threadIdx.x == 0) out_counts[img] = cnt;
+    const int fit = (int)min((int64_t)min(cnt, cap), max((int64_t)0, out_cap - off));
+    const int chunks = L.size / 16;
+    for (int r = wave; r < fit; r += 4) {
+        const pp_ann &a = anns[(int64_t)img * cap + r];
+        // compact-form check: entry e's x / y equal the data rows of its joints
+        const int nd = a.n_decoding, nf = a.n_frontier;
+        bool bad = (L.dec && nd > L.K) || (L.front && nf > L.F) || nd < 0 || nf < 0;
+        if (L.dec && lane < min(nd, L.K)) {
+            const int js = a.decoding_pairs[lane][0], jt = a.decoding_pairs[lane][1];
+            if (js >= L.K || jt >= L.K) {
+                bad = true;
+            } else {
+                const float *x = a.decoding_xyv[lane];
+                bad |= __float_as_uint(x[0]) != __float_as_uint(a.data[js][0]) ||
+                       __float_as_uint(x[1]) != __float_as_uint(a.data[js][1]) ||
+                       __float_as_uint(x[3]) != __float_as_uint(a.data[jt][0]) ||
+                       __float_as_uint(x[4]) != __float_as_uint(a.data[jt][1]);
+            }
+        }
+        bad = __ballot(bad) != 0ull;
+        const uint32_t w3 = (uint32_t)(L.dec ? min(nd, L.K) : 0) | (bad ? PP_PACK_REFETCH : 0u) |
+                            ((uint32_t)(L.front ? min(nf, L.F) : 0) << 16);
+        uint4 *dst = reinterpret_cast<uint4 *>(out + (off + r) * (int64_t)L.size);
+        for (int c = lane; c < chunks; c += 64) {
+            uint4 v;
+            v.x = packed_word(a, L, 4 * c, w3);
+            v.y = packed_word(a, L, 4 * c + 1, w3);
+            v.z = packed_word(a, L, 4 * c + 2, w3);
+            v.w = packed_word(a, L, 4 * c + 3, w3);
+            dst[c] = v;
+        }
+    }
+}
+
 }  // namespace pp
 
 using namespace pp;
@@ -221,6 +338,41 @@ int pp_pack_records(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img
                        (hipStream_t)stream, d_anns, d_counts, n_img, ann_capacity,
                        (pp_ann *)dst[0], out_capacity, (int *)dst[1]);
     return check_launch("pp_pack_records");
+}
+
+int64_t pp_packed_record_size(int32_t K, int32_t C, uint32_t flags) {
+    if (K <= 0 || K > PP_MAX_KP || C <= 0 || C > PP_MAX_EDGES) return 0;
+    return pack_layout(K, C, flags).size;
+}
+
+int pp_pack_compact(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img,
+                    int32_t ann_capacity, int32_t K, int32_t C, uint32_t flags, void *out,
+                    int64_t out_capacity, int32_t *out_counts, void *stream) {
+    if (!d_anns || !d_counts || !out || !out_counts)
+        return fail(PP_EINVAL, "pp_pack_compact: NULL argument");
+    if (n_img < 0 || ann_capacity <= 0 || out_capacity < 0 || K <= 0 || K > PP_MAX_KP || C <= 0 ||
+        C > PP_MAX_EDGES)
+        return fail(PP_ESHAPE, "pp_pack_compact: bad shape");
+    if (flags & ~(uint32_t)(PP_PACK_DECODING | PP_PACK_FRONTIER))
+        return fail(PP_EINVAL, "pp_pack_compact: unknown flag");
+    if (n_img == 0) return PP_OK;
+    void *dst[2] = {out, out_counts};
+    for (void *&d : dst) {
+        hipPointerAttribute_t at;
+        if (hipPointerGetAttributes(&at, d) != hipSuccess || !at.devicePointer ||
+            (at.type != hipMemoryTypeDevice && at.type != hipMemoryTypeHost)) {
+            (void)hipGetLastError();
+            return fail(PP_EINVAL, "pp_pack_compact: destination is neither device memory nor "
+                                   "pinned host memory");
+        }
+        d = at.devicePointer;
+    }
+    if (reinterpret_cast<uintptr_t>(dst[0]) & 15)
+        return fail(PP_EINVAL, "pp_pack_compact: destination not 16-byte aligned");
+    hipLaunchKernelGGL(pack_compact_kernel, dim3((unsigned)n_img), dim3(256), 0,
+                       (hipStream_t)stream, d_anns, d_counts, n_img, ann_capacity,
+                       pack_layout(K, C, flags), (char *)dst[0], out_capacity, (int *)dst[1]);
+    return check_launch("pp_pack_compact");
 }
 
 }  // extern "C"

@@ -14,7 +14,7 @@ import time
 import numpy as np
 
 from ... import _device
-from ..._abi import make_config, skeleton_array
+from ..._abi import PACK_ALL, make_config, skeleton_array
 from ...annotation import Annotation
 from ...engine import HeadSet, engine
 from ...functional import grow_connection_blend
@@ -110,37 +110,39 @@ class CifCaf(Generator):
         LOG.debug('%d annotations, %.3fs', len(anns), time.perf_counter() - start)
         return anns
 
-    def decode_records(self, cif_batch, caf_batch, keep_cifhr=False):
-        """Device decode of a batch -> (packed pp_ann records, per-image offsets, buffers)."""
+    def decode_records(self, cif_batch, caf_batch, keep_cifhr=False, compact=None):
+        """Device decode of a batch -> (packed records, per-image offsets, buffers): full
+        pp_ann records, or compact ones (pp_pack_compact) with `compact` flags."""
         cif = _device.to_device(cif_batch)
         caf = _device.to_device(caf_batch)
         return engine().decode(cif, caf, skeleton_array(self.skeleton), self.config(),
-                               keep_cifhr=keep_cifhr)
+                               keep_cifhr=keep_cifhr, compact=compact)
 
-    def decode_fields_records(self, fields_batch, keep_cifhr=False):
+    def decode_fields_records(self, fields_batch, keep_cifhr=False, compact=None):
         """Multi-scale device decode (pp_decode_multi): fields_batch is the head output list
         with a batch dimension, indexed by the FieldConfig (factory.py:153-180)."""
         heads = HeadSet([None if f is None else _device.to_device(f) for f in fields_batch],
                         self.field_config)
         return engine().decode(None, None, skeleton_array(self.skeleton), self.config(),
-                               keep_cifhr=keep_cifhr, heads=heads)
+                               keep_cifhr=keep_cifhr, heads=heads, compact=compact)
 
-    def _annotations(self, recs, offsets):
+    def annotations_from_records(self, recs, offsets):
+        """Full or compact records + per-image offsets -> one list of Annotation per image."""
         out = []
         for i in range(len(offsets) - 1):
-            out.append([Annotation.from_record(r, self.keypoints, self.out_skeleton)
+            out.append([Annotation.from_any(r, self.keypoints, self.out_skeleton)
                         for r in recs[offsets[i]:offsets[i + 1]]])
         return out
 
     def decode_batch(self, cif_batch, caf_batch):
         """(B, K, 5, H, W) + (B, C, 9, H, W) -> one list of Annotation per image."""
-        recs, offsets, _ = self.decode_records(cif_batch, caf_batch)
-        return self._annotations(recs, offsets)
+        recs, offsets, _ = self.decode_records(cif_batch, caf_batch, compact=PACK_ALL)
+        return self.annotations_from_records(recs, offsets)
 
     def decode_fields_batch(self, fields_batch):
         """Batched head outputs of any FieldConfig -> one list of Annotation per image."""
-        recs, offsets, _ = self.decode_fields_records(fields_batch)
-        return self._annotations(recs, offsets)
+        recs, offsets, _ = self.decode_fields_records(fields_batch, compact=PACK_ALL)
+        return self.annotations_from_records(recs, offsets)
 
     # -- reference building blocks, on the device ------------------------------------------
     def _grow_connection(self, xy, xy_scale, caf_field):

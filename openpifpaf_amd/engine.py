@@ -13,8 +13,8 @@ import numpy as np
 import torch
 
 from . import _device
-from ._abi import (ANN_DTYPE, PP_ST_ANN_OVERFLOW, PP_ST_DEC_OVERFLOW, PP_ST_NMS_OVERFLOW,
-                   scale_list, skeleton_array)
+from ._abi import (ANN_DTYPE, PP_PACK_REFETCH, PP_ST_ANN_OVERFLOW, PP_ST_DEC_OVERFLOW,
+                   PP_ST_NMS_OVERFLOW, packed_dtype, scale_list, skeleton_array)
 from ._lib import PPError, call, load
 
 LOG = logging.getLogger(__name__)
@@ -172,9 +172,12 @@ class DecodeEngine:
              _device.stream())
         return b
 
-    def decode(self, cif, caf, skeleton, cfg, cap=None, keep_cifhr=False, heads=None):
+    def decode(self, cif, caf, skeleton, cfg, cap=None, keep_cifhr=False, heads=None,
+               compact=None):
         """Full decode with overflow retry.  Returns (records, offsets, buffers).  With a
-        HeadSet `heads`, cif / caf are ignored and the multi-scale decode runs."""
+        HeadSet `heads`, cif / caf are ignored and the multi-scale decode runs.  `compact`
+        flags (e.g. _abi.PACK_ALL) fetch compact records (pp_pack_compact) instead of full
+        pp_ann records."""
         h, w = (cif.shape[3], cif.shape[4]) if heads is None else (heads.h, heads.w)
         cap = cap or default_ann_capacity(h, w)
         while True:
@@ -192,30 +195,43 @@ class DecodeEngine:
                           'the field); status={}'.format(status.tolist()))
         if (status & PP_ST_DEC_OVERFLOW).any():
             raise PPError('decoding/frontier order exceeded the record capacity')
-        recs, offsets = self.fetch(b)
+        k = cif.shape[1] if heads is None else heads.k
+        recs, offsets = self.fetch(b, None if compact is None else
+                                   (k, len(skeleton_array(skeleton)), compact))
         return recs, offsets, b
 
     @staticmethod
-    def fetch(b):
+    def fetch(b, compact=None):
         """Packed records of all images and per-image offsets of the last decode into `b`
         (fetch_async(b).result())."""
-        return DecodeEngine.fetch_async(b).result()
+        return DecodeEngine.fetch_async(b, compact).result()
 
     @staticmethod
-    def fetch_async(b):
-        """Enqueue the record fetch of the last decode into `b` on the current stream and
-        return a PendingRecords; its result() waits for it.  pp_pack_records writes the
-        counts and the records, image after image, straight into a pinned host block
-        (zero-copy), so one synchronisation hands over everything.  The block is sized from
-        the largest batch seen so far; a batch that outgrows it is fetched again from the
-        device records by the gather path.  The slot stays valid until the second decode
-        after this one, so a caller may launch the next decode before calling result()."""
-        n, width = b.n, ANN_DTYPE.itemsize
-        est = max(getattr(b, 'pack_cap', 0), 16 * n)
-        head = -(-4 * n // 256) * 256
-        # pinned block from torch's caching host allocator: the returned records own it
-        # (released to the cache when the caller drops them)
-        host = torch.empty(head + est * width, dtype=torch.uint8, pin_memory=True)
+    def fetch_async(b, compact=None, device_out=False, capacity=0):
+        """Enqueue the record fetch of the last decode into `b` on a side stream and return a
+        PendingRecords; its result() waits for it.
+
+        The records are packed image after image straight into a pinned host block
+        (zero-copy through its mapped device address) together with the per-image counts,
+        so one synchronisation hands over everything.  `compact` = (K, C, flags) selects
+        pp_pack_compact's compact records (include/pifpaf_amd.h); None the full pp_ann
+        records (pp_pack_records).  `device_out` packs the records into a device buffer
+        instead (the multi-GPU gather sends them from there); the counts still land in
+        pinned host memory.  The block is sized from the largest batch seen so far; a batch
+        that outgrows it, or a compact record flagged PP_PACK_REFETCH, is fetched again as
+        full records (`capacity` = records to reserve at least).  The slot stays valid
+        until the second decode after this one, so a caller may launch the next decode
+        before calling result()."""
+        n = b.n
+        dtype = ANN_DTYPE if compact is None else packed_dtype(*compact)
+        width = dtype.itemsize
+        est = max(getattr(b, 'pack_cap', 0), 16 * n, capacity)
+        head = -(-8 * n // 256) * 256  # counts (n int32), then the slot's status (n int32)
+        host = torch.empty(head + (0 if device_out else est * width), dtype=torch.uint8,
+                           pin_memory=True)
+        dev = (torch.empty(est * width, dtype=torch.uint8, device=b.anns.device)
+               if device_out else None)
+        out_ptr = dev.data_ptr() if device_out else host.data_ptr() + head
         # the pack runs on a side stream after the decode, so its PCIe writes overlap the
         # next decode; the slot is not rewritten before it is done (DecodeBuffers.next_slot)
         decoded = torch.cuda.Event()
@@ -223,13 +239,22 @@ class DecodeEngine:
         side = DecodeEngine._pack_stream(b.anns.device)
         side.wait_event(decoded)
         with torch.cuda.stream(side):
-            call('pp_pack_records', _device.ptr(b.anns), _device.ptr(b.counts), n, b.cap,
-                 ctypes.c_void_p(host.data_ptr() + head), est, ctypes.c_void_p(host.data_ptr()),
-                 _device.stream())
+            if compact is None:
+                call('pp_pack_records', _device.ptr(b.anns), _device.ptr(b.counts), n, b.cap,
+                     ctypes.c_void_p(out_ptr), est, ctypes.c_void_p(host.data_ptr()),
+                     _device.stream())
+            else:
+                k, c, flags = compact
+                call('pp_pack_compact', _device.ptr(b.anns), _device.ptr(b.counts), n, b.cap,
+                     k, c, ctypes.c_uint32(flags), ctypes.c_void_p(out_ptr), est,
+                     ctypes.c_void_p(host.data_ptr()), _device.stream())
+            host[4 * n:8 * n].copy_(b.status.view(torch.uint8), non_blocking=True)
             done = torch.cuda.Event()
             done.record()
+            if dev is not None:
+                dev.record_stream(side)
         b._free[b._cur] = done
-        return PendingRecords(b, b.anns, b.counts, host, head, est, done)
+        return PendingRecords(b, b.anns, b.counts, host, head, est, done, dtype, dev)
 
     _pack_streams = {}
 
@@ -265,22 +290,70 @@ class DecodeEngine:
 class PendingRecords:
     """A record fetch enqueued by DecodeEngine.fetch_async."""
 
-    def __init__(self, b, anns, counts, host, head, est, done):
+    def __init__(self, b, anns, counts, host, head, est, done, dtype, dev=None):
         self._b, self._anns, self._counts = b, anns, counts
         self._host, self._head, self._est, self._done = host, head, est, done
+        self.dtype, self.device_records = dtype, dev
+        self._waited = False
+
+    def __del__(self):
+        # the pinned block goes back to torch's host cache when this object dies; the raw
+        # pack kernel must have finished writing it by then
+        if not self._waited and self._done is not None:
+            try:
+                self._done.synchronize()
+            except Exception:  # pylint: disable=broad-except
+                pass
+
+    def wait(self):
+        """Wait for the pack; per-image counts (int64).  Raises PPError when the decode set
+        an overflow bit (its records are truncated)."""
+        n = self._b.n
+        self._done.synchronize()
+        self._waited = True
+        status = self._host[4 * n:8 * n].numpy().view(np.int32)
+        bad = status & (PP_ST_ANN_OVERFLOW | PP_ST_DEC_OVERFLOW | PP_ST_NMS_OVERFLOW)
+        if bad.any():
+            raise PPError('decode status flags set (records truncated; decode() retries with '
+                          'more capacity): {}'.format(status[bad != 0][:8].tolist()))
+        return self._host[:4 * n].numpy().view(np.int32).astype(np.int64)
+
+    @property
+    def done_event(self):
+        return self._done
+
+    def host_records(self):
+        """The pinned block's record area (a CPU uint8 tensor; valid after wait())."""
+        return self._host[self._head:]
+
+    def fits(self, total):
+        return total <= self._est
 
     def result(self):
-        """(records, offsets) once the fetch has completed (waits for it)."""
-        b, n, width = self._b, self._b.n, ANN_DTYPE.itemsize
-        self._done.synchronize()
-        counts = self._host[:4 * n].numpy().view(np.int32).astype(np.int64)
+        """(records, offsets) once the fetch has completed (waits for it).  Records are
+        self.dtype, or full ANN_DTYPE records after a refetch."""
+        width = self.dtype.itemsize
+        counts = self.wait()
         offsets = np.concatenate([[0], np.cumsum(counts)])
         total = int(offsets[-1])
         if total > self._est:
-            b.pack_cap = 2 * total
-            return DecodeEngine.fetch_gather(b, self._anns, self._counts)
-        return (self._host[self._head:self._head + total * width].numpy().view(ANN_DTYPE),
-                offsets)
+            self._b.pack_cap = 2 * total
+            return DecodeEngine.fetch_gather(self._b, self._anns, self._counts)
+        if self.device_records is not None:
+            host = torch.empty(total * width, dtype=torch.uint8, pin_memory=True)
+            host.copy_(self.device_records[:total * width])
+            recs = host.numpy().view(self.dtype)
+        else:
+            recs = self._host[self._head:self._head + total * width].numpy().view(self.dtype)
+        if needs_refetch(recs):
+            return DecodeEngine.fetch_gather(self._b, self._anns, self._counts)
+        return recs, offsets
+
+
+def needs_refetch(recs):
+    """True when a compact record is flagged PP_PACK_REFETCH (its orders do not fit)."""
+    return (recs.dtype != ANN_DTYPE and len(recs) > 0 and
+            bool((recs['n_decoding'] & PP_PACK_REFETCH).any()))
 
 
 _ENGINE = None

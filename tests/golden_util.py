@@ -11,12 +11,41 @@ from openpifpaf_amd._abi import EVAL_CONFIG, PREDICT_CONFIG, make_config
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 
-# keypoint (x, y, v) and joint-scale tolerance: BASELINE.json north_star "within 1e-4"
-# (absolute), plus 1e-5 relative: hi-res pixel coordinates reach 1273 px where one f32 ulp is
-# 1.2e-4, and the reference's SIMD np.exp differs from a correctly rounded exp by up to
-# 2 ulp, which the blend propagates by a few ulp.
+# Grow-stage tolerance against the reference's own outputs (BASELINE.json north_star
+# "within 1e-4").  The reference's SIMD np.exp differs from the device's
+# correctly rounded exp by up to 2 ulp, which the blend carries into the keypoint
+# coordinates.  Coordinates reach 1273 px, where one f32 ulp (1.2e-4) already exceeds
+# 1e-4, so x / y pass when within ATOL absolute OR within XY_ULPS ulps (at most 4.9e-4 at
+# 1273 px); v within ATOL; joint scales (score-weighted means of CAF scales) within
+# ATOL + SCALE_RTOL * |s|; the f64 score within SCORE_ATOL.  Observed maxima over the
+# fixtures (oracle == device): x / y 8 ulp = 7.6e-6 at x ~ 10 and 2 ulp = 2.4e-4 at x ~ 1236
+# (u160_s0_dense_eval), v 1.1e-6, joint scale 1.3e-4 at s ~ 19, score 1.2e-7.
+XY_ULPS = 4
 ATOL = 1e-4
-RTOL = 1e-5
+SCALE_RTOL = 1e-5
+SCORE_ATOL = 1e-6
+
+
+def ulp_distance(a, b):
+    """Number of representable f32 values between a and b (elementwise; NaN == NaN -> 0)."""
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+
+    def ordered(x):
+        i = x.view(np.int32).astype(np.int64)
+        return np.where(i < 0, -(i & 0x7fffffff), i)
+
+    d = np.abs(ordered(a) - ordered(b))
+    return np.where(np.isnan(a) & np.isnan(b), 0, d)
+
+
+def xy_close(got, ref):
+    """(ok, max ulps) for keypoint coordinates: within ATOL absolute or XY_ULPS ulps."""
+    got = np.asarray(got, np.float32)
+    ref = np.asarray(ref, np.float32)
+    u = ulp_distance(got, ref)
+    ok = (u <= XY_ULPS) | (np.abs(got.astype(np.float64) - ref) <= ATOL)
+    return bool(ok.all()), int(u.max(initial=0))
 
 
 def sha(*arrays):
@@ -78,15 +107,19 @@ def seeds_as_rows(seeds):
                      seeds['s']], axis=1).astype(np.float32)
 
 
-def compare_annotations(g, recs, k=17):
+def compare_annotations(g, recs, k=17, stats=None):
     """Compare pp_ann records with the golden annotation list.
 
-    Connectivity (decoding_order / frontier_order pairs) must match exactly; (x, y, v),
-    joint scales and the decoding_order xyv copies within ATOL/RTOL; score to 1e-6.
-    Returns a list of human-readable mismatch strings (empty = parity).
+    Connectivity (decoding_order / frontier_order pairs) must match exactly; x / y of the
+    keypoints and of the decoding_order xyv copies within XY_ULPS; v and joint scales within
+    ATOL; score within SCORE_ATOL.  Returns a list of human-readable mismatch strings
+    (empty = parity); `stats` (a dict, optional) receives the largest deviations seen.
     """
     errs = []
     n = len(g['ann_score'])
+    if stats is None:
+        stats = {}
+    stats.update(xy_ulps=0, v=0.0, scale=0.0, score=0.0)
     if len(recs) != n:
         return ['annotation count %d != golden %d' % (len(recs), n)]
     for i in range(n):
@@ -101,15 +134,30 @@ def compare_annotations(g, recs, k=17):
         if int(r['n_frontier']) != nf or not np.array_equal(
                 r['frontier_pairs'][:nf].astype(np.int16), gf[:nf]):
             errs.append('ann %d frontier_order differs' % i)
-        if not np.allclose(r['data'][:k], g['ann_data'][i], atol=ATOL, rtol=RTOL):
-            errs.append('ann %d data max|d|=%g' % (
-                i, np.abs(r['data'][:k] - g['ann_data'][i]).max()))
-        if not np.allclose(r['joint_scales'][:k], g['ann_joint_scales'][i], atol=ATOL, rtol=RTOL):
-            errs.append('ann %d joint_scales differ' % i)
-        if nd and not np.allclose(r['decoding_xyv'][:nd], g['ann_decoding_xyv'][i][:nd],
-                                  atol=ATOL, rtol=RTOL):
-            errs.append('ann %d decoding_order xyv differ' % i)
-        if not np.isclose(r['score'], g['ann_score'][i], rtol=RTOL, atol=1e-9):
+        gdat = g['ann_data'][i]
+        ok, u = xy_close(r['data'][:k, :2], gdat[:, :2])
+        stats['xy_ulps'] = max(stats['xy_ulps'], u)
+        if not ok:
+            errs.append('ann %d x/y differ by %d ulp' % (i, u))
+        dv = float(np.abs(r['data'][:k, 2] - gdat[:, 2]).max(initial=0))
+        stats['v'] = max(stats['v'], dv)
+        if not dv <= ATOL:
+            errs.append('ann %d v max|d|=%g' % (i, dv))
+        gs = g['ann_joint_scales'][i]
+        ds = float(np.abs(r['joint_scales'][:k] - gs).max(initial=0))
+        stats['scale'] = max(stats['scale'], ds)
+        if not (np.abs(r['joint_scales'][:k] - gs) <= ATOL + SCALE_RTOL * np.abs(gs)).all():
+            errs.append('ann %d joint_scales max|d|=%g' % (i, ds))
+        if nd:
+            gx = g['ann_decoding_xyv'][i][:nd].reshape(nd, 2, 3)
+            rx = r['decoding_xyv'][:nd].reshape(nd, 2, 3)
+            ok, u = xy_close(rx[:, :, :2], gx[:, :, :2])
+            stats['xy_ulps'] = max(stats['xy_ulps'], u)
+            if not ok or not np.abs(rx[:, :, 2] - gx[:, :, 2]).max() <= ATOL:
+                errs.append('ann %d decoding_order xyv differ (%d ulp)' % (i, u))
+        dsc = abs(float(r['score']) - float(g['ann_score'][i]))
+        stats['score'] = max(stats['score'], dsc)
+        if not dsc <= SCORE_ATOL:
             errs.append('ann %d score %r != %r' % (i, r['score'], g['ann_score'][i]))
     return errs
 

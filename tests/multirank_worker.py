@@ -1,0 +1,55 @@
+"""One rank of tests/test_gpu_multirank.py (not collected by pytest): decodes its shard()
+of a 32-image planted + uniform batch on cuda:0, packs compact records (rank 0 into pinned
+host memory, the others into device memory), and gathers them to rank 0 over gloo; rank 0
+compares the gathered records byte for byte with a one-process decode of the whole batch.
+Environment: RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT."""
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from openpifpaf_amd import constants, synthetic  # noqa: E402
+from openpifpaf_amd._abi import EVAL_CONFIG, PACK_ALL, make_config  # noqa: E402
+from openpifpaf_amd.distributed import gather_packed, max_shard, shard  # noqa: E402
+from openpifpaf_amd.engine import DecodeEngine  # noqa: E402
+
+N = 32
+
+
+def main():
+    rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
+    dist.init_process_group('gloo')
+    torch.cuda.set_device(0)
+    skel = constants.COCO_PERSON_SKELETON
+    cfg = make_config(**EVAL_CONFIG)
+    cp, ap = synthetic.batch('planted', N // 2, 80, 80)
+    cu, au = synthetic.batch('uniform', N // 2, 80, 80, first_seed=N // 2)
+    cif = torch.from_numpy(np.concatenate([cp, cu])).cuda()
+    caf = torch.from_numpy(np.concatenate([ap, au])).cuda()
+    a, b = shard(N, rank, world)
+    eng = DecodeEngine()
+    buf = eng.launch(cif[a:b].contiguous(), caf[a:b].contiguous(), skel, cfg)
+    pend = eng.fetch_async(buf, (17, len(skel), PACK_ALL), device_out=rank != 0,
+                           capacity=1024 * (b - a))
+    counts = pend.wait()
+    nbytes = int(counts.sum()) * pend.dtype.itemsize
+    src = (pend.device_records if rank != 0 else pend.host_records())[:nbytes].cpu()
+    recs, offs = gather_packed(src, counts, dist, n_max=max_shard(N, world), dtype=pend.dtype,
+                               device=torch.device('cpu'))
+    if rank == 0:
+        ref, ref_offs, _ = DecodeEngine().decode(cif, caf, skel, cfg, compact=PACK_ALL)
+        assert ref.dtype == recs.dtype, 'one-process decode fell back to full records'
+        assert np.array_equal(offs, ref_offs), (offs[:8], ref_offs[:8])
+        assert recs.tobytes() == ref.tobytes(), 'gathered records differ'
+        print('multirank ok: {} records, {} images, world {}'.format(len(recs), N, world),
+              flush=True)
+    else:
+        assert recs is None
+    dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

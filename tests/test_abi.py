@@ -146,3 +146,16 @@ def test_scale_struct_and_multi_workspace():
     cif_only = scale_list([(0, 41, 41)], [], [8], [])
     assert lib.pp_decode_multi_workspace_size(cif_only, 1, 0, 1, 17, 19, ctypes.byref(cfg), 128) == 0
     assert lib.pp_cifhr_multi_workspace_size(cif_only, 1, 0, 1, 17) > 0
+
+
+def test_packed_record_size_matches_python_layout():
+    """pp_packed_record_size (a host function) agrees with _abi.packed_dtype for every flag
+    set, COCO and dense skeletons; compact records are at least 2x smaller than pp_ann."""
+    from openpifpaf_amd._abi import ANN_DTYPE, packed_dtype
+    lib = _lib.load()
+    for k, c in ((17, 19), (17, 44), (24, 64), (1, 1), (5, 3)):
+        for flags in (0, 1, 2, 3):
+            assert lib.pp_packed_record_size(k, c, flags) == packed_dtype(k, c, flags).itemsize
+            assert packed_dtype(k, c, flags).itemsize % 16 == 0
+    assert lib.pp_packed_record_size(0, 19, 3) == 0 and lib.pp_packed_record_size(17, 65, 3) == 0
+    assert 2 * packed_dtype(17, 19, 3).itemsize < ANN_DTYPE.itemsize

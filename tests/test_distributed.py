@@ -11,7 +11,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from openpifpaf_amd._abi import ANN_DTYPE  # noqa: E402
+from openpifpaf_amd._abi import ANN_DTYPE, PACK_ALL, packed_dtype  # noqa: E402
 from openpifpaf_amd.distributed import gather_records, shard  # noqa: E402
 
 
@@ -28,28 +28,39 @@ def test_shard_covers_batch():
         shard(4, 2, 2)
 
 
-def _rank_records(rank, n_img):
+DTYPES = {'full': ANN_DTYPE, 'compact': packed_dtype(17, 19, PACK_ALL)}
+
+
+def _rank_records(rank, n_img, dtype):
     """Deterministic fake decode output of one rank: image i has (rank + i) % 3 records."""
     rng = np.random.default_rng(100 + rank)
     counts = [(rank + i) % 3 for i in range(n_img)]
-    recs = np.zeros(sum(counts), ANN_DTYPE)
+    recs = np.zeros(sum(counts), dtype)
     recs['image'] = np.repeat(np.arange(n_img), counts)
     recs['data'] = rng.random(recs['data'].shape, dtype=np.float32)
     recs['score'] = rng.random(len(recs))
-    recs['n_keypoints'] = 17
     return recs, np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
 
 
-def _worker(rank, world, port, n_imgs):
+def _worker(rank, world, port, n_imgs, kind):
     dist.init_process_group('gloo', init_method='tcp://127.0.0.1:{}'.format(port),
                             rank=rank, world_size=world)
+    dtype = DTYPES[kind]
     try:
-        recs, offs = _rank_records(rank, n_imgs[rank])
+        recs, offs = _rank_records(rank, n_imgs[rank], dtype)
         got, got_offs = gather_records(recs, offs, dist, torch.device('cpu'))
-        exp = [_rank_records(r, n_imgs[r]) for r in range(world)]
-        exp_recs = np.concatenate([e[0] for e in exp])
-        assert got.dtype == ANN_DTYPE
-        assert got.tobytes() == exp_recs.tobytes()
+        if rank != 0:  # records are collected on rank 0 only
+            assert got is None and got_offs is None
+            return
+        exp = [_rank_records(r, n_imgs[r], dtype) for r in range(world)]
+        assert got.dtype == dtype
+        # image indices rebased to the global batch (rank r's images follow rank r - 1's)
+        bases = np.concatenate([[0], np.cumsum(n_imgs)[:-1]])
+        for (r_recs, _), b in zip(exp, bases):
+            r_recs['image'] += b
+        # bytes of each rank's array, padding included (np.concatenate would not copy the
+        # gaps of a structured dtype)
+        assert got.tobytes() == b''.join(e[0].tobytes() for e in exp)
         # offsets: images of rank 0 first, then rank 1, each shifted by the records before
         exp_offs, base = [0], 0
         for r_recs, r_offs in exp:
@@ -66,6 +77,8 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize('n_imgs', [(4, 4), (3, 5), (0, 2)])
-def test_gather_records_world2(n_imgs):
-    mp.spawn(_worker, args=(2, _free_port(), n_imgs), nprocs=2, join=True)
+@pytest.mark.parametrize('kind', sorted(DTYPES))
+@pytest.mark.parametrize('n_imgs', [(4, 4), (3, 5), (0, 2), (2, 0), (3, 3, 2, 0)])
+def test_gather_records(n_imgs, kind):
+    world = len(n_imgs)
+    mp.spawn(_worker, args=(world, _free_port(), n_imgs, kind), nprocs=world, join=True)

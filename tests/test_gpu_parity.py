@@ -1,7 +1,7 @@
 """HIP path vs the reference (golden fixtures) and vs the oracle, on an MI355X.
 
 Bit-exact: CifHr maps, seed lists, CafScored column sets, every functional primitive.
-Tolerance (golden_util.ATOL/RTOL) only for the grow-stage floats against the reference's
+Tolerance (golden_util: XY_ULPS, ATOL, SCORE_ATOL) only for the grow-stage floats against the reference's
 own outputs (np.exp rounding); against the oracle the device decode must match exactly.
 """
 import os
@@ -223,12 +223,14 @@ def test_cifcaf_vs_reference(dec, name):
     cc = dec.CifCaf(dec.FieldConfig(), keypoints=constants.COCO_KEYPOINTS, skeleton=skeleton,
                     out_skeleton=constants.COCO_PERSON_SKELETON)
     recs, _, _ = cc.decode_records(cif[None], caf[None])
-    errs = gu.compare_annotations(g, recs)
+    stats = {}
+    errs = gu.compare_annotations(g, recs, stats=stats)
+    print('max deviation vs reference:', stats)
     assert not errs, errs[:10]
     anns = cc([cif, caf])
     assert len(anns) == len(g['ann_score'])
     for a, s in zip(anns, g['ann_score']):
-        assert np.isclose(a.score(), s, rtol=gu.RTOL, atol=1e-9)
+        assert abs(a.score() - s) <= gu.SCORE_ATOL
 
 
 @pytest.mark.parametrize('name', CASES)
@@ -638,7 +640,9 @@ def test_multi_cifcaf_vs_reference(dec, name, mode):
     cc = dec.CifCaf(dec.FieldConfig(**kw), keypoints=constants.COCO_KEYPOINTS,
                     skeleton=constants.COCO_PERSON_SKELETON)
     recs, _, _ = cc.decode_fields_records([f[None] for f in fields])
-    errs = gu.compare_annotations(g, recs)
+    stats = {}
+    errs = gu.compare_annotations(g, recs, stats=stats)
+    print('max deviation vs reference:', stats)
     assert not errs, errs[:10]
     oracle_recs = oracle.decode_multi(oracle.Members(fields, **kw),
                                       constants.COCO_PERSON_SKELETON, gu.case_config(g))
@@ -646,7 +650,7 @@ def test_multi_cifcaf_vs_reference(dec, name, mode):
     anns = cc(fields)
     assert len(anns) == len(g['ann_score'])
     for a, s in zip(anns, g['ann_score']):
-        assert np.isclose(a.score(), s, rtol=gu.RTOL, atol=1e-9)
+        assert abs(a.score() - s) <= gu.SCORE_ATOL
 
 
 def _multi_batch(name, n, first_seed=100, n_people=4):
@@ -839,3 +843,110 @@ def test_fetch_async_two_deep():
         j, q = pending
         got, off = q.result()
         assert np.array_equal(off, ref[j][1]) and got.tobytes() == ref[j][0].tobytes(), j
+
+
+# ---- compact records (pp_pack_compact) -----------------------------------------------------
+
+def _compact_vs_full(recs_full, recs_c, k=17):
+    from openpifpaf_amd import constants
+    from openpifpaf_amd.annotation import Annotation
+    from openpifpaf_amd._abi import PP_PACK_REFETCH
+    assert len(recs_full) == len(recs_c)
+    assert not (recs_c['n_decoding'] & PP_PACK_REFETCH).any()
+    kps, sk = constants.COCO_KEYPOINTS[:k], constants.COCO_PERSON_SKELETON
+    for rf, rc in zip(recs_full, recs_c):
+        a, b = Annotation.from_record(rf, kps, sk), Annotation.from_packed(rc, kps, sk)
+        assert a.data.tobytes() == b.data.tobytes()
+        assert a.joint_scales.tobytes() == b.joint_scales.tobytes()
+        assert rf['score'] == rc['score'] and rf['image'] == rc['image']
+        assert a.frontier_order == b.frontier_order
+        assert len(a.decoding_order) == len(b.decoding_order)
+        for (j1, k1, x1, y1), (j2, k2, x2, y2) in zip(a.decoding_order, b.decoding_order):
+            assert (j1, k1) == (j2, k2)
+            assert x1.tobytes() == x2.tobytes() and y1.tobytes() == y2.tobytes()
+
+
+@pytest.mark.parametrize('name', CASES)
+def test_compact_records_equal_full(dec, name):
+    """Compact records (PP_PACK_DECODING | PP_PACK_FRONTIER) rebuild exactly the
+    Annotation of the full pp_ann record, with no record flagged for a refetch."""
+    from openpifpaf_amd import constants
+    from openpifpaf_amd._abi import PACK_ALL
+    g = gu.load_case(name)
+    cif, caf, skeleton = gu.case_inputs(g)
+    _configure(dec, g)
+    cc = dec.CifCaf(dec.FieldConfig(), keypoints=constants.COCO_KEYPOINTS, skeleton=skeleton)
+    full, off_f, _ = cc.decode_records(cif[None], caf[None])
+    full = full.copy()
+    comp, off_c, _ = cc.decode_records(cif[None], caf[None], compact=PACK_ALL)
+    assert np.array_equal(off_f, off_c)
+    assert comp.dtype.itemsize < full.dtype.itemsize / 2
+    _compact_vs_full(full, comp)
+
+
+def test_compact_records_batch_and_device_out():
+    """256-image planted + 32-image uniform batches: compact records into pinned host memory
+    and into device memory (the multi-GPU send buffer) equal the full records; flag subsets."""
+    import torch
+    from openpifpaf_amd import constants, engine, synthetic
+    from openpifpaf_amd._abi import (EVAL_CONFIG, PACK_ALL, PP_PACK_DECODING, make_config,
+                                     packed_dtype)
+    cfg = make_config(**EVAL_CONFIG)
+    sk = constants.COCO_PERSON_SKELETON
+    for kind, n in (('planted', 256), ('uniform', 32)):
+        cif, caf = synthetic.batch(kind, n, 80, 80, first_seed=300)
+        eng = engine.DecodeEngine()
+        b = eng.launch(torch.from_numpy(cif).cuda(), torch.from_numpy(caf).cuda(), sk, cfg)
+        full, off = eng.fetch_gather(b)
+        full = full.copy()
+        for flags in (PACK_ALL, PP_PACK_DECODING, 0):
+            p = eng.fetch_async(b, (17, 19, flags), capacity=len(full))
+            got, got_off = p.result()
+            assert got.dtype == packed_dtype(17, 19, flags)
+            assert np.array_equal(off, got_off)
+            assert np.array_equal(got['data'], full['data'][:, :17])
+            assert np.array_equal(got['score'], full['score'])
+            if flags == PACK_ALL:
+                _compact_vs_full(full, got)
+        p = eng.fetch_async(b, (17, 19, PACK_ALL), device_out=True, capacity=len(full))
+        counts = p.wait()
+        assert np.array_equal(np.concatenate([[0], np.cumsum(counts)]), off)
+        got = p.device_records[:len(full) * p.dtype.itemsize].cpu().numpy().view(p.dtype)
+        _compact_vs_full(full, got)
+
+
+def test_compact_refetch_flag():
+    """A record whose decoding_order x / y differ from its data rows (or whose order is too
+    long) is flagged PP_PACK_REFETCH, and PendingRecords.result() then returns the full
+    records."""
+    import ctypes
+    import torch
+    from openpifpaf_amd import _device, constants, engine, synthetic
+    from openpifpaf_amd._abi import (ANN_DTYPE, EVAL_CONFIG, PACK_ALL, PP_PACK_REFETCH,
+                                     make_config, packed_dtype)
+    from openpifpaf_amd._lib import call
+    cfg = make_config(**EVAL_CONFIG)
+    sk = constants.COCO_PERSON_SKELETON
+    cif, caf = synthetic.batch('planted', 4, 48, 48, first_seed=3)
+    eng = engine.DecodeEngine()
+    b = eng.launch(torch.from_numpy(cif).cuda(), torch.from_numpy(caf).cuda(), sk, cfg)
+    full, off = eng.fetch_gather(b)
+    full = full.copy()
+    assert off[1] >= 2
+    rows = b.anns.view(b.n * b.cap, ANN_DTYPE.itemsize)
+    tampered = full[:2].copy()
+    tampered[0]['decoding_xyv'][0, 0] += np.float32(1.0)
+    tampered[1]['n_frontier'] = 200  # > 4 * 19
+    rows[:2] = torch.from_numpy(tampered.view(np.uint8).reshape(2, -1)).cuda()
+    dt = packed_dtype(17, 19, PACK_ALL)
+    out = torch.zeros(int(off[-1]) * dt.itemsize, dtype=torch.uint8, device='cuda')
+    cnt = torch.zeros(b.n, dtype=torch.int32, device='cuda')
+    call('pp_pack_compact', _device.ptr(b.anns), _device.ptr(b.counts), b.n, b.cap, 17, 19,
+         ctypes.c_uint32(PACK_ALL), _device.ptr(out), int(off[-1]), _device.ptr(cnt),
+         _device.stream())
+    got = out.cpu().numpy().view(dt)
+    flagged = (got['n_decoding'] & PP_PACK_REFETCH) != 0
+    assert flagged[:2].all() and not flagged[2:].any()
+    recs, _ = eng.fetch_async(b, (17, 19, PACK_ALL)).result()
+    assert recs.dtype == ANN_DTYPE and recs.tobytes() == b''.join(
+        [tampered.tobytes(), full[2:].tobytes()])

@@ -2,7 +2,7 @@
 
 The golden fixtures were produced by running the reference decoder
 (tests/golden/gen_golden.py).  Bit-exact for CifHr, seeds, CafScored and every
-functional primitive; tolerance (golden_util.ATOL/RTOL) for the grow-stage floats.
+functional primitive; tolerance (golden_util: XY_ULPS, ATOL, SCORE_ATOL) for the grow-stage floats.
 """
 import os
 
@@ -129,7 +129,9 @@ def test_decode(name):
     g = gu.load_case(name)
     cif, caf, skeleton = gu.case_inputs(g)
     recs = oracle.decode(cif, caf, skeleton, gu.case_config(g))
-    errs = gu.compare_annotations(g, recs)
+    stats = {}
+    errs = gu.compare_annotations(g, recs, stats=stats)
+    print('max deviation vs reference:', stats)
     assert not errs, errs[:10]
 
 
@@ -253,5 +255,7 @@ def test_oracle_multi_vs_reference(name, mode):
         assert [b.shape[1] for b in bwd] == list(g['caf_%s_bwd_counts' % tag])
         assert [gu.sha(f) for f in fwd] == [str(s) for s in g['caf_%s_fwd_sha' % tag]]
         assert [gu.sha(b) for b in bwd] == [str(s) for s in g['caf_%s_bwd_sha' % tag]]
-    errs = gu.compare_annotations(g, oracle.decode_multi(mem, skel, cfg))
+    stats = {}
+    errs = gu.compare_annotations(g, oracle.decode_multi(mem, skel, cfg), stats=stats)
+    print('max deviation vs reference:', stats)
     assert not errs, errs[:10]
