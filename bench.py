@@ -104,10 +104,20 @@ def spawn_ranks(n):
     return status if status >= 0 else 128 - status
 
 
+def log(msg):
+    print('[bench {:.1f}s] {}'.format(time.perf_counter() - T_START, msg), file=sys.stderr,
+          flush=True)
+
+
+T_START = time.perf_counter()
+
+
 def main():
     args = parse()
     if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
+    import faulthandler
+    faulthandler.enable()
     import torch
     import torch.distributed as dist
 
@@ -215,7 +225,8 @@ def main():
                 counts = pending.wait()
                 if not pending.fits(int(counts.sum())):
                     raise SystemExit('record block too small after warmup')
-                comm.wait_event(pending.done_event)
+                if comm is not None:
+                    comm.wait_event(pending.done_event)
                 src = pending.device_records if rank != 0 else pending.host_records()
                 if comm_dev.type == 'cpu':
                     src = src[:int(counts.sum()) * pending.dtype.itemsize].cpu()
@@ -262,7 +273,9 @@ def main():
             elapsed = float(t.item())
         return elapsed, stage_ms / steps, n_anns
 
+    log('rank {}/{}: {} on {}'.format(rank, world, args.workload, dev))
     elapsed, stage_avg, n_anns = timed_run(cif, caf, args.steps, args.warmup)
+    log('main workload done')
 
     images = batch * world * args.steps
     value = images / elapsed
@@ -292,8 +305,10 @@ def main():
             'workload': '{}: {} images/GPU at {}x{}, 17 CIF / {} CAF, full CifCaf decode, {} '
                         'defaults'.format(args.workload, batch, h, w, len(skeleton), args.mode),
             'global_batch': batch * world,
-            'parallelism': 'image-sharded dp{} (compact records gathered to rank 0, RCCL '
-                           'send/recv)'.format(world) if world > 1 else 'single GPU',
+            'parallelism': 'image-sharded dp{} (compact records gathered to rank 0, {} '
+                           'send/recv)'.format(world, 'RCCL' if args.backend == 'nccl' else
+                                               'gloo rehearsal, ranks sharing GPUs')
+                           if world > 1 else 'single GPU',
         },
         # the hand-over format: compact records (pp_pack_compact) instead of 1544-byte pp_ann
         'records': {
@@ -341,6 +356,7 @@ def main():
         ucif, ucaf = torch.from_numpy(ucif).to(dev), torch.from_numpy(ucaf).to(dev)
         u_steps = max(3, args.steps // 2)
         u_el, u_stage, u_anns = timed_run(ucif, ucaf, u_steps, 2)
+        log('uniform done')
         line['uniform'] = {
             'value': round(batch * u_steps / u_el, 1), 'unit': 'images/s',
             'ms_per_step': round(1e3 * u_el / u_steps, 4),
@@ -372,10 +388,12 @@ def main():
                 'annotations_per_image': round(m_anns / (m_steps * n_img), 3),
             }
             del heads, fields
+            log('multi {} done'.format(name))
     if default_run and world == 1 and not args.no_configs:
         # configs[1] (cfg2): batch-1 CifHr + seeds latency, host wall clock per call
         # (launch overhead + one synchronisation) and device time
         line['cfg2'] = {g: cfg2_latency(g, cfg, dev) for g in ('planted', 'uniform')}
+        log('cfg2 done')
         # configs[4] (cfg5): 160x160, dense 44-CAF skeleton, 64 images per GPU
         w5 = WORKLOADS['cfg5']
         line['cfg5'] = {}
@@ -395,6 +413,7 @@ def main():
                 'annotations_per_image': round(an5 / (s5 * w5['batch']), 3),
             }
             del c5, a5
+            log('cfg5 {} done'.format(g))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line['cpu_baseline'] = cpu_baseline(cif_h, caf_h, skeleton, cfg, args.cpu_seconds)
     if rank == 0:

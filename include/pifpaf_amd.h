@@ -381,11 +381,13 @@ int pp_pack_records(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img
  *   8   i32 image
  *   12  u16 n_decoding | PP_PACK_REFETCH (bit 15), 14 u16 n_frontier
  *   16  f32 data[K][3], f32 joint_scales[K]                       annotation.py:17-18
- *   PP_PACK_DECODING: u8 decoding_pairs[K][2] (padded to 4 B), f32 decoding_v[K][2]: the
- *       (jsi, jti) pairs of decoding_order (cifcaf.py:305-306) and v of xyv_jsi / xyv_jti;
- *       their x / y are data[jsi][0:2] / data[jti][0:2] (checked on the device)
+ *   PP_PACK_DECODING: u8 decoding_pairs[K][2] (padded to 4 B), f32 decoding_v[K][2],
+ *       f32 decoding_xy[K][2]: the (jsi, jti) pairs of decoding_order (cifcaf.py:305-306),
+ *       v of xyv_jsi / xyv_jti, and per joint the x / y it had when it entered the order:
+ *       xyv_jsi = (decoding_xy[jsi], v[0]), xyv_jti = (decoding_xy[jti], v[1]) (checked on
+ *       the device for every entry)
  *   PP_PACK_FRONTIER: u8 frontier_pairs[F][2] (padded to 4 B), F = min(PP_MAX_FRONTIER, 4*C)
- * A record whose decoding entries do not satisfy the x / y identity, or whose orders exceed
+ * A record whose decoding entries disagree with the per-joint x / y, or whose orders exceed
  * K / F entries, carries PP_PACK_REFETCH: fetch that decode's full pp_ann records instead.
  * `out` (16-byte aligned) holds out_capacity records; device or pinned host memory as for
  * pp_pack_records.  Reference consumer: Generator.batch's per-image lists

@@ -51,10 +51,10 @@ def packed_dtype(k, c, flags=PACK_ALL):
     offsets = [0, 8, 12, 14, 16, 16 + 12 * k]
     o = 16 + 16 * k
     if flags & PP_PACK_DECODING:
-        names += ['decoding_pairs', 'decoding_v']
-        formats += [('u1', (k, 2)), ('<f4', (k, 2))]
-        offsets += [o, o + _up(2 * k, 4)]
-        o += _up(2 * k, 4) + 8 * k
+        names += ['decoding_pairs', 'decoding_v', 'decoding_xy']
+        formats += [('u1', (k, 2)), ('<f4', (k, 2)), ('<f4', (k, 2))]
+        offsets += [o, o + _up(2 * k, 4), o + _up(2 * k, 4) + 8 * k]
+        o += _up(2 * k, 4) + 16 * k
     if flags & PP_PACK_FRONTIER:
         names.append('frontier_pairs')
         formats.append(('u1', (f, 2)))

@@ -45,9 +45,9 @@ class Annotation:
 
     @classmethod
     def from_packed(cls, rec, keypoints, skeleton):
-        """Build from one compact record (pp_pack_compact, include/pifpaf_amd.h): the
-        decoding_order coordinates are the data rows of the entry's joints, its v values
-        come with the record."""
+        """Build from one compact record (pp_pack_compact, include/pifpaf_amd.h): each
+        decoding_order entry is (jsi, jti, (x, y of jsi, v), (x, y of jti, v)) from the
+        per-joint coordinates and the entry's two v values."""
         k = len(keypoints)
         ann = cls(keypoints, skeleton)
         ann.data = np.array(rec['data'][:k], dtype=np.float32)
@@ -55,12 +55,12 @@ class Annotation:
         names = rec.dtype.names
         if 'decoding_pairs' in names:
             nd = int(rec['n_decoding']) & 0x7fff
-            pairs, dv = rec['decoding_pairs'], rec['decoding_v']
+            pairs, dv, dxy = rec['decoding_pairs'], rec['decoding_v'], rec['decoding_xy']
             order = []
             for t in range(nd):
                 js, jt = int(pairs[t, 0]), int(pairs[t, 1])
-                a, b = ann.data[js].copy(), ann.data[jt].copy()
-                a[2], b[2] = dv[t, 0], dv[t, 1]
+                a = np.array([dxy[js, 0], dxy[js, 1], dv[t, 0]], dtype=np.float32)
+                b = np.array([dxy[jt, 0], dxy[jt, 1], dv[t, 1]], dtype=np.float32)
                 order.append((js, jt, a, b))
             ann.decoding_order = order
         if 'frontier_pairs' in names:

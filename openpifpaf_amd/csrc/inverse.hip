@@ -167,15 +167,17 @@ __global__ __launch_bounds__(256) void pack_records_kernel(const pp_ann *__restr
 
 // -------------------------------------------------------------------------------------
 // compact records (pp_pack_compact): a pp_ann cut to K keypoints and the skeleton's frontier
-// bound, for the PCIe hand-over and the multi-GPU gather.  decoding_order keeps the pairs
-// and the two v of each entry; x / y of an entry equal the final data rows of its joints
-// (set once by _grow, cifcaf.py:300-306, and moved together by every later transform),
-// which the kernel checks bit for bit.  A record where that does not hold, or whose
-// orders exceed the compact bounds, is flagged PP_PACK_REFETCH for a full-record fetch.
+// bound, for the PCIe hand-over and the multi-GPU gather.  decoding_order keeps the pairs,
+// the two v of each entry and, once per joint, the x / y the joint had when it entered the
+// order (set once by _grow, cifcaf.py:300-306; nms.Keypoints may zero the data row later,
+// nms.py:22, so the data rows cannot stand in for them).  The kernel checks that every
+// entry's coordinates equal its joints' recorded x / y bit for bit; a record where that does
+// not hold, or whose orders exceed the compact bounds, is flagged PP_PACK_REFETCH for a
+// full-record fetch.
 // -------------------------------------------------------------------------------------
 struct PackLayout {
     int K, F, dec, front;
-    int off_data, off_scales, off_pairs, off_decv, off_front, size;
+    int off_data, off_scales, off_pairs, off_decv, off_decxy, off_front, size;
 };
 
 __host__ __device__ inline PackLayout pack_layout(int K, int C, uint32_t flags) {
@@ -193,15 +195,18 @@ __host__ __device__ inline PackLayout pack_layout(int K, int C, uint32_t flags) 
     if (L.dec) o += (2 * K + 3) / 4 * 4;
     L.off_decv = o;
     if (L.dec) o += 8 * K;
+    L.off_decxy = o;
+    if (L.dec) o += 8 * K;
     L.off_front = o;
     if (L.front) o += (2 * L.F + 3) / 4 * 4;
     L.size = (o + 15) / 16 * 16;
     return L;
 }
 
-// 4-byte word i of the compact record of `a` (w3 = the count word)
+// 4-byte word i of the compact record of `a` (w3 = the count word; jxy = the wave's LDS
+// copy of the recorded joint coordinates)
 __device__ __forceinline__ uint32_t packed_word(const pp_ann &a, const PackLayout &L, int i,
-                                                uint32_t w3) {
+                                                uint32_t w3, const float *jxy) {
     const uint32_t *s = reinterpret_cast<const uint32_t *>(&a);
     const int b = 4 * i;
     if (i < 2) return s[offsetof(pp_ann, score) / 4 + i];
@@ -216,9 +221,12 @@ __device__ __forceinline__ uint32_t packed_word(const pp_ann &a, const PackLayou
         const int keep = min(max(2 * nd - q, 0), 4);
         return keep == 4 ? w : (w & ((1u << (8 * keep)) - 1u));
     }
-    if (b < L.off_front) {  // (v of the source joint, v of the target joint) per entry
+    if (b < L.off_decxy) {  // (v of the source joint, v of the target joint) per entry
         const int t = (b - L.off_decv) / 4, e = t >> 1;
         return e < nd ? __float_as_uint(a.decoding_xyv[e][2 + 3 * (t & 1)]) : 0u;
+    }
+    if (b < L.off_front) {  // (x, y) per joint as it entered decoding_order
+        return __float_as_uint(jxy[(b - L.off_decxy) / 4]);
     }
     if (b < L.off_front + (2 * L.F + 3) / 4 * 4 && L.front) {
         const int q = b - L.off_front;
@@ -237,6 +245,7 @@ __global__ __launch_bounds__(256) void pack_compact_kernel(const pp_ann *__restr
                                                            int cap, PackLayout L, char *out,
                                                            int64_t out_cap, int *out_counts) {
     __shared__ int s_off;
+    __shared__ float s_jxy[4][2 * PP_MAX_KP];
     const int img = blockIdx.x;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (threadIdx.x == 0) s_off = 0;
@@ -252,33 +261,57 @@ __global__ __launch_bounds__(256) void pack_compact_kernel(const pp_ann *__restr
     const int chunks = L.size / 16;
     for (int r = wave; r < fit; r += 4) {
         const pp_ann &a = anns[(int64_t)img * cap + r];
-        // compact-form check: entry e's x / y equal the data rows of its joints
+        // compact form: lane j records joint j's x / y at its first appearance in
+        // decoding_order; every entry must agree with its joints' records
         const int nd = a.n_decoding, nf = a.n_frontier;
+        const int ndc = min(max(nd, 0), L.K);
         bool bad = (L.dec && nd > L.K) || (L.front && nf > L.F) || nd < 0 || nf < 0;
-        if (L.dec && lane < min(nd, L.K)) {
-            const int js = a.decoding_pairs[lane][0], jt = a.decoding_pairs[lane][1];
-            if (js >= L.K || jt >= L.K) {
-                bad = true;
-            } else {
+        float jx = 0.0f, jy = 0.0f;
+        if (L.dec) {
+            bool found = false;
+            for (int e = 0; e < ndc; e++) {  // wave-uniform walk, nd <= K entries
+                const int js = a.decoding_pairs[e][0], jt = a.decoding_pairs[e][1];
+                if (!found && (js == lane || jt == lane)) {
+                    const int h = js == lane ? 0 : 3;
+                    jx = a.decoding_xyv[e][h];
+                    jy = a.decoding_xyv[e][h + 1];
+                    found = true;
+                }
+            }
+            int js = 0, jt = 0;
+            if (lane < ndc) {
+                js = a.decoding_pairs[lane][0];
+                jt = a.decoding_pairs[lane][1];
+                bad |= js >= L.K || jt >= L.K;
+            }
+            const float sx = __shfl(jx, js), sy = __shfl(jy, js);
+            const float tx = __shfl(jx, jt), ty = __shfl(jy, jt);
+            if (lane < ndc) {
                 const float *x = a.decoding_xyv[lane];
-                bad |= __float_as_uint(x[0]) != __float_as_uint(a.data[js][0]) ||
-                       __float_as_uint(x[1]) != __float_as_uint(a.data[js][1]) ||
-                       __float_as_uint(x[3]) != __float_as_uint(a.data[jt][0]) ||
-                       __float_as_uint(x[4]) != __float_as_uint(a.data[jt][1]);
+                bad |= __float_as_uint(x[0]) != __float_as_uint(sx) ||
+                       __float_as_uint(x[1]) != __float_as_uint(sy) ||
+                       __float_as_uint(x[3]) != __float_as_uint(tx) ||
+                       __float_as_uint(x[4]) != __float_as_uint(ty);
             }
         }
         bad = __ballot(bad) != 0ull;
+        if (lane < L.K) {
+            s_jxy[wave][2 * lane] = jx;
+            s_jxy[wave][2 * lane + 1] = jy;
+        }
+        wave_sync();
         const uint32_t w3 = (uint32_t)(L.dec ? min(nd, L.K) : 0) | (bad ? PP_PACK_REFETCH : 0u) |
                             ((uint32_t)(L.front ? min(nf, L.F) : 0) << 16);
         uint4 *dst = reinterpret_cast<uint4 *>(out + (off + r) * (int64_t)L.size);
         for (int c = lane; c < chunks; c += 64) {
             uint4 v;
-            v.x = packed_word(a, L, 4 * c, w3);
-            v.y = packed_word(a, L, 4 * c + 1, w3);
-            v.z = packed_word(a, L, 4 * c + 2, w3);
-            v.w = packed_word(a, L, 4 * c + 3, w3);
+            v.x = packed_word(a, L, 4 * c, w3, s_jxy[wave]);
+            v.y = packed_word(a, L, 4 * c + 1, w3, s_jxy[wave]);
+            v.z = packed_word(a, L, 4 * c + 2, w3, s_jxy[wave]);
+            v.w = packed_word(a, L, 4 * c + 3, w3, s_jxy[wave]);
             dst[c] = v;
         }
+        wave_sync();  // s_jxy is rewritten for the wave's next record
     }
 }
 

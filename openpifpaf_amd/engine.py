@@ -217,44 +217,50 @@ class DecodeEngine:
         pp_pack_compact's compact records (include/pifpaf_amd.h); None the full pp_ann
         records (pp_pack_records).  `device_out` packs the records into a device buffer
         instead (the multi-GPU gather sends them from there); the counts still land in
-        pinned host memory.  The block is sized from the largest batch seen so far; a batch
-        that outgrows it, or a compact record flagged PP_PACK_REFETCH, is fetched again as
-        full records (`capacity` = records to reserve at least).  The slot stays valid
-        until the second decode after this one, so a caller may launch the next decode
-        before calling result()."""
+        pinned host memory.  The block is sized from the largest batch seen so far
+        (`capacity` = records to reserve at least); result() re-packs a batch that outgrew
+        it, and fetches full records when a compact record is flagged PP_PACK_REFETCH.  The
+        slot stays valid until the second decode after this one, so a caller may launch the
+        next decode before calling result()."""
+        est = max(getattr(b, 'pack_cap', 0), 16 * b.n, capacity)
+        decoded = torch.cuda.Event()
+        decoded.record()
+        p = DecodeEngine._pack(b, b.anns, b.counts, b.status, compact, device_out, est, decoded)
+        b._free[b._cur] = p.done_event
+        return p
+
+    @staticmethod
+    def _pack(b, anns, counts, status, compact, device_out, est, after):
         n = b.n
         dtype = ANN_DTYPE if compact is None else packed_dtype(*compact)
         width = dtype.itemsize
-        est = max(getattr(b, 'pack_cap', 0), 16 * n, capacity)
         head = -(-8 * n // 256) * 256  # counts (n int32), then the slot's status (n int32)
         host = torch.empty(head + (0 if device_out else est * width), dtype=torch.uint8,
                            pin_memory=True)
-        dev = (torch.empty(est * width, dtype=torch.uint8, device=b.anns.device)
+        dev = (torch.empty(est * width, dtype=torch.uint8, device=anns.device)
                if device_out else None)
         out_ptr = dev.data_ptr() if device_out else host.data_ptr() + head
         # the pack runs on a side stream after the decode, so its PCIe writes overlap the
         # next decode; the slot is not rewritten before it is done (DecodeBuffers.next_slot)
-        decoded = torch.cuda.Event()
-        decoded.record()
-        side = DecodeEngine._pack_stream(b.anns.device)
-        side.wait_event(decoded)
+        side = DecodeEngine._pack_stream(anns.device)
+        side.wait_event(after)
         with torch.cuda.stream(side):
             if compact is None:
-                call('pp_pack_records', _device.ptr(b.anns), _device.ptr(b.counts), n, b.cap,
+                call('pp_pack_records', _device.ptr(anns), _device.ptr(counts), n, b.cap,
                      ctypes.c_void_p(out_ptr), est, ctypes.c_void_p(host.data_ptr()),
                      _device.stream())
             else:
                 k, c, flags = compact
-                call('pp_pack_compact', _device.ptr(b.anns), _device.ptr(b.counts), n, b.cap,
+                call('pp_pack_compact', _device.ptr(anns), _device.ptr(counts), n, b.cap,
                      k, c, ctypes.c_uint32(flags), ctypes.c_void_p(out_ptr), est,
                      ctypes.c_void_p(host.data_ptr()), _device.stream())
-            host[4 * n:8 * n].copy_(b.status.view(torch.uint8), non_blocking=True)
+            host[4 * n:8 * n].copy_(status.view(torch.uint8), non_blocking=True)
             done = torch.cuda.Event()
             done.record()
             if dev is not None:
                 dev.record_stream(side)
-        b._free[b._cur] = done
-        return PendingRecords(b, b.anns, b.counts, host, head, est, done, dtype, dev)
+        return PendingRecords(b, (anns, counts, status), host, head, est, done, dtype, dev,
+                              compact, device_out)
 
     _pack_streams = {}
 
@@ -290,10 +296,12 @@ class DecodeEngine:
 class PendingRecords:
     """A record fetch enqueued by DecodeEngine.fetch_async."""
 
-    def __init__(self, b, anns, counts, host, head, est, done, dtype, dev=None):
-        self._b, self._anns, self._counts = b, anns, counts
+    def __init__(self, b, slot, host, head, est, done, dtype, dev=None, compact=None,
+                 device_out=False):
+        self._b, self._slot = b, slot
         self._host, self._head, self._est, self._done = host, head, est, done
         self.dtype, self.device_records = dtype, dev
+        self._compact, self._device_out = compact, device_out
         self._waited = False
 
     def __del__(self):
@@ -336,9 +344,12 @@ class PendingRecords:
         counts = self.wait()
         offsets = np.concatenate([[0], np.cumsum(counts)])
         total = int(offsets[-1])
-        if total > self._est:
+        if total > self._est:  # outgrew the block: pack again into one that fits
             self._b.pack_cap = 2 * total
-            return DecodeEngine.fetch_gather(self._b, self._anns, self._counts)
+            after = torch.cuda.Event()
+            after.record(DecodeEngine._pack_stream(self._slot[0].device))
+            return DecodeEngine._pack(self._b, *self._slot, self._compact, self._device_out,
+                                      2 * total, after).result()
         if self.device_records is not None:
             host = torch.empty(total * width, dtype=torch.uint8, pin_memory=True)
             host.copy_(self.device_records[:total * width])
@@ -346,7 +357,7 @@ class PendingRecords:
         else:
             recs = self._host[self._head:self._head + total * width].numpy().view(self.dtype)
         if needs_refetch(recs):
-            return DecodeEngine.fetch_gather(self._b, self._anns, self._counts)
+            return DecodeEngine.fetch_gather(self._b, self._slot[0], self._slot[1])
         return recs, offsets
 
 
