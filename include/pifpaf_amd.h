@@ -294,12 +294,14 @@ int pp_cifdet_hr(const float *d_det, int32_t n_img, int32_t K, int32_t H, int32_
                  void *stream);
 /* nms.Detection.annotations (nms.py:79-102) over caller records: n_img groups, d_in
  * (n_img, capacity) with d_counts[i] records (field, score, bbox) in list order.  Output
- * as pp_cifdet_decode; d_out_index (optional) = input index of each output record. */
+ * as pp_cifdet_decode; d_out_index (optional) = input index of each output record;
+ * d_scores_out (optional, (n_img, capacity)) = every input record's score after the
+ * reference's in-place edits (soft suppression; nms.py:90-99), in input order. */
 size_t pp_nms_detection_workspace_size(int32_t n_img, int32_t capacity);
 int pp_nms_detection(const pp_det *d_in, const int32_t *d_counts, int32_t n_img, int32_t capacity,
                      const pp_det_nms *nms, pp_det *d_out, int32_t *d_out_counts,
-                     int32_t *d_out_index, void *d_workspace, size_t workspace_bytes,
-                     void *stream);
+                     int32_t *d_out_index, float *d_scores_out, void *d_workspace,
+                     size_t workspace_bytes, void *stream);
 /* CifDetSeeds.fill_cif (cif_seeds.py:67-90) per (image, field), in cell order:
  * d_seg (n_img, K, 5, H*W) = v, x, y, w, h of the first d_seg_counts[i, f] entries;
  * d_cifhr (n_img, K, H', pitch).  get() = sorted((v, f, x, y, w, h), reverse=True). */
@@ -463,6 +465,20 @@ int pp_scalar_values(const float *d_field, int64_t h, int64_t w, int64_t pitch,
 int pp_scalar_lookup(const void *d_field, int64_t h, int64_t w, int64_t pitch, int32_t mode,
                      const float *d_x, const float *d_y, int64_t n, float default_value,
                      float reduction, void *d_out, void *stream);
+/*
+ * Occupancy.set (decoder/occupancy.py:36-44) with scalar_square_add_single
+ * (decoder/utils.py:61-66) for n marks, in order: plane d_f[i] of d_occ (n_planes, h, w) u8
+ * with row pitch `pitch` gets += 1 (wrapping) on the box of half-width
+ * round(max(min_scale_reduced, sigma / reduction)) around (round(x / reduction),
+ * round(y / reduction)); f32 division, round half to even, NumPy slice clipping.  Marks
+ * with d_f[i] outside [0, n_planes) are skipped, as the reference's early return; marks
+ * with non-finite coordinates are skipped (the reference's round() raises).  Occupancy.get
+ * is pp_scalar_lookup mode 4.
+ */
+int pp_occupancy_set(uint8_t *d_occ, int32_t n_planes, int64_t h, int64_t w, int64_t pitch,
+                     const int32_t *d_f, const float *d_x, const float *d_y, const float *d_sigma,
+                     int64_t n, float reduction, float min_scale_reduced, void *stream);
+
 /*
  * Column filters over a (rows, n) field with row pitch `pitch` (functional.pyx:214-228,
  * 289-359), order preserving.  mode: 0 caf_center_s, 1 paf_center, 2 paf_center_b,

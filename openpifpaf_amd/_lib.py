@@ -81,12 +81,15 @@ _SIGNATURES = {
     'pp_cifdet_hr': ([_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _sz, _vp], ctypes.c_int),
     'pp_cifdet_seeds': ([_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp], ctypes.c_int),
     'pp_nms_detection_workspace_size': ([_i32, _i32], _sz),
-    'pp_nms_detection': ([_vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _sz, _vp], ctypes.c_int),
+    'pp_nms_detection': ([_vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp],
+                         ctypes.c_int),
     'pp_cifdet_workspace_size': ([_i32, _i32, _i32, _i32, _vp, _i32], _sz),
     'pp_cifdet_decode': ([_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp,
                           _sz, _vp], ctypes.c_int),
     'pp_fields_from_conv': ([_vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp], ctypes.c_int),
     'pp_nms_keypoints': ([_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _sz, _vp],
+                         ctypes.c_int),
+    'pp_occupancy_set': ([_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _f, _f, _vp],
                          ctypes.c_int),
     'pp_center_filter': ([_vp, _i64, _i64, _i64, _i32, _f, _f, _f, _vp, _i64, _vp, _vp],
                          ctypes.c_int),

@@ -428,7 +428,7 @@ __global__ __launch_bounds__(256) void det_output_kernel(DetArgs a) {
 
 // standalone nms.Detection over caller records (input order = list order)
 __global__ __launch_bounds__(256) void det_nms_kernel(DetArgs a, const pp_det *in, const int *in_n,
-                                                      int *out_index) {
+                                                      int *out_index, float *scores_out) {
     const int img = blockIdx.x;
     const int n = min(max(in_n[img], 0), a.cap);
     float *cand = a.cand + (int64_t)img * a.cap * kCand;
@@ -452,6 +452,11 @@ __global__ __launch_bounds__(256) void det_nms_kernel(DetArgs a, const pp_det *i
     const int m = det_nms_output(a, img, cand, perm, perm2, order, n, a.out + (int64_t)img * a.cap,
                                  out_index ? out_index + (int64_t)img * a.cap : nullptr);
     if (threadIdx.x == 0) a.counts[img] = m;
+    if (scores_out) {  // every input's score after the in-place edits (nms.py:90-99)
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += blockDim.x)
+            scores_out[(int64_t)img * a.cap + i] = cand[kCand * i + 7];
+    }
 }
 
 static inline size_t align_up(size_t v) { return (v + 255) / 256 * 256; }
@@ -545,8 +550,8 @@ size_t pp_nms_detection_workspace_size(int32_t n_img, int32_t capacity) {
 
 int pp_nms_detection(const pp_det *d_in, const int32_t *d_counts, int32_t n_img, int32_t capacity,
                      const pp_det_nms *nms, pp_det *d_out, int32_t *d_out_counts,
-                     int32_t *d_out_index, void *d_workspace, size_t workspace_bytes,
-                     void *stream) {
+                     int32_t *d_out_index, float *d_scores_out, void *d_workspace,
+                     size_t workspace_bytes, void *stream) {
     if (!d_in || !d_counts || !nms || !d_out || !d_out_counts || !d_workspace)
         return fail(PP_EINVAL, "pp_nms_detection: NULL argument");
     if (n_img < 0 || capacity <= 0) return fail(PP_ESHAPE, "pp_nms_detection: bad shape");
@@ -563,7 +568,7 @@ int pp_nms_detection(const pp_det *d_in, const int32_t *d_counts, int32_t n_img,
     a.out = d_out;
     a.counts = d_out_counts;
     hipLaunchKernelGGL(det_nms_kernel, dim3((unsigned)n_img), dim3(256), 0, (hipStream_t)stream, a,
-                       d_in, d_counts, d_out_index);
+                       d_in, d_counts, d_out_index, d_scores_out);
     return check_launch("pp_nms_detection");
 }
 

@@ -117,7 +117,54 @@ __global__ void weiszfeld_kernel(const float *__restrict__ x, int64_t n, int64_t
 
 using namespace pp;
 
+// Occupancy.set (occupancy.py:36-44) + scalar_square_add_single (decoder/utils.py:61-66),
+// marks applied in order by one workgroup: lanes cover one mark's box, a barrier between
+// marks.  u8 += 1 wraps as NumPy's in-place add.
+__global__ __launch_bounds__(256) void occupancy_set_kernel(uint8_t *occ, int n_planes, int64_t h,
+                                                            int64_t w, int64_t pitch,
+                                                            const int *fs, const float *xs,
+                                                            const float *ys, const float *sig,
+                                                            int64_t n, float r, float msr) {
+    for (int64_t i = 0; i < n; i++) {
+        const int f = fs[i];
+        const float x = xs[i], y = ys[i], s = sig[i];
+        // round(x / reduction) etc.: float32 scalar division (NEP 50), half-to-even rounding;
+        // Python's max(min_scale_reduced, s) keeps the first argument unless s is larger
+        const float xr = x / r, yr = y / r, sr = s / r;
+        const float sm = sr > msr ? sr : msr;
+        const bool ok = f >= 0 && f < n_planes && fabsf(xr) < 0x1p60f && fabsf(yr) < 0x1p60f &&
+                        fabsf(sm) < 0x1p60f;  // NaN / inf: the reference's round() raises
+        if (ok) {
+            const int64_t xi = (int64_t)rintf(xr), yi = (int64_t)rintf(yr), si = (int64_t)rintf(sm);
+            const int64_t minx = max((int64_t)0, xi - si), miny = max((int64_t)0, yi - si);
+            const int64_t maxx = min(max(minx + 1, min(w, xi + si + 1)), w);
+            const int64_t maxy = min(max(miny + 1, min(h, yi + si + 1)), h);
+            const int64_t bw = maxx - minx, cells = bw > 0 && maxy > miny ? bw * (maxy - miny) : 0;
+            uint8_t *plane = occ + (int64_t)f * h * pitch;
+            for (int64_t c = threadIdx.x; c < cells; c += 256) {
+                uint8_t *p = plane + (miny + c / bw) * pitch + minx + c % bw;
+                *p = (uint8_t)(*p + 1);
+            }
+        }
+        __syncthreads();
+    }
+}
+
 extern "C" {
+
+int pp_occupancy_set(uint8_t *d_occ, int32_t n_planes, int64_t h, int64_t w, int64_t pitch,
+                     const int32_t *d_f, const float *d_x, const float *d_y, const float *d_sigma,
+                     int64_t n, float reduction, float min_scale_reduced, void *stream) {
+    if (!d_occ || (n > 0 && (!d_f || !d_x || !d_y || !d_sigma)))
+        return fail(PP_EINVAL, "pp_occupancy_set: NULL argument");
+    if (n_planes < 0 || h < 0 || w < 0 || pitch < w || n < 0 || !(reduction > 0.0f))
+        return fail(PP_ESHAPE, "pp_occupancy_set: bad shape");
+    if (n == 0 || h == 0 || w == 0) return PP_OK;
+    hipLaunchKernelGGL(occupancy_set_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, d_occ,
+                       n_planes, h, w, pitch, d_f, d_x, d_y, d_sigma, n, reduction,
+                       min_scale_reduced);
+    return check_launch("pp_occupancy_set");
+}
 
 int pp_scalar_values(const float *d_field, int64_t h, int64_t w, int64_t pitch, const float *d_x,
                      const float *d_y, int64_t n, float default_value, float *d_out, void *stream) {

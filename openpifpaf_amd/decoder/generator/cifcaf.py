@@ -134,6 +134,14 @@ class CifCaf(Generator):
                         for r in recs[offsets[i]:offsets[i + 1]]])
         return out
 
+    def decode_heads(self, heads):
+        """Generator.batch: the model's head list (each (B, ...)) through the FieldConfig."""
+        if self.field_config.is_single_scale():
+            cif_i, caf_i, _ = self.field_config.single_scale()
+            return self.decode_batch(heads[cif_i], heads[caf_i])
+        used = set(self.field_config.cif_indices) | set(self.field_config.caf_indices)
+        return self.decode_fields_batch([h if i in used else None for i, h in enumerate(heads)])
+
     def decode_batch(self, cif_batch, caf_batch):
         """(B, K, 5, H, W) + (B, C, 9, H, W) -> one list of Annotation per image."""
         recs, offsets, _ = self.decode_records(cif_batch, caf_batch, compact=PACK_ALL)

@@ -84,6 +84,11 @@ class CifDet(Generator):
         return [[AnnotationDet.from_record(r, self.categories)
                  for r in recs[offsets[i]:offsets[i + 1]]] for i in range(len(offsets) - 1)]
 
+    def decode_heads(self, heads):
+        """Generator.batch: the model's head list (each (B, ...)); reads the CifDet head."""
+        cif_i, _, _ = self.field_config.single_scale()
+        return self.decode_batch(heads[cif_i])
+
     def __call__(self, fields):
         cif_i, _, _ = self.field_config.single_scale()
         return self.decode_batch(_device.to_device(fields[cif_i])[None])[0]

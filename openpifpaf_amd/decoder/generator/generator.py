@@ -43,16 +43,20 @@ class Generator:
     def __call__(self, fields, *, initial_annotations=None):
         raise NotImplementedError()
 
-    def decode_batch(self, *heads):
+    def decode_heads(self, heads):
+        """Every head output of a batch (the model's list, each (B, ...)) -> one list of
+        annotations per image; the subclass reads the heads its FieldConfig names."""
         raise NotImplementedError()
 
     def batch(self, model, image_batch, *, device=None):
-        """From image batch straight to annotations batch (generator.py:84-101)."""
+        """From image batch straight to annotations batch (generator.py:84-101): the head
+        list of any FieldConfig (single-scale, dense connections, multi-scale) is decoded
+        as one device batch instead of per image over a worker pool."""
         start_nn = time.perf_counter()
         heads = self.fields_batch(model, image_batch, device=device)
         self.last_nn_time = time.perf_counter() - start_nn
         start = time.perf_counter()
-        result = self.decode_batch(*heads)
+        result = self.decode_heads(heads)
         self.last_decoder_time = time.perf_counter() - start
         LOG.debug('time: nn = %.3fs, dec = %.3fs', self.last_nn_time, self.last_decoder_time)
         return result

@@ -109,18 +109,18 @@ class Detection:
         d_counts = torch.tensor([n], dtype=torch.int32, device=dev)
         d_out_counts = torch.empty(1, dtype=torch.int32, device=dev)
         d_out_index = torch.empty(n, dtype=torch.int32, device=dev)
+        d_scores = torch.empty(n, dtype=torch.float32, device=dev)
         ws = torch.empty(int(load().pp_nms_detection_workspace_size(1, n)), dtype=torch.uint8,
                          device=dev)
         z = self.config()
         call('pp_nms_detection', _device.ptr(d_in), _device.ptr(d_counts), 1, n,
              ctypes.byref(z), _device.ptr(d_out), _device.ptr(d_out_counts),
-             _device.ptr(d_out_index), _device.ptr(ws), ctypes.c_size_t(ws.numel()),
-             _device.stream())
+             _device.ptr(d_out_index), _device.ptr(d_scores), _device.ptr(ws),
+             ctypes.c_size_t(ws.numel()), _device.stream())
         m = int(d_out_counts.cpu().item())
         order = d_out_index[:m].cpu().numpy()
-        # the reference edits every annotation's score in place: the kernel's candidate
-        # scratch (workspace head, 10 floats per input, score at 7) holds them all
-        scores = ws[:n * 40].view(torch.float32).reshape(n, 10)[:, 7].cpu().numpy()
+        # the reference edits every annotation's score in place (nms.py:90-99)
+        scores = d_scores.cpu().numpy()
         for ann, sc in zip(anns, scores):
             if ann.score >= self.instance_threshold:
                 ann.score = np.float32(sc)

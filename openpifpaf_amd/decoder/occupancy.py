@@ -1,18 +1,20 @@
-"""Occupancy grid (occupancy.py:10-47).  The decoder's own occupancy lives inside the
-device grow kernel (csrc/grow.hip); this class keeps the reference API for callers that
-use it directly."""
+"""Occupancy grid (decoder/occupancy.py:10-47) held in device memory.
+
+The decoder's own occupancy lives inside the seed-loop kernel (csrc/grow.hip).  This class
+serves callers of the reference API: the grid is a (fields, H / r, W / r) u8 device tensor,
+`set` marks boxes with pp_occupancy_set (decoder/utils.py:61-66 semantics: the box around
+the rounded reduced position, u8 add that wraps) and `get` reads with
+scalar_nonzero_clipped_with_reduction (pp_scalar_lookup).  `mark` takes arrays of marks in
+one launch.
+"""
+import ctypes
+
 import numpy as np
+import torch
 
+from .. import _device
+from .._lib import call
 from ..functional import scalar_nonzero_clipped_with_reduction
-
-
-def scalar_square_add_single(field, x, y, sigma, value):
-    """decoder/utils.py:61-66"""
-    minx = max(0, int(x - sigma))
-    miny = max(0, int(y - sigma))
-    maxx = max(minx + 1, min(field.shape[1], int(x + sigma) + 1))
-    maxy = max(miny + 1, min(field.shape[0], int(y + sigma) + 1))
-    field[miny:maxy, minx:maxx] += value
 
 
 class Occupancy():
@@ -24,20 +26,28 @@ class Occupancy():
         self.reduction = reduction
         self.min_scale = min_scale
         self.min_scale_reduced = min_scale / reduction
-        self.occupancy = np.zeros((shape[0], int(shape[1] / reduction),
-                                   int(shape[2] / reduction)), dtype=np.uint8)
+        grid = (shape[0], int(shape[1] / reduction), int(shape[2] / reduction))
+        self.occupancy = torch.zeros(grid, dtype=torch.uint8, device=_device.require())
 
     def __len__(self):
         return len(self.occupancy)
 
+    def mark(self, fields, xs, ys, sigmas):
+        """Occupancy.set for every (f, x, y, sigma), in order, in one device launch."""
+        f = torch.as_tensor(np.asarray(fields, np.int32), device=self.occupancy.device)
+        pts = [torch.as_tensor(np.asarray(a, np.float32), device=self.occupancy.device)
+               for a in (xs, ys, sigmas)]
+        _, h, w = self.occupancy.shape
+        call('pp_occupancy_set', _device.ptr(self.occupancy), len(self.occupancy), h, w, w,
+             _device.ptr(f), *[_device.ptr(t) for t in pts], ctypes.c_int64(len(f)),
+             ctypes.c_float(self.reduction), ctypes.c_float(self.min_scale_reduced),
+             _device.stream())
+
     def set(self, f, x, y, sigma):
-        """Mark a box centred at the rounded (x, y) (u8 += 1, wraps)."""
+        """Setting is centered at the rounded (x, y) (u8 += 1 on the box, wrapping)."""
         if f >= len(self.occupancy):
             return
-        xi = round(x / self.reduction)
-        yi = round(y / self.reduction)
-        si = round(max(self.min_scale_reduced, sigma / self.reduction))
-        scalar_square_add_single(self.occupancy[f], xi, yi, si, 1)
+        self.mark([f], [x], [y], [sigma])
 
     def get(self, f, x, y):
         """Read at the floor of (x, y) / reduction, clipped to the grid."""

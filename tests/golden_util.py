@@ -99,6 +99,41 @@ def case_config(g):
     return make_config(**kw)
 
 
+def configure_decoder(dec, g):
+    """Decoder class attributes of a fixture's mode (what decoder.configure() writes)."""
+    mode = str(g['mode'])
+    dec.CifHr.v_threshold = 0.1
+    dec.CafScored.default_score_th = 0.1
+    dec.CifSeeds.threshold = 0.2 if mode == 'eval' else 0.5
+    dec.CifCaf.force_complete = mode == 'eval'
+    dec.CifCaf.keypoint_threshold = 0.0 if mode == 'eval' else 0.001
+    dec.CifCaf.greedy = bool(int(g['greedy']))
+    dec.CifCaf.connection_method = str(g['connection_method'])
+    dec.nms.Keypoints.instance_threshold = 0.0 if mode == 'eval' else 0.1
+    dec.nms.Keypoints.keypoint_threshold = 0.0 if mode == 'eval' else 0.001
+
+
+def annotations_as_records(anns, k=17):
+    """Annotation objects -> pp_ann records (for compare_annotations / oracle checks)."""
+    from openpifpaf_amd._abi import ANN_DTYPE
+    recs = np.zeros(len(anns), ANN_DTYPE)
+    for i, a in enumerate(anns):
+        r = recs[i]
+        r['data'][:k] = a.data
+        r['joint_scales'][:k] = a.joint_scales
+        r['score'] = a.score()
+        r['n_keypoints'] = k
+        r['n_decoding'] = len(a.decoding_order)
+        for t, (js, jt, xa, xb) in enumerate(a.decoding_order):
+            r['decoding_pairs'][t] = (js, jt)
+            r['decoding_xyv'][t, :3] = xa
+            r['decoding_xyv'][t, 3:] = xb
+        r['n_frontier'] = len(a.frontier_order)
+        for t, pair in enumerate(a.frontier_order):
+            r['frontier_pairs'][t] = pair
+    return recs
+
+
 def seeds_as_rows(seeds):
     """pp_seed structured array -> (n, 5) float32 rows (v, f, x, y, s)."""
     if len(seeds) == 0:

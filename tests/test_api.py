@@ -102,3 +102,82 @@ def test_generators_deterministic():
 def test_make_config_rejects_unknown_method():
     with pytest.raises(Exception):
         make_config(connection_method='nearest')
+
+
+# ---- decoder factory (decoder/factory.py:100-213), construction only -----------------------
+
+def _args(extra=()):
+    from openpifpaf_amd import decoder
+    parser = argparse.ArgumentParser()
+    decoder.cli(parser)
+    args = parser.parse_args(list(extra))
+    args.debug = False
+    return args
+
+
+def test_configure_detection_threshold_and_workers():
+    from openpifpaf_amd import decoder
+    args = _args(['--instance-threshold', '0.25', '--no-force-complete-pose'])
+    args.batch_size = 8
+    decoder.configure(args)
+    assert decoder.nms.Detection.instance_threshold == 0.25
+    assert decoder.nms.Keypoints.instance_threshold == 0.25
+    assert args.decoder_workers == 8  # factory.py:93-98
+    args = _args()
+    args.batch_size = 1
+    decoder.configure(args)
+    assert args.decoder_workers is None
+
+
+def test_factory_decode_variants():
+    import factory_util as fu
+    from openpifpaf_amd import constants, decoder
+    cc = decoder.factory_decode([fu.cif_head(), fu.caf_head()], basenet_stride=16)
+    assert isinstance(cc, decoder.CifCaf) and cc.field_config.is_single_scale()
+    assert cc.skeleton == constants.COCO_PERSON_SKELETON
+    # dense connections: skeleton extended in place with the 25 denser edges (factory.py:182-188)
+    heads = [fu.cif_head(), fu.caf_head(), fu.caf25_head()]
+    cc = decoder.factory_decode(heads, basenet_stride=16, dense_connections=True,
+                                dense_coupling=0.01)
+    assert len(cc.skeleton) == 44 and cc.skeleton == constants.DENSE_DECODE_SKELETON
+    assert cc.field_config.confidence_scales == [1.0] * 19 + [0.01] * 25
+    # multi-scale, no hflip: 5 scales of (cif, caf, caf25)
+    strides = [8, 16, 8, 16, 8]
+    cc = decoder.factory_decode(fu.multi_heads(strides), basenet_stride=16, multi_scale=True,
+                                multi_scale_hflip=False)
+    fc = cc.field_config
+    assert fc.cif_indices == [0, 3, 6, 9, 12] and fc.caf_indices == [1, 4, 7, 10, 13]
+    assert fc.cif_strides == strides and fc.caf_strides == strides
+    assert fc.cif_min_scales == [0.0, 12.0, 16.0, 24.0, 40.0]
+    assert fc.caf_min_distances == [0.0, 36.0, 48.0, 72.0, 120.0]
+    assert fc.caf_max_distances == [160.0, 240.0, 320.0, 480.0, None]
+    # multi-scale with hflip: 10 heads, lists repeated (factory.py:169-180)
+    cc = decoder.factory_decode(fu.multi_heads(strides * 2), basenet_stride=16, multi_scale=True)
+    fc = cc.field_config
+    assert fc.cif_indices == [3 * v for v in range(10)]
+    assert fc.cif_min_scales == [0.0, 12.0, 16.0, 24.0, 40.0] * 2
+    assert fc.caf_max_distances == [160.0, 240.0, 320.0, 480.0, None] * 2
+    # detection heads -> CifDet
+    cd = decoder.factory_decode([fu.det_head(['a', 'b'])], basenet_stride=16)
+    assert isinstance(cd, decoder.CifDet) and cd.categories == ['a', 'b']
+    with pytest.raises(Exception):
+        decoder.factory_decode([fu.caf_head()], basenet_stride=16)
+
+
+def test_factory_from_args_profile_decoder(tmp_path):
+    import types
+    import factory_util as fu
+    from openpifpaf_amd import decoder
+    from openpifpaf_amd.decoder.profiler import Profiler, ProfilerAutograd
+    args = _args(['--profile-decoder', str(tmp_path / 'dec.prof')])
+    model = types.SimpleNamespace(head_nets=[fu.cif_head(), fu.caf_head()],
+                                  base_net=types.SimpleNamespace(stride=16))
+    cls_call = decoder.CifCaf.__call__
+    try:
+        dec = decoder.factory_from_args(args, model)
+        assert isinstance(type(dec).__call__, Profiler)
+        assert isinstance(dec.fields_batch, ProfilerAutograd)
+        out = Profiler(lambda x: x + 1, out_name=str(tmp_path / 'p.prof'))(1)
+        assert out == 2 and (tmp_path / 'p.prof').exists()
+    finally:
+        decoder.CifCaf.__call__ = cls_call

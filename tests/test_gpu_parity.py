@@ -184,16 +184,7 @@ def _oracle_grow_connection(cols, x, y, s):
 # ---- decoder stages (single image, reference API) --------------------------------------
 
 def _configure(dec, g):
-    mode = str(g['mode'])
-    dec.CifHr.v_threshold = 0.1
-    dec.CafScored.default_score_th = 0.1
-    dec.CifSeeds.threshold = 0.2 if mode == 'eval' else 0.5
-    dec.CifCaf.force_complete = mode == 'eval'
-    dec.CifCaf.keypoint_threshold = 0.0 if mode == 'eval' else 0.001
-    dec.CifCaf.greedy = bool(int(g['greedy']))
-    dec.CifCaf.connection_method = str(g['connection_method'])
-    dec.nms.Keypoints.instance_threshold = 0.0 if mode == 'eval' else 0.1
-    dec.nms.Keypoints.keypoint_threshold = 0.0 if mode == 'eval' else 0.001
+    gu.configure_decoder(dec, g)
 
 
 @pytest.mark.parametrize('name', CASES)
@@ -950,3 +941,42 @@ def test_compact_refetch_flag():
     recs, _ = eng.fetch_async(b, (17, 19, PACK_ALL)).result()
     assert recs.dtype == ANN_DTYPE and recs.tobytes() == b''.join(
         [tampered.tobytes(), full[2:].tobytes()])
+
+
+def test_occupancy_device_grid():
+    """decoder.Occupancy on the device (pp_occupancy_set + pp_scalar_lookup) against the
+    reference's set / get (occupancy.py:36-47, utils.py:61-66) restated on a NumPy grid,
+    including the u8 wrap and marks on planes past the grid."""
+    from openpifpaf_amd.decoder import Occupancy
+    from openpifpaf_amd.functional import scalar_nonzero_clipped_with_reduction
+    rng = np.random.default_rng(3)
+    occ = Occupancy((5, 37, 29), 2, min_scale=4)
+    ref = np.zeros((5, 18, 14), np.uint8)
+
+    def ref_set(f, x, y, sigma):
+        if f >= len(ref):
+            return
+        xi, yi = round(x / 2), round(y / 2)
+        si = round(max(2.0, sigma / 2))
+        minx, miny = max(0, int(xi - si)), max(0, int(yi - si))
+        maxx = max(minx + 1, min(ref.shape[2], int(xi + si) + 1))
+        maxy = max(miny + 1, min(ref.shape[1], int(yi + si) + 1))
+        ref[f][miny:maxy, minx:maxx] += np.uint8(1)
+
+    marks = [(int(rng.integers(0, 6)), np.float32(rng.uniform(-5, 40)),
+              np.float32(rng.uniform(-5, 45)), np.float32(rng.uniform(0, 12)))
+             for _ in range(200)]
+    marks += [(1, np.float32(9.0), np.float32(11.0), np.float32(1.0))] * 260  # wraps past 255
+    for m in marks[:30]:
+        occ.set(*m)
+        ref_set(*m)
+    rest = marks[30:]
+    occ.mark([m[0] for m in rest], [m[1] for m in rest], [m[2] for m in rest],
+             [m[3] for m in rest])
+    for m in rest:
+        ref_set(*m)
+    assert np.array_equal(occ.occupancy.cpu().numpy(), ref)
+    for _ in range(50):
+        f, x, y = int(rng.integers(0, 6)), float(rng.uniform(-4, 40)), float(rng.uniform(-4, 40))
+        want = 1.0 if f >= 5 else scalar_nonzero_clipped_with_reduction(ref[f], x, y, 2)
+        assert occ.get(f, x, y) == want
