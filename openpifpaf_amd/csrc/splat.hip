@@ -17,6 +17,8 @@
 // from that XCD's L2.  Template MODE selects the functional.pyx primitive.
 #include "pp_common.hpp"
 
+#include <algorithm>
+
 #ifdef PP_STAMPS
 #include <stdio.h>
 #include <stdlib.h>
@@ -34,6 +36,7 @@ struct Splat {
 enum SplatMode { M_GAUSS_MAX = 0, M_GAUSS = 1, M_MAXG = 2, M_CONST = 3, M_CUMAVG = 4 };
 
 constexpr int kTile = 64;     // output tile edge (pixels)
+constexpr int kSpCand = 64;   // CifHr candidates per wave pass (lane = candidate)
 constexpr int kCand = 512;    // LDS candidate capacity per pass (>= 256 for progress)
 constexpr int kOutPad = 72;   // LDS staging row pitch (conflict-free ds_write_b32 columns)
 
@@ -53,6 +56,241 @@ __device__ __forceinline__ int4 splat_box(float cx, float cy, float ext, int h, 
 }
 
 // -------------------------------------------------------------------------------------
+// Block fold (both CifHr kernels): lanes own the 64 pixels of an 8x8 block and fold them
+// over the block's candidates in ascending splat order, in registers.  Per candidate the
+// constant parts of the pixel test are prepared once (FoldCand):
+//   - the box test is one packed 16-bit clamp of the lane's (x, y) key against the box
+//     corners (v_pk_max_i16 / v_pk_min_i16) and a compare;
+//   - the "closest pixel" branch (functional.pyx:132) is a key compare against the one
+//     pixel with dx^2 < 0.25 and dy^2 < 0.25 (found per candidate with the same float ops);
+//   - approx_exp's range test is dropped: a folded pixel has sum <= sigma^2, so
+//     q in [-0.5, 0] (NaN keeps NaN either way);
+//   - sigma^2's reciprocal is refined once (recip_of) instead of per pixel;
+//   - blocks the circle misses entirely (distance from the center to the block's nearest
+//     pixel > sigma * (1 + 2^-19), checked in f64) get no fold at all.
+// Candidates are folded two at a time: both terms are independent of the accumulator, only
+// the two updates are ordered.  All of this keeps per-(block, candidate) instructions low:
+// the fold is issue-bound (rocprof: SQ_INSTS_VALU + SQ_INSTS_SALU per pair).
+// -------------------------------------------------------------------------------------
+struct FoldCand {  // 32 B in LDS
+    float cx, cy, v, s2;
+    float r;        // recip_of(s2).r (div_refined); the slow path divides
+    uint32_t lo;    // box corner (x0, y0) as packed 16-bit (x | y << 16)
+    uint32_t hi;    // box corner (x1 - 1, y1 - 1), end-inclusive
+    uint32_t nkey;  // nearest pixel key (dx^2 < 0.25 and dy^2 < 0.25), ~0u: none
+};
+
+// the integer coordinate k with fl(fl(k - c)^2) < 0.25 (at most one exists), or -1
+__device__ __forceinline__ int nearest_coord(float c) {
+    if (!(fabsf(c) < 0x1p24f)) return -1;
+    const int k = (int)floorf(c);
+    for (int d = 0; d <= 1; d++) {
+        const float dd = (float)(k + d) - c;
+        if (dd * dd < 0.25f) return k + d;
+    }
+    return -1;
+}
+
+__device__ __forceinline__ uint32_t pix_key(int x, int y) {
+    return (uint32_t)(x & 0xffff) | ((uint32_t)y << 16);
+}
+
+// candidates the fast fold cannot take exactly: div_refined outside its domain
+__device__ __forceinline__ bool cand_slow(float s2) { return !recip_ok(s2); }
+
+__device__ __forceinline__ FoldCand make_cand(int4 b, float4 p) {
+    FoldCand c;
+    c.cx = p.x;
+    c.cy = p.y;
+    c.v = p.z;
+    c.s2 = p.w;
+    c.r = cand_slow(p.w) ? 0.0f : recip_of(p.w).r;
+    c.lo = pix_key(b.x, b.z);
+    c.hi = pix_key(b.y - 1, b.w - 1);
+    const int nx = nearest_coord(p.x), ny = nearest_coord(p.y);
+    c.nkey = (nx < 0 || ny < 0) ? ~0u : pix_key(nx, ny);
+    return c;
+}
+
+// 8x8 blocks of the 64x64 tile at (tx0, ty0) (bit 8 * by + bx) that candidate c's box
+// touches and its circle reaches.  Box corners unpack from the keys.
+__device__ __forceinline__ uint64_t cand_live(const FoldCand &c, int tx0, int ty0) {
+    const int x0 = (int)(c.lo & 0xffff), y0 = (int)(c.lo >> 16);
+    const int x1 = (int)(c.hi & 0xffff) + 1, y1 = (int)(c.hi >> 16) + 1;
+    if (x1 <= tx0 || x0 >= tx0 + kTile || y1 <= ty0 || y0 >= ty0 + kTile) return 0ull;
+    const int bxa = max(x0 - tx0, 0) >> 3, bxb = (min(x1 - tx0, kTile) - 1) >> 3;
+    const int bya = max(y0 - ty0, 0) >> 3, byb = (min(y1 - ty0, kTile) - 1) >> 3;
+    const double cx = c.cx, cy = c.cy;
+    const double thr = (double)c.s2 * (1.0 + 0x1p-19);  // NaN: never culled
+    uint64_t live = 0ull;
+    for (int by = bya; by <= byb; by++) {
+        const int Y0 = ty0 + 8 * by;
+        const double qy = fmin(fmax(cy, (double)Y0), (double)(Y0 + 7)) - cy;
+        for (int bx = bxa; bx <= bxb; bx++) {
+            const int X0 = tx0 + 8 * bx;
+            const double qx = fmin(fmax(cx, (double)X0), (double)(X0 + 7)) - cx;
+            if (!(qx * qx + qy * qy > thr)) live |= 1ull << (8 * by + bx);
+        }
+    }
+    return live;
+}
+
+typedef short pp_short2 __attribute__((ext_vector_type(2)));
+
+// fold_pixel<M_GAUSS_MAX> (truncate 1, max_value 1; functional.pyx:127-141): the term one
+// candidate adds to this lane's pixel (vv) and whether the pixel takes it
+struct FoldTerm {
+    float vv;
+    bool take;
+};
+
+template <bool SLOW>
+__device__ __forceinline__ FoldTerm fold_term(const FoldCand &c, float fx, float fy,
+                                              uint32_t key) {
+    const float dx = fx - c.cx, dy = fy - c.cy;
+    const float dx2 = dx * dx, dy2 = dy * dy;  // powf(d, 2.0)
+    const float sum = dx2 + dy2;
+    const float num = -0.5f * sum;
+    float q = SLOW ? num / c.s2 : div_refined(num, Recip{c.s2, c.r});
+    // "closest pixel" (vv = v): q = 0 gives t = 1 exactly, so v * t = v; a select on q keeps
+    // the fold branch-free
+    q = (key == c.nkey) ? 0.0f : q;
+    float t = __builtin_fmaf(q, 0.125f, 1.0f);  // 1 + q / 8 (q * 0.125 is exact)
+    t = t * t;
+    t = t * t;
+    t = t * t;
+    // box: clamp the packed (x, y) key into [lo, hi] per 16-bit half; unchanged = inside
+    const pp_short2 k2 = __builtin_bit_cast(pp_short2, key);
+    const pp_short2 cl = __builtin_elementwise_min(
+        __builtin_elementwise_max(k2, __builtin_bit_cast(pp_short2, c.lo)),
+        __builtin_bit_cast(pp_short2, c.hi));
+    FoldTerm f;
+    f.vv = c.v * t;
+    f.take = !(sum > c.s2) & (__builtin_bit_cast(uint32_t, cl) == key);
+    return f;
+}
+
+__device__ __forceinline__ float fold_apply(float acc, const FoldTerm &f) {
+    const float a = acc + f.vv;
+    return f.take ? ((a < 1.0f) ? a : 1.0f) : acc;  // min(max_value, f)
+}
+
+// Folds the candidates `q` (bits, ascending) of FoldCand array `cand` into this lane's
+// pixel: two at a time on the fast path, one at a time when the set holds a slow one.
+__device__ __forceinline__ float fold_block(float acc, const FoldCand *cand, uint64_t q,
+                                            uint64_t slow, float fx, float fy, uint32_t key) {
+#ifdef PP_EXP_NOFOLD
+    return acc + (float)__popcll(q);  // timing experiment: the fold switched off
+#endif
+    if (q & slow) {
+        for (; q; q &= q - 1) {
+            const int c = __builtin_ctzll(q);
+            acc = fold_apply(acc, ((slow >> c) & 1ull) ? fold_term<true>(cand[c], fx, fy, key)
+                                                       : fold_term<false>(cand[c], fx, fy, key));
+        }
+        return acc;
+    }
+    while (q) {
+        const int c1 = __builtin_ctzll(q);
+        q &= q - 1;
+        if (!q) return fold_apply(acc, fold_term<false>(cand[c1], fx, fy, key));
+        const int c2 = __builtin_ctzll(q);
+        q &= q - 1;
+        const FoldTerm f1 = fold_term<false>(cand[c1], fx, fy, key);
+        const FoldTerm f2 = fold_term<false>(cand[c2], fx, fy, key);
+        acc = fold_apply(fold_apply(acc, f1), f2);
+    }
+    return acc;
+}
+
+// wave-wide OR of a 64-bit value through one LDS word
+__device__ __forceinline__ uint64_t wave_or64(uint64_t v, uint64_t *s_slot) {
+    if (lane_id() == 0) *s_slot = 0ull;
+    wave_sync();
+    if (v) atomicOr((unsigned long long *)s_slot, (unsigned long long)v);
+    wave_sync();
+    const uint64_t r = *s_slot;
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(r >> 32)) << 32);
+}
+
+// Row bins of a candidate list: bin r gets, in list order, every entry whose box rows meet
+// tile row r (rows [64 r, 64 r + 64)), for maps of at most kMaxBinRows tile rows.  A counting
+// sweep (LDS atomics per row, plus each row's first / last list index) sizes the bins,
+// which are laid out back to back in `bins` (capacity bins_cap entries); then one block
+// compaction per (row, 256 entries) over only that row's index range fills them in order.
+// rowcnt[r] / rowoff[r] (LDS or global) = entries and offset of row r; rowcnt[r] = -1 for
+// every row when the bins would exceed bins_cap (consumers then scan the whole list).
+// Ends with a barrier.
+constexpr int kMaxBinRows = 32;
+constexpr int kBinMin = 512;  // shorter lists are scanned whole (binning would cost more)
+
+__host__ __device__ inline int64_t bins_capacity(int64_t cells) { return cells + cells / 2 + 2048; }
+
+struct RowBinLds {
+    int cnt[kMaxBinRows], first[kMaxBinRows], last[kMaxBinRows], off[kMaxBinRows + 1];
+    int tmp[4];
+};
+
+__device__ void hr_row_bins(const FoldCand *list, int total, FoldCand *bins, int64_t bins_cap,
+                            int tiles_y, RowBinLds &L, int *rowcnt, int *rowoff) {
+    if (threadIdx.x < kMaxBinRows) {
+        L.cnt[threadIdx.x] = 0;
+        L.first[threadIdx.x] = INT32_MAX;
+        L.last[threadIdx.x] = -1;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < total; i += 256) {
+        const FoldCand c = list[i];
+        const int ra = (int)(c.lo >> 16) >> 6, rb = (int)(c.hi >> 16) >> 6;
+        for (int r = ra; r <= rb && r < tiles_y; r++) {
+            atomicAdd(&L.cnt[r], 1);
+            atomicMin(&L.first[r], i);
+            atomicMax(&L.last[r], i);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int o = 0;
+        for (int r = 0; r < tiles_y; r++) {
+            L.off[r] = o;
+            o += L.cnt[r];
+        }
+        L.off[tiles_y] = o;
+    }
+    __syncthreads();
+    const bool fits = L.off[tiles_y] <= bins_cap;
+    if (threadIdx.x < tiles_y) {
+        rowcnt[threadIdx.x] = fits ? L.cnt[threadIdx.x] : -1;
+        rowoff[threadIdx.x] = L.off[threadIdx.x];
+    }
+    if (!fits) {
+        __syncthreads();
+        return;
+    }
+    for (int r = 0; r < tiles_y; r++) {
+        if (L.cnt[r] == 0) continue;  // block-uniform
+        FoldCand *bin = bins + L.off[r];
+        const uint32_t lo_y = (uint32_t)(r * kTile), hi_y = lo_y + kTile;
+        int running = 0;
+        for (int base = L.first[r]; base <= L.last[r]; base += 256) {
+            const int i = base + (int)threadIdx.x;
+            FoldCand c;
+            bool hit = false;
+            if (i <= L.last[r]) {
+                c = list[i];
+                hit = (c.lo >> 16) < hi_y && (c.hi >> 16) >= lo_y;  // box rows y0 .. y1 - 1
+            }
+            int tot;
+            const int slot = block_compact<4>(hit, L.tmp, tot);
+            if (hit) bin[running + slot] = c;
+            running += tot;
+        }
+    }
+    __syncthreads();
+}
+
+// -------------------------------------------------------------------------------------
 // K1: CIF cells -> splat records (cif_hr.py:26-40)
 // -------------------------------------------------------------------------------------
 constexpr int kTileBits = 1024;  // per-field tile bitmap capacity (32x32 tiles of 64x64 px)
@@ -68,17 +306,21 @@ struct HrSplatArgs {
     Heads h;
     int K, hh, ww;
     float v_th, neighbors;
-    Splat *splats;        // (n_img * K, list_cap); group g's list at goff[g]
+    FoldCand *list;       // (n_img * K, list_cap); group g's list at goff[g]
     int64_t list_cap;     // cells of all heads
     int64_t goff[kMaxHeads];
     int *counts;          // (n_img * K, n_groups)
     uint32_t *tile_bits;  // (n_img * K, n_groups, kTileBits / 32)
-    int tiles_x, tiles;
+    FoldCand *bins;       // (n_img * K, n_groups, bins_cap): the list per tile row (hr_row_bins)
+    int *rowcnt, *rowoff; // (n_img * K, n_groups, kMaxBinRows): bin sizes (-1: none), offsets
+    int64_t bins_cap;     // 0: no bins (maps of more than kMaxBinRows tile rows)
+    int tiles_x, tiles, tiles_y;
 };
 
 template <bool DET>
 __global__ __launch_bounds__(256) void cifhr_splats_kernel(HrSplatArgs a) {
     __shared__ int s_tmp[4];
+    __shared__ RowBinLds s_rb;
     __shared__ uint32_t s_bits[kTileBits / 32];
     const bool use_bits = a.tiles <= kTileBits;
     if (threadIdx.x < kTileBits / 32) s_bits[threadIdx.x] = 0u;
@@ -90,7 +332,7 @@ __global__ __launch_bounds__(256) void cifhr_splats_kernel(HrSplatArgs a) {
     const bool ms_on = (a.h.ms_on >> g) & 1u;
     const float ms_th = a.h.ms_th[g];
     const float len_cifs = (float)a.h.group_size();
-    Splat *out = a.splats + fld * a.list_cap + a.goff[g];
+    FoldCand *out = a.list + fld * a.list_cap + a.goff[g];
     int running = 0;
     for (int i = 0; i < a.h.group_size(); i++) {
         const int m = a.h.member(g, i);
@@ -136,13 +378,11 @@ __global__ __launch_bounds__(256) void cifhr_splats_kernel(HrSplatArgs a) {
                     }
                     const float sigma = (sg != sg) ? sg : fmaxf(1.0f, sg);  // np.maximum keeps NaN
                     const float v = (c[k] / a.neighbors) / len_cifs;        // v / neighbors / len_cifs
-                    Splat sp;
-                    sp.box = splat_box<M_GAUSS_MAX>(cx, cy, 1.0f * sigma, a.hh, a.ww);
-                    sp.par = make_float4(cx, cy, v, sigma * sigma);
-                    out[running + slot] = sp;
+                    const int4 box = splat_box<M_GAUSS_MAX>(cx, cy, 1.0f * sigma, a.hh, a.ww);
+                    out[running + slot] = make_cand(box, make_float4(cx, cy, v, sigma * sigma));
                     if (use_bits) {  // mark the 64x64 output tiles this splat's box touches
-                        for (int ty = sp.box.z / kTile; ty <= (sp.box.w - 1) / kTile; ty++)
-                            for (int tx = sp.box.x / kTile; tx <= (sp.box.y - 1) / kTile; tx++) {
+                        for (int ty = box.z / kTile; ty <= (box.w - 1) / kTile; ty++)
+                            for (int tx = box.x / kTile; tx <= (box.y - 1) / kTile; tx++) {
                                 const int t = ty * a.tiles_x + tx;
                                 atomicOr(&s_bits[t >> 5], 1u << (t & 31));
                             }
@@ -157,6 +397,11 @@ __global__ __launch_bounds__(256) void cifhr_splats_kernel(HrSplatArgs a) {
     if (threadIdx.x < kTileBits / 32)
         a.tile_bits[(int64_t)blockIdx.x * (kTileBits / 32) + threadIdx.x] =
             use_bits ? s_bits[threadIdx.x] : ~0u;
+    // the list by tile row for the tile kernel (blockIdx.x = (image * K + field) * groups + g)
+    if (a.bins_cap > 0 && running > kBinMin)
+        hr_row_bins(out, running, a.bins + (int64_t)blockIdx.x * a.bins_cap, a.bins_cap,
+                    a.tiles_y, s_rb, a.rowcnt + (int64_t)blockIdx.x * kMaxBinRows,
+                    a.rowoff + (int64_t)blockIdx.x * kMaxBinRows);
 }
 
 // -------------------------------------------------------------------------------------
@@ -333,24 +578,28 @@ __global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
 // -------------------------------------------------------------------------------------
 // The field's tile bitmap says which tiles any splat box touches.  Untouched tiles cost a
 // zero-fill (one tile per workgroup streams best: many short workgroups keep every CU's
-// store queue full, and a touched tile's fold delays no zero-fill); the field's splat lists
-// are loaded into LDS once when they fit (kHrCand entries over all groups), and each touched
-// tile selects its candidates from LDS by ballot compaction, keeping splat order.  Bigger
-// lists gather per tile from global memory in kCand chunks.
+// store queue full, and a touched tile's fold delays no zero-fill).  In a touched tile each
+// wave owns 16 rows (16 of the tile's 8x8 blocks): it gathers the candidates of its stripe
+// from the tile row's bin (the splats kernel's hr_row_bins; the whole list when the bin
+// overflowed) in passes of kSpCand, folds its blocks with fold_block into a private LDS
+// stripe, and writes the stripe with 16-B nontemporal stores.  Waves never wait for each
+// other.
 //
 // MULTI (CifHr over several groups, cif_hr.py:59-73): each group's list folds into a zero
-// tile and the groups combine by np.maximum(ta, accumulated), all in registers.  A group
-// with no splat on the tile contributes max(0, acc) = acc (every fold value is >= 0 and
+// stripe and the groups combine by np.maximum(ta, accumulated) in registers.  A group
+// with no splat on the stripe contributes max(0, acc) = acc (every fold value is >= 0 and
 // the clamp maps NaN to max_value), so it is skipped.
 constexpr int kChunkTiles = 1;  // tiles per workgroup: 1.209 ms vs 1.409 ms at 32 (cfg3)
-constexpr int kHrCand = 256;  // LDS list / candidate capacity (>= 256 for progress)
-constexpr int kHrPad = 68;    // accumulator row pitch: ~26 KB of LDS per workgroup
+constexpr int kHrPad = 68;    // stripe row pitch (floats)
 
 struct HrTileArgs {
     float *field;           // dense (n_fields, h, pitch)
-    const Splat *splats;    // field fld's group g list at splats + fld * splat_cap + goff[g]
+    const FoldCand *list;   // field fld's group g list at list + fld * splat_cap + goff[g]
     const int *counts;      // (n_fields, n_groups)
     const uint32_t *tile_bits;  // (n_fields, n_groups, kTileBits / 32)
+    const FoldCand *bins;   // (n_fields, n_groups, bins_cap)
+    const int *rowcnt, *rowoff;  // (n_fields, n_groups, kMaxBinRows), rowcnt -1: scan the list
+    int64_t bins_cap;       // 0: no bins
     int64_t splat_cap;
     int64_t field_stride;
     int h, w, pitch;
@@ -363,12 +612,9 @@ struct HrTileArgs {
 
 template <bool MULTI>
 __global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
-    __shared__ int4 s_box[kHrCand];
-    __shared__ float4 s_par[kHrCand];
-    __shared__ uint16_t s_idx[kHrCand];
+    __shared__ FoldCand s_cand[4][kSpCand];
     __shared__ __attribute__((aligned(16))) float s_out[kTile * kHrPad];
-    __shared__ int s_tmp[4];
-    __shared__ int s_ns[kMaxHeads], s_loff[kMaxHeads];  // per group: list size, LDS offset
+    __shared__ uint64_t s_live[4];
 
     const int64_t wid = xcd_remap(blockIdx.x, gridDim.x);
     if (wid >= a.n_work) return;
@@ -378,7 +624,7 @@ __global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
     const int ng = MULTI ? a.n_groups : 1;
 
     // touched tiles of the chunk over all groups: one round trip of scalar loads (a list's
-    // bitmap is all zero when the list is empty), the lists' sizes only if a tile is touched
+    // bitmap is all zero when the list is empty)
     uint32_t live = 0;
     for (int g = 0; g < ng; g++)
         live |= a.tile_bits[(fld * ng + g) * (kTileBits / 32) + (t0 >> 5)] >> (t0 & 31);
@@ -401,123 +647,82 @@ __global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
     }
     if (!live) return;
 
-    int total = 0;
-    for (int g = 0; g < ng; g++) {
-        const int ns = a.counts[fld * ng + g];
-        if (threadIdx.x == 0) {
-            s_ns[g] = ns;
-            s_loff[g] = total;
-        }
-        total += ns;
-    }
-    // the field's lists in LDS when they fit (one round trip for the whole chunk)
-    const bool pre = total <= kHrCand;
-    __syncthreads();  // s_ns / s_loff
-    if (pre) {
-        for (int g = 0; g < ng; g++) {
-            const Splat *sp = a.splats + fld * a.splat_cap + (MULTI ? a.goff[g] : 0);
-            const int o = s_loff[g], ns = s_ns[g];
-            for (int i = threadIdx.x; i < ns; i += 256) {
-                s_box[o + i] = sp[i].box;
-                s_par[o + i] = sp[i].par;
-            }
-        }
-        __syncthreads();
-    }
-
+    // touched tiles: wave w owns the tile's rows [16 w, 16 w + 16) = its blocks 16 w .. 16 w + 15
+    // (block b = 8 * by + bx), folds them from its own candidate passes in a private LDS
+    // stripe and writes the stripe; the waves never wait for each other
     const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & 63;
     const int lx = lane & 7, ly = lane >> 3;
     float *s_acc = s_out + wave * 16 * kHrPad;  // this wave's 64 x 16 stripe
+    FoldCand *cand = s_cand[wave];
     for (uint32_t rest = live; rest; rest &= rest - 1) {
         const int tile = t0 + __builtin_ctz(rest);
         const int tx0 = (tile % a.tiles_x) * kTile;
         const int ty0 = (tile / a.tiles_x) * kTile;
+        const int row = tile / a.tiles_x;
         const int wy0 = ty0 + wave * 16;  // stripe rows [wy0, wy0 + 16)
         float res[MULTI ? 16 : 1];
-        if (MULTI) {
 #pragma unroll
-            for (int r = 0; r < 16; r++) res[r] = 0.0f;
-        }
+        for (int r = 0; r < (MULTI ? 16 : 1); r++) res[r] = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; r++) s_acc[(r >> 3) * 8 * kHrPad + ly * kHrPad + (r & 7) * 8 + lx] = 0.0f;
         for (int g = 0; g < ng; g++) {
             const int64_t lst = fld * ng + g;
-            const int64_t ns = s_ns[g];
-            const int loff = s_loff[g];
+            const int ns = a.counts[lst];
             if (ns == 0 || !((a.tile_bits[lst * (kTileBits / 32) + (tile >> 5)] >> (tile & 31)) & 1u)) continue;
-            // zero the stripe accumulator (wave-private rows)
+            if (MULTI && g > 0) {  // each group folds from zero (cif_hr.py:59-62)
+                wave_sync();
 #pragma unroll
-            for (int r = 0; r < 16; r++) s_acc[(r >> 3) * 8 * kHrPad + ly * kHrPad + (r & 7) * 8 + lx] = 0.0f;
-            wave_sync();
-            const Splat *sp = a.splats + fld * a.splat_cap + (MULTI ? a.goff[g] : 0);
-            int64_t cursor = 0;
+                for (int r = 0; r < 16; r++) s_acc[(r >> 3) * 8 * kHrPad + ly * kHrPad + (r & 7) * 8 + lx] = 0.0f;
+            }
+            const int rc = (a.bins_cap > 0 && ns > kBinMin) ? a.rowcnt[lst * kMaxBinRows + row] : -1;
+            const FoldCand *src = rc >= 0 ? a.bins + lst * a.bins_cap + a.rowoff[lst * kMaxBinRows + row]
+                                          : a.list + fld * a.splat_cap + (MULTI ? a.goff[g] : 0);
+            const int src_n = rc >= 0 ? rc : ns;
             bool hit_any = false;
-            while (cursor < ns) {
-                // ---- gather: this tile's candidates in splat order ----
+            int cursor = 0;
+            while (true) {
+                // ---- the stripe's candidates in list order ----
                 int n = 0;
-                while (cursor < ns) {
-                    const int64_t i = cursor + threadIdx.x;
+                while (cursor < src_n) {
+                    const int e = cursor + lane;
                     bool hit = false;
-                    int4 b = make_int4(0, 0, 0, 0);
-                    if (i < ns) {
-                        b = pre ? s_box[loff + i] : sp[i].box;
-                        hit = b.y > tx0 && b.x < tx0 + kTile && b.w > ty0 && b.z < ty0 + kTile;
+                    FoldCand c;
+                    if (e < src_n) {
+                        c = src[e];
+                        const int x0 = (int)(c.lo & 0xffff), x1 = (int)(c.hi & 0xffff) + 1;
+                        const int y0 = (int)(c.lo >> 16), y1 = (int)(c.hi >> 16) + 1;
+                        hit = x1 > tx0 && x0 < tx0 + kTile && y1 > wy0 && y0 < wy0 + 16;
                     }
-                    int tot;
-                    const int slot = block_compact<4>(hit, s_tmp, tot);
-                    if (!pre && n + tot > kHrCand) break;  // block-uniform; re-read next pass
-                    if (hit) {
-                        if (pre) {
-                            s_idx[n + slot] = (uint16_t)(loff + i);
-                        } else {
-                            s_box[n + slot] = b;
-                            s_par[n + slot] = sp[i].par;
-                        }
-                    }
-                    n += tot;
-                    cursor += 256;
+                    const uint64_t mk = __ballot(hit);
+                    const int cnt = __popcll(mk);
+                    if (n + cnt > kSpCand) break;  // wave-uniform; chunk re-read next pass
+                    if (hit) cand[n + lane_prefix(mk)] = c;
+                    n += cnt;
+                    cursor += 64;
                 }
-                __syncthreads();
+                const bool last = cursor >= src_n;
                 hit_any = hit_any || n > 0;
-                // ---- fold, splat-major: for each candidate in ascending order, the wave's
-                // lanes cover the candidate's box clipped to the stripe; each pixel is
-                // read-modified-written in LDS by one lane, in candidate order (a wave's LDS
-                // operations execute in issue order)
-                for (int c = 0; c < n; c++) {
-                    const int e = pre ? (int)s_idx[c] : c;
-                    const int bx0 = max(__builtin_amdgcn_readfirstlane(s_box[e].x), tx0);
-                    const int bx1 = min(__builtin_amdgcn_readfirstlane(s_box[e].y), tx0 + kTile);
-                    const int by0 = max(__builtin_amdgcn_readfirstlane(s_box[e].z), wy0);
-                    const int by1 = min(__builtin_amdgcn_readfirstlane(s_box[e].w), wy0 + 16);
-                    if (bx1 <= bx0 || by1 <= by0) continue;  // wave-uniform
-                    const float4 par = s_par[e];
-                    const float t2s2 = 1.0f * par.w;  // truncate = 1 (cif_hr.py:40)
-                    const int bw = bx1 - bx0, area = bw * (by1 - by0);
-                    const float inv_bw = 1.0f / (float)bw;
-                    const bool fast = recip_ok(par.w);  // wave-uniform
-                    const Recip R = recip_of(par.w);
-                    for (int base = 0; base < area; base += 64) {
-                        const int i = base + lane;
-                        if (i >= area) break;
-                        const int yo = (int)(((float)i + 0.5f) * inv_bw);  // exact: i < 1024
-                        const int px = bx0 + (i - yo * bw), py = by0 + yo;
-                        // fold_pixel<M_GAUSS_MAX> for an in-box pixel (functional.pyx:127-141)
-                        const float dx = (float)px - par.x, dy = (float)py - par.y;
-                        const float dx2 = dx * dx, dy2 = dy * dy;
-                        const float sum = dx2 + dy2;
-                        if (sum > t2s2) continue;
-                        float vv;
-                        if (dx2 < 0.25f && dy2 < 0.25f) {
-                            vv = par.z;  // "closest pixel"
-                        } else {
-                            const float num = -0.5f * sum;
-                            vv = par.z * approx_exp_ref(fast ? div_refined(num, R) : num / par.w);
-                        }
-                        float *cell = &s_out[(py - ty0) * kHrPad + (px - tx0)];
-                        float v = *cell + vv;
-                        *cell = (v < 1.0f) ? v : 1.0f;  // min(max_value, f)
-                    }
+                wave_sync();
+                // ---- lane = candidate: its blocks among the wave's 16 ----
+                uint64_t cl = 0ull;
+                bool slow_l = false;
+                if (lane < n) {
+                    cl = (cand_live(cand[lane], tx0, ty0) >> (16 * wave)) & 0xFFFFull;
+                    slow_l = cand_slow(cand[lane].s2);
                 }
-                __syncthreads();
+                const uint64_t slow = __ballot(slow_l);
+                const uint64_t lv = wave_or64(cl, &s_live[wave]);
+                for (uint64_t bl = lv; bl; bl &= bl - 1) {
+                    const int b = __builtin_ctzll(bl);
+                    const int bx = b & 7, byl = b >> 3;
+                    const int px = tx0 + 8 * bx + lx, py = wy0 + 8 * byl + ly;
+                    float *cell = &s_acc[(byl * 8 + ly) * kHrPad + bx * 8 + lx];
+                    *cell = fold_block(*cell, cand, __ballot((cl >> b) & 1ull), slow, (float)px,
+                                       (float)py, pix_key(px, py));
+                }
+                if (last) break;
+                wave_sync();  // the candidate array is rewritten by the next pass
             }
             if (MULTI) {
                 wave_sync();
@@ -540,14 +745,13 @@ __global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const int q = k * 64 + lane;  // float4 index in the stripe
-            const int row = q >> 4, c4 = (q & 15) * 4;
-            const v4f v = *reinterpret_cast<const v4f *>(&s_acc[row * kHrPad + c4]);
-            const int trow = wave * 16 + row;
-            const int gy = ty0 + trow, gx = tx0 + c4;
+            const int row16 = q >> 4, c4 = (q & 15) * 4;
+            const v4f v = *reinterpret_cast<const v4f *>(&s_acc[row16 * kHrPad + c4]);
+            const int gy = wy0 + row16, gx = tx0 + c4;
             if (gy < a.h && gx < a.pitch)
                 __builtin_nontemporal_store(v, reinterpret_cast<v4f *>(&out[(int64_t)gy * a.pitch + gx]));
         }
-        __syncthreads();  // s_out / s_idx reuse by the next tile
+        wave_sync();  // the stripe is reused by the next tile
     }
 }
 
@@ -555,16 +759,19 @@ __global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
 // The decoder's CifHr: block-sparse map (HrMap with masks), one workgroup per field
 // -------------------------------------------------------------------------------------
 // Phase 1 compacts the field's splats (every group, cif_hr.py:26-40, 55-57) in the
-// reference's order: each thread loads kSpU cells per round, one barrier per round
-// orders the (cell batch, wave) counts, the first kSpList entries stay in LDS and the rest
-// go to the field's global list; a bitmap marks the 64x64 tiles the boxes touch.
+// reference's order into the field's global list of fold candidates (FoldCand): each
+// thread loads kSpU cells per round, one barrier per round orders the (cell batch, wave)
+// counts; a bitmap marks the 64x64 tiles the boxes touch.  Single-scale fields then bin the
+// list by tile row (row r: the entries whose box meets rows [64 r, 64 r + 64), in list
+// order, one block compaction per 256 entries), so a tile scans only its row's entries
+// instead of the whole list (a bin that would overflow its capacity falls back to the list).
 //
 // Phase 2: the four waves take the touched tiles round robin, each on its own (no
-// barriers).  Per tile a wave gathers the intersecting splats in order (ballot
-// compaction, kSpCand per pass), lane b builds block b's candidate bitmask (8x8 blocks),
-// and for every block with candidates the 64 lanes fold their pixel over the block's
-// candidates in ascending order in registers (functional.pyx:127-141) and store the
-// block's 256 contiguous bytes.  Blocks no splat box touches are never written: the
+// barriers).  Per tile a wave gathers the intersecting candidates in order (ballot
+// compaction, kSpCand per pass), lane c computes the 8x8 blocks candidate c reaches, and
+// for every block with candidates the 64 lanes fold their pixel over the block's
+// candidates in ascending order in registers (fold_block) and store the block's 256
+// contiguous bytes.  Blocks no splat box touches are never written: the
 // tile's u64 mask says which blocks hold data, and HrMap::at reads the rest as 0.
 // A tile with more than kSpCand candidates takes several passes; a block touched again
 // reloads its fold state from the map (each lane reads back only the pixel it wrote).
@@ -572,61 +779,24 @@ __global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
 // MULTI (cif_hr.py:59-73): groups fold into zero separately and combine by np.maximum;
 // candidates carry their group, and a change of group closes the running fold into res.
 // Across passes res stays in the map and the open group's fold in `aux`.
-constexpr int kSpList = 256;  // splat entries of a field kept in LDS
-constexpr int kSpCand = 64;   // candidates per wave pass (one u64 block bitmask per lane)
 constexpr int kSpU = 8;       // cells per thread per compaction round
 
 struct HrSparseArgs {
     Heads h;
     int hh, ww;
     float v_th, neighbors;
-    Splat *splats;    // (n_img * K, list_cap): the entries >= kSpList of each field's list
+    FoldCand *list;   // (n_img * K, list_cap): each field's splats in the reference's order
     int64_t list_cap;
+    FoldCand *bins;   // single-scale: (n_img * K, bins_cap) the list by tile row (hr_row_bins)
+    int64_t bins_cap; // 0: no bins (multi-scale, or maps of more than kMaxBinRows tile rows)
     float *map;       // (n_img * K, tiles, 64 blocks, 64 px)
     float *aux;       // MULTI: open-group folds between passes, same shape as map
     uint64_t *masks;  // (n_img * K, tiles) written blocks
-    int tiles_x, tiles;
+    int tiles_x, tiles, tiles_y;
 };
-
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
-    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
-    return ((uint64_t)hi << 32) | lo;
-}
 
 __device__ __forceinline__ float nan_max(float a, float b) {  // np.maximum
     return (a != a || b != b) ? NAN : (a > b ? a : b);
-}
-
-// the 8x8 blocks of the 64x64 tile at (tx0, ty0) that box b (end-exclusive, intersecting
-// the tile) covers: bit 8 * by + bx
-__device__ __forceinline__ uint64_t block_rect_mask(int4 b, int tx0, int ty0) {
-    const int bx0 = max(b.x - tx0, 0) >> 3, bx1 = (min(b.y - tx0, kTile) - 1) >> 3;
-    const int by0 = max(b.z - ty0, 0) >> 3, by1 = (min(b.w - ty0, kTile) - 1) >> 3;
-    const uint64_t row = (0xFFull >> (7 - bx1)) & (0xFFull << bx0);
-    const uint64_t rows = (~0ull >> (8 * (7 - by1))) & (~0ull << (8 * by0));
-    return (row * 0x0101010101010101ull) & rows;
-}
-
-// fold_pixel<M_GAUSS_MAX> with truncate 1 (functional.pyx:127-141) as straight-line selects:
-// pixel (px, py) inside box b and the circle adds v (nearest pixel) or v * approx_exp(q),
-// then min(max_value = 1, f)
-__device__ __forceinline__ float fold_gauss_max(float acc, int px, int py, float fx, float fy,
-                                                int4 b, float4 par) {
-    const bool in = (px >= b.x) & (px < b.y) & (py >= b.z) & (py < b.w);
-    const float dx = fx - par.x, dy = fy - par.y;
-    const float dx2 = dx * dx, dy2 = dy * dy;  // powf(d, 2.0)
-    const float sum = dx2 + dy2;
-    const bool take = in & !(sum > 1.0f * par.w);
-    const bool nearest = (dx2 < 0.25f) & (dy2 < 0.25f);
-    const float num = -0.5f * sum;
-    float q;
-    if (recip_ok(par.w)) q = div_refined(num, recip_of(par.w));
-    else q = num / par.w;
-    const float vv = nearest ? par.z : par.z * approx_exp_ref(q);
-    const float v = acc + vv;
-    const float f = (v < 1.0f) ? v : 1.0f;
-    return take ? f : acc;
 }
 
 #ifdef PP_STAMPS
@@ -644,18 +814,18 @@ __device__ uint64_t *g_hr_stamps;
     } while (0)
 #endif
 
-// Phase 1 of the CifHr kernels: the field's splat list in the reference's order (every
-// group, cif_hr.py:26-40, 55-57).  Each thread loads kSpU cells per round and one barrier
-// per round orders the (cell batch, wave) counts; the first kSpList entries stay in LDS
-// (s_lbox / s_lpar), the rest go to the field's global list; s_bits marks the 64x64 tiles
-// the boxes touch (cleared by the caller before the first barrier).  Returns the list
-// length; s_gbeg[g] = start of group g's entries.  Ends with a barrier.
+// Phase 1 of the CifHr kernel: the field's splat list in the reference's order (every
+// group, cif_hr.py:26-40, 55-57) as fold candidates in the field's global list.  Each
+// thread loads kSpU cells per round and one barrier per round orders the (cell batch, wave)
+// counts; s_bits marks the 64x64 tiles the boxes touch (cleared by the caller before the
+// first barrier).  Returns the list length; s_gbeg[g] = start of group g's entries.  Ends
+// with a barrier.
 template <bool MULTI>
-__device__ int hr_splat_list(const HrSparseArgs &a, int64_t fld, int4 *s_lbox, float4 *s_lpar,
-                             uint32_t *s_bits, int (*s_cnt)[kSpU][4], int *s_gbeg) {
+__device__ int hr_splat_list(const HrSparseArgs &a, int64_t fld, uint32_t *s_bits,
+                             int (*s_cnt)[kSpU][4], int *s_gbeg) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ng = MULTI ? a.h.n_groups : 1;
-    Splat *glist = a.splats + fld * a.list_cap;
+    FoldCand *glist = a.list + fld * a.list_cap;
     int running = 0, buf = 0;
     for (int g = 0; g < ng; g++) {
         if (threadIdx.x == 0) s_gbeg[g] = running;
@@ -708,14 +878,7 @@ __device__ int hr_splat_list(const HrSparseArgs &a, int64_t fld, int4 *s_lbox, f
                         const float sigma = (sg != sg) ? sg : fmaxf(1.0f, sg);  // np.maximum keeps NaN
                         const float v = (c[k] / a.neighbors) / len_cifs;        // v / neighbors / len_cifs
                         const int4 box = splat_box<M_GAUSS_MAX>(cx, cy, 1.0f * sigma, a.hh, a.ww);
-                        const float4 par = make_float4(cx, cy, v, sigma * sigma);
-                        if (pos < kSpList) {
-                            s_lbox[pos] = box;
-                            s_lpar[pos] = par;
-                        } else {
-                            glist[pos].box = box;
-                            glist[pos].par = par;
-                        }
+                        glist[pos] = make_cand(box, make_float4(cx, cy, v, sigma * sigma));
                         for (int ty = box.z / kTile; ty <= (box.w - 1) / kTile; ty++)
                             for (int tx = box.x / kTile; tx <= (box.y - 1) / kTile; tx++) {
                                 const int t = ty * a.tiles_x + tx;
@@ -735,13 +898,12 @@ __device__ int hr_splat_list(const HrSparseArgs &a, int64_t fld, int4 *s_lbox, f
 
 template <bool MULTI>
 __global__ __launch_bounds__(256) void cifhr_sparse_kernel(HrSparseArgs a) {
-    __shared__ int4 s_lbox[kSpList];
-    __shared__ float4 s_lpar[kSpList];
     __shared__ uint32_t s_bits[kTileBits / 32];
+    __shared__ RowBinLds s_rb;
+    __shared__ int s_rowcnt[kMaxBinRows], s_rowoff[kMaxBinRows];  // bins (hr_row_bins)
     __shared__ __attribute__((aligned(16))) int s_cnt[2][kSpU][4];
     __shared__ int s_gbeg[kMaxHeads + 1];
-    __shared__ int4 s_cbox[4][kSpCand];
-    __shared__ float4 s_cpar[4][kSpCand];
+    __shared__ FoldCand s_cand[4][kSpCand];
     __shared__ uint8_t s_cg[4][MULTI ? kSpCand : 1];
     __shared__ int8_t s_bg[4][MULTI ? 64 : 1];
     __shared__ uint64_t s_live[4];
@@ -753,9 +915,13 @@ __global__ __launch_bounds__(256) void cifhr_sparse_kernel(HrSparseArgs a) {
     if (threadIdx.x < kTileBits / 32) s_bits[threadIdx.x] = 0u;
     if (threadIdx.x == 0) s_next = 0;
 
-    const int total = hr_splat_list<MULTI>(a, fld, s_lbox, s_lpar, s_bits, s_cnt, s_gbeg);
+    const int total = hr_splat_list<MULTI>(a, fld, s_bits, s_cnt, s_gbeg);
+    const bool use_bins = !MULTI && a.bins_cap > 0 && total > kBinMin;
+    if (use_bins)
+        hr_row_bins(a.list + fld * a.list_cap, total, a.bins + fld * a.bins_cap, a.bins_cap,
+                    a.tiles_y, s_rb, s_rowcnt, s_rowoff);
     const int ng = MULTI ? a.h.n_groups : 1;
-    Splat *glist = a.splats + fld * a.list_cap;
+    const FoldCand *glist = a.list + fld * a.list_cap;
 #ifdef PP_STAMPS
     if (wave == 0) {
         HR_STAMP(1);
@@ -770,8 +936,7 @@ __global__ __launch_bounds__(256) void cifhr_sparse_kernel(HrSparseArgs a) {
         if (!((s_bits[t >> 5] >> (t & 31)) & 1u)) a.masks[fld * a.tiles + t] = 0ull;
 
     // ---- phase 2: touched tiles, one wave each, claimed from an LDS counter ----
-    int4 *cbox = s_cbox[wave];
-    float4 *cpar = s_cpar[wave];
+    FoldCand *cand = s_cand[wave];
     const int lx = lane & 7, ly = lane >> 3;
     const int nwords = (a.tiles + 31) >> 5;
     int wd = 0, li = 0;  // this wave's walk over the set bits (live index li)
@@ -799,39 +964,32 @@ __global__ __launch_bounds__(256) void cifhr_sparse_kernel(HrSparseArgs a) {
         float *mp = a.map + (fld * a.tiles + t) * (int64_t)(kTile * kTile);
         float *ap = MULTI ? a.aux + (fld * a.tiles + t) * (int64_t)(kTile * kTile) : nullptr;
         uint64_t done = 0;  // blocks written by earlier passes
+        // candidates come from the tile row's bin, or from the whole list (MULTI, overflow)
+        const int row = t / a.tiles_x;
+        const int rc = use_bins ? s_rowcnt[row] : -1;
+        const FoldCand *src = rc >= 0 ? a.bins + fld * a.bins_cap + s_rowoff[row] : glist;
+        const int src_n = rc >= 0 ? rc : total;
         int cursor = 0;
         while (true) {
             // ---- this tile's candidates, in list order ----
             int n = 0;
-            while (cursor < total) {
-                // chunks never straddle kSpList (a multiple of 64): LDS or global per chunk;
-                // the two paths stay apart so the loads keep their address space (a merged
-                // pointer would become a flat load)
+            while (cursor < src_n) {
                 const int e = cursor + lane;
-                const bool in_lds = cursor < kSpList;
                 bool hit = false;
-                int4 b = make_int4(0, 0, 0, 0);
-                float4 pr = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-                if (e < total) {
-                    if (in_lds) {
-                        b = s_lbox[e];
-                        hit = b.y > tx0 && b.x < tx0 + kTile && b.w > ty0 && b.z < ty0 + kTile;
-                        if (hit) pr = s_lpar[e];
-                    } else {
-                        const Splat sp = glist[e];
-                        b = sp.box;
-                        pr = sp.par;
-                        hit = b.y > tx0 && b.x < tx0 + kTile && b.w > ty0 && b.z < ty0 + kTile;
-                    }
+                FoldCand c;
+                if (e < src_n) {
+                    c = src[e];
+                    const int x0 = (int)(c.lo & 0xffff), x1 = (int)(c.hi & 0xffff) + 1;
+                    const int y0 = (int)(c.lo >> 16), y1 = (int)(c.hi >> 16) + 1;
+                    hit = x1 > tx0 && x0 < tx0 + kTile && y1 > ty0 && y0 < ty0 + kTile;
                 }
                 const uint64_t mk = __ballot(hit);
                 const int cnt = __popcll(mk);
                 if (n + cnt > kSpCand) break;  // wave-uniform; chunk re-read next pass
                 if (hit) {
                     const int pos = n + lane_prefix(mk);
-                    cbox[pos] = b;
-                    cpar[pos] = pr;
-                    if (MULTI) {
+                    cand[pos] = c;
+                    if (MULTI) {  // list index e -> group
                         int gg = 0;
                         while (gg + 1 < ng && e >= s_gbeg[gg + 1]) gg++;
                         s_cg[wave][pos] = (uint8_t)gg;
@@ -840,25 +998,24 @@ __global__ __launch_bounds__(256) void cifhr_sparse_kernel(HrSparseArgs a) {
                 n += cnt;
                 cursor += 64;
             }
-            const bool last = cursor >= total;
-            if (lane == 0) s_live[wave] = 0ull;
+            const bool last = cursor >= src_n;
             wave_sync();
-            // ---- lane = candidate: the tile's 8x8 blocks its box covers ----
-            uint64_t cm0 = 0, cm1 = 0;
-            if (lane < n) cm0 = block_rect_mask(cbox[lane], tx0, ty0);
-            if (lane + 64 < n) cm1 = block_rect_mask(cbox[lane + 64], tx0, ty0);
-            if (cm0 | cm1) atomicOr((unsigned long long *)&s_live[wave], (unsigned long long)(cm0 | cm1));
-            wave_sync();
-            // readfirstlane returns int: widen through uint32_t, or a low half with bit 31
-            // set sign-extends over the high half (blocks 32-63 live without candidates)
-            const uint64_t live =
-                (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)s_live[wave]) |
-                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_live[wave] >> 32)) << 32);
+            // ---- lane = candidate: its blocks of the tile ----
+            uint64_t cl = 0ull;
+            bool slow_l = false;
+            if (lane < n) {
+                cl = cand_live(cand[lane], tx0, ty0);
+                slow_l = cand_slow(cand[lane].s2);
+            }
+            const uint64_t slow = __ballot(slow_l);
+            const uint64_t live = wave_or64(cl, &s_live[wave]);
             // ---- fold: block by block, lane = pixel, candidates ascending ----
             for (uint64_t rest = live; rest; rest &= rest - 1) {
                 const int blk = __builtin_ctzll(rest);
                 const int px = tx0 + 8 * (blk & 7) + lx, py = ty0 + 8 * (blk >> 3) + ly;
                 const float fx = (float)px, fy = (float)py;
+                const uint32_t key = pix_key(px, py);
+                const uint64_t bq = __ballot((cl >> blk) & 1ull);
                 float acc = 0.0f, res = 0.0f;
                 int gcur = -1;
                 if ((done >> blk) & 1ull) {  // state of an earlier pass (own pixel)
@@ -870,32 +1027,19 @@ __global__ __launch_bounds__(256) void cifhr_sparse_kernel(HrSparseArgs a) {
                         acc = mp[blk * 64 + lane];
                     }
                 }
-                uint64_t qa = __ballot((cm0 >> blk) & 1ull), qb = __ballot((cm1 >> blk) & 1ull);
-                // candidates in ascending order; the next one's LDS reads are issued before
-                // the current one folds
-                int c = qa ? __builtin_ctzll(qa) : 64 + __builtin_ctzll(qb);
-                if (qa) qa &= qa - 1; else qb &= qb - 1;
-                int4 b = cbox[c];
-                float4 par = cpar[c];
-                int gc = MULTI ? s_cg[wave][c] : 0;
-                while (true) {
-                    const bool more = (qa | qb) != 0;
-                    const int cn = !more ? c : (qa ? __builtin_ctzll(qa) : 64 + __builtin_ctzll(qb));
-                    if (qa) qa &= qa - 1; else qb &= qb - 1;
-                    const int4 bn = cbox[cn];
-                    const float4 pn = cpar[cn];
-                    const int gn = MULTI ? s_cg[wave][cn] : 0;
-                    if (MULTI && gc != gcur) {  // np.maximum(ta, accumulated) per group
-                        res = nan_max(acc, res);
-                        acc = 0.0f;
-                        gcur = gc;
+                if (!MULTI) {
+                    acc = fold_block(acc, cand, bq, slow, fx, fy, key);
+                } else {
+                    for (uint64_t q = bq; q; q &= q - 1) {
+                        const int c = __builtin_ctzll(q);
+                        const int gc = s_cg[wave][c];
+                        if (gc != gcur) {  // np.maximum(ta, accumulated) per group
+                            res = nan_max(acc, res);
+                            acc = 0.0f;
+                            gcur = gc;
+                        }
+                        acc = fold_block(acc, cand, 1ull << c, slow, fx, fy, key);
                     }
-                    acc = fold_gauss_max(acc, px, py, fx, fy, b, par);
-                    if (!more) break;
-                    c = cn;
-                    b = bn;
-                    par = pn;
-                    gc = gn;
                 }
                 if (!MULTI) {
                     mp[blk * 64 + lane] = acc;
@@ -956,11 +1100,28 @@ size_t pp_cifhr_workspace_size(int32_t n_img, int32_t K, int32_t H, int32_t W) {
 
 namespace pp {
 
+// dense CifHr workspace: FoldCand lists, counts, tile bitmaps, row-bin sizes / offsets, row
+// bins (bins_capacity entries per list, independent of the stride: pp_cifhr_workspace_size
+// has no stride argument)
+struct HeadsWs {
+    size_t off_counts, off_bits, off_rowcnt, off_rowoff, off_bins, total;
+};
+
+static HeadsWs heads_ws(const Heads &h, int n_img, int K) {
+    const size_t nf = (size_t)n_img * K, nl = nf * h.n_groups;
+    HeadsWs w;
+    w.off_counts = round_up((int64_t)(nf * (size_t)h.cif_cells() * sizeof(FoldCand)), 256);
+    w.off_bits = w.off_counts + round_up((int64_t)(nl * sizeof(int)), 256);
+    w.off_rowcnt = w.off_bits + round_up((int64_t)(nl * (kTileBits / 32) * sizeof(uint32_t)), 256);
+    w.off_rowoff = w.off_rowcnt + round_up((int64_t)(nl * kMaxBinRows * sizeof(int)), 256);
+    w.off_bins = w.off_rowoff + round_up((int64_t)(nl * kMaxBinRows * sizeof(int)), 256);
+    w.total = w.off_bins +
+              round_up((int64_t)(nl * (size_t)bins_capacity(h.cif_cells()) * sizeof(FoldCand)), 256);
+    return w;
+}
+
 size_t cifhr_heads_workspace_size(const Heads &h, int n_img, int K) {
-    const size_t nf = (size_t)n_img * K;
-    return round_up((int64_t)(nf * (size_t)h.cif_cells() * sizeof(Splat)), 256) +
-           round_up((int64_t)(nf * h.n_groups * sizeof(int)), 256) +
-           round_up((int64_t)(nf * h.n_groups * (kTileBits / 32) * sizeof(uint32_t)), 256);
+    return heads_ws(h, n_img, K).total;
 }
 
 // CifHr.fill (cif_hr.py:59-73) over the heads: the map has head 0's field size and stride
@@ -985,23 +1146,33 @@ int cifhr_heads_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config
     sa.ww = ww;
     sa.v_th = cfg->cif_threshold;
     sa.neighbors = (float)cfg->cif_neighbors;
-    sa.splats = (Splat *)d_workspace;
+    sa.list = (FoldCand *)d_workspace;
     sa.list_cap = h.cif_cells();
     int64_t o = 0;
     for (int g = 0; g < h.n_groups; g++) {
         sa.goff[g] = o;
         for (int i = 0; i < h.group_size(); i++) o += h.cif_hw(h.member(g, i));
     }
-    sa.counts = (int *)((char *)d_workspace + round_up((int64_t)(nf * sa.list_cap * sizeof(Splat)), 256));
-    sa.tile_bits = (uint32_t *)((char *)sa.counts + round_up((int64_t)(nf * h.n_groups * sizeof(int)), 256));
+    const HeadsWs wl = heads_ws(h, n_img, K);
+    sa.counts = (int *)((char *)d_workspace + wl.off_counts);
+    sa.tile_bits = (uint32_t *)((char *)d_workspace + wl.off_bits);
+    sa.rowcnt = (int *)((char *)d_workspace + wl.off_rowcnt);
+    sa.rowoff = (int *)((char *)d_workspace + wl.off_rowoff);
+    sa.bins = (FoldCand *)((char *)d_workspace + wl.off_bins);
     sa.tiles_x = (int)((pitch + kTile - 1) / kTile);
-    sa.tiles = sa.tiles_x * ((hh + kTile - 1) / kTile);
+    sa.tiles_y = (hh + kTile - 1) / kTile;
+    sa.tiles = sa.tiles_x * sa.tiles_y;
+    sa.bins_cap = sa.tiles_y <= kMaxBinRows ? bins_capacity(h.cif_cells()) : 0;
     hipLaunchKernelGGL(cifhr_splats_kernel<DET>, dim3((unsigned)(nf * h.n_groups)), dim3(256), 0, s, sa);
     HrTileArgs a{};
     a.field = d_cifhr;
-    a.splats = sa.splats;
+    a.list = sa.list;
     a.counts = sa.counts;
     a.tile_bits = sa.tile_bits;
+    a.bins = sa.bins;
+    a.rowcnt = sa.rowcnt;
+    a.rowoff = sa.rowoff;
+    a.bins_cap = sa.bins_cap;
     a.splat_cap = sa.list_cap;
     a.h = hh;
     a.w = ww;
@@ -1027,7 +1198,11 @@ template int cifhr_heads_launch<false>(const Heads &, int32_t, int32_t, const pp
                                        void *, size_t, hipStream_t, const char *);
 
 size_t cifhr_sparse_workspace_size(const Heads &h, int n_img, int K) {
-    return round_up((int64_t)((size_t)n_img * K * (size_t)h.cif_cells() * sizeof(Splat)), 256);
+    const size_t nf = (size_t)n_img * K;
+    size_t bytes = round_up((int64_t)(nf * (size_t)h.cif_cells() * sizeof(FoldCand)), 256);
+    if (h.n_groups == 1)
+        bytes += round_up((int64_t)(nf * (size_t)bins_capacity(h.cif_cells()) * sizeof(FoldCand)), 256);
+    return bytes;
 }
 
 int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config *cfg,
@@ -1051,13 +1226,18 @@ int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_confi
     a.ww = ww;
     a.v_th = cfg->cif_threshold;
     a.neighbors = (float)cfg->cif_neighbors;
-    a.splats = (Splat *)d_workspace;
+    a.list = (FoldCand *)d_workspace;
     a.list_cap = h.cif_cells();
+    a.tiles_x = geo.tiles_x;
+    a.tiles = geo.tiles;
+    a.tiles_y = (hh + kTile - 1) / kTile;
+    // row bins for single-scale maps of at most kMaxBinRows tile rows
+    a.bins_cap = (h.n_groups == 1 && a.tiles_y <= kMaxBinRows) ? bins_capacity(h.cif_cells()) : 0;
+    a.bins = (FoldCand *)((char *)d_workspace +
+                          round_up((int64_t)((size_t)n_img * K * a.list_cap * sizeof(FoldCand)), 256));
     a.map = d_map;
     a.aux = d_aux;
     a.masks = d_masks;
-    a.tiles_x = geo.tiles_x;
-    a.tiles = geo.tiles;
     const unsigned nblocks = (unsigned)((int64_t)n_img * K);
 #ifdef PP_STAMPS
     uint64_t *st = nullptr;
