@@ -363,6 +363,18 @@ def main():
             'stage_ms': {n: round(float(v), 4) for n, v in zip(names, u_stage)},
             'annotations_per_image': round(u_anns / (u_steps * batch), 3),
         }
+        # the dense CifHr map (pp_cifhr) on the uniform batch: ~15.5M pixel-visits per image
+        # make it fold-bound, far from the write-bound planted case of `roofline`
+        u_dense_ms = dense_cifhr_ms(ucif, cfg, stream, max(3, args.steps // 4), 1)
+        u_gbs = dense_bytes / (u_dense_ms * 1e-3) / 1e9
+        line['roofline_uniform'] = {
+            'bound': 'hbm', 'kernel': 'cifhr_splats_kernel + cifhr_tile_kernel (pp_cifhr), '
+                                      'uniform generator',
+            'achieved': round(u_gbs, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
+            'frac': round(u_gbs / PEAK_HBM_GBS, 4), 'ms_per_launch': round(u_dense_ms, 4),
+            'algorithmic_bytes_per_launch': dense_bytes,
+            'decoder_cifhr_ms': round(float(u_stage[0]), 4),
+        }
     if default_run and world == 1 and not args.no_multi:
         # multi-scale FieldConfigs (factory.py:153-180) on pp_decode_multi: the same people
         # seen by several heads; 'ms2' = stride 8 + 16 heads, 'ms10' = the reference's

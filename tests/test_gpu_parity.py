@@ -278,6 +278,33 @@ def test_batch_predict(dec):
     _batch_vs_oracle(dec, 'planted', 64, 80, 16, mode='predict')
 
 
+@pytest.mark.parametrize('kind', ['planted', 'uniform'])
+def test_batch160_dense_vs_oracle(dec, kind):
+    """BASELINE configs[4] shapes: 160x160 fields with the 44-edge dense skeleton, a batch of
+    4 images per generator in one device decode (workspace, capacities and the dense CAF set
+    at ~1.4k annotations per uniform image), every image against the oracle byte for byte."""
+    from openpifpaf_amd import constants, synthetic
+    from openpifpaf_amd._abi import EVAL_CONFIG, make_config
+    g = {'mode': np.array('eval'), 'greedy': 0, 'connection_method': np.array('blend')}
+    _configure(dec, g)
+    sk = constants.DENSE_DECODE_SKELETON
+    kw = {'n_caf': len(sk)} if kind == 'uniform' else {'skeleton': sk, 'n_people': 16}
+    cif, caf = synthetic.batch(kind, 4, 160, 160, first_seed=60, **kw)
+    cc = dec.CifCaf(dec.FieldConfig(), keypoints=constants.COCO_KEYPOINTS, skeleton=sk,
+                    out_skeleton=constants.COCO_PERSON_SKELETON)
+    recs, offsets, _ = cc.decode_records(cif, caf)
+    cfg = make_config(**EVAL_CONFIG)
+    for i in range(4):
+        ref = oracle.decode(cif[i], caf[i], sk, cfg)
+        got = recs[offsets[i]:offsets[i + 1]]
+        assert len(got) == len(ref), (i, len(got), len(ref))
+        for r, o in zip(got, ref):
+            for key in ('data', 'joint_scales', 'score', 'decoding_pairs', 'decoding_xyv',
+                        'frontier_pairs'):
+                assert np.array_equal(r[key], o[key]), (i, key)
+    assert offsets[-1] > (4 * 12 if kind == 'planted' else 4 * 1000)
+
+
 def test_cifhr_batch_bit_exact():
     """CifHr over a 256-image batch: every image equals the oracle bit for bit."""
     import torch
