@@ -163,6 +163,52 @@ __device__ __forceinline__ uint64_t seed_key(float v, int f, int e) {
 __device__ __forceinline__ int key_emit(uint64_t k) { return (int)(kEmitMask - ((uint32_t)k & kEmitMask)); }
 
 // stage 2: one workgroup per image — concatenate the segments in order and sort
+// compare-exchange result for element i of the pair (i, i ^ j) in stage (k, j) of a
+// descending bitonic network: the lower element of a descending block keeps the max
+__device__ __forceinline__ uint64_t bitonic_pick(int i, int j, int k, uint64_t a, uint64_t b) {
+    const bool lower = (i & j) == 0, desc = (i & k) == 0;
+    const uint64_t mx = a > b ? a : b, mn = a > b ? b : a;
+    return lower == desc ? mx : mn;
+}
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// descending bitonic sort of kSortLds (4096) u64 keys, 4 per thread of a 1024-thread block
+// (element 4 * thread + e in key[e]); s_buf (kSortLds) is scratch for the cross-wave stages
+static_assert(kSortLds == 4096, "bitonic4096_desc sorts 4 keys per thread of 1024");
+__device__ void bitonic4096_desc(uint64_t key[4], uint64_t *s_buf) {
+    const int t = threadIdx.x;
+    for (int k = 2; k <= kSortLds; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j >= 256) {  // partner in another wave: through LDS
+                __syncthreads();  // earlier readers of s_buf are done
+#pragma unroll
+                for (int e = 0; e < 4; e++) s_buf[4 * t + e] = key[e];
+                __syncthreads();
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int i = 4 * t + e;
+                    key[e] = bitonic_pick(i, j, k, key[e], s_buf[i ^ j]);
+                }
+            } else if (j >= 4) {  // partner thread t ^ (j / 4), same slot, same wave
+#pragma unroll
+                for (int e = 0; e < 4; e++)
+                    key[e] = bitonic_pick(4 * t + e, j, k, key[e], shfl_xor64(key[e], j >> 2));
+            } else {  // partner slot e ^ j of this thread
+                uint64_t nk[4];
+#pragma unroll
+                for (int e = 0; e < 4; e++) nk[e] = bitonic_pick(4 * t + e, j, k, key[e], key[e ^ j]);
+#pragma unroll
+                for (int e = 0; e < 4; e++) key[e] = nk[e];
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
     __shared__ uint64_t s_key[kSortLds];
     __shared__ float s_x[kSortLds], s_y[kSortLds], s_s[kSortLds];
@@ -200,24 +246,21 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
                 s_s[o + i] = gs[k];
             }
         }
-        for (int i = n + threadIdx.x; i < np; i += blockDim.x) s_key[i] = 0;  // sorts last
         __syncthreads();
-        for (int k = 2; k <= np; k <<= 1) {  // bitonic network, descending
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                for (int i = threadIdx.x; i < np; i += blockDim.x) {
-                    const int ixj = i ^ j;
-                    if (ixj > i) {
-                        const uint64_t ka = s_key[i], kb = s_key[ixj];
-                        const bool desc = (i & k) == 0;
-                        if (desc ? ka < kb : ka > kb) {
-                            s_key[i] = kb;
-                            s_key[ixj] = ka;
-                        }
-                    }
-                }
-                __syncthreads();
-            }
+        // bitonic network, descending, on kSortLds keys held 4 per thread (keys past n are
+        // 0 and sort last): only the stages whose partner lies in another wave go through
+        // LDS (10 of 78); the others exchange in registers / across lanes
+        uint64_t key[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int i = 4 * (int)threadIdx.x + e;
+            key[e] = i < n ? s_key[i] : 0ull;
         }
+        bitonic4096_desc(key, s_key);
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < 4; e++) s_key[4 * threadIdx.x + e] = key[e];
+        __syncthreads();
         // runs of equal (v, field): insertion sort by (x, y, s) descending, then emission
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
             const uint64_t ki = s_key[i] >> 27;
