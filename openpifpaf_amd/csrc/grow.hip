@@ -314,8 +314,38 @@ struct Best2 {
     float x1, y1, c1, x2, y2, c2;
 };
 
+__device__ __forceinline__ uint64_t rl_u64(uint64_t v, int l) {
+    const uint32_t lo = (uint32_t)rl_i((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)rl_i((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// at most two lanes hold candidates (the usual case: the 2*scale box passes a handful of
+// columns): merge them with scalar reads instead of the two DPP reductions
 __device__ __forceinline__ Best2 top2_wave(const Top2 &t) {
     Best2 b;
+    const uint64_t cm = __ballot(t.k1 != 0);
+    if (__popcll(cm) <= 2) {
+        const uint64_t cm2 = cm & (cm - 1);
+        const int la = cm ? __ffsll((unsigned long long)cm) - 1 : 0;
+        const int lb = cm2 ? __ffsll((unsigned long long)cm2) - 1 : la;
+        const uint64_t ka1 = rl_u64(t.k1, la), ka2 = rl_u64(t.k2, la);
+        const uint64_t kb1 = cm2 ? rl_u64(t.k1, lb) : 0, kb2 = cm2 ? rl_u64(t.k2, lb) : 0;
+        const bool a_first = ka1 > kb1;  // equal only when both are 0
+        const int l1 = a_first ? la : lb, lo = a_first ? lb : la;
+        const uint64_t own2 = a_first ? ka2 : kb2, oth1 = a_first ? kb1 : ka1;
+        const bool own_second = own2 > oth1;  // the best lane's runner-up beats the other's best
+        b.k1 = a_first ? ka1 : kb1;
+        b.k2 = own_second ? own2 : oth1;
+        b.x1 = rl_f(t.x1, l1);
+        b.y1 = rl_f(t.y1, l1);
+        b.c1 = rl_f(t.c1, l1);
+        const int l2 = own_second ? l1 : lo;
+        b.x2 = own_second ? rl_f(t.x2, l2) : rl_f(t.x1, l2);
+        b.y2 = own_second ? rl_f(t.y2, l2) : rl_f(t.y1, l2);
+        b.c2 = own_second ? rl_f(t.c2, l2) : rl_f(t.c1, l2);
+        return b;
+    }
     b.k1 = wave_max_u64(t.k1);
     b.k2 = wave_max_u64(t.k1 == b.k1 ? t.k2 : t.k1);
     const uint64_t m1 = __ballot(t.k1 == b.k1 && b.k1 != 0);
@@ -356,24 +386,27 @@ __device__ __forceinline__ ColQuery make_query(float x, float y, float xy_scale)
 // with the column's position k as its index.
 template <bool MAXM>
 __device__ __forceinline__ void consider_vals(const ColQuery &q, float c0, float c1, float c2, float tx,
-                                              float ty, float tc, int o, Top2 &t, int &m) {
+                                              float ty, float tc, int o, Top2 &t) {
     if (c1 < q.lo_x || c1 > q.hi_x || c2 < q.lo_y || c2 > q.hi_y) return;
     const float dx = q.x - c1, dy = q.y - c2;
     const float dd = sqrtf(dx * dx + dy * dy);  // np.linalg.norm(axis=0)
     const float qq = (-0.5f * (dd * dd)) / q.sigma2;
+#ifdef PP_EXP_FEXP
+    const float score = expf(qq) * c0;  // timing experiment only
+#else
     const float score = (float)exp((double)qq) * c0;  // np.exp, correctly rounded
-    m++;
+#endif
     top2_insert(t, cand_key<MAXM>(score, o), tx, ty, tc);
 }
 
 template <bool MAXM, bool PACKED>
 __device__ __forceinline__ void consider(const float *__restrict__ cf, int64_t hw, const ColQuery &q,
-                                         int k, Top2 &t, int &m) {
+                                         int k, Top2 &t) {
     const float c1 = cf[hw + k], c2 = cf[2 * hw + k], c0 = cf[k];
     const float tx = cf[(PACKED ? 3 : 5) * hw + k], ty = cf[(PACKED ? 4 : 6) * hw + k];
     const float tc = cf[(PACKED ? 5 : 8) * hw + k];
     const int o = PACKED ? __float_as_int(cf[6 * hw + k]) : k;
-    consider_vals<MAXM>(q, c0, c1, c2, tx, ty, tc, o, t, m);
+    consider_vals<MAXM>(q, c0, c1, c2, tx, ty, tc, o, t);
 }
 
 // a set-B column: concatenated cell index -> the head's raw CAF values (caf_scored.py:58-81
@@ -388,7 +421,7 @@ struct RawSet {
 
 template <bool MAXM>
 __device__ __forceinline__ void consider_raw(const GrowArgs &g, const RawSet &r, const ColQuery &q,
-                                             int k, Top2 &t, int &m) {
+                                             int k, Top2 &t) {
     const int key = r.idx[k];
     const Heads &h = g.heads;
     int hm = 0, cell = key;
@@ -413,19 +446,17 @@ __device__ __forceinline__ void consider_raw(const GrowArgs &g, const RawSet &r,
     const float dd = sqrtf(dx * dx + dy * dy);
     const float qq = (-0.5f * (dd * dd)) / q.sigma2;
     const float score = (float)exp((double)qq) * c0;
-    m++;
     top2_insert(t, cand_key<MAXM>(score, key), tx, ty, tc);
 }
 
 // _target_with_blend / _target_with_maxscore (cifcaf.py:147-192) on the merged top-2
 template <bool MAXM>
-__device__ void finish_connection(const Top2 &t, int m, float out[4]) {
-    m = wave_total(m);
-    if (m == 0) {
+__device__ __forceinline__ void finish_connection(const Top2 &t, float out[4]) {
+    const Best2 b = top2_wave(t);
+    if (b.k1 == 0) {  // no candidate (every candidate's key is nonzero)
         out[0] = out[1] = out[2] = out[3] = 0.0f;
         return;
     }
-    const Best2 b = top2_wave(t);
     const float s1 = key_score(b.k1), s2 = key_score(b.k2);
     if (MAXM) {
         out[0] = b.x1;
@@ -434,7 +465,9 @@ __device__ void finish_connection(const Top2 &t, int m, float out[4]) {
         out[3] = s1;
         return;
     }
-    if (m == 1 || s2 < 0.01f || s2 < 0.5f * s1) {
+    // one candidate (len(scores) == 1): k2 = 0, s2 = 0.0 takes this branch with the same
+    // result
+    if (s2 < 0.01f || s2 < 0.5f * s1) {
         out[0] = b.x1;
         out[1] = b.y1;
         out[2] = b.c1;
@@ -471,9 +504,8 @@ __device__ void grow_connection_flat(const float *__restrict__ cf, int n, int64_
     const int lane = threadIdx.x & 63;
     const ColQuery q = make_query(x, y, xy_scale);
     Top2 t = top2_empty();
-    int m = 0;
-    for (int i = lane; i < n; i += 64) consider<MAXM, false>(cf, hw, q, i, t, m);
-    finish_connection<MAXM>(t, m, out);
+    for (int i = lane; i < n; i += 64) consider<MAXM, false>(cf, hw, q, i, t);
+    finish_connection<MAXM>(t, out);
 }
 
 #ifdef PP_STAMPS
@@ -491,7 +523,7 @@ __device__ uint64_t *g_gc_stamps;  // diagnostic: [img][4] section sums of grow_
 // bucketed column set (caf_bucketed_kernel): visit only the buckets the 2*scale box
 // overlaps (+ the NaN-source bucket); segments flattened over the 64 lanes
 template <bool MAXM, bool RAW>
-__device__ void grow_connection(const GrowArgs &g, const float *__restrict__ cf, const RawSet &raw,
+__device__ __forceinline__ void grow_connection(const GrowArgs &g, const float *__restrict__ cf, const RawSet &raw,
                                 const int *__restrict__ off, float x, float y, float xy_scale,
                                 float out[4]) {
     const int lane = threadIdx.x & 63;
@@ -501,7 +533,6 @@ __device__ void grow_connection(const GrowArgs &g, const float *__restrict__ cf,
     const int64_t hw = g.col_cap;
     const ColQuery q = make_query(x, y, xy_scale);
     Top2 t = top2_empty();
-    int m = 0;
     int bx0, bx1, by0, by1;
     if (q.lo_x != q.lo_x || q.hi_x != q.hi_x || q.lo_y != q.lo_y || q.hi_y != q.hi_y) {
         bx0 = 0;  // NaN bounds pass every column (every comparison is false): scan all
@@ -545,14 +576,14 @@ __device__ void grow_connection(const GrowArgs &g, const float *__restrict__ cf,
             }
             if (k >= 0) {
                 if (RAW)
-                    consider_raw<MAXM>(g, raw, q, k, t, m);
+                    consider_raw<MAXM>(g, raw, q, k, t);
                 else
-                    consider<MAXM, true>(cf, hw, q, k, t, m);
+                    consider<MAXM, true>(cf, hw, q, k, t);
             }
         }
         GSTAMP(1);
     }
-    finish_connection<MAXM>(t, m, out);
+    finish_connection<MAXM>(t, out);
     GSTAMP(2);
 }
 
@@ -583,7 +614,7 @@ __device__ __forceinline__ const int *col_offs(const GrowArgs &g, int set, int i
 }
 
 // cifcaf.py:194-217 for start joint (jx, jy, jv, js) along CAF caf_i in direction fwd
-__device__ void connection_value(const GrowArgs &g, int img, int set, int caf_i, int fwd,
+__device__ __forceinline__ void connection_value(const GrowArgs &g, int img, int set, int caf_i, int fwd,
                                  float jx, float jy, float jv, float js, bool reverse_match,
                                  float out[4]) {
     const int df = fwd ? 1 : 0, db = fwd ? 0 : 1;
@@ -670,7 +701,7 @@ __device__ __forceinline__ bool slot_less(const Frontier &F, int a, int b) {
 }
 
 // PriorityQueue.get(): remove and return the smallest live entry (false when empty)
-__device__ bool frontier_pop(Frontier &F, Entry &e) {
+__device__ __forceinline__ bool frontier_pop(Frontier &F, Entry &e) {
     const int lane = threadIdx.x & 63;
     int lb = -1;
     if (F.st[0]) lb = 0;
@@ -726,7 +757,7 @@ __device__ bool frontier_pop(Frontier &F, Entry &e) {
 }
 
 // add_to_frontier (cifcaf.py:251-263): the start joint's slots in dict order, one pass
-__device__ void add_to_frontier(const GrowArgs &g, GrowLDS &L, Frontier &F, float av, int start,
+__device__ __forceinline__ void add_to_frontier(const GrowArgs &g, GrowLDS &L, Frontier &F, float av, int start,
                                 float start_v, int &nfr, uint64_t added[2]) {
     const int lane = threadIdx.x & 63;
     const int lo = g.j_off[start], hi = g.j_off[start + 1];
@@ -758,10 +789,10 @@ __device__ void add_to_frontier(const GrowArgs &g, GrowLDS &L, Frontier &F, floa
 // An unevaluated frontier entry (j, k) is evaluated when popped (cifcaf.py:275-279), but
 // its connection_value depends only on the CAF columns and on joint j, which never changes
 // once set.  So when joint j enters the frontier, the connections of all its new entries
-// are computed at once: up to kAhead edges, each direction's column rows of all of them
-// loaded in ONE round trip (flat scan of small set-A column sets, <= kFlatCols columns,
-// count from LDS), instead of two dependent round trips (bucket offsets, then columns) per
-// edge and direction.  The pop then takes the stored result; the frontier order, the
+// are computed at once: up to kAhead edges, the column rows of both directions of all of
+// them loaded in ONE round trip (flat scan of small set-A column sets, <= kFlatCols
+// columns, count from LDS), instead of two dependent round trips (bucket offsets, then
+// columns) per edge and direction.  The pop then takes the stored result; the frontier order, the
 // evaluation results and everything the reference observes are unchanged.  Edges whose
 // sets are larger stay lazy (grow_connection over the buckets).
 constexpr int kAhead = 2;
@@ -779,6 +810,75 @@ __device__ __forceinline__ void flat_load(const float *__restrict__ cf, int64_t 
     }
 }
 
+// Set-A column sets staged in LDS by the seed loop: every small set (<= kFlatCols columns)
+// that fits kColLds floats, in (CAF, direction) order, column-major (kColPad floats per
+// column: two 16-byte reads).  cofs[q] = its offset, -1 = global.
+constexpr int kColPad = 8;
+constexpr int kColLds = 20480;  // 80 KB
+struct ColStage {
+    const int *ncol;   // set-A column counts per (CAF, direction)
+    const int *cofs;
+    const float *lds;
+};
+
+// the same from the LDS copy of the set (offset `lo`, -1 = not staged)
+__device__ __forceinline__ void flat_load_set(const float *__restrict__ cf, int64_t hw, int n,
+                                              const float *lds, int lo,
+                                              float v[kFlatPer][kColRows]) {
+    if (lo < 0) {
+        flat_load(cf, hw, n, v);
+        return;
+    }
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int p = 0; p < kFlatPer; p++) {
+        const int k = p * 64 + lane;
+        float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f), b = a;
+        if (k < n) {
+            const float4 *c = reinterpret_cast<const float4 *>(lds + lo + k * kColPad);
+            a = c[0];
+            b = c[1];
+        }
+        v[p][0] = a.x;
+        v[p][1] = a.y;
+        v[p][2] = a.z;
+        v[p][3] = a.w;
+        v[p][4] = b.x;
+        v[p][5] = b.y;
+        v[p][6] = b.z;
+    }
+}
+
+// per directed-edge slot (one per lane and half, like the Frontier): both directions' set
+// sizes and LDS offsets packed as (count << 16) | (offset + 1), and whether both are small
+struct SlotSets {
+    int f[2], b[2];
+    uint64_t small[2];
+};
+
+__device__ __forceinline__ SlotSets slot_sets(const GrowArgs &g, const ColStage &cs) {
+    const int lane = threadIdx.x & 63;
+    SlotSets t;
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const int d = lane + 64 * r;
+        int f = 0, b = 0;
+        bool small = false;
+        if (d < g.nd) {
+            const int caf = g.d_caf[d], df = g.d_fwd[d] ? 1 : 0;
+            const int qf = caf * 2 + df, qb = caf * 2 + 1 - df;
+            const int nf = cs.ncol[qf], nb = cs.ncol[qb];
+            small = nf <= kFlatCols && nb <= kFlatCols;
+            f = (nf << 16) | (cs.cofs[qf] + 1);
+            b = (nb << 16) | (cs.cofs[qb] + 1);
+        }
+        t.f[r] = f;
+        t.b[r] = b;
+        t.small[r] = __ballot(small);
+    }
+    return t;
+}
+
 // grow_connection over every column of a flat-loaded set (same columns pass caf_center_s
 // as through the buckets; the merge is independent of visiting order: unique keys)
 template <bool MAXM>
@@ -787,90 +887,76 @@ __device__ __forceinline__ void flat_query(const float v[kFlatPer][kColRows], in
     const int lane = threadIdx.x & 63;
     const ColQuery q = make_query(x, y, xy_scale);
     Top2 t = top2_empty();
-    int m = 0;
 #pragma unroll
     for (int p = 0; p < kFlatPer; p++)
         if (p * 64 + lane < n)
             consider_vals<MAXM>(q, v[p][0], v[p][1], v[p][2], v[p][3], v[p][4], v[p][5],
-                                __float_as_int(v[p][6]), t, m);
-    finish_connection<MAXM>(t, m, out);
+                                __float_as_int(v[p][6]), t);
+    finish_connection<MAXM>(t, out);
 }
 
 // the new entries `added` (slot masks, add_to_frontier) of a start joint: connection_value
 // with reverse_match (cifcaf.py:194-217) for those whose two column sets are small
 template <bool MAXM>
-__device__ void eval_ahead(const GrowArgs &g, Frontier &F, int img, const int *ncol, uint64_t r0,
-                           uint64_t r1, float ax, float ay, float av, float as) {
+__device__ __forceinline__ void eval_ahead(const GrowArgs &g, Frontier &F, int img, const ColStage &cs,
+                                           const SlotSets &ss, uint64_t r0, uint64_t r1, float ax,
+                                           float ay, float av, float as) {
     const int lane = threadIdx.x & 63;
     const int64_t hw = g.col_cap;
+    r0 &= ss.small[0];  // the others stay lazy
+    r1 &= ss.small[1];
     while (r0 | r1) {
         int sl[kAhead];
 #pragma unroll
-        for (int b = 0; b < kAhead; b++) {  // the next kAhead slots with small sets
+        for (int b = 0; b < kAhead; b++) {  // the next kAhead slots
             sl[b] = -1;
-            while (r0 | r1) {
-                const int d = r0 ? __ffsll((unsigned long long)r0) - 1
-                                 : 64 + __ffsll((unsigned long long)r1) - 1;
-                if (r0)
-                    r0 &= r0 - 1;
-                else
-                    r1 &= r1 - 1;
-                const int caf = g.d_caf[d], df = g.d_fwd[d] ? 1 : 0;
-                if (ncol[caf * 2 + df] <= kFlatCols && ncol[caf * 2 + 1 - df] <= kFlatCols) {
-                    sl[b] = d;
-                    break;
-                }
+            if (r0) {
+                sl[b] = __ffsll((unsigned long long)r0) - 1;
+                r0 &= r0 - 1;
+            } else if (r1) {
+                sl[b] = 64 + __ffsll((unsigned long long)r1) - 1;
+                r1 &= r1 - 1;
             }
         }
-        if (sl[0] < 0) break;
-        float v[kAhead][kFlatPer][kColRows];
-        float nx[kAhead][4], jx[kAhead], jy[kAhead], jv[kAhead], js[kAhead];
-        // forward queries: all columns of every edge in one round trip
+        // both directions' columns of every edge at once: the reverse query's set is known
+        // before the forward result (only its start point is not)
+        float vf[kAhead][kFlatPer][kColRows], vb[kAhead][kFlatPer][kColRows];
+        int nf[kAhead], nb[kAhead], jj[kAhead];
 #pragma unroll
         for (int b = 0; b < kAhead; b++) {
             if (sl[b] < 0) continue;
-            const int d = sl[b], caf = g.d_caf[d], df = g.d_fwd[d] ? 1 : 0;
-            flat_load(col_set(g, 0, img, caf, df), hw, ncol[caf * 2 + df], v[b]);
+            const int d = sl[b], l = d & 63;
+            const bool h = d >= 64;
+            const int pf = rl_i(h ? ss.f[1] : ss.f[0], l), pb = rl_i(h ? ss.b[1] : ss.b[0], l);
+            const int caf = rl_i(h ? F.scaf[1] : F.scaf[0], l);
+            const int df = rl_i(h ? F.sfwd[1] : F.sfwd[0], l) ? 1 : 0;
+            jj[b] = rl_i(h ? F.sj[1] : F.sj[0], l);
+            nf[b] = pf >> 16;
+            nb[b] = pb >> 16;
+            flat_load_set(col_set(g, 0, img, caf, df), hw, nf[b], cs.lds, (pf & 0xFFFF) - 1, vf[b]);
+            flat_load_set(col_set(g, 0, img, caf, 1 - df), hw, nb[b], cs.lds, (pb & 0xFFFF) - 1,
+                          vb[b]);
         }
 #pragma unroll
         for (int b = 0; b < kAhead; b++) {
             if (sl[b] < 0) continue;
-            const int d = sl[b], j = g.d_j[d], caf = g.d_caf[d], df = g.d_fwd[d] ? 1 : 0;
-            jx[b] = rl_f(ax, j);
-            jy[b] = rl_f(ay, j);
-            jv[b] = rl_f(av, j);
-            js[b] = rl_f(as, j);
-            flat_query<MAXM>(v[b], ncol[caf * 2 + df], jx[b], jy[b], max0(js[b]), nx[b]);
-        }
-        // reverse queries from the new points (cifcaf.py:210-214), again one round trip
-        bool ok[kAhead];
-#pragma unroll
-        for (int b = 0; b < kAhead; b++) {
-            ok[b] = false;
-            if (sl[b] < 0) continue;
-            const float ks = sqrtf(nx[b][3] * jv[b]);
-            ok[b] = !(ks < g.cfg.keypoint_threshold) && nx[b][3] != 0.0f;
-            if (!ok[b]) continue;
-            const int d = sl[b], caf = g.d_caf[d], db = g.d_fwd[d] ? 0 : 1;
-            flat_load(col_set(g, 0, img, caf, db), hw, ncol[caf * 2 + db], v[b]);
-        }
-#pragma unroll
-        for (int b = 0; b < kAhead; b++) {
-            if (sl[b] < 0) continue;
+            const int d = sl[b], j = jj[b];
+            const float jx = rl_f(ax, j), jy = rl_f(ay, j), jv = rl_f(av, j), js = rl_f(as, j);
+            float nx[4];
+            flat_query<MAXM>(vf[b], nf[b], jx, jy, max0(js), nx);
             float res[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (ok[b]) {
-                const int d = sl[b], caf = g.d_caf[d], db = g.d_fwd[d] ? 0 : 1;
+            const float ks = sqrtf(nx[3] * jv);
+            if (!(ks < g.cfg.keypoint_threshold) && nx[3] != 0.0f) {
+                // reverse query from the new point (cifcaf.py:210-214)
                 float rv[4];
-                flat_query<MAXM>(v[b], ncol[caf * 2 + db], nx[b][0], nx[b][1], max0(nx[b][2]), rv);
-                const float xy_scale_s = max0(js[b]);
-                if (rv[2] != 0.0f && !(fabsf(jx[b] - rv[0]) + fabsf(jy[b] - rv[1]) > xy_scale_s)) {
-                    res[0] = nx[b][0];
-                    res[1] = nx[b][1];
-                    res[2] = nx[b][2];
-                    res[3] = sqrtf(nx[b][3] * jv[b]);
+                flat_query<MAXM>(vb[b], nb[b], nx[0], nx[1], max0(nx[2]), rv);
+                if (rv[2] != 0.0f && !(fabsf(jx - rv[0]) + fabsf(jy - rv[1]) > max0(js))) {
+                    res[0] = nx[0];
+                    res[1] = nx[1];
+                    res[2] = nx[2];
+                    res[3] = ks;
                 }
             }
-            const int d = sl[b];
             if (lane == (d & 63)) {
                 if (d < 64) {
                     F.pc[0] = 1;
@@ -891,11 +977,11 @@ __device__ void eval_ahead(const GrowArgs &g, Frontier &F, int img, const int *n
 }
 
 // _grow (cifcaf.py:247-307) on the record in L.a (joint data mirrored into registers).
-// AHEAD (seed loop: set A, reverse_match): new entries' connections via eval_ahead, with
-// ncol = the image's set-A column counts per (CAF, direction).
+// AHEAD (seed loop: set A, reverse_match): new entries' connections via eval_ahead from
+// the image's set-A column counts and LDS-staged sets.
 template <bool AHEAD>
-__device__ void grow(const GrowArgs &g, GrowLDS &L, int img, int set, bool reverse_match,
-                     const int *ncol = nullptr) {
+__device__ __forceinline__ void grow(const GrowArgs &g, GrowLDS &L, int img, int set, bool reverse_match,
+                                     const ColStage &cs = ColStage{}) {
     const int lane = threadIdx.x & 63;
     const int K = g.K;
     float ax = 0.0f, ay = 0.0f, av = 0.0f, as = 0.0f;
@@ -923,13 +1009,15 @@ __device__ void grow(const GrowArgs &g, GrowLDS &L, int img, int set, bool rever
         F.px[r] = F.py[r] = F.ps[r] = F.pv[r] = 0.0f;
     }
     const bool maxm = g.cfg.connection_method == 1;
+    SlotSets ss{};
+    if (AHEAD) ss = slot_sets(g, cs);
     auto ahead = [&](const uint64_t added[2]) {
         if (!AHEAD || !(added[0] | added[1])) return;
         FSTAMP_BEGIN
         if (maxm)
-            eval_ahead<true>(g, F, img, ncol, added[0], added[1], ax, ay, av, as);
+            eval_ahead<true>(g, F, img, cs, ss, added[0], added[1], ax, ay, av, as);
         else
-            eval_ahead<false>(g, F, img, ncol, added[0], added[1], ax, ay, av, as);
+            eval_ahead<false>(g, F, img, cs, ss, added[0], added[1], ax, ay, av, as);
         FSTAMP_END(L, 1)
     };
     for (int j = 0; j < K; j++) {  // seeding the frontier (cifcaf.py:288-291)
@@ -1095,7 +1183,7 @@ __device__ __forceinline__ OccGrid occ_grid(uint8_t *p, int f, int h, int w) {
 __device__ __forceinline__ long round_half_even(float x) { return (long)rintf(x); }
 
 // Occupancy.get (occupancy.py:41-47): nonzero at floor((x, y) / reduction), clipped
-__device__ bool occ_get(const OccGrid &o, int f, float x, float y, float red) {
+__device__ __forceinline__ bool occ_get(const OccGrid &o, int f, float x, float y, float red) {
     if (f >= o.f) return true;
     if (o.h <= 0 || o.w <= 0) return false;  // the reference reads out of bounds here
     x = clip_ref(x / red, 0.0f, (float)(o.w - 1));
@@ -1105,7 +1193,7 @@ __device__ bool occ_get(const OccGrid &o, int f, float x, float y, float red) {
 }
 
 // Occupancy.set box (occupancy.py:31-39 + utils.py:61-66) of joint f; false when empty
-__device__ bool occ_box(const GrowArgs &g, const OccGrid &o, int f, float x, float y, float sigma,
+__device__ __forceinline__ bool occ_box(const GrowArgs &g, const OccGrid &o, int f, float x, float y, float sigma,
                         int box[4]) {
     if (f >= o.f) return false;
     const float red = (float)g.cfg.occupancy_reduction;
@@ -1134,7 +1222,7 @@ __device__ bool occ_box(const GrowArgs &g, const OccGrid &o, int f, float x, flo
 // occupancy planes, so the per-joint `+= 1` boxes are independent and spread over the 64
 // lanes.  Each marked box is logged for occ_clear.  Collective (all 64 lanes).
 template <typename MarkFn>
-__device__ void occ_mark(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccGrid &o,
+__device__ __forceinline__ void occ_mark(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccGrid &o,
                          const float (*xy)[3], const float *scales, int K, MarkFn mark) {
     const int lane = threadIdx.x & 63;
     int box[4] = {0, 0, 0, 0};
@@ -1229,7 +1317,7 @@ __device__ void occ_mark(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccGr
 }
 
 // zero every box the launch marked, so the next launch starts from a clean grid
-__device__ void occ_clear(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccGrid &o) {
+__device__ __forceinline__ void occ_clear(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccGrid &o) {
     wave_sync();
     const int n = L.log_n < g.log_cap ? L.log_n : g.log_cap;
     const int lane = threadIdx.x & 63;
@@ -1274,7 +1362,7 @@ __device__ double pw_sum(const double *a, int K) {
     return res;
 }
 
-__device__ void copy_ann(pp_ann *dst, const pp_ann *src) {
+__device__ __forceinline__ void copy_ann(pp_ann *dst, const pp_ann *src) {
     const uint32_t *s = reinterpret_cast<const uint32_t *>(src);
     uint32_t *d = reinterpret_cast<uint32_t *>(dst);
     constexpr int nw = sizeof(pp_ann) / 4;
@@ -1325,7 +1413,18 @@ __device__ void sort_by_score(int *perm, int np, int n, const double *score) {
 // Helpers pick free seeds after the committed one that lie far (kSpecFar joint scales,
 // Chebyshev) from it, from each other and from the cached ones, since seeds near an
 // annotation's joints are the ones its occupancy marks will cover.
+//
+// Nothing waits for the slowest wave: wave 0 hands a seed to each IDLE helper when it has
+// to grow one itself, and a helper publishes its annotation (cache slot state 2) whenever
+// it finishes.  Wave 0 waits on a helper only for the seed it needs next, if that helper
+// is still growing it.  The handshake is LDS flags with workgroup-scope acquire/release.
+#if defined(PP_EXP_W4)
+constexpr int kSeedWaves = 4;
+#elif defined(PP_EXP_W6)
+constexpr int kSeedWaves = 6;
+#else
 constexpr int kSeedWaves = 8;      // 16 (cache 32, scan 256): 1.79 vs 1.28 ms per cfg3 step
+#endif
 constexpr int kSpecCache = 16;     // speculative annotations kept per image
 constexpr int kSpecScan = 128;     // seeds after the committed one examined per round
 // distance (joint scales) a helper's seed keeps from the committed one and from the
@@ -1334,14 +1433,21 @@ constexpr int kSpecScan = 128;     // seeds after the committed one examined per
 constexpr float kSpecFar = 4.0f;
 
 struct SeedLoopShared {
-    int task[kSeedWaves];          // seed each wave grows this round (-1 idle)
-    int task_slot[kSeedWaves];     // cache slot a helper's annotation goes to
+    int task[kSeedWaves];          // seed a helper is to grow (-1 idle), set by wave 0
+    int task_slot[kSeedWaves];     // cache slot its annotation goes to
     int cache_seed[kSpecCache];    // seed index held by a cache slot (< current: dead)
     float cache_x[kSpecCache], cache_y[kSpecCache], cache_s[kSpecCache];  // seed position
-    int cache_ready[kSpecCache];   // the slot's annotation is grown (joints below valid)
+    int cache_state[kSpecCache];   // 0 free, 1 being grown, 2 grown (joints below valid)
     float4 cache_j[kSpecCache][kKP];  // its joints (x, y, v, scale)
     int done;
 };
+
+__device__ __forceinline__ int lds_acquire(int *p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_release(int *p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 __device__ __forceinline__ bool spec_far(float far, float xa, float ya, float sa, float xb,
                                          float yb, float sb) {
@@ -1350,7 +1456,7 @@ __device__ __forceinline__ bool spec_far(float far, float xa, float ya, float sa
 }
 
 // Annotation(keypoints, out_skeleton).add(f, (x, y, v)); joint_scales[f] = s
-__device__ void ann_from_seed(GrowLDS &L, const pp_seed &sd, int K, int img) {
+__device__ __forceinline__ void ann_from_seed(GrowLDS &L, const pp_seed &sd, int K, int img) {
     const int lane = threadIdx.x & 63;
     uint32_t *z = reinterpret_cast<uint32_t *>(&L.a);
     for (int t = lane; t < (int)(sizeof(pp_ann) / 4); t += 64) z[t] = 0u;
@@ -1370,11 +1476,39 @@ __global__ __launch_bounds__(64 * kSeedWaves) void seed_loop_kernel(GrowArgs g) 
     __shared__ GrowLDS Ls[kSeedWaves];
     __shared__ SeedLoopShared S;
     __shared__ int s_ncol[2 * PP_MAX_EDGES];  // set-A column counts per (CAF, direction)
+    __shared__ int s_cofs[2 * PP_MAX_EDGES];  // their LDS offsets in s_cols (-1: global)
+    __shared__ float s_cols[kColLds];
     const int img = blockIdx.x;
     const int K = g.K;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     GrowLDS &L = Ls[wave];
     for (int q = threadIdx.x; q < 2 * g.C; q += blockDim.x) s_ncol[q] = col_offs(g, 0, img, q >> 1, q & 1)[g.nb];
+    __syncthreads();
+    if (threadIdx.x == 0) {  // LDS placement of the small sets, in order while they fit
+        int o = 0;
+        for (int q = 0; q < 2 * g.C; q++) {
+            const int sz = kColPad * s_ncol[q];
+            const bool fit = s_ncol[q] <= kFlatCols && o + sz <= kColLds;
+            s_cofs[q] = fit ? o : -1;
+            o += fit ? sz : 0;
+        }
+    }
+    __syncthreads();
+    for (int q = wave; q < 2 * g.C; q += kSeedWaves) {  // one set per wave
+        const int n = s_ncol[q];
+        if (s_cofs[q] < 0 || n == 0) continue;
+        const float *cf = col_set(g, 0, img, q >> 1, q & 1);
+        float *dst = s_cols + s_cofs[q];
+        for (int k = lane; k < n; k += 64) {
+            float c[kColRows];
+#pragma unroll
+            for (int r = 0; r < kColRows; r++) c[r] = cf[r * g.col_cap + k];
+            float4 *o = reinterpret_cast<float4 *>(dst + k * kColPad);
+            o[0] = make_float4(c[0], c[1], c[2], c[3]);
+            o[1] = make_float4(c[4], c[5], c[6], 0.0f);
+        }
+    }
+    const ColStage cstage{s_ncol, s_cofs, s_cols};
     if (lane == 0) {
         L.status = 0;
         L.log_n = 0;
@@ -1384,8 +1518,9 @@ __global__ __launch_bounds__(64 * kSeedWaves) void seed_loop_kernel(GrowArgs g) 
     }
     if (threadIdx.x < kSpecCache) {
         S.cache_seed[threadIdx.x] = -1;
-        S.cache_ready[threadIdx.x] = 0;
+        S.cache_state[threadIdx.x] = 0;
     }
+    if (threadIdx.x < kSeedWaves) S.task[threadIdx.x] = -1;
     if (threadIdx.x == 0) S.done = 0;
     __syncthreads();
 
@@ -1416,140 +1551,164 @@ __global__ __launch_bounds__(64 * kSeedWaves) void seed_loop_kernel(GrowArgs g) 
                  [&](int j) { return src->data[j][2] != 0.0f; });
     };
 
-    for (;;) {
-        if (wave == 0) {
+    if (wave > 0) {  // helper: grow the seeds wave 0 hands over until it is done
+        for (;;) {
+            int my;
             for (;;) {
-                // the next free seed (cifcaf.py:100-104): 64 occupancy tests per step
-                int t = -1;
-                while (s < n_seeds) {
-                    const int idx = s + lane;
-                    bool is_free = false;
-                    if (idx < n_seeds) {
-                        const pp_seed c = seeds[idx];
-                        is_free = !occ_get(occ, c.field, c.x, c.y, red);
-                    }
-                    const uint64_t m = __ballot(is_free);
-                    if (m == 0) {
-                        s += 64;
-                        continue;
-                    }
-                    t = s + __ffsll((unsigned long long)m) - 1;
-                    break;
-                }
-                STAMP(0);
-                if (t < 0 || n_anns >= g.ann_cap) {
-                    if (lane == 0) {
-                        if (t >= 0) L.status |= PP_ST_ANN_OVERFLOW;
-                        S.done = 1;
-                    }
-                    break;
-                }
-                const int cs = lane < kSpecCache ? S.cache_seed[lane] : -1;
-                const uint64_t hit = __ballot(lane < kSpecCache && cs == t);
-                if (hit) {  // a helper grew it already
-                    const int slot = __ffsll((unsigned long long)hit) - 1;
-                    commit(&cache[slot]);
-                    s = t + 1;
-#ifdef PP_STAMPS
-                    n_hits++;
+                my = lds_acquire(&S.task[wave]);
+                if (my >= 0 || lds_acquire(&S.done)) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (my < 0) break;
+            const int q = S.task_slot[wave];
+            ann_from_seed(L, seeds[my], K, img);
+            grow<true>(g, L, img, 0, true, cstage);
+            copy_ann(&cache[q], &L.a);
+            if (lane < kKP)
+                S.cache_j[q][lane] = make_float4(L.a.data[lane][0], L.a.data[lane][1],
+                                                 L.a.data[lane][2], L.a.joint_scales[lane]);
+            // the record's global stores complete before the flag (the workgroup-scope
+            // release alone does not wait for them)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            wave_sync();
+            if (lane == 0) {
+                lds_release(&S.cache_state[q], 2);
+                lds_release(&S.task[wave], -1);
+            }
+            wave_sync();
+        }
+    } else {
+#ifndef PP_EXP_NOPRIO
+        __builtin_amdgcn_s_setprio(3);  // the committer is the critical path: issue first
 #endif
-                    STAMP(4);
+        for (;;) {
+            // the next free seed (cifcaf.py:100-104): 64 occupancy tests per step
+            int t = -1;
+            while (s < n_seeds) {
+                const int idx = s + lane;
+                bool is_free = false;
+                if (idx < n_seeds) {
+                    const pp_seed c = seeds[idx];
+                    is_free = !occ_get(occ, c.field, c.x, c.y, red);
+                }
+                const uint64_t m = __ballot(is_free);
+                if (m == 0) {
+                    s += 64;
                     continue;
                 }
-                // plan a round: t on wave 0, far-away free seeds on the helpers
-                const pp_seed st = seeds[t];
-                int nsp = 0;
-                const int scan_end = min(n_seeds, t + 1 + kSpecScan);
-                for (int base = t + 1; base < scan_end && nsp < kSeedWaves - 1; base += 64) {
-                    const int idx = base + lane;
-                    bool ok = idx < scan_end;
-                    pp_seed c{};
-                    if (ok) {
-                        c = seeds[idx];
-                        ok = spec_far(g.spec_far, c.x, c.y, c.s, st.x, st.y, st.s) &&
-                             !occ_get(occ, c.field, c.x, c.y, red);
-                    }
-                    // live cache entries (uniform loop): skip seeds they hold or that their
-                    // annotation's occupancy boxes will cover once committed
-                    const int cxi = (int)clip_ref(c.x / red, 0.0f, (float)(occ.w - 1));
-                    const int cyi = (int)clip_ref(c.y / red, 0.0f, (float)(occ.h - 1));
-                    for (int q = 0; q < kSpecCache; q++) {
-                        const int sq = S.cache_seed[q];
-                        if (sq <= t) continue;
-                        if (sq == idx) ok = false;
-                        if (!ok || !S.cache_ready[q]) continue;  // this round's picks: below
-                        const float4 jq = S.cache_j[q][c.field];
-                        int box[4];
-                        if (jq.z != 0.0f && occ_box(g, occ, c.field, jq.x, jq.y, jq.w, box) &&
-                            cxi >= box[0] && cxi < box[1] && cyi >= box[2] && cyi < box[3])
-                            ok = false;
-                    }
-                    uint64_t m = __ballot(ok);
-                    while (m && nsp < kSeedWaves - 1) {
-                        const int l = __ffsll((unsigned long long)m) - 1;
-                        m &= m - 1;
-                        const float cx = rl_f(c.x, l), cy = rl_f(c.y, l), csc = rl_f(c.s, l);
-                        bool far = true;
-                        for (int r = 0; r < nsp; r++) {
-                            const int q = S.task_slot[1 + r];
-                            far = far && spec_far(g.spec_far, cx, cy, csc, S.cache_x[q],
-                                                  S.cache_y[q], S.cache_s[q]);
-                        }
-                        if (!far) continue;
-                        const int cq = lane < kSpecCache ? S.cache_seed[lane] : 0;
-                        const uint64_t freeq = __ballot(lane < kSpecCache && cq < t);
-                        if (!freeq) {
-                            m = 0;
-                            break;
-                        }
-                        const int q = __ffsll((unsigned long long)freeq) - 1;
-                        if (lane == 0) {
-                            S.task[1 + nsp] = base + l;
-                            S.task_slot[1 + nsp] = q;
-                            S.cache_seed[q] = base + l;
-                            S.cache_x[q] = cx;
-                            S.cache_y[q] = cy;
-                            S.cache_s[q] = csc;
-                            S.cache_ready[q] = 0;
-                        }
-                        wave_sync();
-                        nsp++;
-                    }
-                }
-                if (lane == 0) {
-                    S.task[0] = t;
-                    for (int r = 1 + nsp; r < kSeedWaves; r++) S.task[r] = -1;
-                }
-#ifdef PP_STAMPS
-                n_rounds++;
-#endif
-                STAMP(1);
+                t = s + __ffsll((unsigned long long)m) - 1;
                 break;
             }
-        }
-        __syncthreads();
-        if (S.done) break;
-        const int my = S.task[wave];
-        if (my >= 0) {
-            ann_from_seed(L, seeds[my], K, img);
-            grow<true>(g, L, img, 0, true, s_ncol);
-            if (wave > 0) {
-                const int q = S.task_slot[wave];
-                copy_ann(&cache[q], &L.a);
-                if (lane < kKP)
-                    S.cache_j[q][lane] = make_float4(L.a.data[lane][0], L.a.data[lane][1],
-                                                     L.a.data[lane][2], L.a.joint_scales[lane]);
-                if (lane == 0) S.cache_ready[q] = 1;
+            STAMP(0);
+            if (t < 0 || n_anns >= g.ann_cap) {
+                if (lane == 0 && t >= 0) L.status |= PP_ST_ANN_OVERFLOW;
+                break;
             }
-        }
-        __syncthreads();
-        STAMP(2);
-        if (wave == 0) {
+            const int cs = lane < kSpecCache ? S.cache_seed[lane] : -1;
+            const uint64_t hit = __ballot(lane < kSpecCache && cs == t);
+            if (hit) {  // a helper grew it, or is growing it
+                const int slot = __ffsll((unsigned long long)hit) - 1;
+                while (lds_acquire(&S.cache_state[slot]) != 2) __builtin_amdgcn_s_sleep(1);
+                commit(&cache[slot]);
+                s = t + 1;
+#ifdef PP_STAMPS
+                n_hits++;
+#endif
+                STAMP(4);
+                continue;
+            }
+            // hand far-away free seeds to the idle helpers, then grow t here
+            const pp_seed st = seeds[t];
+            const int tk = lane > 0 && lane < kSeedWaves ? lds_acquire(&S.task[lane]) : 0;
+            uint64_t idle = __ballot(lane > 0 && lane < kSeedWaves && tk < 0);
+            // the seeds in flight: later picks keep kSpecFar from them
+            const int cst = lane < kSpecCache ? lds_acquire(&S.cache_state[lane]) : 0;
+            uint64_t fly = __ballot(lane < kSpecCache && cst == 1);
+            const int scan_end = min(n_seeds, t + 1 + kSpecScan);
+            for (int base = t + 1; base < scan_end && idle; base += 64) {
+                const int idx = base + lane;
+                bool ok = idx < scan_end;
+                pp_seed c{};
+                if (ok) {
+                    c = seeds[idx];
+                    ok = spec_far(g.spec_far, c.x, c.y, c.s, st.x, st.y, st.s) &&
+                         !occ_get(occ, c.field, c.x, c.y, red);
+                }
+                // cache entries (uniform loop): skip seeds they hold, seeds that a grown
+                // annotation's occupancy boxes will cover once committed, and seeds near
+                // one still being grown
+                const int cxi = (int)clip_ref(c.x / red, 0.0f, (float)(occ.w - 1));
+                const int cyi = (int)clip_ref(c.y / red, 0.0f, (float)(occ.h - 1));
+                for (int q = 0; q < kSpecCache; q++) {
+                    const int sq = S.cache_seed[q];
+                    if (sq <= t) continue;
+                    if (sq == idx) ok = false;
+                    if (!ok) continue;
+                    if ((fly >> q) & 1) {
+                        ok = spec_far(g.spec_far, c.x, c.y, c.s, S.cache_x[q], S.cache_y[q],
+                                      S.cache_s[q]);
+                        continue;
+                    }
+                    const float4 jq = S.cache_j[q][c.field];
+                    int box[4];
+                    if (jq.z != 0.0f && occ_box(g, occ, c.field, jq.x, jq.y, jq.w, box) &&
+                        cxi >= box[0] && cxi < box[1] && cyi >= box[2] && cyi < box[3])
+                        ok = false;
+                }
+                uint64_t m = __ballot(ok);
+                while (m && idle) {
+                    const int l = __ffsll((unsigned long long)m) - 1;
+                    m &= m - 1;
+                    const float cx = rl_f(c.x, l), cy = rl_f(c.y, l), csc = rl_f(c.s, l);
+                    bool far = true;  // from this plan's earlier picks (now in flight too)
+                    uint64_t f2 = fly;
+                    while (f2) {
+                        const int q = __ffsll((unsigned long long)f2) - 1;
+                        f2 &= f2 - 1;
+                        far = far && spec_far(g.spec_far, cx, cy, csc, S.cache_x[q],
+                                              S.cache_y[q], S.cache_s[q]);
+                    }
+                    if (!far) continue;
+                    // a free slot: never grown into, or grown for a seed already passed
+                    const int cq = lane < kSpecCache ? S.cache_seed[lane] : 0;
+                    const int cst2 = lane < kSpecCache ? S.cache_state[lane] : 1;
+                    const uint64_t freeq = __ballot(lane < kSpecCache &&
+                                                    (cst2 == 0 || (cst2 == 2 && cq < t)));
+                    if (!freeq) {
+                        m = 0;
+                        idle = 0;
+                        break;
+                    }
+                    const int q = __ffsll((unsigned long long)freeq) - 1;
+                    const int w = __ffsll((unsigned long long)idle) - 1;
+                    idle &= idle - 1;
+                    fly |= 1ull << q;
+                    if (lane == 0) {
+                        S.cache_seed[q] = base + l;
+                        S.cache_x[q] = cx;
+                        S.cache_y[q] = cy;
+                        S.cache_s[q] = csc;
+                        S.cache_state[q] = 1;
+                        S.task_slot[w] = q;
+                        lds_release(&S.task[w], base + l);
+                    }
+                    wave_sync();
+                }
+            }
+#ifdef PP_STAMPS
+            n_rounds++;
+#endif
+            STAMP(1);
+            ann_from_seed(L, st, K, img);
+            grow<true>(g, L, img, 0, true, cstage);
+            STAMP(2);
             commit(&L.a);
-            s = S.task[0] + 1;
+            s = t + 1;
             STAMP(3);
         }
+        if (lane == 0) lds_release(&S.done, 1);
     }
+    __syncthreads();  // helpers drained: no wave is still growing into the cache
     if (wave == 0) {
         occ_clear(g, L, log, occ);
         STAMP(5);

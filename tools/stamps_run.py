@@ -40,6 +40,12 @@ for kind, n, h in (('planted', 256, 80), ('uniform', 32, 80)):
             print('    {:14s} {:12.0f}  {:5.1f}%'.format(name, m, 100 * m / max(tot, 1)))
         if ph == 0:
             print('    rounds {:.1f}  cache hits {:.1f}'.format(st[:, 0, 6].mean(), st[:, 0, 7].mean()))
+            per = st[:, 0, :6].sum(axis=1)
+            w = int(np.argmax(per))
+            print('    per-image total: p50 {:.3e} p90 {:.3e} max {:.3e} (image {}: rounds {:.0f}, '
+                  'hits {:.0f}, round_grow {:.3e})'.format(
+                      np.percentile(per, 50), np.percentile(per, 90), per[w], w, st[w, 0, 6],
+                      st[w, 0, 7], st[w, 0, 2]))
         for i, name in ((8, 'n connection'), (9, 'in-grow pop'), (10, 'in-grow connection'),
                         (11, 'in-grow add')):
             print('    {:14s} {:12.0f}'.format(name, st[:, ph, i].mean()))
