@@ -779,7 +779,12 @@ __global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
 // MULTI (cif_hr.py:59-73): groups fold into zero separately and combine by np.maximum;
 // candidates carry their group, and a change of group closes the running fold into res.
 // Across passes res stays in the map and the open group's fold in `aux`.
-constexpr int kSpU = 8;       // cells per thread per compaction round
+#ifdef PP_EXP_SPU16
+constexpr int kSpU = 16;
+#else
+constexpr int kSpU = 32;      // cells per thread per compaction round (confidences in flight)
+#endif
+constexpr int kSpStage = 1024; // kept cells of a round staged in LDS (phase 2's s_cand space)
 
 struct HrSparseArgs {
     Heads h;
@@ -815,14 +820,18 @@ __device__ uint64_t *g_hr_stamps;
 #endif
 
 // Phase 1 of the CifHr kernel: the field's splat list in the reference's order (every
-// group, cif_hr.py:26-40, 55-57) as fold candidates in the field's global list.  Each
-// thread loads kSpU cells per round and one barrier per round orders the (cell batch, wave)
-// counts; s_bits marks the 64x64 tiles the boxes touch (cleared by the caller before the
-// first barrier).  Returns the list length; s_gbeg[g] = start of group g's entries.  Ends
-// with a barrier.
+// group, cif_hr.py:26-40, 55-57) as fold candidates in the field's global list.  A round
+// covers 256 * kSpU cells: each thread loads its kSpU confidences at once (plus the scale
+// of the cells above threshold when a min scale applies), one barrier orders the (cell
+// batch, wave) counts, and the kept cells are staged in LDS (`stage`: kSpStage cell
+// indices) in list order; then one thread per staged cell reads its x, y, scale and writes
+// its candidate.  So a round costs about three memory round trips however many cells it
+// keeps (a round keeping more than kSpStage reads them per batch instead).  s_bits marks
+// the 64x64 tiles the boxes touch (cleared by the caller before the first barrier).
+// Returns the list length; s_gbeg[g] = start of group g's entries.  Ends with a barrier.
 template <bool MULTI>
 __device__ int hr_splat_list(const HrSparseArgs &a, int64_t fld, uint32_t *s_bits,
-                             int (*s_cnt)[kSpU][4], int *s_gbeg) {
+                             int (*s_cnt)[kSpU][4], int *s_gbeg, int *stage) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ng = MULTI ? a.h.n_groups : 1;
     FoldCand *glist = a.list + fld * a.list_cap;
@@ -833,61 +842,95 @@ __device__ int hr_splat_list(const HrSparseArgs &a, int64_t fld, uint32_t *s_bit
         const bool ms_on = (a.h.ms_on >> g) & 1u;
         const float ms_th = a.h.ms_th[g];
         const float len_cifs = (float)a.h.group_size();
+        // candidate of cell `cell` (c > v_th, scale test passed) at list position pos
+        auto emit = [&](const float *p, int hw, int cell, float c, int pos) {
+            const float x = p[hw + cell], y = p[2 * hw + cell], s4 = p[4 * hw + cell];
+            const float cx = x * stride, cy = y * stride;
+            const float sg = (0.5f * s4) * stride;
+            const float sigma = (sg != sg) ? sg : fmaxf(1.0f, sg);  // np.maximum keeps NaN
+            const float v = (c / a.neighbors) / len_cifs;           // v / neighbors / len_cifs
+            const int4 box = splat_box<M_GAUSS_MAX>(cx, cy, 1.0f * sigma, a.hh, a.ww);
+            glist[pos] = make_cand(box, make_float4(cx, cy, v, sigma * sigma));
+            for (int ty = box.z / kTile; ty <= (box.w - 1) / kTile; ty++)
+                for (int tx = box.x / kTile; tx <= (box.y - 1) / kTile; tx++) {
+                    const int t = ty * a.tiles_x + tx;
+                    atomicOr(&s_bits[t >> 5], 1u << (t & 31));
+                }
+        };
         for (int i = 0; i < a.h.group_size(); i++) {
             const int m = a.h.member(g, i);
             const int hw = a.h.cH[m] * a.h.cW[m];
             const float *p = a.h.cif[m] + fld * 5 * (int64_t)hw;
             for (int base = 0; base < hw; base += 256 * kSpU) {
-                float c[kSpU], x[kSpU], y[kSpU], s4[kSpU];
+                float c[kSpU];
 #pragma unroll
                 for (int k = 0; k < kSpU; k++) {
                     const int cell = base + k * 256 + (int)threadIdx.x;
                     c[k] = cell < hw ? p[cell] : NAN;  // NaN: never > v_th
-                    x[k] = y[k] = s4[k] = 0.0f;
+                }
+                uint32_t keep = 0;
+#pragma unroll
+                for (int k = 0; k < kSpU; k++) keep |= (c[k] > a.v_th) ? (1u << k) : 0u;
+                if (ms_on) {  // p[4] > min_scale / stride (cif_hr.py:29-30)
+                    uint32_t km = keep;
+#pragma unroll
+                    for (int k = 0; k < kSpU; k++)
+                        if ((keep >> k) & 1u) {
+                            const int cell = base + k * 256 + (int)threadIdx.x;
+                            if (!(p[4 * hw + cell] > ms_th)) km &= ~(1u << k);
+                        }
+                    keep = km;
                 }
 #pragma unroll
                 for (int k = 0; k < kSpU; k++) {
-                    const int cell = base + k * 256 + (int)threadIdx.x;
-                    if (c[k] > a.v_th) {
-                        x[k] = p[hw + cell];
-                        y[k] = p[2 * hw + cell];
-                        s4[k] = p[4 * hw + cell];
-                    }
-                }
-                bool keep[kSpU];
-                uint64_t bal[kSpU];
-#pragma unroll
-                for (int k = 0; k < kSpU; k++) {
-                    keep[k] = c[k] > a.v_th;
-                    if (keep[k] && ms_on) keep[k] = s4[k] > ms_th;  // p[4] > min_scale / stride
-                    bal[k] = __ballot(keep[k]);
-                    if (lane == 0) s_cnt[buf][k][wave] = __popcll(bal[k]);
+                    const uint64_t bal = __ballot((keep >> k) & 1u);
+                    if (lane == 0) s_cnt[buf][k][wave] = __popcll(bal);
                 }
                 __syncthreads();  // (also orders the s_bits clear before the first atomicOr)
-                int off = running;
-#pragma unroll
+                int off = 0;
+#pragma unroll 4
                 for (int k = 0; k < kSpU; k++) {
                     const int4 q = *reinterpret_cast<const int4 *>(&s_cnt[buf][k][0]);
-                    const int mine = off + (wave > 0 ? q.x : 0) + (wave > 1 ? q.y : 0) +
-                                     (wave > 2 ? q.z : 0);
                     off += q.x + q.y + q.z + q.w;
-                    if (keep[k]) {
-                        const int pos = mine + lane_prefix(bal[k]);
-                        const float cx = x[k] * stride, cy = y[k] * stride;
-                        const float sg = (0.5f * s4[k]) * stride;
-                        const float sigma = (sg != sg) ? sg : fmaxf(1.0f, sg);  // np.maximum keeps NaN
-                        const float v = (c[k] / a.neighbors) / len_cifs;        // v / neighbors / len_cifs
-                        const int4 box = splat_box<M_GAUSS_MAX>(cx, cy, 1.0f * sigma, a.hh, a.ww);
-                        glist[pos] = make_cand(box, make_float4(cx, cy, v, sigma * sigma));
-                        for (int ty = box.z / kTile; ty <= (box.w - 1) / kTile; ty++)
-                            for (int tx = box.x / kTile; tx <= (box.y - 1) / kTile; tx++) {
-                                const int t = ty * a.tiles_x + tx;
-                                atomicOr(&s_bits[t >> 5], 1u << (t & 31));
-                            }
+                }
+                // list position of batch k's kept cell in this thread (ballot order = cell order)
+                auto place = [&](auto fn) {
+                    int o = 0;
+#pragma unroll 4
+                    for (int k = 0; k < kSpU; k++) {
+                        const int4 q = *reinterpret_cast<const int4 *>(&s_cnt[buf][k][0]);
+                        const uint64_t bal = __ballot((keep >> k) & 1u);
+                        if ((keep >> k) & 1u)
+                            fn(base + k * 256 + (int)threadIdx.x,
+                               o + (wave > 0 ? q.x : 0) + (wave > 1 ? q.y : 0) + (wave > 2 ? q.z : 0) +
+                                   lane_prefix(bal));
+                        o += q.x + q.y + q.z + q.w;
+                    }
+                };
+                if (off <= kSpStage) {
+                    place([&](int cell, int pos) { stage[pos] = cell; });
+                    __syncthreads();
+                    for (int e = threadIdx.x; e < off; e += 256) {
+                        const int cell = stage[e];
+                        emit(p, hw, cell, p[cell], running + e);
+                    }
+                } else {  // more than the stage holds: batch by batch (not unrolled)
+                    int o = 0;
+                    for (int k = 0; k < kSpU; k++) {
+                        const int4 q = *reinterpret_cast<const int4 *>(&s_cnt[buf][k][0]);
+                        const uint64_t bal = __ballot((keep >> k) & 1u);
+                        if ((keep >> k) & 1u) {
+                            const int cell = base + k * 256 + (int)threadIdx.x;
+                            emit(p, hw, cell, p[cell],
+                                 running + o + (wave > 0 ? q.x : 0) + (wave > 1 ? q.y : 0) +
+                                     (wave > 2 ? q.z : 0) + lane_prefix(bal));
+                        }
+                        o += q.x + q.y + q.z + q.w;
                     }
                 }
-                running = off;
+                running += off;
                 buf ^= 1;
+                __syncthreads();  // the stage is rewritten by the next round
             }
         }
     }
@@ -897,7 +940,8 @@ __device__ int hr_splat_list(const HrSparseArgs &a, int64_t fld, uint32_t *s_bit
 }
 
 template <bool MULTI>
-__global__ __launch_bounds__(256) void cifhr_sparse_kernel(HrSparseArgs a) {
+// 8 waves per SIMD (<= 64 VGPRs): the kernel is latency-bound, occupancy hides it
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void cifhr_sparse_kernel(HrSparseArgs a) {
     __shared__ uint32_t s_bits[kTileBits / 32];
     __shared__ RowBinLds s_rb;
     __shared__ int s_rowcnt[kMaxBinRows], s_rowoff[kMaxBinRows];  // bins (hr_row_bins)
@@ -915,7 +959,8 @@ __global__ __launch_bounds__(256) void cifhr_sparse_kernel(HrSparseArgs a) {
     if (threadIdx.x < kTileBits / 32) s_bits[threadIdx.x] = 0u;
     if (threadIdx.x == 0) s_next = 0;
 
-    const int total = hr_splat_list<MULTI>(a, fld, s_bits, s_cnt, s_gbeg);
+    const int total = hr_splat_list<MULTI>(a, fld, s_bits, s_cnt, s_gbeg,
+                                           reinterpret_cast<int *>(&s_cand[0][0]));
     const bool use_bins = !MULTI && a.bins_cap > 0 && total > kBinMin;
     if (use_bins)
         hr_row_bins(a.list + fld * a.list_cap, total, a.bins + fld * a.bins_cap, a.bins_cap,

@@ -482,6 +482,12 @@ __device__ __forceinline__ int caf_bucket(float x, float y, int bw, int bh, floa
 // bucket ids.  A set-A stash that overflows (more than kStashA kept columns in a direction)
 // makes pass 2 recompute from the fields, as the non-STASH kernel always does.
 constexpr int kStashA = 256;      // kept columns per direction (set A stash): 29 KB of LDS, 5 workgroups per CU
+// Set A, one head: pass 1 first lists the cells above the threshold (confidence plane only,
+// kConfU loads per thread in flight), then reads the other rows and the CifHr values of the
+// listed cells only: three memory round trips per workgroup instead of three per
+// NT * kU cells.  More than kCandA cells fall back to the batched scan.
+constexpr int kCandA = 1024;
+constexpr int kConfU = 16;
 constexpr int kStashCells = 8192; // cells of all heads (set B stash: u16 bucket per direction)
 constexpr uint16_t kNoBucket = 0xFFFF;
 
@@ -497,7 +503,10 @@ __global__ __launch_bounds__(STASH && INDEX_ONLY ? 512 : 256) void caf_bucketed_
     __shared__ int s_cnt[2][kMaxBuckets + 1];
     __shared__ int s_wsum[2][NW];
     __shared__ __attribute__((aligned(16))) char s_stash[STASH ? (INDEX_ONLY ? 2 * kStashCells * 2 : 2 * kStashA * (int)sizeof(StashCol)) : 16];
-    __shared__ int s_sn[2], s_ovf;
+    __shared__ int s_sn[2], s_ovf, s_nc;
+    constexpr bool kList = STASH && !INDEX_ONLY;
+    __shared__ int s_cand[kList ? kCandA : 1];
+    __shared__ float s_cand_c[kList ? kCandA : 1];
     StashCol *stash_a = reinterpret_cast<StashCol *>(s_stash);       // [2][kStashA]
     uint16_t *stash_b = reinterpret_cast<uint16_t *>(s_stash);       // [2][kStashCells]
     const int64_t fld = blockIdx.x;  // image * C + caf field
@@ -527,6 +536,7 @@ __global__ __launch_bounds__(STASH && INDEX_ONLY ? 512 : 256) void caf_bucketed_
     if (threadIdx.x == 0) {
         s_sn[0] = s_sn[1] = 0;
         s_ovf = 0;
+        s_nc = 0;
     }
     __syncthreads();
 
@@ -590,6 +600,140 @@ __global__ __launch_bounds__(STASH && INDEX_ONLY ? 512 : 256) void caf_bucketed_
 
     // pass 1: bucket histograms (backward sources are (x2, y2), forward (x1, y1)); no
     // barrier inside the loop, so the cells' loads overlap freely
+    // one scored cell of pass 1: histogram counts and the stash
+    auto account = [&](const Batch &B, int k, int cell, int hw, int coff) {
+        const float *nine = B.nine[k];
+        const int bkb = B.kb[k] ? caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e) : -1;
+        const int bkf = B.kf[k] ? caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e) : -1;
+        if (bkb >= 0) atomicAdd(&s_cnt[0][bkb], 1);
+        if (bkf >= 0) atomicAdd(&s_cnt[1][bkf], 1);
+        if (STASH && INDEX_ONLY) {
+            if (cell < hw) {
+                stash_b[coff + cell] = bkb >= 0 ? (uint16_t)bkb : kNoBucket;
+                stash_b[kStashCells + coff + cell] = bkf >= 0 ? (uint16_t)bkf : kNoBucket;
+            }
+        } else if (STASH) {
+            const float key = __int_as_float(coff + cell);
+            if (bkb >= 0) {
+                const int sl = atomicAdd(&s_sn[0], 1);
+                if (sl < kStashA) {
+                    StashCol &e = stash_a[sl];
+                    e.v[0] = B.sb[k];
+                    e.v[1] = nine[5];
+                    e.v[2] = nine[6];
+                    e.v[3] = nine[1];
+                    e.v[4] = nine[2];
+                    e.v[5] = nine[4];
+                    e.v[6] = key;
+                    e.bucket = bkb;
+                } else {
+                    s_ovf = 1;
+                }
+            }
+            if (bkf >= 0) {
+                const int sl = atomicAdd(&s_sn[1], 1);
+                if (sl < kStashA) {
+                    StashCol &e = stash_a[kStashA + sl];
+                    e.v[0] = B.sf[k];
+                    e.v[1] = nine[1];
+                    e.v[2] = nine[2];
+                    e.v[3] = nine[5];
+                    e.v[4] = nine[6];
+                    e.v[5] = nine[8];
+                    e.v[6] = key;
+                    e.bucket = bkf;
+                } else {
+                    s_ovf = 1;
+                }
+            }
+        }
+    };
+
+    bool listed = false;
+    if (kList && a.h.n_caf == 1) {
+        // list the cells above the threshold (confidence plane only)
+        const int hw = a.h.aH[0] * a.h.aW[0];
+        const float *p = a.h.caf[0] + fld * 9 * hw;
+        const int lane = threadIdx.x & 63;
+        for (int base = 0; base < hw; base += NT * kConfU) {
+            float v[kConfU];
+#pragma unroll
+            for (int k = 0; k < kConfU; k++) {
+                const int cell = base + k * NT + (int)threadIdx.x;
+                v[k] = cell < hw ? p[cell] : NAN;
+            }
+#pragma unroll
+            for (int k = 0; k < kConfU; k++) {
+                const bool pass = v[k] > a.th;  // mask = nine[0] > score_th
+                const uint64_t bm = __ballot(pass);
+                if (!bm) continue;
+                int wb = 0;
+                if (lane == 0) wb = atomicAdd(&s_nc, __popcll(bm));
+                wb = __shfl(wb, 0);
+                if (pass) {
+                    const int i = wb + __popcll(bm & ((1ull << lane) - 1));
+                    if (i < kCandA) {
+                        s_cand[i] = base + k * NT + (int)threadIdx.x;
+                        s_cand_c[i] = v[k];
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        listed = s_nc <= kCandA;
+    }
+    if (listed) {
+        const int n = s_nc;
+        const int hw = a.h.aH[0] * a.h.aW[0];
+        const float stride = (float)a.h.astride[0];
+        const float *p = a.h.caf[0] + fld * 9 * hw;
+        const int coff = (int)a.h.caf_off[0];
+        const bool on_min = a.h.dmin_on & 1u, on_max = a.h.dmax_on & 1u;
+        for (int i0 = 0; i0 < n; i0 += NT * kU) {
+            Batch B;
+            int cells[kU];
+#pragma unroll
+            for (int k = 0; k < kU; k++) {
+                const int i = i0 + k * NT + (int)threadIdx.x;
+                cells[k] = i < n ? s_cand[i] : 0;
+                B.nine[k][0] = i < n ? s_cand_c[i] : NAN;
+                B.kb[k] = B.kf[k] = false;
+            }
+#pragma unroll
+            for (int k = 0; k < kU; k++) {
+                if (!(B.nine[k][0] > a.th)) continue;
+#pragma unroll
+                for (int r = 1; r < 9; r++) {
+                    const bool need = r == 1 || r == 2 || r == 4 || r == 5 || r == 6 || r == 8;
+                    B.nine[k][r] = need ? p[r * hw + cells[k]] : 0.0f;  // b1, b2 never read
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kU; k++) {
+                if (!(B.nine[k][0] > a.th)) continue;
+                if (on_min || on_max) {  // caf_scored.py:46-56 on the raw (unstrided) vectors
+                    const float dx = B.nine[k][1] - B.nine[k][5], dy = B.nine[k][2] - B.nine[k][6];
+                    const float dist = sqrtf(dx * dx + dy * dy);
+                    if ((on_min && !(dist > a.h.dmin_th[0])) || (on_max && !(dist < a.h.dmax_th[0])))
+                        continue;
+                }
+#pragma unroll
+                for (int r = 1; r < 9; r++) B.nine[k][r] = B.nine[k][r] * stride;
+                const float score = B.nine[k][0];
+                float sb = score, sf = score;
+                if (use1)
+                    sb = score * (a.cif_floor + a.one_minus_floor * a.hr.at(t1, B.nine[k][1], B.nine[k][2], 0.0f));
+                if (use2)
+                    sf = score * (a.cif_floor + a.one_minus_floor * a.hr.at(t2, B.nine[k][5], B.nine[k][6], 0.0f));
+                B.sb[k] = sb;
+                B.sf[k] = sf;
+                B.kb[k] = need_b && sb > a.th;
+                B.kf[k] = need_f && sf > a.th;
+            }
+#pragma unroll
+            for (int k = 0; k < kU; k++) account(B, k, cells[k], hw, coff);
+        }
+    } else {
     for (int m = 0; m < a.h.n_caf; m++) {
         const int hw = a.h.aH[m] * a.h.aW[m];
         const float stride = (float)a.h.astride[m];
@@ -599,55 +743,9 @@ __global__ __launch_bounds__(STASH && INDEX_ONLY ? 512 : 256) void caf_bucketed_
             Batch B;
             score_batch(p, hw, stride, m, base, B);
 #pragma unroll
-            for (int k = 0; k < kU; k++) {
-                const int cell = base + k * NT + (int)threadIdx.x;
-                const float *nine = B.nine[k];
-                const int bkb = B.kb[k] ? caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e) : -1;
-                const int bkf = B.kf[k] ? caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e) : -1;
-                if (bkb >= 0) atomicAdd(&s_cnt[0][bkb], 1);
-                if (bkf >= 0) atomicAdd(&s_cnt[1][bkf], 1);
-                if (STASH && INDEX_ONLY) {
-                    if (cell < hw) {
-                        stash_b[coff + cell] = bkb >= 0 ? (uint16_t)bkb : kNoBucket;
-                        stash_b[kStashCells + coff + cell] = bkf >= 0 ? (uint16_t)bkf : kNoBucket;
-                    }
-                } else if (STASH) {
-                    const float key = __int_as_float(coff + cell);
-                    if (bkb >= 0) {
-                        const int sl = atomicAdd(&s_sn[0], 1);
-                        if (sl < kStashA) {
-                            StashCol &e = stash_a[sl];
-                            e.v[0] = B.sb[k];
-                            e.v[1] = nine[5];
-                            e.v[2] = nine[6];
-                            e.v[3] = nine[1];
-                            e.v[4] = nine[2];
-                            e.v[5] = nine[4];
-                            e.v[6] = key;
-                            e.bucket = bkb;
-                        } else {
-                            s_ovf = 1;
-                        }
-                    }
-                    if (bkf >= 0) {
-                        const int sl = atomicAdd(&s_sn[1], 1);
-                        if (sl < kStashA) {
-                            StashCol &e = stash_a[kStashA + sl];
-                            e.v[0] = B.sf[k];
-                            e.v[1] = nine[1];
-                            e.v[2] = nine[2];
-                            e.v[3] = nine[5];
-                            e.v[4] = nine[6];
-                            e.v[5] = nine[8];
-                            e.v[6] = key;
-                            e.bucket = bkf;
-                        } else {
-                            s_ovf = 1;
-                        }
-                    }
-                }
-            }
+            for (int k = 0; k < kU; k++) account(B, k, base + k * NT + (int)threadIdx.x, hw, coff);
         }
+    }
     }
     __syncthreads();
     // exclusive prefix over the buckets (thread-contiguous ranges + block scan)
@@ -898,7 +996,8 @@ static int seeds_entry(const Heads &h, const float *d_cifhr, int32_t n_img, int3
     const HrMap hr = dense_hr(d_cifhr, (int)hr_dim(h.cH[0], h.cstride[0]),
                               (int)hr_dim(h.cW[0], h.cstride[0]));
     int rc = launch_seeds(h, hr, n_img, K, cfg, d_seeds, seed_capacity, d_counts, scratch, s);
-    hipFreeAsync(scratch, s);
+    if (hipFreeAsync(scratch, s) != hipSuccess && rc == PP_OK)
+        rc = fail(PP_EHIP, "pp_seeds: scratch release failed");
     return rc;
 }
 
