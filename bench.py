@@ -69,7 +69,10 @@ def parse():
     p.add_argument('--no-configs', action='store_true',
                    help='skip the cfg2 / cfg5 lines added to the default run')
     p.add_argument('--stage-breakdown', action='store_true',
-                   help='one library call per stage (per-stage times)')
+                   help='one library call per stage (per-stage times); implies --no-overlap')
+    p.add_argument('--no-overlap', action='store_true',
+                   help='run each step on one stream (no front / back half overlap of '
+                        'consecutive steps, engine.DecodePipeline)')
     return p.parse_args()
 
 
@@ -147,7 +150,7 @@ def main():
     from openpifpaf_amd._abi import (ANN_DTYPE, EVAL_CONFIG, PACK_ALL, PREDICT_CONFIG, make_config,
                                      packed_dtype)
     from openpifpaf_amd.engine import (STAGE_CAF, STAGE_CIFHR, STAGE_GROW, STAGE_SEEDS,
-                                       DecodeEngine)
+                                       DecodeEngine, DecodePipeline)
 
     wl = dict(WORKLOADS[args.workload])
     batch = args.batch or wl['batch']
@@ -165,15 +168,23 @@ def main():
 
     eng = DecodeEngine()
     stream = torch.cuda.current_stream()
-    # default: CifHr alone (its events give the roofline), then the other stages in one
+    # default: consecutive steps overlap, the front half (CifHr, seeds, CafScored) of step
+    # k + 1 beside the back half (seed loop, force-complete, NMS) of step k
+    # (engine.DecodePipeline).  --no-overlap: CifHr alone, then the other stages in one
     # call; --stage-breakdown: one call per stage
+    overlap = not (args.no_overlap or args.stage_breakdown) and stages == 15
+    pipe = DecodePipeline(dev) if overlap else None
     groups = ((STAGE_CIFHR, STAGE_SEEDS, STAGE_CAF, STAGE_GROW) if args.stage_breakdown else
               (STAGE_CIFHR, STAGE_SEEDS | STAGE_CAF | STAGE_GROW))
     names = (('cifhr', 'seeds', 'caf_scored', 'grow_nms') if args.stage_breakdown else
-             ('cifhr', 'seeds+caf+grow+nms'))
+             ('cifhr', 'seeds+caf', 'grow+nms') if overlap else ('cifhr', 'seeds+caf+grow+nms'))
+    # event pairs per stage: the pipeline's five events (front stream: CifHr, the other
+    # front stages; back stream: the back half), else one event between groups
+    ev_pairs = ((0, 1), (1, 2), (3, 4)) if overlap else tuple(
+        (i, i + 1) for i in range(len(groups)))
     # two event sets: with the two-deep pipeline, step k's events are read after step k + 1
     # has recorded its own
-    ev_sets = [[torch.cuda.Event(enable_timing=True) for _ in range(len(groups) + 1)]
+    ev_sets = [[torch.cuda.Event(enable_timing=True) for _ in range(max(5, len(groups) + 1))]
                for _ in range(2)]
 
     comm = torch.cuda.Stream(device=dev) if world > 1 and args.backend == 'nccl' else None
@@ -188,11 +199,16 @@ def main():
         k_img = heads.k if heads is not None else cif.shape[1]
         n_img = heads.n if heads is not None else cif.shape[0]
         compact = (k_img, len(skel), PACK_ALL)
-        stage_ms = np.zeros(len(groups))
+        stage_ms = np.zeros(len(ev_pairs))
 
         def step(timed, k=0):
             """Enqueue one decode and its record fetch; returns (PendingRecords, events)."""
             ev = ev_sets[k % 2]
+            if pipe is not None and n_stages == 15:
+                b, pending = pipe.submit(cif, caf, skel, cfg, heads=heads, compact=compact,
+                                         device_out=world > 1 and rank != 0,
+                                         events=ev if timed else None)
+                return b, (pending, ev)
             b = None
             for si, bits in enumerate(groups):
                 if timed:
@@ -234,9 +250,10 @@ def main():
                                         device=comm_dev, stream=comm)
                 n_recs = len(recs) if recs is not None else 0
             if timed:
-                ev[len(groups)].synchronize()
-                for si in range(len(groups)):
-                    stage_ms[si] += ev[si].elapsed_time(ev[si + 1])
+                last = max(j for _, j in ev_pairs)
+                ev[last].synchronize()
+                for si, (i, j) in enumerate(ev_pairs):
+                    stage_ms[si] += ev[i].elapsed_time(ev[j])
             return n_recs
 
         for _ in range(warmup):

@@ -2294,6 +2294,10 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
     }
     // CifSeeds and CafScored both read only the fields and the CifHr map: with both stages
     // requested, CafScored runs on a side stream beside the seeds (fork / join events)
+    // PP_STAGE_COMPLETE_SETS_EARLY: the force-complete sets (every field and direction) with
+    // CafScored instead of gated after the seed loop
+    const bool early_b = (stages & PP_STAGE_COMPLETE_SETS_EARLY) && (stages & 4u) &&
+                         cfg->force_complete;
     const SideStream *side = (stages & 6u) == 6u ? side_stream() : nullptr;
     if (side) {
         std::lock_guard<std::mutex> lock(side->mu);
@@ -2302,6 +2306,10 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
             return fail(PP_EHIP, "pp_decode_batch: side-stream fork failed");
         rc = launch_caf_bucketed(h, hr, n_img, K, C, skeleton, cfg, cfg->caf_threshold, cols[0],
                                  offs[0], nullptr, false, side->stream);
+        if (!rc && early_b)
+            rc = launch_caf_bucketed(h, hr, n_img, K, C, skeleton, cfg,
+                                     cfg->complete_caf_threshold, cols[1], offs[1], nullptr, true,
+                                     side->stream);
         if (!rc)
             rc = launch_seeds(h, hr, n_img, K, cfg, seeds, d.seed_cap, seed_counts,
                               ws + d.off_seed_ws, s);
@@ -2319,6 +2327,10 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
         if (stages & 4u) {  // CafScored at caf_threshold; the force-complete set is lazy
             rc = launch_caf_bucketed(h, hr, n_img, K, C, skeleton, cfg, cfg->caf_threshold,
                                      cols[0], offs[0], nullptr, false, s);
+            if (!rc && early_b)
+                rc = launch_caf_bucketed(h, hr, n_img, K, C, skeleton, cfg,
+                                         cfg->complete_caf_threshold, cols[1], offs[1], nullptr,
+                                         true, s);
             if (rc) return rc;
         }
     }
@@ -2414,7 +2426,7 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
         hipLaunchKernelGGL(seed_loop_kernel, dim3(n_img), dim3(64 * kSeedWaves), 0, s, g);
         rc = check_launch("pp_decode_batch(seed loop)");
         if (rc) return rc;
-        if (cfg->force_complete) {
+        if (cfg->force_complete && !(stages & PP_STAGE_COMPLETE_SETS_EARLY)) {
             // complete_annotations' CafScored(score_th=0.0001) only where phase 1 left work
             rc = launch_caf_bucketed(h, hr, n_img, K, C, skeleton, cfg, cfg->complete_caf_threshold,
                                      cols[1], offs[1], g.need_complete, true, s);

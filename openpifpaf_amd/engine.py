@@ -21,6 +21,8 @@ LOG = logging.getLogger(__name__)
 
 STAGE_CIFHR, STAGE_SEEDS, STAGE_CAF, STAGE_GROW = 1, 2, 4, 8
 STAGE_ALL = 15
+# PP_STAGE_COMPLETE_SETS_EARLY: the force-complete column sets with the CAF stage
+STAGE_COMPLETE_EARLY = 16
 
 
 def default_ann_capacity(h, w):
@@ -365,6 +367,73 @@ def needs_refetch(recs):
     """True when a compact record is flagged PP_PACK_REFETCH (its orders do not fit)."""
     return (recs.dtype != ANN_DTYPE and len(recs) > 0 and
             bool((recs['n_decoding'] & PP_PACK_REFETCH).any()))
+
+
+class DecodePipeline:
+    """Decodes a sequence of batches with consecutive batches overlapped on the device.
+
+    A decode has a bandwidth-bound front half (CifHr, seeds, CafScored: stages 1 | 2 | 4,
+    here with the force-complete column sets too, STAGE_COMPLETE_EARLY) and a
+    latency-bound back half (seed loop, force-complete, NMS: stage 8).  Batch i's
+    front half runs on the caller's current stream, its back half on a back stream that
+    waits for it, so batch i + 1's front half runs beside batch i's back half.  Two engines
+    (two workspaces) alternate; a workspace's front half waits until the back half that
+    last used it is done, and its output slots are released by their record packs as in
+    DecodeEngine.  (The front half stays on the current stream so that the streams in use
+    -- current, back, the library's CafScored side stream, the record pack -- each get a
+    hardware queue of their own: HIP shares 4 per process between streams.)
+
+    submit() returns (buffers, PendingRecords of the batch: DecodeEngine.fetch_async).
+    The current stream does not wait for the back half; the fields must stay unchanged
+    until the batch's records are fetched."""
+
+    def __init__(self, device=None):
+        self.device = _device.require() if device is None else device
+        self.engines = (DecodeEngine(), DecodeEngine())
+        self.back = torch.cuda.Stream(device=self.device)
+        self._back_done = [None, None]
+        self._i = 0
+
+    def submit(self, cif, caf, skeleton, cfg, cap=None, heads=None, compact=None,
+               device_out=False, events=None):
+        """Enqueue one batch (cif / caf, or a multi-scale HeadSet `heads`).  `events`
+        (five torch.cuda.Events, optional) are recorded around the CifHr stage, the other
+        front stages (front stream) and the back half (back stream)."""
+        par = self._i % 2
+        self._i += 1
+        eng = self.engines[par]
+        front = torch.cuda.current_stream(self.device)
+
+        def launch(stages):
+            if heads is None:
+                return eng.launch(cif, caf, skeleton, cfg, cap=cap, stages=stages)
+            return eng.launch_multi(heads, skeleton, cfg, cap=cap, stages=stages)
+
+        if self._back_done[par] is not None:  # the workspace's previous back half
+            front.wait_event(self._back_done[par])
+        with torch.cuda.stream(front):
+            if events:
+                events[0].record()
+            launch(STAGE_CIFHR)
+            if events:
+                events[1].record()
+            launch(STAGE_SEEDS | STAGE_CAF | STAGE_COMPLETE_EARLY)
+            if events:
+                events[2].record()
+            front_done = torch.cuda.Event()
+            front_done.record()
+        self.back.wait_event(front_done)
+        with torch.cuda.stream(self.back):
+            if events:
+                events[3].record()
+            b = launch(STAGE_GROW | STAGE_COMPLETE_EARLY)
+            if events:
+                events[4].record()
+            back_done = torch.cuda.Event()
+            back_done.record()
+            pending = DecodeEngine.fetch_async(b, compact, device_out=device_out)
+        self._back_done[par] = back_done
+        return b, pending
 
 
 _ENGINE = None

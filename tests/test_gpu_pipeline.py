@@ -1,0 +1,33 @@
+"""engine.DecodePipeline (consecutive batches overlapped on two streams, two workspaces):
+every batch's records are byte-identical to a one-stream DecodeEngine.decode of it."""
+import numpy as np
+import pytest
+
+from openpifpaf_amd import constants, synthetic
+from openpifpaf_amd._abi import EVAL_CONFIG, PACK_ALL, make_config
+
+
+@pytest.mark.gpu
+def test_pipeline_matches_engine_decode():
+    import torch
+    from openpifpaf_amd.engine import DecodeEngine, DecodePipeline
+    skel = constants.COCO_PERSON_SKELETON
+    cfg = make_config(**EVAL_CONFIG)
+    compact = (17, len(skel), PACK_ALL)
+    batches = []
+    for i, kind in enumerate(('planted', 'uniform', 'planted', 'planted', 'uniform')):
+        kw = {'n_caf': len(skel)} if kind == 'uniform' else {'skeleton': skel, 'n_people': 8}
+        cif, caf = synthetic.batch(kind, 8, 40, 40, first_seed=100 * i, **kw)
+        batches.append((torch.from_numpy(cif).cuda(), torch.from_numpy(caf).cuda()))
+    eng = DecodeEngine()
+    want = []
+    for cif, caf in batches:
+        recs, offsets, _ = eng.decode(cif, caf, skel, cfg, cap=1024, compact=PACK_ALL)
+        want.append((recs.tobytes(), offsets.copy()))
+    pipe = DecodePipeline()
+    pend = [pipe.submit(cif, caf, skel, cfg, cap=1024, compact=compact)[1]
+            for cif, caf in batches]  # all five in flight before any result is read
+    for (w_bytes, w_off), p in zip(want, pend):
+        recs, offsets = p.result()
+        np.testing.assert_array_equal(offsets, w_off)
+        assert recs.tobytes() == w_bytes
