@@ -134,9 +134,11 @@ struct GrowArgs {
     int *status;
 };
 
-struct GrowLDS {
+// per-wave LDS of the grow kernels; HEAP: the flood-fill heap (force-complete only)
+template <bool HEAP>
+struct GrowLDST {
     pp_ann a;                     // record being built (lists; data synced from registers)
-    FFEntry ff[kHeap];
+    FFEntry ff[HEAP ? kHeap : 1];
     int mark_pre[kKP + 1];        // occupancy boxes of one annotation: area prefix
     int mark_box[kKP][4];
     int ff_n;
@@ -146,6 +148,8 @@ struct GrowLDS {
     uint64_t fst[8];  // inside-grow section sums (diagnostic build)
 #endif
 };
+using GrowLDS = GrowLDST<true>;
+using SeedLDS = GrowLDST<false>;  // the seed loop's waves (no flood fill)
 
 
 __device__ __forceinline__ float rl_f(float v, int l) {
@@ -757,7 +761,8 @@ __device__ __forceinline__ bool frontier_pop(Frontier &F, Entry &e) {
 }
 
 // add_to_frontier (cifcaf.py:251-263): the start joint's slots in dict order, one pass
-__device__ __forceinline__ void add_to_frontier(const GrowArgs &g, GrowLDS &L, Frontier &F, float av, int start,
+template <typename LDS>
+__device__ __forceinline__ void add_to_frontier(const GrowArgs &g, LDS &L, Frontier &F, float av, int start,
                                 float start_v, int &nfr, uint64_t added[2]) {
     const int lane = threadIdx.x & 63;
     const int lo = g.j_off[start], hi = g.j_off[start + 1];
@@ -814,7 +819,7 @@ __device__ __forceinline__ void flat_load(const float *__restrict__ cf, int64_t 
 // that fits kColLds floats, in (CAF, direction) order, column-major (kColPad floats per
 // column: two 16-byte reads).  cofs[q] = its offset, -1 = global.
 constexpr int kColPad = 8;
-constexpr int kColLds = 20480;  // 80 KB
+constexpr int kColLds = 20480;  // 80 KB (40 KB: same speed)
 struct ColStage {
     const int *ncol;   // set-A column counts per (CAF, direction)
     const int *cofs;
@@ -979,8 +984,8 @@ __device__ __forceinline__ void eval_ahead(const GrowArgs &g, Frontier &F, int i
 // _grow (cifcaf.py:247-307) on the record in L.a (joint data mirrored into registers).
 // AHEAD (seed loop: set A, reverse_match): new entries' connections via eval_ahead from
 // the image's set-A column counts and LDS-staged sets.
-template <bool AHEAD>
-__device__ __forceinline__ void grow(const GrowArgs &g, GrowLDS &L, int img, int set, bool reverse_match,
+template <bool AHEAD, typename LDS>
+__device__ __forceinline__ void grow(const GrowArgs &g, LDS &L, int img, int set, bool reverse_match,
                                      const ColStage &cs = ColStage{}) {
     const int lane = threadIdx.x & 63;
     const int K = g.K;
@@ -1221,8 +1226,8 @@ __device__ __forceinline__ bool occ_box(const GrowArgs &g, const OccGrid &o, int
 // Mark the boxes of every joint j with mark(j) in one pass: joints live on different
 // occupancy planes, so the per-joint `+= 1` boxes are independent and spread over the 64
 // lanes.  Each marked box is logged for occ_clear.  Collective (all 64 lanes).
-template <typename MarkFn>
-__device__ __forceinline__ void occ_mark(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccGrid &o,
+template <typename LDS, typename MarkFn>
+__device__ __forceinline__ void occ_mark(const GrowArgs &g, LDS &L, OccLog *log, const OccGrid &o,
                          const float (*xy)[3], const float *scales, int K, MarkFn mark) {
     const int lane = threadIdx.x & 63;
     int box[4] = {0, 0, 0, 0};
@@ -1317,7 +1322,8 @@ __device__ __forceinline__ void occ_mark(const GrowArgs &g, GrowLDS &L, OccLog *
 }
 
 // zero every box the launch marked, so the next launch starts from a clean grid
-__device__ __forceinline__ void occ_clear(const GrowArgs &g, GrowLDS &L, OccLog *log, const OccGrid &o) {
+template <typename LDS>
+__device__ __forceinline__ void occ_clear(const GrowArgs &g, LDS &L, OccLog *log, const OccGrid &o) {
     wave_sync();
     const int n = L.log_n < g.log_cap ? L.log_n : g.log_cap;
     const int lane = threadIdx.x & 63;
@@ -1456,7 +1462,8 @@ __device__ __forceinline__ bool spec_far(float far, float xa, float ya, float sa
 }
 
 // Annotation(keypoints, out_skeleton).add(f, (x, y, v)); joint_scales[f] = s
-__device__ __forceinline__ void ann_from_seed(GrowLDS &L, const pp_seed &sd, int K, int img) {
+template <typename LDS>
+__device__ __forceinline__ void ann_from_seed(LDS &L, const pp_seed &sd, int K, int img) {
     const int lane = threadIdx.x & 63;
     uint32_t *z = reinterpret_cast<uint32_t *>(&L.a);
     for (int t = lane; t < (int)(sizeof(pp_ann) / 4); t += 64) z[t] = 0u;
@@ -1472,16 +1479,21 @@ __device__ __forceinline__ void ann_from_seed(GrowLDS &L, const pp_seed &sd, int
     wave_sync();
 }
 
-__global__ __launch_bounds__(64 * kSeedWaves) void seed_loop_kernel(GrowArgs g) {
-    __shared__ GrowLDS Ls[kSeedWaves];
+// <= 168 VGPRs (3 waves per SIMD; a few spills) and the column stage in dynamic LDS: the
+// image's workgroup leaves room on its CU for the next batch's CifHr / seeds / CafScored
+// workgroups (DecodePipeline).  Planted 1.031 -> 1.013 ms, uniform 21.7 -> 20.4 ms per
+// overlapped step; 4 waves per SIMD (128 VGPRs, 532 spills): 1.37 ms.
+__global__ __launch_bounds__(64 * kSeedWaves) __attribute__((amdgpu_waves_per_eu(3)))
+void seed_loop_kernel(GrowArgs g) {
+    __shared__ SeedLDS Ls[kSeedWaves];
     __shared__ SeedLoopShared S;
     __shared__ int s_ncol[2 * PP_MAX_EDGES];  // set-A column counts per (CAF, direction)
     __shared__ int s_cofs[2 * PP_MAX_EDGES];  // their LDS offsets in s_cols (-1: global)
-    __shared__ float s_cols[kColLds];
+    extern __shared__ float s_cols[];  // kColLds floats (dynamic: the launch sizes it)
     const int img = blockIdx.x;
     const int K = g.K;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    GrowLDS &L = Ls[wave];
+    SeedLDS &L = Ls[wave];
     for (int q = threadIdx.x; q < 2 * g.C; q += blockDim.x) s_ncol[q] = col_offs(g, 0, img, q >> 1, q & 1)[g.nb];
     __syncthreads();
     if (threadIdx.x == 0) {  // LDS placement of the small sets, in order while they fit
@@ -2423,7 +2435,8 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
         g.out = d_anns;
         g.counts = d_counts;
         g.status = d_status;
-        hipLaunchKernelGGL(seed_loop_kernel, dim3(n_img), dim3(64 * kSeedWaves), 0, s, g);
+        hipLaunchKernelGGL(seed_loop_kernel, dim3(n_img), dim3(64 * kSeedWaves),
+                           kColLds * sizeof(float), s, g);
         rc = check_launch("pp_decode_batch(seed loop)");
         if (rc) return rc;
         if (cfg->force_complete && !(stages & PP_STAGE_COMPLETE_SETS_EARLY)) {
