@@ -174,6 +174,9 @@ def main():
     # call; --stage-breakdown: one call per stage
     overlap = not (args.no_overlap or args.stage_breakdown) and stages == 15
     pipe = DecodePipeline(dev) if overlap else None
+    # steps in flight on the host: 3 with the overlapped pipeline (two workspaces x two
+    # output slots), 2 on one stream (two output slots)
+    depth = 3 if overlap else 2
     groups = ((STAGE_CIFHR, STAGE_SEEDS, STAGE_CAF, STAGE_GROW) if args.stage_breakdown else
               (STAGE_CIFHR, STAGE_SEEDS | STAGE_CAF | STAGE_GROW))
     names = (('cifhr', 'seeds', 'caf_scored', 'grow_nms') if args.stage_breakdown else
@@ -185,7 +188,7 @@ def main():
     # two event sets: with the two-deep pipeline, step k's events are read after step k + 1
     # has recorded its own
     ev_sets = [[torch.cuda.Event(enable_timing=True) for _ in range(max(5, len(groups) + 1))]
-               for _ in range(2)]
+               for _ in range(depth)]
 
     comm = torch.cuda.Stream(device=dev) if world > 1 and args.backend == 'nccl' else None
     counters = {'refetch_steps': 0, 'pack_bytes': 0}
@@ -203,7 +206,7 @@ def main():
 
         def step(timed, k=0):
             """Enqueue one decode and its record fetch; returns (PendingRecords, events)."""
-            ev = ev_sets[k % 2]
+            ev = ev_sets[k % len(ev_sets)]
             if pipe is not None and n_stages == 15:
                 b, pending = pipe.submit(cif, caf, skel, cfg, heads=heads, compact=compact,
                                          device_out=world > 1 and rank != 0,
@@ -269,17 +272,19 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         n_anns = 0
-        # two-deep pipeline: step k + 1 is enqueued before step k's records are waited for
-        # (decode outputs are double-buffered, engine.DecodeBuffers), so the host's record
-        # handling and next launches overlap the device work; every step's records are on
-        # rank 0's host before the clock stops
-        pending = None
+        # `depth` steps in flight: step k + depth - 1 is enqueued before step k's records are
+        # waited for (decode outputs are double-buffered per workspace, engine.DecodeBuffers),
+        # so the host's record handling and the next launches overlap the device work, and
+        # with the overlapped pipeline the next front half is queued while the current back
+        # half runs; every step's records are on rank 0's host before the clock stops
+        inflight = []
         for k in range(steps):
             b, p = step(True, k)
-            if pending is not None:
-                n_anns += finish(pending, True)
-            pending = p
-        n_anns += finish(pending, True)
+            inflight.append(p)
+            if len(inflight) >= depth:
+                n_anns += finish(inflight.pop(0), True)
+        while inflight:
+            n_anns += finish(inflight.pop(0), True)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()

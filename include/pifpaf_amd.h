@@ -412,11 +412,16 @@ int pp_pack_compact(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img
  * Bit 16 (PP_STAGE_COMPLETE_SETS_EARLY) moves the complete_caf_threshold column sets into
  * stage 4, built for every (field, direction) (stage 8 then reads them): the same result,
  * for callers that overlap one batch's stages 1-4 with the previous batch's stage 8.
+ * With bit 16, stage 8 may run in two calls on the same workspace and outputs: first with
+ * PP_STAGE_SEED_LOOP_ONLY (32), then with PP_STAGE_AFTER_SEED_LOOP (64: force-complete and
+ * NMS), so the second part can run on another stream beside the next batch's seed loop.
  *
  * Workspace contract: bytes [pp_decode_workspace_zero_offset(), end) must be zero before
  * the first call (e.g. hipMemset once at allocation); every call leaves them zero again.
  */
 #define PP_STAGE_COMPLETE_SETS_EARLY 16u
+#define PP_STAGE_SEED_LOOP_ONLY 32u
+#define PP_STAGE_AFTER_SEED_LOOP 64u
 int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int32_t K,
                      int32_t C, int32_t H, int32_t W, const int32_t *skeleton,
                      const pp_config *cfg, float *d_cifhr, pp_ann *d_anns,

@@ -2437,23 +2437,29 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
         g.out = d_anns;
         g.counts = d_counts;
         g.status = d_status;
-        hipLaunchKernelGGL(seed_loop_kernel, dim3(n_img), dim3(64 * kSeedWaves),
-                           kColLds * sizeof(float), s, g);
-        rc = check_launch("pp_decode_batch(seed loop)");
-        if (rc) return rc;
-        if (cfg->force_complete && !(stages & PP_STAGE_COMPLETE_SETS_EARLY)) {
+        // PP_STAGE_SEED_LOOP_ONLY / PP_STAGE_AFTER_SEED_LOOP split stage 8 in two calls
+        const bool run_rest = !(stages & PP_STAGE_SEED_LOOP_ONLY);
+        if (!(stages & PP_STAGE_AFTER_SEED_LOOP)) {
+            hipLaunchKernelGGL(seed_loop_kernel, dim3(n_img), dim3(64 * kSeedWaves),
+                               kColLds * sizeof(float), s, g);
+            rc = check_launch("pp_decode_batch(seed loop)");
+            if (rc) return rc;
+        }
+        if (run_rest && cfg->force_complete && !(stages & PP_STAGE_COMPLETE_SETS_EARLY)) {
             // complete_annotations' CafScored(score_th=0.0001) only where phase 1 left work
             rc = launch_caf_bucketed(h, hr, n_img, K, C, skeleton, cfg, cfg->complete_caf_threshold,
                                      cols[1], offs[1], g.need_complete, true, s);
             if (rc) return rc;
         }
-        if (cfg->force_complete) {
+        if (run_rest && cfg->force_complete) {
             hipLaunchKernelGGL(complete_kernel, dim3(n_img, kCompleteWays), dim3(64), 0, s, g);
             rc = check_launch("pp_decode_batch(force complete)");
             if (rc) return rc;
         }
-        hipLaunchKernelGGL(nms_kernel, dim3(n_img), dim3(64 * kNmsWaves), 0, s, g);
-        rc = check_launch("pp_decode_batch(nms)");
+        if (run_rest) {
+            hipLaunchKernelGGL(nms_kernel, dim3(n_img), dim3(64 * kNmsWaves), 0, s, g);
+            rc = check_launch("pp_decode_batch(nms)");
+        }
 #ifdef PP_STAMPS
         hipStreamSynchronize(s);
         const size_t nst = (size_t)n_img * 3 * 12;

@@ -23,6 +23,8 @@ STAGE_CIFHR, STAGE_SEEDS, STAGE_CAF, STAGE_GROW = 1, 2, 4, 8
 STAGE_ALL = 15
 # PP_STAGE_COMPLETE_SETS_EARLY: the force-complete column sets with the CAF stage
 STAGE_COMPLETE_EARLY = 16
+# PP_STAGE_SEED_LOOP_ONLY / PP_STAGE_AFTER_SEED_LOOP: stage 8 in two calls (same slot)
+STAGE_SEED_LOOP_ONLY, STAGE_AFTER_SEED_LOOP = 32, 64
 
 
 def default_ann_capacity(h, w):
@@ -146,7 +148,7 @@ class DecodeEngine:
             raise ValueError('skeleton has {} edges but caf has {} fields'.format(len(skel), c))
         cap = cap or default_ann_capacity(h, w)
         b = self.buffers(n, k, c, h, w, cfg, cap)
-        if stages & STAGE_GROW:
+        if stages & STAGE_GROW and not stages & STAGE_AFTER_SEED_LOOP:
             b.next_slot()
         hr = b.cifhr_buffer() if keep_cifhr else None
         call('pp_decode_stages', _device.ptr(cif), _device.ptr(caf), n, k, c, h, w,
@@ -164,7 +166,7 @@ class DecodeEngine:
                                                                                   heads.c))
         cap = cap or default_ann_capacity(heads.h, heads.w)
         b = self.buffers(heads.n, heads.k, heads.c, heads.h, heads.w, cfg, cap, heads)
-        if stages & STAGE_GROW:
+        if stages & STAGE_GROW and not stages & STAGE_AFTER_SEED_LOOP:
             b.next_slot()
         hr = b.cifhr_buffer() if keep_cifhr else None
         call('pp_decode_multi', heads.arr, len(heads.arr), heads.pairs, heads.n, heads.k,
@@ -209,7 +211,7 @@ class DecodeEngine:
         return DecodeEngine.fetch_async(b, compact).result()
 
     @staticmethod
-    def fetch_async(b, compact=None, device_out=False, capacity=0):
+    def fetch_async(b, compact=None, device_out=False, capacity=0, stream=None):
         """Enqueue the record fetch of the last decode into `b` on a side stream and return a
         PendingRecords; its result() waits for it.
 
@@ -223,16 +225,18 @@ class DecodeEngine:
         (`capacity` = records to reserve at least); result() re-packs a batch that outgrew
         it, and fetches full records when a compact record is flagged PP_PACK_REFETCH.  The
         slot stays valid until the second decode after this one, so a caller may launch the
-        next decode before calling result()."""
+        next decode before calling result().  `stream`: pack there instead of on the
+        engine's pack stream."""
         est = max(getattr(b, 'pack_cap', 0), 16 * b.n, capacity)
         decoded = torch.cuda.Event()
         decoded.record()
-        p = DecodeEngine._pack(b, b.anns, b.counts, b.status, compact, device_out, est, decoded)
+        p = DecodeEngine._pack(b, b.anns, b.counts, b.status, compact, device_out, est, decoded,
+                               stream)
         b._free[b._cur] = p.done_event
         return p
 
     @staticmethod
-    def _pack(b, anns, counts, status, compact, device_out, est, after):
+    def _pack(b, anns, counts, status, compact, device_out, est, after, stream=None):
         n = b.n
         dtype = ANN_DTYPE if compact is None else packed_dtype(*compact)
         width = dtype.itemsize
@@ -244,7 +248,7 @@ class DecodeEngine:
         out_ptr = dev.data_ptr() if device_out else host.data_ptr() + head
         # the pack runs on a side stream after the decode, so its PCIe writes overlap the
         # next decode; the slot is not rewritten before it is done (DecodeBuffers.next_slot)
-        side = DecodeEngine._pack_stream(anns.device)
+        side = DecodeEngine._pack_stream(anns.device) if stream is None else stream
         side.wait_event(after)
         with torch.cuda.stream(side):
             if compact is None:
@@ -374,14 +378,16 @@ class DecodePipeline:
 
     A decode has a bandwidth-bound front half (CifHr, seeds, CafScored: stages 1 | 2 | 4,
     here with the force-complete column sets too, STAGE_COMPLETE_EARLY) and a
-    latency-bound back half (seed loop, force-complete, NMS: stage 8).  Batch i's
-    front half runs on the caller's current stream, its back half on a back stream that
-    waits for it, so batch i + 1's front half runs beside batch i's back half.  Two engines
-    (two workspaces) alternate; a workspace's front half waits until the back half that
-    last used it is done, and its output slots are released by their record packs as in
-    DecodeEngine.  (The front half stays on the current stream so that the streams in use
-    -- current, back, the library's CafScored side stream, the record pack -- each get a
-    hardware queue of their own: HIP shares 4 per process between streams.)
+    latency-bound back half: the seed loop, then force-complete and NMS (stage 8 in two
+    calls).  Batch i's front half runs on the caller's current stream, its seed loop on a
+    back stream that waits for it, and its force-complete, NMS and record pack on a tail
+    stream that waits for the seed loop.  So batch i + 1's front half runs beside batch i's
+    seed loop, and batch i + 1's seed loop beside batch i's tail.  Two engines (two
+    workspaces) alternate; a workspace's front half waits until the tail that last used it
+    is done, and its output slots are released by their record packs as in DecodeEngine.
+    (The front half stays on the current stream and the pack on the tail stream so that
+    the streams in use -- current, back, tail, the library's CafScored side stream -- each
+    get a hardware queue of their own: HIP shares 4 per process between streams.)
 
     submit() returns (buffers, PendingRecords of the batch: DecodeEngine.fetch_async).
     The current stream does not wait for the back half; the fields must stay unchanged
@@ -391,6 +397,7 @@ class DecodePipeline:
         self.device = _device.require() if device is None else device
         self.engines = (DecodeEngine(), DecodeEngine())
         self.back = torch.cuda.Stream(device=self.device)
+        self.tail = torch.cuda.Stream(device=self.device)
         self._back_done = [None, None]
         self._i = 0
 
@@ -398,7 +405,8 @@ class DecodePipeline:
                device_out=False, events=None):
         """Enqueue one batch (cif / caf, or a multi-scale HeadSet `heads`).  `events`
         (five torch.cuda.Events, optional) are recorded around the CifHr stage, the other
-        front stages (front stream) and the back half (back stream)."""
+        front stages (front stream), at the seed loop's start (back stream) and at the end
+        of NMS (tail stream)."""
         par = self._i % 2
         self._i += 1
         eng = self.engines[par]
@@ -426,12 +434,18 @@ class DecodePipeline:
         with torch.cuda.stream(self.back):
             if events:
                 events[3].record()
-            b = launch(STAGE_GROW | STAGE_COMPLETE_EARLY)
+            launch(STAGE_GROW | STAGE_COMPLETE_EARLY | STAGE_SEED_LOOP_ONLY)
+            loop_done = torch.cuda.Event()
+            loop_done.record()
+        self.tail.wait_event(loop_done)
+        with torch.cuda.stream(self.tail):
+            b = launch(STAGE_GROW | STAGE_COMPLETE_EARLY | STAGE_AFTER_SEED_LOOP)
             if events:
                 events[4].record()
             back_done = torch.cuda.Event()
             back_done.record()
-            pending = DecodeEngine.fetch_async(b, compact, device_out=device_out)
+            pending = DecodeEngine.fetch_async(b, compact, device_out=device_out,
+                                               stream=self.tail)
         self._back_done[par] = back_done
         return b, pending
 
