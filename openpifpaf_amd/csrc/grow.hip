@@ -67,7 +67,9 @@ namespace pp {
 
 constexpr int kKP = PP_MAX_KP;
 constexpr int kSlots = 2 * PP_MAX_EDGES;   // directed edges (two lanes' worth of slots)
-constexpr int kHeap = 4 * PP_MAX_EDGES + 8; // flood-fill heap capacity
+// flood-fill heap capacity: every joint is expanded at most once, pushing its by_source
+// entries, so a fill pushes at most 2C <= 2 * PP_MAX_EDGES entries
+constexpr int kHeap = 2 * PP_MAX_EDGES + 8;
 constexpr int kOccMargin = 64;              // NMS occupancy slack beyond the main grid
 constexpr int kCompleteWays = 64;           // force-complete workgroups per image
 
@@ -1749,6 +1751,7 @@ void seed_loop_kernel(GrowArgs g) {
 // annotations of an image are spread over kCompleteWays workgroups.  Ones with every joint
 // set are unchanged by it (their frontier is empty) and are skipped, and images the seed
 // loop did not flag return at once.
+// (5 or 6 waves per SIMD via amdgpu_waves_per_eu: 21 / 46 spills, slower)
 __global__ __launch_bounds__(64) void complete_kernel(GrowArgs g) {
     __shared__ GrowLDS L;
     const int img = blockIdx.x;
