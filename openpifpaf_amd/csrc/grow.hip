@@ -1230,13 +1230,14 @@ __device__ __forceinline__ bool occ_box(const GrowArgs &g, const OccGrid &o, int
 // Mark the boxes of every joint j with mark(j) in one pass: joints live on different
 // occupancy planes, so the per-joint `+= 1` boxes are independent and spread over the 64
 // lanes.  Each marked box is logged for occ_clear.  Collective (all 64 lanes).
-template <typename LDS, typename MarkFn>
+// lane j < K holds joint j: (jx, jy), scale js, `on` = mark it
+template <typename LDS>
 __device__ __forceinline__ void occ_mark(const GrowArgs &g, LDS &L, OccLog *log, const OccGrid &o,
-                         const float (*xy)[3], const float *scales, int K, MarkFn mark) {
+                                         float jx, float jy, float js, bool on, int K) {
     const int lane = threadIdx.x & 63;
     int box[4] = {0, 0, 0, 0};
     bool has = false;
-    if (lane < K && mark(lane)) has = occ_box(g, o, lane, xy[lane][0], xy[lane][1], scales[lane], box);
+    if (lane < K && on) has = occ_box(g, o, lane, jx, jy, js, box);
     // work items: (row, 16-byte chunk) pairs of the box
     const int area = has ? (box[3] - box[2]) * (((box[1] - 1) >> 4) - (box[0] >> 4) + 1) : 0;
     int pre = 0, total = 0;
@@ -1372,11 +1373,20 @@ __device__ double pw_sum(const double *a, int K) {
     return res;
 }
 
+// all loads first, then all stores: one round trip (the two records may alias as far as the
+// compiler knows, so a plain copy loop waits for every load in turn)
 __device__ __forceinline__ void copy_ann(pp_ann *dst, const pp_ann *src) {
     const uint32_t *s = reinterpret_cast<const uint32_t *>(src);
     uint32_t *d = reinterpret_cast<uint32_t *>(dst);
     constexpr int nw = sizeof(pp_ann) / 4;
-    for (int t = threadIdx.x & 63; t < nw; t += 64) d[t] = s[t];
+    constexpr int per = (nw + 63) / 64;
+    const int lane = threadIdx.x & 63;
+    uint32_t v[per];
+#pragma unroll
+    for (int u = 0; u < per; u++) v[u] = (u * 64 + lane < nw) ? s[u * 64 + lane] : 0u;
+#pragma unroll
+    for (int u = 0; u < per; u++)
+        if (u * 64 + lane < nw) d[u * 64 + lane] = v[u];
     wave_sync();
 }
 
@@ -1559,12 +1569,13 @@ void seed_loop_kernel(GrowArgs g) {
 #endif
 
     // append one finished annotation and mark_occupied (cifcaf.py:87-93): wave 0 only
-    auto commit = [&](const pp_ann *src) {
+    // (lane j < K holds joint j of the record: x, y, v, scale, from LDS)
+    auto commit = [&](const pp_ann *src, float jx, float jy, float jv, float js) {
         copy_ann(&work[n_anns], src);
         n_anns++;
-        for (int j = 0; j < K; j++) unset_mask |= (src->data[j][2] > 0.0f) ? 0u : (1u << j);
-        occ_mark(g, L, log, occ, src->data, src->joint_scales, K,
-                 [&](int j) { return src->data[j][2] != 0.0f; });
+        const uint32_t set = (uint32_t)__ballot(lane < K && jv > 0.0f);
+        unset_mask |= ~set & (K >= 32 ? 0xFFFFFFFFu : ((1u << K) - 1u));
+        occ_mark(g, L, log, occ, jx, jy, js, jv != 0.0f, K);
     };
 
     if (wave > 0) {  // helper: grow the seeds wave 0 hands over until it is done
@@ -1625,7 +1636,8 @@ void seed_loop_kernel(GrowArgs g) {
             if (hit) {  // a helper grew it, or is growing it
                 const int slot = __ffsll((unsigned long long)hit) - 1;
                 while (lds_acquire(&S.cache_state[slot]) != 2) __builtin_amdgcn_s_sleep(1);
-                commit(&cache[slot]);
+                const float4 jq = lane < kKP ? S.cache_j[slot][lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+                commit(&cache[slot], jq.x, jq.y, jq.z, jq.w);
                 s = t + 1;
 #ifdef PP_STAMPS
                 n_hits++;
@@ -1718,7 +1730,8 @@ void seed_loop_kernel(GrowArgs g) {
             ann_from_seed(L, st, K, img);
             grow<true>(g, L, img, 0, true, cstage);
             STAMP(2);
-            commit(&L.a);
+            commit(&L.a, lane < K ? L.a.data[lane][0] : 0.0f, lane < K ? L.a.data[lane][1] : 0.0f,
+                   lane < K ? L.a.data[lane][2] : 0.0f, lane < K ? L.a.joint_scales[lane] : 0.0f);
             s = t + 1;
             STAMP(3);
         }
