@@ -411,7 +411,10 @@ int pp_pack_compact(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img
  * pp_decode_batch call.  pp_decode_batch == pp_decode_stages(..., 15, stream).
  * Bit 16 (PP_STAGE_COMPLETE_SETS_EARLY) moves the complete_caf_threshold column sets into
  * stage 4, built for every (field, direction) (stage 8 then reads them): the same result,
- * for callers that overlap one batch's stages 1-4 with the previous batch's stage 8.
+ * for callers that overlap one batch's stages 1-4 with the previous batch's stage 8.  In a
+ * call with stage 1 (and without 8) they start on the library's side stream before the
+ * CifHr map instead (they read only the CAF fields); a later call with stages 2 | 4 joins
+ * that stream.
  * With bit 16, stage 8 may run in two calls on the same workspace and outputs: first with
  * PP_STAGE_SEED_LOOP_ONLY (32), then with PP_STAGE_AFTER_SEED_LOOP (64: force-complete and
  * NMS), so the second part can run on another stream beside the next batch's seed loop.

@@ -2312,6 +2312,26 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
     float *cols[2] = {(float *)(ws + d.off_cols[0]), (float *)(ws + d.off_cols[1])};
     int *offs[2] = {(int *)(ws + d.off_offs[0]), (int *)(ws + d.off_offs[1])};
     int rc = PP_OK;
+    // PP_STAGE_COMPLETE_SETS_EARLY with stage 1 (and without 8): the force-complete sets read
+    // only the CAF fields, so they start on the side stream before the CifHr map, and a later
+    // call's side-stream join (stages 2 | 4) covers them
+    const bool b_first = (stages & PP_STAGE_COMPLETE_SETS_EARLY) && (stages & 1u) &&
+                         !(stages & 8u) && cfg->force_complete;
+    if (b_first) {
+        const SideStream *side = side_stream();
+        if (!side) return fail(PP_EHIP, "pp_decode_stages: no side stream for stage 16");
+        std::lock_guard<std::mutex> lock(side->mu);
+        if (hipEventRecord(side->fork, s) != hipSuccess ||
+            hipStreamWaitEvent(side->stream, side->fork, 0) != hipSuccess)
+            return fail(PP_EHIP, "pp_decode_batch: side-stream fork failed");
+        rc = launch_caf_bucketed(h, hr, n_img, K, C, skeleton, cfg, cfg->complete_caf_threshold,
+                                 cols[1], offs[1], nullptr, true, side->stream);
+        if (rc) {
+            (void)hipEventRecord(side->join, side->stream);
+            (void)hipStreamWaitEvent(s, side->join, 0);
+            return rc;
+        }
+    }
     if (stages & 1u) {
         if (d_cifhr)
             rc = cifhr_heads_launch<false>(h, n_img, K, cfg, d_cifhr, ws + d.off_cifhr_ws,
@@ -2327,7 +2347,7 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
     // PP_STAGE_COMPLETE_SETS_EARLY: the force-complete sets (every field and direction) with
     // CafScored instead of gated after the seed loop
     const bool early_b = (stages & PP_STAGE_COMPLETE_SETS_EARLY) && (stages & 4u) &&
-                         cfg->force_complete;
+                         !(stages & 1u) && cfg->force_complete;
     const SideStream *side = (stages & 6u) == 6u ? side_stream() : nullptr;
     if (side) {
         std::lock_guard<std::mutex> lock(side->mu);

@@ -8,6 +8,7 @@ Annotation objects.
 """
 import ctypes
 import logging
+import os
 
 import numpy as np
 import torch
@@ -309,6 +310,7 @@ class PendingRecords:
         self.dtype, self.device_records = dtype, dev
         self._compact, self._device_out = compact, device_out
         self._waited = False
+        self.on_counts = None  # callback(counts) once the pack is waited for
 
     def __del__(self):
         # the pinned block goes back to torch's host cache when this object dies; the raw
@@ -326,6 +328,8 @@ class PendingRecords:
         self._done.synchronize()
         self._waited = True
         status = self._host[4 * n:8 * n].numpy().view(np.int32)
+        if self.on_counts is not None:
+            self.on_counts(self._host[:4 * n].numpy().view(np.int32))
         bad = status & (PP_ST_ANN_OVERFLOW | PP_ST_DEC_OVERFLOW | PP_ST_NMS_OVERFLOW)
         if bad.any():
             raise PPError('decode status flags set (records truncated; decode() retries with '
@@ -373,6 +377,12 @@ def needs_refetch(recs):
             bool((recs['n_decoding'] & PP_PACK_REFETCH).any()))
 
 
+# PP_PIPE_BFIRST=1 / 0 forces the force-complete set order of DecodePipeline (auto below)
+_B_FIRST = {'1': True, '0': False}.get(os.environ.get('PP_PIPE_BFIRST', ''))
+# auto: sets first once a batch averaged this many annotations per image
+_B_FIRST_DENSITY = 32.0
+
+
 class DecodePipeline:
     """Decodes a sequence of batches with consecutive batches overlapped on the device.
 
@@ -389,6 +399,12 @@ class DecodePipeline:
     the streams in use -- current, back, tail, the library's CafScored side stream -- each
     get a hardware queue of their own: HIP shares 4 per process between streams.)
 
+    The force-complete sets go either after set A on the side stream (sparse batches) or
+    first, on the side stream before the CifHr map (dense batches, from the annotations
+    per image of the last batch whose records were read: >= 32; PP_PIPE_BFIRST=1 / 0
+    forces it).  Measured: planted 0.882 vs 0.905-0.930 ms, uniform 18.1 vs 17.3 ms per
+    step.  Either order gives the same records.
+
     submit() returns (buffers, PendingRecords of the batch: DecodeEngine.fetch_async).
     The current stream does not wait for the back half; the fields must stay unchanged
     until the batch's records are fetched."""
@@ -400,6 +416,7 @@ class DecodePipeline:
         self.tail = torch.cuda.Stream(device=self.device)
         self._back_done = [None, None]
         self._i = 0
+        self.density = 0.0  # annotations per image of the last batch whose records were read
 
     def submit(self, cif, caf, skeleton, cfg, cap=None, heads=None, compact=None,
                device_out=False, events=None):
@@ -422,10 +439,16 @@ class DecodePipeline:
         with torch.cuda.stream(front):
             if events:
                 events[0].record()
-            launch(STAGE_CIFHR)
+            b_first = _B_FIRST if _B_FIRST is not None else self.density >= _B_FIRST_DENSITY
+            if b_first:
+                # the force-complete sets start on the library's side stream before the
+                # CifHr map (they read only the CAF fields); the next call's join covers them
+                launch(STAGE_CIFHR | STAGE_COMPLETE_EARLY)
+            else:
+                launch(STAGE_CIFHR)
             if events:
                 events[1].record()
-            launch(STAGE_SEEDS | STAGE_CAF | STAGE_COMPLETE_EARLY)
+            launch(STAGE_SEEDS | STAGE_CAF | (0 if b_first else STAGE_COMPLETE_EARLY))
             if events:
                 events[2].record()
             front_done = torch.cuda.Event()
@@ -446,8 +469,12 @@ class DecodePipeline:
             back_done.record()
             pending = DecodeEngine.fetch_async(b, compact, device_out=device_out,
                                                stream=self.tail)
+        pending.on_counts = self._note_counts
         self._back_done[par] = back_done
         return b, pending
+
+    def _note_counts(self, counts):
+        self.density = float(counts.mean()) if len(counts) else 0.0
 
 
 _ENGINE = None
