@@ -393,7 +393,10 @@ def test_stage_calls_equal_full_decode(dec):
     eng = engine.DecodeEngine()
     ref, ref_off = eng.fetch(eng.launch(c, f, sk, cfg))
     ref = ref.copy()
-    for groups in ((1, 2, 4, 8), (1, 14), (15,)):
+    # 16: force-complete sets built early (with stage 4, or before the CifHr map with
+    # stage 1); 32 / 64: stage 8 split into the seed loop and the rest (same output slot)
+    for groups in ((1, 2, 4, 8), (1, 14), (15,), (1, 2 | 4 | 16, 8 | 16),
+                   (1, 2 | 4 | 16, 8 | 16 | 32, 8 | 16 | 64), (1 | 16, 2 | 4, 8 | 16 | 32, 8 | 16 | 64)):
         for bits in groups:
             b = eng.launch(c, f, sk, cfg, stages=bits)
         got, off = eng.fetch(b)
