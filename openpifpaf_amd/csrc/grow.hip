@@ -1789,9 +1789,10 @@ __global__ __launch_bounds__(64) void complete_kernel(GrowArgs g) {
         if (lane == 0) i = atomicAdd(&g.complete_next[img], 1);
         i = __builtin_amdgcn_readfirstlane(i);
         if (i >= n_anns) break;
-        bool has0 = false;
-        for (int j = 0; j < K; j++) has0 = has0 || work[i].data[j][2] == 0.0f;
-        if (!has0) continue;
+        // one vector load for the K visibilities (a short-circuit loop over them would wait
+        // for each in turn)
+        const float vj = lane < K ? work[i].data[lane][2] : 1.0f;
+        if (!__ballot(lane < K && vj == 0.0f)) continue;
         copy_ann(&L.a, &work[i]);
         uint32_t unfilled = 0;
         for (int j = 0; j < K; j++) unfilled |= (L.a.data[j][2] == 0.0f) ? (1u << j) : 0u;
