@@ -1,9 +1,11 @@
-// grow.hip — the CifCaf greedy decoder (generator/cifcaf.py) as one gfx950 wave per image.
+// grow.hip — the CifCaf greedy decoder (generator/cifcaf.py) on gfx950.
 //
 // The seed loop is sequential by construction (each annotation's occupancy marks decide
-// whether later seeds start annotations, cifcaf.py:100-108), so an image is one wave64
-// workgroup and a batch fills the chip with one workgroup per image.  A single wave has no
-// other wave to hide latency behind, so the serial state lives in REGISTERS, not memory:
+// whether later seeds start annotations, cifcaf.py:100-108), so an image is one workgroup
+// and a batch fills the chip with one workgroup per image.  Inside it, wave 0 commits in
+// the reference order while seven helper waves grow seeds it is likely to reach (a grow is
+// a pure function of the seed and the CAF columns); each wave's serial state lives in
+// REGISTERS, not memory:
 //
 //   * the annotation being grown: lane j holds joint j's (x, y, v, scale);
 //   * the frontier (cifcaf.py:248 PriorityQueue): at most one entry per directed skeleton
@@ -11,23 +13,23 @@
 //     the popped unevaluated entry), so lane d holds the entry of directed edge d (by_source
 //     order, cifcaf.py:62-65) and pop-min is a wave reduction with the reference's tuple
 //     order (-score, None|xysv, j, k);
-//   * caf_center_s + scoring (functional.pyx:338-359, cifcaf.py:124-145): 64 lanes scan the
-//     CAF columns of the buckets the 2*scale box overlaps (caf_bucketed_kernel), loading
-//     each candidate's rows in one round, and a 6-step xor-shuffle merge yields the argsort
-//     top-2 _target_with_blend (cifcaf.py:157-192) needs, targets included;
+//   * caf_center_s + scoring (functional.pyx:338-359, cifcaf.py:124-145): the lanes scan
+//     the CAF columns (the image's small set-A sets from LDS, else the buckets the 2*scale
+//     box overlaps, caf_bucketed_kernel) and merge the argsort top-2 _target_with_blend
+//     (cifcaf.py:157-192) needs, targets included;
 //   * occupancy grids (occupancy.py, u8 += 1 with wrap) live in a per-image workspace that
 //     every launch leaves zeroed: each box a launch marks is logged and cleared again.
 //
-// Float arithmetic is f32 op-for-op as NumPy evaluates it (NEP 50); np.exp is computed
-// correctly rounded through f64.
+// Force-complete (cifcaf.py:333-351) spreads an image's annotations over 64 workgroups;
+// NMS (nms.py:17-57) is one 8-wave workgroup per image.  Float arithmetic is f32
+// op-for-op as NumPy evaluates it (NEP 50); np.exp is computed correctly rounded through
+// f64.
 #include "pp_common.hpp"
-
-#include <stdlib.h>
-
-#include <mutex>
 
 #include <stdio.h>
 #include <stdlib.h>
+
+#include <mutex>
 
 // Diagnostic build only (-DPP_STAMPS, libpifpaf_amd_stamps.so): per-section shader-cycle
 // sums of the decode kernel, dumped to $PP_STAMPS_OUT.  The product build compiles these
