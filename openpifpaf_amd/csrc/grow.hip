@@ -399,11 +399,7 @@ __device__ __forceinline__ void consider_vals(const ColQuery &q, float c0, float
     const float dx = q.x - c1, dy = q.y - c2;
     const float dd = sqrtf(dx * dx + dy * dy);  // np.linalg.norm(axis=0)
     const float qq = (-0.5f * (dd * dd)) / q.sigma2;
-#ifdef PP_EXP_FEXP
-    const float score = expf(qq) * c0;  // timing experiment only
-#else
     const float score = (float)exp((double)qq) * c0;  // np.exp, correctly rounded
-#endif
     top2_insert(t, cand_key<MAXM>(score, o), tx, ty, tc);
 }
 
@@ -1440,13 +1436,8 @@ __device__ void sort_by_score(int *perm, int np, int n, const double *score) {
 // to grow one itself, and a helper publishes its annotation (cache slot state 2) whenever
 // it finishes.  Wave 0 waits on a helper only for the seed it needs next, if that helper
 // is still growing it.  The handshake is LDS flags with workgroup-scope acquire/release.
-#if defined(PP_EXP_W4)
-constexpr int kSeedWaves = 4;
-#elif defined(PP_EXP_W6)
-constexpr int kSeedWaves = 6;
-#else
-constexpr int kSeedWaves = 8;      // 16 (cache 32, scan 256): 1.79 vs 1.28 ms per cfg3 step
-#endif
+// 8 waves; 16 (cache 32, scan 256): 1.79 vs 1.28 ms per cfg3 step; 4 / 6: no better
+constexpr int kSeedWaves = 8;
 constexpr int kSpecCache = 16;     // speculative annotations kept per image
 constexpr int kSpecScan = 128;     // seeds after the committed one examined per round
 // distance (joint scales) a helper's seed keeps from the committed one and from the
@@ -1607,9 +1598,7 @@ void seed_loop_kernel(GrowArgs g) {
             wave_sync();
         }
     } else {
-#ifndef PP_EXP_NOPRIO
         __builtin_amdgcn_s_setprio(3);  // the committer is the critical path: issue first
-#endif
         for (;;) {
             // the next free seed (cifcaf.py:100-104): 64 occupancy tests per step
             int t = -1;

@@ -779,11 +779,7 @@ __global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
 // MULTI (cif_hr.py:59-73): groups fold into zero separately and combine by np.maximum;
 // candidates carry their group, and a change of group closes the running fold into res.
 // Across passes res stays in the map and the open group's fold in `aux`.
-#ifdef PP_EXP_SPU16
-constexpr int kSpU = 16;
-#else
 constexpr int kSpU = 32;      // cells per thread per compaction round (confidences in flight)
-#endif
 constexpr int kSpStage = 1024; // kept cells of a round staged in LDS (phase 2's s_cand space)
 
 struct HrSparseArgs {
