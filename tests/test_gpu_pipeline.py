@@ -34,3 +34,35 @@ def test_pipeline_matches_engine_decode(b_first, monkeypatch):
         recs, offsets = p.result()
         np.testing.assert_array_equal(offsets, w_off)
         assert recs.tobytes() == w_bytes
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', ['ms2', 'ms10'])
+def test_pipeline_multi_scale_matches_engine_decode(name):
+    """The pipeline over multi-scale HeadSets (pp_decode_multi, stage by stage on three
+    streams) gives the one-stream records byte for byte."""
+    import torch
+    from openpifpaf_amd.decoder import FieldConfig
+    from openpifpaf_amd.engine import DecodeEngine, DecodePipeline, HeadSet
+    skel = constants.COCO_PERSON_SKELETON
+    cfg = make_config(**EVAL_CONFIG)
+    sets = []
+    for rep in range(3):
+        per = [synthetic.multi_case(name, seed=10 * rep + i, h_px=161, w_px=161, n_people=4)
+               for i in range(4)]
+        fields = [torch.from_numpy(np.stack([p[0][j] for p in per])).cuda()
+                  for j in range(len(per[0][0]))]
+        sets.append(HeadSet(fields, FieldConfig(**per[0][1])))
+    eng = DecodeEngine()
+    want = []
+    for heads in sets:
+        recs, offsets, _ = eng.decode(None, None, skel, cfg, cap=512, heads=heads,
+                                      compact=PACK_ALL)
+        want.append((recs.tobytes(), offsets.copy()))
+    pipe = DecodePipeline()
+    pend = [pipe.submit(None, None, skel, cfg, cap=512, heads=heads,
+                        compact=(heads.k, len(skel), PACK_ALL))[1] for heads in sets]
+    for (w_bytes, w_off), p in zip(want, pend):
+        recs, offsets = p.result()
+        np.testing.assert_array_equal(offsets, w_off)
+        assert recs.tobytes() == w_bytes
