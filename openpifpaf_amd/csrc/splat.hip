@@ -150,12 +150,14 @@ __device__ __forceinline__ FoldTerm fold_term(const FoldCand &c, float fx, float
     const float dx = fx - c.cx, dy = fy - c.cy;
     const float dx2 = dx * dx, dy2 = dy * dy;  // powf(d, 2.0)
     const float sum = dx2 + dy2;
-    const float num = -0.5f * sum;
-    float q = SLOW ? num / c.s2 : div_refined(num, Recip{c.s2, c.r});
+    // approx_exp(-0.5 * sum / s2) starts with 1 + x / 8: x = (-0.5 * sum) / s2 is
+    // -0.5 * (sum / s2) exactly (scaling by a power of two commutes with rounding; where
+    // sum / s2 is subnormal both give 1 + x / 8 = 1), so the -0.5 / 8 goes into the fma
+    float q = SLOW ? sum / c.s2 : div_refined(sum, Recip{c.s2, c.r});
     // "closest pixel" (vv = v): q = 0 gives t = 1 exactly, so v * t = v; a select on q keeps
     // the fold branch-free
     q = (key == c.nkey) ? 0.0f : q;
-    float t = __builtin_fmaf(q, 0.125f, 1.0f);  // 1 + q / 8 (q * 0.125 is exact)
+    float t = __builtin_fmaf(q, -0.0625f, 1.0f);  // 1 + x / 8 (q * -0.0625 is exact)
     t = t * t;
     t = t * t;
     t = t * t;

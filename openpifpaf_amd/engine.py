@@ -377,8 +377,9 @@ def needs_refetch(recs):
             bool((recs['n_decoding'] & PP_PACK_REFETCH).any()))
 
 
-# PP_PIPE_BFIRST=1 / 0 forces the force-complete set order of DecodePipeline (auto below)
-_B_FIRST = {'1': True, '0': False}.get(os.environ.get('PP_PIPE_BFIRST', ''))
+# PP_PIPE_BFIRST=1 / 0 / lazy forces the force-complete set order of DecodePipeline (auto
+# below); lazy: gated after the seed loop, on the tail stream
+_B_FIRST = {'1': True, '0': False, 'lazy': 'lazy'}.get(os.environ.get('PP_PIPE_BFIRST', ''))
 # auto: sets first once a batch averaged this many annotations per image
 _B_FIRST_DENSITY = 32.0
 
@@ -440,7 +441,10 @@ class DecodePipeline:
             if events:
                 events[0].record()
             b_first = _B_FIRST if _B_FIRST is not None else self.density >= _B_FIRST_DENSITY
-            if b_first:
+            early = 0 if b_first == 'lazy' else STAGE_COMPLETE_EARLY
+            if b_first == 'lazy':
+                launch(STAGE_CIFHR)
+            elif b_first:
                 # the force-complete sets start on the library's side stream before the
                 # CifHr map (they read only the CAF fields); the next call's join covers them
                 launch(STAGE_CIFHR | STAGE_COMPLETE_EARLY)
@@ -448,7 +452,7 @@ class DecodePipeline:
                 launch(STAGE_CIFHR)
             if events:
                 events[1].record()
-            launch(STAGE_SEEDS | STAGE_CAF | (0 if b_first else STAGE_COMPLETE_EARLY))
+            launch(STAGE_SEEDS | STAGE_CAF | (0 if b_first else early))
             if events:
                 events[2].record()
             front_done = torch.cuda.Event()
@@ -457,12 +461,12 @@ class DecodePipeline:
         with torch.cuda.stream(self.back):
             if events:
                 events[3].record()
-            launch(STAGE_GROW | STAGE_COMPLETE_EARLY | STAGE_SEED_LOOP_ONLY)
+            launch(STAGE_GROW | early | STAGE_SEED_LOOP_ONLY)
             loop_done = torch.cuda.Event()
             loop_done.record()
         self.tail.wait_event(loop_done)
         with torch.cuda.stream(self.tail):
-            b = launch(STAGE_GROW | STAGE_COMPLETE_EARLY | STAGE_AFTER_SEED_LOOP)
+            b = launch(STAGE_GROW | early | STAGE_AFTER_SEED_LOOP)
             if events:
                 events[4].record()
             back_done = torch.cuda.Event()

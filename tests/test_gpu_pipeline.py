@@ -8,12 +8,12 @@ from openpifpaf_amd._abi import EVAL_CONFIG, PACK_ALL, make_config
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('b_first', [False, True])
+@pytest.mark.parametrize('b_first', [False, True, 'lazy'])
 def test_pipeline_matches_engine_decode(b_first, monkeypatch):
     import torch
     from openpifpaf_amd import engine
     from openpifpaf_amd.engine import DecodeEngine, DecodePipeline
-    monkeypatch.setattr(engine, '_B_FIRST', b_first)  # both orders of the force-complete sets
+    monkeypatch.setattr(engine, '_B_FIRST', b_first)  # every placement of the force-complete sets
     skel = constants.COCO_PERSON_SKELETON
     cfg = make_config(**EVAL_CONFIG)
     compact = (17, len(skel), PACK_ALL)
