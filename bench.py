@@ -144,7 +144,12 @@ def main():
         args.workload = 'cfg3' if world == 1 else 'cfg4'
 
     from openpifpaf_amd import build as ppbuild
-    ppbuild.build(verbose=False)
+    # a no-op when the in-tree library is newer than its sources; otherwise only rank 0
+    # builds, so ranks started together never link or load a half-written library
+    if rank == 0:
+        ppbuild.build(verbose=False)
+    if world > 1:
+        dist.barrier()
     from openpifpaf_amd import constants, synthetic
     from openpifpaf_amd.distributed import gather_packed
     from openpifpaf_amd._abi import (ANN_DTYPE, EVAL_CONFIG, PACK_ALL, PREDICT_CONFIG, make_config,
