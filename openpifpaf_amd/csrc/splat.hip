@@ -977,6 +977,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
 #endif
     for (int t = threadIdx.x; t < a.tiles; t += 256)  // untouched tiles: no block written
         if (!((s_bits[t >> 5] >> (t & 31)) & 1u)) a.masks[fld * a.tiles + t] = 0ull;
+#ifdef PP_EXP_PHASE1
+    return;  // timing / counter experiment: phase 1 (list, bins, tile masks) only
+#endif
 
     // ---- phase 2: touched tiles, one wave each, claimed from an LDS counter ----
     FoldCand *cand = s_cand[wave];
