@@ -192,16 +192,18 @@ __device__ __forceinline__ float fold_block(float acc, const FoldCand *cand, uin
         }
         return acc;
     }
-    while (q) {
+    // a counted loop over the pairs, the odd one after it: one scalar branch per pair
+    const int np = __popcll(q);
+    for (int i = 1; i < np; i += 2) {
         const int c1 = __builtin_ctzll(q);
         q &= q - 1;
-        if (!q) return fold_apply(acc, fold_term<false>(cand[c1], fx, fy, key));
         const int c2 = __builtin_ctzll(q);
         q &= q - 1;
         const FoldTerm f1 = fold_term<false>(cand[c1], fx, fy, key);
         const FoldTerm f2 = fold_term<false>(cand[c2], fx, fy, key);
         acc = fold_apply(fold_apply(acc, f1), f2);
     }
+    if (np & 1) acc = fold_apply(acc, fold_term<false>(cand[__builtin_ctzll(q)], fx, fy, key));
     return acc;
 }
 
