@@ -196,9 +196,9 @@ __device__ __forceinline__ float fold_block(float acc, const FoldCand *cand, uin
     const int np = __popcll(q);
     for (int i = 1; i < np; i += 2) {
         const int c1 = __builtin_ctzll(q);
-        q &= q - 1;
+        q &= ~(1ull << c1);  // one s_bitset0 (q &= q - 1 takes three scalar ops)
         const int c2 = __builtin_ctzll(q);
-        q &= q - 1;
+        q &= ~(1ull << c2);
         const FoldTerm f1 = fold_term<false>(cand[c1], fx, fy, key);
         const FoldTerm f2 = fold_term<false>(cand[c2], fx, fy, key);
         acc = fold_apply(fold_apply(acc, f1), f2);
