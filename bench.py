@@ -197,6 +197,8 @@ def main():
 
     comm = torch.cuda.Stream(device=dev) if world > 1 and args.backend == 'nccl' else None
     counters = {'refetch_steps': 0, 'pack_bytes': 0}
+    gather = {'steps': 0, 'verified_steps': 0, 'ranks_seen': world, 'full_record_steps': 0,
+              'bytes': 0}
 
     def timed_run(cif, caf, steps, warmup, heads=None, skel=None, n_stages=None):
         """warmup + `steps` timed decode steps of one resident batch (cif / caf, or a
@@ -251,12 +253,27 @@ def main():
                     raise SystemExit('record block too small after warmup')
                 if comm is not None:
                     comm.wait_event(pending.done_event)
-                src = pending.device_records if rank != 0 else pending.host_records()
+                # a pack that flagged PP_PACK_REFETCH sends the full records instead
+                full = pending.refetch
+                with torch.cuda.stream(comm) if comm is not None else torch.cuda.stream(None):
+                    src = (pending.full_device_records() if full else
+                           pending.device_records if rank != 0 else pending.host_records())
+                width = (ANN_DTYPE if full else pending.dtype).itemsize
                 if comm_dev.type == 'cpu':
-                    src = src[:int(counts.sum()) * pending.dtype.itemsize].cpu()
+                    src = src[:int(counts.sum()) * width].cpu()
+                rep = {}
                 recs, _ = gather_packed(src, counts, dist, n_max=n_img, dtype=pending.dtype,
-                                        device=comm_dev, stream=comm)
+                                        device=comm_dev, stream=comm, full=full, k=k_img,
+                                        c=len(skel), report=rep)
                 n_recs = len(recs) if recs is not None else 0
+                if rank == 0:
+                    # every step's transfers are checked: each sender's digest of its record
+                    # bytes against rank 0's digest of what arrived
+                    gather['steps'] += 1
+                    gather['verified_steps'] += int(rep['ranks_verified'] == world)
+                    gather['ranks_seen'] = min(gather['ranks_seen'], rep['ranks_seen'])
+                    gather['full_record_steps'] += int(rep['full_records'])
+                    gather['bytes'] = rep['bytes']
             if timed:
                 last = max(j for _, j in ev_pairs)
                 ev[last].synchronize()
@@ -368,6 +385,15 @@ def main():
             'dense_equivalent_gbs': round(dense_bytes / (stage_avg[0] * 1e-3) / 1e9, 1),
         },
     }
+    if world > 1:
+        # the multi-GPU hand-over proves itself: every gathered step (the untimed one before
+        # the clock and all timed ones) had each sender's record digest match on rank 0
+        line['gather_verified'] = bool(gather['steps'] > 0 and
+                                       gather['verified_steps'] == gather['steps'])
+        line['ranks_seen'] = gather['ranks_seen']
+        line['gather'] = {'steps': gather['steps'], 'verified_steps': gather['verified_steps'],
+                          'full_record_steps': gather['full_record_steps'],
+                          'bytes_per_step_rank0': gather['bytes']}
     default_run = (args.workload in ('cfg3', 'cfg4') and args.generator == 'planted' and
                    args.mode == 'eval' and batch == WORKLOADS['cfg3']['batch'])
     if default_run:

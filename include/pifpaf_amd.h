@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PP_ABI_VERSION 1
+#define PP_ABI_VERSION 2
 
 /* capacities of one annotation record (COCO person: 17 keypoints, 19 or 44 edges) */
 #define PP_MAX_KP 24
@@ -391,6 +391,9 @@ int pp_pack_records(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img
  *   PP_PACK_FRONTIER: u8 frontier_pairs[F][2] (padded to 4 B), F = min(PP_MAX_FRONTIER, 4*C)
  * A record whose decoding entries disagree with the per-joint x / y, or whose orders exceed
  * K / F entries, carries PP_PACK_REFETCH: fetch that decode's full pp_ann records instead.
+ * `out_flags` (optional, NULL to skip; device or pinned host memory, n_img int32): set to 1
+ * for an image with at least one flagged record, else 0 -- so a caller whose records stay in
+ * device memory (the multi-GPU gather) learns of a refetch without reading them.
  * `out` (16-byte aligned) holds out_capacity records; device or pinned host memory as for
  * pp_pack_records.  Reference consumer: Generator.batch's per-image lists
  * (generator.py:96-97).
@@ -401,7 +404,8 @@ int pp_pack_records(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img
 int64_t pp_packed_record_size(int32_t K, int32_t C, uint32_t flags);
 int pp_pack_compact(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img,
                     int32_t ann_capacity, int32_t K, int32_t C, uint32_t flags, void *out,
-                    int64_t out_capacity, int32_t *out_counts, void *stream);
+                    int64_t out_capacity, int32_t *out_counts, int32_t *out_flags,
+                    void *stream);
 
 /*
  * The same decode split into stages for measurement: bit 1 CifHr, 2 CifSeeds,

@@ -3,7 +3,7 @@ import ctypes
 
 import numpy as np
 
-PP_ABI_VERSION = 1
+PP_ABI_VERSION = 2
 PP_MAX_KP = 24
 PP_MAX_EDGES = 64
 PP_MAX_FRONTIER = 4 * PP_MAX_EDGES

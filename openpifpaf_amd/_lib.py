@@ -40,7 +40,7 @@ _SIGNATURES = {
                       ctypes.c_int),
     'pp_pack_records': ([_vp, _vp, _i32, _i32, _vp, _i64, _vp, _vp], ctypes.c_int),
     'pp_packed_record_size': ([_i32, _i32, _u32], _i64),
-    'pp_pack_compact': ([_vp, _vp, _i32, _i32, _i32, _i32, _u32, _vp, _i64, _vp, _vp],
+    'pp_pack_compact': ([_vp, _vp, _i32, _i32, _i32, _i32, _u32, _vp, _i64, _vp, _vp, _vp],
                         ctypes.c_int),
     'pp_decode_workspace_size': ([_i32, _i32, _i32, _i32, _i32, _vp, _i32], _sz),
     'pp_decode_workspace_zero_offset': ([_i32, _i32, _i32, _i32, _i32, _vp, _i32], _sz),

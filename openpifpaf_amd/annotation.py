@@ -53,8 +53,11 @@ class Annotation:
         ann.data = np.array(rec['data'][:k], dtype=np.float32)
         ann.joint_scales = np.array(rec['joint_scales'][:k], dtype=np.float32)
         names = rec.dtype.names
+        if int(rec['n_decoding']) & 0x8000:  # PP_PACK_REFETCH: the compact form is incomplete
+            raise ValueError('compact record flagged PP_PACK_REFETCH: its decoding / frontier '
+                             'order does not fit; fetch the full pp_ann record instead')
         if 'decoding_pairs' in names:
-            nd = int(rec['n_decoding']) & 0x7fff
+            nd = int(rec['n_decoding'])
             pairs, dv, dxy = rec['decoding_pairs'], rec['decoding_v'], rec['decoding_xy']
             order = []
             for t in range(nd):

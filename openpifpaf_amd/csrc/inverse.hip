@@ -243,12 +243,13 @@ __device__ __forceinline__ uint32_t packed_word(const pp_ann &a, const PackLayou
 __global__ __launch_bounds__(256) void pack_compact_kernel(const pp_ann *__restrict__ anns,
                                                            const int *__restrict__ counts, int n,
                                                            int cap, PackLayout L, char *out,
-                                                           int64_t out_cap, int *out_counts) {
-    __shared__ int s_off;
+                                                           int64_t out_cap, int *out_counts,
+                                                           int *out_flags) {
+    __shared__ int s_off, s_bad;
     __shared__ float s_jxy[4][2 * PP_MAX_KP];
     const int img = blockIdx.x;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (threadIdx.x == 0) s_off = 0;
+    if (threadIdx.x == 0) s_off = s_bad = 0;
     __syncthreads();
     int part = 0;
     for (int j = threadIdx.x; j < img; j += 256) part += counts[j];
@@ -295,6 +296,7 @@ __global__ __launch_bounds__(256) void pack_compact_kernel(const pp_ann *__restr
             }
         }
         bad = __ballot(bad) != 0ull;
+        if (bad && lane == 0) s_bad = 1;
         if (lane < L.K) {
             s_jxy[wave][2 * lane] = jx;
             s_jxy[wave][2 * lane + 1] = jy;
@@ -312,6 +314,10 @@ __global__ __launch_bounds__(256) void pack_compact_kernel(const pp_ann *__restr
             dst[c] = v;
         }
         wave_sync();  // s_jxy is rewritten for the wave's next record
+    }
+    if (out_flags) {  // one plain store per image: no atomics across PCIe
+        __syncthreads();
+        if (threadIdx.x == 0) out_flags[img] = s_bad;
     }
 }
 
@@ -380,7 +386,8 @@ int64_t pp_packed_record_size(int32_t K, int32_t C, uint32_t flags) {
 
 int pp_pack_compact(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img,
                     int32_t ann_capacity, int32_t K, int32_t C, uint32_t flags, void *out,
-                    int64_t out_capacity, int32_t *out_counts, void *stream) {
+                    int64_t out_capacity, int32_t *out_counts, int32_t *out_flags,
+                    void *stream) {
     if (!d_anns || !d_counts || !out || !out_counts)
         return fail(PP_EINVAL, "pp_pack_compact: NULL argument");
     if (n_img < 0 || ann_capacity <= 0 || out_capacity < 0 || K <= 0 || K > PP_MAX_KP || C <= 0 ||
@@ -389,8 +396,9 @@ int pp_pack_compact(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img
     if (flags & ~(uint32_t)(PP_PACK_DECODING | PP_PACK_FRONTIER))
         return fail(PP_EINVAL, "pp_pack_compact: unknown flag");
     if (n_img == 0) return PP_OK;
-    void *dst[2] = {out, out_counts};
+    void *dst[3] = {out, out_counts, out_flags};
     for (void *&d : dst) {
+        if (!d) continue;  // out_flags is optional
         hipPointerAttribute_t at;
         if (hipPointerGetAttributes(&at, d) != hipSuccess || !at.devicePointer ||
             (at.type != hipMemoryTypeDevice && at.type != hipMemoryTypeHost)) {
@@ -404,7 +412,8 @@ int pp_pack_compact(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img
         return fail(PP_EINVAL, "pp_pack_compact: destination not 16-byte aligned");
     hipLaunchKernelGGL(pack_compact_kernel, dim3((unsigned)n_img), dim3(256), 0,
                        (hipStream_t)stream, d_anns, d_counts, n_img, ann_capacity,
-                       pack_layout(K, C, flags), (char *)dst[0], out_capacity, (int *)dst[1]);
+                       pack_layout(K, C, flags), (char *)dst[0], out_capacity, (int *)dst[1],
+                       (int *)dst[2]);
     return check_launch("pp_pack_compact");
 }
 

@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 from . import _device
-from ._abi import (ANN_DTYPE, PP_PACK_REFETCH, PP_ST_ANN_OVERFLOW, PP_ST_DEC_OVERFLOW,
+from ._abi import (ANN_DTYPE, PP_ST_ANN_OVERFLOW, PP_ST_DEC_OVERFLOW,
                    PP_ST_NMS_OVERFLOW, packed_dtype, scale_list, skeleton_array)
 from ._lib import PPError, call, load
 
@@ -241,9 +241,13 @@ class DecodeEngine:
         n = b.n
         dtype = ANN_DTYPE if compact is None else packed_dtype(*compact)
         width = dtype.itemsize
-        head = -(-8 * n // 256) * 256  # counts (n int32), then the slot's status (n int32)
+        # head: counts (n int32), the slot's status (n int32), per-image refetch flags
+        # (n int32, pp_pack_compact's out_flags), then the records
+        head = -(-12 * n // 256) * 256
         host = torch.empty(head + (0 if device_out else est * width), dtype=torch.uint8,
                            pin_memory=True)
+        if compact is None:
+            host[8 * n:12 * n].zero_()
         dev = (torch.empty(est * width, dtype=torch.uint8, device=anns.device)
                if device_out else None)
         out_ptr = dev.data_ptr() if device_out else host.data_ptr() + head
@@ -260,7 +264,8 @@ class DecodeEngine:
                 k, c, flags = compact
                 call('pp_pack_compact', _device.ptr(anns), _device.ptr(counts), n, b.cap,
                      k, c, ctypes.c_uint32(flags), ctypes.c_void_p(out_ptr), est,
-                     ctypes.c_void_p(host.data_ptr()), _device.stream())
+                     ctypes.c_void_p(host.data_ptr()),
+                     ctypes.c_void_p(host.data_ptr() + 8 * n), _device.stream())
             host[4 * n:8 * n].copy_(status.view(torch.uint8), non_blocking=True)
             done = torch.cuda.Event()
             done.record()
@@ -340,6 +345,14 @@ class PendingRecords:
     def done_event(self):
         return self._done
 
+    @property
+    def refetch(self):
+        """True when a compact record of this fetch is flagged PP_PACK_REFETCH (valid after
+        wait(); from pp_pack_compact's per-image flags, so device-resident records need not
+        be read)."""
+        n = self._b.n
+        return bool(self._host[8 * n:12 * n].numpy().view(np.int32).any())
+
     def host_records(self):
         """The pinned block's record area (a CPU uint8 tensor; valid after wait())."""
         return self._host[self._head:]
@@ -366,15 +379,20 @@ class PendingRecords:
             recs = host.numpy().view(self.dtype)
         else:
             recs = self._host[self._head:self._head + total * width].numpy().view(self.dtype)
-        if needs_refetch(recs):
+        if self.refetch:
             return DecodeEngine.fetch_gather(self._b, self._slot[0], self._slot[1])
         return recs, offsets
 
-
-def needs_refetch(recs):
-    """True when a compact record is flagged PP_PACK_REFETCH (its orders do not fit)."""
-    return (recs.dtype != ANN_DTYPE and len(recs) > 0 and
-            bool((recs['n_decoding'] & PP_PACK_REFETCH).any()))
+    def full_device_records(self):
+        """The decode's full pp_ann records as one device uint8 tensor (image after image;
+        what a multi-GPU rank sends instead of compact records after a refetch)."""
+        b, anns = self._b, self._slot[0]
+        counts = self.wait()
+        offsets = np.concatenate([[0], np.cumsum(counts)])
+        idx = np.arange(int(offsets[-1]), dtype=np.int64) + np.repeat(
+            np.arange(len(counts), dtype=np.int64) * b.cap - offsets[:-1], counts)
+        rows = anns.view(b.n * b.cap, ANN_DTYPE.itemsize)
+        return rows.index_select(0, torch.from_numpy(idx).to(rows.device)).reshape(-1)
 
 
 # PP_PIPE_BFIRST=1 / 0 / lazy forces the force-complete set order of DecodePipeline (auto

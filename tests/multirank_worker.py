@@ -37,9 +37,12 @@ def main():
     counts = pend.wait()
     nbytes = int(counts.sum()) * pend.dtype.itemsize
     src = (pend.device_records if rank != 0 else pend.host_records())[:nbytes].cpu()
+    assert not pend.refetch
+    report = {}
     recs, offs = gather_packed(src, counts, dist, n_max=max_shard(N, world), dtype=pend.dtype,
-                               device=torch.device('cpu'))
+                               device=torch.device('cpu'), report=report)
     if rank == 0:
+        assert report['ranks_seen'] == world and report['ranks_verified'] == world, report
         ref, ref_offs, _ = DecodeEngine().decode(cif, caf, skel, cfg, compact=PACK_ALL)
         assert ref.dtype == recs.dtype, 'one-process decode fell back to full records'
         assert np.array_equal(offs, ref_offs), (offs[:8], ref_offs[:8])

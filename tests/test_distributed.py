@@ -12,7 +12,8 @@ import torch.multiprocessing as mp
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from openpifpaf_amd._abi import ANN_DTYPE, PACK_ALL, packed_dtype  # noqa: E402
-from openpifpaf_amd.distributed import gather_records, shard  # noqa: E402
+from openpifpaf_amd.distributed import (digest, expand_compact, gather_packed,  # noqa: E402
+                                        gather_records, shard)
 
 
 def test_shard_covers_batch():
@@ -42,16 +43,37 @@ def _rank_records(rank, n_img, dtype):
     return recs, np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
 
 
+def _compact_records(rank, n_img):
+    """Fake compact records that expand_compact accepts: valid joint indices in the
+    decoding pairs, counts within K / F."""
+    dtype = DTYPES['compact']
+    recs, offs = _rank_records(rank, n_img, dtype)
+    rng = np.random.default_rng(7 + rank)
+    recs['n_decoding'] = rng.integers(0, 17, len(recs))
+    recs['n_frontier'] = rng.integers(0, 4 * 19, len(recs))
+    recs['decoding_pairs'] = rng.integers(0, 17, recs['decoding_pairs'].shape)
+    recs['decoding_xy'] = rng.random(recs['decoding_xy'].shape, dtype=np.float32)
+    recs['decoding_v'] = rng.random(recs['decoding_v'].shape, dtype=np.float32)
+    recs['frontier_pairs'] = rng.integers(0, 17, recs['frontier_pairs'].shape)
+    return recs, offs
+
+
 def _worker(rank, world, port, n_imgs, kind):
     dist.init_process_group('gloo', init_method='tcp://127.0.0.1:{}'.format(port),
                             rank=rank, world_size=world)
-    dtype = DTYPES[kind]
     try:
-        recs, offs = _rank_records(rank, n_imgs[rank], dtype)
-        got, got_offs = gather_records(recs, offs, dist, torch.device('cpu'))
-        if rank != 0:  # records are collected on rank 0 only
-            assert got is None and got_offs is None
+        if kind == 'mixed':
+            _mixed_worker(rank, world, n_imgs)
             return
+        dtype = DTYPES[kind]
+        recs, offs = _rank_records(rank, n_imgs[rank], dtype)
+        report = {}
+        got, got_offs = gather_records(recs, offs, dist, torch.device('cpu'), report=report)
+        if rank != 0:  # records are collected on rank 0 only
+            assert got is None and got_offs is None and not report
+            return
+        # every rank's metadata arrived and every sender's digest matched on rank 0
+        assert report['ranks_seen'] == world and report['ranks_verified'] == world
         exp = [_rank_records(r, n_imgs[r], dtype) for r in range(world)]
         assert got.dtype == dtype
         # image indices rebased to the global batch (rank r's images follow rank r - 1's)
@@ -69,6 +91,76 @@ def _worker(rank, world, port, n_imgs, kind):
         assert got_offs.tolist() == exp_offs
     finally:
         dist.destroy_process_group()
+
+
+def _mixed_worker(rank, world, n_imgs):
+    """Rank 1 had a PP_PACK_REFETCH and sends full records; the others send compact ones,
+    which rank 0 expands so the gathered array has one dtype."""
+    recs, offs = _compact_records(rank, n_imgs[rank])
+    full = rank == 1
+    if full:
+        recs = expand_compact(recs, 17, 19)
+    data = torch.from_numpy(recs.view(np.uint8).reshape(-1))
+    report = {}
+    got, got_offs = gather_packed(data, np.diff(offs), dist, n_max=max(n_imgs),
+                                  dtype=DTYPES['compact'], device=torch.device('cpu'),
+                                  full=full, k=17, c=19, report=report)
+    if rank != 0:
+        assert got is None
+        return
+    assert report['full_records'] and report['ranks_verified'] == world
+    exp, base = [], 0
+    for r in range(world):
+        e = expand_compact(_compact_records(r, n_imgs[r])[0], 17, 19)
+        e['image'] += base
+        base += n_imgs[r]
+        exp.append(e)
+    assert got.dtype == ANN_DTYPE
+    assert got.tobytes() == b''.join(e.tobytes() for e in exp)
+    assert got_offs[-1] == len(got)
+
+
+def test_digest_detects_changes():
+    rng = np.random.default_rng(0)
+    a = torch.from_numpy(rng.integers(0, 256, 4096, dtype=np.uint8))
+    d0 = digest(a)
+    assert torch.equal(d0, digest(a.clone()))
+    for pos in (0, 1, 2047, 4095):
+        b = a.clone()
+        b[pos] ^= 1
+        assert not torch.equal(d0, digest(b))
+    # swapping two words changes it too (position-weighted)
+    b = a.clone()
+    b[0:4], b[4:8] = a[4:8].clone(), a[0:4].clone()
+    assert torch.equal(a[0:4], a[4:8]) or not torch.equal(d0, digest(b))
+    assert digest(a[:0]).tolist() == [0, 0]
+
+
+def test_expand_compact_roundtrip_fields():
+    recs, _ = _compact_records(0, 6)
+    full = expand_compact(recs, 17, 19)
+    for i, r in enumerate(recs):
+        f = full[i]
+        nd = int(r['n_decoding'])
+        assert f['n_decoding'] == nd and f['n_frontier'] == r['n_frontier']
+        assert np.array_equal(f['data'][:17], r['data'])
+        for t in range(nd):
+            js, jt = r['decoding_pairs'][t]
+            assert np.array_equal(f['decoding_xyv'][t][:2], r['decoding_xy'][js])
+            assert f['decoding_xyv'][t][2] == r['decoding_v'][t][0]
+            assert np.array_equal(f['decoding_xyv'][t][3:5], r['decoding_xy'][jt])
+            assert f['decoding_xyv'][t][5] == r['decoding_v'][t][1]
+        assert not f['decoding_xyv'][nd:].any() and not f['decoding_pairs'][nd:].any()
+    flagged = recs.copy()
+    flagged['n_decoding'][0] |= 0x8000
+    with pytest.raises(ValueError):
+        expand_compact(flagged, 17, 19)
+
+
+@pytest.mark.parametrize('n_imgs', [(3, 4), (2, 3, 0)])
+def test_gather_mixed_full_and_compact(n_imgs):
+    world = len(n_imgs)
+    mp.spawn(_worker, args=(world, _free_port(), n_imgs, 'mixed'), nprocs=world, join=True)
 
 
 def _free_port():

@@ -962,15 +962,46 @@ def test_compact_refetch_flag():
     dt = packed_dtype(17, 19, PACK_ALL)
     out = torch.zeros(int(off[-1]) * dt.itemsize, dtype=torch.uint8, device='cuda')
     cnt = torch.zeros(b.n, dtype=torch.int32, device='cuda')
+    flg = torch.full((b.n,), -1, dtype=torch.int32, device='cuda')
     call('pp_pack_compact', _device.ptr(b.anns), _device.ptr(b.counts), b.n, b.cap, 17, 19,
          ctypes.c_uint32(PACK_ALL), _device.ptr(out), int(off[-1]), _device.ptr(cnt),
-         _device.stream())
+         _device.ptr(flg), _device.stream())
     got = out.cpu().numpy().view(dt)
     flagged = (got['n_decoding'] & PP_PACK_REFETCH) != 0
     assert flagged[:2].all() and not flagged[2:].any()
+    # per-image flags: image 0 holds the two tampered records
+    assert flg.cpu().tolist() == [1] + [0] * (b.n - 1)
     recs, _ = eng.fetch_async(b, (17, 19, PACK_ALL)).result()
     assert recs.dtype == ANN_DTYPE and recs.tobytes() == b''.join(
         [tampered.tobytes(), full[2:].tobytes()])
+
+
+def test_expand_compact_matches_full_records():
+    """distributed.expand_compact (rank 0's merge when another rank sent full records)
+    rebuilds every live field of the device's full pp_ann records from the compact ones."""
+    import torch
+    from openpifpaf_amd import constants, engine, synthetic
+    from openpifpaf_amd._abi import EVAL_CONFIG, PACK_ALL, make_config
+    from openpifpaf_amd.distributed import expand_compact
+    cfg = make_config(**EVAL_CONFIG)
+    sk = constants.COCO_PERSON_SKELETON
+    cif, caf = synthetic.batch('uniform', 3, 40, 40, first_seed=11)
+    eng = engine.DecodeEngine()
+    b = eng.launch(torch.from_numpy(cif).cuda(), torch.from_numpy(caf).cuda(), sk, cfg)
+    full, _ = eng.fetch_gather(b)
+    full = full.copy()
+    comp, _ = eng.fetch_async(b, (17, 19, PACK_ALL)).result()
+    assert len(full) > 20 and len(comp) == len(full)
+    got = expand_compact(comp, 17, 19)
+    for name in ('score', 'image', 'n_decoding', 'n_frontier'):
+        assert np.array_equal(got[name], full[name]), name
+    assert np.array_equal(got['data'][:, :17], full['data'][:, :17])
+    assert np.array_equal(got['joint_scales'][:, :17], full['joint_scales'][:, :17])
+    for g, f in zip(got, full):
+        nd, nf = int(f['n_decoding']), int(f['n_frontier'])
+        assert np.array_equal(g['decoding_pairs'][:nd], f['decoding_pairs'][:nd])
+        assert g['decoding_xyv'][:nd].tobytes() == f['decoding_xyv'][:nd].tobytes()
+        assert np.array_equal(g['frontier_pairs'][:nf], f['frontier_pairs'][:nf])
 
 
 def test_occupancy_device_grid():
