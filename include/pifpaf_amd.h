@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PP_ABI_VERSION 2
+#define PP_ABI_VERSION 3
 
 /* capacities of one annotation record (COCO person: 17 keypoints, 19 or 44 edges) */
 #define PP_MAX_KP 24
@@ -141,6 +141,11 @@ typedef struct pp_inverse_meta {
  * means unused (the reference tests them for truthiness). */
 #define PP_ROLE_CIF 1
 #define PP_ROLE_CAF 2
+/* An entry that only names the CifHr map's geometry, (H-1)*stride+1 x (W-1)*stride+1,
+ * instead of CIF head 0's (no field is read): the stage entry points then read or write a
+ * map made at another head's size (CifSeeds.fill_cif / CafScored.fill_caf at any stride,
+ * CifHr.fill_multiple into an existing map, cif_hr.py:42-57). */
+#define PP_ROLE_HRMAP 4
 typedef struct pp_scale {
     const float *cif;        /* (n_img, K, 5, H, W) when a CIF head */
     const float *caf;        /* (n_img, C, 9, H, W) when a CAF head */
@@ -236,10 +241,14 @@ int pp_decode_batch(const float *d_cif, const float *d_caf, int32_t n_img, int32
  * Multi-scale decode: the same stages over a FieldConfig of CIF and CAF heads
  * (field_config.py:7-13; the heads' scale / min-distance lists of factory.py:153-180) given
  * as n_scales pp_scale entries (see PP_ROLE_*), device arrays of each head's own size.
- * cif_pairs != 0 is the reference's 10-head hflip layout (cif_hr.py:63-68): CifHr
- * accumulates CIF heads g and g + n/2 into one map at head g's stride and min scale; the
- * reference pairs exactly when len(cif_indices) == 10.  The CifHr map has CIF head 0's
- * size: (n_img, K, H', pitch) with H' = (H_0 - 1) * stride_0 + 1.  cfg->stride is unused.
+ * cif_pairs groups the CIF heads for CifHr (fill_multiple, cif_hr.py:42-57): 0 = one group
+ * per head; 1 = the reference's 10-head hflip layout (cif_hr.py:63-68), heads g and g + n/2
+ * accumulated into one map at head g's stride and min scale (the reference pairs exactly
+ * when len(cif_indices) == 10); m >= 2 = groups of m heads, head g + i * (n / m) being
+ * member i of group g, each splat weighted v / neighbors / m.  The groups' maps are combined
+ * by np.maximum.  The CifHr map has CIF head 0's size, (n_img, K, H', pitch) with
+ * H' = (H_0 - 1) * stride_0 + 1, unless a PP_ROLE_HRMAP entry names another.  cfg->stride
+ * is unused.
  *   pp_cifhr_multi       CifHr.fill (cif_hr.py:59-73), maps combined by np.maximum
  *   pp_seeds_multi       CifSeeds.fill over every CIF head (cif_seeds.py:56-64), sorted;
  *                        seed_capacity >= K * (sum of the CIF heads' H * W)
@@ -277,6 +286,28 @@ int pp_decode_multi(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs,
                     float *d_cifhr, pp_ann *d_anns, int32_t ann_capacity, int32_t *d_counts,
                     int32_t *d_status, void *d_workspace, size_t workspace_bytes,
                     uint32_t stages, void *stream);
+
+/*
+ * CifCaf.__call__(fields, initial_annotations) (cifcaf.py:67-71, 95-98): pp_decode_multi
+ * where each image first grows its initial annotations d_initial[img * initial_capacity + i],
+ * i < d_initial_counts[img] (set A, reverse matching, from every joint with v != 0; the
+ * records' decoding / frontier orders are kept and appended to), appends them to its
+ * annotation list in that order and marks them occupied, then runs the seed loop; force-
+ * complete and NMS see them like any other annotation.  A record needs data,
+ * joint_scales, n_decoding, decoding_pairs / decoding_xyv, n_frontier and frontier_pairs;
+ * image and n_keypoints are set by the decoder.  d_initial / d_initial_counts may be NULL
+ * (then this is pp_decode_multi).  d_out_index (optional, (n_img, ann_capacity) int32):
+ * for each output record its position in the image's annotation list before NMS, so
+ * positions < d_initial_counts[img] are the initial annotations (the reference returns those
+ * objects, mutated).  Workspace as pp_decode_multi (pp_decode_multi_workspace_size).
+ * Reference interface: openpifpaf.decoder.CifCaf.__call__ (cifcaf.py:67).
+ */
+int pp_decode_initial(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs, int32_t n_img,
+                      int32_t K, int32_t C, const int32_t *skeleton, const pp_config *cfg,
+                      float *d_cifhr, pp_ann *d_anns, int32_t ann_capacity, int32_t *d_counts,
+                      int32_t *d_status, const pp_ann *d_initial, const int32_t *d_initial_counts,
+                      int32_t initial_capacity, int32_t *d_out_index, void *d_workspace,
+                      size_t workspace_bytes, uint32_t stages, void *stream);
 
 /*
  * CifDet detection decoder (decoder/generator/cifdet.py:27-52), batched:

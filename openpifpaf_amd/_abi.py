@@ -3,7 +3,7 @@ import ctypes
 
 import numpy as np
 
-PP_ABI_VERSION = 2
+PP_ABI_VERSION = 3
 PP_MAX_KP = 24
 PP_MAX_EDGES = 64
 PP_MAX_FRONTIER = 4 * PP_MAX_EDGES
@@ -135,7 +135,7 @@ class DetNms(ctypes.Structure):
                 ('iou_threshold_soft', ctypes.c_float), ('apply', ctypes.c_int32)]
 
 
-ROLE_CIF, ROLE_CAF = 1, 2
+ROLE_CIF, ROLE_CAF, ROLE_HRMAP = 1, 2, 4
 
 
 class Scale(ctypes.Structure):

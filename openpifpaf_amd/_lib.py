@@ -58,6 +58,8 @@ _SIGNATURES = {
                                               _sz),
     'pp_decode_multi': ([_vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp, _vp,
                          _vp, _sz, _u32, _vp], ctypes.c_int),
+    'pp_decode_initial': ([_vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp,
+                           _vp, _vp, _vp, _i32, _vp, _vp, _sz, _u32, _vp], ctypes.c_int),
     'pp_scalar_square_add_gauss_with_max': ([_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _f,
                                              _f, _vp], ctypes.c_int),
     'pp_scalar_square_add_gauss': ([_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _f, _vp],

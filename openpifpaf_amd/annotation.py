@@ -43,6 +43,39 @@ class Annotation:
                               for t in range(min(int(rec['n_frontier']), len(fr)))]
         return ann
 
+    def update_from_record(self, rec):
+        """Take data, joint scales and both orders from a pp_ann record: what the
+        reference's decoder does to an initial annotation in place (cifcaf.py:95-98 grows
+        it, complete_annotations and nms.Keypoints mutate it)."""
+        new = Annotation.from_record(rec, self.keypoints, self.skeleton)
+        self.data = new.data
+        self.joint_scales = new.joint_scales
+        self.decoding_order = new.decoding_order
+        self.frontier_order = new.frontier_order
+        return self
+
+    def to_record(self):
+        """This annotation as a pp_ann record (the input form of pp_decode_initial)."""
+        from ._abi import ANN_DTYPE, PP_MAX_FRONTIER, PP_MAX_KP  # pylint: disable=import-outside-toplevel
+        k = len(self.data)
+        if k > PP_MAX_KP or len(self.decoding_order) > PP_MAX_KP or \
+                len(self.frontier_order) > PP_MAX_FRONTIER:
+            raise ValueError('annotation exceeds the record bounds (PP_MAX_KP keypoints / '
+                             'decoding entries, PP_MAX_FRONTIER frontier entries)')
+        r = np.zeros((), ANN_DTYPE)
+        r['data'][:k] = self.data
+        r['joint_scales'][:k] = self.joint_scales
+        r['n_keypoints'] = k
+        r['n_decoding'] = len(self.decoding_order)
+        for t, (js, jt, xa, xb) in enumerate(self.decoding_order):
+            r['decoding_pairs'][t] = (js, jt)
+            r['decoding_xyv'][t, :3] = xa
+            r['decoding_xyv'][t, 3:] = xb
+        r['n_frontier'] = len(self.frontier_order)
+        for t, pair in enumerate(self.frontier_order):
+            r['frontier_pairs'][t] = pair
+        return r
+
     @classmethod
     def from_packed(cls, rec, keypoints, skeleton):
         """Build from one compact record (pp_pack_compact, include/pifpaf_amd.h): each

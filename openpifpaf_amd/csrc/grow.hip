@@ -131,6 +131,11 @@ struct GrowArgs {
                               // kernel, ordered after completion, resets them)
     int *need_complete;       // (n_img) bitmask of joints left unset by the seed loop in any
                               // annotation (force-complete has work iff != 0; gates the B sets)
+    // initial annotations (cifcaf.py:95-98), optional: (n_img, init_cap) records, the
+    // first init_counts[img] of an image grown and committed before its seed loop
+    const pp_ann *init;
+    const int *init_counts;
+    int init_cap;
     // outputs
     int *out_idx;             // optional (n_img, ann_cap): input index of each output record
     pp_ann *out;
@@ -1599,6 +1604,25 @@ void seed_loop_kernel(GrowArgs g) {
         }
     } else {
         __builtin_amdgcn_s_setprio(3);  // the committer is the critical path: issue first
+        // initial annotations (cifcaf.py:95-98): each is grown with set A and reverse
+        // matching from all its set joints (its decoding / frontier orders are appended to),
+        // appended and marked occupied, in order, before any seed is looked at
+        const int n_init = g.init ? min(g.init_counts[img], g.init_cap) : 0;
+        for (int i = 0; i < n_init; i++) {
+            if (n_anns >= g.ann_cap) {
+                if (lane == 0) L.status |= PP_ST_ANN_OVERFLOW;
+                break;
+            }
+            copy_ann(&L.a, &g.init[(int64_t)img * g.init_cap + i]);
+            if (lane == 0) {
+                L.a.image = img;
+                L.a.n_keypoints = K;
+            }
+            wave_sync();
+            grow<true>(g, L, img, 0, true, cstage);
+            commit(&L.a, lane < K ? L.a.data[lane][0] : 0.0f, lane < K ? L.a.data[lane][1] : 0.0f,
+                   lane < K ? L.a.data[lane][2] : 0.0f, lane < K ? L.a.joint_scales[lane] : 0.0f);
+        }
         for (;;) {
             // the next free seed (cifcaf.py:100-104): 64 occupancy tests per step
             int t = -1;
@@ -2130,8 +2154,8 @@ struct DecodeLayout {
 static DecodeLayout make_layout(int n_img, int K, int C, const Heads &h, const pp_config *cfg,
                                 int ann_cap) {
     DecodeLayout d{};
-    d.hh = (int)hr_dim(h.cH[0], h.cstride[0]);
-    d.ww = (int)hr_dim(h.cW[0], h.cstride[0]);
+    d.hh = h.hr_hh;
+    d.ww = h.hr_ww;
     d.pitch = pp_cifhr_pitch(d.ww);
     d.hw = h.caf_cells();
     d.seed_cap = (int)(K * h.cif_cells());  // every cell of every field: no seed overflow
@@ -2264,11 +2288,19 @@ static const SideStream *side_stream() {
     return per_dev[dev];
 }
 
+// optional inputs of pp_decode_initial
+struct DecodeInit {
+    const pp_ann *anns = nullptr;
+    const int32_t *counts = nullptr;
+    int32_t cap = 0;
+    int32_t *out_index = nullptr;
+};
+
 static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
                         const int32_t *skeleton, const pp_config *cfg, float *d_cifhr,
                         pp_ann *d_anns, int32_t ann_capacity, int32_t *d_counts,
                         int32_t *d_status, void *d_workspace, size_t workspace_bytes,
-                        uint32_t stages, void *stream) {
+                        uint32_t stages, void *stream, const DecodeInit &init = DecodeInit{}) {
     if (!skeleton || !cfg || !d_anns || !d_counts || !d_status || !d_workspace)
         return fail(PP_EINVAL, "pp_decode_batch: NULL argument");
     for (int m = 0; m < h.n_cif; m++)
@@ -2289,8 +2321,9 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
     if (n_img == 0) return PP_OK;
     const DecodeLayout d = make_layout(n_img, K, C, h, cfg, ann_capacity);
     if (workspace_bytes < d.total) return fail(PP_ENOMEM, "pp_decode_batch: workspace too small");
-    if ((int64_t)d.hh >= 32767 * 2 || (int64_t)d.ww >= 32767 * 2)
-        return fail(PP_ESHAPE, "pp_decode_batch: field too large");
+    if ((int64_t)d.hh >= kMaxHrSide || (int64_t)d.ww >= kMaxHrSide)
+        return fail(PP_ESHAPE, "pp_decode_batch: field too large (CifHr map of 32768 px or "
+                               "more per side)");
     char *ws = (char *)d_workspace;
     hipStream_t s = (hipStream_t)stream;
     // the caller's d_cifhr gets the dense map; otherwise the decoder keeps the block-sparse
@@ -2462,6 +2495,10 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
         g.n_work = (int *)(ws + d.off_n_work);
         g.need_complete = (int *)(ws + d.off_need);
         g.complete_next = (int *)(ws + d.off_wq);
+        g.init = init.anns;
+        g.init_counts = init.counts;
+        g.init_cap = init.cap;
+        g.out_idx = init.out_index;
         g.out = d_anns;
         g.counts = d_counts;
         g.status = d_status;
@@ -2544,6 +2581,28 @@ int pp_decode_multi(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs,
     if (rc) return rc;
     return decode_heads(h, n_img, K, C, skeleton, cfg, d_cifhr, d_anns, ann_capacity, d_counts,
                         d_status, d_workspace, workspace_bytes, stages, stream);
+}
+
+int pp_decode_initial(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs, int32_t n_img,
+                      int32_t K, int32_t C, const int32_t *skeleton, const pp_config *cfg,
+                      float *d_cifhr, pp_ann *d_anns, int32_t ann_capacity, int32_t *d_counts,
+                      int32_t *d_status, const pp_ann *d_initial, const int32_t *d_initial_counts,
+                      int32_t initial_capacity, int32_t *d_out_index, void *d_workspace,
+                      size_t workspace_bytes, uint32_t stages, void *stream) {
+    Heads h;
+    const int rc = make_heads(scales, n_scales, cif_pairs, 3, &h, "pp_decode_initial");
+    if (rc) return rc;
+    if ((d_initial == nullptr) != (d_initial_counts == nullptr))
+        return fail(PP_EINVAL, "pp_decode_initial: d_initial and d_initial_counts go together");
+    if (d_initial && initial_capacity <= 0)
+        return fail(PP_ESHAPE, "pp_decode_initial: bad initial_capacity");
+    DecodeInit init;
+    init.anns = d_initial;
+    init.counts = d_initial_counts;
+    init.cap = d_initial ? initial_capacity : 0;
+    init.out_index = d_out_index;
+    return decode_heads(h, n_img, K, C, skeleton, cfg, d_cifhr, d_anns, ann_capacity, d_counts,
+                        d_status, d_workspace, workspace_bytes, stages, stream, init);
 }
 
 // ---- standalone nms.Keypoints.annotations (nms.py:17-57) over caller records ----------

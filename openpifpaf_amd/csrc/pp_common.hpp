@@ -24,6 +24,9 @@ int fail(int status, const std::string &msg);
 int check_launch(const char *what);
 
 inline int64_t hr_dim(int64_t n, int stride) { return (n - 1) * stride + 1; }
+// CifHr maps must stay below this many pixels per side: the fold packs a pixel's (x, y)
+// into two signed 16-bit halves for its box test
+constexpr int kMaxHrSide = 32768;
 
 // -------------------------------------------------------------------------------------
 // device helpers
@@ -184,8 +187,12 @@ struct Heads {
     float ms_th[kMaxHeads];       // fl32(cif_min_scale / stride)  (p[4] > ms_th)
     uint32_t ms_on;               // heads whose min scale is set (truthy in the reference)
     int n_cif;
-    int pairs;                    // CifHr groups heads g and g + n/2 (cif_hr.py:63-68)
+    // CifHr groups (cif_hr.py:42-73 fill_multiple): gsize heads per group, member i of group
+    // g is head g + i * n_groups (gsize 2: the hflip pairs g, g + n/2; gsize n: one group)
+    int gsize;
     int n_groups;
+    // the CifHr map's size: from a PP_ROLE_HRMAP entry, else CIF head 0's (H-1)*stride+1
+    int hr_hh, hr_ww;
     // CAF heads (caf_indices order)
     const float *caf[kMaxHeads];  // (n_img, C, 9, H, W)
     int aH[kMaxHeads], aW[kMaxHeads], astride[kMaxHeads];
@@ -199,8 +206,8 @@ struct Heads {
     __host__ __device__ __forceinline__ int64_t cif_cells() const { return cif_off[n_cif]; }
     __host__ __device__ __forceinline__ int64_t caf_cells() const { return caf_off[n_caf]; }
     // CifHr group g: its members; the group uses head g's stride and min scale
-    __host__ __device__ __forceinline__ int group_size() const { return pairs ? 2 : 1; }
-    __host__ __device__ __forceinline__ int member(int g, int i) const { return i ? g + n_cif / 2 : g; }
+    __host__ __device__ __forceinline__ int group_size() const { return gsize; }
+    __host__ __device__ __forceinline__ int member(int g, int i) const { return g + i * n_groups; }
     // CAF head of a concatenated cell index (n <= 16: a short scalar scan)
     __host__ __device__ __forceinline__ int caf_head_of(int64_t idx) const {
         int m = 0;

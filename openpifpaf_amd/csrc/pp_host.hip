@@ -23,12 +23,21 @@ int make_heads(const pp_scale *sc, int n, int pairs, int need, Heads *h, const c
     if (n <= 0 || n > 2 * kMaxHeads) return fail(PP_ESHAPE, std::string(who) + ": bad scale count");
     *h = Heads{};
     int64_t coff = 0, aoff = 0;
+    int64_t geo_hh = 0, geo_ww = 0;
     for (int i = 0; i < n; i++) {
         const pp_scale &s = sc[i];
         const int role = s.role ? s.role : (PP_ROLE_CIF | PP_ROLE_CAF);
-        if (role & ~(PP_ROLE_CIF | PP_ROLE_CAF)) return fail(PP_EINVAL, std::string(who) + ": bad role");
+        if (role & ~(PP_ROLE_CIF | PP_ROLE_CAF | PP_ROLE_HRMAP) ||
+            ((role & PP_ROLE_HRMAP) && role != PP_ROLE_HRMAP))
+            return fail(PP_EINVAL, std::string(who) + ": bad role");
         if (s.H <= 0 || s.W <= 0 || s.stride <= 0)
             return fail(PP_ESHAPE, std::string(who) + ": bad head shape / stride");
+        if (role == PP_ROLE_HRMAP) {  // geometry only: no field is read
+            if (geo_hh) return fail(PP_EINVAL, std::string(who) + ": two PP_ROLE_HRMAP entries");
+            geo_hh = hr_dim(s.H, s.stride);
+            geo_ww = hr_dim(s.W, s.stride);
+            continue;
+        }
         // `if min_scale:` / `if min_distance:` / `if max_distance:` (truthiness); the
         // thresholds are Python float / int divisions rounded to the f32 comparand
         if (role & PP_ROLE_CIF) {
@@ -62,10 +71,23 @@ int make_heads(const pp_scale *sc, int n, int pairs, int need, Heads *h, const c
     h->caf_off[h->n_caf] = aoff;
     if ((need & PP_ROLE_CIF) && h->n_cif == 0) return fail(PP_EINVAL, std::string(who) + ": no CIF head");
     if ((need & PP_ROLE_CAF) && h->n_caf == 0) return fail(PP_EINVAL, std::string(who) + ": no CAF head");
-    if (pairs && (h->n_cif & 1))
-        return fail(PP_ESHAPE, std::string(who) + ": paired CIF heads need an even count");
-    h->pairs = pairs ? 1 : 0;
-    h->n_groups = pairs ? h->n_cif / 2 : h->n_cif;
+    // cif_pairs: 0 = one CifHr group per head, 1 = hflip pairs (2 heads per group),
+    // n >= 2 = n heads per group
+    const int gsize = pairs <= 0 ? 1 : (pairs == 1 ? 2 : pairs);
+    if (h->n_cif % gsize)
+        return fail(PP_ESHAPE, std::string(who) + ": CIF head count is not a multiple of the "
+                                                  "CifHr group size");
+    h->gsize = gsize;
+    h->n_groups = h->n_cif / gsize;
+    if (geo_hh) {
+        h->hr_hh = (int)geo_hh;
+        h->hr_ww = (int)geo_ww;
+    } else if (h->n_cif) {
+        h->hr_hh = (int)hr_dim(h->cH[0], h->cstride[0]);
+        h->hr_ww = (int)hr_dim(h->cW[0], h->cstride[0]);
+    }
+    if (geo_hh > INT32_MAX / 2 || geo_ww > INT32_MAX / 2)
+        return fail(PP_ESHAPE, std::string(who) + ": CifHr map too large");
     if (coff * PP_MAX_KP > INT32_MAX || aoff > INT32_MAX)
         return fail(PP_ESHAPE, std::string(who) + ": too many cells");
     return PP_OK;

@@ -1184,7 +1184,9 @@ int cifhr_heads_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config
     if (n_img == 0) return PP_OK;
     if (workspace_bytes < cifhr_heads_workspace_size(h, n_img, K))
         return fail(PP_ENOMEM, std::string(who) + ": workspace too small");
-    const int hh = (int)hr_dim(h.cH[0], h.cstride[0]), ww = (int)hr_dim(h.cW[0], h.cstride[0]);
+    const int hh = h.hr_hh, ww = h.hr_ww;
+    if (hh >= kMaxHrSide || ww >= kMaxHrSide)  // fold candidates pack pixel (x, y) as int16
+        return fail(PP_ESHAPE, std::string(who) + ": CifHr map of 32768 px or more per side");
     const int64_t pitch = pp_cifhr_pitch(ww);
     const int64_t nf = (int64_t)n_img * K;
     HrSplatArgs sa{};
@@ -1264,7 +1266,9 @@ int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_confi
     if (n_img == 0) return PP_OK;
     if (workspace_bytes < cifhr_sparse_workspace_size(h, n_img, K))
         return fail(PP_ENOMEM, std::string(who) + ": workspace too small");
-    const int hh = (int)hr_dim(h.cH[0], h.cstride[0]), ww = (int)hr_dim(h.cW[0], h.cstride[0]);
+    const int hh = h.hr_hh, ww = h.hr_ww;
+    if (hh >= kMaxHrSide || ww >= kMaxHrSide)  // fold candidates pack pixel (x, y) as int16
+        return fail(PP_ESHAPE, std::string(who) + ": CifHr map of 32768 px or more per side");
     const HrMap geo = dense_hr(nullptr, hh, ww);
     if (geo.tiles > kTileBits) return fail(PP_ESHAPE, std::string(who) + ": CifHr map too large");
     if (h.n_groups > 8) return fail(PP_ESHAPE, std::string(who) + ": too many CifHr groups");

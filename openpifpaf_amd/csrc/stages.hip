@@ -993,8 +993,7 @@ static int seeds_entry(const Heads &h, const float *d_cifhr, int32_t n_img, int3
     hipStream_t s = (hipStream_t)stream;
     if (hipMallocAsync(&scratch, seeds_scratch_size(n_img, seed_capacity), s) != hipSuccess)
         return fail(PP_EHIP, "pp_seeds: scratch allocation failed");
-    const HrMap hr = dense_hr(d_cifhr, (int)hr_dim(h.cH[0], h.cstride[0]),
-                              (int)hr_dim(h.cW[0], h.cstride[0]));
+    const HrMap hr = dense_hr(d_cifhr, h.hr_hh, h.hr_ww);
     int rc = launch_seeds(h, hr, n_img, K, cfg, d_seeds, seed_capacity, d_counts, scratch, s);
     if (hipFreeAsync(scratch, s) != hipSuccess && rc == PP_OK)
         rc = fail(PP_EHIP, "pp_seeds: scratch release failed");
@@ -1042,9 +1041,11 @@ int pp_caf_scored_multi(const pp_scale *scales, int32_t n_scales, const float *d
                         float score_th, const pp_config *cfg, float *d_cols,
                         int64_t col_capacity, int32_t *d_counts, void *stream) {
     Heads h;
-    // the CIF heads give the CifHr map's geometry (CIF head 0); their fields are not read
-    const int rc = make_heads(scales, n_scales, 0, PP_ROLE_CIF | PP_ROLE_CAF, &h, "pp_caf_scored_multi");
+    // CIF head 0 (or a PP_ROLE_HRMAP entry) gives the CifHr map's geometry; CIF fields are
+    // not read
+    const int rc = make_heads(scales, n_scales, 0, PP_ROLE_CAF, &h, "pp_caf_scored_multi");
     if (rc) return rc;
+    if (h.hr_hh <= 0) return fail(PP_EINVAL, "pp_caf_scored_multi: no CIF head or PP_ROLE_HRMAP entry");
     if (!d_cifhr || !skeleton || !cfg || !d_cols || !d_counts)
         return fail(PP_EINVAL, "pp_caf_scored_multi: NULL argument");
     for (int m = 0; m < h.n_caf; m++)
@@ -1054,8 +1055,7 @@ int pp_caf_scored_multi(const pp_scale *scales, int32_t n_scales, const float *d
     float *cols[1] = {d_cols};
     int *counts[1] = {d_counts};
     return launch_caf_scored(h,
-                             dense_hr(d_cifhr, (int)hr_dim(h.cH[0], h.cstride[0]),
-                                      (int)hr_dim(h.cW[0], h.cstride[0])),
+                             dense_hr(d_cifhr, h.hr_hh, h.hr_ww),
                              n_img, K, C, skeleton, cfg, 1, &score_th, cols, col_capacity, counts,
                              (hipStream_t)stream, nullptr);
 }

@@ -55,3 +55,16 @@ def head_scales(fields, config, role):
                      config.cif_strides, config.caf_strides, None, config.caf_min_distances,
                      config.caf_max_distances)
     return arr, ts
+
+
+def geometry_entry(hr_shape):
+    """pp_scale entry (PP_ROLE_HRMAP) naming a CifHr map of hr_shape[-2:] = (hh, ww): the
+    stage entry points then read / write a map made at another head's size."""
+    from .._abi import ROLE_HRMAP, Scale  # pylint: disable=import-outside-toplevel
+    return Scale(None, None, int(hr_shape[-2]), int(hr_shape[-1]), 1, 0.0, 0.0, 0.0, ROLE_HRMAP)
+
+
+def with_geometry(arr, hr_shape):
+    """A pp_scale array followed by the geometry entry of hr_shape."""
+    from .._abi import Scale  # pylint: disable=import-outside-toplevel
+    return (Scale * (len(arr) + 1))(*arr, geometry_entry(hr_shape))

@@ -6,9 +6,9 @@ import numpy as np
 import torch
 
 from .. import _device
-from .._abi import make_config, skeleton_array
+from .._abi import make_config, scale_list, skeleton_array
 from .._lib import call
-from ._fields import batch1, head_scales, pitched_hr
+from ._fields import batch1, head_scales, pitched_hr, with_geometry
 from .field_config import FieldConfig
 
 
@@ -30,31 +30,40 @@ class CafScored:
         return self.backward[caf_i], self.forward[caf_i]
 
     def fill_caf(self, caf, stride, min_distance=0.0, max_distance=None):
-        if min_distance or max_distance:
-            raise NotImplementedError('CAF distance masks (multi-scale) are not implemented')
-        if self.forward is not None:
-            raise NotImplementedError('several CAF heads (multi-scale) are not implemented')
+        """caf_scored.py:32-86 for one head at `stride` with its distance masks; the
+        columns are appended to those of earlier calls (np.concatenate per field)."""
         c = batch1(caf)
         _, n_caf, _, h, w = c.shape
+        arr = scale_list([], [(c.data_ptr(), h, w)], [], [int(stride)], None, [min_distance],
+                         [max_distance])
+        return self._run(with_geometry(arr, self.cifhr.shape), n_caf, h * w, c.device,
+                         not _device.is_device(caf))
+
+    def _run(self, arr, n_caf, cap, device, host):
         hr = pitched_hr(self.cifhr)
         k = hr.shape[1]
         skel = skeleton_array(self.skeleton)[:n_caf]
-        cols = torch.empty((1, n_caf, 2, 9, h * w), dtype=torch.float32, device=c.device)
-        counts = torch.zeros((1, n_caf, 2), dtype=torch.int32, device=c.device)
-        cfg = make_config(cif_floor=self.cif_floor, stride=int(stride))
-        call('pp_caf_scored', _device.ptr(c), _device.ptr(hr), 1, k, n_caf, h, w,
+        cols = torch.empty((1, n_caf, 2, 9, max(1, cap)), dtype=torch.float32, device=device)
+        counts = torch.zeros((1, n_caf, 2), dtype=torch.int32, device=device)
+        cfg = make_config(cif_floor=self.cif_floor)
+        call('pp_caf_scored_multi', arr, len(arr), _device.ptr(hr), 1, k, n_caf,
              skel.ctypes.data_as(ctypes.c_void_p), ctypes.c_float(self.score_th),
-             ctypes.byref(cfg), _device.ptr(cols), _device.ptr(counts), _device.stream())
-        return self._set_columns(cols, counts, n_caf, not _device.is_device(caf))
-
-    def _set_columns(self, cols, counts, n_caf, host):
+             ctypes.byref(cfg), _device.ptr(cols), ctypes.c_int64(max(1, cap)),
+             _device.ptr(counts), _device.stream())
         cnt = counts.cpu().numpy()[0]
         data = cols.cpu().numpy()[0] if host else cols[0]
-        self.forward = [data[i, 1, :, :cnt[i, 1]] for i in range(n_caf)]
-        self.backward = [data[i, 0, :, :cnt[i, 0]] for i in range(n_caf)]
+        fwd = [data[i, 1, :, :cnt[i, 1]] for i in range(n_caf)]
+        bwd = [data[i, 0, :, :cnt[i, 0]] for i in range(n_caf)]
         if host:
-            self.forward = [np.ascontiguousarray(a) for a in self.forward]
-            self.backward = [np.ascontiguousarray(a) for a in self.backward]
+            fwd = [np.ascontiguousarray(a) for a in fwd]
+            bwd = [np.ascontiguousarray(a) for a in bwd]
+        if self.forward is None:
+            self.forward, self.backward = fwd, bwd
+        else:
+            cat = (lambda a, b: np.concatenate((a, np.asarray(b)), axis=1)) if host else \
+                (lambda a, b: torch.cat((_device.to_device(a), b), dim=1))
+            self.forward = [cat(a, b) for a, b in zip(self.forward, fwd)]
+            self.backward = [cat(a, b) for a, b in zip(self.backward, bwd)]
         return self
 
     def fill(self, fields):
@@ -62,20 +71,8 @@ class CafScored:
         if self.config.is_single_scale():
             _, caf_i, stride = self.config.single_scale()
             return self.fill_caf(fields[caf_i], stride)
-        if self.forward is not None:
-            raise NotImplementedError('several fill() calls are not implemented')
         arr, ts = head_scales(fields, self.config, 'caf')
-        n_caf = ts[0].shape[1]
         cap = sum(t.shape[3] * t.shape[4] for t in ts)
-        hr = pitched_hr(self.cifhr)
-        k = hr.shape[1]
-        skel = skeleton_array(self.skeleton)[:n_caf]
-        cols = torch.empty((1, n_caf, 2, 9, cap), dtype=torch.float32, device=ts[0].device)
-        counts = torch.zeros((1, n_caf, 2), dtype=torch.int32, device=ts[0].device)
-        cfg = make_config(cif_floor=self.cif_floor)
-        call('pp_caf_scored_multi', arr, len(arr), _device.ptr(hr), 1, k, n_caf,
-             skel.ctypes.data_as(ctypes.c_void_p), ctypes.c_float(self.score_th),
-             ctypes.byref(cfg), _device.ptr(cols), ctypes.c_int64(cap), _device.ptr(counts),
-             _device.stream())
         host = not any(_device.is_device(fields[i]) for i in self.config.caf_indices)
-        return self._set_columns(cols, counts, n_caf, host)
+        return self._run(with_geometry(arr, self.cifhr.shape), ts[0].shape[1], cap,
+                         ts[0].device, host)

@@ -10,10 +10,10 @@ import numpy as np
 import torch
 
 from .. import _device
-from .._abi import make_config
+from .._abi import make_config, scale_list
 from .._lib import call, load
 from ..functional import scalar_square_add_gauss_with_max
-from ._fields import batch1, head_scales, hr_geometry
+from ._fields import batch1, head_scales, hr_geometry, with_geometry
 from .field_config import FieldConfig
 
 
@@ -101,52 +101,74 @@ class CifHr:
                                          truncate=1.0)
 
     def fill_cif(self, cif, stride, min_scale=0.0):
-        if min_scale:
-            raise NotImplementedError('min_scale masks (multi-scale) are not implemented')
-        if self.accumulated is not None:
-            raise NotImplementedError('accumulating several CIF heads (multi-scale) is not '
-                                      'implemented on the device decoder')
-        hr = cifhr_device(batch1(cif), int(stride), self.v_threshold, self.neighbors)
-        ww = (cif.shape[3] - 1) * int(stride) + 1
-        acc = hr[0, :, :, :ww]
-        self.accumulated = acc if _device.is_device(cif) else np.ascontiguousarray(
-            acc.cpu().numpy())
-        return self
+        return self.fill_multiple([cif], stride, min_scale)
 
     def fill_multiple(self, cifs, stride, min_scale=0.0):
-        """cif_hr.py:42-57 for the first group (1 or 2 heads at one stride)."""
-        if self.accumulated is not None:
-            raise NotImplementedError('accumulating into an existing map: use fill()')
-        if len(cifs) == 1 and not min_scale:
-            return self.fill_cif(cifs[0], stride)
-        if len(cifs) > 2:
-            raise NotImplementedError('fill_multiple over more than two heads')
-        n = len(cifs)
-        fc = FieldConfig(cif_indices=list(range(n)), cif_strides=[stride] * n,
-                         cif_min_scales=[min_scale] * n)
-        return self._fill_heads(cifs, fc, pairs=int(n == 2))
+        """cif_hr.py:42-57: the heads accumulated into one zero map with len_cifs =
+        len(cifs) (pp_cifhr_multi, one group of len(cifs) heads), at the size of the
+        existing map if there is one (else from cifs[0] and stride), then combined with it
+        by np.maximum."""
+        ts = [batch1(c) for c in cifs]
+        k, h, w = ts[0].shape[1], ts[0].shape[3], ts[0].shape[4]
+        if self.accumulated is None:
+            hh, ww, _ = hr_geometry(h, w, int(stride))
+        else:
+            if self.accumulated.shape[0] != k:
+                raise ValueError('CIF heads with {} fields into a map of {}'.format(
+                    k, self.accumulated.shape[0]))
+            hh, ww = self.accumulated.shape[1:]
+        n = len(ts)
+        arr = scale_list([(t.data_ptr(), t.shape[3], t.shape[4]) for t in ts], [],
+                         [int(stride)] * n, [], [min_scale] * n)
+        arr = with_geometry(arr, (hh, ww))
+        groups = n if n > 1 else 0  # one group of all n heads
+        ta = self._run_multi(arr, groups, k, hh, ww, ts[0].device)
+        device = any(_device.is_device(c) for c in cifs) or _device.is_device(self.accumulated)
+        if self.accumulated is None:
+            self.accumulated = ta if device else np.ascontiguousarray(ta.cpu().numpy())
+        elif device:
+            self.accumulated = torch.maximum(ta, _device.to_device(self.accumulated))
+        else:  # np.maximum(ta, accumulated): NaN propagates, as torch.maximum does
+            self.accumulated = np.maximum(ta.cpu().numpy(), self.accumulated)
+        return self
+
+    def _run_multi(self, arr, groups, k, hh, ww, device):
+        """pp_cifhr_multi -> the (K, hh, ww) device view of its pitched output."""
+        lib = load()
+        pitch = int(lib.pp_cifhr_pitch(ww))
+        out = torch.empty((1, k, hh, pitch), dtype=torch.float32, device=device)
+        ws = torch.empty(max(1, int(lib.pp_cifhr_multi_workspace_size(arr, len(arr), groups, 1,
+                                                                      k))),
+                         dtype=torch.uint8, device=device)
+        cfg = make_config(cif_threshold=self.v_threshold, cif_neighbors=self.neighbors)
+        call('pp_cifhr_multi', arr, len(arr), groups, 1, k, ctypes.byref(cfg), _device.ptr(out),
+             _device.ptr(ws), ctypes.c_size_t(ws.numel()), _device.stream())
+        return out[0, :, :, :ww]
 
     def fill(self, fields):
-        """cif_hr.py:59-73: every CIF head of the FieldConfig, pairs when there are 10."""
+        """cif_hr.py:59-73: every CIF head of the FieldConfig, pairs when there are 10 (one
+        pp_cifhr_multi call; the groups' maps are combined by np.maximum on the device)."""
         if self.config.is_single_scale():
             cif_i, _, stride = self.config.single_scale()
             return self.fill_cif(fields[cif_i], stride)
-        return self._fill_heads(fields, self.config, pairs=int(len(self.config.cif_indices) == 10))
-
-    def _fill_heads(self, fields, config, pairs):
-        arr, ts = head_scales(fields, config, 'cif')
+        if self.accumulated is not None:  # into an existing map: head group by head group
+            if len(self.config.cif_indices) == 10:
+                for i1, i2, stride, ms in zip(self.config.cif_indices[:5],
+                                              self.config.cif_indices[5:],
+                                              self.config.cif_strides[:5],
+                                              self.config.cif_min_scales[:5]):
+                    self.fill_multiple([fields[i1], fields[i2]], stride, min_scale=ms)
+            else:
+                for i, stride, ms in zip(self.config.cif_indices, self.config.cif_strides,
+                                         self.config.cif_min_scales):
+                    self.fill_cif(fields[i], stride, min_scale=ms)
+            return self
+        arr, ts = head_scales(fields, self.config, 'cif')
         _, k, _, h, w = ts[0].shape
-        stride = int(config.cif_strides[0])
-        hh, ww, pitch = hr_geometry(h, w, stride)
-        lib = load()
-        out = torch.empty((1, k, hh, pitch), dtype=torch.float32, device=ts[0].device)
-        ws = torch.empty(int(lib.pp_cifhr_multi_workspace_size(arr, len(arr), pairs, 1, k)),
-                         dtype=torch.uint8, device=ts[0].device)
-        cfg = make_config(cif_threshold=self.v_threshold, cif_neighbors=self.neighbors)
-        call('pp_cifhr_multi', arr, len(arr), pairs, 1, k, ctypes.byref(cfg), _device.ptr(out),
-             _device.ptr(ws), ctypes.c_size_t(ws.numel()), _device.stream())
-        acc = out[0, :, :, :ww]
-        host = not any(_device.is_device(fields[i]) for i in config.cif_indices)
+        hh, ww, _ = hr_geometry(h, w, int(self.config.cif_strides[0]))
+        acc = self._run_multi(arr, int(len(self.config.cif_indices) == 10), k, hh, ww,
+                              ts[0].device)
+        host = not any(_device.is_device(fields[i]) for i in self.config.cif_indices)
         self.accumulated = np.ascontiguousarray(acc.cpu().numpy()) if host else acc
         return self
 
@@ -176,4 +198,16 @@ class CifDetHr(CifHr):
         acc = hr[0, :, :, :ww]
         self.accumulated = acc if _device.is_device(cif) else np.ascontiguousarray(
             acc.cpu().numpy())
+        return self
+
+    def fill_multiple(self, cifs, stride, min_scale=0.0):
+        """One detection head (the reference's CifDet decodes a single head, cifdet.py:39)."""
+        if len(cifs) != 1:
+            raise NotImplementedError('several CifDet heads are not implemented')
+        return self.fill_cif(cifs[0], stride, min_scale)
+
+    def fill(self, fields):
+        for cif_i, stride, min_scale in zip(self.config.cif_indices, self.config.cif_strides,
+                                            self.config.cif_min_scales):
+            self.fill_cif(fields[cif_i], stride, min_scale=min_scale)
         return self

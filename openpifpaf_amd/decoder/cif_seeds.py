@@ -4,9 +4,9 @@ import numpy as np
 import torch
 
 from .. import _device
-from .._abi import SEED_DTYPE, make_config
+from .._abi import SEED_DTYPE, make_config, scale_list
 from .._lib import call
-from ._fields import batch1, cfg_ptr, head_scales, pitched_hr
+from ._fields import batch1, cfg_ptr, head_scales, pitched_hr, with_geometry
 from .field_config import FieldConfig
 
 
@@ -20,27 +20,38 @@ class CifSeeds:
         self.seeds = []
 
     def fill_cif(self, cif, stride, *, min_scale=0.0, seed_mask=None):
+        """cif_seeds.py:23-50 for one head at `stride` (any stride: CifHr lookups go through
+        the map's own geometry), appended to the seeds of earlier calls."""
+        self._check_threshold()
+        c = batch1(cif)
+        _, k, _, h, w = c.shape
+        arr = scale_list([(c.data_ptr(), h, w)], [], [int(stride)], [], [min_scale])
+        self._run(with_geometry(arr, self.cifhr.shape), k, k * h * w, c.device, seed_mask)
+        return self
+
+    def _check_threshold(self):
         if self.threshold is None:
             raise TypeError("'>' not supported between instances of 'numpy.ndarray' and "
                             "'NoneType' (CifSeeds.threshold is not configured)")
-        if min_scale or seed_mask is not None:
-            raise NotImplementedError('min_scale / seed_mask are not implemented')
-        c = batch1(cif)
-        _, k, _, h, w = c.shape
+
+    def _run(self, arr, k, cap, device, seed_mask):
+        """pp_seeds_multi over the CIF entries of `arr`; the seeds of fields whose
+        seed_mask entry is falsy are dropped (cif_seeds.py:28-29; the kernel's order is
+        the sorted order, which dropping entries keeps)."""
         hr = pitched_hr(self.cifhr)
-        cap = k * h * w
-        out = torch.empty(cap * SEED_DTYPE.itemsize, dtype=torch.uint8, device=c.device)
-        count = torch.zeros(1, dtype=torch.int32, device=c.device)
-        cfg = make_config(seed_threshold=self.threshold, seed_score_scale=self.score_scale,
-                          stride=int(stride))
-        call('pp_seeds', _device.ptr(c), _device.ptr(hr), 1, k, h, w, cfg_ptr(cfg),
-             _device.ptr(out), cap, _device.ptr(count), _device.stream())
+        out = torch.empty(max(1, cap) * SEED_DTYPE.itemsize, dtype=torch.uint8, device=device)
+        count = torch.zeros(1, dtype=torch.int32, device=device)
+        cfg = make_config(seed_threshold=self.threshold, seed_score_scale=self.score_scale)
+        call('pp_seeds_multi', arr, len(arr), _device.ptr(hr), 1, k, cfg_ptr(cfg),
+             _device.ptr(out), max(1, cap), _device.ptr(count), _device.stream())
         n = int(count.item())
         recs = np.frombuffer(out[:n * SEED_DTYPE.itemsize].cpu().numpy().tobytes(),
                              dtype=SEED_DTYPE)
+        if seed_mask is not None:
+            keep = np.array([bool(m) for m in seed_mask] + [False] * k)[:k]
+            recs = recs[keep[recs['field']]]
         self.seeds.extend((v, int(f), x, y, s) for v, f, x, y, s in
                           zip(recs['v'], recs['field'], recs['x'], recs['y'], recs['s']))
-        return self
 
     def get(self):
         """cif_seeds.py:52-54 (the kernel already emits this order)."""
@@ -48,28 +59,15 @@ class CifSeeds:
 
     def fill(self, fields):
         """cif_seeds.py:56-64: every CIF head of the FieldConfig, in order."""
+        self._check_threshold()
         if self.config.is_single_scale():
             cif_i, _, stride = self.config.single_scale()
             return self.fill_cif(fields[cif_i], stride, seed_mask=self.config.seed_mask)
-        if self.threshold is None:
-            raise TypeError("'>' not supported between instances of 'numpy.ndarray' and "
-                            "'NoneType' (CifSeeds.threshold is not configured)")
-        if self.config.seed_mask is not None:
-            raise NotImplementedError('seed_mask is not implemented')
         arr, ts = head_scales(fields, self.config, 'cif')
         k = ts[0].shape[1]
         cap = k * sum(t.shape[3] * t.shape[4] for t in ts)
-        hr = pitched_hr(self.cifhr)
-        out = torch.empty(cap * SEED_DTYPE.itemsize, dtype=torch.uint8, device=ts[0].device)
-        count = torch.zeros(1, dtype=torch.int32, device=ts[0].device)
-        cfg = make_config(seed_threshold=self.threshold, seed_score_scale=self.score_scale)
-        call('pp_seeds_multi', arr, len(arr), _device.ptr(hr), 1, k, cfg_ptr(cfg),
-             _device.ptr(out), cap, _device.ptr(count), _device.stream())
-        n = int(count.item())
-        recs = np.frombuffer(out[:n * SEED_DTYPE.itemsize].cpu().numpy().tobytes(),
-                             dtype=SEED_DTYPE)
-        self.seeds.extend((v, int(f), x, y, s) for v, f, x, y, s in
-                          zip(recs['v'], recs['field'], recs['x'], recs['y'], recs['s']))
+        self._run(with_geometry(arr, self.cifhr.shape), k, cap, ts[0].device,
+                  self.config.seed_mask)
         return self
 
 

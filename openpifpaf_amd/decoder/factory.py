@@ -93,6 +93,10 @@ def factory_from_args(args, model):
         decode.fields_batch = ProfilerAutograd(decode.fields_batch,
                                                device=getattr(args, 'device', 'cuda'),
                                                out_name=args.profile_decoder)
+        # batch() runs the network through _heads (batch-major, no per-image split)
+        decode._heads = ProfilerAutograd(decode._heads,  # pylint: disable=protected-access
+                                         device=getattr(args, 'device', 'cuda'),
+                                         out_name=args.profile_decoder)
     return decode
 
 

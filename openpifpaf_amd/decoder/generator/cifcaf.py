@@ -16,7 +16,7 @@ import numpy as np
 from ... import _device
 from ..._abi import PACK_ALL, make_config, skeleton_array
 from ...annotation import Annotation
-from ...engine import HeadSet, engine
+from ...engine import HeadSet, InitialAnnotations, engine
 from ...functional import grow_connection_blend
 from .. import nms as nms_module
 from ..caf_scored import CafScored
@@ -95,9 +95,11 @@ class CifCaf(Generator):
     def __call__(self, fields, initial_annotations=None):
         """One image: fields = the head outputs [cif (K, 5, H, W), caf (C, 9, H, W), ...]
         (numpy or device), read through the FieldConfig (single- or multi-scale)."""
-        if initial_annotations:
-            raise NotImplementedError('initial_annotations are not implemented on the device')
         start = time.perf_counter()
+        if initial_annotations:
+            anns = self._call_initial(fields, list(initial_annotations))
+            LOG.debug('%d annotations, %.3fs', len(anns), time.perf_counter() - start)
+            return anns
         if self.field_config.is_single_scale():
             cif_i, caf_i, _ = self.field_config.single_scale()
             anns = self.decode_batch(_device.to_device(fields[cif_i])[None],
@@ -109,6 +111,35 @@ class CifCaf(Generator):
             anns = self.decode_fields_batch(batched)[0]
         LOG.debug('%d annotations, %.3fs', len(anns), time.perf_counter() - start)
         return anns
+
+    def _call_initial(self, fields, initial):
+        """cifcaf.py:67-71, 95-98: the initial annotations are grown first, marked occupied
+        and kept in the annotation list (pp_decode_initial).  As in the reference, the
+        returned list holds the same initial Annotation objects, mutated (grown, completed,
+        NMS-suppressed); one that NMS drops keeps its input state here."""
+        init = InitialAnnotations([np.stack([a.to_record() for a in initial])],
+                                  _device.require())
+        skel = skeleton_array(self.skeleton)
+        if self.field_config.is_single_scale():
+            cif_i, caf_i, _ = self.field_config.single_scale()
+            recs, offsets, b = engine().decode(_device.to_device(fields[cif_i])[None],
+                                               _device.to_device(fields[caf_i])[None], skel,
+                                               self.config(), initial=init)
+        else:
+            used = set(self.field_config.cif_indices) | set(self.field_config.caf_indices)
+            heads = HeadSet([_device.to_device(f)[None] if i in used else None
+                             for i, f in enumerate(fields)], self.field_config)
+            recs, offsets, b = engine().decode(None, None, skel, self.config(), heads=heads,
+                                               initial=init)
+        n = int(offsets[1])
+        index = b.out_index[:n].cpu().numpy()
+        out = []
+        for rec, idx in zip(recs[:n], index):
+            if 0 <= idx < len(initial):
+                out.append(initial[idx].update_from_record(rec))
+            else:
+                out.append(Annotation.from_record(rec, self.keypoints, self.out_skeleton))
+        return out
 
     def decode_records(self, cif_batch, caf_batch, keep_cifhr=False, compact=None):
         """Device decode of a batch -> (packed records, per-image offsets, buffers): full

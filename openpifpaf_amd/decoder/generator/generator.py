@@ -13,6 +13,24 @@ import torch
 LOG = logging.getLogger(__name__)
 
 
+def _apply(f, items):
+    """generator.py:48-54: f on every item that is not a list or tuple, nested."""
+    if items is None:
+        return None
+    if isinstance(items, (list, tuple)):
+        return [_apply(f, i) for i in items]
+    return f(items)
+
+
+def per_image(heads):
+    """Batch-major head outputs -> one nested head list per image (generator.py:66-74:
+    the reference zips iterators over the batch dimension until the first runs out)."""
+    lens = []
+    _apply(lambda t: lens.append(len(t)), heads)
+    n = min(lens) if lens else 0
+    return [_apply(lambda t, i=i: t[i], heads) for i in range(n)]
+
+
 class DummyPool():
     @staticmethod
     def starmap(f, iterable):
@@ -29,8 +47,8 @@ class Generator:
         return {k: v for k, v in self.__dict__.items() if k not in ('worker_pool',)}
 
     @staticmethod
-    def fields_batch(model, image_batch, *, device=None):
-        """Network forward; the head outputs stay on the device (no .cpu().numpy())."""
+    def _heads(model, image_batch, *, device=None):
+        """Network forward: the model's head outputs, batch-major tensors on the device."""
         start = time.time()
         with torch.no_grad():
             if device is not None:
@@ -39,6 +57,15 @@ class Generator:
                 heads = model(image_batch)
         LOG.debug('nn processing time: %.3fs', time.time() - start)
         return heads
+
+    @staticmethod
+    def fields_batch(model, image_batch, *, device=None):
+        """From image batch to field batch (generator.py:43-78): one entry per image, each
+        the model's (nested) head list indexed by that image, as the reference returns it.
+        The per-image fields are views of the device outputs (the reference's
+        `.cpu().numpy()` copy is skipped)."""
+        heads = Generator._heads(model, image_batch, device=device)
+        return per_image(heads)
 
     def __call__(self, fields, *, initial_annotations=None):
         raise NotImplementedError()
@@ -53,7 +80,7 @@ class Generator:
         list of any FieldConfig (single-scale, dense connections, multi-scale) is decoded
         as one device batch instead of per image over a worker pool."""
         start_nn = time.perf_counter()
-        heads = self.fields_batch(model, image_batch, device=device)
+        heads = self._heads(model, image_batch, device=device)
         self.last_nn_time = time.perf_counter() - start_nn
         start = time.perf_counter()
         result = self.decode_heads(heads)

@@ -33,7 +33,9 @@ class Occupancy():
         return len(self.occupancy)
 
     def mark(self, fields, xs, ys, sigmas):
-        """Occupancy.set for every (f, x, y, sigma), in order, in one device launch."""
+        """Occupancy.set for every (f, x, y, sigma), in order, in one device launch: x, y and
+        sigma as float32 (the division and rounding run in f32 on the device, as the
+        reference computes them for the decoder's float32 coordinates); f in range."""
         f = torch.as_tensor(np.asarray(fields, np.int32), device=self.occupancy.device)
         pts = [torch.as_tensor(np.asarray(a, np.float32), device=self.occupancy.device)
                for a in (xs, ys, sigmas)]
@@ -43,14 +45,36 @@ class Occupancy():
              ctypes.c_float(self.reduction), ctypes.c_float(self.min_scale_reduced),
              _device.stream())
 
+    def _plane(self, f):
+        """self.occupancy[f] of the reference: negative f counts from the end."""
+        n = len(self.occupancy)
+        if not -n <= f < n:
+            raise IndexError('index {} is out of bounds for axis 0 with size {}'.format(f, n))
+        return f + n if f < 0 else f
+
     def set(self, f, x, y, sigma):
-        """Setting is centered at the rounded (x, y) (u8 += 1 on the box, wrapping)."""
+        """Setting is centered at the rounded (x, y) (u8 += 1 on the box, wrapping).  The
+        box corners are rounded here exactly as occupancy.py:36-39 does (Python round() on
+        the operands' own types: f32 for numpy float32 inputs, f64 for Python floats), then
+        marked on the device."""
         if f >= len(self.occupancy):
             return
-        self.mark([f], [x], [y], [sigma])
+        f = self._plane(f)
+        xi = round(x / self.reduction)
+        yi = round(y / self.reduction)
+        si = round(max(self.min_scale_reduced, sigma / self.reduction))
+        # the kernel's own rounding of the already integral values is the identity
+        _, h, w = self.occupancy.shape
+        fa = torch.tensor([f], dtype=torch.int32, device=self.occupancy.device)
+        pts = [torch.tensor([float(v)], dtype=torch.float32, device=self.occupancy.device)
+               for v in (xi, yi, si)]
+        call('pp_occupancy_set', _device.ptr(self.occupancy), len(self.occupancy), h, w, w,
+             _device.ptr(fa), *[_device.ptr(t) for t in pts], ctypes.c_int64(1),
+             ctypes.c_float(1.0), ctypes.c_float(0.0), _device.stream())
 
     def get(self, f, x, y):
         """Read at the floor of (x, y) / reduction, clipped to the grid."""
         if f >= len(self.occupancy):
             return 1.0
-        return scalar_nonzero_clipped_with_reduction(self.occupancy[f], x, y, self.reduction)
+        return scalar_nonzero_clipped_with_reduction(self.occupancy[self._plane(f)], x, y,
+                                                     self.reduction)

@@ -67,6 +67,7 @@ class DecodeBuffers:
         self.ww = (w - 1) * stride + 1
         self.pitch = int(lib.pp_cifhr_pitch(self.ww))
         self.cifhr = None
+        self.out_index = None  # pp_decode_initial's (n, cap) positions before NMS
 
     anns = property(lambda self: self._slots[self._cur][0])
     counts = property(lambda self: self._slots[self._cur][1])
@@ -85,6 +86,23 @@ class DecodeBuffers:
             self.cifhr = torch.empty((self.n, self.k, self.hh, self.pitch), dtype=torch.float32,
                                      device=self.ws.device)
         return self.cifhr
+
+
+class InitialAnnotations:
+    """Per-image initial annotations (CifCaf.__call__'s initial_annotations,
+    cifcaf.py:67-71) as device pp_ann records for pp_decode_initial: `records` (n, cap)
+    ANN_DTYPE rows, `counts` (n) int32.  `per_image`: one list of ANN_DTYPE record arrays
+    per image."""
+
+    def __init__(self, per_image, device):
+        self.n = len(per_image)
+        self.cap = max(1, max((len(r) for r in per_image), default=0))
+        host = np.zeros((self.n, self.cap), ANN_DTYPE)
+        for i, r in enumerate(per_image):
+            host[i, :len(r)] = r
+        self.records = torch.from_numpy(host.view(np.uint8).reshape(-1)).to(device)
+        self.counts = torch.tensor([len(r) for r in per_image], dtype=torch.int32,
+                                   device=device)
 
 
 class HeadSet:
@@ -136,8 +154,10 @@ class DecodeEngine:
             self._bufs = DecodeBuffers(key, n, k, c, h, w, cfg, cap, _device.require(), heads)
         return self._bufs
 
-    def launch(self, cif, caf, skeleton, cfg, cap=None, keep_cifhr=False, stages=STAGE_ALL):
-        """Enqueue the decode on the current stream; returns the DecodeBuffers."""
+    def launch(self, cif, caf, skeleton, cfg, cap=None, keep_cifhr=False, stages=STAGE_ALL,
+               initial=None):
+        """Enqueue the decode on the current stream; returns the DecodeBuffers.  `initial`
+        (InitialAnnotations) selects pp_decode_initial."""
         if cif.dim() != 5 or caf.dim() != 5 or cif.shape[2] != 5 or caf.shape[2] != 9:
             raise ValueError('expected cif (B, K, 5, H, W) and caf (B, C, 9, H, W)')
         n, k, _, h, w = cif.shape
@@ -152,6 +172,11 @@ class DecodeEngine:
         if stages & STAGE_GROW and not stages & STAGE_AFTER_SEED_LOOP:
             b.next_slot()
         hr = b.cifhr_buffer() if keep_cifhr else None
+        if initial is not None:
+            arr = scale_list([(cif.data_ptr(), h, w)], [(caf.data_ptr(), h, w)], [cfg.stride],
+                             [cfg.stride])
+            self._launch_initial(b, arr, 0, n, k, c, skel, cfg, hr, cap, initial, stages)
+            return b
         call('pp_decode_stages', _device.ptr(cif), _device.ptr(caf), n, k, c, h, w,
              skel.ctypes.data_as(ctypes.c_void_p), ctypes.byref(cfg), _device.ptr(hr),
              _device.ptr(b.anns), cap, _device.ptr(b.counts), _device.ptr(b.status),
@@ -159,8 +184,24 @@ class DecodeEngine:
              _device.stream())
         return b
 
-    def launch_multi(self, heads, skeleton, cfg, cap=None, keep_cifhr=False, stages=STAGE_ALL):
-        """pp_decode_multi over a HeadSet; returns the DecodeBuffers."""
+    @staticmethod
+    def _launch_initial(b, arr, pairs, n, k, c, skel, cfg, hr, cap, initial, stages):
+        if initial.n != n:
+            raise ValueError('initial annotations for {} images, batch has {}'.format(
+                initial.n, n))
+        if b.out_index is None or b.out_index.numel() < n * cap:
+            b.out_index = torch.empty(n * cap, dtype=torch.int32, device=b.ws.device)
+        call('pp_decode_initial', arr, len(arr), pairs, n, k, c,
+             skel.ctypes.data_as(ctypes.c_void_p), ctypes.byref(cfg), _device.ptr(hr),
+             _device.ptr(b.anns), cap, _device.ptr(b.counts), _device.ptr(b.status),
+             _device.ptr(initial.records), _device.ptr(initial.counts), initial.cap,
+             _device.ptr(b.out_index), _device.ptr(b.ws), ctypes.c_size_t(b.ws.numel()),
+             ctypes.c_uint32(stages), _device.stream())
+
+    def launch_multi(self, heads, skeleton, cfg, cap=None, keep_cifhr=False, stages=STAGE_ALL,
+                     initial=None):
+        """pp_decode_multi over a HeadSet (pp_decode_initial with `initial`); returns the
+        DecodeBuffers."""
         skel = skeleton_array(skeleton)
         if len(skel) != heads.c:
             raise ValueError('skeleton has {} edges but caf has {} fields'.format(len(skel),
@@ -170,6 +211,10 @@ class DecodeEngine:
         if stages & STAGE_GROW and not stages & STAGE_AFTER_SEED_LOOP:
             b.next_slot()
         hr = b.cifhr_buffer() if keep_cifhr else None
+        if initial is not None:
+            self._launch_initial(b, heads.arr, heads.pairs, heads.n, heads.k, heads.c, skel, cfg,
+                                 hr, cap, initial, stages)
+            return b
         call('pp_decode_multi', heads.arr, len(heads.arr), heads.pairs, heads.n, heads.k,
              heads.c, skel.ctypes.data_as(ctypes.c_void_p), ctypes.byref(cfg), _device.ptr(hr),
              _device.ptr(b.anns), cap, _device.ptr(b.counts), _device.ptr(b.status),
@@ -178,18 +223,21 @@ class DecodeEngine:
         return b
 
     def decode(self, cif, caf, skeleton, cfg, cap=None, keep_cifhr=False, heads=None,
-               compact=None):
+               compact=None, initial=None):
         """Full decode with overflow retry.  Returns (records, offsets, buffers).  With a
         HeadSet `heads`, cif / caf are ignored and the multi-scale decode runs.  `compact`
         flags (e.g. _abi.PACK_ALL) fetch compact records (pp_pack_compact) instead of full
-        pp_ann records."""
+        pp_ann records.  `initial` (InitialAnnotations): grown before the seed loop; the
+        buffers then hold out_index (see pp_decode_initial)."""
         h, w = (cif.shape[3], cif.shape[4]) if heads is None else (heads.h, heads.w)
         cap = cap or default_ann_capacity(h, w)
         while True:
             if heads is None:
-                b = self.launch(cif, caf, skeleton, cfg, cap=cap, keep_cifhr=keep_cifhr)
+                b = self.launch(cif, caf, skeleton, cfg, cap=cap, keep_cifhr=keep_cifhr,
+                                initial=initial)
             else:
-                b = self.launch_multi(heads, skeleton, cfg, cap=cap, keep_cifhr=keep_cifhr)
+                b = self.launch_multi(heads, skeleton, cfg, cap=cap, keep_cifhr=keep_cifhr,
+                                      initial=initial)
             status = b.status.cpu().numpy()
             if not (status & PP_ST_ANN_OVERFLOW).any():
                 break

@@ -1032,25 +1032,40 @@ static int role_list(const pp_scale *sc, int n, int bit, const pp_scale **out) {
     return k;
 }
 
-/* CifHr.fill: with pairs (10 CIF heads) heads i and i + 5 accumulate into one map with
- * len_cifs = 2 at head i's stride / min scale; otherwise every head on its own.  Maps
- * combine by np.maximum in order.  out (K, H', W') from head 0's field size and stride. */
+/* the CifHr map's geometry: a PP_ROLE_HRMAP (4) entry's, else CIF head 0's */
+static void hr_geometry(const pp_scale *all, int n_all, long *hh, long *ww) {
+    for (int i = 0; i < n_all; i++)
+        if (all[i].role == 4) {
+            *hh = hr_dim(all[i].H, all[i].stride);
+            *ww = hr_dim(all[i].W, all[i].stride);
+            return;
+        }
+    const pp_scale *cl[2 * PP_MAX_SCALES];
+    role_list(all, n_all, 1, cl);
+    *hh = hr_dim(cl[0]->H, cl[0]->stride);
+    *ww = hr_dim(cl[0]->W, cl[0]->stride);
+}
+
+/* CifHr.fill / fill_multiple (cif_hr.py:42-73): groups of len heads (pairs 0: len 1, every
+ * head on its own; 1: hflip pairs, heads i and i + n/2; m >= 2: len m, member t of group i =
+ * head i + t * n/m) accumulate into one map with len_cifs = len at head i's stride / min
+ * scale.  Maps combine by np.maximum in order.  out (K, H', W') (hr_geometry). */
 EXPORT void orc_cifhr_multi(const pp_scale *all, int n_all, int pairs, int K, const pp_config *cfg,
                             float *out) {
     const pp_scale *cl[2 * PP_MAX_SCALES];
     int n = role_list(all, n_all, 1, cl);
-    long hh = hr_dim(cl[0]->H, cl[0]->stride), ww = hr_dim(cl[0]->W, cl[0]->stride);
+    long hh, ww;
+    hr_geometry(all, n_all, &hh, &ww);
     size_t plane = (size_t)hh * ww;
     float *ta = (float *)malloc(sizeof(float) * K * plane);
-    int n_groups = pairs ? n / 2 : n;
+    int len = pairs <= 0 ? 1 : (pairs == 1 ? 2 : pairs);
+    int n_groups = n / len;
     for (int gi = 0; gi < n_groups; gi++) {
-        int members[2] = {gi, pairs ? gi + n / 2 : -1};
-        int len = pairs ? 2 : 1;
         float stride = (float)cl[gi]->stride;
         float min_scale = cl[gi]->cif_min_scale;
         memset(ta, 0, sizeof(float) * K * plane);
         for (int mi = 0; mi < len; mi++) {
-            const pp_scale *m = cl[members[mi]];
+            const pp_scale *m = cl[gi + mi * n_groups];
             long hw = (long)m->H * m->W;
             float *xs = (float *)malloc(sizeof(float) * 4 * (size_t)(hw + 1));
             float *ys = xs + hw, *ss = ys + hw, *vs = ss + hw;
@@ -1198,19 +1213,25 @@ EXPORT void orc_caf_scored_multi(const pp_scale *all, int n_all, int K, int C, c
 }
 
 /* cifcaf.py:67-122 over a FieldConfig of n CIF / CAF heads (one image): CifHr, CifSeeds and
- * CafScored fill from every head (the functions above), the rest as one scale. */
-EXPORT long orc_decode_multi(const pp_scale *sc, int n, int pairs, int K, int C,
-                             const int32_t *skel, const pp_config *cfg, pp_ann *out, long cap) {
-    if (K > PP_MAX_KP || C > PP_MAX_EDGES || K <= 0 || C <= 0 || n <= 0) return -1;
+ * CafScored fill from every head (the functions above), the rest as one scale.  `init`
+ * (n_init records, may be NULL): initial_annotations, grown, appended and marked occupied
+ * before the seed loop (cifcaf.py:95-98).  out_index (optional, cap entries): each output
+ * annotation's position in the list before NMS. */
+EXPORT long orc_decode_initial(const pp_scale *sc, int n, int pairs, int K, int C,
+                               const int32_t *skel, const pp_config *cfg, const pp_ann *init,
+                               long n_init, pp_ann *out, long cap, int32_t *out_index) {
+    if (K > PP_MAX_KP || C > PP_MAX_EDGES || K <= 0 || C <= 0 || n <= 0 || n_init < 0) return -1;
     const pp_scale *cl[2 * PP_MAX_SCALES], *al[2 * PP_MAX_SCALES];
     int n_cif = role_list(sc, n, 1, cl), n_caf = role_list(sc, n, 2, al);
-    if (n_cif == 0 || n_caf == 0 || (pairs && (n_cif & 1))) return -1;
+    int gsize = pairs <= 0 ? 1 : (pairs == 1 ? 2 : pairs);
+    if (n_cif == 0 || n_caf == 0 || (n_cif % gsize)) return -1;
     long total_hw = 0, cif_hw = 0;
     for (int m = 0; m < n; m++)
         if (sc[m].H <= 0 || sc[m].W <= 0 || sc[m].stride <= 0) return -1;
     for (int m = 0; m < n_cif; m++) cif_hw += (long)cl[m]->H * cl[m]->W;
     for (int m = 0; m < n_caf; m++) total_hw += (long)al[m]->H * al[m]->W;
-    long hh = hr_dim(cl[0]->H, cl[0]->stride), ww = hr_dim(cl[0]->W, cl[0]->stride);
+    long hh, ww;
+    hr_geometry(sc, n, &hh, &ww);
     float *hr = (float *)malloc(sizeof(float) * (size_t)K * hh * ww);
     orc_cifhr_multi(sc, n, pairs, K, cfg, hr);
     pp_seed *seeds = (pp_seed *)malloc(sizeof(pp_seed) * (size_t)(K * cif_hw + 1));
@@ -1233,8 +1254,16 @@ EXPORT long orc_decode_multi(const pp_scale *sc, int n, int pairs, int K, int C,
 
     occ_t o;
     occ_init(&o, K, hh, ww, cfg->occupancy_reduction, cfg->occupancy_min_scale);
-    long acap = 64, na = 0;
+    long acap = 64 + n_init, na = 0;
     pp_ann *anns = (pp_ann *)malloc(sizeof(pp_ann) * (size_t)acap);
+    for (long i = 0; i < n_init; i++) { /* cifcaf.py:95-98 */
+        pp_ann *a = &anns[na++];
+        *a = init[i];
+        a->n_keypoints = K;
+        a->image = 0;
+        grow(&d, a, 1);
+        mark_occupied(&o, a, K);
+    }
     for (long s = 0; s < n_seeds; s++) {
         const pp_seed *sd = &seeds[s];
         if (occ_get(&o, sd->field, sd->x, sd->y)) continue;
@@ -1270,9 +1299,12 @@ EXPORT long orc_decode_multi(const pp_scale *sc, int n, int pairs, int K, int C,
             if (any0) flood_fill(&d, a);
         }
     }
+    for (long i = 0; i < na; i++) anns[i].image = (int32_t)i; /* tracks positions through NMS */
     if (cfg->apply_nms) na = nms_keypoints(&d, anns, (int)na);
     for (long i = 0; i < na; i++) {
         anns[i].score = ann_score(&anns[i], K);
+        if (out_index && i < cap) out_index[i] = anns[i].image;
+        anns[i].image = 0;
         if (i < cap) out[i] = anns[i];
     }
     free(anns);
@@ -1281,6 +1313,11 @@ EXPORT long orc_decode_multi(const pp_scale *sc, int n, int pairs, int K, int C,
     free(seeds);
     free(hr);
     return na;
+}
+
+EXPORT long orc_decode_multi(const pp_scale *sc, int n, int pairs, int K, int C,
+                             const int32_t *skel, const pp_config *cfg, pp_ann *out, long cap) {
+    return orc_decode_initial(sc, n, pairs, K, C, skel, cfg, NULL, 0, out, cap, NULL);
 }
 
 /* ---- CifDet (decoder/generator/cifdet.py:27-52) ---------------------------------------- */

@@ -22,6 +22,11 @@ Fixtures:
                        CifCafCollector / CifdetCollector on random conv outputs, quad 0-2
   nms.npz              nms.Keypoints().annotations on random overlapping Annotation lists
                        (inputs, output order as input indices, mutated data), per config
+  api_initial_<mode>.npz  CifCaf.__call__(fields, initial_annotations) (cifcaf.py:95-98):
+                       the initial annotations, the output list and which outputs are them
+  api_stages.npz       CifSeeds.fill_cif min_scale / seed_mask and two heads, CafScored
+                       fill_caf distance masks and two calls, CifHr fill_cif min_scale,
+                       fill_multiple over three heads and into an existing map
   decode_<case>.npz    per-stage vectors of the full CifCaf decoder: CifHr digest +
                        per-field sums + windows, full seed list, CafScored counts + digests,
                        full annotation lists (data, joint_scales, score, decoding_order,
@@ -559,6 +564,115 @@ def gen_det(op):
     CifSeeds.threshold = None
 
 
+# initial_annotations (cifcaf.py:67-71,95-98): a decode of API_INIT_FIELDS grows three
+# annotations derived from a decode of API_INIT_PREV first
+API_INIT_FIELDS = dict(h=40, w=40, n_people=8, seed=5)
+API_INIT_PREV = dict(h=40, w=40, n_people=8, seed=6)
+
+
+def api_initial_annotations(prev_anns, annotation_cls, keypoints, skeleton):
+    """Three tracking-style initial annotations from a previous decode: (0) the first
+    annotation cut to joints 0-4, its decoding / frontier orders cut to match; (1) one joint
+    of the second annotation, moved; (2) the third annotation shifted 4 px, orders cleared."""
+    import copy  # pylint: disable=import-outside-toplevel
+    a0 = copy.deepcopy(prev_anns[0])
+    a0.data[5:] = 0.0
+    a0.joint_scales[5:] = 0.0
+    a0.decoding_order = [e for e in a0.decoding_order if e[0] < 5 and e[1] < 5]
+    a0.frontier_order = list(a0.frontier_order[:4])
+    src = prev_anns[1]
+    j = int(np.argmax(src.data[:, 2]))
+    a1 = annotation_cls(keypoints, skeleton).add(j, (src.data[j, 0] + 3.0, src.data[j, 1] - 2.0,
+                                                     0.6))
+    a1.joint_scales[j] = src.joint_scales[j]
+    a2 = copy.deepcopy(prev_anns[2])
+    a2.data[a2.data[:, 2] > 0, 0] += 4.0
+    a2.decoding_order = []
+    a2.frontier_order = []
+    return [a0, a1, a2]
+
+
+def gen_api(op):
+    """Drop-in API surface beyond the default decode: initial_annotations, the stage
+    classes' min-scale / seed-mask / distance arguments, repeated fill_caf / fill_cif calls
+    and fill_multiple over three heads or into an existing map."""
+    from openpifpaf import decoder  # pylint: disable=import-outside-toplevel
+    from openpifpaf.annotation import Annotation  # pylint: disable=import-outside-toplevel
+    from openpifpaf.decoder import CafScored, CifCaf, CifHr, CifSeeds, FieldConfig  # pylint: disable=import-outside-toplevel
+    kps, skel = constants.COCO_KEYPOINTS, list(constants.COCO_PERSON_SKELETON)
+    for mode in ('eval', 'predict'):
+        configure(decoder, mode, {})
+        fc = FieldConfig()
+        pc, pa = synthetic.planted(API_INIT_PREV['h'], API_INIT_PREV['w'],
+                                   n_people=API_INIT_PREV['n_people'], seed=API_INIT_PREV['seed'])
+        prev = CifCaf(fc, keypoints=kps, skeleton=skel)([pc, pa])
+        init = api_initial_annotations(prev, Annotation, kps, skel)
+        ins = ann_arrays(init, len(skel))  # before the decode mutates them
+        ins['ann_n_decoding'] = np.array([len(a.decoding_order) for a in init], np.int64)
+        ins['ann_n_frontier'] = np.array([len(a.frontier_order) for a in init], np.int64)
+        cif, caf = synthetic.planted(API_INIT_FIELDS['h'], API_INIT_FIELDS['w'],
+                                     n_people=API_INIT_FIELDS['n_people'],
+                                     seed=API_INIT_FIELDS['seed'])
+        ids = {id(a): i for i, a in enumerate(init)}
+        anns = CifCaf(fc, keypoints=kps, skeleton=skel)([cif, caf], initial_annotations=init)
+        out = {'mode': np.array(mode), 'input_sha': np.array(sha(cif, caf)),
+               'prev_sha': np.array(sha(pc, pa)),
+               'init_index': np.array([ids.get(id(a), -1) for a in anns], np.int64)}
+        out.update({'init_' + k[4:]: v for k, v in ins.items()})
+        out.update(ann_arrays(anns, len(skel)))
+        np.savez_compressed(os.path.join(HERE, 'api_initial_%s.npz' % mode), **out)
+        print('api initial', mode, len(prev), '->', len(anns), 'init at',
+              out['init_index'][out['init_index'] >= 0].tolist())
+
+    configure(decoder, 'eval', {})
+    fc = FieldConfig()
+    heads = synthetic.planted_multi(321, 321, [8, 16, 16, 16], n_people=5, seed=21)
+    (cif, caf), (c16a, a16), (c16b, _), (c16c, _) = heads
+    out = {'input_sha': np.array(sha(*[f for hd in heads for f in hd]))}
+
+    def hr_entry(tag, hr):
+        out[tag + '_sha'] = np.array(sha(hr))
+        out[tag + '_sums'] = hr.astype(np.float64).sum(axis=(1, 2))
+        out[tag + '_shape'] = np.array(hr.shape)
+
+    hr = CifHr(fc).fill_cif(cif, 8).accumulated
+    hr_entry('hr_base', hr)
+    hr_entry('hr_minscale', CifHr(fc).fill_cif(cif, 8, min_scale=12.0).accumulated)
+    h2 = CifHr(fc).fill_cif(cif, 8)
+    h2.fill_multiple([c16a, c16b, c16c], 16, min_scale=10.0)
+    hr_entry('hr_into', h2.accumulated)
+    hr_entry('hr_three', CifHr(fc).fill_multiple([c16a, c16b, c16c], 16).accumulated)
+
+    def seed_arr(seeds):
+        return np.array([[float(t) for t in sd] for sd in seeds], np.float32).reshape(-1, 5)
+
+    mask = [f % 3 != 1 for f in range(17)]
+    out['seed_mask'] = np.array(mask)
+    out['seeds_masked'] = seed_arr(CifSeeds(hr, fc).fill_cif(cif, 8, min_scale=10.0,
+                                                             seed_mask=mask).get())
+    sd = CifSeeds(hr, fc).fill_cif(cif, 8)
+    sd.fill_cif(c16a, 16, min_scale=12.0)
+    out['seeds_two'] = seed_arr(sd.get())
+
+    def caf_entry(tag, cs):
+        out[tag + '_fwd_counts'] = np.array([f.shape[1] for f in cs.forward], np.int32)
+        out[tag + '_bwd_counts'] = np.array([b.shape[1] for b in cs.backward], np.int32)
+        out[tag + '_fwd_sha'] = np.array([sha(f) for f in cs.forward])
+        out[tag + '_bwd_sha'] = np.array([sha(b) for b in cs.backward])
+
+    caf_entry('caf_dist', CafScored(hr, fc, skel).fill_caf(caf, 8, min_distance=24.0,
+                                                           max_distance=80.0))
+    cs = CafScored(hr, fc, skel).fill_caf(caf, 8)
+    cs.fill_caf(a16, 16, min_distance=20.0)
+    caf_entry('caf_two', cs)
+    caf_entry('caf_b_two', CafScored(hr, fc, skel, score_th=0.0001).fill_caf(caf, 8).fill_caf(
+        a16, 16, max_distance=200.0))
+    np.savez_compressed(os.path.join(HERE, 'api_stages.npz'), **out)
+    print('api stages: seeds', len(out['seeds_masked']), len(out['seeds_two']),
+          'caf', out['caf_two_fwd_counts'].sum())
+    CifSeeds.threshold = None
+
+
 def main():
     op = ref_loader.load()
     import Cython  # pylint: disable=import-outside-toplevel
@@ -587,6 +701,9 @@ def main():
     if only == ['multi']:
         gen_multi(op)
         return
+    if only == ['api']:
+        gen_api(op)
+        return
     if only == ['det']:
         gen_det(op)
         gen_det_nms(op)
@@ -599,6 +716,7 @@ def main():
     gen_det_nms(op)
     gen_inverse(op)
     gen_multi(op)
+    gen_api(op)
     for case in CASES:
         if only and case[0] not in only:
             continue

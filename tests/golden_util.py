@@ -198,3 +198,53 @@ def compare_annotations(g, recs, k=17, stats=None):
 
 
 DENSE = constants.DENSE_DECODE_SKELETON
+
+
+def load_api(name):
+    """api_initial_<mode>.npz / api_stages.npz (gen_golden.gen_api)."""
+    with np.load(os.path.join(GOLDEN, 'api_%s.npz' % name), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def api_initial_inputs(g):
+    """(cif, caf) of an api_initial fixture and its initial annotations as pp_ann records."""
+    from openpifpaf_amd._abi import ANN_DTYPE
+    cif, caf = synthetic.planted(40, 40, n_people=8, seed=5)
+    assert sha(cif, caf) == str(g['input_sha']), 'synthetic generator drifted from the fixture'
+    n = len(g['init_score'])
+    recs = np.zeros(n, ANN_DTYPE)
+    recs['data'][:, :17] = g['init_data']
+    recs['joint_scales'][:, :17] = g['init_joint_scales']
+    recs['n_keypoints'] = 17
+    recs['n_decoding'] = g['init_n_decoding']
+    recs['n_frontier'] = g['init_n_frontier']
+    for i in range(n):
+        nd, nf = int(g['init_n_decoding'][i]), int(g['init_n_frontier'][i])
+        recs['decoding_pairs'][i, :nd] = g['init_decoding_pairs'][i, :nd]
+        recs['decoding_xyv'][i, :nd] = g['init_decoding_xyv'][i, :nd]
+        recs['frontier_pairs'][i, :nf] = g['init_frontier_pairs'][i, :nf]
+    return cif, caf, recs
+
+
+def api_initial_annotations(g):
+    """The fixture's initial annotations as openpifpaf_amd Annotation objects."""
+    from openpifpaf_amd.annotation import Annotation
+    out = []
+    for i in range(len(g['init_score'])):
+        a = Annotation(constants.COCO_KEYPOINTS, constants.COCO_PERSON_SKELETON)
+        a.data = g['init_data'][i].copy()
+        a.joint_scales = g['init_joint_scales'][i].copy()
+        nd, nf = int(g['init_n_decoding'][i]), int(g['init_n_frontier'][i])
+        a.decoding_order = [(int(p[0]), int(p[1]), x[:3].copy(), x[3:].copy())
+                            for p, x in zip(g['init_decoding_pairs'][i, :nd],
+                                            g['init_decoding_xyv'][i, :nd])]
+        a.frontier_order = [(int(p[0]), int(p[1])) for p in g['init_frontier_pairs'][i, :nf]]
+        out.append(a)
+    return out
+
+
+def api_stage_heads(g):
+    """The four heads of api_stages.npz: (cif8, caf8), then three stride-16 (cif, caf)."""
+    heads = synthetic.planted_multi(321, 321, [8, 16, 16, 16], n_people=5, seed=21)
+    assert sha(*[f for hd in heads for f in hd]) == str(g['input_sha'])
+    return heads

@@ -181,3 +181,25 @@ def test_factory_from_args_profile_decoder(tmp_path):
         assert out == 2 and (tmp_path / 'p.prof').exists()
     finally:
         decoder.CifCaf.__call__ = cls_call
+
+
+def test_fields_batch_indexes_by_image():
+    """Generator.fields_batch (generator.py:43-78): one entry per image, each the model's
+    nested head list indexed by that image (None kept); the reference's .cpu().numpy() copy
+    is skipped, so the entries are views of the model's outputs."""
+    import torch
+    from openpifpaf_amd.decoder.generator.generator import Generator
+
+    heads = [torch.arange(3 * 4.0).reshape(3, 4), None,
+             (torch.zeros(3, 2, 5), [torch.ones(4, 1)])]
+
+    def model(image_batch):
+        assert image_batch.shape[0] == 3
+        return heads
+
+    out = Generator.fields_batch(model, torch.zeros(3, 3, 8, 8))
+    assert len(out) == 3  # the shortest batch dimension (the reference stops there)
+    for i, f in enumerate(out):
+        assert torch.equal(f[0], heads[0][i]) and f[1] is None
+        assert f[2][0].shape == (2, 5) and torch.equal(f[2][1][0], heads[2][1][0][i])
+        assert f[0].data_ptr() == heads[0][i].data_ptr()  # a view, not a copy

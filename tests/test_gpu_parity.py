@@ -1028,10 +1028,14 @@ def test_occupancy_device_grid():
               np.float32(rng.uniform(-5, 45)), np.float32(rng.uniform(0, 12)))
              for _ in range(200)]
     marks += [(1, np.float32(9.0), np.float32(11.0), np.float32(1.0))] * 260  # wraps past 255
+    # Python floats divide in f64 (9.000000000000002 / 2 rounds to 5; in f32 it would be
+    # 4.5 -> 4) and negative planes count from the end, as self.occupancy[f] does
+    marks[:0] = [(2, 9.000000000000002, 7.0, 1.0), (-1, 20.0, 30.0, 5.0),
+                 (-5, np.float32(3.0), np.float32(4.0), np.float32(9.0))]
     for m in marks[:30]:
         occ.set(*m)
         ref_set(*m)
-    rest = marks[30:]
+    rest = [m for m in marks[30:] if m[0] >= 0]
     occ.mark([m[0] for m in rest], [m[1] for m in rest], [m[2] for m in rest],
              [m[3] for m in rest])
     for m in rest:
@@ -1041,3 +1045,4 @@ def test_occupancy_device_grid():
         f, x, y = int(rng.integers(0, 6)), float(rng.uniform(-4, 40)), float(rng.uniform(-4, 40))
         want = 1.0 if f >= 5 else scalar_nonzero_clipped_with_reduction(ref[f], x, y, 2)
         assert occ.get(f, x, y) == want
+    assert occ.get(-2, 9.0, 9.0) == scalar_nonzero_clipped_with_reduction(ref[-2], 9.0, 9.0, 2)

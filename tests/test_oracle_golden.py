@@ -259,3 +259,58 @@ def test_oracle_multi_vs_reference(name, mode):
     errs = gu.compare_annotations(g, oracle.decode_multi(mem, skel, cfg), stats=stats)
     print('max deviation vs reference:', stats)
     assert not errs, errs[:10]
+
+
+# ---- drop-in API surface beyond the default decode (gen_golden.gen_api) ----------------
+
+@pytest.mark.parametrize('mode', ['eval', 'predict'])
+def test_oracle_initial_annotations(mode):
+    """cifcaf.py:95-98: initial annotations grown, appended and marked before the seeds."""
+    g = gu.load_api('initial_' + mode)
+    cif, caf, init = gu.api_initial_inputs(g)
+    cfg = gu.case_config({'mode': mode, 'connection_method': 'blend', 'greedy': 0})
+    recs, idx = oracle.decode_initial(cif, caf, gu.constants.COCO_PERSON_SKELETON, init, cfg)
+    assert gu.compare_annotations(g, recs) == []
+    # which outputs are the initial annotations (the reference returns those objects)
+    assert np.array_equal(np.where(idx < len(init), idx, -1), g['init_index'])
+
+
+def _hr_check(g, tag, hr):
+    assert list(hr.shape) == g[tag + '_shape'].tolist()
+    assert gu.sha(hr) == str(g[tag + '_sha']), tag
+
+
+def test_oracle_stage_api():
+    """CifHr fill_cif(min_scale) / fill_multiple (3 heads, into a map), CifSeeds fill_cif
+    (min_scale, seed_mask, two heads), CafScored fill_caf (distances, two calls)."""
+    from openpifpaf_amd._abi import make_config
+    g = gu.load_api('stages')
+    (cif, caf), (c16a, a16), (c16b, _), (c16c, _) = gu.api_stage_heads(g)
+    cfg = make_config()
+    hr = oracle.cifhr_group([cif], 8, cfg=cfg)
+    _hr_check(g, 'hr_base', hr)
+    _hr_check(g, 'hr_minscale', oracle.cifhr_group([cif], 8, 12.0, cfg=cfg))
+    ta = oracle.cifhr_group([c16a, c16b, c16c], 16, 10.0, hr_shape_=hr.shape, cfg=cfg)
+    _hr_check(g, 'hr_into', np.maximum(ta, hr))
+    _hr_check(g, 'hr_three', oracle.cifhr_group([c16a, c16b, c16c], 16, cfg=cfg))
+    scfg = make_config(seed_threshold=0.2)
+    s = gu.seeds_as_rows(oracle.seeds_head(cif, 8, hr, 10.0, cfg=scfg))
+    s = s[g['seed_mask'][s[:, 1].astype(int)]]
+    assert np.array_equal(s, g['seeds_masked'])
+    both = np.concatenate([gu.seeds_as_rows(oracle.seeds_head(cif, 8, hr, cfg=scfg)),
+                           gu.seeds_as_rows(oracle.seeds_head(c16a, 16, hr, 12.0, cfg=scfg))])
+    order = sorted(range(len(both)), key=lambda i: tuple(both[i]), reverse=True)
+    assert np.array_equal(both[order], g['seeds_two'])
+    skel = gu.constants.COCO_PERSON_SKELETON
+    fw, bw = oracle.caf_scored_head(caf, 8, hr, skel, 0.1, 24.0, 80.0, cfg=cfg)
+    assert [gu.sha(f) for f in fw] == g['caf_dist_fwd_sha'].tolist()
+    assert [gu.sha(b) for b in bw] == g['caf_dist_bwd_sha'].tolist()
+    for tag, th, kw in (('caf_two', 0.1, {'min_distance': 20.0}),
+                        ('caf_b_two', 0.0001, {'max_distance': 200.0})):
+        f1, b1 = oracle.caf_scored_head(caf, 8, hr, skel, th, cfg=cfg)
+        f2, b2 = oracle.caf_scored_head(a16, 16, hr, skel, th, cfg=cfg, **kw)
+        fw = [np.concatenate([x, y], axis=1) for x, y in zip(f1, f2)]
+        bw = [np.concatenate([x, y], axis=1) for x, y in zip(b1, b2)]
+        assert [f.shape[1] for f in fw] == g[tag + '_fwd_counts'].tolist()
+        assert [gu.sha(f) for f in fw] == g[tag + '_fwd_sha'].tolist()
+        assert [gu.sha(b) for b in bw] == g[tag + '_bwd_sha'].tolist()
