@@ -20,7 +20,8 @@ on the launch stream; algorithmic bytes = 4*K*(5*H*W + H'*W') per image (SURVEY.
 over its launch time.  `roofline_decoder_cifhr` is the decoder's own block-sparse CifHr
 stage inside `value` (its bytes: bench.cifhr_stage_bytes).
 `cpu_baseline` is the oracle (oracle/pp_oracle.c, C restatement of the reference decoder)
-on one host core over a bounded sample of the same workload.
+on one host core, then on every CPU of the job's share, over bounded samples of the same
+workload (planted, and a uniform leg).
 """
 import argparse
 import json
@@ -56,7 +57,7 @@ def parse():
     p.add_argument('--generator', default='planted', choices=('planted', 'uniform'))
     p.add_argument('--mode', default='eval', choices=('eval', 'predict'))
     p.add_argument('--batch', type=int, default=None, help='images per GPU (override)')
-    p.add_argument('--cpu-seconds', type=float, default=12.0,
+    p.add_argument('--cpu-seconds', type=float, default=18.0,
                    help='budget of the oracle CPU baseline sample (rank 0, N=1)')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--no-uniform', action='store_true',
@@ -480,7 +481,9 @@ def main():
             del c5, a5
             log('cfg5 {} done'.format(g))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line['cpu_baseline'] = cpu_baseline(cif_h, caf_h, skeleton, cfg, args.cpu_seconds)
+        uc = synthetic.batch('uniform', 64, h, w, n_caf=len(skeleton)) if default_run else None
+        line['cpu_baseline'] = cpu_baseline(cif_h, caf_h, skeleton, cfg, args.cpu_seconds,
+                                            *(uc or (None, None)))
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -620,54 +623,85 @@ def cfg2_latency(gen, cfg, dev, calls=200):
             'calls': calls}
 
 
-def cpu_baseline(cif, caf, skeleton, cfg, budget_s):
+def cpu_share():
+    """(threads to use, how they were counted): the CPUs this process may run on
+    (sched_getaffinity), capped by the cgroup's CPU quota where one is set (cpu.max, as on
+    the GPU box, whose affinity mask shows the whole machine)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            q, period = f.read().split()[:2]
+        if q != 'max':
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    cores = min(aff, quota) if quota else aff
+    return cores, {'affinity_cpus': aff, 'cgroup_cpu_quota': quota}
+
+
+def cpu_baseline(cif, caf, skeleton, cfg, budget_s, ucif=None, ucaf=None):
     """The oracle (C restatement of the reference decoder) on the host cores, over a bounded
-    sample of the same images: one thread, then one thread per core of this job's CPU share
-    (ctypes releases the GIL for the C decode; the oracle has no global state).  The
-    reference's own Cython decoder cannot travel to the GPU box; profiles/cpu_ratio.json
-    (tools/cpu_ratio.py, measured in the build container on the same images) gives the
-    reference/oracle time ratio, so `reference_equivalent` = oracle rate / ratio."""
+    sample of the same images: one thread, then one thread per CPU of this job's share
+    (cpu_share(); ctypes releases the GIL for the C decode; the oracle has no global state),
+    cycling over the batch; then the uniform batch on every thread.  The reference's own
+    Cython decoder cannot travel to the GPU box; profiles/cpu_ratio.json (tools/cpu_ratio.py,
+    measured in the build container on the same generators) gives the reference/oracle time
+    ratio per generator, so `reference_equivalent` = oracle rate / ratio."""
     import concurrent.futures
     sys.path.insert(0, os.path.join(REPO, 'oracle'))
     import oracle  # pylint: disable=import-outside-toplevel
     oracle.lib()
 
-    def worker(first, budget):
+    def worker(c, a, first, budget):
         n, t0 = 0, time.perf_counter()
         while time.perf_counter() - t0 < budget:
-            i = (first + n) % len(cif)
-            oracle.decode(cif[i], caf[i], skeleton, cfg)
+            i = (first + n) % len(c)
+            oracle.decode(c[i], a[i], skeleton, cfg)
             n += 1
         return n, time.perf_counter() - t0
 
-    n1, dt1 = worker(0, budget_s / 2)
+    def all_threads(c, a, budget):
+        with concurrent.futures.ThreadPoolExecutor(cores) as ex:
+            res = list(ex.map(lambda t: worker(c, a, 17 * t, budget), range(cores)))
+        return sum(n for n, _ in res), max(dt for _, dt in res)
+
+    n1, dt1 = worker(cif, caf, 0, budget_s / 3)
     one = n1 / dt1
-    try:
-        share = len(os.sched_getaffinity(0))
-    except AttributeError:
-        share = os.cpu_count()
-    cores = max(1, min(share, int(os.environ.get('OMP_NUM_THREADS', '16') or 16)))
-    with concurrent.futures.ThreadPoolExecutor(cores) as ex:
-        res = list(ex.map(lambda t: worker(17 * t, budget_s / 2), range(cores)))
-    allc = sum(n for n, _ in res) / max(dt for _, dt in res)
+    cores, share = cpu_share()
+    na, dta = all_threads(cif, caf, budget_s / 3)
+    allc = na / dta
     out = {'value': round(allc, 2), 'unit': 'images/s', 'cores': cores, 'kind': 'port',
            'single_core': round(one, 2),
            'sample': '{} single-image decodes on one core in {:.1f} s, then {} on {} threads in '
-                     '{:.1f} s, cycling over the batch; oracle/pp_oracle.c'.format(
-                         n1, dt1, sum(n for n, _ in res), cores, max(dt for _, dt in res)),
-           'host_cpu_count': os.cpu_count()}
+                     '{:.1f} s, cycling over the planted batch; oracle/pp_oracle.c'.format(
+                         n1, dt1, na, cores, dta),
+           'cores_from': share, 'host_cpu_count': os.cpu_count()}
     try:
         with open(os.path.join(REPO, 'profiles', 'cpu_ratio.json')) as f:
-            ratio = json.load(f)['cases']['planted']
-        out['reference_over_oracle_time'] = ratio['ratio']
-        out['reference_equivalent'] = {
-            'single_core': round(one / ratio['ratio'], 2),
-            'all_cores': round(allc / ratio['ratio'], 2),
-            'source': 'profiles/cpu_ratio.json (reference {} ms vs oracle {} ms per planted '
-                      '80x80 eval image, one thread, build container)'.format(
-                          ratio['reference_ms_per_image'], ratio['oracle_ms_per_image'])}
+            ratios = json.load(f)['cases']
     except (OSError, KeyError, ValueError):
-        pass
+        ratios = {}
+    if 'planted' in ratios:
+        r = ratios['planted']
+        out['reference_over_oracle_time'] = r['ratio']
+        out['reference_equivalent'] = {
+            'single_core': round(one / r['ratio'], 2),
+            'all_cores': round(allc / r['ratio'], 2),
+            'source': 'profiles/cpu_ratio.json (reference vs oracle total time over {} planted '
+                      '80x80 eval images, one thread, build container)'.format(r['images'])}
+    if ucif is not None:
+        nu, dtu = all_threads(ucif, ucaf, budget_s / 3)
+        out['uniform'] = {'value': round(nu / dtu, 2), 'unit': 'images/s', 'cores': cores,
+                          'sample': '{} uniform decodes on {} threads in {:.1f} s'.format(
+                              nu, cores, dtu)}
+        if 'uniform' in ratios:
+            out['uniform']['reference_over_oracle_time'] = ratios['uniform']['ratio']
+            out['uniform']['reference_equivalent'] = round(
+                nu / dtu / ratios['uniform']['ratio'], 2)
     return out
 
 

@@ -52,10 +52,8 @@ def build(force=False, verbose=True, variant=''):
     os.makedirs(bdir, exist_ok=True)
     if (not force and os.path.exists(lib) and os.path.getmtime(lib) >= _deps_mtime()):
         return lib
-    # diagnostic variants: 'stamps' (cycle stamps), 'exp_*' (-DPP_EXP_*: timing experiments
-    # that switch parts of a kernel off; never correct, never loaded by default)
-    extra = (['-DPP_STAMPS'] if variant == 'stamps' else
-             ['-DPP_' + variant.upper()] if variant.startswith('exp_') else [])
+    # diagnostic variant: 'stamps' (in-kernel cycle stamps; never loaded by default)
+    extra = ['-DPP_STAMPS'] if variant == 'stamps' else []
     workers = min(8, len(sources()))
     with concurrent.futures.ThreadPoolExecutor(workers) as ex:
         objs = list(ex.map(lambda src: _compile(src, bdir, extra), sources()))
@@ -72,6 +70,3 @@ if __name__ == '__main__':
     build(force='--force' in sys.argv)
     if '--stamps' in sys.argv:
         build(force='--force' in sys.argv, variant='stamps')
-    for arg in sys.argv[1:]:
-        if arg.startswith('--exp_'):
-            build(force='--force' in sys.argv, variant=arg[2:])

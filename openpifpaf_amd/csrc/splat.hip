@@ -181,9 +181,6 @@ __device__ __forceinline__ float fold_apply(float acc, const FoldTerm &f) {
 // pixel: two at a time on the fast path, one at a time when the set holds a slow one.
 __device__ __forceinline__ float fold_block(float acc, const FoldCand *cand, uint64_t q,
                                             uint64_t slow, float fx, float fy, uint32_t key) {
-#ifdef PP_EXP_NOFOLD
-    return acc + (float)__popcll(q);  // timing experiment: the fold switched off
-#endif
     if (q & slow) {
         for (; q; q &= q - 1) {
             const int c = __builtin_ctzll(q);
@@ -979,9 +976,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
 #endif
     for (int t = threadIdx.x; t < a.tiles; t += 256)  // untouched tiles: no block written
         if (!((s_bits[t >> 5] >> (t & 31)) & 1u)) a.masks[fld * a.tiles + t] = 0ull;
-#ifdef PP_EXP_PHASE1
-    return;  // timing / counter experiment: phase 1 (list, bins, tile masks) only
-#endif
 
     // ---- phase 2: touched tiles, one wave each, claimed from an LDS counter ----
     FoldCand *cand = s_cand[wave];
