@@ -71,6 +71,8 @@ typedef struct pp_config {
     int32_t apply_nms;            /* CifCaf(nms=True) -> nms.Keypoints()  cifcaf.py:43-44   */
     int32_t occupancy_reduction;  /* Occupancy(shape, 2, min_scale=4)  cifcaf.py:84         */
     int32_t occupancy_min_scale;
+    uint32_t seed_skip_mask;      /* bit f set: field f emits no seeds, FieldConfig.seed_mask[f]
+                                     falsy (cif_seeds.py:28-29); 0 = every field seeds       */
 } pp_config;
 
 /*

@@ -91,6 +91,7 @@ class PPConfig(ctypes.Structure):
         ('apply_nms', ctypes.c_int32),
         ('occupancy_reduction', ctypes.c_int32),
         ('occupancy_min_scale', ctypes.c_int32),
+        ('seed_skip_mask', ctypes.c_uint32),
     ]
 
 
@@ -99,7 +100,7 @@ def make_config(*, cif_threshold=0.1, seed_threshold=0.2, seed_score_scale=1.0,
                 keypoint_threshold=0.0, nms_keypoint_threshold=0.0,
                 nms_instance_threshold=0.0, nms_suppression=0.0, stride=8, cif_neighbors=16,
                 force_complete=True, greedy=False, connection_method='blend', apply_nms=True,
-                occupancy_reduction=2, occupancy_min_scale=4):
+                occupancy_reduction=2, occupancy_min_scale=4, seed_mask=None):
     """Defaults = eval_coco defaults (decoder/factory.py:17-22, eval_coco.py:215)."""
     if connection_method not in ('blend', 'max'):
         raise Exception('connection method not known')
@@ -109,7 +110,17 @@ def make_config(*, cif_threshold=0.1, seed_threshold=0.2, seed_score_scale=1.0,
         nms_instance_threshold, nms_suppression, int(stride), int(cif_neighbors),
         int(bool(force_complete)), int(bool(greedy)),
         0 if connection_method == 'blend' else 1, int(bool(apply_nms)),
-        int(occupancy_reduction), int(occupancy_min_scale))
+        int(occupancy_reduction), int(occupancy_min_scale), seed_skip_mask(seed_mask))
+
+
+def seed_skip_mask(seed_mask):
+    """pp_config.seed_skip_mask of FieldConfig.seed_mask: bit f set where seed_mask[f] is
+    falsy (cif_seeds.py:28-29); None = every field seeds."""
+    if seed_mask is None:
+        return 0
+    if len(seed_mask) > 32:
+        raise ValueError('seed_mask longer than 32 fields')
+    return sum(1 << f for f, m in enumerate(seed_mask) if not m)
 
 
 EVAL_CONFIG = dict(seed_threshold=0.2, force_complete=True, keypoint_threshold=0.0,

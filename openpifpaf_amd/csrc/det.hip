@@ -26,6 +26,7 @@ struct DetArgs {
     int K, H, W, hh, ww;
     int64_t pitch;
     float stride, th, score_scale;
+    uint32_t skip;         // pp_config.seed_skip_mask (cif_seeds.py:70-71 seed_mask)
     // per (image, field) segments: v, x, y, w, h (each H*W) and counts
     float *seg;
     int *seg_n;
@@ -60,7 +61,8 @@ __global__ __launch_bounds__(256) void det_seeds_emit_kernel(DetArgs a) {
     float *sv = a.seg + seg_base(a, fld), *sx = sv + hw, *sy = sx + hw, *sw = sy + hw,
           *sh = sw + hw;
     int running = 0;
-    for (int base = 0; base < hw; base += 256) {
+    const int hw_seed = ((a.skip >> f) & 1u) ? 0 : hw;  // a masked field emits nothing
+    for (int base = 0; base < hw_seed; base += 256) {
         const int cell = base + threadIdx.x;
         bool keep = false;
         float v = 0.0f, x = 0.0f, y = 0.0f, w = 0.0f, h = 0.0f;
@@ -532,6 +534,7 @@ int pp_cifdet_seeds(const float *d_det, const float *d_cifhr, int32_t n_img, int
     a.pitch = pp_cifhr_pitch(a.ww);
     a.stride = (float)cfg->stride;
     a.th = cfg->seed_threshold;
+    a.skip = cfg->seed_skip_mask;
     a.score_scale = cfg->seed_score_scale;
     a.seg = d_seg;
     a.seg_n = d_seg_counts;
@@ -611,6 +614,7 @@ int pp_cifdet_decode(const float *d_det, int32_t n_img, int32_t K, int32_t H, in
     a.pitch = d.pitch;
     a.stride = (float)cfg->stride;
     a.th = cfg->seed_threshold;
+    a.skip = cfg->seed_skip_mask;
     a.score_scale = cfg->seed_score_scale;
     a.seg = (float *)(ws + d.off_seg);
     a.seg_n = (int *)(ws + d.off_seg_n);

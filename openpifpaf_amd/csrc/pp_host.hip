@@ -135,6 +135,7 @@ void pp_default_config(pp_config *c) {
     c->apply_nms = 1;
     c->occupancy_reduction = 2;
     c->occupancy_min_scale = 4;
+    c->seed_skip_mask = 0u;
 }
 
 }  // extern "C"

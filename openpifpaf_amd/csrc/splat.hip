@@ -781,6 +781,8 @@ __global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
 // candidates carry their group, and a change of group closes the running fold into res.
 // Across passes res stays in the map and the open group's fold in `aux`.
 constexpr int kSpU = 32;      // cells per thread per compaction round (confidences in flight)
+constexpr int kSplitSlots = 1024;  // small batches: workgroups per field = kSplitSlots / fields
+constexpr int kMaxSplit = 64;
 constexpr int kSpStage = 1024; // kept cells of a round staged in LDS (phase 2's s_cand space)
 
 struct HrSparseArgs {
@@ -795,6 +797,8 @@ struct HrSparseArgs {
     float *aux;       // MULTI: open-group folds between passes, same shape as map
     uint64_t *masks;  // (n_img * K, tiles) written blocks
     int tiles_x, tiles, tiles_y;
+    int split;        // workgroups per field (small batches): each builds the field's list
+                      // (identical writes) and folds every split-th touched tile
 };
 
 __device__ __forceinline__ float nan_max(float a, float b) {  // np.maximum
@@ -827,11 +831,11 @@ __device__ uint64_t *g_hr_stamps;
 // the 64x64 tiles the boxes touch (cleared by the caller before the first barrier).
 // Returns the list length; s_gbeg[g] = start of group g's entries.  Ends with a barrier.
 template <bool MULTI>
-__device__ int hr_splat_list(const HrSparseArgs &a, int64_t fld, uint32_t *s_bits,
+__device__ int hr_splat_list(const HrSparseArgs &a, int64_t fld, int64_t slot, uint32_t *s_bits,
                              int (*s_cnt)[kSpU][4], int *s_gbeg, int *stage) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ng = MULTI ? a.h.n_groups : 1;
-    FoldCand *glist = a.list + fld * a.list_cap;
+    FoldCand *glist = a.list + slot * a.list_cap;  // this workgroup's own copy
     int running = 0, buf = 0;
     for (int g = 0; g < ng; g++) {
         if (threadIdx.x == 0) s_gbeg[g] = running;
@@ -950,20 +954,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
     __shared__ uint64_t s_live[4];
     __shared__ int s_next;
 
-    const int64_t fld = blockIdx.x;  // image * K + field
+    const int64_t fld = blockIdx.x / a.split;  // image * K + field
+    const int part = (int)(blockIdx.x % a.split);
+    const int64_t slot = blockIdx.x;  // list / bins copy of this workgroup (fld * split + part)
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (wave == 0) HR_STAMP(0);
     if (threadIdx.x < kTileBits / 32) s_bits[threadIdx.x] = 0u;
     if (threadIdx.x == 0) s_next = 0;
 
-    const int total = hr_splat_list<MULTI>(a, fld, s_bits, s_cnt, s_gbeg,
+    const int total = hr_splat_list<MULTI>(a, fld, slot, s_bits, s_cnt, s_gbeg,
                                            reinterpret_cast<int *>(&s_cand[0][0]));
     const bool use_bins = !MULTI && a.bins_cap > 0 && total > kBinMin;
     if (use_bins)
-        hr_row_bins(a.list + fld * a.list_cap, total, a.bins + fld * a.bins_cap, a.bins_cap,
+        hr_row_bins(a.list + slot * a.list_cap, total, a.bins + slot * a.bins_cap, a.bins_cap,
                     a.tiles_y, s_rb, s_rowcnt, s_rowoff);
     const int ng = MULTI ? a.h.n_groups : 1;
-    const FoldCand *glist = a.list + fld * a.list_cap;
+    const FoldCand *glist = a.list + slot * a.list_cap;
 #ifdef PP_STAMPS
     if (wave == 0) {
         HR_STAMP(1);
@@ -986,7 +992,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
     while (true) {
         int claim = 0;
         if (lane == 0) claim = atomicAdd(&s_next, 1);
-        claim = __builtin_amdgcn_readfirstlane(claim);
+        // this workgroup's claim-th tile is the field's (claim * split + part)-th touched one
+        claim = __builtin_amdgcn_readfirstlane(claim) * a.split + part;
         // advance to the claim-th touched tile (claims grow, so the walk only moves on)
         int t = -1;
         while (wd < nwords) {
@@ -1009,7 +1016,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
         // candidates come from the tile row's bin, or from the whole list (MULTI, overflow)
         const int row = t / a.tiles_x;
         const int rc = use_bins ? s_rowcnt[row] : -1;
-        const FoldCand *src = rc >= 0 ? a.bins + fld * a.bins_cap + s_rowoff[row] : glist;
+        const FoldCand *src = rc >= 0 ? a.bins + slot * a.bins_cap + s_rowoff[row] : glist;
         const int src_n = rc >= 0 ? rc : total;
         int cursor = 0;
         while (true) {
@@ -1241,8 +1248,15 @@ int cifhr_heads_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config
 template int cifhr_heads_launch<false>(const Heads &, int32_t, int32_t, const pp_config *, float *,
                                        void *, size_t, hipStream_t, const char *);
 
+// workgroups per field of cifhr_sparse_kernel: fewer fields than kSplitSlots split each
+// field's tiles over several workgroups (each builds its own copy of the field's list: a
+// re-read of its confidences, no extra round trip, no shared writes)
+static int sparse_split(int64_t nf) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, kSplitSlots / std::max<int64_t>(1, nf)));
+}
+
 size_t cifhr_sparse_workspace_size(const Heads &h, int n_img, int K) {
-    const size_t nf = (size_t)n_img * K;
+    const size_t nf = (size_t)n_img * K * sparse_split((int64_t)n_img * K);
     size_t bytes = round_up((int64_t)(nf * (size_t)h.cif_cells() * sizeof(FoldCand)), 256);
     if (h.n_groups == 1)
         bytes += round_up((int64_t)(nf * (size_t)bins_capacity(h.cif_cells()) * sizeof(FoldCand)), 256);
@@ -1280,11 +1294,14 @@ int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_confi
     // row bins for single-scale maps of at most kMaxBinRows tile rows
     a.bins_cap = (h.n_groups == 1 && a.tiles_y <= kMaxBinRows) ? bins_capacity(h.cif_cells()) : 0;
     a.bins = (FoldCand *)((char *)d_workspace +
-                          round_up((int64_t)((size_t)n_img * K * a.list_cap * sizeof(FoldCand)), 256));
+                          round_up((int64_t)((size_t)n_img * K * sparse_split((int64_t)n_img * K) *
+                                             a.list_cap * sizeof(FoldCand)), 256));
     a.map = d_map;
     a.aux = d_aux;
     a.masks = d_masks;
-    const unsigned nblocks = (unsigned)((int64_t)n_img * K);
+    const int64_t nf = (int64_t)n_img * K;
+    a.split = sparse_split(nf);
+    const unsigned nblocks = (unsigned)(nf * a.split);
 #ifdef PP_STAMPS
     uint64_t *st = nullptr;
     hipMalloc((void **)&st, (size_t)nblocks * 9 * sizeof(uint64_t));

@@ -64,6 +64,7 @@ struct SeedArgs {
     HrMap hr;
     int K;
     float th, score_scale;
+    uint32_t skip;      // pp_config.seed_skip_mask: fields that emit no seeds
     pp_seed *seeds;     // (n_img, cap) sorted output
     int cap;            // K * sum of the heads' H * W
     int *counts;        // (n_img) seeds per image
@@ -79,9 +80,19 @@ struct SeedArgs {
 };
 
 // stage 1: one workgroup per (image, head, field) — cif_seeds.py:28-47 for that field, in
-// row-major cell order, into the segment's slot range
+// row-major cell order, into the segment's slot range.  A round covers 256 * kEmitU cells:
+// every thread loads its kEmitU confidences at once, the cells above threshold are staged
+// in LDS in cell order (one barrier orders the (cell batch, wave) counts), then one thread
+// per staged cell reads x, y, scale and the CifHr value and the seeds are compacted in the
+// staged order.  So a round is about four memory round trips however many cells it keeps
+// (a round staging more than kEmitStage falls back to batches of 256).
+constexpr int kEmitU = 32;
+constexpr int kEmitStage = 256 * kEmitU;  // a whole round: no fallback for one 80x80 field
+
 __global__ __launch_bounds__(256) void seeds_emit_kernel(SeedArgs a) {
     __shared__ int s_tmp[4];
+    __shared__ __attribute__((aligned(16))) int s_cnt[kEmitU][4];
+    __shared__ int s_stage[kEmitStage];
     const int nseg = a.h.n_cif * a.K;
     const int img = (int)(blockIdx.x / nseg), seg = (int)(blockIdx.x % nseg);
     const int m = seg / a.K, f = seg % a.K;
@@ -90,61 +101,107 @@ __global__ __launch_bounds__(256) void seeds_emit_kernel(SeedArgs a) {
     const bool ms_on = (a.h.ms_on >> m) & 1u;
     const float ms_th = a.h.ms_th[m];
     const int64_t cap = a.cap;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     float *gv = a.g_keys + (int64_t)img * 4 * cap + a.seg_base(m, f);
     float *gx = gv + cap, *gy = gx + cap, *gs = gy + cap;
     int *gf = a.g_f + (int64_t)img * cap + a.seg_base(m, f);
     const float *p = a.h.cif[m] + ((int64_t)img * a.K + f) * 5 * hw;
     const int64_t plane = (int64_t)img * a.K + f;
-    // kU cells per thread per batch (cells base + k * 256 + tid): confidences, then the rows
-    // of passing cells, then the CifHr lookups, each issued for the whole batch at once
-    constexpr int kU = 8;
     int running = 0;
-    for (int base = 0; base < hw; base += 256 * kU) {
-        float c[kU], x[kU], y[kU], sc[kU], v[kU];
-        bool keep[kU];
+    if ((a.skip >> f) & 1u) {  // `if seed_mask is not None and not seed_mask[field_i]: continue`
+        if (threadIdx.x == 0) a.f_counts[blockIdx.x] = 0;
+        return;
+    }
+    // cif_seeds.py:28-47 for one cell above threshold: (kept, v, x, y, s)
+    auto score = [&](int cell, float c, float &v, float &x, float &y, float &sc) {
+        x = p[hw + cell];
+        y = p[2 * hw + cell];
+        sc = p[4 * hw + cell];
+        if (ms_on && !(sc > ms_th)) return false;  // then p[4] > min_scale / stride
+        x = x * stride;
+        y = y * stride;
+        const float hv = a.hr.at(plane, x, y, 0.0f);
+        float vv = 0.9f * hv + 0.1f * c;  // 0.9 * v + 0.1 * c
+        if (a.score_scale != 1.0f) vv = vv * a.score_scale;
+        v = vv;
+        sc = sc * stride;
+        return vv > a.th;
+    };
+    for (int base = 0; base < hw; base += 256 * kEmitU) {
+        float c[kEmitU];
 #pragma unroll
-        for (int k = 0; k < kU; k++) {
+        for (int k = 0; k < kEmitU; k++) {
             const int cell = base + k * 256 + (int)threadIdx.x;
-            c[k] = cell < hw ? p[cell] : NAN;
-            x[k] = y[k] = sc[k] = v[k] = 0.0f;
+            c[k] = cell < hw ? p[cell] : NAN;  // NaN: never > threshold
         }
+        uint32_t keep = 0;
 #pragma unroll
-        for (int k = 0; k < kU; k++) {
-            const int cell = base + k * 256 + (int)threadIdx.x;
-            if (c[k] > a.th) {  // p[:, p[0] > threshold]
-                x[k] = p[hw + cell];
-                y[k] = p[2 * hw + cell];
-                sc[k] = p[4 * hw + cell];
+        for (int k = 0; k < kEmitU; k++) keep |= (c[k] > a.th) ? (1u << k) : 0u;
+#pragma unroll
+        for (int k = 0; k < kEmitU; k++) {
+            const uint64_t bal = __ballot((keep >> k) & 1u);
+            if (lane == 0) s_cnt[k][wave] = __popcll(bal);
+        }
+        __syncthreads();
+        int staged = 0;
+#pragma unroll 4
+        for (int k = 0; k < kEmitU; k++) {
+            const int4 q = *reinterpret_cast<const int4 *>(&s_cnt[k][0]);
+            staged += q.x + q.y + q.z + q.w;
+        }
+        if (staged <= kEmitStage) {
+            int o = 0;  // stage position of batch k's cell in this thread (ballot = cell order)
+#pragma unroll 4
+            for (int k = 0; k < kEmitU; k++) {
+                const int4 q = *reinterpret_cast<const int4 *>(&s_cnt[k][0]);
+                const uint64_t bal = __ballot((keep >> k) & 1u);
+                if ((keep >> k) & 1u)
+                    s_stage[o + (wave > 0 ? q.x : 0) + (wave > 1 ? q.y : 0) + (wave > 2 ? q.z : 0) +
+                            lane_prefix(bal)] = base + k * 256 + (int)threadIdx.x;
+                o += q.x + q.y + q.z + q.w;
+            }
+            __syncthreads();
+            for (int e0 = 0; e0 < staged; e0 += 256) {  // block-uniform
+                const int e = e0 + (int)threadIdx.x;
+                float v = 0.0f, x = 0.0f, y = 0.0f, sc = 0.0f;
+                bool ok = false;
+                if (e < staged) {
+                    const int cell = s_stage[e];
+                    ok = score(cell, p[cell], v, x, y, sc);
+                }
+                int total;
+                const int slot = block_compact<4>(ok, s_tmp, total);
+                if (ok) {
+                    const int pos = running + slot;
+                    gv[pos] = v;
+                    gx[pos] = x;
+                    gy[pos] = y;
+                    gs[pos] = sc;
+                    gf[pos] = f;
+                }
+                running += total;
+            }
+        } else {  // more than the stage holds: batch by batch
+#pragma unroll 1
+            for (int k = 0; k < kEmitU; k++) {
+                float v = 0.0f, x = 0.0f, y = 0.0f, sc = 0.0f;
+                bool ok = false;
+                const int cell = base + k * 256 + (int)threadIdx.x;
+                if ((keep >> k) & 1u) ok = score(cell, p[cell], v, x, y, sc);  // no dynamic c[k]
+                int total;
+                const int slot = block_compact<4>(ok, s_tmp, total);
+                if (ok) {
+                    const int pos = running + slot;
+                    gv[pos] = v;
+                    gx[pos] = x;
+                    gy[pos] = y;
+                    gs[pos] = sc;
+                    gf[pos] = f;
+                }
+                running += total;
             }
         }
-#pragma unroll
-        for (int k = 0; k < kU; k++) {
-            keep[k] = c[k] > a.th && (!ms_on || sc[k] > ms_th);  // then p[4] > min_scale / stride
-            if (keep[k]) {
-                x[k] = x[k] * stride;
-                y[k] = y[k] * stride;
-                const float hv = a.hr.at(plane, x[k], y[k], 0.0f);
-                float vv = 0.9f * hv + 0.1f * c[k];  // 0.9 * v + 0.1 * c
-                if (a.score_scale != 1.0f) vv = vv * a.score_scale;
-                v[k] = vv;
-                keep[k] = vv > a.th;
-                sc[k] = sc[k] * stride;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < kU; k++) {
-            int total;
-            const int slot = block_compact<4>(keep[k], s_tmp, total);
-            if (keep[k]) {
-                const int pos = running + slot;
-                gv[pos] = v[k];
-                gx[pos] = x[k];
-                gy[pos] = y[k];
-                gs[pos] = sc[k];
-                gf[pos] = f;
-            }
-            running += total;
-        }
+        __syncthreads();  // s_cnt / s_stage are rewritten by the next round
     }
     if (threadIdx.x == 0) a.f_counts[blockIdx.x] = running;
 }
@@ -171,62 +228,162 @@ __device__ __forceinline__ uint64_t bitonic_pick(int i, int j, int k, uint64_t a
     return lower == desc ? mx : mn;
 }
 
+// lane ^ M for a constant M: DPP moves within a row of 16 (quad_perm for 1 and 2; the row
+// half-mirror (lane ^ 7) or mirror (lane ^ 15) composed with a quad_perm / half-mirror for
+// 4 and 8), a bpermute across rows
+template <int M>
+__device__ __forceinline__ uint32_t lane_xor32(uint32_t v) {
+    if constexpr (M == 1) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+    } else if constexpr (M == 2) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+    } else if constexpr (M == 4) {  // (lane ^ 7) ^ 3
+        const int h = __builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, h, 0x1B, 0xF, 0xF, false);
+    } else if constexpr (M == 8) {  // (lane ^ 15) ^ 7
+        const int h = __builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, h, 0x141, 0xF, 0xF, false);
+    } else {
+        return (uint32_t)__shfl_xor((int)v, M);
+    }
+}
+
+template <int M>
+__device__ __forceinline__ uint64_t lane_xor64(uint64_t v) {
+    return ((uint64_t)lane_xor32<M>((uint32_t)(v >> 32)) << 32) | lane_xor32<M>((uint32_t)v);
+}
+
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
     const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
     const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
     return ((uint64_t)hi << 32) | lo;
 }
 
-// descending bitonic sort of kSortLds (4096) u64 keys, 4 per thread of a 1024-thread block
-// (element 4 * thread + e in key[e]); s_buf (kSortLds) is scratch for the cross-wave stages
-static_assert(kSortLds == 4096, "bitonic4096_desc sorts 4 keys per thread of 1024");
-__device__ void bitonic4096_desc(uint64_t key[4], uint64_t *s_buf) {
+// descending bitonic sort of the first NP (a power of two, 4 <= NP <= kSortLds = 4096) u64
+// keys held 4 per thread of a 1024-thread block (element 4 * thread + e in key[e]; elements
+// past NP are left alone); s_buf (kSortLds) is scratch for the cross-wave stages, which
+// only NP > 256 needs.  Every stage (K, J) is a compile-time instance (BitonicMerge /
+// BitonicStages below): register partners stay static register names and lane partners
+// constant shuffle masks, which a runtime stage loop turns into select chains and
+// bpermute address arithmetic.
+static_assert(kSortLds == 4096, "bitonic_desc sorts 4 keys per thread of 1024");
+template <int K, int J>
+__device__ __forceinline__ void bitonic_stage(uint64_t key[4], uint64_t *s_buf) {
     const int t = threadIdx.x;
-    for (int k = 2; k <= kSortLds; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            if (j >= 256) {  // partner in another wave: through LDS
-                __syncthreads();  // earlier readers of s_buf are done
+    if constexpr (J >= 256) {  // partner in another wave: through LDS
+        __syncthreads();       // earlier readers of s_buf are done
 #pragma unroll
-                for (int e = 0; e < 4; e++) s_buf[4 * t + e] = key[e];
-                __syncthreads();
+        for (int e = 0; e < 4; e++) s_buf[4 * t + e] = key[e];
+        __syncthreads();
 #pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    const int i = 4 * t + e;
-                    key[e] = bitonic_pick(i, j, k, key[e], s_buf[i ^ j]);
-                }
-            } else if (j >= 4) {  // partner thread t ^ (j / 4), same slot, same wave
-#pragma unroll
-                for (int e = 0; e < 4; e++)
-                    key[e] = bitonic_pick(4 * t + e, j, k, key[e], shfl_xor64(key[e], j >> 2));
-            } else {  // partner slot e ^ j of this thread
-                uint64_t nk[4];
-#pragma unroll
-                for (int e = 0; e < 4; e++) nk[e] = bitonic_pick(4 * t + e, j, k, key[e], key[e ^ j]);
-#pragma unroll
-                for (int e = 0; e < 4; e++) key[e] = nk[e];
-            }
+        for (int e = 0; e < 4; e++) {
+            const int i = 4 * t + e;
+            key[e] = bitonic_pick(i, J, K, key[e], s_buf[i ^ J]);
         }
+    } else if constexpr (J >= 4) {  // partner thread t ^ (J / 4), same slot, same wave
+#pragma unroll
+        for (int e = 0; e < 4; e++)
+            key[e] = bitonic_pick(4 * t + e, J, K, key[e], lane_xor64<(J >> 2)>(key[e]));
+    } else {  // partner slot e ^ J of this thread
+        uint64_t nk[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) nk[e] = bitonic_pick(4 * t + e, J, K, key[e], key[e ^ J]);
+#pragma unroll
+        for (int e = 0; e < 4; e++) key[e] = nk[e];
     }
+}
+
+template <int K, int J>
+struct BitonicStages {  // stages J, J / 2, ..., 1 of the merge of blocks of K
+    __device__ __forceinline__ static void run(uint64_t key[4], uint64_t *s_buf) {
+        bitonic_stage<K, J>(key, s_buf);
+        BitonicStages<K, J / 2>::run(key, s_buf);
+    }
+};
+template <int K>
+struct BitonicStages<K, 0> {
+    __device__ __forceinline__ static void run(uint64_t *, uint64_t *) {}
+};
+
+template <int K, int NP>
+struct BitonicMerge {  // merges of block sizes K, 2K, ..., NP
+    __device__ __forceinline__ static void run(uint64_t key[4], uint64_t *s_buf) {
+        BitonicStages<K, K / 2>::run(key, s_buf);
+        BitonicMerge<2 * K, NP>::run(key, s_buf);
+    }
+};
+template <int NP>
+struct BitonicMerge<2 * NP, NP> {
+    __device__ __forceinline__ static void run(uint64_t *, uint64_t *) {}
+};
+
+template <int NP>
+__device__ __forceinline__ void bitonic_desc_np(uint64_t key[4], uint64_t *s_buf) {
+    BitonicMerge<2, NP>::run(key, s_buf);
+}
+
+// the sort of the first np keys (np a power of two, rounded up to 4); block-uniform np
+__device__ void bitonic_desc(uint64_t key[4], uint64_t *s_buf, int np) {
+    switch (np <= 4 ? 4 : np) {
+    case 4: bitonic_desc_np<4>(key, s_buf); break;
+    case 8: bitonic_desc_np<8>(key, s_buf); break;
+    case 16: bitonic_desc_np<16>(key, s_buf); break;
+    case 32: bitonic_desc_np<32>(key, s_buf); break;
+    case 64: bitonic_desc_np<64>(key, s_buf); break;
+    case 128: bitonic_desc_np<128>(key, s_buf); break;
+    case 256: bitonic_desc_np<256>(key, s_buf); break;
+    case 512: bitonic_desc_np<512>(key, s_buf); break;
+    case 1024: bitonic_desc_np<1024>(key, s_buf); break;
+    case 2048: bitonic_desc_np<2048>(key, s_buf); break;
+    default: bitonic_desc_np<4096>(key, s_buf); break;
+    }
+}
+
+// exclusive prefix sum over one int per thread of a 1024-thread block (wave shuffles, then
+// the 16 wave totals through LDS); `total` = the block's sum.  s_w holds 16 ints.
+__device__ __forceinline__ int block_scan_1024(int v, int *s_w, int &total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int u = __shfl_up(incl, d);
+        if (lane >= d) incl += u;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    int before = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+        const int c = s_w[w];
+        before += w < wave ? c : 0;
+        tot += c;
+    }
+    __syncthreads();
+    total = tot;
+    return before + incl - v;
 }
 
 __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
     __shared__ uint64_t s_key[kSortLds];
     __shared__ float s_x[kSortLds], s_y[kSortLds], s_s[kSortLds];
     __shared__ int s_off[kMaxHeads * PP_MAX_KP + 1];
+    __shared__ int s_scan[16];
+    static_assert(kMaxHeads * PP_MAX_KP < 1024, "one thread per segment");
     const int img = blockIdx.x;
     const int nseg = a.h.n_cif * a.K;
     const int64_t cap = a.cap;
     const float *gv = a.g_keys + (int64_t)img * 4 * cap, *gx = gv + cap, *gy = gx + cap,
                 *gs = gy + cap;
     int *gf = a.g_f + (int64_t)img * cap;
-    if (threadIdx.x == 0) {
-        int o = 0;
-        for (int q = 0; q < nseg; q++) {
-            s_off[q] = o;
-            o += a.f_counts[(int64_t)img * nseg + q];
-        }
-        s_off[nseg] = o;
-        a.counts[img] = o;
+    // segment offsets: every segment's count in one round trip, then a block scan
+    // (s_off[nseg] = the total: counts past nseg are 0)
+    {
+        const int q = threadIdx.x;
+        const int cnt = q < nseg ? a.f_counts[(int64_t)img * nseg + q] : 0;
+        int total;
+        const int pre = block_scan_1024(cnt, s_scan, total);
+        if (q <= nseg) s_off[q] = pre;
+        if (q == 0) a.counts[img] = total;
     }
     __syncthreads();
     const int n = s_off[nseg];
@@ -234,29 +391,35 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
     while (np < n) np <<= 1;
     pp_seed *out = a.seeds + (int64_t)img * cap;
     if (n <= kSortLds) {
-        for (int q = 0; q < nseg; q++) {
-            const int o = s_off[q], c = s_off[q + 1] - o;
-            const int f = q % a.K;
-            const int64_t sb = a.seg_base(q / a.K, f);
-            for (int i = threadIdx.x; i < c; i += blockDim.x) {
-                const int64_t k = sb + i;
-                s_key[o + i] = seed_key(gv[k], f, o + i);
-                s_x[o + i] = gx[k];
-                s_y[o + i] = gy[k];
-                s_s[o + i] = gs[k];
-            }
-        }
-        __syncthreads();
-        // bitonic network, descending, on kSortLds keys held 4 per thread (keys past n are
-        // 0 and sort last): only the stages whose partner lies in another wave go through
-        // LDS (10 of 78); the others exchange in registers / across lanes
+        // thread t gathers seeds 4t .. 4t + 3 (all loads independent: one round trip): its
+        // segment by binary search over the offsets, then the keys straight into registers
         uint64_t key[4];
 #pragma unroll
         for (int e = 0; e < 4; e++) {
             const int i = 4 * (int)threadIdx.x + e;
-            key[e] = i < n ? s_key[i] : 0ull;
+            key[e] = 0ull;  // past n: sorts last
+            if (i < n) {
+                int lo = 0, hi = nseg - 1;  // largest segment with s_off[seg] <= i
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (s_off[mid] <= i)
+                        lo = mid;
+                    else
+                        hi = mid - 1;
+                }
+                const int f = lo % a.K;
+                const int64_t k = a.seg_base(lo / a.K, f) + (i - s_off[lo]);
+                key[e] = seed_key(gv[k], f, i);
+                s_x[i] = gx[k];
+                s_y[i] = gy[k];
+                s_s[i] = gs[k];
+            }
         }
-        bitonic4096_desc(key, s_key);
+        // bitonic network, descending, on the first max(4, np) keys held 4 per thread (keys
+        // past n are 0 and sort last): only the stages whose partner lies in another wave go
+        // through LDS (np > 256; 10 of 78 at 4096); the others exchange in registers / across
+        // lanes
+        bitonic_desc(key, s_key, np < 4 ? 4 : np);
         __syncthreads();
 #pragma unroll
         for (int e = 0; e < 4; e++) s_key[4 * threadIdx.x + e] = key[e];
@@ -877,6 +1040,7 @@ int launch_seeds(const Heads &h, const HrMap &hr, int n_img, int K, const pp_con
     a.K = K;
     a.th = cfg->seed_threshold;
     a.score_scale = cfg->seed_score_scale;
+    a.skip = cfg->seed_skip_mask;
     a.seeds = seeds;
     a.cap = cap;
     a.counts = counts;

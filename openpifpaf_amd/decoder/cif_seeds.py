@@ -78,15 +78,15 @@ class CifDetSeeds(CifSeeds):
         if self.threshold is None:
             raise TypeError("'>' not supported between instances of 'float' and 'NoneType' "
                             "(CifSeeds.threshold is not configured)")
-        if min_scale or seed_mask is not None:
-            raise NotImplementedError('min_scale / seed_mask are not implemented')
+        if min_scale:
+            raise NotImplementedError('min_scale masks of detection heads are not implemented')
         c = batch1(cif)
         _, k, _, h, w = c.shape
         hr = pitched_hr(self.cifhr)
         seg = torch.empty((k, 5, h * w), dtype=torch.float32, device=c.device)
         counts = torch.zeros(k, dtype=torch.int32, device=c.device)
         cfg = make_config(seed_threshold=self.threshold, seed_score_scale=self.score_scale,
-                          stride=int(stride))
+                          stride=int(stride), seed_mask=seed_mask)
         call('pp_cifdet_seeds', _device.ptr(c), _device.ptr(hr), 1, k, h, w, cfg_ptr(cfg),
              _device.ptr(seg), _device.ptr(counts), _device.stream())
         seg, counts = seg.cpu().numpy(), counts.cpu().numpy()

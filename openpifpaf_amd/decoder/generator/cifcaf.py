@@ -89,6 +89,7 @@ class CifCaf(Generator):
             greedy=self.greedy,
             connection_method=self.connection_method,
             apply_nms=nms is not None,
+            seed_mask=self.field_config.seed_mask,
         )
 
     # -- decoding ------------------------------------------------------------------------

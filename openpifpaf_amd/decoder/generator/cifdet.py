@@ -45,7 +45,7 @@ class CifDet(Generator):
         _, _, stride = self.field_config.single_scale()
         return make_config(cif_threshold=CifHr.v_threshold, seed_threshold=CifSeeds.threshold,
                            seed_score_scale=CifSeeds.score_scale, stride=int(stride),
-                           cif_neighbors=CifHr.neighbors)
+                           cif_neighbors=CifHr.neighbors, seed_mask=self.field_config.seed_mask)
 
     def decode_records(self, det_batch, cap=None):
         """det_batch (B, K, 7, H, W) -> (pp_det records, per-image offsets)."""

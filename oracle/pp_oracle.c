@@ -344,6 +344,7 @@ EXPORT long orc_seeds(const float *cif, const float *hr, long hr_pitch, int K, i
     float *tmp = (float *)malloc(sizeof(float) * 6 * (size_t)(K * hw + 1));
     long n = 0;
     for (int f = 0; f < K; f++) {
+        if ((cfg->seed_skip_mask >> f) & 1u) continue; /* cif_seeds.py:28-29 seed_mask */
         const float *p = cif + (size_t)f * 5 * hw;
         const float *t = hr + (size_t)f * hh * hr_pitch;
         for (long c = 0; c < hw; c++) {
@@ -1113,6 +1114,7 @@ EXPORT long orc_seeds_multi(const pp_scale *all, int n_all, int K, const float *
         long hw = (long)cl[m]->H * cl[m]->W;
         float stride = (float)cl[m]->stride;
         for (int f = 0; f < K; f++) {
+            if ((cfg->seed_skip_mask >> f) & 1u) continue; /* cif_seeds.py:28-29 seed_mask */
             const float *p = cl[m]->cif + (size_t)f * 5 * hw;
             const float *t = hr + (size_t)f * hh * ww;
             for (long c = 0; c < hw; c++) {
@@ -1369,6 +1371,7 @@ EXPORT long orc_cifdet_seeds(const float *det, const float *hr, long hr_pitch, i
     float *tmp = (float *)malloc(sizeof(float) * 7 * (size_t)(K * hw + 1));
     long n = 0;
     for (int f = 0; f < K; f++) {
+        if ((cfg->seed_skip_mask >> f) & 1u) continue; /* cif_seeds.py:70-71 seed_mask */
         const float *p = det + (size_t)f * 7 * hw;
         const float *t = hr + (size_t)f * hh * hr_pitch;
         for (long c = 0; c < hw; c++) {

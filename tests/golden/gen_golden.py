@@ -24,6 +24,7 @@ Fixtures:
                        (inputs, output order as input indices, mutated data), per config
   api_initial_<mode>.npz  CifCaf.__call__(fields, initial_annotations) (cifcaf.py:95-98):
                        the initial annotations, the output list and which outputs are them
+  api_seedmask_<mode>.npz  CifCaf with FieldConfig(seed_mask=...) (cif_seeds.py:28-29)
   api_stages.npz       CifSeeds.fill_cif min_scale / seed_mask and two heads, CafScored
                        fill_caf distance masks and two calls, CifHr fill_cif min_scale,
                        fill_multiple over three heads and into an existing map
@@ -623,6 +624,18 @@ def gen_api(op):
         np.savez_compressed(os.path.join(HERE, 'api_initial_%s.npz' % mode), **out)
         print('api initial', mode, len(prev), '->', len(anns), 'init at',
               out['init_index'][out['init_index'] >= 0].tolist())
+
+    # FieldConfig.seed_mask through the whole decode (cif_seeds.py:28-29, 63)
+    mask = [f % 4 != 2 for f in range(17)]
+    for mode in ('eval', 'predict'):
+        configure(decoder, mode, {})
+        cif, caf = synthetic.planted(40, 40, n_people=8, seed=5)
+        anns = CifCaf(FieldConfig(seed_mask=mask), keypoints=kps, skeleton=skel)([cif, caf])
+        out = {'mode': np.array(mode), 'input_sha': np.array(sha(cif, caf)),
+               'seed_mask': np.array(mask)}
+        out.update(ann_arrays(anns, len(skel)))
+        np.savez_compressed(os.path.join(HERE, 'api_seedmask_%s.npz' % mode), **out)
+        print('api seed_mask', mode, len(anns))
 
     configure(decoder, 'eval', {})
     fc = FieldConfig()

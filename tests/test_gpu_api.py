@@ -167,3 +167,17 @@ def test_fill_multiple_pairs_match_fill(dec):
     assert np.asarray(one).tobytes() == np.asarray(step.accumulated).tobytes()
     ref = oracle.cifhr_multi(oracle.Members(fields, **kw))
     assert np.asarray(one).tobytes() == ref.tobytes()
+
+
+@pytest.mark.parametrize('mode', ['eval', 'predict'])
+def test_seed_mask_decode_vs_reference(dec, mode):
+    """CifCaf with FieldConfig(seed_mask=...) (cif_seeds.py:28-29, 63): masked fields seed
+    nothing (pp_config.seed_skip_mask), through the whole device decode."""
+    g = gu.load_api('seedmask_' + mode)
+    cif, caf = gu.synthetic.planted(40, 40, n_people=8, seed=5)
+    gu.configure_decoder(dec, _mode_fixture(mode))
+    cc = dec.CifCaf(dec.FieldConfig(seed_mask=g['seed_mask'].tolist()),
+                    keypoints=gu.constants.COCO_KEYPOINTS, skeleton=SKEL)
+    anns = cc([cif, caf])
+    errs = gu.compare_annotations(g, gu.annotations_as_records(anns))
+    assert not errs, errs[:10]

@@ -314,3 +314,16 @@ def test_oracle_stage_api():
         assert [f.shape[1] for f in fw] == g[tag + '_fwd_counts'].tolist()
         assert [gu.sha(f) for f in fw] == g[tag + '_fwd_sha'].tolist()
         assert [gu.sha(b) for b in bw] == g[tag + '_bwd_sha'].tolist()
+
+
+@pytest.mark.parametrize('mode', ['eval', 'predict'])
+def test_oracle_seed_mask(mode):
+    """FieldConfig(seed_mask=...) through the whole decode (cif_seeds.py:28-29)."""
+    from openpifpaf_amd._abi import EVAL_CONFIG, PREDICT_CONFIG, make_config
+    g = gu.load_api('seedmask_' + mode)
+    cif, caf = gu.synthetic.planted(40, 40, n_people=8, seed=5)
+    assert gu.sha(cif, caf) == str(g['input_sha'])
+    kw = dict(EVAL_CONFIG if mode == 'eval' else PREDICT_CONFIG)
+    cfg = make_config(seed_mask=g['seed_mask'].tolist(), **kw)
+    recs = oracle.decode(cif, caf, gu.constants.COCO_PERSON_SKELETON, cfg)
+    assert gu.compare_annotations(g, recs) == []

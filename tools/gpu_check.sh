@@ -1,0 +1,24 @@
+# One GPU call for an iteration: the -m gpu parity tests, then (if green) the cfg2 kernel
+# profile and the default bench line without the CPU leg.
+# Usage (via gpurun): bash tools/gpu_check.sh <tag> [pytest -k expression]
+set -u
+TAG=${1:-chk}
+K=${2:-}
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+if [ -n "$K" ]; then SEL=(-k "$K"); else SEL=(); fi
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu "${SEL[@]}" --timeout 120 \
+  --timeout-method thread -p no:cacheprovider > gpurun_out/${TAG}_tests.log 2>&1
+rc=$?
+tail -3 gpurun_out/${TAG}_tests.log
+[ $rc -eq 0 ] || exit $rc
+bash tools/gpu_profile_cfg2.sh "$TAG" || exit $?
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-multi > gpurun_out/${TAG}_bench.json \
+  2> gpurun_out/${TAG}_bench.err || exit $?
+python3 - "$TAG" <<'PY'
+import json, sys
+d = json.load(open('gpurun_out/%s_bench.json' % sys.argv[1]))
+print(d['value'], d['ms_per_step'], d['stage_ms'])
+for k in ('uniform', 'cfg2', 'cfg5', 'roofline', 'roofline_uniform'):
+    print(k, d.get(k))
+PY
