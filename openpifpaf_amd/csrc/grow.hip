@@ -1835,7 +1835,9 @@ __global__ __launch_bounds__(64) void complete_kernel(GrowArgs g) {
 // "occupied" iff the number of earlier marked boxes covering its cell is non-zero mod 256
 // (the grid's u8 += 1 wraps), which is exactly what the grid lookup returns.
 constexpr int kNmsWaves = 8;
-constexpr int kNmsBoxLds = 1024;  // boxes per plane kept in LDS (global scratch beyond)
+// boxes per plane kept in LDS (global scratch beyond): 448 keeps the kernel at 29 KB of LDS,
+// so a workgroup fits on a CU beside the seed loop's 103 KB (DecodePipeline overlaps them)
+constexpr int kNmsBoxLds = 448;
 
 struct ScoreLDS {
     double prod[kKP];

@@ -363,9 +363,10 @@ __device__ __forceinline__ int block_scan_1024(int v, int *s_w, int &total) {
     return before + incl - v;
 }
 
+// 33 KB of LDS (keys + segment offsets; x / y / s stay in the emission buffer), so a
+// workgroup fits beside the seed loop's 104 KB on one CU (DecodePipeline overlaps them)
 __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
     __shared__ uint64_t s_key[kSortLds];
-    __shared__ float s_x[kSortLds], s_y[kSortLds], s_s[kSortLds];
     __shared__ int s_off[kMaxHeads * PP_MAX_KP + 1];
     __shared__ int s_scan[16];
     static_assert(kMaxHeads * PP_MAX_KP < 1024, "one thread per segment");
@@ -390,29 +391,29 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
     int np = 1;
     while (np < n) np <<= 1;
     pp_seed *out = a.seeds + (int64_t)img * cap;
+    // emission slot of concatenated seed i: its segment by binary search over the offsets
+    auto slot = [&](int i) {
+        int lo = 0, hi = nseg - 1;  // largest segment with s_off[seg] <= i
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_off[mid] <= i)
+                lo = mid;
+            else
+                hi = mid - 1;
+        }
+        return a.seg_base(lo / a.K, lo % a.K) + (i - s_off[lo]);
+    };
     if (n <= kSortLds) {
-        // thread t gathers seeds 4t .. 4t + 3 (all loads independent: one round trip): its
-        // segment by binary search over the offsets, then the keys straight into registers
+        // thread t gathers seeds 4t .. 4t + 3 (all loads independent: one round trip), the
+        // keys straight into registers
         uint64_t key[4];
 #pragma unroll
         for (int e = 0; e < 4; e++) {
             const int i = 4 * (int)threadIdx.x + e;
             key[e] = 0ull;  // past n: sorts last
             if (i < n) {
-                int lo = 0, hi = nseg - 1;  // largest segment with s_off[seg] <= i
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (s_off[mid] <= i)
-                        lo = mid;
-                    else
-                        hi = mid - 1;
-                }
-                const int f = lo % a.K;
-                const int64_t k = a.seg_base(lo / a.K, f) + (i - s_off[lo]);
-                key[e] = seed_key(gv[k], f, i);
-                s_x[i] = gx[k];
-                s_y[i] = gy[k];
-                s_s[i] = gs[k];
+                const int64_t k = slot(i);
+                key[e] = seed_key(gv[k], gf[k], i);
             }
         }
         // bitonic network, descending, on the first max(4, np) keys held 4 per thread (keys
@@ -434,9 +435,10 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
             while (end < n && (s_key[end] >> 27) == ki) end++;
             auto before = [&](uint64_t p, uint64_t q) {  // p must precede q
                 const int ep = key_emit(p), eq = key_emit(q);
-                if (s_x[ep] != s_x[eq]) return s_x[ep] > s_x[eq];
-                if (s_y[ep] != s_y[eq]) return s_y[ep] > s_y[eq];
-                if (s_s[ep] != s_s[eq]) return s_s[ep] > s_s[eq];
+                const int64_t kp = slot(ep), kq = slot(eq);
+                if (gx[kp] != gx[kq]) return gx[kp] > gx[kq];
+                if (gy[kp] != gy[kq]) return gy[kp] > gy[kq];
+                if (gs[kp] != gs[kq]) return gs[kp] > gs[kq];
                 return ep < eq;
             };
             for (int u = i + 1; u < end; u++) {
@@ -452,13 +454,13 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
         __syncthreads();
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
             const uint64_t k = s_key[i];
-            const int e = key_emit(k);
+            const int64_t e = slot(key_emit(k));
             pp_seed r;
             r.v = __uint_as_float((uint32_t)(k >> 32));
             r.field = (int)((k >> 27) & 31u);
-            r.x = s_x[e];
-            r.y = s_y[e];
-            r.s = s_s[e];
+            r.x = gx[e];
+            r.y = gy[e];
+            r.s = gs[e];
             out[i] = r;
         }
     } else {

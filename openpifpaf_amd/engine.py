@@ -446,8 +446,10 @@ class PendingRecords:
 # PP_PIPE_BFIRST=1 / 0 / lazy forces the force-complete set order of DecodePipeline (auto
 # below); lazy: gated after the seed loop, on the tail stream
 _B_FIRST = {'1': True, '0': False, 'lazy': 'lazy'}.get(os.environ.get('PP_PIPE_BFIRST', ''))
-# auto: sets first once a batch averaged this many annotations per image
-_B_FIRST_DENSITY = 32.0
+# auto: sets first once a batch averaged this many annotations per image.  0: always (round
+# 3, after the seeds kernels shrank: planted 0.838 vs 0.868 ms and 0.845 vs 0.898 ms per
+# step on two boxes; uniform was already sets-first)
+_B_FIRST_DENSITY = 0.0
 
 
 class DecodePipeline:
@@ -466,11 +468,12 @@ class DecodePipeline:
     the streams in use -- current, back, tail, the library's CafScored side stream -- each
     get a hardware queue of their own: HIP shares 4 per process between streams.)
 
-    The force-complete sets go either after set A on the side stream (sparse batches) or
-    first, on the side stream before the CifHr map (dense batches, from the annotations
-    per image of the last batch whose records were read: >= 32; PP_PIPE_BFIRST=1 / 0
-    forces it).  Measured: planted 0.882 vs 0.905-0.930 ms, uniform 18.1 vs 17.3 ms per
-    step.  Either order gives the same records.
+    The force-complete sets go first, on the side stream before the CifHr map (they read
+    only the CAF fields), then set A after them, beside the CifHr map and the seeds on the
+    current stream (PP_PIPE_BFIRST=0 puts them after set A, lazy gates them after the seed
+    loop on the tail stream).  Measured in round 3: planted 0.838 vs 0.868 ms (after set
+    A) vs 0.837 ms (lazy), uniform 18.2-18.9 vs 19.0 vs 19.2 ms per step.  Either order
+    gives the same records.
 
     submit() returns (buffers, PendingRecords of the batch: DecodeEngine.fetch_async).
     The current stream does not wait for the back half; the fields must stay unchanged
