@@ -95,8 +95,22 @@ __device__ __forceinline__ uint32_t pix_key(int x, int y) {
     return (uint32_t)(x & 0xffff) | ((uint32_t)y << 16);
 }
 
-// candidates the fast fold cannot take exactly: div_refined outside its domain
-__device__ __forceinline__ bool cand_slow(float s2) { return !recip_ok(s2); }
+// candidates the fast fold cannot take exactly: div_refined outside its domain, or a
+// non-finite v (v * 0 would not vanish for the pixels the fast term excludes)
+__device__ __forceinline__ bool cand_slow(const FoldCand &c) {
+    return !recip_ok(c.s2) || !(__builtin_fabsf(c.v) < __builtin_inff());
+}
+
+typedef short pp_short2 __attribute__((ext_vector_type(2)));
+
+// box: clamp the packed (x, y) key into [lo, hi] per 16-bit half; unchanged = inside
+__device__ __forceinline__ bool in_box(const FoldCand &c, uint32_t key) {
+    const pp_short2 k2 = __builtin_bit_cast(pp_short2, key);
+    const pp_short2 cl = __builtin_elementwise_min(
+        __builtin_elementwise_max(k2, __builtin_bit_cast(pp_short2, c.lo)),
+        __builtin_bit_cast(pp_short2, c.hi));
+    return __builtin_bit_cast(uint32_t, cl) == key;
+}
 
 __device__ __forceinline__ FoldCand make_cand(int4 b, float4 p) {
     FoldCand c;
@@ -104,11 +118,14 @@ __device__ __forceinline__ FoldCand make_cand(int4 b, float4 p) {
     c.cy = p.y;
     c.v = p.z;
     c.s2 = p.w;
-    c.r = cand_slow(p.w) ? 0.0f : recip_of(p.w).r;
+    c.r = recip_ok(p.w) ? recip_of(p.w).r : 0.0f;
     c.lo = pix_key(b.x, b.z);
     c.hi = pix_key(b.y - 1, b.w - 1);
     const int nx = nearest_coord(p.x), ny = nearest_coord(p.y);
     c.nkey = (nx < 0 || ny < 0) ? ~0u : pix_key(nx, ny);
+    // the fast fold applies q = 0 after the box test: keep nkey only inside the box (the
+    // box is clipped to the map, the nearest pixel may lie past its edge)
+    if (c.nkey != ~0u && !in_box(c, c.nkey)) c.nkey = ~0u;
     return c;
 }
 
@@ -135,46 +152,61 @@ __device__ __forceinline__ uint64_t cand_live(const FoldCand &c, int tx0, int ty
     return live;
 }
 
-typedef short pp_short2 __attribute__((ext_vector_type(2)));
 
 // fold_pixel<M_GAUSS_MAX> (truncate 1, max_value 1; functional.pyx:127-141): the term one
-// candidate adds to this lane's pixel (vv) and whether the pixel takes it
+// candidate adds to this lane's pixel (vv) and whether the pixel takes it (slow path)
 struct FoldTerm {
     float vv;
     bool take;
 };
 
-template <bool SLOW>
-__device__ __forceinline__ FoldTerm fold_term(const FoldCand &c, float fx, float fy,
-                                              uint32_t key) {
+__device__ __forceinline__ FoldTerm fold_term_slow(const FoldCand &c, float fx, float fy,
+                                                   uint32_t key) {
     const float dx = fx - c.cx, dy = fy - c.cy;
     const float dx2 = dx * dx, dy2 = dy * dy;  // powf(d, 2.0)
     const float sum = dx2 + dy2;
     // approx_exp(-0.5 * sum / s2) starts with 1 + x / 8: x = (-0.5 * sum) / s2 is
     // -0.5 * (sum / s2) exactly (scaling by a power of two commutes with rounding; where
     // sum / s2 is subnormal both give 1 + x / 8 = 1), so the -0.5 / 8 goes into the fma
-    float q = SLOW ? sum / c.s2 : div_refined(sum, Recip{c.s2, c.r});
-    // "closest pixel" (vv = v): q = 0 gives t = 1 exactly, so v * t = v; a select on q keeps
-    // the fold branch-free
-    q = (key == c.nkey) ? 0.0f : q;
+    float q = sum / c.s2;
+    q = (key == c.nkey) ? 0.0f : q;  // "closest pixel": q = 0 gives t = 1, v * t = v
     float t = __builtin_fmaf(q, -0.0625f, 1.0f);  // 1 + x / 8 (q * -0.0625 is exact)
     t = t * t;
     t = t * t;
     t = t * t;
-    // box: clamp the packed (x, y) key into [lo, hi] per 16-bit half; unchanged = inside
-    const pp_short2 k2 = __builtin_bit_cast(pp_short2, key);
-    const pp_short2 cl = __builtin_elementwise_min(
-        __builtin_elementwise_max(k2, __builtin_bit_cast(pp_short2, c.lo)),
-        __builtin_bit_cast(pp_short2, c.hi));
     FoldTerm f;
     f.vv = c.v * t;
-    f.take = !(sum > c.s2) & (__builtin_bit_cast(uint32_t, cl) == key);
+    f.take = !(sum > c.s2) & in_box(c, key);
     return f;
 }
 
 __device__ __forceinline__ float fold_apply(float acc, const FoldTerm &f) {
     const float a = acc + f.vv;
     return f.take ? ((a < 1.0f) ? a : 1.0f) : acc;  // min(max_value, f)
+}
+
+// The fast term (s2 in div_refined's domain, v finite): a pixel outside the box or the
+// circle gets q = 16, so t = (1 - 16 / 16)^8 = 0 and vv = v * 0 = +0, and the update
+// min(acc + vv, 1) leaves it as it was (acc in [0, 1]).  The closest pixel lies inside both
+// (sum < 0.5 <= sigma^2, sigma >= 1), so its q = 0 is applied last.  Every pixel then takes
+// the same update, with the two tests as selects on q (vector compares + cndmask: no
+// scalar mask arithmetic).
+__device__ __forceinline__ float fold_vv(const FoldCand &c, float fx, float fy, uint32_t key) {
+    const float dx = fx - c.cx, dy = fy - c.cy;
+    const float sum = dx * dx + dy * dy;
+    float q = div_refined(sum, Recip{c.s2, c.r});
+    q = in_box(c, key) ? q : 16.0f;
+    q = (sum > c.s2) ? 16.0f : q;
+    q = (key == c.nkey) ? 0.0f : q;
+    float t = __builtin_fmaf(q, -0.0625f, 1.0f);
+    t = t * t;
+    t = t * t;
+    t = t * t;
+    return c.v * t;
+}
+
+__device__ __forceinline__ float fold_add(float acc, float vv) {
+    return __builtin_fminf(acc + vv, 1.0f);  // (a < 1) ? a : 1; a NaN gives 1 either way
 }
 
 // Folds the candidates `q` (bits, ascending) of FoldCand array `cand` into this lane's
@@ -184,8 +216,10 @@ __device__ __forceinline__ float fold_block(float acc, const FoldCand *cand, uin
     if (q & slow) {
         for (; q; q &= q - 1) {
             const int c = __builtin_ctzll(q);
-            acc = fold_apply(acc, ((slow >> c) & 1ull) ? fold_term<true>(cand[c], fx, fy, key)
-                                                       : fold_term<false>(cand[c], fx, fy, key));
+            if ((slow >> c) & 1ull)
+                acc = fold_apply(acc, fold_term_slow(cand[c], fx, fy, key));
+            else
+                acc = fold_add(acc, fold_vv(cand[c], fx, fy, key));
         }
         return acc;
     }
@@ -193,14 +227,14 @@ __device__ __forceinline__ float fold_block(float acc, const FoldCand *cand, uin
     const int np = __popcll(q);
     for (int i = 1; i < np; i += 2) {
         const int c1 = __builtin_ctzll(q);
-        q &= ~(1ull << c1);  // one s_bitset0 (q &= q - 1 takes three scalar ops)
+        q &= ~(1ull << c1);
         const int c2 = __builtin_ctzll(q);
         q &= ~(1ull << c2);
-        const FoldTerm f1 = fold_term<false>(cand[c1], fx, fy, key);
-        const FoldTerm f2 = fold_term<false>(cand[c2], fx, fy, key);
-        acc = fold_apply(fold_apply(acc, f1), f2);
+        const float v1 = fold_vv(cand[c1], fx, fy, key);
+        const float v2 = fold_vv(cand[c2], fx, fy, key);
+        acc = fold_add(fold_add(acc, v1), v2);
     }
-    if (np & 1) acc = fold_apply(acc, fold_term<false>(cand[__builtin_ctzll(q)], fx, fy, key));
+    if (np & 1) acc = fold_add(acc, fold_vv(cand[__builtin_ctzll(q)], fx, fy, key));
     return acc;
 }
 
@@ -710,7 +744,7 @@ __global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
                 bool slow_l = false;
                 if (lane < n) {
                     cl = (cand_live(cand[lane], tx0, ty0) >> (16 * wave)) & 0xFFFFull;
-                    slow_l = cand_slow(cand[lane].s2);
+                    slow_l = cand_slow(cand[lane]);
                 }
                 const uint64_t slow = __ballot(slow_l);
                 const uint64_t lv = wave_or64(cl, &s_live[wave]);
@@ -1054,7 +1088,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
             bool slow_l = false;
             if (lane < n) {
                 cl = cand_live(cand[lane], tx0, ty0);
-                slow_l = cand_slow(cand[lane].s2);
+                slow_l = cand_slow(cand[lane]);
             }
             const uint64_t slow = __ballot(slow_l);
             const uint64_t live = wave_or64(cl, &s_live[wave]);
@@ -1090,10 +1124,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
                         acc = fold_block(acc, cand, 1ull << c, slow, fx, fy, key);
                     }
                 }
+                // nontemporal: the map is read by later kernels only, and streaming it past
+                // L2 keeps the row bins the next tiles scan resident there
                 if (!MULTI) {
-                    mp[blk * 64 + lane] = acc;
+                    __builtin_nontemporal_store(acc, &mp[blk * 64 + lane]);
                 } else if (last) {
-                    mp[blk * 64 + lane] = nan_max(acc, res);
+                    __builtin_nontemporal_store(nan_max(acc, res), &mp[blk * 64 + lane]);
                 } else {
                     mp[blk * 64 + lane] = res;
                     ap[blk * 64 + lane] = acc;
