@@ -87,6 +87,8 @@ struct OccLog {
     int16_t x0, x1, y0, y1;
 };
 
+struct SeedExt;  // the seed loop's external-helper words (below)
+
 struct GrowArgs {
     const pp_seed *seeds;
     const int *seed_counts;
@@ -119,6 +121,9 @@ struct GrowArgs {
     pp_ann *work;             // working annotations
     pp_ann *spec;             // (n_img, kSpecCache) speculatively grown annotations
     float spec_far;           // seed-loop speculation distance, in joint scales
+    int n_ext;                // external helper workgroups per image (seed loop)
+    SeedExt *xext;            // (n_img) their hand-off words (zeroed before each launch)
+    pp_ann *xrec;             // (n_img, kExtCache) their published annotations
     double *nms_score;        // (n_img, 2 * ann_cap)
     int *nms_idx;             // (n_img, 4 * ann_cap + ann_np)
     float *nms_f;             // (n_img, 2 * ann_cap) per-annotation max x, max y
@@ -826,7 +831,7 @@ __device__ __forceinline__ void flat_load(const float *__restrict__ cf, int64_t 
 // that fits kColLds floats, in (CAF, direction) order, column-major (kColPad floats per
 // column: two 16-byte reads).  cofs[q] = its offset, -1 = global.
 constexpr int kColPad = 8;
-constexpr int kColLds = 20480;  // 80 KB (40 KB: same speed)
+constexpr int kColLds = 20480;  // 80 KB (64 KB: 1-2% slower per planted cfg3 step)
 struct ColStage {
     const int *ncol;   // set-A column counts per (CAF, direction)
     const int *cofs;
@@ -1443,22 +1448,132 @@ __device__ void sort_by_score(int *perm, int np, int n, const double *score) {
 // is still growing it.  The handshake is LDS flags with workgroup-scope acquire/release.
 // 8 waves; 16 (cache 32, scan 256): 1.79 vs 1.28 ms per cfg3 step; 4 / 6: no better
 constexpr int kSeedWaves = 8;
-constexpr int kSpecCache = 16;     // speculative annotations kept per image
+constexpr int kSpecCache = 16;     // speculative annotations of this CU's helpers
 constexpr int kSpecScan = 128;     // seeds after the committed one examined per round
 // distance (joint scales) a helper's seed keeps from the committed one and from the
 // round's other picks; cached annotations are excluded by their exact occupancy boxes.
 // Throughput is flat for 0-4 (both generators) and drops beyond 8.
 constexpr float kSpecFar = 4.0f;
 
-struct SeedLoopShared {
+// External helpers.  A batch of fewer images than CUs leaves CUs without a seed loop, so
+// each image may get n_ext (<= kExtWgMax) more workgroups whose waves are all helpers.
+// They take seeds from wave 0 through per-image global words (SeedExt) and publish into
+// kExtCache more cache slots, whose records live in global memory, across CUs and XCDs
+// with the agent-scope publish / consume form of cdna_hip_programming.md Guideline 16: the
+// record is stored write-through (sc1) and drained (s_waitcnt vmcnt(0)) before one lane
+// stores the slot's tag (seed + 1); wave 0 polls tags relaxed and reads records and joints
+// with sc1 loads.  A helper announces itself (task word 1 = idle) before wave 0 may hand
+// it a seed (CAS 1 -> assigned), so a workgroup that is not resident never holds one; an
+// idle helper leaves when wave 0 finishes (fin) or after kExtIdleTicks without work (CAS
+// 1 -> 3; losing that CAS to an assignment means: grow it).  Every polled word is zeroed
+// by a memset before each launch.
+constexpr int kExtWgMax = 3;
+constexpr int kExtHelpers = kExtWgMax * kSeedWaves;
+constexpr int kExtCache = 32;
+constexpr int kCacheSlots = kSpecCache + kExtCache;  // one lane per slot
+static_assert(kCacheSlots <= 64 && kSeedWaves + kExtHelpers <= 64, "one lane per slot / helper");
+// Policy (s_memrealtime ticks, 100 MHz).  Wave 0 waits for an external slot it needs next
+// only if that grow is at least half done by the running mean of external grows (at most
+// 2 s: a helper always finishes); otherwise it grows the seed itself and the slot is a
+// zombie (state 4) until its tag arrives.  An idle helper leaves after 300 us, so that on
+// images with few annotations its CU goes back to the other stages' kernels; once an image
+// has kExtHeavyAnns annotations wave 0 flags it heavy (SeedExt.heavy) and helpers stay up
+// to 1 s idle.  cfg5 (64 images, 160x160; 16 / 1370 annotations per image), images/s,
+// planted / uniform: no helpers 26.4k / 795; this 27.7k / 969; helpers that stay 1 ms idle
+// 22.7k / 1024; wave 0 always waiting 22.5k / 1027; also handing out seeds after every 4th
+// cached commit 21.7k / 986; a 100 us light idle and no wait before 32 annotations 27.0k / 907.
+constexpr int kExtHeavyAnns = 8;
+constexpr uint64_t kExtIdleLight = 30000ull, kExtIdleHeavy = 100000000ull;
+constexpr uint64_t kExtWaitMax = 200000000ull;
+
+struct SeedExt {  // per image; zeroed before every launch that has external helpers
+    unsigned long long task[kExtHelpers];  // 0 absent, 1 idle, 3 left; assigned: 2 |
+                                           // slot << 8 | seed << 32
+    unsigned int tag[kExtCache];           // seed + 1 of the record published in the slot
+    unsigned int fin;                      // wave 0 is done
+    unsigned int heavy;                    // wave 0 switched to the heavy regime
+    unsigned int pad[2];
+};
+static_assert(sizeof(SeedExt) % 16 == 0, "memset block of whole 16-byte units");
+
+typedef __attribute__((address_space(1))) unsigned int gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+__device__ __forceinline__ unsigned int ld_agent(const unsigned int *p) {
+    return __hip_atomic_load((gu32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_agent(const unsigned long long *p) {
+    return __hip_atomic_load((gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(unsigned int *p, unsigned int v) {
+    __hip_atomic_store((gu32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_store((gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool cas_agent(unsigned long long *p, unsigned long long expect,
+                                          unsigned long long v) {
+    return __hip_atomic_compare_exchange_strong((gu64 *)p, &expect, v, __ATOMIC_RELAXED,
+                                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// lane 0's CAS, its result on every lane
+__device__ __forceinline__ bool cas_agent_wave(unsigned long long *p, unsigned long long expect,
+                                               unsigned long long v) {
+    int ok = 0;
+    if ((threadIdx.x & 63) == 0) ok = cas_agent(p, expect, v) ? 1 : 0;
+    return __builtin_amdgcn_readfirstlane(ok) != 0;
+}
+
+// an LDS record to global memory, write-through (sc1), drained
+__device__ __forceinline__ void publish_ann(pp_ann *dst, const pp_ann *src) {
+    const unsigned long long *s = reinterpret_cast<const unsigned long long *>(src);
+    unsigned long long *d = reinterpret_cast<unsigned long long *>(dst);
+    constexpr int nw = sizeof(pp_ann) / 8;
+    for (int t = threadIdx.x & 63; t < nw; t += 64) st_agent(d + t, s[t]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// copy_ann from another CU's published record (sc1 loads)
+__device__ __forceinline__ void copy_ann_agent(pp_ann *dst, const pp_ann *src) {
+    const unsigned long long *s = reinterpret_cast<const unsigned long long *>(src);
+    unsigned long long *d = reinterpret_cast<unsigned long long *>(dst);
+    constexpr int nw = sizeof(pp_ann) / 8;
+    constexpr int per = (nw + 63) / 64;
+    const int lane = threadIdx.x & 63;
+    unsigned long long v[per];
+#pragma unroll
+    for (int u = 0; u < per; u++) v[u] = (u * 64 + lane < nw) ? ld_agent(s + u * 64 + lane) : 0ull;
+#pragma unroll
+    for (int u = 0; u < per; u++)
+        if (u * 64 + lane < nw) d[u * 64 + lane] = v[u];
+    wave_sync();
+}
+
+template <int NSLOT>
+struct SeedLoopSharedT {
     int task[kSeedWaves];          // seed a helper is to grow (-1 idle), set by wave 0
     int task_slot[kSeedWaves];     // cache slot its annotation goes to
-    int cache_seed[kSpecCache];    // seed index held by a cache slot (< current: dead)
-    float cache_x[kSpecCache], cache_y[kSpecCache], cache_s[kSpecCache];  // seed position
-    int cache_state[kSpecCache];   // 0 free, 1 being grown, 2 grown (joints below valid)
-    float4 cache_j[kSpecCache][kKP];  // its joints (x, y, v, scale)
+    int cache_seed[NSLOT];         // seed index held by a cache slot (< current: dead)
+    float cache_x[NSLOT], cache_y[NSLOT], cache_s[NSLOT];  // seed position
+    // 0 free, 1 being grown, 2 grown (joints below valid), 4 zombie (external slot whose
+    // seed wave 0 grew itself; free once its tag arrives); external slots' 1 -> 2 and
+    // 4 -> 0 are wave 0's, on seeing the slot's tag
+    int cache_state[NSLOT];
+    float4 cache_j[kSpecCache][kKP];  // its joints (x, y, v, scale); the external slots'
+                                      // after the column stage in dynamic LDS (cache_joints)
     int done;
 };
+using SeedLoopShared = SeedLoopSharedT<kSpecCache>;
+struct SeedLoopSharedX : SeedLoopSharedT<kCacheSlots> {
+    uint32_t cache_t[kCacheSlots];  // external slots: s_memrealtime (low bits) at hand-over
+    uint32_t ext_ticks;             // running mean of hand-over -> tag seen (0: none yet)
+};
+
+// joints of cache slot q (LDS): this CU's slots in SeedLoopShared, the external ones in the
+// dynamic LDS after the kColLds column floats (launched only when n_ext > 0)
+__device__ __forceinline__ float4 *cache_joints(SeedLoopSharedX &S, float *s_cols, int q) {
+    return q < kSpecCache ? S.cache_j[q]
+                          : reinterpret_cast<float4 *>(s_cols + kColLds) + (q - kSpecCache) * kKP;
+}
 
 __device__ __forceinline__ int lds_acquire(int *p) {
     return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1491,10 +1606,55 @@ __device__ __forceinline__ void ann_from_seed(LDS &L, const pp_seed &sd, int K, 
     wave_sync();
 }
 
+// wave 0: external slots being grown whose tag has arrived become grown (joints into LDS);
+// `only` >= 0 restricts the check to that slot
+__device__ __forceinline__ void ext_refresh(SeedLoopSharedX &S, float *s_cols, const SeedExt *X,
+                                            const pp_ann *xrec, int only) {
+    const int lane = threadIdx.x & 63;
+    const int q = kSpecCache + lane;
+    bool ready = false;
+    const int st = lane < kExtCache ? S.cache_state[q] : 0;
+    if (lane < kExtCache && (only < 0 || only == q) && (st == 1 || st == 4))
+        ready = ld_agent(&X->tag[lane]) == (unsigned int)S.cache_seed[q] + 1u;
+    if (ready && st == 4) {  // the zombie's helper is done: free
+        S.cache_state[q] = 0;
+        ready = false;
+    }
+    wave_sync();
+    const uint64_t rm = __ballot(ready);
+    if (rm) {
+        const uint32_t now = (uint32_t)__builtin_amdgcn_s_memrealtime();
+        const uint32_t dur = ready ? now - S.cache_t[q] : 0u;
+        uint32_t mt = S.ext_ticks;
+        for (uint64_t b = rm; b; b &= b - 1) {
+            const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)dur, __ffsll((unsigned long long)b) - 1);
+            mt = mt ? 3u * (mt >> 2) + (d >> 2) : d;
+        }
+        wave_sync();
+        if (lane == 0) S.ext_ticks = mt;
+    }
+    for (uint64_t m = rm; m; m &= m - 1) {
+        const int e = __ffsll((unsigned long long)m) - 1;
+        const pp_ann *r = xrec + e;
+        if (lane < kKP) {
+            const unsigned int *d = reinterpret_cast<const unsigned int *>(&r->data[lane][0]);
+            cache_joints(S, s_cols, kSpecCache + e)[lane] = make_float4(
+                __uint_as_float(ld_agent(d)), __uint_as_float(ld_agent(d + 1)),
+                __uint_as_float(ld_agent(d + 2)),
+                __uint_as_float(ld_agent(reinterpret_cast<const unsigned int *>(&r->joint_scales[lane]))));
+        }
+        wave_sync();
+        if (lane == 0) S.cache_state[kSpecCache + e] = 2;
+        wave_sync();
+    }
+}
+
 // <= 168 VGPRs (3 waves per SIMD; a few spills) and the column stage in dynamic LDS: the
 // image's workgroup leaves room on its CU for the next batch's CifHr / seeds / CafScored
 // workgroups (DecodePipeline).  Planted 1.031 -> 1.013 ms, uniform 21.7 -> 20.4 ms per
 // overlapped step; 4 waves per SIMD (128 VGPRs, 532 spills): 1.37 ms.
+// Grid: n_img image workgroups, then n_ext * n_img external helper workgroups (helper
+// workgroup x of image i is block n_img * (1 + x) + i, on image i's XCD when n_img % 8 == 0).
 __global__ __launch_bounds__(64 * kSeedWaves) __attribute__((amdgpu_waves_per_eu(3)))
 void seed_loop_kernel(GrowArgs g) {
     __shared__ SeedLDS Ls[kSeedWaves];
@@ -1753,6 +1913,401 @@ void seed_loop_kernel(GrowArgs g) {
         if (lane == 0) lds_release(&S.done, 1);
     }
     __syncthreads();  // helpers drained: no wave is still growing into the cache
+    if (wave == 0) {
+        occ_clear(g, L, log, occ);
+        STAMP(5);
+#ifdef PP_STAMPS
+        st_acc[6] = n_rounds;
+        st_acc[7] = n_hits;
+#endif
+        STAMP_FLUSH(1);
+        if (lane == 0) {
+            int st = 0;
+            for (int w = 0; w < kSeedWaves; w++) st |= Ls[w].status;
+            g.n_work[img] = n_anns;
+            g.need_complete[img] = g.cfg.force_complete ? (int)unset_mask : 0;
+            g.status[img] = st;
+        }
+    }
+}
+
+
+// The same loop with external helpers (n_ext > 0).  A separate kernel: the big-batch one
+// above carries none of the hand-off state, whose registers cost it 4% per planted cfg3
+// step when merged into it (spills inside the grow).
+__global__ __launch_bounds__(64 * kSeedWaves) __attribute__((amdgpu_waves_per_eu(3)))
+void seed_loop_ext_kernel(GrowArgs g) {
+    constexpr int NS = kCacheSlots;
+    __shared__ SeedLDS Ls[kSeedWaves];
+    __shared__ SeedLoopSharedX S;
+    __shared__ int s_ncol[2 * PP_MAX_EDGES];  // set-A column counts per (CAF, direction)
+    __shared__ int s_cofs[2 * PP_MAX_EDGES];  // their LDS offsets in s_cols (-1: global)
+    // kColLds floats (dynamic: the launch sizes it), then with n_ext > 0 the external
+    // slots' joints (cache_joints)
+    extern __shared__ float s_cols[];
+    const int n_img = (int)gridDim.x / (1 + g.n_ext);
+    const bool external = (int)blockIdx.x >= n_img;
+    const int img = (int)blockIdx.x % n_img;
+    const int K = g.K;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    SeedLDS &L = Ls[wave];
+    for (int q = threadIdx.x; q < 2 * g.C; q += blockDim.x) s_ncol[q] = col_offs(g, 0, img, q >> 1, q & 1)[g.nb];
+    __syncthreads();
+    if (threadIdx.x == 0) {  // LDS placement of the small sets, in order while they fit
+        int o = 0;
+        for (int q = 0; q < 2 * g.C; q++) {
+            const int sz = kColPad * s_ncol[q];
+            const bool fit = s_ncol[q] <= kFlatCols && o + sz <= kColLds;
+            s_cofs[q] = fit ? o : -1;
+            o += fit ? sz : 0;
+        }
+    }
+    __syncthreads();
+    for (int q = wave; q < 2 * g.C; q += kSeedWaves) {  // one set per wave
+        const int n = s_ncol[q];
+        if (s_cofs[q] < 0 || n == 0) continue;
+        const float *cf = col_set(g, 0, img, q >> 1, q & 1);
+        float *dst = s_cols + s_cofs[q];
+        for (int k = lane; k < n; k += 64) {
+            float c[kColRows];
+#pragma unroll
+            for (int r = 0; r < kColRows; r++) c[r] = cf[r * g.col_cap + k];
+            float4 *o = reinterpret_cast<float4 *>(dst + k * kColPad);
+            o[0] = make_float4(c[0], c[1], c[2], c[3]);
+            o[1] = make_float4(c[4], c[5], c[6], 0.0f);
+        }
+    }
+    const ColStage cstage{s_ncol, s_cofs, s_cols};
+    if (lane == 0) {
+        L.status = 0;
+        L.log_n = 0;
+#ifdef PP_STAMPS
+        for (int q = 0; q < 8; q++) L.fst[q] = 0;
+#endif
+    }
+    if (threadIdx.x < NS) {
+        S.cache_seed[threadIdx.x] = -1;
+        S.cache_state[threadIdx.x] = 0;
+    }
+    if (threadIdx.x < kSeedWaves) S.task[threadIdx.x] = -1;
+    if (threadIdx.x == 0) {
+        S.done = 0;
+        S.ext_ticks = 0u;
+    }
+    __syncthreads();
+
+    const int n_seeds = min(g.seed_counts[img], g.seed_cap);
+    bool heavy = false;  // wave 0's regime (see kExtHeavyAnns)
+    const pp_seed *seeds = g.seeds + (int64_t)img * g.seed_cap;
+    SeedExt *X = g.xext + img;
+    pp_ann *xrec = g.xrec + (int64_t)img * kExtCache;
+
+    STAMP_DECL
+    uint8_t *occ_base = g.occ + (int64_t)img * g.occ_cap;
+    OccLog *log = g.log + (int64_t)img * g.log_cap;
+    pp_ann *work = g.work + (int64_t)img * g.ann_cap;
+    pp_ann *cache = g.spec + (int64_t)img * kSpecCache;
+    const float red = (float)g.cfg.occupancy_reduction;
+    const OccGrid occ = occ_grid(occ_base, K, (int)((double)g.hh / g.cfg.occupancy_reduction),
+                                 (int)((double)g.ww / g.cfg.occupancy_reduction));
+    const int n_help = kSeedWaves + (X ? g.n_ext * kSeedWaves : 0);  // helper lanes 1 .. n_help-1
+
+    // committer state (wave 0)
+    int n_anns = 0, s = 0;
+    uint32_t unset_mask = 0;
+#ifdef PP_STAMPS
+    int n_rounds = 0, n_hits = 0;
+#endif
+
+    // append one finished annotation and mark_occupied (cifcaf.py:87-93): wave 0 only
+    // (lane j < K holds joint j of the record: x, y, v, scale, from LDS)
+    auto commit = [&](const pp_ann *src, bool other_cu, float jx, float jy, float jv, float js) {
+        if (other_cu)
+            copy_ann_agent(&work[n_anns], src);
+        else
+            copy_ann(&work[n_anns], src);
+        n_anns++;
+        const uint32_t set = (uint32_t)__ballot(lane < K && jv > 0.0f);
+        unset_mask |= ~set & (K >= 32 ? 0xFFFFFFFFu : ((1u << K) - 1u));
+        occ_mark(g, L, log, occ, jx, jy, js, jv != 0.0f, K);
+    };
+
+    if (external || wave > 0) {
+        // helper: grow the seeds wave 0 hands over until it is done.  This CU's helpers
+        // take them from LDS words and publish into LDS-flagged slots; external ones poll
+        // their global word and publish write-through (see SeedExt)
+        unsigned long long *tw =
+            external ? &X->task[((int)blockIdx.x / n_img - 1) * kSeedWaves + wave] : nullptr;
+        if (external && lane == 0) st_agent(tw, 1ull);
+        uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            int my = -1, q = 0;
+            if (!external) {
+                for (;;) {
+                    my = lds_acquire(&S.task[wave]);
+                    if (my >= 0 || lds_acquire(&S.done)) break;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (my < 0) break;
+                q = S.task_slot[wave];
+            } else {
+                const unsigned long long v = ld_agent(tw);
+                if ((v & 0xFFull) != 2ull) {
+                    const bool quit = ld_agent(&X->fin) != 0u ||
+                                      __builtin_amdgcn_s_memrealtime() - t0 >
+                                          (ld_agent(&X->heavy) ? kExtIdleHeavy : kExtIdleLight);
+                    if (quit && cas_agent_wave(tw, 1ull, 3ull)) break;
+                    __builtin_amdgcn_s_sleep(2);
+                    continue;
+                }
+                q = (int)((v >> 8) & 0xFFFFull);
+                my = (int)(v >> 32);
+            }
+            ann_from_seed(L, seeds[my], K, img);
+            grow<true>(g, L, img, 0, true, cstage);
+            if (external) {
+                publish_ann(&xrec[q], &L.a);
+                if (lane == 0) {
+                    st_agent(&X->tag[q], (unsigned int)my + 1u);
+                    st_agent(tw, 1ull);
+                }
+                wave_sync();
+                t0 = __builtin_amdgcn_s_memrealtime();
+                continue;
+            }
+            copy_ann(&cache[q], &L.a);
+            if (lane < kKP)
+                S.cache_j[q][lane] = make_float4(L.a.data[lane][0], L.a.data[lane][1],
+                                                 L.a.data[lane][2], L.a.joint_scales[lane]);
+            // the record's global stores complete before the flag (the workgroup-scope
+            // release alone does not wait for them)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            wave_sync();
+            if (lane == 0) {
+                lds_release(&S.cache_state[q], 2);
+                lds_release(&S.task[wave], -1);
+            }
+            wave_sync();
+        }
+        if (external) return;
+    } else {
+        __builtin_amdgcn_s_setprio(3);  // the committer is the critical path: issue first
+        // initial annotations (cifcaf.py:95-98): each is grown with set A and reverse
+        // matching from all its set joints (its decoding / frontier orders are appended to),
+        // appended and marked occupied, in order, before any seed is looked at
+        const int n_init = g.init ? min(g.init_counts[img], g.init_cap) : 0;
+        for (int i = 0; i < n_init; i++) {
+            if (n_anns >= g.ann_cap) {
+                if (lane == 0) L.status |= PP_ST_ANN_OVERFLOW;
+                break;
+            }
+            copy_ann(&L.a, &g.init[(int64_t)img * g.init_cap + i]);
+            if (lane == 0) {
+                L.a.image = img;
+                L.a.n_keypoints = K;
+            }
+            wave_sync();
+            grow<true>(g, L, img, 0, true, cstage);
+            commit(&L.a, false, lane < K ? L.a.data[lane][0] : 0.0f,
+                   lane < K ? L.a.data[lane][1] : 0.0f, lane < K ? L.a.data[lane][2] : 0.0f,
+                   lane < K ? L.a.joint_scales[lane] : 0.0f);
+        }
+        for (;;) {
+            // the next free seed (cifcaf.py:100-104): 64 occupancy tests per step
+            int t = -1;
+            while (s < n_seeds) {
+                const int idx = s + lane;
+                bool is_free = false;
+                if (idx < n_seeds) {
+                    const pp_seed c = seeds[idx];
+                    is_free = !occ_get(occ, c.field, c.x, c.y, red);
+                }
+                const uint64_t m = __ballot(is_free);
+                if (m == 0) {
+                    s += 64;
+                    continue;
+                }
+                t = s + __ffsll((unsigned long long)m) - 1;
+                break;
+            }
+            STAMP(0);
+            if (t < 0 || n_anns >= g.ann_cap) {
+                if (lane == 0 && t >= 0) L.status |= PP_ST_ANN_OVERFLOW;
+                break;
+            }
+            if (!heavy && n_anns >= kExtHeavyAnns) {  // helpers stay (kExtIdleHeavy)
+                heavy = true;
+                if (lane == 0) st_agent(&X->heavy, 1u);
+            }
+            const int cs = lane < NS ? S.cache_seed[lane] : -1;
+            const int cst0 = lane < NS ? S.cache_state[lane] : 0;
+            const uint64_t hit = __ballot(lane < NS && cs == t && cst0 != 4);
+            bool taken = false;
+            int hslot = -1;
+            if (hit) {  // a helper grew it, or is growing it
+                const int slot = __ffsll((unsigned long long)hit) - 1;
+                if (slot < kSpecCache) {
+                    while (lds_acquire(&S.cache_state[slot]) != 2) __builtin_amdgcn_s_sleep(1);
+                } else {
+                    // another CU's: wait for its tag (bounded; a helper always finishes), or
+                    // on a light image grow the seed here and leave the slot a zombie
+                    const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
+                    const uint32_t el = (uint32_t)w0 - S.cache_t[slot];
+                    const uint64_t limit =
+                        (S.ext_ticks == 0u || el >= S.ext_ticks / 2u) ? kExtWaitMax : 0ull;
+                    for (;;) {
+                        ext_refresh(S, s_cols, X, xrec, slot);
+                        if (S.cache_state[slot] == 2) break;
+                        if (__builtin_amdgcn_s_memrealtime() - w0 >= limit) {
+                            if (lane == 0) S.cache_state[slot] = 4;  // grow it here instead
+                            wave_sync();
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(2);
+                    }
+                }
+                taken = S.cache_state[slot] == 2;
+                hslot = slot;
+            }
+            if (taken) {
+                const float4 jq = lane < kKP ? cache_joints(S, s_cols, hslot)[lane]
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+                if (hslot < kSpecCache)
+                    commit(&cache[hslot], false, jq.x, jq.y, jq.z, jq.w);
+                else
+                    commit(&xrec[hslot - kSpecCache], true, jq.x, jq.y, jq.z, jq.w);
+                s = t + 1;
+#ifdef PP_STAMPS
+                n_hits++;
+#endif
+                STAMP(4);
+                continue;
+            }
+            // a miss: hand far-away free seeds to the idle helpers, then grow t here
+            const pp_seed st = seeds[t];
+            ext_refresh(S, s_cols, X, xrec, -1);
+            int tk = 0;
+            if (lane > 0 && lane < kSeedWaves)
+                tk = lds_acquire(&S.task[lane]) < 0 ? 1 : 0;
+            else if (lane >= kSeedWaves && lane < n_help)
+                tk = ld_agent(&X->task[lane - kSeedWaves]) == 1ull ? 1 : 0;
+            uint64_t idle = __ballot(tk != 0);
+            // the seeds in flight: later picks keep kSpecFar from them
+            const int cst = lane < NS ? lds_acquire(&S.cache_state[lane]) : 0;
+            uint64_t fly = __ballot(lane < NS && cst == 1);
+            const int scan_end = min(n_seeds, t + 1 + kSpecScan);
+            // the slots holding seeds after t (the others are free or passed)
+            const int csd = lane < NS ? S.cache_seed[lane] : -1;
+            uint64_t ahead = __ballot(lane < NS && csd > t);
+            for (int base = t + 1; base < scan_end && idle; base += 64) {
+                const int idx = base + lane;
+                bool ok = idx < scan_end;
+                pp_seed c{};
+                if (ok) {
+                    c = seeds[idx];
+                    ok = spec_far(g.spec_far, c.x, c.y, c.s, st.x, st.y, st.s) &&
+                         !occ_get(occ, c.field, c.x, c.y, red);
+                }
+                // cache entries (uniform loop): skip seeds they hold, seeds that a grown
+                // annotation's occupancy boxes will cover once committed, and seeds near
+                // one still being grown
+                const int cxi = (int)clip_ref(c.x / red, 0.0f, (float)(occ.w - 1));
+                const int cyi = (int)clip_ref(c.y / red, 0.0f, (float)(occ.h - 1));
+                for (uint64_t aq = ahead; aq; aq &= aq - 1) {
+                    const int q = __ffsll((unsigned long long)aq) - 1;
+                    const int sq = S.cache_seed[q];
+                    if (sq == idx) ok = false;
+                    if (!ok) continue;
+                    if ((fly >> q) & 1) {
+                        ok = spec_far(g.spec_far, c.x, c.y, c.s, S.cache_x[q], S.cache_y[q],
+                                      S.cache_s[q]);
+                        continue;
+                    }
+                    if (S.cache_state[q] != 2) continue;
+                    const float4 jq = cache_joints(S, s_cols, q)[c.field];
+                    int box[4];
+                    if (jq.z != 0.0f && occ_box(g, occ, c.field, jq.x, jq.y, jq.w, box) &&
+                        cxi >= box[0] && cxi < box[1] && cyi >= box[2] && cyi < box[3])
+                        ok = false;
+                }
+                uint64_t m = __ballot(ok);
+                while (m && idle) {
+                    const int l = __ffsll((unsigned long long)m) - 1;
+                    m &= m - 1;
+                    const float cx = rl_f(c.x, l), cy = rl_f(c.y, l), csc = rl_f(c.s, l);
+                    bool far = true;  // from this plan's earlier picks (now in flight too)
+                    uint64_t f2 = fly;
+                    while (f2) {
+                        const int q = __ffsll((unsigned long long)f2) - 1;
+                        f2 &= f2 - 1;
+                        far = far && spec_far(g.spec_far, cx, cy, csc, S.cache_x[q],
+                                              S.cache_y[q], S.cache_s[q]);
+                    }
+                    if (!far) continue;
+                    // a free slot of the helper's kind (this CU's: 0 .. kSpecCache-1; the
+                    // external ones after): never grown into, or grown for a seed passed
+                    const int cq = lane < NS ? S.cache_seed[lane] : 0;
+                    const int cst2 = lane < NS ? S.cache_state[lane] : 1;
+                    const uint64_t freeq = __ballot(lane < NS &&
+                                                    (cst2 == 0 || (cst2 == 2 && cq < t)));
+                    const uint64_t free_l = freeq & ((1ull << kSpecCache) - 1ull);
+                    const uint64_t free_x = freeq & ~((1ull << kSpecCache) - 1ull);
+                    const uint64_t idle_l = idle & ((1ull << kSeedWaves) - 1ull);
+                    const uint64_t idle_x = idle & ~((1ull << kSeedWaves) - 1ull);
+                    const bool use_l = idle_l && free_l;
+                    if (!use_l && !(idle_x && free_x)) {
+                        m = 0;
+                        idle = 0;
+                        break;
+                    }
+                    const int q = __ffsll((unsigned long long)(use_l ? free_l : free_x)) - 1;
+                    const int w = __ffsll((unsigned long long)(use_l ? idle_l : idle_x)) - 1;
+                    idle &= ~(1ull << w);
+                    const int sd = base + l;
+                    if (!use_l) {  // the helper may have just left: then skip it
+                        const unsigned long long job = 2ull | ((unsigned long long)(q - kSpecCache) << 8) |
+                                                       ((unsigned long long)sd << 32);
+                        if (!cas_agent_wave(&X->task[w - kSeedWaves], 1ull, job)) {
+                            m |= 1ull << l;  // the seed is still unassigned
+                            continue;
+                        }
+                    }
+                    fly |= 1ull << q;
+                    ahead |= 1ull << q;
+                    if (lane == 0) {
+                        S.cache_seed[q] = sd;
+                        S.cache_x[q] = cx;
+                        S.cache_y[q] = cy;
+                        S.cache_s[q] = csc;
+                        S.cache_state[q] = 1;
+                        S.cache_t[q] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                        if (use_l) {
+                            S.task_slot[w] = q;
+                            lds_release(&S.task[w], sd);
+                        }
+                    }
+                    wave_sync();
+                }
+            }
+#ifdef PP_STAMPS
+            n_rounds++;
+#endif
+            STAMP(1);
+            ann_from_seed(L, st, K, img);
+            grow<true>(g, L, img, 0, true, cstage);
+            STAMP(2);
+            commit(&L.a, false, lane < K ? L.a.data[lane][0] : 0.0f,
+                   lane < K ? L.a.data[lane][1] : 0.0f, lane < K ? L.a.data[lane][2] : 0.0f,
+                   lane < K ? L.a.joint_scales[lane] : 0.0f);
+            s = t + 1;
+            STAMP(3);
+        }
+        if (lane == 0) {
+            lds_release(&S.done, 1);
+            if (X) st_agent(&X->fin, 1u);
+        }
+    }
+    __syncthreads();  // helpers drained: no wave of this CU is still growing into the cache
     if (wave == 0) {
         occ_clear(g, L, log, occ);
         STAMP(5);
@@ -2147,7 +2702,7 @@ struct DecodeLayout {
     float inv_e;
     int64_t occ_cap;
     size_t off_cifhr, off_hr_aux, off_hr_masks, off_cifhr_ws, off_seeds, off_seed_counts, off_seed_ws, off_cols[2],
-        off_offs[2], off_n_work, off_need, off_occ, off_wq, off_log, off_work, off_spec, off_nms_score,
+        off_offs[2], off_n_work, off_need, off_occ, off_wq, off_log, off_work, off_spec, off_xext, off_xrec, off_nms_score,
         off_nms_idx, off_nms_f, off_nms_box, total;
     size_t cifhr_ws_bytes;
 };
@@ -2199,6 +2754,8 @@ static DecodeLayout make_layout(int n_img, int K, int C, const Heads &h, const p
     d.off_log = take(n * d.log_cap * sizeof(OccLog));
     d.off_work = take(n * ann_cap * sizeof(pp_ann));
     d.off_spec = take(n * kSpecCache * sizeof(pp_ann));
+    d.off_xext = take(n * sizeof(SeedExt));
+    d.off_xrec = take(n * kExtCache * sizeof(pp_ann));
     d.off_nms_score = take(n * 2 * ann_cap * sizeof(double));
     d.off_nms_idx = take(n * (4 * ann_cap + d.ann_np) * sizeof(int));
     d.off_nms_f = take(n * 2 * ann_cap * sizeof(float));
@@ -2288,6 +2845,27 @@ static const SideStream *side_stream() {
         per_dev[dev] = ss;
     }
     return per_dev[dev];
+}
+
+// External helper workgroups per image for the seed loop: enough to give every CU a seed
+// loop workgroup when the batch has fewer images than CUs (at most kExtWgMax); PP_SEED_EXT
+// overrides (diagnostics: 0 = none).
+static int seed_ext_per_image(int n_img) {
+    static int cus[64] = {};
+    static const int env = [] {
+        const char *e = getenv("PP_SEED_EXT");
+        return e ? atoi(e) : -1;
+    }();
+    if (env >= 0) return std::min(env, kExtWgMax);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (cus[dev] <= 0 &&
+        hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+        (void)hipGetLastError();
+        cus[dev] = 0;
+    }
+    if (n_img <= 0 || cus[dev] <= 0) return 0;
+    return std::max(0, std::min(kExtWgMax, cus[dev] / n_img - 1));
 }
 
 // optional inputs of pp_decode_initial
@@ -2478,6 +3056,9 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
         g.work = (pp_ann *)(ws + d.off_work);
         g.spec = (pp_ann *)(ws + d.off_spec);
         g.spec_far = kSpecFar;
+        g.n_ext = seed_ext_per_image(n_img);
+        g.xext = (SeedExt *)(ws + d.off_xext);
+        g.xrec = (pp_ann *)(ws + d.off_xrec);
         g.nms_score = (double *)(ws + d.off_nms_score);
         g.nms_idx = (int *)(ws + d.off_nms_idx);
         g.nms_f = (float *)(ws + d.off_nms_f);
@@ -2507,8 +3088,17 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
         // PP_STAGE_SEED_LOOP_ONLY / PP_STAGE_AFTER_SEED_LOOP split stage 8 in two calls
         const bool run_rest = !(stages & PP_STAGE_SEED_LOOP_ONLY);
         if (!(stages & PP_STAGE_AFTER_SEED_LOOP)) {
-            hipLaunchKernelGGL(seed_loop_kernel, dim3(n_img), dim3(64 * kSeedWaves),
-                               kColLds * sizeof(float), s, g);
+            if (g.n_ext > 0 &&
+                hipMemsetAsync(g.xext, 0, (size_t)n_img * sizeof(SeedExt), s) != hipSuccess)
+                return fail(PP_EHIP, "pp_decode_batch: seed-loop hand-off reset failed");
+            const size_t dyn = kColLds * sizeof(float) +
+                               (g.n_ext > 0 ? (size_t)kExtCache * kKP * sizeof(float4) : 0);
+            if (g.n_ext > 0)
+                hipLaunchKernelGGL(seed_loop_ext_kernel, dim3(n_img * (1 + g.n_ext)),
+                                   dim3(64 * kSeedWaves), dyn, s, g);
+            else
+                hipLaunchKernelGGL(seed_loop_kernel, dim3(n_img), dim3(64 * kSeedWaves),
+                                   dyn, s, g);
             rc = check_launch("pp_decode_batch(seed loop)");
             if (rc) return rc;
         }

@@ -1,6 +1,8 @@
 """Diagnostic: run the decode with the stamps build and print per-section cycle shares.
 
-    PP_LIB_VARIANT=stamps PP_STAMPS_OUT=gpurun_out/stamps.bin python tools/stamps_run.py
+    PP_LIB_VARIANT=stamps PP_STAMPS_OUT=gpurun_out/stamps.bin python tools/stamps_run.py \
+        [kind:n:side[:dense] ...]   (default planted:256:80 uniform:32:80; dense = the
+        44-CAF DENSE_DECODE_SKELETON of cfg5)
 """
 import os
 import sys
@@ -20,18 +22,26 @@ P3 = ['load', '-', 'nms_filter', 'nms_sort', 'nms_occ', 'nms_clear', 'nms_refilt
       'nms_sort2', 'output']
 
 out = os.environ.get('PP_STAMPS_OUT', 'pp_stamps.bin')
-for kind, n, h in (('planted', 256, 80), ('uniform', 32, 80)):
+cases = sys.argv[1:] or ['planted:256:80', 'uniform:32:80']
+for case in cases:
+    kind, n, h = case.split(':')[:3]
+    n, h = int(n), int(h)
+    dense = case.endswith(':dense')
+    skel = constants.DENSE_DECODE_SKELETON if dense else constants.COCO_PERSON_SKELETON
+    kw = {}
+    if dense:
+        kw = {'n_caf': len(skel)} if kind == 'uniform' else {'skeleton': skel, 'n_people': 16}
     if os.path.exists(out):
         os.remove(out)
-    cif, caf = synthetic.batch(kind, n, h, h)
+    cif, caf = synthetic.batch(kind, n, h, h, **kw)
     eng = DecodeEngine()
     cfg = make_config(**EVAL_CONFIG)
     c, f = torch.from_numpy(cif).cuda(), torch.from_numpy(caf).cuda()
     for _ in range(2):
-        eng.launch(c, f, constants.COCO_PERSON_SKELETON, cfg)
+        eng.launch(c, f, skel, cfg)
     torch.cuda.synchronize()
     st = np.fromfile(out, dtype=np.uint64).reshape(-1, n, 3, 12)[-1].astype(np.float64)
-    print('== {} n={} (mean shader cycles per image)'.format(kind, n))
+    print('== {} (mean shader cycles per image)'.format(case))
     for ph, names in ((0, P1), (1, P2), (2, P3)):
         tot = st[:, ph, :min(len(names), 6 if ph == 0 else 8)].sum(axis=1).mean()
         print('  phase {} total {:.3e}'.format(ph + 1, tot))
