@@ -2390,9 +2390,12 @@ __global__ __launch_bounds__(64) void complete_kernel(GrowArgs g) {
 // "occupied" iff the number of earlier marked boxes covering its cell is non-zero mod 256
 // (the grid's u8 += 1 wraps), which is exactly what the grid lookup returns.
 constexpr int kNmsWaves = 8;
-// boxes per plane kept in LDS (global scratch beyond): 448 keeps the kernel at 29 KB of LDS,
-// so a workgroup fits on a CU beside the seed loop's 103 KB (DecodePipeline overlaps them)
-constexpr int kNmsBoxLds = 448;
+// boxes per plane kept in REGISTERS, kNmsRegBoxes per lane (box i: lane i % 64, slot
+// i / 64), global scratch beyond: a check is ALU over the lane's slots plus one wave sum,
+// and the kernel needs no LDS for them (it fits beside the seed loop's 104 KB).  With the
+// list in LDS (448 per plane) and global memory beyond, uniform cfg5 (1370 annotations per
+// image) spent 20M cycles per image in the suppression pass on global-list loads.
+constexpr int kNmsRegBoxes = 24;
 
 struct ScoreLDS {
     double prod[kKP];
@@ -2438,7 +2441,6 @@ __device__ __forceinline__ int occ_cell(const OccGrid &o, int f, float x, float 
 
 __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
     __shared__ ScoreLDS Ls[kNmsWaves];
-    __shared__ int2 s_box[kNmsWaves][kNmsBoxLds];
     __shared__ int s_m, s_m2, s_status;
     __shared__ float s_mx, s_my;
     const int img = blockIdx.x;
@@ -2564,9 +2566,11 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
         const long oh = (long)((double)(long)(s_my + 1.0f) / g.cfg.occupancy_reduction);
         const long ow = (long)((double)(long)(s_mx + 1.0f) / g.cfg.occupancy_reduction);
         const OccGrid no = occ_grid(nullptr, K, (int)(oh > 0 ? oh : 0), (int)(ow > 0 ? ow : 0));
-        int2 *boxes = m <= kNmsBoxLds ? s_box[wave] : gbox;
         for (int f = wave; f < K; f += kNmsWaves) {  // nms.py:34-45, one plane per pass
             int nbox = 0;
+            int2 rb[kNmsRegBoxes];  // (x0 | x1 << 16, y0 | y1 << 16); zero: covers nothing
+#pragma unroll
+            for (int q = 0; q < kNmsRegBoxes; q++) rb[q] = make_int2(0, 0);
             for (int r0 = 0; r0 < m; r0 += 64) {
                 const int r = r0 + lane;
                 int wi = 0;
@@ -2587,8 +2591,18 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
                     const int fixed = occ_cell(no, f, x, y, red, xi, yi);
                     int cnt = 0;
                     if (fixed < 0) {
-                        for (int q = lane; q < nbox; q += 64) {
-                            const int2 b = boxes[q];
+#pragma unroll
+                        for (int q = 0; q < kNmsRegBoxes; q += 4) {  // unused slots are zero
+                            if (q * 64 >= nbox) continue;  // uniform: skip empty groups
+#pragma unroll
+                            for (int u = 0; u < 4; u++) {
+                                const int2 b = rb[q + u];
+                                cnt += (xi >= (b.x & 0xFFFF) && xi < (b.x >> 16) &&
+                                        yi >= (b.y & 0xFFFF) && yi < (b.y >> 16));
+                            }
+                        }
+                        for (int q = kNmsRegBoxes * 64 + lane; q < nbox; q += 64) {
+                            const int2 b = gbox[q];
                             cnt += (xi >= (b.x & 0xFFFF) && xi < (b.x >> 16) &&
                                     yi >= (b.y & 0xFFFF) && yi < (b.y >> 16));
                         }
@@ -2600,8 +2614,14 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
                     } else {
                         int box[4];
                         if (occ_box(g, no, f, x, y, rl_f(js, l), box)) {
-                            if (lane == 0)
-                                boxes[nbox] = make_int2(box[0] | (box[1] << 16), box[2] | (box[3] << 16));
+                            const int2 nb = make_int2(box[0] | (box[1] << 16), box[2] | (box[3] << 16));
+                            if (nbox < kNmsRegBoxes * 64) {
+#pragma unroll
+                                for (int q = 0; q < kNmsRegBoxes; q++)
+                                    if (q == (nbox >> 6) && lane == (nbox & 63)) rb[q] = nb;
+                            } else if (lane == 0) {
+                                gbox[nbox] = nb;
+                            }
                             nbox++;
                             wave_sync();
                         }
