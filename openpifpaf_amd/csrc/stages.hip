@@ -259,83 +259,86 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-// descending bitonic sort of the first NP (a power of two, 4 <= NP <= kSortLds = 4096) u64
-// keys held 4 per thread of a 1024-thread block (element 4 * thread + e in key[e]; elements
-// past NP are left alone); s_buf (kSortLds) is scratch for the cross-wave stages, which
-// only NP > 256 needs.  Every stage (K, J) is a compile-time instance (BitonicMerge /
-// BitonicStages below): register partners stay static register names and lane partners
-// constant shuffle masks, which a runtime stage loop turns into select chains and
-// bpermute address arithmetic.
-static_assert(kSortLds == 4096, "bitonic_desc sorts 4 keys per thread of 1024");
-template <int K, int J>
-__device__ __forceinline__ void bitonic_stage(uint64_t key[4], uint64_t *s_buf) {
+// descending bitonic sort of the first NP (a power of two, KPT <= NP <= 1024 * KPT) u64
+// keys held KPT (4 or 8) per thread of a 1024-thread block (element KPT * thread + e in
+// key[e]; elements past NP are left alone); s_buf (kSortLds = 4096 keys) is scratch for the
+// cross-wave stages, which only NP > 64 * KPT needs (8 keys per thread: in two passes of 4).
+// Every stage (K, J) is a compile-time instance (BitonicMerge / BitonicStages below):
+// register partners stay static register names and lane partners constant shuffle masks,
+// which a runtime stage loop turns into select chains and bpermute address arithmetic.
+static_assert(kSortLds == 4096, "bitonic_desc's LDS passes hold 4 keys per thread of 1024");
+template <int KPT, int K, int J>
+__device__ __forceinline__ void bitonic_stage(uint64_t key[KPT], uint64_t *s_buf) {
     const int t = threadIdx.x;
-    if constexpr (J >= 256) {  // partner in another wave: through LDS
-        __syncthreads();       // earlier readers of s_buf are done
+    if constexpr (J >= 64 * KPT) {  // partner thread t ^ (J / KPT) in another wave: via LDS
 #pragma unroll
-        for (int e = 0; e < 4; e++) s_buf[4 * t + e] = key[e];
-        __syncthreads();
+        for (int h = 0; h < KPT; h += 4) {
+            __syncthreads();  // earlier readers of s_buf are done
 #pragma unroll
-        for (int e = 0; e < 4; e++) {
-            const int i = 4 * t + e;
-            key[e] = bitonic_pick(i, J, K, key[e], s_buf[i ^ J]);
+            for (int e = 0; e < 4; e++) s_buf[4 * t + e] = key[h + e];
+            __syncthreads();
+            const int tp = t ^ (J / KPT);
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+                key[h + e] = bitonic_pick(KPT * t + h + e, J, K, key[h + e], s_buf[4 * tp + e]);
         }
-    } else if constexpr (J >= 4) {  // partner thread t ^ (J / 4), same slot, same wave
+    } else if constexpr (J >= KPT) {  // partner thread t ^ (J / KPT), same slot, same wave
 #pragma unroll
-        for (int e = 0; e < 4; e++)
-            key[e] = bitonic_pick(4 * t + e, J, K, key[e], lane_xor64<(J >> 2)>(key[e]));
+        for (int e = 0; e < KPT; e++)
+            key[e] = bitonic_pick(KPT * t + e, J, K, key[e], lane_xor64<(J / KPT)>(key[e]));
     } else {  // partner slot e ^ J of this thread
-        uint64_t nk[4];
+        uint64_t nk[KPT];
 #pragma unroll
-        for (int e = 0; e < 4; e++) nk[e] = bitonic_pick(4 * t + e, J, K, key[e], key[e ^ J]);
+        for (int e = 0; e < KPT; e++) nk[e] = bitonic_pick(KPT * t + e, J, K, key[e], key[e ^ J]);
 #pragma unroll
-        for (int e = 0; e < 4; e++) key[e] = nk[e];
+        for (int e = 0; e < KPT; e++) key[e] = nk[e];
     }
 }
 
-template <int K, int J>
+template <int KPT, int K, int J>
 struct BitonicStages {  // stages J, J / 2, ..., 1 of the merge of blocks of K
-    __device__ __forceinline__ static void run(uint64_t key[4], uint64_t *s_buf) {
-        bitonic_stage<K, J>(key, s_buf);
-        BitonicStages<K, J / 2>::run(key, s_buf);
+    __device__ __forceinline__ static void run(uint64_t key[KPT], uint64_t *s_buf) {
+        bitonic_stage<KPT, K, J>(key, s_buf);
+        BitonicStages<KPT, K, J / 2>::run(key, s_buf);
     }
 };
-template <int K>
-struct BitonicStages<K, 0> {
+template <int KPT, int K>
+struct BitonicStages<KPT, K, 0> {
     __device__ __forceinline__ static void run(uint64_t *, uint64_t *) {}
 };
 
-template <int K, int NP>
+template <int KPT, int K, int NP>
 struct BitonicMerge {  // merges of block sizes K, 2K, ..., NP
-    __device__ __forceinline__ static void run(uint64_t key[4], uint64_t *s_buf) {
-        BitonicStages<K, K / 2>::run(key, s_buf);
-        BitonicMerge<2 * K, NP>::run(key, s_buf);
+    __device__ __forceinline__ static void run(uint64_t key[KPT], uint64_t *s_buf) {
+        BitonicStages<KPT, K, K / 2>::run(key, s_buf);
+        BitonicMerge<KPT, 2 * K, NP>::run(key, s_buf);
     }
 };
-template <int NP>
-struct BitonicMerge<2 * NP, NP> {
+template <int KPT, int NP>
+struct BitonicMerge<KPT, 2 * NP, NP> {
     __device__ __forceinline__ static void run(uint64_t *, uint64_t *) {}
 };
 
-template <int NP>
-__device__ __forceinline__ void bitonic_desc_np(uint64_t key[4], uint64_t *s_buf) {
-    BitonicMerge<2, NP>::run(key, s_buf);
+template <int KPT, int NP>
+__device__ __forceinline__ void bitonic_desc_np(uint64_t key[KPT], uint64_t *s_buf) {
+    BitonicMerge<KPT, 2, NP>::run(key, s_buf);
 }
 
-// the sort of the first np keys (np a power of two, rounded up to 4); block-uniform np
+// the sort of the first np keys (np a power of two, rounded up to 4), 4 keys per thread;
+// block-uniform np
 __device__ void bitonic_desc(uint64_t key[4], uint64_t *s_buf, int np) {
     switch (np <= 4 ? 4 : np) {
-    case 4: bitonic_desc_np<4>(key, s_buf); break;
-    case 8: bitonic_desc_np<8>(key, s_buf); break;
-    case 16: bitonic_desc_np<16>(key, s_buf); break;
-    case 32: bitonic_desc_np<32>(key, s_buf); break;
-    case 64: bitonic_desc_np<64>(key, s_buf); break;
-    case 128: bitonic_desc_np<128>(key, s_buf); break;
-    case 256: bitonic_desc_np<256>(key, s_buf); break;
-    case 512: bitonic_desc_np<512>(key, s_buf); break;
-    case 1024: bitonic_desc_np<1024>(key, s_buf); break;
-    case 2048: bitonic_desc_np<2048>(key, s_buf); break;
-    default: bitonic_desc_np<4096>(key, s_buf); break;
+    case 4: bitonic_desc_np<4, 4>(key, s_buf); break;
+    case 8: bitonic_desc_np<4, 8>(key, s_buf); break;
+    case 16: bitonic_desc_np<4, 16>(key, s_buf); break;
+    case 32: bitonic_desc_np<4, 32>(key, s_buf); break;
+    case 64: bitonic_desc_np<4, 64>(key, s_buf); break;
+    case 128: bitonic_desc_np<4, 128>(key, s_buf); break;
+    case 256: bitonic_desc_np<4, 256>(key, s_buf); break;
+    case 512: bitonic_desc_np<4, 512>(key, s_buf); break;
+    case 1024: bitonic_desc_np<4, 1024>(key, s_buf); break;
+    case 2048: bitonic_desc_np<4, 2048>(key, s_buf); break;
+    default: bitonic_desc_np<4, 4096>(key, s_buf); break;
     }
 }
 
@@ -403,6 +406,48 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
         }
         return a.seg_base(lo / a.K, lo % a.K) + (i - s_off[lo]);
     };
+    // the sorted keys kb[0 .. n) (LDS, or global scratch for more than kSortLds keys):
+    // runs of equal (v, field) re-sorted by (x, y, s) descending, then emission order (one
+    // thread per run, insertion sort), then the records written in order
+    auto finish = [&](uint64_t *kb) {
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const uint64_t ki = kb[i] >> 27;
+            const bool tie_prev = i > 0 && (kb[i - 1] >> 27) == ki;
+            const bool tie_next = i + 1 < n && (kb[i + 1] >> 27) == ki;
+            if (tie_prev || !tie_next) continue;
+            int end = i + 1;
+            while (end < n && (kb[end] >> 27) == ki) end++;
+            auto before = [&](uint64_t p, uint64_t q) {  // p must precede q
+                const int ep = key_emit(p), eq = key_emit(q);
+                const int64_t kp = slot(ep), kq = slot(eq);
+                if (gx[kp] != gx[kq]) return gx[kp] > gx[kq];
+                if (gy[kp] != gy[kq]) return gy[kp] > gy[kq];
+                if (gs[kp] != gs[kq]) return gs[kp] > gs[kq];
+                return ep < eq;
+            };
+            for (int u = i + 1; u < end; u++) {
+                const uint64_t cur = kb[u];
+                int w = u;
+                while (w > i && before(cur, kb[w - 1])) {
+                    kb[w] = kb[w - 1];
+                    w--;
+                }
+                kb[w] = cur;
+            }
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const uint64_t k = kb[i];
+            const int64_t e = slot(key_emit(k));
+            pp_seed r;
+            r.v = __uint_as_float((uint32_t)(k >> 32));
+            r.field = (int)((k >> 27) & 31u);
+            r.x = gx[e];
+            r.y = gy[e];
+            r.s = gs[e];
+            out[i] = r;
+        }
+    };
     if (n <= kSortLds) {
         // thread t gathers seeds 4t .. 4t + 3 (all loads independent: one round trip), the
         // keys straight into registers
@@ -425,45 +470,66 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; e++) s_key[4 * threadIdx.x + e] = key[e];
         __syncthreads();
-        // runs of equal (v, field): insertion sort by (x, y, s) descending, then emission
-        for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            const uint64_t ki = s_key[i] >> 27;
-            const bool tie_prev = i > 0 && (s_key[i - 1] >> 27) == ki;
-            const bool tie_next = i + 1 < n && (s_key[i + 1] >> 27) == ki;
-            if (tie_prev || !tie_next) continue;
-            int end = i + 1;
-            while (end < n && (s_key[end] >> 27) == ki) end++;
-            auto before = [&](uint64_t p, uint64_t q) {  // p must precede q
-                const int ep = key_emit(p), eq = key_emit(q);
-                const int64_t kp = slot(ep), kq = slot(eq);
-                if (gx[kp] != gx[kq]) return gx[kp] > gx[kq];
-                if (gy[kp] != gy[kq]) return gy[kp] > gy[kq];
-                if (gs[kp] != gs[kq]) return gs[kp] > gs[kq];
-                return ep < eq;
-            };
-            for (int u = i + 1; u < end; u++) {
-                const uint64_t cur = s_key[u];
-                int w = u;
-                while (w > i && before(cur, s_key[w - 1])) {
-                    s_key[w] = s_key[w - 1];
-                    w--;
-                }
-                s_key[w] = cur;
+        finish(s_key);
+        return;
+    }
+    if (n <= 2 * kSortLds) {
+        // 4096 < n <= 8192: the same network with 8 keys per thread (cross-wave stages in
+        // two LDS passes), output straight from the registers, or, when a run of equal
+        // (v, field) needs the full comparator's insertion sort, through global scratch
+        uint64_t key[8];
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            const int i = 8 * (int)threadIdx.x + e;
+            key[e] = 0ull;
+            if (i < n) {
+                const int64_t k = slot(i);
+                key[e] = seed_key(gv[k], gf[k], i);
             }
         }
+        bitonic_desc_np<8, 2 * kSortLds>(key, s_key);
         __syncthreads();
-        for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            const uint64_t k = s_key[i];
-            const int64_t e = slot(key_emit(k));
-            pp_seed r;
-            r.v = __uint_as_float((uint32_t)(k >> 32));
-            r.field = (int)((k >> 27) & 31u);
-            r.x = gx[e];
-            r.y = gy[e];
-            r.s = gs[e];
-            out[i] = r;
+        s_key[threadIdx.x] = key[0];  // each thread's first key, for its predecessor
+        __syncthreads();
+        // keys are nonzero for real seeds (v > 0), zero past n
+        bool tie = false;
+#pragma unroll
+        for (int e = 0; e < 7; e++)
+            tie |= key[e + 1] != 0ull && (key[e] >> 27) == (key[e + 1] >> 27);
+        if (threadIdx.x + 1 < blockDim.x) {
+            const uint64_t nx = s_key[threadIdx.x + 1];
+            tie |= nx != 0ull && (key[7] >> 27) == (nx >> 27);
         }
-    } else {
+        if (!__syncthreads_or(tie)) {
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const int i = 8 * (int)threadIdx.x + e;
+                if (i >= n) continue;
+                const uint64_t k = key[e];
+                const int64_t q = slot(key_emit(k));
+                pp_seed r;
+                r.v = __uint_as_float((uint32_t)(k >> 32));
+                r.field = (int)((k >> 27) & 31u);
+                r.x = gx[q];
+                r.y = gy[q];
+                r.s = gs[q];
+                out[i] = r;
+            }
+            return;
+        }
+        // ties: the sorted keys to global scratch (the permutation buffer holds 2 * np
+        // ints = np keys), then as the LDS path
+        uint64_t *gk = reinterpret_cast<uint64_t *>(a.g_perm + (int64_t)img * a.np_cap);
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+            const int i = 8 * (int)threadIdx.x + e;
+            if (i < n) gk[i] = key[e];
+        }
+        __syncthreads();
+        finish(gk);
+        return;
+    }
+    {
         // large seed sets: network over a permutation in global memory; keys are read
         // through an emission-index -> slot map
         int *perm = a.g_perm + (int64_t)img * a.np_cap;

@@ -352,7 +352,9 @@ def test_cifhr_sparse_bit_exact():
     assert 0.0 < on <= 1.0
 
 
-@pytest.mark.parametrize('hw', [12, 20])  # 17*144 seeds sort in LDS, 17*400 globally
+# 17*144 seeds sort in registers (4 per thread), 17*400 in the 8-per-thread network (ties
+# re-sorted through global scratch), 17*576 in the global network
+@pytest.mark.parametrize('hw', [12, 20, 24])
 def test_seed_ties(dec, hw):
     """Saturated CifHr gives equal v within a field: the sort must fall back to the full
     tuple order (x, y, s descending, then emission order), cif_seeds.py:54."""
@@ -378,6 +380,33 @@ def test_seed_ties(dec, hw):
     assert len(got) == len(exp) > 17 * hw * hw // 2
     assert np.array_equal(got, exp)
     assert (np.diff(exp[:, 0]) == 0).sum() > len(exp) // 2  # the case really has ties
+
+
+# 17*324 seeds, no (v, field) ties: sorted with 8 keys per thread, output from registers;
+# 17*441 (6958 seeds, three ties where 0.9 + 0.1 * conf rounds equal): the same network,
+# then the ties re-sorted with the full comparator through global scratch
+@pytest.mark.parametrize('hw', [18, 21])
+def test_seeds_8k_network(dec, hw):
+    """Seed sets of 4096 < n <= 8192 (stages.hip seeds_sort_kernel), against the oracle."""
+    g = {'mode': np.array('eval'), 'greedy': 0, 'connection_method': np.array('blend')}
+    _configure(dec, g)
+    rng = np.random.default_rng(11)
+    yy, xx = np.mgrid[0:hw, 0:hw].astype(np.float32)
+    cif = np.zeros((17, 5, hw, hw), np.float32)
+    cif[:, 0] = rng.uniform(0.8, 1.0, (17, hw, hw)).astype(np.float32)  # distinct: no ties
+    cif[:, 1] = np.floor(xx / 2) * 2  # shared positions: CifHr saturates, every cell seeds
+    cif[:, 2] = np.floor(yy / 2) * 2
+    cif[:, 3] = 0.5
+    cif[:, 4] = rng.uniform(0.5, 1.5, (17, hw, hw)).astype(np.float32)
+    caf = np.zeros((19, 9, hw, hw), np.float32)
+    fc = dec.FieldConfig()
+    hr = dec.CifHr(fc).fill([cif, caf]).accumulated
+    seeds = dec.CifSeeds(hr, fc).fill([cif, caf]).get()
+    got = np.array([tuple(float(t) for t in sd) for sd in seeds], np.float32).reshape(-1, 5)
+    ref = oracle.seeds(cif, hr)
+    exp = np.stack([ref['v'], ref['field'].astype(np.float32), ref['x'], ref['y'], ref['s']], 1)
+    assert 4096 < len(exp) <= 8192, len(exp)
+    assert np.array_equal(got, exp)
 
 
 def test_stage_calls_equal_full_decode(dec):
