@@ -450,6 +450,8 @@ _B_FIRST = {'1': True, '0': False, 'lazy': 'lazy'}.get(os.environ.get('PP_PIPE_B
 # 3, after the seeds kernels shrank: planted 0.838 vs 0.868 ms and 0.845 vs 0.898 ms per
 # step on two boxes; uniform was already sets-first)
 _B_FIRST_DENSITY = 0.0
+# workspaces in flight (PP_PIPE_DEPTH): batch i + depth's front half waits for batch i's tail
+_PIPE_DEPTH = 2
 
 
 class DecodePipeline:
@@ -479,15 +481,18 @@ class DecodePipeline:
     The current stream does not wait for the back half; the fields must stay unchanged
     until the batch's records are fetched."""
 
-    def __init__(self, device=None):
+    def __init__(self, device=None, depth=None):
         self.device = _device.require() if device is None else device
-        self.engines = (DecodeEngine(), DecodeEngine())
+        if depth is None:
+            depth = int(os.environ.get('PP_PIPE_DEPTH', _PIPE_DEPTH))
+        self.depth = max(2, depth)  # workspaces in flight (DESIGN.md: 3 or 4 measured slower)
+        self.engines = tuple(DecodeEngine() for _ in range(self.depth))
         # one back stream: consecutive seed loops serialise.  Two (one per workspace, so the
         # next batch's images fill the CUs whose image of this batch finished) measured
         # slower: planted 0.91-1.01 vs 0.84-0.85 ms per step, uniform unchanged (round 3)
         self.back = torch.cuda.Stream(device=self.device)
         self.tail = torch.cuda.Stream(device=self.device)
-        self._back_done = [None, None]
+        self._back_done = [None] * self.depth
         self._i = 0
         self.density = 0.0  # annotations per image of the last batch whose records were read
 
@@ -497,7 +502,7 @@ class DecodePipeline:
         (five torch.cuda.Events, optional) are recorded around the CifHr stage, the other
         front stages (front stream), at the seed loop's start (back stream) and at the end
         of NMS (tail stream)."""
-        par = self._i % 2
+        par = self._i % self.depth
         self._i += 1
         eng = self.engines[par]
         front = torch.cuda.current_stream(self.device)
