@@ -409,6 +409,53 @@ def test_seeds_8k_network(dec, hw):
     assert np.array_equal(got, exp)
 
 
+def _tie_fields(hw, distinct):
+    rng = np.random.default_rng(3 if not distinct else 11)
+    yy, xx = np.mgrid[0:hw, 0:hw].astype(np.float32)
+    cif = np.zeros((17, 5, hw, hw), np.float32)
+    cif[:, 0] = rng.uniform(0.8, 1.0, (17, hw, hw)).astype(np.float32) if distinct else 0.9
+    cif[:, 1] = np.floor(xx / 2) * 2
+    cif[:, 2] = np.floor(yy / 2) * 2
+    cif[:, 3] = 0.5
+    cif[:, 4] = rng.choice(np.array([1.0, 2.0], np.float32), (17, hw, hw))
+    return cif
+
+
+# the DEVICE order of the seeds (the seed loop's order; the API's get() re-sorts on the
+# host), one image and a batch of 17: seeds_sort_kernel with 4 keys per thread up to 4096
+# seeds (ties re-sorted in LDS), 8 up to 8192 (ties through global scratch), the global
+# network beyond
+@pytest.mark.parametrize('n_img', [1, 17])
+@pytest.mark.parametrize('hw,distinct', [(12, False), (18, True), (20, False), (24, False)])
+def test_seeds_device_order(dec, n_img, hw, distinct):
+    import torch
+    from openpifpaf_amd import _device
+    from openpifpaf_amd._abi import SEED_DTYPE, make_config, scale_list
+    from openpifpaf_amd._lib import call
+    from openpifpaf_amd.decoder._fields import cfg_ptr, pitched_hr, with_geometry
+    cfg = make_config()
+    cif = _tie_fields(hw, distinct)
+    hr = oracle.cifhr(cif)
+    ref = oracle.seeds(cif, hr, cfg)
+    c = torch.from_numpy(np.ascontiguousarray(np.broadcast_to(cif, (n_img,) + cif.shape))).cuda()
+    h1 = pitched_hr(hr)
+    hrb = h1.expand(n_img, -1, -1, -1).contiguous()
+    k = 17
+    cap = k * hw * hw
+    arr = with_geometry(scale_list([(c.data_ptr(), hw, hw)], [], [8], [], [0.0]), hr.shape)
+    out = torch.empty(n_img * cap * SEED_DTYPE.itemsize, dtype=torch.uint8, device='cuda')
+    count = torch.zeros(n_img, dtype=torch.int32, device='cuda')
+    call('pp_seeds_multi', arr, len(arr), _device.ptr(hrb), n_img, k, cfg_ptr(cfg),
+         _device.ptr(out), cap, _device.ptr(count), _device.stream())
+    recs = np.frombuffer(out.cpu().numpy().tobytes(), dtype=SEED_DTYPE).reshape(n_img, cap)
+    counts = count.cpu().numpy()
+    for i in range(n_img):
+        got = recs[i, :counts[i]]
+        assert len(got) == len(ref), (i, len(got), len(ref))
+        for name in ('v', 'field', 'x', 'y', 's'):
+            assert np.array_equal(got[name], ref[name]), (i, name)
+
+
 def test_stage_calls_equal_full_decode(dec):
     """pp_decode_stages called stage by stage, or with several stages per call, gives the
     same records as pp_decode_batch (the stage contract of include/pifpaf_amd.h)."""

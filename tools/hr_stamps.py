@@ -1,6 +1,7 @@
 """Diagnostic: per-workgroup timeline of cifhr_sparse_kernel (stamps build).
 
-    PP_LIB_VARIANT=stamps PP_HR_STAMPS_OUT=gpurun_out/hr_stamps.bin python tools/hr_stamps.py
+    PP_LIB_VARIANT=stamps PP_HR_STAMPS_OUT=gpurun_out/hr_stamps.bin python tools/hr_stamps.py \
+        [kind:n ...]   (default planted:256 uniform:64)
 """
 import os
 import sys
@@ -13,7 +14,9 @@ from openpifpaf_amd import synthetic  # noqa: E402
 from openpifpaf_amd.decoder.cif_hr import cifhr_sparse_device  # noqa: E402
 
 out = os.environ.get('PP_HR_STAMPS_OUT', 'pp_hr_stamps.bin')
-for kind, n in (('planted', 256), ('uniform', 64)):
+cases = [(c.split(':')[0], int(c.split(':')[1])) for c in sys.argv[1:]] or [('planted', 256),
+                                                                           ('uniform', 64)]
+for kind, n in cases:
     if os.path.exists(out):
         os.remove(out)
     cif, _ = synthetic.batch(kind, n, 80, 80)
