@@ -95,11 +95,18 @@ __device__ __forceinline__ uint32_t pix_key(int x, int y) {
     return (uint32_t)(x & 0xffff) | ((uint32_t)y << 16);
 }
 
-// candidates the fast fold cannot take exactly: div_refined outside its domain, or a
-// non-finite v (v * 0 would not vanish for the pixels the fast term excludes)
+// candidates the fast fold cannot take exactly: div_refined outside its domain or a box
+// the circle does not cover (make_cand sets r = 0 for both), or a non-finite v (v * 0 would
+// not vanish for the pixels the fast term excludes)
 __device__ __forceinline__ bool cand_slow(const FoldCand &c) {
-    return !recip_ok(c.s2) || !(__builtin_fabsf(c.v) < __builtin_inff());
+    return !(c.r > 0.0f) || !(__builtin_fabsf(c.v) < __builtin_inff());
 }
+
+// Lanes whose pixel lies outside the map fold at these coordinates: dx^2 = 2^120 fails every
+// fast candidate's circle test (s2 <= 2^100), and the key matches no candidate's nearest
+// pixel (nkey is a pixel of the map, or ~0u).
+constexpr float kOffMapCoord = 0x1p60f;
+constexpr uint32_t kOffMapKey = 0xFFFFFFFEu;
 
 typedef short pp_short2 __attribute__((ext_vector_type(2)));
 
@@ -112,13 +119,35 @@ __device__ __forceinline__ bool in_box(const FoldCand &c, uint32_t key) {
     return __builtin_bit_cast(uint32_t, cl) == key;
 }
 
-__device__ __forceinline__ FoldCand make_cand(int4 b, float4 p) {
+// The fast fold has no box test (functional.pyx:122-129 bounds): the circle test alone
+// excludes every pixel outside the box when the first pixel past each of the box's four
+// edges fails it on its own axis, RN(d^2) > s2 with d = k - c.  Further out |d| only grows
+// (rounding is monotone), and the fold's sum = RN(RN(dx^2) + RN(dy^2)) >= RN(dx^2).  The
+// box ends at most a rounding error inside the circle's reach on the low side (x0 =
+// trunc(cx - sigma)) and within one pixel on the high side (x1 = trunc(cx + sigma + 1)),
+// so this fails only when an edge sits a few ulps from the circle; such candidates, and
+// non-finite or huge centers, keep the box test on the slow path.  Pixels past the map's
+// edge never fold (kOffMapCoord).
+__device__ __forceinline__ bool box_in_circle(int4 b, float cx, float cy, float s2, int hh, int ww) {
+    if (!(__builtin_fabsf(cx) < 0x1p20f && __builtin_fabsf(cy) < 0x1p20f)) return false;
+    const auto out = [s2](int k, float c) {
+        const float d = (float)k - c;
+        return d * d > s2;
+    };
+    if (b.x > 0 && !out(b.x - 1, cx)) return false;
+    if (b.y < ww && !out(b.y, cx)) return false;
+    if (b.z > 0 && !out(b.z - 1, cy)) return false;
+    if (b.w < hh && !out(b.w, cy)) return false;
+    return true;
+}
+
+__device__ __forceinline__ FoldCand make_cand(int4 b, float4 p, int hh, int ww) {
     FoldCand c;
     c.cx = p.x;
     c.cy = p.y;
     c.v = p.z;
     c.s2 = p.w;
-    c.r = recip_ok(p.w) ? recip_of(p.w).r : 0.0f;
+    c.r = (recip_ok(p.w) && box_in_circle(b, p.x, p.y, p.w, hh, ww)) ? recip_of(p.w).r : 0.0f;
     c.lo = pix_key(b.x, b.z);
     c.hi = pix_key(b.y - 1, b.w - 1);
     const int nx = nearest_coord(p.x), ny = nearest_coord(p.y);
@@ -185,17 +214,16 @@ __device__ __forceinline__ float fold_apply(float acc, const FoldTerm &f) {
     return f.take ? ((a < 1.0f) ? a : 1.0f) : acc;  // min(max_value, f)
 }
 
-// The fast term (s2 in div_refined's domain, v finite): a pixel outside the box or the
-// circle gets q = 16, so t = (1 - 16 / 16)^8 = 0 and vv = v * 0 = +0, and the update
-// min(acc + vv, 1) leaves it as it was (acc in [0, 1]).  The closest pixel lies inside both
-// (sum < 0.5 <= sigma^2, sigma >= 1), so its q = 0 is applied last.  Every pixel then takes
-// the same update, with the two tests as selects on q (vector compares + cndmask: no
-// scalar mask arithmetic).
+// The fast term (s2 in div_refined's domain, v finite, the box inside the circle's reach:
+// make_cand): a pixel outside the circle gets q = 16, so t = (1 - 16 / 16)^8 = 0 and
+// vv = v * 0 = +0, and the update min(acc + vv, 1) leaves it as it was (acc in [0, 1]).
+// The closest pixel lies inside (sum < 0.5 <= sigma^2, sigma >= 1), so its q = 0 is applied
+// last.  Every pixel then takes the same update, with the tests as selects on q (vector
+// compares + cndmask: no scalar mask arithmetic).
 __device__ __forceinline__ float fold_vv(const FoldCand &c, float fx, float fy, uint32_t key) {
     const float dx = fx - c.cx, dy = fy - c.cy;
     const float sum = dx * dx + dy * dy;
     float q = div_refined(sum, Recip{c.s2, c.r});
-    q = in_box(c, key) ? q : 16.0f;
     q = (sum > c.s2) ? 16.0f : q;
     q = (key == c.nkey) ? 0.0f : q;
     float t = __builtin_fmaf(q, -0.0625f, 1.0f);
@@ -414,7 +442,7 @@ __global__ __launch_bounds__(256) void cifhr_splats_kernel(HrSplatArgs a) {
                     const float sigma = (sg != sg) ? sg : fmaxf(1.0f, sg);  // np.maximum keeps NaN
                     const float v = (c[k] / a.neighbors) / len_cifs;        // v / neighbors / len_cifs
                     const int4 box = splat_box<M_GAUSS_MAX>(cx, cy, 1.0f * sigma, a.hh, a.ww);
-                    out[running + slot] = make_cand(box, make_float4(cx, cy, v, sigma * sigma));
+                    out[running + slot] = make_cand(box, make_float4(cx, cy, v, sigma * sigma), a.hh, a.ww);
                     if (use_bits) {  // mark the 64x64 output tiles this splat's box touches
                         for (int ty = box.z / kTile; ty <= (box.w - 1) / kTile; ty++)
                             for (int tx = box.x / kTile; tx <= (box.y - 1) / kTile; tx++) {
@@ -752,9 +780,11 @@ __global__ __launch_bounds__(256) void cifhr_tile_kernel(HrTileArgs a) {
                     const int b = __builtin_ctzll(bl);
                     const int bx = b & 7, byl = b >> 3;
                     const int px = tx0 + 8 * bx + lx, py = wy0 + 8 * byl + ly;
+                    const bool on = px < a.w && py < a.h;
                     float *cell = &s_acc[(byl * 8 + ly) * kHrPad + bx * 8 + lx];
-                    *cell = fold_block(*cell, cand, __ballot((cl >> b) & 1ull), slow, (float)px,
-                                       (float)py, pix_key(px, py));
+                    *cell = fold_block(*cell, cand, __ballot((cl >> b) & 1ull), slow,
+                                       on ? (float)px : kOffMapCoord, on ? (float)py : kOffMapCoord,
+                                       on ? pix_key(px, py) : kOffMapKey);
                 }
                 if (last) break;
                 wave_sync();  // the candidate array is rewritten by the next pass
@@ -885,7 +915,7 @@ __device__ int hr_splat_list(const HrSparseArgs &a, int64_t fld, int64_t slot, u
             const float sigma = (sg != sg) ? sg : fmaxf(1.0f, sg);  // np.maximum keeps NaN
             const float v = (c / a.neighbors) / len_cifs;           // v / neighbors / len_cifs
             const int4 box = splat_box<M_GAUSS_MAX>(cx, cy, 1.0f * sigma, a.hh, a.ww);
-            glist[pos] = make_cand(box, make_float4(cx, cy, v, sigma * sigma));
+            glist[pos] = make_cand(box, make_float4(cx, cy, v, sigma * sigma), a.hh, a.ww);
             for (int ty = box.z / kTile; ty <= (box.w - 1) / kTile; ty++)
                 for (int tx = box.x / kTile; tx <= (box.y - 1) / kTile; tx++) {
                     const int t = ty * a.tiles_x + tx;
@@ -1096,8 +1126,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
             for (uint64_t rest = live; rest; rest &= rest - 1) {
                 const int blk = __builtin_ctzll(rest);
                 const int px = tx0 + 8 * (blk & 7) + lx, py = ty0 + 8 * (blk >> 3) + ly;
-                const float fx = (float)px, fy = (float)py;
-                const uint32_t key = pix_key(px, py);
+                const bool on = px < a.ww && py < a.hh;
+                const float fx = on ? (float)px : kOffMapCoord, fy = on ? (float)py : kOffMapCoord;
+                const uint32_t key = on ? pix_key(px, py) : kOffMapKey;
                 const uint64_t bq = __ballot((cl >> blk) & 1ull);
                 float acc = 0.0f, res = 0.0f;
                 int gcur = -1;
