@@ -861,8 +861,14 @@ struct HrSparseArgs {
     float *aux;       // MULTI: open-group folds between passes, same shape as map
     uint64_t *masks;  // (n_img * K, tiles) written blocks
     int tiles_x, tiles, tiles_y;
-    int split;        // workgroups per field (small batches): each builds the field's list
-                      // (identical writes) and folds every split-th touched tile
+    int split;        // workgroups per field (small batches): each folds every split-th
+                      // touched tile of the field
+    // split > 1: the field's list, bins and tile bits are built once by
+    // cifhr_sparse_list_kernel (prebuilt; NULL: every split workgroup builds its own copy)
+    int *pre_total;         // (n_img * K) list lengths
+    uint32_t *pre_bits;     // (n_img * K, kTileBits / 32) touched tiles
+    int *pre_rowcnt;        // (n_img * K, kMaxBinRows) bin sizes (-1: none), offsets
+    int *pre_rowoff;
 };
 
 __device__ __forceinline__ float nan_max(float a, float b) {  // np.maximum
@@ -1004,6 +1010,30 @@ __device__ int hr_splat_list(const HrSparseArgs &a, int64_t fld, int64_t slot, u
     return running;
 }
 
+// Small batches (split > 1, one CifHr group): phase 1 once per field, into the field's
+// list / bins / tile bits in global memory, so that the split workgroups of
+// cifhr_sparse_kernel only fold.  Untouched tiles get their empty block masks here.
+__global__ __launch_bounds__(256) void cifhr_sparse_list_kernel(HrSparseArgs a) {
+    __shared__ uint32_t s_bits[kTileBits / 32];
+    __shared__ RowBinLds s_rb;
+    __shared__ __attribute__((aligned(16))) int s_cnt[2][kSpU][4];
+    __shared__ int s_gbeg[kMaxHeads + 1];
+    __shared__ int s_stage[kSpStage];
+    const int64_t fld = blockIdx.x;
+    if (threadIdx.x < kTileBits / 32) s_bits[threadIdx.x] = 0u;
+    const int total = hr_splat_list<false>(a, fld, fld, s_bits, s_cnt, s_gbeg, s_stage);
+    int *rowcnt = a.pre_rowcnt + fld * kMaxBinRows, *rowoff = a.pre_rowoff + fld * kMaxBinRows;
+    if (a.bins_cap > 0 && total > kBinMin)
+        hr_row_bins(a.list + fld * a.list_cap, total, a.bins + fld * a.bins_cap, a.bins_cap,
+                    a.tiles_y, s_rb, rowcnt, rowoff);
+    else if (threadIdx.x < kMaxBinRows)
+        rowcnt[threadIdx.x] = -1;
+    if (threadIdx.x == 0) a.pre_total[fld] = total;
+    if (threadIdx.x < kTileBits / 32) a.pre_bits[fld * (kTileBits / 32) + threadIdx.x] = s_bits[threadIdx.x];
+    for (int t = threadIdx.x; t < a.tiles; t += 256)  // untouched tiles: no block written
+        if (!((s_bits[t >> 5] >> (t & 31)) & 1u)) a.masks[fld * a.tiles + t] = 0ull;
+}
+
 template <bool MULTI>
 // 8 waves per SIMD (<= 64 VGPRs): the kernel is latency-bound, occupancy hides it
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void cifhr_sparse_kernel(HrSparseArgs a) {
@@ -1020,18 +1050,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
 
     const int64_t fld = blockIdx.x / a.split;  // image * K + field
     const int part = (int)(blockIdx.x % a.split);
-    const int64_t slot = blockIdx.x;  // list / bins copy of this workgroup (fld * split + part)
+    const bool pre = !MULTI && a.pre_total;
+    // list / bins copy of this workgroup (fld * split + part), or the field's prebuilt one
+    const int64_t slot = pre ? fld : (int64_t)blockIdx.x;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (wave == 0) HR_STAMP(0);
-    if (threadIdx.x < kTileBits / 32) s_bits[threadIdx.x] = 0u;
     if (threadIdx.x == 0) s_next = 0;
-
-    const int total = hr_splat_list<MULTI>(a, fld, slot, s_bits, s_cnt, s_gbeg,
-                                           reinterpret_cast<int *>(&s_cand[0][0]));
-    const bool use_bins = !MULTI && a.bins_cap > 0 && total > kBinMin;
-    if (use_bins)
-        hr_row_bins(a.list + slot * a.list_cap, total, a.bins + slot * a.bins_cap, a.bins_cap,
-                    a.tiles_y, s_rb, s_rowcnt, s_rowoff);
+    int total;
+    bool use_bins;
+    if (pre) {
+        if (threadIdx.x < kTileBits / 32) s_bits[threadIdx.x] = a.pre_bits[fld * (kTileBits / 32) + threadIdx.x];
+        if (threadIdx.x < kMaxBinRows) {
+            s_rowcnt[threadIdx.x] = a.pre_rowcnt[fld * kMaxBinRows + threadIdx.x];
+            s_rowoff[threadIdx.x] = a.pre_rowoff[fld * kMaxBinRows + threadIdx.x];
+        }
+        total = a.pre_total[fld];
+        use_bins = a.bins_cap > 0 && total > kBinMin;
+        __syncthreads();
+    } else {
+        if (threadIdx.x < kTileBits / 32) s_bits[threadIdx.x] = 0u;
+        total = hr_splat_list<MULTI>(a, fld, slot, s_bits, s_cnt, s_gbeg,
+                                     reinterpret_cast<int *>(&s_cand[0][0]));
+        use_bins = !MULTI && a.bins_cap > 0 && total > kBinMin;
+        if (use_bins)
+            hr_row_bins(a.list + slot * a.list_cap, total, a.bins + slot * a.bins_cap, a.bins_cap,
+                        a.tiles_y, s_rb, s_rowcnt, s_rowoff);
+    }
     const int ng = MULTI ? a.h.n_groups : 1;
     const FoldCand *glist = a.list + slot * a.list_cap;
 #ifdef PP_STAMPS
@@ -1044,10 +1088,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
         }
     }
 #endif
-    for (int t = threadIdx.x; t < a.tiles; t += 256)  // untouched tiles: no block written
-        if (!((s_bits[t >> 5] >> (t & 31)) & 1u)) a.masks[fld * a.tiles + t] = 0ull;
+    if (!pre)
+        for (int t = threadIdx.x; t < a.tiles; t += 256)  // untouched tiles: no block written
+            if (!((s_bits[t >> 5] >> (t & 31)) & 1u)) a.masks[fld * a.tiles + t] = 0ull;
 
-    // ---- phase 2: touched tiles, one wave each, claimed from an LDS counter ----
+    // ---- phase 2: units of touched tiles, one wave each, claimed from an LDS counter ----
+    // A unit is a whole tile, or, for split fields (small batches, one group), a 16-row
+    // stripe of one: the four stripes of a busy tile then fold on four waves.  (Stripes for
+    // every batch measured slower: each stripe re-scans the tile's candidates; uniform cfg3
+    // CifHr 7.6 -> 9.1 ms per overlapped step.)
+    const int kParts = (!MULTI && a.split > 1) ? 4 : 1;
     FoldCand *cand = s_cand[wave];
     const int lx = lane & 7, ly = lane >> 3;
     const int nwords = (a.tiles + 31) >> 5;
@@ -1056,16 +1106,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
     while (true) {
         int claim = 0;
         if (lane == 0) claim = atomicAdd(&s_next, 1);
-        // this workgroup's claim-th tile is the field's (claim * split + part)-th touched one
-        claim = __builtin_amdgcn_readfirstlane(claim) * a.split + part;
-        // advance to the claim-th touched tile (claims grow, so the walk only moves on)
+        // this workgroup's claim-th unit is the field's (claim * split + part)-th one: stripe
+        // unit % kParts of the (unit / kParts)-th touched tile
+        const int unit = __builtin_amdgcn_readfirstlane(claim) * a.split + part;
+        const int target = unit / kParts, q = unit % kParts;
+        // advance to the target-th touched tile (claims grow, so the walk only moves on)
         int t = -1;
         while (wd < nwords) {
             if (!bits) {
                 if (++wd < nwords) bits = __builtin_amdgcn_readfirstlane(s_bits[wd]);
                 continue;
             }
-            if (li == claim) {
+            if (li == target) {
                 t = wd * 32 + __builtin_ctz(bits);
                 break;
             }
@@ -1074,6 +1126,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
         }
         if (t < 0) break;
         const int tx0 = (t % a.tiles_x) * kTile, ty0 = (t / a.tiles_x) * kTile;
+        const int kRows = kTile / kParts;
+        const int wy0 = ty0 + q * kRows;  // the unit's rows [wy0, wy0 + kRows)
+        const uint64_t unit_blocks = kParts == 1 ? ~0ull : (0xFFFFull << (16 * q));
         float *mp = a.map + (fld * a.tiles + t) * (int64_t)(kTile * kTile);
         float *ap = MULTI ? a.aux + (fld * a.tiles + t) * (int64_t)(kTile * kTile) : nullptr;
         uint64_t done = 0;  // blocks written by earlier passes
@@ -1094,7 +1149,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
                     c = src[e];
                     const int x0 = (int)(c.lo & 0xffff), x1 = (int)(c.hi & 0xffff) + 1;
                     const int y0 = (int)(c.lo >> 16), y1 = (int)(c.hi >> 16) + 1;
-                    hit = x1 > tx0 && x0 < tx0 + kTile && y1 > ty0 && y0 < ty0 + kTile;
+                    hit = x1 > tx0 && x0 < tx0 + kTile && y1 > wy0 && y0 < wy0 + kRows;
                 }
                 const uint64_t mk = __ballot(hit);
                 const int cnt = __popcll(mk);
@@ -1117,7 +1172,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
             uint64_t cl = 0ull;
             bool slow_l = false;
             if (lane < n) {
-                cl = cand_live(cand[lane], tx0, ty0);
+                cl = cand_live(cand[lane], tx0, ty0) & unit_blocks;
                 slow_l = cand_slow(cand[lane]);
             }
             const uint64_t slow = __ballot(slow_l);
@@ -1179,7 +1234,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
             }
             wave_sync();  // candidate arrays are rewritten by the next pass
         }
-        if (lane == 0) a.masks[fld * a.tiles + t] = done;
+        if (lane == 0) {
+            if (kParts == 1)
+                a.masks[fld * a.tiles + t] = done;
+            else  // the unit's 16 bits of the tile's mask (blocks 16 q .. 16 q + 15)
+                reinterpret_cast<uint16_t *>(&a.masks[fld * a.tiles + t])[q] = (uint16_t)(done >> (16 * q));
+        }
     }
     HR_STAMP(2 + wave);
 }
@@ -1369,6 +1429,22 @@ int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_confi
     const int64_t nf = (int64_t)n_img * K;
     a.split = sparse_split(nf);
     const unsigned nblocks = (unsigned)(nf * a.split);
+    // split fields: one list per field, built before the fold (cifhr_sparse_list_kernel);
+    // its lengths, tile bits and bin sizes go past the nf lists the prebuilt mode uses (the
+    // workspace holds nf * split of them)
+    const size_t pre_bytes = (size_t)nf * (1 + kTileBits / 32 + 2 * kMaxBinRows) * sizeof(int);
+    // (cfg2 uniform: CifHr stage 0.173 -> 0.125 ms with the prebuilt list and stripe units;
+    // planted unchanged within noise)
+    const bool prebuilt = a.split > 1 && h.n_groups == 1 &&
+                          (size_t)nf * (a.split - 1) * a.list_cap * sizeof(FoldCand) >= pre_bytes;
+    if (prebuilt) {
+        int *p = reinterpret_cast<int *>(a.list + nf * a.list_cap);
+        a.pre_total = p;
+        a.pre_bits = reinterpret_cast<uint32_t *>(p + nf);
+        a.pre_rowcnt = p + nf * (1 + kTileBits / 32);
+        a.pre_rowoff = a.pre_rowcnt + nf * kMaxBinRows;
+        hipLaunchKernelGGL(cifhr_sparse_list_kernel, dim3((unsigned)nf), dim3(256), 0, s, a);
+    }
 #ifdef PP_STAMPS
     uint64_t *st = nullptr;
     hipMalloc((void **)&st, (size_t)nblocks * 9 * sizeof(uint64_t));
