@@ -1010,10 +1010,12 @@ __device__ int hr_splat_list(const HrSparseArgs &a, int64_t fld, int64_t slot, u
     return running;
 }
 
-// Small batches (split > 1, one CifHr group): phase 1 once per field, into the field's
-// list / bins / tile bits in global memory, so that the split workgroups of
-// cifhr_sparse_kernel only fold.  Untouched tiles get their empty block masks here.
-__global__ __launch_bounds__(256) void cifhr_sparse_list_kernel(HrSparseArgs a) {
+// Phase 1 once per field (one CifHr group), into the field's list / bins / tile bits in
+// global memory (pre_*): for small batches (split > 1) before cifhr_sparse_kernel, whose
+// split workgroups then only fold, and for the dense map (pp_cifhr) before
+// cifhr_tile_kernel, in HrSplatArgs' layout (masks NULL).  Untouched tiles of the sparse map
+// get their empty block masks here.
+__global__ __launch_bounds__(256) void cifhr_list_kernel(HrSparseArgs a) {
     __shared__ uint32_t s_bits[kTileBits / 32];
     __shared__ RowBinLds s_rb;
     __shared__ __attribute__((aligned(16))) int s_cnt[2][kSpU][4];
@@ -1030,8 +1032,9 @@ __global__ __launch_bounds__(256) void cifhr_sparse_list_kernel(HrSparseArgs a) 
         rowcnt[threadIdx.x] = -1;
     if (threadIdx.x == 0) a.pre_total[fld] = total;
     if (threadIdx.x < kTileBits / 32) a.pre_bits[fld * (kTileBits / 32) + threadIdx.x] = s_bits[threadIdx.x];
-    for (int t = threadIdx.x; t < a.tiles; t += 256)  // untouched tiles: no block written
-        if (!((s_bits[t >> 5] >> (t & 31)) & 1u)) a.masks[fld * a.tiles + t] = 0ull;
+    if (a.masks)
+        for (int t = threadIdx.x; t < a.tiles; t += 256)  // untouched tiles: no block written
+            if (!((s_bits[t >> 5] >> (t & 31)) & 1u)) a.masks[fld * a.tiles + t] = 0ull;
 }
 
 template <bool MULTI>
@@ -1341,7 +1344,32 @@ int cifhr_heads_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config
     sa.tiles_y = (hh + kTile - 1) / kTile;
     sa.tiles = sa.tiles_x * sa.tiles_y;
     sa.bins_cap = sa.tiles_y <= kMaxBinRows ? bins_capacity(h.cif_cells()) : 0;
-    hipLaunchKernelGGL(cifhr_splats_kernel<DET>, dim3((unsigned)(nf * h.n_groups)), dim3(256), 0, s, sa);
+    if (!DET && h.n_groups == 1) {
+        // the decoder's phase 1 (hr_splat_list: 32 confidences per thread in flight, one
+        // barrier per round, kept cells staged in LDS), writing this layout
+        HrSparseArgs la{};
+        la.h = h;
+        la.hh = hh;
+        la.ww = ww;
+        la.v_th = sa.v_th;
+        la.neighbors = sa.neighbors;
+        la.list = sa.list;
+        la.list_cap = sa.list_cap;
+        la.bins = sa.bins;
+        la.bins_cap = sa.bins_cap;
+        la.tiles_x = sa.tiles_x;
+        la.tiles = sa.tiles;
+        la.tiles_y = sa.tiles_y;
+        la.split = 1;
+        la.pre_total = sa.counts;
+        la.pre_bits = sa.tile_bits;
+        la.pre_rowcnt = sa.rowcnt;
+        la.pre_rowoff = sa.rowoff;
+        if (sa.tiles > kTileBits) return fail(PP_ESHAPE, std::string(who) + ": CifHr map too large");
+        hipLaunchKernelGGL(cifhr_list_kernel, dim3((unsigned)nf), dim3(256), 0, s, la);
+    } else {
+        hipLaunchKernelGGL(cifhr_splats_kernel<DET>, dim3((unsigned)(nf * h.n_groups)), dim3(256), 0, s, sa);
+    }
     HrTileArgs a{};
     a.field = d_cifhr;
     a.list = sa.list;
@@ -1443,7 +1471,7 @@ int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_confi
         a.pre_bits = reinterpret_cast<uint32_t *>(p + nf);
         a.pre_rowcnt = p + nf * (1 + kTileBits / 32);
         a.pre_rowoff = a.pre_rowcnt + nf * kMaxBinRows;
-        hipLaunchKernelGGL(cifhr_sparse_list_kernel, dim3((unsigned)nf), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(cifhr_list_kernel, dim3((unsigned)nf), dim3(256), 0, s, a);
     }
 #ifdef PP_STAMPS
     uint64_t *st = nullptr;
