@@ -366,10 +366,10 @@ def main():
         'annotations_per_image': round(n_anns / max(1, args.steps * batch * world), 3)
         if stages & STAGE_GROW else None,
         # CifHr accumulation (the metric's "CifHr HBM GB/s"): CifHr.accumulated of the
-        # reference API, the dense (K, H', W') map, pp_cifhr = cifhr_splats_kernel +
+        # reference API, the dense (K, H', W') map, pp_cifhr = cifhr_list_kernel +
         # cifhr_tile_kernel, timed on its own over `steps` launches on the same batch
         'roofline': {
-            'bound': 'hbm', 'kernel': 'cifhr_splats_kernel + cifhr_tile_kernel (pp_cifhr)',
+            'bound': 'hbm', 'kernel': 'cifhr_list_kernel + cifhr_tile_kernel (pp_cifhr)',
             'achieved': round(dense_gbs, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
             'frac': round(dense_gbs / PEAK_HBM_GBS, 4), 'traffic': None,
             'algorithmic_bytes_per_launch': dense_bytes, 'ms_per_launch': round(dense_ms, 4),
@@ -422,7 +422,7 @@ def main():
         u_dense_ms = dense_cifhr_ms(ucif, cfg, stream, max(3, args.steps // 4), 1)
         u_gbs = dense_bytes / (u_dense_ms * 1e-3) / 1e9
         line['roofline_uniform'] = {
-            'bound': 'hbm', 'kernel': 'cifhr_splats_kernel + cifhr_tile_kernel (pp_cifhr), '
+            'bound': 'hbm', 'kernel': 'cifhr_list_kernel + cifhr_tile_kernel (pp_cifhr), '
                                       'uniform generator',
             'achieved': round(u_gbs, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
             'frac': round(u_gbs / PEAK_HBM_GBS, 4), 'ms_per_launch': round(u_dense_ms, 4),
@@ -564,7 +564,7 @@ def dense_cifhr_ms(cif, cfg, stream, steps, warmup):
 
 
 # roofline key -> the kernels whose PMC bytes it reports (tools/prof_summary.py)
-TRAFFIC_KERNELS = {'roofline': 'cifhr_splats_kernel+cifhr_tile_kernel',
+TRAFFIC_KERNELS = {'roofline': 'cifhr_list_kernel+cifhr_tile_kernel',
                    'roofline_decoder_cifhr': 'cifhr_sparse_kernel'}
 
 
