@@ -864,7 +864,7 @@ struct HrSparseArgs {
     int split;        // workgroups per field (small batches): each folds every split-th
                       // touched tile of the field
     // split > 1: the field's list, bins and tile bits are built once by
-    // cifhr_sparse_list_kernel (prebuilt; NULL: every split workgroup builds its own copy)
+    // cifhr_list_kernel (prebuilt; NULL: every split workgroup builds its own copy)
     int *pre_total;         // (n_img * K) list lengths
     uint32_t *pre_bits;     // (n_img * K, kTileBits / 32) touched tiles
     int *pre_rowcnt;        // (n_img * K, kMaxBinRows) bin sizes (-1: none), offsets
