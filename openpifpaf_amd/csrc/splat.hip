@@ -1458,7 +1458,7 @@ int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_confi
     const int64_t nf = (int64_t)n_img * K;
     a.split = sparse_split(nf);
     const unsigned nblocks = (unsigned)(nf * a.split);
-    // split fields: one list per field, built before the fold (cifhr_sparse_list_kernel);
+    // split fields: one list per field, built before the fold (cifhr_list_kernel);
     // its lengths, tile bits and bin sizes go past the nf lists the prebuilt mode uses (the
     // workspace holds nf * split of them)
     const size_t pre_bytes = (size_t)nf * (1 + kTileBits / 32 + 2 * kMaxBinRows) * sizeof(int);
