@@ -304,6 +304,23 @@ int pp_decode_multi(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs,
  * objects, mutated).  Workspace as pp_decode_multi (pp_decode_multi_workspace_size).
  * Reference interface: openpifpaf.decoder.CifCaf.__call__ (cifcaf.py:67).
  */
+/*
+ * Byte offset, inside a decode workspace of that shape, of the (n_img, ann_capacity) pp_ann
+ * working records: after a decode with the grow stage, image img's annotation list before
+ * NMS (positions as d_out_index reports them), in the state NMS left every one of them in,
+ * including those it dropped (nms.py:20-53 edits the Annotation objects in place before it
+ * filters them).  Valid until the next decode into the workspace.  pp_decode_work_offset
+ * for pp_decode_batch / pp_decode_stages workspaces, pp_decode_multi_work_offset for
+ * pp_decode_multi / pp_decode_initial ones; 0 on a bad shape.
+ * Reference interface: the initial_annotations objects CifCaf.__call__ mutates
+ * (cifcaf.py:67-71, 95-98, 117-118).
+ */
+size_t pp_decode_work_offset(int32_t n_img, int32_t K, int32_t C, int32_t H, int32_t W,
+                             const pp_config *cfg, int32_t ann_capacity);
+size_t pp_decode_multi_work_offset(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs,
+                                   int32_t n_img, int32_t K, int32_t C, const pp_config *cfg,
+                                   int32_t ann_capacity);
+
 int pp_decode_initial(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs, int32_t n_img,
                       int32_t K, int32_t C, const int32_t *skeleton, const pp_config *cfg,
                       float *d_cifhr, pp_ann *d_anns, int32_t ann_capacity, int32_t *d_counts,

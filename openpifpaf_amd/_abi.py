@@ -113,6 +113,14 @@ def make_config(*, cif_threshold=0.1, seed_threshold=0.2, seed_score_scale=1.0,
         int(occupancy_reduction), int(occupancy_min_scale), seed_skip_mask(seed_mask))
 
 
+def check_seed_mask(seed_mask, k):
+    """The reference indexes seed_mask[field_i] for every one of the K fields
+    (cif_seeds.py:28-29): a shorter mask raises its IndexError on every path here too."""
+    if seed_mask is not None and len(seed_mask) < k:
+        raise IndexError('list index out of range (seed_mask has {} entries for {} fields)'
+                         .format(len(seed_mask), k))
+
+
 def seed_skip_mask(seed_mask):
     """pp_config.seed_skip_mask of FieldConfig.seed_mask: bit f set where seed_mask[f] is
     falsy (cif_seeds.py:28-29); None = every field seeds."""

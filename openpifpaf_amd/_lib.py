@@ -44,6 +44,8 @@ _SIGNATURES = {
                         ctypes.c_int),
     'pp_decode_workspace_size': ([_i32, _i32, _i32, _i32, _i32, _vp, _i32], _sz),
     'pp_decode_workspace_zero_offset': ([_i32, _i32, _i32, _i32, _i32, _vp, _i32], _sz),
+    'pp_decode_work_offset': ([_i32, _i32, _i32, _i32, _i32, _vp, _i32], _sz),
+    'pp_decode_multi_work_offset': ([_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32], _sz),
     'pp_decode_batch': ([_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp,
                          _vp, _vp, _sz, _vp], ctypes.c_int),
     'pp_decode_stages': ([_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp,

@@ -2808,6 +2808,25 @@ size_t pp_decode_workspace_zero_offset(int32_t n_img, int32_t K, int32_t C, int3
                        ann_capacity).off_occ;
 }
 
+size_t pp_decode_work_offset(int32_t n_img, int32_t K, int32_t C, int32_t H, int32_t W,
+                             const pp_config *cfg, int32_t ann_capacity) {
+    if (!cfg || n_img <= 0 || K <= 0 || C <= 0 || H <= 0 || W <= 0 || ann_capacity <= 0 ||
+        cfg->stride <= 0)
+        return 0;
+    return make_layout(n_img, K, C, single_head(nullptr, nullptr, H, W, cfg->stride), cfg,
+                       ann_capacity).off_work;
+}
+
+size_t pp_decode_multi_work_offset(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs,
+                                   int32_t n_img, int32_t K, int32_t C, const pp_config *cfg,
+                                   int32_t ann_capacity) {
+    Heads h;
+    if (!cfg || make_heads(scales, n_scales, cif_pairs, 3, &h, "pp_decode_multi_work_offset") ||
+        n_img <= 0 || K <= 0 || C <= 0 || ann_capacity <= 0)
+        return 0;
+    return make_layout(n_img, K, C, h, cfg, ann_capacity).off_work;
+}
+
 size_t pp_decode_multi_workspace_size(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs,
                                       int32_t n_img, int32_t K, int32_t C, const pp_config *cfg,
                                       int32_t ann_capacity) {

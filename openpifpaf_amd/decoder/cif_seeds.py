@@ -4,7 +4,7 @@ import numpy as np
 import torch
 
 from .. import _device
-from .._abi import SEED_DTYPE, make_config, scale_list
+from .._abi import SEED_DTYPE, check_seed_mask, make_config, scale_list
 from .._lib import call
 from ._fields import batch1, cfg_ptr, head_scales, pitched_hr, with_geometry
 from .field_config import FieldConfig
@@ -38,6 +38,7 @@ class CifSeeds:
         """pp_seeds_multi over the CIF entries of `arr`; the seeds of fields whose
         seed_mask entry is falsy are dropped (cif_seeds.py:28-29; the kernel's order is
         the sorted order, which dropping entries keeps)."""
+        check_seed_mask(seed_mask, k)
         hr = pitched_hr(self.cifhr)
         out = torch.empty(max(1, cap) * SEED_DTYPE.itemsize, dtype=torch.uint8, device=device)
         count = torch.zeros(1, dtype=torch.int32, device=device)
@@ -48,7 +49,7 @@ class CifSeeds:
         recs = np.frombuffer(out[:n * SEED_DTYPE.itemsize].cpu().numpy().tobytes(),
                              dtype=SEED_DTYPE)
         if seed_mask is not None:
-            keep = np.array([bool(m) for m in seed_mask] + [False] * k)[:k]
+            keep = np.array([bool(m) for m in seed_mask[:k]])
             recs = recs[keep[recs['field']]]
         self.seeds.extend((v, int(f), x, y, s) for v, f, x, y, s in
                           zip(recs['v'], recs['field'], recs['x'], recs['y'], recs['s']))

@@ -14,8 +14,9 @@ import time
 import numpy as np
 
 from ... import _device
-from ..._abi import PACK_ALL, make_config, skeleton_array
+from ..._abi import PACK_ALL, check_seed_mask, make_config, skeleton_array
 from ...annotation import Annotation
+from ...distributed import decode_sharded, shard
 from ...engine import HeadSet, InitialAnnotations, engine
 from ...functional import grow_connection_blend
 from .. import nms as nms_module
@@ -73,6 +74,7 @@ class CifCaf(Generator):
         if CifSeeds.threshold is None:
             raise TypeError('CifSeeds.threshold is not configured (decoder.configure sets it)')
         nms = self.nms
+        check_seed_mask(self.field_config.seed_mask, len(self.keypoints))
         return make_config(
             cif_threshold=CifHr.v_threshold,
             seed_threshold=CifSeeds.threshold,
@@ -117,7 +119,9 @@ class CifCaf(Generator):
         """cifcaf.py:67-71, 95-98: the initial annotations are grown first, marked occupied
         and kept in the annotation list (pp_decode_initial).  As in the reference, the
         returned list holds the same initial Annotation objects, mutated (grown, completed,
-        NMS-suppressed); one that NMS drops keeps its input state here."""
+        NMS-suppressed); one that NMS drops is mutated too (the reference edits the objects
+        in place before filtering, nms.py:20-53), from the decode's working records
+        (pp_decode_multi_work_offset)."""
         init = InitialAnnotations([np.stack([a.to_record() for a in initial])],
                                   _device.require())
         skel = skeleton_array(self.skeleton)
@@ -140,6 +144,10 @@ class CifCaf(Generator):
                 out.append(initial[idx].update_from_record(rec))
             else:
                 out.append(Annotation.from_record(rec, self.keypoints, self.out_skeleton))
+        dropped = sorted(set(range(len(initial))) - set(int(i) for i in index))
+        if dropped:
+            for i, rec in zip(dropped, b.work_records(0, dropped)):
+                initial[i].update_from_record(rec)
         return out
 
     def decode_records(self, cif_batch, caf_batch, keep_cifhr=False, compact=None):
@@ -166,22 +174,70 @@ class CifCaf(Generator):
                         for r in recs[offsets[i]:offsets[i + 1]]])
         return out
 
-    def decode_heads(self, heads):
-        """Generator.batch: the model's head list (each (B, ...)) through the FieldConfig."""
+    def decode_heads(self, heads, *, group=None, dst=0, local=False):
+        """Generator.batch: the model's head list (each (B, ...)) through the FieldConfig.
+        `group` / `dst` / `local`: image-sharded over a process group (decode_batch)."""
+        kw = {} if group is None else {'group': group, 'dst': dst, 'local': local}
+        if heads is None:  # this rank's shard of a sharded batch is empty
+            return self.decode_batch(None, None, **kw)
         if self.field_config.is_single_scale():
             cif_i, caf_i, _ = self.field_config.single_scale()
-            return self.decode_batch(heads[cif_i], heads[caf_i])
+            return self.decode_batch(heads[cif_i], heads[caf_i], **kw)
         used = set(self.field_config.cif_indices) | set(self.field_config.caf_indices)
-        return self.decode_fields_batch([h if i in used else None for i, h in enumerate(heads)])
+        return self.decode_fields_batch([h if i in used else None for i, h in enumerate(heads)],
+                                        **kw)
 
-    def decode_batch(self, cif_batch, caf_batch):
-        """(B, K, 5, H, W) + (B, C, 9, H, W) -> one list of Annotation per image."""
-        recs, offsets, _ = self.decode_records(cif_batch, caf_batch, compact=PACK_ALL)
-        return self.annotations_from_records(recs, offsets)
+    def decode_batch(self, cif_batch, caf_batch, *, group=None, dst=0, local=False):
+        """(B, K, 5, H, W) + (B, C, 9, H, W) -> one list of Annotation per image.
 
-    def decode_fields_batch(self, fields_batch):
-        """Batched head outputs of any FieldConfig -> one list of Annotation per image."""
-        recs, offsets, _ = self.decode_fields_records(fields_batch, compact=PACK_ALL)
+        With a torch.distributed process `group` (e.g. `dist.group.WORLD`: one rank per
+        GPU, nccl = RCCL over xGMI, or gloo), the batch is image-sharded: each rank decodes
+        its contiguous `distributed.shard` of the B images (every rank passes the whole
+        batch; `local=True`: the arguments are already this rank's images, possibly None
+        for none), and rank `dst` returns the annotation lists of all images in rank order,
+        gathered as compact records whose digests it checks (distributed.decode_sharded;
+        GatherMismatch on a mismatch).  Other ranks return None.  This replaces the
+        reference's worker_pool.starmap over the batch (generator.py:96-97)."""
+        if group is None:
+            recs, offsets, _ = self.decode_records(cif_batch, caf_batch, compact=PACK_ALL)
+            return self.annotations_from_records(recs, offsets)
+        n = 0 if cif_batch is None else len(cif_batch)
+        return self._decode_sharded(
+            n, lambda a, b: (_device.to_device(cif_batch[a:b]).contiguous(),
+                             _device.to_device(caf_batch[a:b]).contiguous(), None),
+            group, dst, local)
+
+    def decode_fields_batch(self, fields_batch, *, group=None, dst=0, local=False):
+        """Batched head outputs of any FieldConfig -> one list of Annotation per image
+        (`group` / `dst` / `local`: image-sharded, as decode_batch)."""
+        if group is None:
+            recs, offsets, _ = self.decode_fields_records(fields_batch, compact=PACK_ALL)
+            return self.annotations_from_records(recs, offsets)
+        n = 0 if fields_batch is None else len(
+            fields_batch[self.field_config.cif_indices[0]])
+
+        def take(a, b):
+            fields = [None if f is None else _device.to_device(f[a:b]).contiguous()
+                      for f in fields_batch]
+            return None, None, HeadSet(fields, self.field_config)
+        return self._decode_sharded(n, take, group, dst, local)
+
+    def _decode_sharded(self, n, take, group, dst, local):
+        import torch.distributed as dist  # pylint: disable=import-outside-toplevel
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        a, b = (0, n) if local else shard(n, rank, world)
+        cfg, skel = self.config(), skeleton_array(self.skeleton)
+
+        def decode_local(device_out):
+            cif, caf, heads = take(a, b)
+            _, pending = engine().decode_async(cif, caf, skel, cfg, heads=heads,
+                                               compact=PACK_ALL, device_out=device_out)
+            return pending
+        self.last_gather = {}
+        recs, offsets = decode_sharded(decode_local, b - a, dist, group=group, dst=dst,
+                                       report=self.last_gather)
+        if recs is None:
+            return None
         return self.annotations_from_records(recs, offsets)
 
     # -- reference building blocks, on the device ------------------------------------------

@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from ... import _device
-from ..._abi import DET_DTYPE, DetNms, make_config
+from ..._abi import DET_DTYPE, DetNms, check_seed_mask, make_config
 from ..._lib import PPError, call, load
 from ...annotation import AnnotationDet
 from .. import nms
@@ -43,6 +43,7 @@ class CifDet(Generator):
             raise TypeError("'>' not supported between instances of 'float' and 'NoneType' "
                             "(CifSeeds.threshold is not configured)")
         _, _, stride = self.field_config.single_scale()
+        check_seed_mask(self.field_config.seed_mask, len(self.categories))
         return make_config(cif_threshold=CifHr.v_threshold, seed_threshold=CifSeeds.threshold,
                            seed_score_scale=CifSeeds.score_scale, stride=int(stride),
                            cif_neighbors=CifHr.neighbors, seed_mask=self.field_config.seed_mask)
@@ -84,8 +85,10 @@ class CifDet(Generator):
         return [[AnnotationDet.from_record(r, self.categories)
                  for r in recs[offsets[i]:offsets[i + 1]]] for i in range(len(offsets) - 1)]
 
-    def decode_heads(self, heads):
+    def decode_heads(self, heads, *, group=None, **_):
         """Generator.batch: the model's head list (each (B, ...)); reads the CifDet head."""
+        if group is not None:
+            raise NotImplementedError('image-sharded decoding is implemented for CifCaf only')
         cif_i, _, _ = self.field_config.single_scale()
         return self.decode_batch(heads[cif_i])
 

@@ -10,6 +10,8 @@ import time
 
 import torch
 
+from ...distributed import shard
+
 LOG = logging.getLogger(__name__)
 
 
@@ -75,15 +77,26 @@ class Generator:
         annotations per image; the subclass reads the heads its FieldConfig names."""
         raise NotImplementedError()
 
-    def batch(self, model, image_batch, *, device=None):
+    def batch(self, model, image_batch, *, device=None, group=None, dst=0):
         """From image batch straight to annotations batch (generator.py:84-101): the head
         list of any FieldConfig (single-scale, dense connections, multi-scale) is decoded
-        as one device batch instead of per image over a worker pool."""
+        as one device batch instead of per image over a worker pool.
+
+        With a torch.distributed process `group` (one rank per GPU), every rank passes the
+        same image batch, runs the model on its `distributed.shard` of the images only and
+        decodes them, and rank `dst` returns the annotation lists of the whole batch
+        (CifCaf.decode_batch); the other ranks return None."""
+        if group is not None:
+            import torch.distributed as dist  # pylint: disable=import-outside-toplevel
+            a, b = shard(len(image_batch), dist.get_rank(group), dist.get_world_size(group))
+            image_batch = image_batch[a:b]
         start_nn = time.perf_counter()
-        heads = self._heads(model, image_batch, device=device)
+        heads = (self._heads(model, image_batch, device=device)
+                 if group is None or len(image_batch) else None)
         self.last_nn_time = time.perf_counter() - start_nn
         start = time.perf_counter()
-        result = self.decode_heads(heads)
+        result = (self.decode_heads(heads) if group is None else
+                  self.decode_heads(heads, group=group, dst=dst, local=True))
         self.last_decoder_time = time.perf_counter() - start
         LOG.debug('time: nn = %.3fs, dec = %.3fs', self.last_nn_time, self.last_decoder_time)
         return result

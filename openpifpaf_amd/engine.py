@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 from . import _device
-from ._abi import (ANN_DTYPE, PP_ST_ANN_OVERFLOW, PP_ST_DEC_OVERFLOW,
+from ._abi import (ANN_DTYPE, PACK_ALL, PP_ST_ANN_OVERFLOW, PP_ST_DEC_OVERFLOW,
                    PP_ST_NMS_OVERFLOW, packed_dtype, scale_list, skeleton_array)
 from ._lib import PPError, call, load
 
@@ -44,11 +44,13 @@ class DecodeBuffers:
         if heads is None:
             size = lib.pp_decode_workspace_size(n, k, c, h, w, ctypes.byref(cfg), cap)
             zero_off = lib.pp_decode_workspace_zero_offset(n, k, c, h, w, ctypes.byref(cfg), cap)
+            self.work_off = lib.pp_decode_work_offset(n, k, c, h, w, ctypes.byref(cfg), cap)
             stride = cfg.stride
         else:
             args = (heads.arr, len(heads.arr), heads.pairs, n, k, c, ctypes.byref(cfg), cap)
             size = lib.pp_decode_multi_workspace_size(*args)
             zero_off = lib.pp_decode_multi_workspace_zero_offset(*args)
+            self.work_off = lib.pp_decode_multi_work_offset(*args)
             stride = heads.stride0
         if size == 0:
             raise PPError('pp_decode_workspace_size rejected the shape: ' +
@@ -68,6 +70,16 @@ class DecodeBuffers:
         self.pitch = int(lib.pp_cifhr_pitch(self.ww))
         self.cifhr = None
         self.out_index = None  # pp_decode_initial's (n, cap) positions before NMS
+
+    def work_records(self, img, positions):
+        """pp_decode_work_offset: image img's annotations at `positions` of its list before
+        NMS, in the state NMS left them (ANN_DTYPE, host), after a decode with the grow
+        stage and before the next decode into this workspace."""
+        rows = self.ws[self.work_off:self.work_off + self.n * self.cap * ANN_DTYPE.itemsize]
+        rows = rows.view(self.n * self.cap, ANN_DTYPE.itemsize)
+        idx = torch.as_tensor([img * self.cap + int(p) for p in positions], dtype=torch.int64,
+                              device=rows.device)
+        return rows.index_select(0, idx).cpu().numpy().reshape(-1).view(ANN_DTYPE)
 
     anns = property(lambda self: self._slots[self._cur][0])
     counts = property(lambda self: self._slots[self._cur][1])
@@ -189,8 +201,14 @@ class DecodeEngine:
         if initial.n != n:
             raise ValueError('initial annotations for {} images, batch has {}'.format(
                 initial.n, n))
-        if b.out_index is None or b.out_index.numel() < n * cap:
-            b.out_index = torch.empty(n * cap, dtype=torch.int32, device=b.ws.device)
+        # out_index is exactly (n * cap) long, image i's rows at [i * cap, (i + 1) * cap) as
+        # the kernel writes them (the store behind it only grows)
+        store = getattr(b, '_out_index_store', None)
+        if store is None or store.numel() < n * cap:
+            store = b._out_index_store = torch.empty(n * cap, dtype=torch.int32,
+                                                     device=b.ws.device)
+        b.out_index = store[:n * cap]
+        b.out_index_cap = cap
         call('pp_decode_initial', arr, len(arr), pairs, n, k, c,
              skel.ctypes.data_as(ctypes.c_void_p), ctypes.byref(cfg), _device.ptr(hr),
              _device.ptr(b.anns), cap, _device.ptr(b.counts), _device.ptr(b.status),
@@ -222,13 +240,11 @@ class DecodeEngine:
              _device.stream())
         return b
 
-    def decode(self, cif, caf, skeleton, cfg, cap=None, keep_cifhr=False, heads=None,
-               compact=None, initial=None):
-        """Full decode with overflow retry.  Returns (records, offsets, buffers).  With a
-        HeadSet `heads`, cif / caf are ignored and the multi-scale decode runs.  `compact`
-        flags (e.g. _abi.PACK_ALL) fetch compact records (pp_pack_compact) instead of full
-        pp_ann records.  `initial` (InitialAnnotations): grown before the seed loop; the
-        buffers then hold out_index (see pp_decode_initial)."""
+    def launch_checked(self, cif, caf, skeleton, cfg, cap=None, keep_cifhr=False, heads=None,
+                       initial=None):
+        """launch / launch_multi with overflow retry (the annotation capacity doubles until
+        no image overflows); returns the DecodeBuffers of a decode whose records are
+        complete.  Raises PPError on the overflows a retry cannot fix."""
         h, w = (cif.shape[3], cif.shape[4]) if heads is None else (heads.h, heads.w)
         cap = cap or default_ann_capacity(h, w)
         while True:
@@ -248,10 +264,31 @@ class DecodeEngine:
                           'the field); status={}'.format(status.tolist()))
         if (status & PP_ST_DEC_OVERFLOW).any():
             raise PPError('decoding/frontier order exceeded the record capacity')
+        return b
+
+    def decode(self, cif, caf, skeleton, cfg, cap=None, keep_cifhr=False, heads=None,
+               compact=None, initial=None):
+        """Full decode with overflow retry.  Returns (records, offsets, buffers).  With a
+        HeadSet `heads`, cif / caf are ignored and the multi-scale decode runs.  `compact`
+        flags (e.g. _abi.PACK_ALL) fetch compact records (pp_pack_compact) instead of full
+        pp_ann records.  `initial` (InitialAnnotations): grown before the seed loop; the
+        buffers then hold out_index (see pp_decode_initial)."""
+        b = self.launch_checked(cif, caf, skeleton, cfg, cap=cap, keep_cifhr=keep_cifhr,
+                                heads=heads, initial=initial)
         k = cif.shape[1] if heads is None else heads.k
         recs, offsets = self.fetch(b, None if compact is None else
                                    (k, len(skeleton_array(skeleton)), compact))
         return recs, offsets, b
+
+    def decode_async(self, cif, caf, skeleton, cfg, heads=None, compact=PACK_ALL,
+                     device_out=False):
+        """decode() up to the record pack: (buffers, PendingRecords of compact records, or
+        full ones with compact=None).  `device_out` packs into device memory (what a
+        multi-GPU rank sends, distributed.decode_sharded)."""
+        b = self.launch_checked(cif, caf, skeleton, cfg, heads=heads)
+        k = cif.shape[1] if heads is None else heads.k
+        spec = None if compact is None else (k, len(skeleton_array(skeleton)), compact)
+        return b, self.fetch_async(b, spec, device_out=device_out)
 
     @staticmethod
     def fetch(b, compact=None):

@@ -572,9 +572,10 @@ API_INIT_PREV = dict(h=40, w=40, n_people=8, seed=6)
 
 
 def api_initial_annotations(prev_anns, annotation_cls, keypoints, skeleton):
-    """Three tracking-style initial annotations from a previous decode: (0) the first
+    """Four tracking-style initial annotations, three from a previous decode: (0) the first
     annotation cut to joints 0-4, its decoding / frontier orders cut to match; (1) one joint
-    of the second annotation, moved; (2) the third annotation shifted 4 px, orders cleared."""
+    of the second annotation, moved; (2) the third annotation shifted 4 px, orders cleared;
+    (3) a weak lone joint that predict-mode NMS drops."""
     import copy  # pylint: disable=import-outside-toplevel
     a0 = copy.deepcopy(prev_anns[0])
     a0.data[5:] = 0.0
@@ -590,7 +591,11 @@ def api_initial_annotations(prev_anns, annotation_cls, keypoints, skeleton):
     a2.data[a2.data[:, 2] > 0, 0] += 4.0
     a2.decoding_order = []
     a2.frontier_order = []
-    return [a0, a1, a2]
+    # (3) a weak lone joint in the corner: score 3 * 0.05 / 23 < the predict-mode
+    # instance_threshold, so nms.Keypoints drops it there after editing it in place
+    a3 = annotation_cls(keypoints, skeleton).add(0, (1.0, 1.0, 0.05))
+    a3.joint_scales[0] = 2.0
+    return [a0, a1, a2, a3]
 
 
 def gen_api(op):
@@ -621,6 +626,12 @@ def gen_api(op):
                'init_index': np.array([ids.get(id(a), -1) for a in anns], np.int64)}
         out.update({'init_' + k[4:]: v for k, v in ins.items()})
         out.update(ann_arrays(anns, len(skel)))
+        # every initial object after the call, also those NMS dropped (the reference edits
+        # them in place before filtering, nms.py:20-53)
+        fin = ann_arrays(init, len(skel))
+        fin['ann_n_decoding'] = np.array([len(a.decoding_order) for a in init], np.int64)
+        fin['ann_n_frontier'] = np.array([len(a.frontier_order) for a in init], np.int64)
+        out.update({'final_' + k[4:]: v for k, v in fin.items()})
         np.savez_compressed(os.path.join(HERE, 'api_initial_%s.npz' % mode), **out)
         print('api initial', mode, len(prev), '->', len(anns), 'init at',
               out['init_index'][out['init_index'] >= 0].tolist())

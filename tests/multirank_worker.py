@@ -19,6 +19,35 @@ from openpifpaf_amd.engine import DecodeEngine  # noqa: E402
 N = 32
 
 
+def _ann_bytes(lists):
+    return [[a.to_record().tobytes() for a in anns] for anns in lists]
+
+
+def api_main(rank, world, cif, caf):
+    """The library's sharded API: CifCaf.decode_batch(group=) and Generator.batch(group=)
+    (the model stand-in maps image indices to their fields), checked on rank 0 against a
+    one-process decode of the whole batch, annotation record by record."""
+    from openpifpaf_amd import decoder
+    decoder.CifSeeds.threshold = 0.2
+    decoder.CifCaf.force_complete = True
+    cc = decoder.CifCaf(decoder.FieldConfig(), keypoints=constants.COCO_KEYPOINTS,
+                        skeleton=constants.COCO_PERSON_SKELETON)
+    got = cc.decode_batch(cif, caf, group=dist.group.WORLD)
+    got_b = cc.batch(lambda idx: [cif[idx], caf[idx]], torch.arange(N), device='cuda',
+                     group=dist.group.WORLD)
+    if rank == 0:
+        assert cc.last_gather['ranks_verified'] == world, cc.last_gather
+        ref = cc.decode_batch(cif, caf)
+        assert len(got) == len(got_b) == len(ref) == N
+        assert _ann_bytes(got) == _ann_bytes(ref), 'decode_batch(group=) differs'
+        assert _ann_bytes(got_b) == _ann_bytes(ref), 'batch(group=) differs'
+        print('multirank ok: api, {} annotations, world {}'.format(
+            sum(len(a) for a in ref), world), flush=True)
+    else:
+        assert got is None and got_b is None
+    dist.destroy_process_group()
+
+
 def main():
     rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
     dist.init_process_group('gloo')
@@ -29,6 +58,9 @@ def main():
     cu, au = synthetic.batch('uniform', N // 2, 80, 80, first_seed=N // 2)
     cif = torch.from_numpy(np.concatenate([cp, cu])).cuda()
     caf = torch.from_numpy(np.concatenate([ap, au])).cuda()
+    if len(sys.argv) > 1 and sys.argv[1] == 'api':
+        api_main(rank, world, cif, caf)
+        return
     a, b = shard(N, rank, world)
     eng = DecodeEngine()
     buf = eng.launch(cif[a:b].contiguous(), caf[a:b].contiguous(), skel, cfg)

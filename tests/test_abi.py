@@ -140,6 +140,11 @@ def test_scale_struct_and_multi_workspace():
     one = scale_list([(0, 41, 41)], [(0, 41, 41)], [8], [8])
     assert (lib.pp_decode_multi_workspace_size(one, 2, 0, 2, 17, 19, ctypes.byref(cfg), 128)
             == lib.pp_decode_workspace_size(2, 17, 19, 41, 41, ctypes.byref(cfg), 128))
+    # ... and puts its working records at the same place (pp_decode_initial into a
+    # single-scale engine workspace; CifCaf reads NMS-dropped initial annotations there)
+    work = lib.pp_decode_work_offset(2, 17, 19, 41, 41, ctypes.byref(cfg), 128)
+    assert 0 < work < lib.pp_decode_workspace_size(2, 17, 19, 41, 41, ctypes.byref(cfg), 128)
+    assert work == lib.pp_decode_multi_work_offset(one, 2, 0, 2, 17, 19, ctypes.byref(cfg), 128)
     # pairs need an even CIF head count; no CAF head is rejected
     odd = scale_list([(0, 41, 41)] * 3, [(0, 41, 41)], [8] * 3, [8])
     assert lib.pp_decode_multi_workspace_size(odd, 4, 1, 1, 17, 19, ctypes.byref(cfg), 128) == 0

@@ -203,3 +203,20 @@ def test_fields_batch_indexes_by_image():
         assert torch.equal(f[0], heads[0][i]) and f[1] is None
         assert f[2][0].shape == (2, 5) and torch.equal(f[2][1][0], heads[2][1][0][i])
         assert f[0].data_ptr() == heads[0][i].data_ptr()  # a view, not a copy
+
+
+def test_short_seed_mask_raises_index_error():
+    """The reference reads seed_mask[field_i] for every field (cif_seeds.py:28-29): a mask
+    shorter than K raises IndexError on every path."""
+    from openpifpaf_amd import constants, decoder
+    from openpifpaf_amd._abi import check_seed_mask
+    decoder.CifSeeds.threshold = 0.2
+    cc = decoder.CifCaf(decoder.FieldConfig(seed_mask=[1] * 5),
+                        keypoints=constants.COCO_KEYPOINTS,
+                        skeleton=constants.COCO_PERSON_SKELETON)
+    with pytest.raises(IndexError):
+        cc.config()
+    check_seed_mask([1] * 17, 17)
+    check_seed_mask(None, 17)
+    with pytest.raises(IndexError):
+        check_seed_mask([0] * 16, 17)

@@ -12,7 +12,8 @@ import torch.multiprocessing as mp
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from openpifpaf_amd._abi import ANN_DTYPE, PACK_ALL, packed_dtype  # noqa: E402
-from openpifpaf_amd.distributed import (digest, expand_compact, gather_packed,  # noqa: E402
+from openpifpaf_amd.distributed import (GatherMismatch, decode_sharded,  # noqa: E402
+                                        digest, expand_compact, gather_packed,
                                         gather_records, shard)
 
 
@@ -64,6 +65,12 @@ def _worker(rank, world, port, n_imgs, kind):
     try:
         if kind == 'mixed':
             _mixed_worker(rank, world, n_imgs)
+            return
+        if kind == 'records_mixed':
+            _records_mixed_worker(rank, world, n_imgs)
+            return
+        if kind.startswith('sharded'):
+            _sharded_worker(rank, world, n_imgs, kind)
             return
         dtype = DTYPES[kind]
         recs, offs = _rank_records(rank, n_imgs[rank], dtype)
@@ -118,6 +125,133 @@ def _mixed_worker(rank, world, n_imgs):
     assert got.dtype == ANN_DTYPE
     assert got.tobytes() == b''.join(e.tobytes() for e in exp)
     assert got_offs[-1] == len(got)
+
+
+def _records_mixed_worker(rank, world, n_imgs):
+    """gather_records with per-rank formats: rank 0 holds full records (its
+    pack was refetched), the others compact ones; rank 0 learns each rank's layout from
+    the metadata and expands the compact ones."""
+    recs, offs = _compact_records(rank, n_imgs[rank])
+    if rank == 0:
+        recs = expand_compact(recs)
+    report = {}
+    got, got_offs = gather_records(recs, offs, dist, torch.device('cpu'), report=report)
+    if rank != 0:
+        assert got is None
+        return
+    assert report['full_records'] and report['ranks_verified'] == world
+    exp, base = [], 0
+    for r in range(world):
+        e = expand_compact(_compact_records(r, n_imgs[r])[0], 17, 19)
+        e['image'] += base
+        base += n_imgs[r]
+        exp.append(e)
+    assert got.dtype == ANN_DTYPE
+    assert got.tobytes() == b''.join(e.tobytes() for e in exp)
+    assert got_offs.tolist() == np.concatenate(
+        [[0], np.cumsum([c for r in range(world) for c in np.diff(_compact_records(r, n_imgs[r])[1])])]).tolist()
+
+
+class _FakePending:
+    """The PendingRecords surface decode_sharded reads: a finished compact pack in host
+    memory (what a gloo rank holds)."""
+
+    def __init__(self, recs, offs, refetch=False):
+        self.dtype = recs.dtype
+        self.device_records = None
+        self._host = torch.from_numpy(recs.view(np.uint8).reshape(-1).copy())
+        self._counts = np.diff(offs).astype(np.int64)
+        self.refetch = refetch
+        self._full = expand_compact(recs) if refetch else None
+
+    def wait(self):
+        return self._counts
+
+    def fits(self, total):
+        return True
+
+    def host_records(self):
+        return self._host
+
+    def full_device_records(self):
+        return torch.from_numpy(self._full.view(np.uint8).reshape(-1).copy())
+
+
+def _sharded_worker(rank, world, n_imgs, kind):
+    """decode_sharded with a stand-in for the device decode: rank r 'decodes' its shard of
+    a global batch into the compact records _compact_records(r, ...) would hold; rank 0
+    gets every rank's records, image indices rebased, and the digests checked."""
+    n_total = sum(n_imgs)
+    a, b = shard(n_total, rank, world)
+    recs, offs = _compact_records(rank, b - a)
+    refetch = kind == 'sharded_refetch' and rank == world - 1
+    calls = []
+
+    def decode_local(device_out):
+        calls.append(device_out)
+        return _FakePending(recs, offs, refetch)
+
+    report = {}
+    got, got_offs = decode_sharded(decode_local, b - a, dist, report=report)
+    assert calls == ([False] if b > a else [])  # gloo: records stay in host memory
+    if rank != 0:
+        assert got is None and got_offs is None
+        return
+    assert report['ranks_seen'] == world and report['ranks_verified'] == world
+    # one rank's full records turn the result into full records (if it had any)
+    la, lb = shard(n_total, world - 1, world)
+    any_full = kind == 'sharded_refetch' and len(_compact_records(world - 1, lb - la)[0]) > 0
+    exp, base, counts = [], 0, []
+    for r in range(world):
+        ra, rb = shard(n_total, r, world)
+        e, eo = _compact_records(r, rb - ra)
+        if any_full:
+            e = expand_compact(e)
+        e['image'] += base
+        base += rb - ra
+        exp.append(e)
+        counts.extend(np.diff(eo).tolist())
+    assert got.dtype == exp[0].dtype
+    assert got.tobytes() == b''.join(e.tobytes() for e in exp)
+    assert got_offs.tolist() == np.concatenate([[0], np.cumsum(counts)]).astype(int).tolist()
+
+
+def _corrupt_worker(rank, world, port):
+    """A sender whose digest does not match its bytes: rank 0 raises GatherMismatch."""
+    dist.init_process_group('gloo', init_method='tcp://127.0.0.1:{}'.format(port),
+                            rank=rank, world_size=world)
+    try:
+        recs, offs = _compact_records(rank, 3)
+        import openpifpaf_amd.distributed as D
+        if rank == 1:
+            real = D.digest
+            D.digest = lambda t: real(t) + 1
+        try:
+            decode_sharded(lambda _: _FakePending(recs, offs), 3, dist)
+        except GatherMismatch:
+            assert rank == 0
+            return
+        assert rank != 0, 'rank 0 accepted a corrupted transfer'
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('n_imgs', [(4, 4), (3, 4), (1, 0), (3, 3, 3)])
+@pytest.mark.parametrize('kind', ['sharded', 'sharded_refetch'])
+def test_decode_sharded_gloo(n_imgs, kind):
+    world = len(n_imgs)
+    mp.spawn(_worker, args=(world, _free_port(), n_imgs, kind), nprocs=world, join=True)
+
+
+def test_decode_sharded_digest_mismatch():
+    mp.spawn(_corrupt_worker, args=(2, _free_port()), nprocs=2, join=True)
+
+
+@pytest.mark.parametrize('n_imgs', [(3, 4), (2, 0, 3)])
+def test_gather_records_mixed_formats(n_imgs):
+    world = len(n_imgs)
+    mp.spawn(_worker, args=(world, _free_port(), n_imgs, 'records_mixed'), nprocs=world,
+             join=True)
 
 
 def test_digest_detects_changes():

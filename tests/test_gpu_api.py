@@ -44,6 +44,13 @@ def test_initial_annotations_vs_reference(dec, mode):
     # the reference returns the initial objects themselves at these positions
     ident = [next((i for i, a0 in enumerate(init) if a0 is a), -1) for a in anns]
     assert ident == g['init_index'].tolist()
+    # every initial object as the reference leaves it, also those NMS dropped (edited in
+    # place before the filter, nms.py:20-53; the fixture's fourth one in predict mode)
+    final = {'ann_' + k[6:]: v for k, v in g.items() if k.startswith('final_')}
+    errs = gu.compare_annotations(final, gu.annotations_as_records(init))
+    assert not errs, errs[:10]
+    if mode == 'predict':
+        assert len({i for i in ident if i >= 0}) < len(init)  # some were dropped
     # and bit-exact against the oracle (same exp), positions included
     ref, idx = oracle.decode_initial(cif, caf, SKEL, init_recs, gu.case_config(_mode_fixture(mode)))
     got = gu.annotations_as_records(anns)
@@ -57,17 +64,33 @@ def test_initial_annotations_batch_vs_oracle():
     """A batch of 6 images (planted and uniform), each with its own initial annotations
     (0-5, from another image's decode, shifted), through engine.decode: every image's
     records and pre-NMS positions byte-equal to the oracle's."""
-    import torch
     from openpifpaf_amd import synthetic
-    from openpifpaf_amd._abi import EVAL_CONFIG, make_config
-    from openpifpaf_amd.engine import DecodeEngine, InitialAnnotations
-    cfg = make_config(**EVAL_CONFIG)
     cp, ap = synthetic.batch('planted', 4, 48, 48, first_seed=30)
     cu, au = synthetic.batch('uniform', 2, 24, 24, first_seed=31)
+    _initial_batch_check(((cp, ap), (cu, au)), range(6))
+
+
+def test_initial_annotations_one_cu_seed_loop():
+    """The same check on a batch of more than CUs / 2 images, which runs the one-CU
+    seed_loop_kernel (no external helper workgroups, seed_ext_per_image = 0) instead of
+    seed_loop_ext_kernel; every 9th image has initial annotations."""
+    from openpifpaf_amd import synthetic
+    cif, caf = synthetic.batch('planted', 136, 40, 40, first_seed=50)
+    _initial_batch_check(((cif, caf),), range(0, 136, 9))
+
+
+def _initial_batch_check(batches, with_init):
+    import torch
+    from openpifpaf_amd._abi import ANN_DTYPE, EVAL_CONFIG, make_config
+    from openpifpaf_amd.engine import DecodeEngine, InitialAnnotations
+    cfg = make_config(**EVAL_CONFIG)
     rng = np.random.default_rng(4)
-    for cif, caf in ((cp, ap), (cu, au)):
+    for cif, caf in batches:
         per_image = []
         for i in range(len(cif)):
+            if i not in with_init:
+                per_image.append(np.zeros(0, ANN_DTYPE))
+                continue
             prev = oracle.decode(cif[(i + 1) % len(cif)], caf[(i + 1) % len(cif)], SKEL, cfg)
             take = prev[:int(rng.integers(0, min(6, len(prev)) + 1))].copy()
             take['data'][:, :, 0] += np.where(take['data'][:, :, 2] > 0, np.float32(2.5), 0)

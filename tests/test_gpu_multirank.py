@@ -20,12 +20,23 @@ def _free_port():
 @pytest.mark.gpu
 @pytest.mark.parametrize('world', [2, 3])
 def test_sharded_decode_gathers_one_process_result(world):
+    _run(world, [])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('world', [2, 3])
+def test_sharded_api_matches_one_process(world):
+    """CifCaf.decode_batch(group=) / Generator.batch(group=) over gloo ranks on cuda:0."""
+    _run(world, ['api'])
+
+
+def _run(world, extra):
     port = str(_free_port())
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
                    MASTER_ADDR='127.0.0.1', MASTER_PORT=port)
-        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, 'multirank_worker.py')],
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, 'multirank_worker.py')] + extra,
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                                       text=True))
     outs = []

@@ -38,8 +38,10 @@ for case in cases:
     cfg = make_config(**EVAL_CONFIG)
     c, f = torch.from_numpy(cif).cuda(), torch.from_numpy(caf).cuda()
     for _ in range(2):
-        eng.launch(c, f, skel, cfg)
+        b = eng.launch(c, f, skel, cfg)
     torch.cuda.synchronize()
+    n_ann = b.counts.cpu().numpy()
+    n_seed_cells = (cif[:, :, 0] > cfg.seed_threshold).reshape(n, -1).sum(axis=1)
     st = np.fromfile(out, dtype=np.uint64).reshape(-1, n, 3, 12)[-1].astype(np.float64)
     print('== {} (mean shader cycles per image)'.format(case))
     for ph, names in ((0, P1), (1, P2), (2, P3)):
@@ -56,6 +58,14 @@ for case in cases:
                   'hits {:.0f}, round_grow {:.3e})'.format(
                       np.percentile(per, 50), np.percentile(per, 90), per[w], w, st[w, 0, 6],
                       st[w, 0, 7], st[w, 0, 2]))
+            top = np.argsort(-per)[:8]
+            print('    heaviest images (cycles, rounds, hits, anns, seed cells):')
+            for t in top:
+                print('      {:4d} {:.3e} {:3.0f} {:3.0f} {:4d} {:5d}'.format(
+                    t, per[t], st[t, 0, 6], st[t, 0, 7], n_ann[t], n_seed_cells[t]))
+            print('    corr(cycles, anns) {:.2f}  corr(cycles, rounds) {:.2f}  corr(cycles, seed cells) {:.2f}'.format(
+                np.corrcoef(per, n_ann)[0, 1], np.corrcoef(per, st[:, 0, 6])[0, 1],
+                np.corrcoef(per, n_seed_cells)[0, 1]))
         for i, name in ((8, 'n connection'), (9, 'in-grow pop'), (10, 'in-grow connection'),
                         (11, 'in-grow add')):
             print('    {:14s} {:12.0f}'.format(name, st[:, ph, i].mean()))
