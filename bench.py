@@ -569,21 +569,35 @@ TRAFFIC_KERNELS = {'roofline': 'cifhr_list_kernel+cifhr_tile_kernel',
 
 
 def committed_traffic():
-    """HBM bytes per launch of the CifHr kernels from the newest committed PMC profile of
-    this same workload (profiles/<tag>_summary.json, written by tools/prof_summary.py from
-    the rocprofv3 FETCH_SIZE / WRITE_SIZE passes of tools/gpu_profile.sh; counters cannot
-    be read from inside the timed process).  {roofline key: {traffic, traffic_source}}."""
+    """HBM bytes per launch of the CifHr kernels from the committed PMC profile of this same
+    workload and this same library (profiles/<tag>_summary.json, written by
+    tools/prof_summary.py from the rocprofv3 FETCH_SIZE / WRITE_SIZE passes of
+    tools/gpu_profile.sh; counters cannot be read from inside the timed process).  A
+    profile counts only when its `src_sha` equals the running library's
+    (openpifpaf_amd.build.source_digest); otherwise traffic is null and `traffic_stale`
+    names the newest profile.  {roofline key: {traffic, traffic_source}}."""
     import glob
+    from openpifpaf_amd.build import source_digest
     paths = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*_summary.json')))
     if not paths:
         return {}
-    with open(paths[-1]) as f:
-        summ = json.load(f)
+    want = source_digest()
+    summ, used = None, None
+    for p in reversed(paths):
+        with open(p) as f:
+            s = json.load(f)
+        if s.get('src_sha') == want:
+            summ, used = s, p
+            break
     out = {}
     for key, kernels in TRAFFIC_KERNELS.items():
-        t = summ.get('traffic_bytes', {}).get(kernels)
+        t = None if summ is None else summ.get('traffic_bytes', {}).get(kernels)
         if t is not None:
-            out[key] = {'traffic': t, 'traffic_source': 'profiles/' + os.path.basename(paths[-1])}
+            out[key] = {'traffic': t, 'traffic_source': 'profiles/{} (src_sha {})'.format(
+                os.path.basename(used), want)}
+        else:
+            out[key] = {'traffic': None, 'traffic_stale': 'no committed profile of library '
+                        '{} (newest: profiles/{})'.format(want, os.path.basename(paths[-1]))}
     return out
 
 

@@ -34,6 +34,20 @@ def sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.hip'))
 
 
+def source_digest():
+    """sha256 (hex, 16 chars) of the library's sources (csrc/* and the C header): names a
+    build, so that a committed profile can be matched with the library it measured."""
+    import hashlib
+    h = hashlib.sha256()
+    paths = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC)
+                   if f.endswith(('.hip', '.hpp')))
+    for p in paths + [os.path.join(REPO, 'include', 'pifpaf_amd.h')]:
+        h.update(os.path.basename(p).encode() + b'\0')
+        with open(p, 'rb') as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def _deps_mtime():
     paths = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
     paths.append(os.path.join(REPO, 'include', 'pifpaf_amd.h'))

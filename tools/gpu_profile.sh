@@ -9,6 +9,7 @@ OUT="$R/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 hipcc --offload-arch=gfx950 -O3 "$R/tools/calib_counters.hip" -o /tmp/calib_counters 2> "$OUT/calib_build.err" || exit $?
+python3 -c "import sys; sys.path.insert(0, '$R'); from openpifpaf_amd.build import source_digest; print(source_digest())" > "$OUT/src_sha.txt" || exit $?
 BENCH="$R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-uniform --no-multi --no-configs"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o run --output-format csv -- python3 $BENCH > "$OUT/kt_bench.json" 2> "$OUT/kt.err" || exit $?
 for C in FETCH_SIZE WRITE_SIZE; do

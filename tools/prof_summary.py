@@ -85,8 +85,11 @@ def main():
                   'cifhr_sparse_kernel': 'read4'}
     write_width = {'cifhr_splats_kernel': 'write16', 'cifhr_list_kernel': 'write16', 'cifhr_tile_kernel': 'write16',
                    'cifhr_sparse_kernel': 'write4'}
+    sha_path = os.path.join(src, 'src_sha.txt')
     summary = {
         'tag': tag,
+        # the library the profile measured (openpifpaf_amd.build.source_digest on the box)
+        'src_sha': open(sha_path).read().strip() if os.path.exists(sha_path) else None,
         'fetch_ratio_16B': round(calib.get('read16', 0.0), 4),
         'fetch_ratio_4B': round(calib.get('read4', 0.0), 4),
         'write_ratio_16B': round(calib.get('write16', 0.0), 4),
