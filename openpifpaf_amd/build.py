@@ -30,6 +30,18 @@ CFLAGS = [
 FILE_FLAGS = {'splat.hip': ['-fno-slp-vectorize']}
 
 
+VARIANTS = {
+    'stamps': ['-DPP_STAMPS'],
+    'nofuse': ['-DPP_NO_FUSED'],         # CifHr without the LDS list / fused seed emission
+    'noself': ['-DPP_NO_SELF_PLAN'],     # seed-loop helpers planned by wave 0 only
+    'norank': ['-DPP_NO_RANK'],          # one seeds-sort workgroup per image at any batch
+    'noahead': ['-DPP_NO_RAW_AHEAD'],    # force-complete set-B connections evaluated lazily
+    'noocc': ['-DPP_NO_SEED_OCC'],        # the seed loop's occupancy in the global grid
+    'base': ['-DPP_NO_FUSED', '-DPP_NO_SELF_PLAN', '-DPP_NO_RANK', '-DPP_NO_RAW_AHEAD',
+             '-DPP_NO_SEED_OCC'],
+}
+
+
 def sources():
     return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith('.hip'))
 
@@ -73,8 +85,9 @@ def build(force=False, verbose=True, variant=''):
     os.makedirs(bdir, exist_ok=True)
     if (not force and os.path.exists(lib) and os.path.getmtime(lib) >= _deps_mtime()):
         return lib
-    # diagnostic variant: 'stamps' (in-kernel cycle stamps; never loaded by default)
-    extra = ['-DPP_STAMPS'] if variant == 'stamps' else []
+    # diagnostic variants (never loaded by default): 'stamps' (in-kernel cycle stamps), and
+    # A/B builds with one round-4 change off each (PP_LIB_VARIANT=<name> selects one)
+    extra = VARIANTS.get(variant, [])
     workers = min(8, len(sources()))
     with concurrent.futures.ThreadPoolExecutor(workers) as ex:
         objs = list(ex.map(lambda src: _compile(src, bdir, extra), sources()))
@@ -91,3 +104,6 @@ if __name__ == '__main__':
     build(force='--force' in sys.argv)
     if '--stamps' in sys.argv:
         build(force='--force' in sys.argv, variant='stamps')
+    for v in sys.argv[1:]:
+        if v.startswith('--variant='):
+            build(force='--force' in sys.argv, variant=v.split('=', 1)[1])

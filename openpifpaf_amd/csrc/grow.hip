@@ -427,7 +427,8 @@ __device__ __forceinline__ void consider(const float *__restrict__ cf, int64_t h
 // for this one column: rows * stride, CifHr rescoring at the target, the second
 // threshold), then as consider
 struct RawSet {
-    const int *idx;      // bucketed concatenated cell indices
+    const int *idx;      // bucketed concatenated cell indices (int32), or
+    const uint16_t *idx16;  // u16 ones (sets of at most kSetBIdx16Max cells)
     int64_t fld;         // image * C + CAF field
     int64_t hrt;         // CifHr plane of the direction's target joint (rescore), or -1
     int src, tgt, tsc;   // raw rows of source x, target x, target scale (y = x + 1)
@@ -436,7 +437,7 @@ struct RawSet {
 template <bool MAXM>
 __device__ __forceinline__ void consider_raw(const GrowArgs &g, const RawSet &r, const ColQuery &q,
                                              int k, Top2 &t) {
-    const int key = r.idx[k];
+    const int key = r.idx16 ? (int)r.idx16[k] : r.idx[k];
     const Heads &h = g.heads;
     int hm = 0, cell = key;
     if (h.n_caf > 1) {
@@ -612,7 +613,10 @@ __device__ __forceinline__ const float *col_set(const GrowArgs &g, int set, int 
 // joint j2; dir 0 backward (x2, y2) -> (x1, y1, s1), rescored at j1 (caf_scored.py:58-81)
 __device__ __forceinline__ RawSet raw_set(const GrowArgs &g, int img, int caf_i, int dir) {
     RawSet r;
-    r.idx = reinterpret_cast<const int *>(col_set(g, 1, img, caf_i, dir));
+    const float *cs = col_set(g, 1, img, caf_i, dir);
+    const bool i16 = g.col_cap <= kSetBIdx16Max;  // caf_bucketed_kernel<true, true>
+    r.idx = i16 ? nullptr : reinterpret_cast<const int *>(cs);
+    r.idx16 = i16 ? reinterpret_cast<const uint16_t *>(cs) : nullptr;
     r.fld = (int64_t)img * g.C + caf_i;
     const int tj = dir ? g.caf_j2[caf_i] : g.caf_j1[caf_i];
     r.hrt = (g.cif_floor < 1.0f && tj < g.K) ? (int64_t)img * g.K + tj : -1;
@@ -993,10 +997,210 @@ __device__ __forceinline__ void eval_ahead(const GrowArgs &g, Frontier &F, int i
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// force-complete: the set-B connections of a joint's new frontier entries, batched
+// ---------------------------------------------------------------------------------------
+// complete_annotations' _grow (reverse_match=False, cifcaf.py:339-344) evaluates each
+// unevaluated entry when it is popped: one set-B query, a chain of four dependent memory
+// round trips (bucket offsets, cell indices, raw CAF rows, CifHr rescoring) of ~22k cycles
+// on dense input.  As eval_ahead does for set A, the entries a joint adds are evaluated
+// when it enters the frontier, kRawAhead edges at a time with their loads interleaved: the
+// batch costs the round trips of one query.  Lanes 16 b .. 16 b + 15 hold edge b's
+// bucket-row segments (<= kRawSegs), every lane one column of every edge per pass.  An edge
+// whose box spans more bucket rows stays lazy.
+constexpr int kRawAhead = 4;
+#ifdef PP_NO_RAW_AHEAD  // A/B builds
+constexpr bool kCompleteAhead = false;
+#else
+constexpr bool kCompleteAhead = true;  // complete_kernel evaluates set B ahead
+#endif
+constexpr int kRawSegs = 64 / kRawAhead;
+
+template <bool MAXM>
+__device__ __forceinline__ void eval_ahead_raw(const GrowArgs &g, Frontier &F, int img, uint64_t r0,
+                                               uint64_t r1, float ax, float ay, float av,
+                                               float as) {
+    const int lane = threadIdx.x & 63;
+    if (g.heads.n_caf != 1) return;  // several CAF heads: every entry stays lazy
+    while (r0 | r1) {
+        int sl[kRawAhead];
+#pragma unroll
+        for (int b = 0; b < kRawAhead; b++) {  // the next kRawAhead slots
+            sl[b] = -1;
+            if (r0) {
+                sl[b] = __ffsll((unsigned long long)r0) - 1;
+                r0 &= r0 - 1;
+            } else if (r1) {
+                sl[b] = 64 + __ffsll((unsigned long long)r1) - 1;
+                r1 &= r1 - 1;
+            }
+        }
+        // per edge: the query (scalar), its set, and this lane's bucket-row segment
+        ColQuery q[kRawAhead];
+        RawSet rs[kRawAhead];
+        float jv_b[kRawAhead];
+        bool ok[kRawAhead];
+        int my_st = 0, my_len = 0;
+#pragma unroll
+        for (int b = 0; b < kRawAhead; b++) {
+            ok[b] = sl[b] >= 0;
+            if (!ok[b]) continue;
+            const int d = sl[b], l = d & 63;
+            const bool h = d >= 64;
+            // wave-uniform values, kept scalar: a per-lane index into GrowArgs' tables would
+            // copy the struct to scratch
+            const int caf = __builtin_amdgcn_readfirstlane(rl_i(h ? F.scaf[1] : F.scaf[0], l));
+            const int dir = __builtin_amdgcn_readfirstlane(rl_i(h ? F.sfwd[1] : F.sfwd[0], l)) ? 1 : 0;
+            const int j = __builtin_amdgcn_readfirstlane(rl_i(h ? F.sj[1] : F.sj[0], l));
+            jv_b[b] = rl_f(av, j);
+            q[b] = make_query(rl_f(ax, j), rl_f(ay, j), max0(rl_f(as, j)));
+            rs[b] = raw_set(g, img, caf, dir);
+            int bx0, bx1, by0, by1;
+            const ColQuery &qq = q[b];
+            if (qq.lo_x != qq.lo_x || qq.hi_x != qq.hi_x || qq.lo_y != qq.lo_y || qq.hi_y != qq.hi_y) {
+                ok[b] = false;  // NaN bounds: the lazy path scans every bucket
+                continue;
+            }
+            bx0 = (int)fminf(fmaxf(floorf(qq.lo_x * g.inv_e), 0.0f), (float)(g.bw - 1));
+            bx1 = (int)fminf(fmaxf(floorf(qq.hi_x * g.inv_e), 0.0f), (float)(g.bw - 1));
+            by0 = (int)fminf(fmaxf(floorf(qq.lo_y * g.inv_e), 0.0f), (float)(g.bh - 1));
+            by1 = (int)fminf(fmaxf(floorf(qq.hi_y * g.inv_e), 0.0f), (float)(g.bh - 1));
+            const int nseg = (by1 - by0 + 1) + 1;  // bucket rows + the NaN bucket
+            if (nseg > kRawSegs) {
+                ok[b] = false;
+                continue;
+            }
+            const int r = lane - kRawSegs * b;
+            if (r >= 0 && r < nseg) {
+                int lo, hi;
+                if (r == nseg - 1) {
+                    lo = g.nb - 1;
+                    hi = g.nb;
+                } else {
+                    lo = (by0 + r) * g.bw + bx0;
+                    hi = (by0 + r) * g.bw + bx1 + 1;
+                }
+                const int *off = col_offs(g, 1, img, caf, dir);
+                my_st = off[lo];
+                my_len = off[hi] - my_st;
+            }
+        }
+        // per edge: its column count (scalar), then passes of 64 columns over all edges
+        int tot[kRawAhead], npass = 0;
+#pragma unroll
+        for (int b = 0; b < kRawAhead; b++) {
+            tot[b] = 0;
+            if (!ok[b]) continue;
+            for (int r = 0; r < kRawSegs; r++) tot[b] += rl_i(my_len, kRawSegs * b + r);
+            npass = max(npass, (tot[b] + 63) >> 6);
+        }
+        Top2 t[kRawAhead];
+#pragma unroll
+        for (int b = 0; b < kRawAhead; b++) t[b] = top2_empty();
+        for (int p = 0; p < npass; p++) {
+            // column of every edge for this lane (-1: none), all loads of a stage together
+            int kc[kRawAhead];
+#pragma unroll
+            for (int b = 0; b < kRawAhead; b++) {
+                kc[b] = -1;
+                if (!ok[b]) continue;
+                const int tt = p * 64 + lane;
+                int run = 0;
+                for (int r = 0; r < kRawSegs; r++) {  // the segment holding tt (uniform loop)
+                    const int l = rl_i(my_len, kRawSegs * b + r);
+                    if (tt >= run && tt < run + l) kc[b] = rl_i(my_st, kRawSegs * b + r) + (tt - run);
+                    run += l;
+                }
+            }
+            int key[kRawAhead];
+#pragma unroll
+            for (int b = 0; b < kRawAhead; b++)
+                key[b] = kc[b] >= 0 ? (rs[b].idx16 ? (int)rs[b].idx16[kc[b]] : rs[b].idx[kc[b]]) : -1;
+            float c[kRawAhead], c1[kRawAhead], c2[kRawAhead], tx[kRawAhead], ty[kRawAhead],
+                tc[kRawAhead];
+#pragma unroll
+            for (int b = 0; b < kRawAhead; b++) {
+                c[b] = c1[b] = c2[b] = tx[b] = ty[b] = tc[b] = 0.0f;
+                if (key[b] < 0) continue;
+                // one CAF head (eval_ahead_raw is not used with several: a per-lane head
+                // index into GrowArgs would copy the struct to scratch)
+                const Heads &hh = g.heads;
+                const int cell = key[b];
+                const int64_t hw = (int64_t)hh.aH[0] * hh.aW[0];
+                const float stride = (float)hh.astride[0];
+                const float *caf9 = hh.caf[0] + rs[b].fld * 9 * hw;
+                c[b] = caf9[cell];
+                c1[b] = caf9[rs[b].src * hw + cell] * stride;
+                c2[b] = caf9[(rs[b].src + 1) * hw + cell] * stride;
+                tx[b] = caf9[rs[b].tgt * hw + cell] * stride;
+                ty[b] = caf9[(rs[b].tgt + 1) * hw + cell] * stride;
+                tc[b] = caf9[rs[b].tsc * hw + cell] * stride;
+            }
+            float hv[kRawAhead];
+#pragma unroll
+            for (int b = 0; b < kRawAhead; b++) {
+                hv[b] = 0.0f;
+                const ColQuery &qq = q[b];
+                if (key[b] < 0 || c1[b] < qq.lo_x || c1[b] > qq.hi_x || c2[b] < qq.lo_y ||
+                    c2[b] > qq.hi_y) {
+                    key[b] = -1;  // outside caf_center_s's box (consider_raw's order of tests)
+                    continue;
+                }
+                if (rs[b].hrt >= 0) hv[b] = g.hr.at(rs[b].hrt, tx[b], ty[b], 0.0f);
+            }
+#pragma unroll
+            for (int b = 0; b < kRawAhead; b++) {
+                if (key[b] < 0) continue;
+                float c0 = c[b];
+                if (rs[b].hrt >= 0) c0 = c[b] * (g.cif_floor + g.one_minus_floor * hv[b]);
+                if (!(c0 > g.th_b)) continue;
+                const ColQuery &qq = q[b];
+                const float dx = qq.x - c1[b], dy = qq.y - c2[b];
+                const float dd = sqrtf(dx * dx + dy * dy);
+                const float qv = (-0.5f * (dd * dd)) / qq.sigma2;
+                const float score = (float)exp((double)qv) * c0;
+                top2_insert(t[b], cand_key<MAXM>(score, key[b]), tx[b], ty[b], tc[b]);
+            }
+        }
+        // connection_value without reverse matching (cifcaf.py:194-208)
+#pragma unroll
+        for (int b = 0; b < kRawAhead; b++) {
+            if (!ok[b]) continue;
+            float nx[4];
+            finish_connection<MAXM>(t[b], nx);
+            float res[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            const float ks = sqrtf(nx[3] * jv_b[b]);
+            if (!(ks < g.cfg.keypoint_threshold) && nx[3] != 0.0f) {
+                res[0] = nx[0];
+                res[1] = nx[1];
+                res[2] = nx[2];
+                res[3] = ks;
+            }
+            const int d = sl[b];
+            if (lane == (d & 63)) {
+                if (d < 64) {
+                    F.pc[0] = 1;
+                    F.px[0] = res[0];
+                    F.py[0] = res[1];
+                    F.ps[0] = res[2];
+                    F.pv[0] = res[3];
+                } else {
+                    F.pc[1] = 1;
+                    F.px[1] = res[0];
+                    F.py[1] = res[1];
+                    F.ps[1] = res[2];
+                    F.pv[1] = res[3];
+                }
+            }
+        }
+    }
+}
+
 // _grow (cifcaf.py:247-307) on the record in L.a (joint data mirrored into registers).
 // AHEAD (seed loop: set A, reverse_match): new entries' connections via eval_ahead from
-// the image's set-A column counts and LDS-staged sets.
-template <bool AHEAD, typename LDS>
+// the image's set-A column counts and LDS-staged sets; RAW_AHEAD (force-complete: set B,
+// no reverse matching) via eval_ahead_raw.
+template <bool AHEAD, typename LDS, bool RAW_AHEAD = false>
 __device__ __forceinline__ void grow(const GrowArgs &g, LDS &L, int img, int set, bool reverse_match,
                                      const ColStage &cs = ColStage{}) {
     const int lane = threadIdx.x & 63;
@@ -1029,12 +1233,19 @@ __device__ __forceinline__ void grow(const GrowArgs &g, LDS &L, int img, int set
     SlotSets ss{};
     if (AHEAD) ss = slot_sets(g, cs);
     auto ahead = [&](const uint64_t added[2]) {
-        if (!AHEAD || !(added[0] | added[1])) return;
+        if (!(AHEAD || RAW_AHEAD) || !(added[0] | added[1])) return;
         FSTAMP_BEGIN
-        if (maxm)
-            eval_ahead<true>(g, F, img, cs, ss, added[0], added[1], ax, ay, av, as);
-        else
-            eval_ahead<false>(g, F, img, cs, ss, added[0], added[1], ax, ay, av, as);
+        if constexpr (RAW_AHEAD) {
+            if (maxm)
+                eval_ahead_raw<true>(g, F, img, added[0], added[1], ax, ay, av, as);
+            else
+                eval_ahead_raw<false>(g, F, img, added[0], added[1], ax, ay, av, as);
+        } else {
+            if (maxm)
+                eval_ahead<true>(g, F, img, cs, ss, added[0], added[1], ax, ay, av, as);
+            else
+                eval_ahead<false>(g, F, img, cs, ss, added[0], added[1], ax, ay, av, as);
+        }
         FSTAMP_END(L, 1)
     };
     for (int j = 0; j < K; j++) {  // seeding the frontier (cifcaf.py:288-291)
@@ -1064,7 +1275,7 @@ __device__ __forceinline__ void grow(const GrowArgs &g, LDS &L, int img, int set
             }
             if (rl_f(av, e.k) > 0.0f) continue;
             float nx[4];
-            if (AHEAD && e.pc) {  // computed by eval_ahead when joint e.j entered
+            if ((AHEAD || RAW_AHEAD) && e.pc) {  // computed ahead when joint e.j entered
                 nx[0] = e.px;
                 nx[1] = e.py;
                 nx[2] = e.ps;
@@ -1151,7 +1362,7 @@ __device__ __forceinline__ void grow(const GrowArgs &g, LDS &L, int img, int set
 }
 
 // cifcaf.py:309-331 (the key is the ENCLOSING xyv, App. D item 5)
-__device__ void flood_fill(const GrowArgs &g, GrowLDS &L) {
+__device__ __forceinline__ void flood_fill(const GrowArgs &g, GrowLDS &L) {  // (inlined: a call would copy GrowArgs to scratch)
     L.ff_n = 0;
     auto add = [&](int start_i, float key_v) {
         for (int e = g.j_off[start_i]; e < g.j_off[start_i + 1]; e++) {
@@ -1209,12 +1420,11 @@ __device__ __forceinline__ bool occ_get(const OccGrid &o, int f, float x, float 
     return o.p[((int64_t)f * o.h + yi) * o.pitch + xi] != 0;
 }
 
-// Occupancy.set box (occupancy.py:31-39 + utils.py:61-66) of joint f; false when empty
-__device__ __forceinline__ bool occ_box(const GrowArgs &g, const OccGrid &o, int f, float x, float y, float sigma,
-                        int box[4]) {
+// Occupancy.set box (occupancy.py:31-39 + utils.py:61-66) of joint f; false when empty.
+// red = reduction, msr = min_scale / reduction (occ_box below takes them from the config)
+__device__ __forceinline__ bool occ_box_r(float red, float msr, const OccGrid &o, int f, float x,
+                                          float y, float sigma, int box[4]) {
     if (f >= o.f) return false;
-    const float red = (float)g.cfg.occupancy_reduction;
-    const float msr = (float)((double)g.cfg.occupancy_min_scale / g.cfg.occupancy_reduction);
     const long xi = (long)rintf(x / red);  // round(): half to even
     const long yi = (long)rintf(y / red);
     const float sr = sigma / red;
@@ -1233,6 +1443,15 @@ __device__ __forceinline__ bool occ_box(const GrowArgs &g, const OccGrid &o, int
     box[2] = (int)miny;
     box[3] = (int)maxy;
     return true;
+}
+
+__device__ __forceinline__ float occ_msr(const GrowArgs &g) {
+    return (float)((double)g.cfg.occupancy_min_scale / g.cfg.occupancy_reduction);
+}
+
+__device__ __forceinline__ bool occ_box(const GrowArgs &g, const OccGrid &o, int f, float x, float y, float sigma,
+                        int box[4]) {
+    return occ_box_r((float)g.cfg.occupancy_reduction, occ_msr(g), o, f, x, y, sigma, box);
 }
 
 // Mark the boxes of every joint j with mark(j) in one pass: joints live on different
@@ -1335,6 +1554,80 @@ __device__ __forceinline__ void occ_mark(const GrowArgs &g, LDS &L, OccLog *log,
 }
 
 // zero every box the launch marked, so the next launch starts from a clean grid
+// ---- the seed loop's occupancy as per-seed counters in LDS ----
+// The seed loop reads its occupancy grid only at seed positions (cifcaf.py:100-102: the
+// free-seed test; the helpers' plans), so for an image with at most kOccSeeds seeds the
+// grid is replaced by one u8 counter per seed: a mark adds 1 (wrapping, as the grid's
+// `+= 1`, utils.py:66) to every seed of the joint's field whose grid cell lies in the
+// joint's box, and a seed is occupied iff its counter is nonzero -- exactly the grid's
+// cell value there.  Marks and tests stay in LDS: no global read-modify-write, no clearing.
+constexpr int kOccSeeds = 2560;
+#ifdef PP_NO_SEED_OCC  // A/B builds
+constexpr bool kSeedOcc = false;
+#else
+constexpr bool kSeedOcc = true;
+#endif
+struct SeedOcc {
+    uint8_t cnt[kOccSeeds];     // counter per seed index
+    uint32_t cell[kOccSeeds];   // grid cell (yi << 16 | xi) per seed index
+    uint16_t byf[kOccSeeds];    // seed indices grouped by field
+    int foff[kKP + 1];          // field f's group: byf[foff[f] .. foff[f + 1])
+    int fcur[kKP];
+};
+
+// collective over the workgroup (ends with a barrier): the counters and field groups of
+// the image's n <= kOccSeeds seeds
+__device__ __forceinline__ void seed_occ_init(SeedOcc &O, const pp_seed *seeds, int n, int K,
+                                              const OccGrid &o, float red) {
+    if (threadIdx.x < kKP) O.fcur[threadIdx.x] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const pp_seed c = seeds[i];
+        const int xi = (int)clip_ref(c.x / red, 0.0f, (float)(o.w - 1));  // occ_get's cell
+        const int yi = (int)clip_ref(c.y / red, 0.0f, (float)(o.h - 1));
+        O.cell[i] = ((uint32_t)yi << 16) | (uint32_t)xi;
+        O.cnt[i] = 0;
+        atomicAdd(&O.fcur[c.field], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int a = 0;
+        for (int f = 0; f < K; f++) {
+            O.foff[f] = a;
+            a += O.fcur[f];
+            O.fcur[f] = 0;
+        }
+        O.foff[K] = a;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int f = seeds[i].field;
+        O.byf[O.foff[f] + atomicAdd(&O.fcur[f], 1)] = (uint16_t)i;
+    }
+    __syncthreads();
+}
+
+// occ_mark on the counters (one wave): lane j < K holds joint j (x, y, scale, `on`)
+__device__ __forceinline__ void seed_occ_mark(const GrowArgs &g, SeedOcc &O, const OccGrid &o,
+                                              float jx, float jy, float js, bool on, int K) {
+    const int lane = threadIdx.x & 63;
+    int box[4] = {0, 0, 0, 0};
+    const bool has = lane < K && on && occ_box(g, o, lane, jx, jy, js, box);
+    const uint64_t hm = __ballot(has);
+    for (uint64_t m = hm; m; m &= m - 1) {
+        const int j = __ffsll((unsigned long long)m) - 1;
+        const int x0 = rl_i(box[0], j), x1 = rl_i(box[1], j);
+        const int y0 = rl_i(box[2], j), y1 = rl_i(box[3], j);
+        for (int i = O.foff[j] + lane; i < O.foff[j + 1]; i += 64) {
+            const int sd = O.byf[i];
+            const uint32_t c = O.cell[sd];
+            const int xi = (int)(c & 0xFFFFu), yi = (int)(c >> 16);
+            if (xi >= x0 && xi < x1 && yi >= y0 && yi < y1) O.cnt[sd] = (uint8_t)(O.cnt[sd] + 1);
+        }
+    }
+    wave_sync();
+}
+
 template <typename LDS>
 __device__ __forceinline__ void occ_clear(const GrowArgs &g, LDS &L, OccLog *log, const OccGrid &o) {
     wave_sync();
@@ -1454,6 +1747,12 @@ constexpr int kSpecScan = 128;     // seeds after the committed one examined per
 // round's other picks; cached annotations are excluded by their exact occupancy boxes.
 // Throughput is flat for 0-4 (both generators) and drops beyond 8.
 constexpr float kSpecFar = 4.0f;
+constexpr int kSelfScan = 256;     // seeds after the decided ones a finished helper examines
+#ifdef PP_NO_SELF_PLAN  // A/B builds
+constexpr bool kSelfPlan = false;
+#else
+constexpr bool kSelfPlan = true;
+#endif
 
 // External helpers.  A batch of fewer images than CUs leaves CUs without a seed loop, so
 // each image may get n_ext (<= kExtWgMax) more workgroups whose waves are all helpers.
@@ -1561,6 +1860,11 @@ struct SeedLoopSharedT {
     float4 cache_j[kSpecCache][kKP];  // its joints (x, y, v, scale); the external slots'
                                       // after the column stage in dynamic LDS (cache_joints)
     int done;
+    // seed_loop_kernel's helper self-planning (spec_plan): the plan lock, the first seed not
+    // yet decided by wave 0 (seeds before it were committed or skipped), and the seed wave 0
+    // grows itself now (own_on)
+    int plan_lock, decided, own_on;
+    float own_x, own_y, own_s;
 };
 using SeedLoopShared = SeedLoopSharedT<kSpecCache>;
 struct SeedLoopSharedX : SeedLoopSharedT<kCacheSlots> {
@@ -1649,6 +1953,121 @@ __device__ __forceinline__ void ext_refresh(SeedLoopSharedX &S, float *s_cols, c
     }
 }
 
+// Speculation plan of seed_loop_kernel, collective over one wave, with S.plan_lock held:
+// free seeds in [first, first + scan) that the committed occupancy and the grown cached
+// annotations' occupancy boxes do not cover, kSpecFar joint scales from every seed in
+// flight (and from wave 0's own seed when S.own_on), each into a free cache slot (never
+// used, or holding a seed before `decided`), for the helper waves in `idle` (bit w = wave
+// w), which get their seeds through S.task.  Returns the helpers left idle.
+// A slot is claimed state first, seed second (both released): wave 0 reads the seed without
+// the lock and, seeing its seed there, waits for state 2.
+// Not inlined: it runs outside the grow and takes no GrowArgs (a non-inlined reference to
+// the kernarg struct makes the compiler copy it to scratch), so the kernel's registers stay
+// the grow's.
+// NS > kSpecCache (seed_loop_ext_kernel): slots kSpecCache.. are the external helpers'
+// (joints at xj, cache_joints); they are avoided like the others but never claimed here.
+template <int NS>
+__device__ __noinline__ uint64_t spec_plan(SeedLoopSharedT<NS> &S, const float4 *xj,
+                                           const pp_seed *seeds, int n_seeds, int first,
+                                           int decided, int scan, OccGrid occ, float red,
+                                           float msr, float far_k, uint64_t idle,
+                                           const uint8_t *socc) {
+    const int lane = threadIdx.x & 63;
+    const int cst = lane < NS ? lds_acquire(&S.cache_state[lane]) : 0;
+    uint64_t fly = __ballot(lane < NS && cst == 1);
+    const bool own = lds_acquire(&S.own_on) != 0;
+    const float ox = S.own_x, oy = S.own_y, osc = S.own_s;
+    const int scan_end = min(n_seeds, first + scan);
+    for (int base = first; base < scan_end && idle; base += 64) {
+        const int idx = base + lane;
+        bool ok = idx < scan_end;
+        pp_seed c{};
+        if (ok) {
+            c = seeds[idx];
+            ok = (!own || spec_far(far_k, c.x, c.y, c.s, ox, oy, osc)) &&
+                 !(socc ? socc[idx] != 0 : occ_get(occ, c.field, c.x, c.y, red));
+        }
+        // cache entries (uniform loop): skip seeds they hold, seeds that a grown
+        // annotation's occupancy boxes will cover once committed, and seeds near one
+        // still being grown
+        const int cxi = (int)clip_ref(c.x / red, 0.0f, (float)(occ.w - 1));
+        const int cyi = (int)clip_ref(c.y / red, 0.0f, (float)(occ.h - 1));
+        for (int q = 0; q < NS; q++) {
+            const int sq = S.cache_seed[q];
+            const int st = S.cache_state[q];
+            if (sq < decided || st == 0 || st == 4) continue;  // free, passed or a zombie
+            if (sq == idx) ok = false;
+            if (!ok) continue;
+            if ((fly >> q) & 1) {
+                ok = spec_far(far_k, c.x, c.y, c.s, S.cache_x[q], S.cache_y[q], S.cache_s[q]);
+                continue;
+            }
+            if (st != 2) continue;
+            const float4 jq = q < kSpecCache ? S.cache_j[q][c.field]
+                                             : xj[(q - kSpecCache) * kKP + c.field];
+            int box[4];
+            if (jq.z != 0.0f && occ_box_r(red, msr, occ, c.field, jq.x, jq.y, jq.w, box) &&
+                cxi >= box[0] && cxi < box[1] && cyi >= box[2] && cyi < box[3])
+                ok = false;
+        }
+        uint64_t m = __ballot(ok);
+        while (m && idle) {
+            const int l = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1;
+            const float cx = rl_f(c.x, l), cy = rl_f(c.y, l), csc = rl_f(c.s, l);
+            bool far = true;  // from this plan's earlier picks (now in flight too)
+            uint64_t f2 = fly;
+            while (f2) {
+                const int q = __ffsll((unsigned long long)f2) - 1;
+                f2 &= f2 - 1;
+                far = far && spec_far(far_k, cx, cy, csc, S.cache_x[q], S.cache_y[q],
+                                      S.cache_s[q]);
+            }
+            if (!far) continue;
+            // a free slot: never grown into, or grown for a seed already decided
+            const int cq = lane < kSpecCache ? S.cache_seed[lane] : 0;
+            const int cst2 = lane < kSpecCache ? S.cache_state[lane] : 1;
+            const uint64_t freeq = __ballot(lane < kSpecCache &&
+                                            (cst2 == 0 || (cst2 == 2 && cq < decided)));
+            if (!freeq) return idle;  // no slot: nobody else can be planned either
+            const int q = __ffsll((unsigned long long)freeq) - 1;
+            const int w = __ffsll((unsigned long long)idle) - 1;
+            idle &= idle - 1;
+            fly |= 1ull << q;
+            if (lane == 0) {
+                S.cache_x[q] = cx;
+                S.cache_y[q] = cy;
+                S.cache_s[q] = csc;
+                lds_release(&S.cache_state[q], 1);
+                lds_release(&S.cache_seed[q], base + l);
+                S.task_slot[w] = q;
+                lds_release(&S.task[w], base + l);
+            }
+            wave_sync();
+        }
+    }
+    return idle;
+}
+
+template <int NS>
+__device__ __forceinline__ void plan_lock(SeedLoopSharedT<NS> &S) {
+    if ((threadIdx.x & 63) == 0) {
+        int expect = 0;
+        while (!__hip_atomic_compare_exchange_strong(&S.plan_lock, &expect, 1, __ATOMIC_ACQUIRE,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            expect = 0;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    wave_sync();
+}
+
+template <int NS>
+__device__ __forceinline__ void plan_unlock(SeedLoopSharedT<NS> &S) {
+    wave_sync();
+    if ((threadIdx.x & 63) == 0) lds_release(&S.plan_lock, 0);
+}
+
 // <= 168 VGPRs (3 waves per SIMD; a few spills) and the column stage in dynamic LDS: the
 // image's workgroup leaves room on its CU for the next batch's CifHr / seeds / CafScored
 // workgroups (DecodePipeline).  Planted 1.031 -> 1.013 ms, uniform 21.7 -> 20.4 ms per
@@ -1661,6 +2080,7 @@ void seed_loop_kernel(GrowArgs g) {
     __shared__ SeedLoopShared S;
     __shared__ int s_ncol[2 * PP_MAX_EDGES];  // set-A column counts per (CAF, direction)
     __shared__ int s_cofs[2 * PP_MAX_EDGES];  // their LDS offsets in s_cols (-1: global)
+    __shared__ SeedOcc s_occ;  // per-seed occupancy (images of at most kOccSeeds seeds)
     extern __shared__ float s_cols[];  // kColLds floats (dynamic: the launch sizes it)
     const int img = blockIdx.x;
     const int K = g.K;
@@ -1705,7 +2125,12 @@ void seed_loop_kernel(GrowArgs g) {
         S.cache_state[threadIdx.x] = 0;
     }
     if (threadIdx.x < kSeedWaves) S.task[threadIdx.x] = -1;
-    if (threadIdx.x == 0) S.done = 0;
+    if (threadIdx.x == 0) {
+        S.done = 0;
+        S.plan_lock = 0;
+        S.decided = 0;
+        S.own_on = 0;
+    }
     __syncthreads();
 
     STAMP_DECL
@@ -1718,6 +2143,10 @@ void seed_loop_kernel(GrowArgs g) {
                                  (int)((double)g.ww / g.cfg.occupancy_reduction));
     const int n_seeds = min(g.seed_counts[img], g.seed_cap);
     const pp_seed *seeds = g.seeds + (int64_t)img * g.seed_cap;
+    // the occupancy at the seeds in LDS (seed_occ_*), or the global grid for more seeds
+    const bool socc_on = kSeedOcc && n_seeds <= kOccSeeds;
+    if (socc_on) seed_occ_init(s_occ, seeds, n_seeds, K, occ, red);
+    const uint8_t *socc = socc_on ? s_occ.cnt : nullptr;
 
     // committer state (wave 0)
     int n_anns = 0, s = 0;
@@ -1733,7 +2162,10 @@ void seed_loop_kernel(GrowArgs g) {
         n_anns++;
         const uint32_t set = (uint32_t)__ballot(lane < K && jv > 0.0f);
         unset_mask |= ~set & (K >= 32 ? 0xFFFFFFFFu : ((1u << K) - 1u));
-        occ_mark(g, L, log, occ, jx, jy, js, jv != 0.0f, K);
+        if (socc_on)
+            seed_occ_mark(g, s_occ, occ, jx, jy, js, jv != 0.0f, K);
+        else
+            occ_mark(g, L, log, occ, jx, jy, js, jv != 0.0f, K);
     };
 
     if (wave > 0) {  // helper: grow the seeds wave 0 hands over until it is done
@@ -1756,11 +2188,20 @@ void seed_loop_kernel(GrowArgs g) {
             // release alone does not wait for them)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             wave_sync();
-            if (lane == 0) {
-                lds_release(&S.cache_state[q], 2);
-                lds_release(&S.task[wave], -1);
-            }
+            if (lane == 0) lds_release(&S.cache_state[q], 2);
             wave_sync();
+            // plan this wave's next grow itself, with its own annotation now in the cache (its
+            // occupancy boxes rule out the other seeds of the same person); wave 0 plans only
+            // when it has to grow a seed itself
+            plan_lock(S);
+            uint64_t left = 1ull << wave;
+            if (kSelfPlan && !lds_acquire(&S.done)) {
+                const int dec = lds_acquire(&S.decided);
+                left = spec_plan(S, nullptr, seeds, n_seeds, dec, dec, kSelfScan, occ, red, occ_msr(g),
+                                 g.spec_far, left, socc);
+            }
+            if (left && lane == 0) lds_release(&S.task[wave], -1);
+            plan_unlock(S);
         }
     } else {
         __builtin_amdgcn_s_setprio(3);  // the committer is the critical path: issue first
@@ -1790,8 +2231,12 @@ void seed_loop_kernel(GrowArgs g) {
                 const int idx = s + lane;
                 bool is_free = false;
                 if (idx < n_seeds) {
-                    const pp_seed c = seeds[idx];
-                    is_free = !occ_get(occ, c.field, c.x, c.y, red);
+                    if (socc_on) {
+                        is_free = s_occ.cnt[idx] == 0;
+                    } else {
+                        const pp_seed c = seeds[idx];
+                        is_free = !occ_get(occ, c.field, c.x, c.y, red);
+                    }
                 }
                 const uint64_t m = __ballot(is_free);
                 if (m == 0) {
@@ -1814,6 +2259,7 @@ void seed_loop_kernel(GrowArgs g) {
                 const float4 jq = lane < kKP ? S.cache_j[slot][lane] : make_float4(0.f, 0.f, 0.f, 0.f);
                 commit(&cache[slot], jq.x, jq.y, jq.z, jq.w);
                 s = t + 1;
+                if (lane == 0) lds_release(&S.decided, s);  // the slot is free again
 #ifdef PP_STAMPS
                 n_hits++;
 #endif
@@ -1822,82 +2268,23 @@ void seed_loop_kernel(GrowArgs g) {
             }
             // hand far-away free seeds to the idle helpers, then grow t here
             const pp_seed st = seeds[t];
-            const int tk = lane > 0 && lane < kSeedWaves ? lds_acquire(&S.task[lane]) : 0;
-            uint64_t idle = __ballot(lane > 0 && lane < kSeedWaves && tk < 0);
-            // the seeds in flight: later picks keep kSpecFar from them
-            const int cst = lane < kSpecCache ? lds_acquire(&S.cache_state[lane]) : 0;
-            uint64_t fly = __ballot(lane < kSpecCache && cst == 1);
-            const int scan_end = min(n_seeds, t + 1 + kSpecScan);
-            for (int base = t + 1; base < scan_end && idle; base += 64) {
-                const int idx = base + lane;
-                bool ok = idx < scan_end;
-                pp_seed c{};
-                if (ok) {
-                    c = seeds[idx];
-                    ok = spec_far(g.spec_far, c.x, c.y, c.s, st.x, st.y, st.s) &&
-                         !occ_get(occ, c.field, c.x, c.y, red);
-                }
-                // cache entries (uniform loop): skip seeds they hold, seeds that a grown
-                // annotation's occupancy boxes will cover once committed, and seeds near
-                // one still being grown
-                const int cxi = (int)clip_ref(c.x / red, 0.0f, (float)(occ.w - 1));
-                const int cyi = (int)clip_ref(c.y / red, 0.0f, (float)(occ.h - 1));
-                for (int q = 0; q < kSpecCache; q++) {
-                    const int sq = S.cache_seed[q];
-                    if (sq <= t) continue;
-                    if (sq == idx) ok = false;
-                    if (!ok) continue;
-                    if ((fly >> q) & 1) {
-                        ok = spec_far(g.spec_far, c.x, c.y, c.s, S.cache_x[q], S.cache_y[q],
-                                      S.cache_s[q]);
-                        continue;
-                    }
-                    const float4 jq = S.cache_j[q][c.field];
-                    int box[4];
-                    if (jq.z != 0.0f && occ_box(g, occ, c.field, jq.x, jq.y, jq.w, box) &&
-                        cxi >= box[0] && cxi < box[1] && cyi >= box[2] && cyi < box[3])
-                        ok = false;
-                }
-                uint64_t m = __ballot(ok);
-                while (m && idle) {
-                    const int l = __ffsll((unsigned long long)m) - 1;
-                    m &= m - 1;
-                    const float cx = rl_f(c.x, l), cy = rl_f(c.y, l), csc = rl_f(c.s, l);
-                    bool far = true;  // from this plan's earlier picks (now in flight too)
-                    uint64_t f2 = fly;
-                    while (f2) {
-                        const int q = __ffsll((unsigned long long)f2) - 1;
-                        f2 &= f2 - 1;
-                        far = far && spec_far(g.spec_far, cx, cy, csc, S.cache_x[q],
-                                              S.cache_y[q], S.cache_s[q]);
-                    }
-                    if (!far) continue;
-                    // a free slot: never grown into, or grown for a seed already passed
-                    const int cq = lane < kSpecCache ? S.cache_seed[lane] : 0;
-                    const int cst2 = lane < kSpecCache ? S.cache_state[lane] : 1;
-                    const uint64_t freeq = __ballot(lane < kSpecCache &&
-                                                    (cst2 == 0 || (cst2 == 2 && cq < t)));
-                    if (!freeq) {
-                        m = 0;
-                        idle = 0;
-                        break;
-                    }
-                    const int q = __ffsll((unsigned long long)freeq) - 1;
-                    const int w = __ffsll((unsigned long long)idle) - 1;
-                    idle &= idle - 1;
-                    fly |= 1ull << q;
-                    if (lane == 0) {
-                        S.cache_seed[q] = base + l;
-                        S.cache_x[q] = cx;
-                        S.cache_y[q] = cy;
-                        S.cache_s[q] = csc;
-                        S.cache_state[q] = 1;
-                        S.task_slot[w] = q;
-                        lds_release(&S.task[w], base + l);
-                    }
-                    wave_sync();
-                }
+            plan_lock(S);
+            if (lane == 0) {
+                S.own_x = st.x;
+                S.own_y = st.y;
+                S.own_s = st.s;
+                lds_release(&S.own_on, 1);
+                lds_release(&S.decided, t);
             }
+            wave_sync();
+            {
+                const int tk = lane > 0 && lane < kSeedWaves ? lds_acquire(&S.task[lane]) : 0;
+                const uint64_t idle = __ballot(lane > 0 && lane < kSeedWaves && tk < 0);
+                if (idle)
+                    spec_plan(S, nullptr, seeds, n_seeds, t + 1, t, kSpecScan, occ, red, occ_msr(g),
+                              g.spec_far, idle, socc);
+            }
+            plan_unlock(S);
 #ifdef PP_STAMPS
             n_rounds++;
 #endif
@@ -1908,6 +2295,10 @@ void seed_loop_kernel(GrowArgs g) {
             commit(&L.a, lane < K ? L.a.data[lane][0] : 0.0f, lane < K ? L.a.data[lane][1] : 0.0f,
                    lane < K ? L.a.data[lane][2] : 0.0f, lane < K ? L.a.joint_scales[lane] : 0.0f);
             s = t + 1;
+            if (lane == 0) {
+                lds_release(&S.own_on, 0);
+                lds_release(&S.decided, s);
+            }
             STAMP(3);
         }
         if (lane == 0) lds_release(&S.done, 1);
@@ -1942,6 +2333,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
     __shared__ SeedLoopSharedX S;
     __shared__ int s_ncol[2 * PP_MAX_EDGES];  // set-A column counts per (CAF, direction)
     __shared__ int s_cofs[2 * PP_MAX_EDGES];  // their LDS offsets in s_cols (-1: global)
+    __shared__ SeedOcc s_occ;  // per-seed occupancy (the image's own workgroup)
     // kColLds floats (dynamic: the launch sizes it), then with n_ext > 0 the external
     // slots' joints (cache_joints)
     extern __shared__ float s_cols[];
@@ -1993,6 +2385,9 @@ void seed_loop_ext_kernel(GrowArgs g) {
     if (threadIdx.x == 0) {
         S.done = 0;
         S.ext_ticks = 0u;
+        S.plan_lock = 0;
+        S.decided = 0;
+        S.own_on = 0;
     }
     __syncthreads();
 
@@ -2011,6 +2406,9 @@ void seed_loop_ext_kernel(GrowArgs g) {
     const OccGrid occ = occ_grid(occ_base, K, (int)((double)g.hh / g.cfg.occupancy_reduction),
                                  (int)((double)g.ww / g.cfg.occupancy_reduction));
     const int n_help = kSeedWaves + (X ? g.n_ext * kSeedWaves : 0);  // helper lanes 1 .. n_help-1
+    // the occupancy at the seeds in LDS (seed_occ_*), or the global grid for more seeds
+    const bool socc_on = kSeedOcc && !external && n_seeds <= kOccSeeds;  // block-uniform
+    if (socc_on) seed_occ_init(s_occ, seeds, n_seeds, K, occ, red);
 
     // committer state (wave 0)
     int n_anns = 0, s = 0;
@@ -2029,7 +2427,10 @@ void seed_loop_ext_kernel(GrowArgs g) {
         n_anns++;
         const uint32_t set = (uint32_t)__ballot(lane < K && jv > 0.0f);
         unset_mask |= ~set & (K >= 32 ? 0xFFFFFFFFu : ((1u << K) - 1u));
-        occ_mark(g, L, log, occ, jx, jy, js, jv != 0.0f, K);
+        if (socc_on)
+            seed_occ_mark(g, s_occ, occ, jx, jy, js, jv != 0.0f, K);
+        else
+            occ_mark(g, L, log, occ, jx, jy, js, jv != 0.0f, K);
     };
 
     if (external || wave > 0) {
@@ -2083,11 +2484,19 @@ void seed_loop_ext_kernel(GrowArgs g) {
             // release alone does not wait for them)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             wave_sync();
-            if (lane == 0) {
-                lds_release(&S.cache_state[q], 2);
-                lds_release(&S.task[wave], -1);
-            }
+            if (lane == 0) lds_release(&S.cache_state[q], 2);
             wave_sync();
+            // plan this wave's next grow itself (as in seed_loop_kernel), into this CU's slots
+            plan_lock(S);
+            uint64_t left = 1ull << wave;
+            if (kSelfPlan && !lds_acquire(&S.done)) {
+                const int dec = lds_acquire(&S.decided);
+                left = spec_plan(S, reinterpret_cast<const float4 *>(s_cols + kColLds), seeds,
+                                 n_seeds, dec, dec, kSelfScan, occ, red, occ_msr(g), g.spec_far,
+                                 left, socc_on ? s_occ.cnt : nullptr);
+            }
+            if (left && lane == 0) lds_release(&S.task[wave], -1);
+            plan_unlock(S);
         }
         if (external) return;
     } else {
@@ -2119,8 +2528,12 @@ void seed_loop_ext_kernel(GrowArgs g) {
                 const int idx = s + lane;
                 bool is_free = false;
                 if (idx < n_seeds) {
-                    const pp_seed c = seeds[idx];
-                    is_free = !occ_get(occ, c.field, c.x, c.y, red);
+                    if (socc_on) {
+                        is_free = s_occ.cnt[idx] == 0;
+                    } else {
+                        const pp_seed c = seeds[idx];
+                        is_free = !occ_get(occ, c.field, c.x, c.y, red);
+                    }
                 }
                 const uint64_t m = __ballot(is_free);
                 if (m == 0) {
@@ -2177,6 +2590,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
                 else
                     commit(&xrec[hslot - kSpecCache], true, jq.x, jq.y, jq.z, jq.w);
                 s = t + 1;
+                if (lane == 0) lds_release(&S.decided, s);  // the slot is free again
 #ifdef PP_STAMPS
                 n_hits++;
 #endif
@@ -2185,6 +2599,15 @@ void seed_loop_ext_kernel(GrowArgs g) {
             }
             // a miss: hand far-away free seeds to the idle helpers, then grow t here
             const pp_seed st = seeds[t];
+            plan_lock(S);  // this CU's helpers plan for themselves too
+            if (lane == 0) {
+                S.own_x = st.x;
+                S.own_y = st.y;
+                S.own_s = st.s;
+                lds_release(&S.own_on, 1);
+                lds_release(&S.decided, t);
+            }
+            wave_sync();
             ext_refresh(S, s_cols, X, xrec, -1);
             int tk = 0;
             if (lane > 0 && lane < kSeedWaves)
@@ -2206,7 +2629,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
                 if (ok) {
                     c = seeds[idx];
                     ok = spec_far(g.spec_far, c.x, c.y, c.s, st.x, st.y, st.s) &&
-                         !occ_get(occ, c.field, c.x, c.y, red);
+                         !(socc_on ? s_occ.cnt[idx] != 0 : occ_get(occ, c.field, c.x, c.y, red));
                 }
                 // cache entries (uniform loop): skip seeds they hold, seeds that a grown
                 // annotation's occupancy boxes will cover once committed, and seeds near
@@ -2275,11 +2698,11 @@ void seed_loop_ext_kernel(GrowArgs g) {
                     fly |= 1ull << q;
                     ahead |= 1ull << q;
                     if (lane == 0) {
-                        S.cache_seed[q] = sd;
                         S.cache_x[q] = cx;
                         S.cache_y[q] = cy;
                         S.cache_s[q] = csc;
-                        S.cache_state[q] = 1;
+                        lds_release(&S.cache_state[q], 1);  // state first (spec_plan)
+                        lds_release(&S.cache_seed[q], sd);
                         S.cache_t[q] = (uint32_t)__builtin_amdgcn_s_memrealtime();
                         if (use_l) {
                             S.task_slot[w] = q;
@@ -2289,6 +2712,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
                     wave_sync();
                 }
             }
+            plan_unlock(S);
 #ifdef PP_STAMPS
             n_rounds++;
 #endif
@@ -2300,6 +2724,10 @@ void seed_loop_ext_kernel(GrowArgs g) {
                    lane < K ? L.a.data[lane][1] : 0.0f, lane < K ? L.a.data[lane][2] : 0.0f,
                    lane < K ? L.a.joint_scales[lane] : 0.0f);
             s = t + 1;
+            if (lane == 0) {
+                lds_release(&S.own_on, 0);
+                lds_release(&S.decided, s);
+            }
             STAMP(3);
         }
         if (lane == 0) {
@@ -2366,7 +2794,7 @@ __global__ __launch_bounds__(64) void complete_kernel(GrowArgs g) {
         copy_ann(&L.a, &work[i]);
         uint32_t unfilled = 0;
         for (int j = 0; j < K; j++) unfilled |= (L.a.data[j][2] == 0.0f) ? (1u << j) : 0u;
-        grow<false>(g, L, img, 1, false);
+        grow<false, GrowLDS, kCompleteAhead>(g, L, img, 1, false);
         bool any0 = false;
         for (int j = 0; j < K; j++) {
             float &v = L.a.data[j][2];
@@ -2566,7 +2994,24 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
         const long oh = (long)((double)(long)(s_my + 1.0f) / g.cfg.occupancy_reduction);
         const long ow = (long)((double)(long)(s_mx + 1.0f) / g.cfg.occupancy_reduction);
         const OccGrid no = occ_grid(nullptr, K, (int)(oh > 0 ? oh : 0), (int)(ow > 0 ? ow : 0));
-        for (int f = wave; f < K; f += kNmsWaves) {  // nms.py:34-45, one plane per pass
+        // the first 64 sorted annotations' joints of every plane this wave walks, loaded in
+        // one round trip (their work indices in one more) instead of three per plane
+        constexpr int kNmsPre = 4;  // planes per wave prefetched (K <= 32)
+        int wi0 = 0;
+        float pre[kNmsPre][4];
+        if (lane < m) wi0 = keep[perm[lane]];
+#pragma unroll
+        for (int u = 0; u < kNmsPre; u++) {
+            const int f = wave + u * kNmsWaves;
+            pre[u][0] = pre[u][1] = pre[u][2] = pre[u][3] = 0.0f;
+            if (f < K && lane < m) {
+                pre[u][0] = work[wi0].data[f][0];
+                pre[u][1] = work[wi0].data[f][1];
+                pre[u][2] = work[wi0].data[f][2];
+                pre[u][3] = work[wi0].joint_scales[f];
+            }
+        }
+        for (int f = wave, u = 0; f < K; f += kNmsWaves, u++) {  // nms.py:34-45, one plane per pass
             int nbox = 0;
             int2 rb[kNmsRegBoxes];  // (x0 | x1 << 16, y0 | y1 << 16); zero: covers nothing
 #pragma unroll
@@ -2575,7 +3020,17 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
                 const int r = r0 + lane;
                 int wi = 0;
                 float jx = 0.0f, jy = 0.0f, jv = 0.0f, js = 0.0f;
-                if (r < m) {
+                if (r0 == 0 && u < kNmsPre) {  // prefetched (selects: no dynamic index)
+                    wi = wi0;
+#pragma unroll
+                    for (int w = 0; w < kNmsPre; w++)
+                        if (w == u) {
+                            jx = pre[w][0];
+                            jy = pre[w][1];
+                            jv = pre[w][2];
+                            js = pre[w][3];
+                        }
+                } else if (r < m) {
                     wi = keep[perm[r]];
                     jx = work[wi].data[f][0];
                     jy = work[wi].data[f][1];
@@ -2623,7 +3078,9 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
                                 gbox[nbox] = nb;
                             }
                             nbox++;
-                            wave_sync();
+                            // only a box in global memory needs the fence (a fence here waits
+                            // for every outstanding store, e.g. the suppressed v above)
+                            if (nbox > kNmsRegBoxes * 64) wave_sync();
                         }
                     }
                 }
@@ -2705,7 +3162,8 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
 namespace pp {
 
 int launch_seeds(const Heads &h, const HrMap &hr, int n_img, int K, const pp_config *cfg,
-                 pp_seed *seeds, int cap, int *counts, void *scratch, hipStream_t s);
+                 pp_seed *seeds, int cap, int *counts, void *scratch, hipStream_t s,
+                 bool emitted);
 size_t seeds_scratch_size(int n_img, int cap);
 int launch_caf_bucketed(const Heads &h, const HrMap &hr, int n_img, int K, int C,
                         const int32_t *skeleton, const pp_config *cfg, float th, float *cols,
@@ -2976,14 +3434,19 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
             return rc;
         }
     }
+    // the block-sparse map's kernel emits the seeds too when it can (stage 1 then writes
+    // what seeds_emit_kernel would; stage 2 sorts them): the same test in both stages
+    const bool fused_seeds = !d_cifhr && cifhr_fuses_seeds(h, n_img, K, cfg);
     if (stages & 1u) {
-        if (d_cifhr)
+        if (d_cifhr) {
             rc = cifhr_heads_launch<false>(h, n_img, K, cfg, d_cifhr, ws + d.off_cifhr_ws,
                                            d.cifhr_ws_bytes, s, "pp_decode_batch(cifhr)");
-        else
+        } else {
+            const SeedSink sink = seed_sink(n_img, K, cfg, d.seed_cap, ws + d.off_seed_ws);
             rc = cifhr_sparse_launch(h, n_img, K, cfg, hr_base, (float *)(ws + d.off_hr_aux),
                                      hr_masks, ws + d.off_cifhr_ws, d.cifhr_ws_bytes, s,
-                                     "pp_decode_batch(cifhr)");
+                                     "pp_decode_batch(cifhr)", fused_seeds ? &sink : nullptr);
+        }
         if (rc) return rc;
     }
     // CifSeeds and CafScored both read only the fields and the CifHr map: with both stages
@@ -3006,7 +3469,7 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
                                      side->stream);
         if (!rc)
             rc = launch_seeds(h, hr, n_img, K, cfg, seeds, d.seed_cap, seed_counts,
-                              ws + d.off_seed_ws, s);
+                              ws + d.off_seed_ws, s, fused_seeds);
         // join even after a failed launch, so the caller's stream never runs ahead
         if (hipEventRecord(side->join, side->stream) != hipSuccess ||
             hipStreamWaitEvent(s, side->join, 0) != hipSuccess)
@@ -3015,7 +3478,7 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
     } else {
         if (stages & 2u) {
             rc = launch_seeds(h, hr, n_img, K, cfg, seeds, d.seed_cap, seed_counts,
-                              ws + d.off_seed_ws, s);
+                              ws + d.off_seed_ws, s, fused_seeds);
             if (rc) return rc;
         }
         if (stages & 4u) {  // CafScored at caf_threshold; the force-complete set is lazy

@@ -172,6 +172,9 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nblocks) {
 // rows of one column of the decoder's bucketed CAF sets (caf_bucketed_kernel): score,
 // source x, y, target x, y, target scale, row-major index (as float bits)
 constexpr int kColRows = 7;
+// force-complete sets (caf_bucketed_kernel<true, ...>) of at most this many cells per
+// (image, field) store u16 cell indices (the LDS-stash build), larger ones int32
+constexpr int kSetBIdx16Max = 8192;
 
 // The CIF and CAF heads of one decode (a FieldConfig, field_config.py:7-13); a
 // single-scale decode is one CIF and one CAF head.  Concatenated cell index of CAF head m =
@@ -232,8 +235,30 @@ int cifhr_heads_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config
 // the decoder's block-sparse scratch map (HrMap with masks): d_map (n_img * K, tiles, 64, 64),
 // d_masks (n_img * K, tiles); d_aux (same size as d_map) only when h.n_groups > 1
 size_t cifhr_sparse_workspace_size(const Heads &h, int n_img, int K);
+
+// Seed emission fused into the decoder's CifHr kernel (cif_seeds.py:28-47 run by the
+// workgroup that has just written the field's map): the per-(image, field) segments
+// seeds_emit_kernel writes, in its layout (SeedArgs in stages.hip), for seeds_sort_kernel.
+struct SeedSink {
+    float *g_keys;   // (n_img, 4, cap): v, x, y, s planes; field f's segment at f * H * W
+    int *g_f;        // (n_img, cap) field of each slot
+    int *f_counts;   // (n_img, K) seeds per field
+    int64_t cap;     // K * H * W
+    int K;
+    float th, score_scale;
+    uint32_t skip;   // pp_config.seed_skip_mask
+};
+// the seeds scratch of launch_seeds as a SeedSink (stages.hip)
+SeedSink seed_sink(int n_img, int K, const pp_config *cfg, int cap, void *scratch);
+// whether the decoder emits the seeds inside its CifHr kernel for this batch: one CIF head,
+// fields not split over workgroups (sparse_split == 1), seed threshold >= CifHr threshold
+// (every seed cell is then a splat of the field's list); launch_seeds then only sorts
+bool cifhr_fuses_seeds(const Heads &h, int n_img, int K, const pp_config *cfg);
+
+// `sink` (NULL: none): emit the seeds too (cifhr_fuses_seeds must hold)
 int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config *cfg,
                         float *d_map, float *d_aux, uint64_t *d_masks, void *d_workspace,
-                        size_t workspace_bytes, hipStream_t s, const char *who);
+                        size_t workspace_bytes, hipStream_t s, const char *who,
+                        const SeedSink *sink = nullptr);
 
 }  // namespace pp

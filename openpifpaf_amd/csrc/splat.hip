@@ -237,17 +237,19 @@ __device__ __forceinline__ float fold_add(float acc, float vv) {
     return __builtin_fminf(acc + vv, 1.0f);  // (a < 1) ? a : 1; a NaN gives 1 either way
 }
 
-// Folds the candidates `q` (bits, ascending) of FoldCand array `cand` into this lane's
-// pixel: two at a time on the fast path, one at a time when the set holds a slow one.
-__device__ __forceinline__ float fold_block(float acc, const FoldCand *cand, uint64_t q,
-                                            uint64_t slow, float fx, float fy, uint32_t key) {
+// Folds the candidates `q` (bits, ascending) of a candidate array into this lane's pixel:
+// two at a time on the fast path, one at a time when the set holds a slow one.  `get(c)`
+// returns candidate c (a FoldCand array, or an index list into the field's LDS list).
+template <typename Get>
+__device__ __forceinline__ float fold_block_g(float acc, Get get, uint64_t q, uint64_t slow,
+                                              float fx, float fy, uint32_t key) {
     if (q & slow) {
         for (; q; q &= q - 1) {
             const int c = __builtin_ctzll(q);
             if ((slow >> c) & 1ull)
-                acc = fold_apply(acc, fold_term_slow(cand[c], fx, fy, key));
+                acc = fold_apply(acc, fold_term_slow(get(c), fx, fy, key));
             else
-                acc = fold_add(acc, fold_vv(cand[c], fx, fy, key));
+                acc = fold_add(acc, fold_vv(get(c), fx, fy, key));
         }
         return acc;
     }
@@ -258,12 +260,18 @@ __device__ __forceinline__ float fold_block(float acc, const FoldCand *cand, uin
         q &= ~(1ull << c1);
         const int c2 = __builtin_ctzll(q);
         q &= ~(1ull << c2);
-        const float v1 = fold_vv(cand[c1], fx, fy, key);
-        const float v2 = fold_vv(cand[c2], fx, fy, key);
+        const float v1 = fold_vv(get(c1), fx, fy, key);
+        const float v2 = fold_vv(get(c2), fx, fy, key);
         acc = fold_add(fold_add(acc, v1), v2);
     }
-    if (np & 1) acc = fold_add(acc, fold_vv(cand[__builtin_ctzll(q)], fx, fy, key));
+    if (np & 1) acc = fold_add(acc, fold_vv(get(__builtin_ctzll(q)), fx, fy, key));
     return acc;
+}
+
+__device__ __forceinline__ float fold_block(float acc, const FoldCand *cand, uint64_t q,
+                                            uint64_t slow, float fx, float fy, uint32_t key) {
+    return fold_block_g(acc, [cand](int c) -> const FoldCand & { return cand[c]; }, q, slow, fx,
+                        fy, key);
 }
 
 // wave-wide OR of a 64-bit value through one LDS word
@@ -869,6 +877,7 @@ struct HrSparseArgs {
     uint32_t *pre_bits;     // (n_img * K, kTileBits / 32) touched tiles
     int *pre_rowcnt;        // (n_img * K, kMaxBinRows) bin sizes (-1: none), offsets
     int *pre_rowoff;
+    SeedSink seeds;         // cifhr_fused_kernel<true>: where the field's seeds go
 };
 
 __device__ __forceinline__ float nan_max(float a, float b) {  // np.maximum
@@ -1249,6 +1258,346 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
 }
 
 // -------------------------------------------------------------------------------------
+// The decoder's CifHr for batches whose fields each get one workgroup (one CIF head, one
+// group, split 1), with the field's candidate list in LDS and, optionally (SEEDS), the
+// field's seeds emitted by the same workgroup (cif_seeds.py:28-47).
+//
+// Phase 1 is hr_splat_list's (one confidence round per 8192 cells, kept cells staged in
+// LDS, then their x / y / scale), but the first kFuList candidates stay in LDS: a field
+// with at most kFuList splats (planted input: about 125) never writes or re-reads a list in
+// global memory.  Longer lists go to the global list (the LDS part copied after it) and
+// take cifhr_sparse_kernel's row bins and per-wave candidate copies, in the same LDS.
+// SEEDS: the kept cells with c > seed_threshold (a subset: seed threshold >= CifHr
+// threshold) are the seed candidates, in row-major order; their (c, x * stride,
+// y * stride, s * stride) go to the field's segment of the seeds scratch in candidate
+// order.
+//
+// Phase 2 as cifhr_sparse_kernel's, whole tiles per wave; with the list in LDS a wave's
+// candidates for a tile are indices into it (no copies, no global reads).
+//
+// Phase 3 (SEEDS), after a barrier (the map's blocks and masks are this workgroup's own
+// stores): each candidate looks up the map at its position (scalar_values, HrMap::at),
+// v = 0.9 h + 0.1 c (times score_scale), and the ones with v > threshold are compacted in
+// order into the same segment, as seeds_emit_kernel writes it; seeds_sort_kernel follows.
+// -------------------------------------------------------------------------------------
+constexpr int kFuList = 256;   // fold candidates of a field held in LDS
+constexpr int kFuStage = 512;  // kept cells of a round staged in LDS
+
+template <bool LDS>
+__device__ __forceinline__ void fused_phase2(const HrSparseArgs &a, int64_t fld, int total,
+                                             bool use_bins, const FoldCand *s_list,
+                                             FoldCand *cand, uint8_t *idx,
+                                             const uint32_t *s_bits, const int *s_rowcnt,
+                                             const int *s_rowoff, uint64_t *s_live, int *s_next) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const FoldCand *glist = a.list + fld * a.list_cap;
+    const int lx = lane & 7, ly = lane >> 3;
+    const int nwords = (a.tiles + 31) >> 5;
+    int wd = 0, li = 0;
+    uint32_t bits = __builtin_amdgcn_readfirstlane(s_bits[0]);
+    auto get = [&](int c) -> const FoldCand & {
+        if constexpr (LDS) return s_list[idx[c]];
+        else return cand[c];
+    };
+    while (true) {
+        int claim = 0;
+        if (lane == 0) claim = atomicAdd(s_next, 1);
+        const int target = __builtin_amdgcn_readfirstlane(claim);
+        int t = -1;
+        while (wd < nwords) {
+            if (!bits) {
+                if (++wd < nwords) bits = __builtin_amdgcn_readfirstlane(s_bits[wd]);
+                continue;
+            }
+            if (li == target) {
+                t = wd * 32 + __builtin_ctz(bits);
+                break;
+            }
+            bits &= bits - 1;
+            li++;
+        }
+        if (t < 0) break;
+        const int tx0 = (t % a.tiles_x) * kTile, ty0 = (t / a.tiles_x) * kTile;
+        float *mp = a.map + (fld * a.tiles + t) * (int64_t)(kTile * kTile);
+        uint64_t done = 0;
+        const int row = t / a.tiles_x;
+        const int rc = (!LDS && use_bins) ? s_rowcnt[row] : -1;
+        const FoldCand *src = rc >= 0 ? a.bins + fld * a.bins_cap + s_rowoff[row] : glist;
+        const int src_n = rc >= 0 ? rc : total;
+        int cursor = 0;
+        while (true) {
+            int n = 0;
+            while (cursor < src_n) {
+                const int e = cursor + lane;
+                bool hit = false;
+                FoldCand c;
+                uint32_t lo = 0, hi = 0;
+                if (e < src_n) {
+                    if constexpr (LDS) {
+                        lo = s_list[e].lo;
+                        hi = s_list[e].hi;
+                    } else {
+                        c = src[e];
+                        lo = c.lo;
+                        hi = c.hi;
+                    }
+                    const int x0 = (int)(lo & 0xffff), x1 = (int)(hi & 0xffff) + 1;
+                    const int y0 = (int)(lo >> 16), y1 = (int)(hi >> 16) + 1;
+                    hit = x1 > tx0 && x0 < tx0 + kTile && y1 > ty0 && y0 < ty0 + kTile;
+                }
+                const uint64_t mk = __ballot(hit);
+                const int cnt = __popcll(mk);
+                if (n + cnt > kSpCand) break;  // wave-uniform; chunk re-read next pass
+                if (hit) {
+                    const int pos = n + lane_prefix(mk);
+                    if constexpr (LDS) idx[pos] = (uint8_t)e;
+                    else cand[pos] = c;
+                }
+                n += cnt;
+                cursor += 64;
+            }
+            const bool last = cursor >= src_n;
+            wave_sync();
+            uint64_t cl = 0ull;
+            bool slow_l = false;
+            if (lane < n) {
+                cl = cand_live(get(lane), tx0, ty0);
+                slow_l = cand_slow(get(lane));
+            }
+            const uint64_t slow = __ballot(slow_l);
+            const uint64_t live = wave_or64(cl, &s_live[wave]);
+            for (uint64_t rest = live; rest; rest &= rest - 1) {
+                const int blk = __builtin_ctzll(rest);
+                const int px = tx0 + 8 * (blk & 7) + lx, py = ty0 + 8 * (blk >> 3) + ly;
+                const bool on = px < a.ww && py < a.hh;
+                const float fx = on ? (float)px : kOffMapCoord, fy = on ? (float)py : kOffMapCoord;
+                const uint32_t key = on ? pix_key(px, py) : kOffMapKey;
+                const uint64_t bq = __ballot((cl >> blk) & 1ull);
+                float acc = ((done >> blk) & 1ull) ? mp[blk * 64 + lane] : 0.0f;
+                acc = fold_block_g(acc, get, bq, slow, fx, fy, key);
+                __builtin_nontemporal_store(acc, &mp[blk * 64 + lane]);
+            }
+            done |= live;
+            if (last) break;
+            wave_sync();  // candidate arrays are rewritten by the next pass
+        }
+        if (lane == 0) a.masks[fld * a.tiles + t] = done;
+    }
+}
+
+template <bool SEEDS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void cifhr_fused_kernel(HrSparseArgs a) {
+    // the field's list (<= kFuList entries), or with a longer list the per-wave candidate
+    // copies of phase 2
+    __shared__ __attribute__((aligned(16))) FoldCand s_list[kFuList];
+    static_assert(kFuList >= 4 * kSpCand, "per-wave candidate copies share the list's LDS");
+    __shared__ uint8_t s_idx[4][kSpCand];
+    __shared__ uint32_t s_bits[kTileBits / 32];
+    __shared__ RowBinLds s_rb;
+    __shared__ int s_rowcnt[kMaxBinRows], s_rowoff[kMaxBinRows];
+    __shared__ __attribute__((aligned(16))) int s_cnt[2][kSpU][4];
+    __shared__ int s_stage[kFuStage];
+    __shared__ int s_tmp[4];
+    __shared__ uint64_t s_live[4];
+    __shared__ int s_next;
+
+    const int64_t fld = blockIdx.x;  // image * K + field
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (threadIdx.x == 0) s_next = 0;
+    if (threadIdx.x < kTileBits / 32) s_bits[threadIdx.x] = 0u;
+    FoldCand *glist = a.list + fld * a.list_cap;
+    const float stride = (float)a.h.cstride[0];
+    const bool ms_on = a.h.ms_on & 1u;
+    const float ms_th = a.h.ms_th[0];
+    const int hw = a.h.cH[0] * a.h.cW[0];
+    const float *p = a.h.cif[0] + fld * 5 * (int64_t)hw;
+    // seeds: field f of image img, its segment of the scratch (SeedArgs::seg_base(0, f))
+    const SeedSink &ss = a.seeds;
+    const int f = SEEDS ? (int)(fld % ss.K) : 0;
+    const int64_t img = SEEDS ? fld / ss.K : 0;
+    const bool seeding = SEEDS && !((ss.skip >> f) & 1u);
+    float *sv = SEEDS ? ss.g_keys + img * 4 * ss.cap + (int64_t)f * hw : nullptr;
+    float *sx = sv + ss.cap, *sy = sx + ss.cap, *sz = sy + ss.cap;
+    int n_seed = 0;
+
+    // ---- phase 1: the list (cif_hr.py:26-40) and the seed candidates (cif_seeds.py:28-33) ----
+    // candidate of kept cell `cell` at list position pos; returns its (c, x, y, s) * stride
+    auto emit = [&](int cell, int pos, float &c, float &x8, float &y8, float &s8) {
+        c = p[cell];
+        const float x = p[hw + cell], y = p[2 * hw + cell], s4 = p[4 * hw + cell];
+        const float cx = x * stride, cy = y * stride;
+        const float sg = (0.5f * s4) * stride;
+        const float sigma = (sg != sg) ? sg : fmaxf(1.0f, sg);  // np.maximum keeps NaN
+        const float v = (c / a.neighbors) / 1.0f;                 // v / neighbors / len_cifs
+        const int4 box = splat_box<M_GAUSS_MAX>(cx, cy, 1.0f * sigma, a.hh, a.ww);
+        const FoldCand fc = make_cand(box, make_float4(cx, cy, v, sigma * sigma), a.hh, a.ww);
+        if (pos < kFuList)
+            s_list[pos] = fc;
+        else
+            glist[pos] = fc;
+        for (int ty = box.z / kTile; ty <= (box.w - 1) / kTile; ty++)
+            for (int tx = box.x / kTile; tx <= (box.y - 1) / kTile; tx++) {
+                const int t = ty * a.tiles_x + tx;
+                atomicOr(&s_bits[t >> 5], 1u << (t & 31));
+            }
+        x8 = cx;
+        y8 = cy;
+        s8 = s4 * stride;
+    };
+    // block-uniform: one seed-candidate compaction over the threads' (flag, values)
+    auto seed_cand = [&](bool cand, float c, float x8, float y8, float s8) {
+        if constexpr (SEEDS) {
+            int tot;
+            const int slot = block_compact<4>(cand, s_tmp, tot);
+            if (cand) {
+                sv[n_seed + slot] = c;
+                sx[n_seed + slot] = x8;
+                sy[n_seed + slot] = y8;
+                sz[n_seed + slot] = s8;
+            }
+            n_seed += tot;
+        }
+    };
+    int running = 0, buf = 0;
+    for (int base = 0; base < hw; base += 256 * kSpU) {
+        float c[kSpU];
+#pragma unroll
+        for (int k = 0; k < kSpU; k++) {
+            const int cell = base + k * 256 + (int)threadIdx.x;
+            c[k] = cell < hw ? p[cell] : NAN;  // NaN: never > v_th
+        }
+        uint32_t keep = 0;
+#pragma unroll
+        for (int k = 0; k < kSpU; k++) keep |= (c[k] > a.v_th) ? (1u << k) : 0u;
+        if (ms_on) {  // p[4] > min_scale / stride (cif_hr.py:29-30, cif_seeds.py:31-32)
+            uint32_t km = keep;
+#pragma unroll
+            for (int k = 0; k < kSpU; k++)
+                if ((keep >> k) & 1u) {
+                    const int cell = base + k * 256 + (int)threadIdx.x;
+                    if (!(p[4 * hw + cell] > ms_th)) km &= ~(1u << k);
+                }
+            keep = km;
+        }
+#pragma unroll
+        for (int k = 0; k < kSpU; k++) {
+            const uint64_t bal = __ballot((keep >> k) & 1u);
+            if (lane == 0) s_cnt[buf][k][wave] = __popcll(bal);
+        }
+        __syncthreads();  // (also orders the s_bits clear before the first atomicOr)
+        int off = 0;
+#pragma unroll 4
+        for (int k = 0; k < kSpU; k++) {
+            const int4 q = *reinterpret_cast<const int4 *>(&s_cnt[buf][k][0]);
+            off += q.x + q.y + q.z + q.w;
+        }
+        if (off <= kFuStage) {
+            int o = 0;
+#pragma unroll 4
+            for (int k = 0; k < kSpU; k++) {
+                const int4 q = *reinterpret_cast<const int4 *>(&s_cnt[buf][k][0]);
+                const uint64_t bal = __ballot((keep >> k) & 1u);
+                if ((keep >> k) & 1u)
+                    s_stage[o + (wave > 0 ? q.x : 0) + (wave > 1 ? q.y : 0) + (wave > 2 ? q.z : 0) +
+                            lane_prefix(bal)] = base + k * 256 + (int)threadIdx.x;
+                o += q.x + q.y + q.z + q.w;
+            }
+            __syncthreads();
+            for (int e0 = 0; e0 < off; e0 += 256) {  // block-uniform
+                const int e = e0 + (int)threadIdx.x;
+                float cc = 0.0f, x8 = 0.0f, y8 = 0.0f, s8 = 0.0f;
+                if (e < off) emit(s_stage[e], running + e, cc, x8, y8, s8);
+                seed_cand(seeding && e < off && cc > ss.th, cc, x8, y8, s8);
+            }
+        } else {  // more than the stage holds: batch by batch (not unrolled)
+            int o = 0;
+#pragma unroll 1
+            for (int k = 0; k < kSpU; k++) {
+                const int4 q = *reinterpret_cast<const int4 *>(&s_cnt[buf][k][0]);
+                const uint64_t bal = __ballot((keep >> k) & 1u);
+                const bool kept = (keep >> k) & 1u;
+                float cc = 0.0f, x8 = 0.0f, y8 = 0.0f, s8 = 0.0f;
+                if (kept)
+                    emit(base + k * 256 + (int)threadIdx.x,
+                         running + o + (wave > 0 ? q.x : 0) + (wave > 1 ? q.y : 0) +
+                             (wave > 2 ? q.z : 0) + lane_prefix(bal),
+                         cc, x8, y8, s8);
+                seed_cand(seeding && kept && cc > ss.th, cc, x8, y8, s8);
+                o += q.x + q.y + q.z + q.w;
+            }
+        }
+        running += off;
+        buf ^= 1;
+        __syncthreads();  // the stage is rewritten by the next round
+    }
+    const int total = running;
+    const bool lds = total <= kFuList;
+    bool use_bins = false;
+    if (!lds) {
+        // the LDS part joins the global list; the LDS then holds phase 2's candidate copies
+        if (threadIdx.x < kFuList) glist[threadIdx.x] = s_list[threadIdx.x];
+        __syncthreads();
+        use_bins = a.bins_cap > 0 && total > kBinMin;
+        if (use_bins)
+            hr_row_bins(glist, total, a.bins + fld * a.bins_cap, a.bins_cap, a.tiles_y, s_rb,
+                        s_rowcnt, s_rowoff);
+    }
+    for (int t = threadIdx.x; t < a.tiles; t += 256)  // untouched tiles: no block written
+        if (!((s_bits[t >> 5] >> (t & 31)) & 1u)) a.masks[fld * a.tiles + t] = 0ull;
+
+    // ---- phase 2: the waves take the touched tiles from an LDS counter ----
+    if (lds)
+        fused_phase2<true>(a, fld, total, false, s_list, nullptr, s_idx[wave], s_bits, s_rowcnt,
+                           s_rowoff, s_live, &s_next);
+    else
+        fused_phase2<false>(a, fld, total, use_bins, nullptr, s_list + wave * kSpCand, nullptr,
+                            s_bits, s_rowcnt, s_rowoff, s_live, &s_next);
+
+    // ---- phase 3: the seeds (cif_seeds.py:35-47) from the finished map ----
+    if constexpr (SEEDS) {
+        __syncthreads();  // every wave's blocks and masks are stored
+        HrMap hm{};
+        hm.base = a.map;
+        hm.masks = a.masks;
+        hm.hh = a.hh;
+        hm.ww = a.ww;
+        hm.tiles_x = a.tiles_x;
+        hm.tiles = a.tiles;
+        int kept = 0;
+        int *sf = ss.g_f + img * ss.cap + (int64_t)f * hw;
+        for (int e0 = 0; e0 < n_seed; e0 += 256) {  // block-uniform
+            const int e = e0 + (int)threadIdx.x;
+            float v = 0.0f, x = 0.0f, y = 0.0f, sc = 0.0f;
+            bool ok = false;
+            if (e < n_seed) {
+                const float c = sv[e];
+                x = sx[e];
+                y = sy[e];
+                sc = sz[e];
+                const float hv = hm.at(fld, x, y, 0.0f);
+                float vv = 0.9f * hv + 0.1f * c;  // 0.9 * v + 0.1 * c
+                if (ss.score_scale != 1.0f) vv = vv * ss.score_scale;
+                v = vv;
+                ok = vv > ss.th;
+            }
+            int tot;
+            // every candidate of this round is in registers before the first write below
+            const int slot = block_compact<4>(ok, s_tmp, tot);
+            if (ok) {
+                const int pos = kept + slot;  // <= e: earlier candidates only
+                sv[pos] = v;
+                sx[pos] = x;
+                sy[pos] = y;
+                sz[pos] = sc;
+                sf[pos] = f;
+            }
+            kept += tot;
+        }
+        if (threadIdx.x == 0) ss.f_counts[fld] = kept;
+    }
+}
+
+// -------------------------------------------------------------------------------------
 // host launchers
 // -------------------------------------------------------------------------------------
 static inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
@@ -1419,9 +1768,18 @@ size_t cifhr_sparse_workspace_size(const Heads &h, int n_img, int K) {
     return bytes;
 }
 
+bool cifhr_fuses_seeds(const Heads &h, int n_img, int K, const pp_config *cfg) {
+#ifdef PP_NO_FUSED  // A/B builds (openpifpaf_amd.build variants)
+    return false;
+#endif
+    return h.n_cif == 1 && h.n_groups == 1 && h.group_size() == 1 && n_img > 0 && K > 0 &&
+           sparse_split((int64_t)n_img * K) == 1 && cfg->seed_threshold >= cfg->cif_threshold;
+}
+
 int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config *cfg,
                         float *d_map, float *d_aux, uint64_t *d_masks, void *d_workspace,
-                        size_t workspace_bytes, hipStream_t s, const char *who) {
+                        size_t workspace_bytes, hipStream_t s, const char *who,
+                        const SeedSink *sink) {
     if (!cfg || !d_map || !d_masks || !d_workspace || (h.n_groups > 1 && !d_aux))
         return fail(PP_EINVAL, std::string(who) + ": NULL argument");
     for (int m = 0; m < h.n_cif; m++)
@@ -1458,6 +1816,23 @@ int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_confi
     const int64_t nf = (int64_t)n_img * K;
     a.split = sparse_split(nf);
     const unsigned nblocks = (unsigned)(nf * a.split);
+    // one workgroup per field, one CIF head: the list-in-LDS kernel (with the seeds when a
+    // sink is given); fields of small batches split over several workgroups, and
+    // multi-scale groups, take cifhr_sparse_kernel
+#ifndef PP_NO_FUSED
+    if (a.split == 1 && h.n_cif == 1 && h.n_groups == 1 && h.group_size() == 1) {
+        if (sink) {
+            if (!cifhr_fuses_seeds(h, n_img, K, cfg) || sink->K != K)
+                return fail(PP_EINVAL, std::string(who) + ": seeds cannot be fused here");
+            a.seeds = *sink;
+            hipLaunchKernelGGL(cifhr_fused_kernel<true>, dim3(nblocks), dim3(256), 0, s, a);
+        } else {
+            hipLaunchKernelGGL(cifhr_fused_kernel<false>, dim3(nblocks), dim3(256), 0, s, a);
+        }
+        return check_launch(who);
+    }
+#endif
+    if (sink) return fail(PP_EINVAL, std::string(who) + ": seeds cannot be fused here");
     // split fields: one list per field, built before the fold (cifhr_list_kernel);
     // its lengths, tile bits and bin sizes go past the nf lists the prebuilt mode uses (the
     // workspace holds nf * split of them)

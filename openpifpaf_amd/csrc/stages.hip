@@ -73,6 +73,7 @@ struct SeedArgs {
     int *f_counts;      // (n_img, n_heads * K) seeds per segment (head, field)
     int *g_perm;        // (n_img, np_cap)
     int np_cap;
+    int parts;          // seeds_sort_kernel workgroups per image (> 1: rank placement)
     // first slot of segment (CIF head m, field f): K * cif_off[m] + f * H_m * W_m
     __device__ __forceinline__ int64_t seg_base(int m, int f) const {
         return (int64_t)K * h.cif_off[m] + (int64_t)f * h.cif_hw(m);
@@ -366,6 +367,19 @@ __device__ __forceinline__ int block_scan_1024(int v, int *s_w, int &total) {
     return before + incl - v;
 }
 
+// Small batches: a.parts workgroups per image.  One workgroup per image sorting ~2k keys
+// is the whole critical path of a one-image CifHr + seeds call (cfg2: 32 us), so up to
+// kRankMax seeds are PLACED instead: every thread holds at most two keys and counts the
+// keys that sort before each (the packed key is unique: its rank is the output position),
+// reading all keys from LDS in kSortLds chunks; keys tied with it in (v, field) are
+// compared by the reference's full tuple (x, y, s, then emission order) as finish() does.
+// More seeds take workgroup 0's sort below.
+constexpr int kRankParts = 4;
+constexpr int kRankMax = 2 * 1024 * kRankParts;  // 2 keys per thread, 4 workgroups of 1024
+// batches of at most this many images.  0: off -- measured much slower than the one-workgroup
+// network on cfg2 planted (2.2k keys: 245 vs 32 us): n^2 comparisons of 64-bit keys on 4 CUs
+constexpr int kRankImgs = 0;
+
 // 33 KB of LDS (keys + segment offsets; x / y / s stay in the emission buffer), so a
 // workgroup fits beside the seed loop's 104 KB on one CU (DecodePipeline overlaps them)
 __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
@@ -373,7 +387,7 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
     __shared__ int s_off[kMaxHeads * PP_MAX_KP + 1];
     __shared__ int s_scan[16];
     static_assert(kMaxHeads * PP_MAX_KP < 1024, "one thread per segment");
-    const int img = blockIdx.x;
+    const int img = blockIdx.x / a.parts, part = blockIdx.x % a.parts;
     const int nseg = a.h.n_cif * a.K;
     const int64_t cap = a.cap;
     const float *gv = a.g_keys + (int64_t)img * 4 * cap, *gx = gv + cap, *gy = gx + cap,
@@ -387,7 +401,7 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
         int total;
         const int pre = block_scan_1024(cnt, s_scan, total);
         if (q <= nseg) s_off[q] = pre;
-        if (q == 0) a.counts[img] = total;
+        if (q == 0 && part == 0) a.counts[img] = total;
     }
     __syncthreads();
     const int n = s_off[nseg];
@@ -406,6 +420,78 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
         }
         return a.seg_base(lo / a.K, lo % a.K) + (i - s_off[lo]);
     };
+    if (a.parts > 1 && n <= kRankMax) {
+        // rank placement: this workgroup's keys i = part * 1024 + tid (+ 4096)
+        uint64_t mk[2];
+        int cnt[2] = {0, 0};
+        bool tie = false;
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            const int i = (r * a.parts + part) * 1024 + (int)threadIdx.x;
+            mk[r] = 0ull;
+            if (i < n) {
+                const int64_t k = slot(i);
+                mk[r] = seed_key(gv[k], gf[k], i);
+            }
+        }
+        for (int c0 = 0; c0 < n; c0 += kSortLds) {  // block-uniform
+            const int m = min(kSortLds, n - c0);
+            __syncthreads();  // the previous chunk is read
+            for (int j = threadIdx.x; j < m; j += 1024) {
+                const int64_t k = slot(c0 + j);
+                s_key[j] = seed_key(gv[k], gf[k], c0 + j);
+            }
+            __syncthreads();
+            const uint64_t h0 = mk[0] >> 27, h1 = mk[1] >> 27;
+            int j = 0;
+            for (; j + 1 < m; j += 2) {  // two keys per LDS read
+                const uint64_t ka = s_key[j], kb = s_key[j + 1];
+                const uint64_t ha = ka >> 27, hb = kb >> 27;
+                cnt[0] += (int)(ha > h0) + (int)(hb > h0);
+                cnt[1] += (int)(ha > h1) + (int)(hb > h1);
+                tie |= (ha == h0 && ka != mk[0]) || (hb == h0 && kb != mk[0]) ||
+                       (ha == h1 && ka != mk[1]) || (hb == h1 && kb != mk[1]);
+            }
+            if (j < m) {
+                const uint64_t ka = s_key[j], ha = ka >> 27;
+                cnt[0] += (int)(ha > h0);
+                cnt[1] += (int)(ha > h1);
+                tie |= (ha == h0 && ka != mk[0]) || (ha == h1 && ka != mk[1]);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            const int i = (r * a.parts + part) * 1024 + (int)threadIdx.x;
+            if (i >= n) continue;
+            const int64_t ki = slot(i);
+            if (tie) {  // equal (v, field): the full tuple order (cif_seeds.py:54)
+                const uint64_t hi = mk[r] >> 27;
+                const int fi = gf[ki];
+                // keys of field fi: its segments (head m, field fi)
+                for (int q = fi; q < nseg; q += a.K)
+                for (int j = s_off[q]; j < s_off[q + 1]; j++) {
+                    if (j == i) continue;
+                    const int64_t kj = a.seg_base(q / a.K, q % a.K) + (j - s_off[q]);
+                    if ((seed_key(gv[kj], gf[kj], j) >> 27) != hi) continue;
+                    bool before;
+                    if (gx[kj] != gx[ki]) before = gx[kj] > gx[ki];
+                    else if (gy[kj] != gy[ki]) before = gy[kj] > gy[ki];
+                    else if (gs[kj] != gs[ki]) before = gs[kj] > gs[ki];
+                    else before = j < i;
+                    cnt[r] += (int)before;
+                }
+            }
+            pp_seed rec;
+            rec.v = gv[ki];
+            rec.field = gf[ki];
+            rec.x = gx[ki];
+            rec.y = gy[ki];
+            rec.s = gs[ki];
+            out[cnt[r]] = rec;
+        }
+        return;
+    }
+    if (part != 0) return;
     // the sorted keys kb[0 .. n) (LDS, or global scratch for more than kSortLds keys):
     // runs of equal (v, field) re-sorted by (x, y, s) descending, then emission order (one
     // thread per run, insertion sort), then the records written in order
@@ -719,7 +805,7 @@ constexpr int kStashA = 256;      // kept columns per direction (set A stash): 2
 // NT * kU cells.  More than kCandA cells fall back to the batched scan.
 constexpr int kCandA = 1024;
 constexpr int kConfU = 16;
-constexpr int kStashCells = 8192; // cells of all heads (set B stash: u16 bucket per direction)
+constexpr int kStashCells = kSetBIdx16Max; // cells of all heads (set B stash: u16 bucket per direction)
 constexpr uint16_t kNoBucket = 0xFFFF;
 
 struct StashCol {
@@ -1027,8 +1113,9 @@ __global__ __launch_bounds__(STASH && INDEX_ONLY ? 512 : 256) void caf_bucketed_
         const int ncell = (int)cc;
         for (int cell = threadIdx.x; cell < ncell; cell += NT) {
             const uint16_t bb = stash_b[cell], bf = stash_b[kStashCells + cell];
-            if (bb != kNoBucket) reinterpret_cast<int *>(bwd)[atomicAdd(&s_cnt[0][bb], 1)] = cell;
-            if (bf != kNoBucket) reinterpret_cast<int *>(fwd)[atomicAdd(&s_cnt[1][bf], 1)] = cell;
+            // u16 cell indices (cells <= kSetBIdx16Max): half the bytes to write and to read
+            if (bb != kNoBucket) reinterpret_cast<uint16_t *>(bwd)[atomicAdd(&s_cnt[0][bb], 1)] = (uint16_t)cell;
+            if (bf != kNoBucket) reinterpret_cast<uint16_t *>(fwd)[atomicAdd(&s_cnt[1][bf], 1)] = (uint16_t)cell;
         }
         return;
     }
@@ -1097,8 +1184,27 @@ __global__ __launch_bounds__(STASH && INDEX_ONLY ? 512 : 256) void caf_bucketed_
 
 static inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 
+SeedSink seed_sink(int n_img, int K, const pp_config *cfg, int cap, void *scratch) {
+    SeedSink k{};
+    char *w = (char *)scratch;
+    k.g_keys = (float *)w;
+    w += round_up((int64_t)n_img * 4 * cap * sizeof(float), 256);
+    k.g_f = (int *)w;
+    w += round_up((int64_t)n_img * cap * sizeof(int), 256);
+    k.f_counts = (int *)w;
+    k.cap = cap;
+    k.K = K;
+    k.th = cfg->seed_threshold;
+    k.score_scale = cfg->seed_score_scale;
+    k.skip = cfg->seed_skip_mask;
+    return k;
+}
+
+// `emitted`: the decoder's CifHr kernel already wrote the seed segments (cifhr_fuses_seeds,
+// SeedSink): only the sort runs
 int launch_seeds(const Heads &h, const HrMap &hr, int n_img, int K, const pp_config *cfg,
-                 pp_seed *seeds, int cap, int *counts, void *scratch, hipStream_t s) {
+                 pp_seed *seeds, int cap, int *counts, void *scratch, hipStream_t s,
+                 bool emitted) {
     if (K > PP_MAX_KP) return fail(PP_ESHAPE, "seeds: more than PP_MAX_KP CIF fields");
     if ((int64_t)cap < (int64_t)K * h.cif_cells())
         return fail(PP_ESHAPE, "seeds: capacity < K * cells");
@@ -1123,8 +1229,15 @@ int launch_seeds(const Heads &h, const HrMap &hr, int n_img, int K, const pp_con
     a.f_counts = (int *)w;
     w += round_up((int64_t)n_img * kMaxHeads * PP_MAX_KP * sizeof(int), 256);
     a.g_perm = (int *)w;
-    hipLaunchKernelGGL(seeds_emit_kernel, dim3((unsigned)((int64_t)n_img * h.n_cif * K)), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(seeds_sort_kernel, dim3(n_img), dim3(1024), 0, s, a);
+    if (!emitted)
+        hipLaunchKernelGGL(seeds_emit_kernel, dim3((unsigned)((int64_t)n_img * h.n_cif * K)), dim3(256), 0, s, a);
+    // small batches place the seeds with several workgroups per image (rank placement)
+#ifdef PP_NO_RANK  // A/B builds
+    a.parts = 1;
+#else
+    a.parts = n_img <= kRankImgs ? kRankParts : 1;
+#endif
+    hipLaunchKernelGGL(seeds_sort_kernel, dim3(n_img * a.parts), dim3(1024), 0, s, a);
     return check_launch("pp_seeds");
 }
 
@@ -1226,7 +1339,8 @@ static int seeds_entry(const Heads &h, const float *d_cifhr, int32_t n_img, int3
     if (hipMallocAsync(&scratch, seeds_scratch_size(n_img, seed_capacity), s) != hipSuccess)
         return fail(PP_EHIP, "pp_seeds: scratch allocation failed");
     const HrMap hr = dense_hr(d_cifhr, h.hr_hh, h.hr_ww);
-    int rc = launch_seeds(h, hr, n_img, K, cfg, d_seeds, seed_capacity, d_counts, scratch, s);
+    int rc = launch_seeds(h, hr, n_img, K, cfg, d_seeds, seed_capacity, d_counts, scratch, s,
+                          false);
     if (hipFreeAsync(scratch, s) != hipSuccess && rc == PP_OK)
         rc = fail(PP_EHIP, "pp_seeds: scratch release failed");
     return rc;

@@ -456,6 +456,31 @@ def test_seeds_device_order(dec, n_img, hw, distinct):
             assert np.array_equal(got[name], ref[name]), (i, name)
 
 
+# the decoder's own seeds at a batch whose fields get one workgroup each (64 images x 17
+# fields >= 1024): emitted by the CifHr kernel itself (cifhr_fused_kernel<true>), then
+# sorted; saturated and tied confidences, the full decode against the oracle
+@pytest.mark.parametrize('hw,distinct', [(12, False), (18, True), (20, False)])
+def test_fused_seeds_decode_ties(dec, hw, distinct):
+    import torch
+    from openpifpaf_amd import constants
+    from openpifpaf_amd._abi import make_config
+    from openpifpaf_amd.engine import DecodeEngine
+    cfg = make_config(seed_threshold=0.2, force_complete=False)
+    cif = _tie_fields(hw, distinct)
+    caf = np.zeros((19, 9, hw, hw), np.float32)
+    skel = constants.COCO_PERSON_SKELETON
+    ref = oracle.decode(cif, caf, skel, cfg)
+    n = 64
+    c = torch.from_numpy(np.ascontiguousarray(np.broadcast_to(cif, (n,) + cif.shape))).cuda()
+    f = torch.from_numpy(np.ascontiguousarray(np.broadcast_to(caf, (n,) + caf.shape))).cuda()
+    recs, offs, _ = DecodeEngine().decode(c, f, skel, cfg)
+    for i in (0, 1, 31, 63):
+        got = recs[offs[i]:offs[i + 1]]
+        assert len(got) == len(ref) > 0, (i, len(got), len(ref))
+        for name in ('data', 'joint_scales', 'decoding_pairs'):
+            assert got[name].tobytes() == ref[name].tobytes(), (i, name)
+
+
 def test_stage_calls_equal_full_decode(dec):
     """pp_decode_stages called stage by stage, or with several stages per call, gives the
     same records as pp_decode_batch (the stage contract of include/pifpaf_amd.h)."""

@@ -22,3 +22,12 @@ print(d['value'], d['ms_per_step'], d['stage_ms'])
 for k in ('uniform', 'cfg2', 'cfg5', 'roofline', 'roofline_uniform'):
     print(k, d.get(k))
 PY
+# KT=1: also a rocprofv3 kernel trace of the default (overlapped) bench (tools/timeline.py)
+if [ "${KT:-0}" = "1" ]; then
+  R="$GRAFT_REPO_ROOT"
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/kt_$TAG" -o run --output-format csv \
+    -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --no-uniform --no-multi --no-configs \
+    > "$R/gpurun_out/kt_${TAG}_bench.json" 2> "$R/gpurun_out/kt_${TAG}.err" || exit $?
+  echo kernel trace done
+fi
