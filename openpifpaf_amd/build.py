@@ -34,11 +34,10 @@ VARIANTS = {
     'stamps': ['-DPP_STAMPS'],
     'nofuse': ['-DPP_NO_FUSED'],         # CifHr without the LDS list / fused seed emission
     'noself': ['-DPP_NO_SELF_PLAN'],     # seed-loop helpers planned by wave 0 only
-    'norank': ['-DPP_NO_RANK'],          # one seeds-sort workgroup per image at any batch
-    'noahead': ['-DPP_NO_RAW_AHEAD'],    # force-complete set-B connections evaluated lazily
+    'ahead': ['-DPP_RAW_AHEAD'],         # force-complete set-B connections evaluated ahead
+    'selfext': ['-DPP_SELF_EXT'],        # helper self-planning in the external-helper kernel
     'noocc': ['-DPP_NO_SEED_OCC'],        # the seed loop's occupancy in the global grid
-    'base': ['-DPP_NO_FUSED', '-DPP_NO_SELF_PLAN', '-DPP_NO_RANK', '-DPP_NO_RAW_AHEAD',
-             '-DPP_NO_SEED_OCC'],
+    'base': ['-DPP_NO_FUSED', '-DPP_NO_SELF_PLAN', '-DPP_NO_SEED_OCC'],  # round 3's kernels
 }
 
 

@@ -1009,10 +1009,14 @@ __device__ __forceinline__ void eval_ahead(const GrowArgs &g, Frontier &F, int i
 // bucket-row segments (<= kRawSegs), every lane one column of every edge per pass.  An edge
 // whose box spans more bucket rows stays lazy.
 constexpr int kRawAhead = 4;
-#ifdef PP_NO_RAW_AHEAD  // A/B builds
-constexpr bool kCompleteAhead = false;
+// complete_kernel evaluates set B ahead (PP_RAW_AHEAD builds): off by default -- with it the
+// kernel needs 224 VGPRs (2 waves per SIMD instead of 4), and the lost occupancy costs more
+// than the batched round trips save: planted cfg3 323k vs 331k images/s, uniform 12.4k vs
+// 15.1-15.7k, cfg5 uniform 725 vs 800-807 (A/B on one box, round 4)
+#ifdef PP_RAW_AHEAD
+constexpr bool kCompleteAhead = true;
 #else
-constexpr bool kCompleteAhead = true;  // complete_kernel evaluates set B ahead
+constexpr bool kCompleteAhead = false;
 #endif
 constexpr int kRawSegs = 64 / kRawAhead;
 
@@ -1200,9 +1204,11 @@ __device__ __forceinline__ void eval_ahead_raw(const GrowArgs &g, Frontier &F, i
 // AHEAD (seed loop: set A, reverse_match): new entries' connections via eval_ahead from
 // the image's set-A column counts and LDS-staged sets; RAW_AHEAD (force-complete: set B,
 // no reverse matching) via eval_ahead_raw.
+// `abort` (a seed-loop helper's speculative grow): stop at the next pop once *abort is set
+// (wave 0 is done: the result would never be read)
 template <bool AHEAD, typename LDS, bool RAW_AHEAD = false>
 __device__ __forceinline__ void grow(const GrowArgs &g, LDS &L, int img, int set, bool reverse_match,
-                                     const ColStage &cs = ColStage{}) {
+                                     const ColStage &cs = ColStage{}, int *abort = nullptr) {
     const int lane = threadIdx.x & 63;
     const int K = g.K;
     float ax = 0.0f, ay = 0.0f, av = 0.0f, as = 0.0f;
@@ -1256,6 +1262,8 @@ __device__ __forceinline__ void grow(const GrowArgs &g, LDS &L, int img, int set
         ahead(added);
     }
     for (;;) {
+        if (abort && __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+            break;
         // frontier_get (cifcaf.py:265-285)
         Entry got;
         bool have = false;
@@ -1753,6 +1761,13 @@ constexpr bool kSelfPlan = false;
 #else
 constexpr bool kSelfPlan = true;
 #endif
+// the same in seed_loop_ext_kernel (PP_SELF_EXT builds): off -- cfg5 uniform (1370
+// annotations per image, external helpers) 725 vs 1080 images/s with it
+#ifdef PP_SELF_EXT
+constexpr bool kSelfPlanExt = true;
+#else
+constexpr bool kSelfPlanExt = false;
+#endif
 
 // External helpers.  A batch of fewer images than CUs leaves CUs without a seed loop, so
 // each image may get n_ext (<= kExtWgMax) more workgroups whose waves are all helpers.
@@ -2179,7 +2194,8 @@ void seed_loop_kernel(GrowArgs g) {
             if (my < 0) break;
             const int q = S.task_slot[wave];
             ann_from_seed(L, seeds[my], K, img);
-            grow<true>(g, L, img, 0, true, cstage);
+            grow<true>(g, L, img, 0, true, cstage, &S.done);
+            if (lds_acquire(&S.done)) break;  // nobody reads the cache any more
             copy_ann(&cache[q], &L.a);
             if (lane < kKP)
                 S.cache_j[q][lane] = make_float4(L.a.data[lane][0], L.a.data[lane][1],
@@ -2465,7 +2481,8 @@ void seed_loop_ext_kernel(GrowArgs g) {
                 my = (int)(v >> 32);
             }
             ann_from_seed(L, seeds[my], K, img);
-            grow<true>(g, L, img, 0, true, cstage);
+            grow<true>(g, L, img, 0, true, cstage, external ? nullptr : &S.done);
+            if (!external && lds_acquire(&S.done)) break;  // nobody reads the cache any more
             if (external) {
                 publish_ann(&xrec[q], &L.a);
                 if (lane == 0) {
@@ -2489,7 +2506,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
             // plan this wave's next grow itself (as in seed_loop_kernel), into this CU's slots
             plan_lock(S);
             uint64_t left = 1ull << wave;
-            if (kSelfPlan && !lds_acquire(&S.done)) {
+            if (kSelfPlanExt && !lds_acquire(&S.done)) {
                 const int dec = lds_acquire(&S.decided);
                 left = spec_plan(S, reinterpret_cast<const float4 *>(s_cols + kColLds), seeds,
                                  n_seeds, dec, dec, kSelfScan, occ, red, occ_msr(g), g.spec_far,

@@ -14,7 +14,29 @@
 // seeds only through the occupancy test in the seed loop (cifcaf.py:100-102).
 #include "pp_common.hpp"
 
+#ifdef PP_STAMPS
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <vector>
+#endif
+
 namespace pp {
+
+#ifdef PP_STAMPS
+// diagnostic build: seeds_sort_kernel per workgroup [start, offsets, keys loaded, sorted,
+// done, n] in s_memtime ticks, dumped to $PP_SORT_STAMPS_OUT by launch_seeds
+__device__ uint64_t *g_sort_stamps;
+#define SORT_STAMP(slot)                                                                     \
+    do {                                                                                     \
+        if (g_sort_stamps && threadIdx.x == 0)                                               \
+            g_sort_stamps[blockIdx.x * 6 + (slot)] = __builtin_amdgcn_s_memtime();           \
+    } while (0)
+#else
+#define SORT_STAMP(slot) \
+    do {                 \
+    } while (0)
+#endif
 
 constexpr int kSortLds = 4096;
 
@@ -73,7 +95,6 @@ struct SeedArgs {
     int *f_counts;      // (n_img, n_heads * K) seeds per segment (head, field)
     int *g_perm;        // (n_img, np_cap)
     int np_cap;
-    int parts;          // seeds_sort_kernel workgroups per image (> 1: rank placement)
     // first slot of segment (CIF head m, field f): K * cif_off[m] + f * H_m * W_m
     __device__ __forceinline__ int64_t seg_base(int m, int f) const {
         return (int64_t)K * h.cif_off[m] + (int64_t)f * h.cif_hw(m);
@@ -367,19 +388,6 @@ __device__ __forceinline__ int block_scan_1024(int v, int *s_w, int &total) {
     return before + incl - v;
 }
 
-// Small batches: a.parts workgroups per image.  One workgroup per image sorting ~2k keys
-// is the whole critical path of a one-image CifHr + seeds call (cfg2: 32 us), so up to
-// kRankMax seeds are PLACED instead: every thread holds at most two keys and counts the
-// keys that sort before each (the packed key is unique: its rank is the output position),
-// reading all keys from LDS in kSortLds chunks; keys tied with it in (v, field) are
-// compared by the reference's full tuple (x, y, s, then emission order) as finish() does.
-// More seeds take workgroup 0's sort below.
-constexpr int kRankParts = 4;
-constexpr int kRankMax = 2 * 1024 * kRankParts;  // 2 keys per thread, 4 workgroups of 1024
-// batches of at most this many images.  0: off -- measured much slower than the one-workgroup
-// network on cfg2 planted (2.2k keys: 245 vs 32 us): n^2 comparisons of 64-bit keys on 4 CUs
-constexpr int kRankImgs = 0;
-
 // 33 KB of LDS (keys + segment offsets; x / y / s stay in the emission buffer), so a
 // workgroup fits beside the seed loop's 104 KB on one CU (DecodePipeline overlaps them)
 __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
@@ -387,7 +395,8 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
     __shared__ int s_off[kMaxHeads * PP_MAX_KP + 1];
     __shared__ int s_scan[16];
     static_assert(kMaxHeads * PP_MAX_KP < 1024, "one thread per segment");
-    const int img = blockIdx.x / a.parts, part = blockIdx.x % a.parts;
+    const int img = blockIdx.x;
+    SORT_STAMP(0);
     const int nseg = a.h.n_cif * a.K;
     const int64_t cap = a.cap;
     const float *gv = a.g_keys + (int64_t)img * 4 * cap, *gx = gv + cap, *gy = gx + cap,
@@ -401,10 +410,14 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
         int total;
         const int pre = block_scan_1024(cnt, s_scan, total);
         if (q <= nseg) s_off[q] = pre;
-        if (q == 0 && part == 0) a.counts[img] = total;
+        if (q == 0) a.counts[img] = total;
     }
     __syncthreads();
     const int n = s_off[nseg];
+    SORT_STAMP(1);
+#ifdef PP_STAMPS
+    if (g_sort_stamps && threadIdx.x == 0) g_sort_stamps[blockIdx.x * 6 + 5] = (uint64_t)n;
+#endif
     int np = 1;
     while (np < n) np <<= 1;
     pp_seed *out = a.seeds + (int64_t)img * cap;
@@ -420,78 +433,6 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
         }
         return a.seg_base(lo / a.K, lo % a.K) + (i - s_off[lo]);
     };
-    if (a.parts > 1 && n <= kRankMax) {
-        // rank placement: this workgroup's keys i = part * 1024 + tid (+ 4096)
-        uint64_t mk[2];
-        int cnt[2] = {0, 0};
-        bool tie = false;
-#pragma unroll
-        for (int r = 0; r < 2; r++) {
-            const int i = (r * a.parts + part) * 1024 + (int)threadIdx.x;
-            mk[r] = 0ull;
-            if (i < n) {
-                const int64_t k = slot(i);
-                mk[r] = seed_key(gv[k], gf[k], i);
-            }
-        }
-        for (int c0 = 0; c0 < n; c0 += kSortLds) {  // block-uniform
-            const int m = min(kSortLds, n - c0);
-            __syncthreads();  // the previous chunk is read
-            for (int j = threadIdx.x; j < m; j += 1024) {
-                const int64_t k = slot(c0 + j);
-                s_key[j] = seed_key(gv[k], gf[k], c0 + j);
-            }
-            __syncthreads();
-            const uint64_t h0 = mk[0] >> 27, h1 = mk[1] >> 27;
-            int j = 0;
-            for (; j + 1 < m; j += 2) {  // two keys per LDS read
-                const uint64_t ka = s_key[j], kb = s_key[j + 1];
-                const uint64_t ha = ka >> 27, hb = kb >> 27;
-                cnt[0] += (int)(ha > h0) + (int)(hb > h0);
-                cnt[1] += (int)(ha > h1) + (int)(hb > h1);
-                tie |= (ha == h0 && ka != mk[0]) || (hb == h0 && kb != mk[0]) ||
-                       (ha == h1 && ka != mk[1]) || (hb == h1 && kb != mk[1]);
-            }
-            if (j < m) {
-                const uint64_t ka = s_key[j], ha = ka >> 27;
-                cnt[0] += (int)(ha > h0);
-                cnt[1] += (int)(ha > h1);
-                tie |= (ha == h0 && ka != mk[0]) || (ha == h1 && ka != mk[1]);
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < 2; r++) {
-            const int i = (r * a.parts + part) * 1024 + (int)threadIdx.x;
-            if (i >= n) continue;
-            const int64_t ki = slot(i);
-            if (tie) {  // equal (v, field): the full tuple order (cif_seeds.py:54)
-                const uint64_t hi = mk[r] >> 27;
-                const int fi = gf[ki];
-                // keys of field fi: its segments (head m, field fi)
-                for (int q = fi; q < nseg; q += a.K)
-                for (int j = s_off[q]; j < s_off[q + 1]; j++) {
-                    if (j == i) continue;
-                    const int64_t kj = a.seg_base(q / a.K, q % a.K) + (j - s_off[q]);
-                    if ((seed_key(gv[kj], gf[kj], j) >> 27) != hi) continue;
-                    bool before;
-                    if (gx[kj] != gx[ki]) before = gx[kj] > gx[ki];
-                    else if (gy[kj] != gy[ki]) before = gy[kj] > gy[ki];
-                    else if (gs[kj] != gs[ki]) before = gs[kj] > gs[ki];
-                    else before = j < i;
-                    cnt[r] += (int)before;
-                }
-            }
-            pp_seed rec;
-            rec.v = gv[ki];
-            rec.field = gf[ki];
-            rec.x = gx[ki];
-            rec.y = gy[ki];
-            rec.s = gs[ki];
-            out[cnt[r]] = rec;
-        }
-        return;
-    }
-    if (part != 0) return;
     // the sorted keys kb[0 .. n) (LDS, or global scratch for more than kSortLds keys):
     // runs of equal (v, field) re-sorted by (x, y, s) descending, then emission order (one
     // thread per run, insertion sort), then the records written in order
@@ -551,12 +492,16 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
         // past n are 0 and sort last): only the stages whose partner lies in another wave go
         // through LDS (np > 256; 10 of 78 at 4096); the others exchange in registers / across
         // lanes
+        SORT_STAMP(2);
         bitonic_desc(key, s_key, np < 4 ? 4 : np);
         __syncthreads();
 #pragma unroll
         for (int e = 0; e < 4; e++) s_key[4 * threadIdx.x + e] = key[e];
         __syncthreads();
+        SORT_STAMP(3);
         finish(s_key);
+        __syncthreads();
+        SORT_STAMP(4);
         return;
     }
     if (n <= 2 * kSortLds) {
@@ -817,15 +762,34 @@ template <bool INDEX_ONLY, bool STASH>
 __global__ __launch_bounds__(STASH && INDEX_ONLY ? 512 : 256) void caf_bucketed_kernel(CafBArgs a) {
     constexpr int NT = STASH && INDEX_ONLY ? 512 : 256;
     constexpr int NW = NT / 64;
-    __shared__ int s_cnt[2][kMaxBuckets + 1];
+    // The set-B build (PK) keeps its LDS small enough to run beside a seed-loop workgroup
+    // (whose LDS leaves ~38 KB of a CU): bucket counts / cursors as u16 pairs (a bucket holds
+    // at most kStashCells cells), and the stash sized by the launch to the field's cells.
+    constexpr bool PK = INDEX_ONLY && STASH;
+    __shared__ int s_cnt[2][PK ? (kMaxBuckets + 2) / 2 : kMaxBuckets + 1];
     __shared__ int s_wsum[2][NW];
-    __shared__ __attribute__((aligned(16))) char s_stash[STASH ? (INDEX_ONLY ? 2 * kStashCells * 2 : 2 * kStashA * (int)sizeof(StashCol)) : 16];
+    __shared__ __attribute__((aligned(16))) char s_stash[STASH && !INDEX_ONLY ? 2 * kStashA * (int)sizeof(StashCol) : 16];
+    extern __shared__ __attribute__((aligned(16))) char s_dyn[];  // PK: 2 * col_cap u16
     __shared__ int s_sn[2], s_ovf, s_nc;
     constexpr bool kList = STASH && !INDEX_ONLY;
     __shared__ int s_cand[kList ? kCandA : 1];
     __shared__ float s_cand_c[kList ? kCandA : 1];
     StashCol *stash_a = reinterpret_cast<StashCol *>(s_stash);       // [2][kStashA]
-    uint16_t *stash_b = reinterpret_cast<uint16_t *>(s_stash);       // [2][kStashCells]
+    uint16_t *stash_b = reinterpret_cast<uint16_t *>(s_dyn);         // [2][col_cap]
+    const int scell = (int)a.col_cap;                                 // stash_b's direction stride
+    // bucket b of direction d: add one (returns the old count / cursor), read
+    auto h_add = [&](int d, int b) -> int {
+        if constexpr (PK) {
+            const unsigned sh = (unsigned)(b & 1) * 16u;
+            return (int)((atomicAdd(reinterpret_cast<unsigned *>(&s_cnt[d][b >> 1]), 1u << sh) >> sh) & 0xFFFFu);
+        } else {
+            return atomicAdd(&s_cnt[d][b], 1);
+        }
+    };
+    auto h_get = [&](int d, int b) -> int {
+        if constexpr (PK) return (int)(((unsigned)s_cnt[d][b >> 1] >> ((b & 1) * 16)) & 0xFFFFu);
+        else return s_cnt[d][b];
+    };
     const int64_t fld = blockIdx.x;  // image * C + caf field
     const int img = (int)(fld / a.C), ci = (int)(fld % a.C);
     const int nb = a.nb;
@@ -846,7 +810,7 @@ __global__ __launch_bounds__(STASH && INDEX_ONLY ? 512 : 256) void caf_bucketed_
     const bool use2 = need_f && a.cif_floor < 1.0f && j2i < a.K;
     const int64_t t1 = (int64_t)img * a.K + (use1 ? j1i : 0);
     const int64_t t2 = (int64_t)img * a.K + (use2 ? j2i : 0);
-    for (int i = threadIdx.x; i <= nb; i += NT) {
+    for (int i = threadIdx.x; i < (PK ? (nb + 2) / 2 : nb + 1); i += NT) {
         s_cnt[0][i] = 0;
         s_cnt[1][i] = 0;
     }
@@ -922,12 +886,12 @@ __global__ __launch_bounds__(STASH && INDEX_ONLY ? 512 : 256) void caf_bucketed_
         const float *nine = B.nine[k];
         const int bkb = B.kb[k] ? caf_bucket(nine[5], nine[6], a.bw, a.bh, a.inv_e) : -1;
         const int bkf = B.kf[k] ? caf_bucket(nine[1], nine[2], a.bw, a.bh, a.inv_e) : -1;
-        if (bkb >= 0) atomicAdd(&s_cnt[0][bkb], 1);
-        if (bkf >= 0) atomicAdd(&s_cnt[1][bkf], 1);
+        if (bkb >= 0) h_add(0, bkb);
+        if (bkf >= 0) h_add(1, bkf);
         if (STASH && INDEX_ONLY) {
             if (cell < hw) {
                 stash_b[coff + cell] = bkb >= 0 ? (uint16_t)bkb : kNoBucket;
-                stash_b[kStashCells + coff + cell] = bkf >= 0 ? (uint16_t)bkf : kNoBucket;
+                stash_b[scell + coff + cell] = bkf >= 0 ? (uint16_t)bkf : kNoBucket;
             }
         } else if (STASH) {
             const float key = __int_as_float(coff + cell);
@@ -1065,12 +1029,13 @@ __global__ __launch_bounds__(STASH && INDEX_ONLY ? 512 : 256) void caf_bucketed_
     }
     }
     __syncthreads();
-    // exclusive prefix over the buckets (thread-contiguous ranges + block scan)
-    const int per = (nb + NT - 1) / NT;
+    // exclusive prefix over the buckets (thread-contiguous ranges + block scan); PK: even
+    // ranges, so that each thread owns the u16 pairs of its range
+    const int per = PK ? (((nb + NT - 1) / NT + 1) & ~1) : (nb + NT - 1) / NT;
     const int b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
     int sum[2] = {0, 0};
     for (int d = 0; d < 2; d++)
-        for (int i = b0; i < b1; i++) sum[d] += s_cnt[d][i];
+        for (int i = b0; i < b1; i++) sum[d] += h_get(d, i);
     int incl[2];
     for (int d = 0; d < 2; d++) {
         int v = sum[d];
@@ -1087,11 +1052,22 @@ __global__ __launch_bounds__(STASH && INDEX_ONLY ? 512 : 256) void caf_bucketed_
         int base = incl[d] - sum[d];
         for (int w = 0; w < (int)(threadIdx.x >> 6); w++) base += s_wsum[d][w];
         int *offs = d == 0 ? offs_b : offs_f;
-        for (int i = b0; i < b1; i++) {
-            const int c = s_cnt[d][i];
-            s_cnt[d][i] = base;  // becomes the bucket cursor
-            offs[i] = base;
-            base += c;
+        if constexpr (PK) {
+            for (int i = b0; i < b1; i += 2) {  // the pair (i, i + 1) becomes two cursors
+                const unsigned w = (unsigned)s_cnt[d][i >> 1];
+                const int c0 = (int)(w & 0xFFFFu), c1 = i + 1 < b1 ? (int)(w >> 16) : 0;
+                offs[i] = base;
+                if (i + 1 < b1) offs[i + 1] = base + c0;
+                s_cnt[d][i >> 1] = (int)((unsigned)base | ((unsigned)(base + c0) << 16));
+                base += c0 + c1;
+            }
+        } else {
+            for (int i = b0; i < b1; i++) {
+                const int c = s_cnt[d][i];
+                s_cnt[d][i] = base;  // becomes the bucket cursor
+                offs[i] = base;
+                base += c;
+            }
         }
         if (threadIdx.x == NT - 1) {
             int tot = 0;
@@ -1112,10 +1088,10 @@ __global__ __launch_bounds__(STASH && INDEX_ONLY ? 512 : 256) void caf_bucketed_
     if (STASH && INDEX_ONLY) {
         const int ncell = (int)cc;
         for (int cell = threadIdx.x; cell < ncell; cell += NT) {
-            const uint16_t bb = stash_b[cell], bf = stash_b[kStashCells + cell];
+            const uint16_t bb = stash_b[cell], bf = stash_b[scell + cell];
             // u16 cell indices (cells <= kSetBIdx16Max): half the bytes to write and to read
-            if (bb != kNoBucket) reinterpret_cast<uint16_t *>(bwd)[atomicAdd(&s_cnt[0][bb], 1)] = (uint16_t)cell;
-            if (bf != kNoBucket) reinterpret_cast<uint16_t *>(fwd)[atomicAdd(&s_cnt[1][bf], 1)] = (uint16_t)cell;
+            if (bb != kNoBucket) reinterpret_cast<uint16_t *>(bwd)[h_add(0, bb)] = (uint16_t)cell;
+            if (bf != kNoBucket) reinterpret_cast<uint16_t *>(fwd)[h_add(1, bf)] = (uint16_t)cell;
         }
         return;
     }
@@ -1231,13 +1207,29 @@ int launch_seeds(const Heads &h, const HrMap &hr, int n_img, int K, const pp_con
     a.g_perm = (int *)w;
     if (!emitted)
         hipLaunchKernelGGL(seeds_emit_kernel, dim3((unsigned)((int64_t)n_img * h.n_cif * K)), dim3(256), 0, s, a);
-    // small batches place the seeds with several workgroups per image (rank placement)
-#ifdef PP_NO_RANK  // A/B builds
-    a.parts = 1;
-#else
-    a.parts = n_img <= kRankImgs ? kRankParts : 1;
+#ifdef PP_STAMPS
+    uint64_t *st = nullptr;
+    hipMalloc((void **)&st, (size_t)n_img * 6 * sizeof(uint64_t));
+    hipMemsetAsync(st, 0, (size_t)n_img * 6 * sizeof(uint64_t), s);
+    hipMemcpyToSymbolAsync(HIP_SYMBOL(g_sort_stamps), &st, sizeof(st), 0, hipMemcpyHostToDevice, s);
 #endif
-    hipLaunchKernelGGL(seeds_sort_kernel, dim3(n_img * a.parts), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(seeds_sort_kernel, dim3(n_img), dim3(1024), 0, s, a);
+#ifdef PP_STAMPS
+    {
+        hipStreamSynchronize(s);
+        std::vector<uint64_t> hb((size_t)n_img * 6);
+        hipMemcpy(hb.data(), st, hb.size() * sizeof(uint64_t), hipMemcpyDeviceToHost);
+        const char *path = getenv("PP_SORT_STAMPS_OUT");
+        FILE *fo = fopen(path ? path : "pp_sort_stamps.bin", "ab");
+        if (fo) {
+            fwrite(hb.data(), sizeof(uint64_t), hb.size(), fo);
+            fclose(fo);
+        }
+        uint64_t *nul = nullptr;
+        hipMemcpyToSymbol(HIP_SYMBOL(g_sort_stamps), &nul, sizeof(nul));
+        hipFree(st);
+    }
+#endif
     return check_launch("pp_seeds");
 }
 
@@ -1314,7 +1306,8 @@ int launch_caf_bucketed(const Heads &h, const HrMap &hr, int n_img, int K, int C
     }
     const dim3 grid((unsigned)((int64_t)n_img * C));
     if (index_only && a.col_cap <= kStashCells)
-        hipLaunchKernelGGL((caf_bucketed_kernel<true, true>), grid, dim3(512), 0, s, a);
+        hipLaunchKernelGGL((caf_bucketed_kernel<true, true>), grid, dim3(512),
+                           (size_t)(2 * a.col_cap * sizeof(uint16_t)), s, a);
     else if (index_only)
         hipLaunchKernelGGL((caf_bucketed_kernel<true, false>), grid, dim3(256), 0, s, a);
     else
