@@ -472,6 +472,10 @@ int pp_pack_compact(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img
  * With bit 16, stage 8 may run in two calls on the same workspace and outputs: first with
  * PP_STAGE_SEED_LOOP_ONLY (32), then with PP_STAGE_AFTER_SEED_LOOP (64: force-complete and
  * NMS), so the second part can run on another stream beside the next batch's seed loop.
+ * The second part may itself run as two calls: PP_STAGE_AFTER_SEED_LOOP | PP_STAGE_COMPLETE_ONLY
+ * (128: force-complete), then PP_STAGE_AFTER_SEED_LOOP | PP_STAGE_NMS_ONLY (256).  NMS reads
+ * only the annotation records and NMS scratch, none of which stages 1-4 write, so the
+ * workspace's next stages 1-4 need wait only for the force-complete call.
  *
  * Workspace contract: bytes [pp_decode_workspace_zero_offset(), end) must be zero before
  * the first call (e.g. hipMemset once at allocation); every call leaves them zero again.
@@ -479,6 +483,8 @@ int pp_pack_compact(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img
 #define PP_STAGE_COMPLETE_SETS_EARLY 16u
 #define PP_STAGE_SEED_LOOP_ONLY 32u
 #define PP_STAGE_AFTER_SEED_LOOP 64u
+#define PP_STAGE_COMPLETE_ONLY 128u
+#define PP_STAGE_NMS_ONLY 256u
 int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int32_t K,
                      int32_t C, int32_t H, int32_t W, const int32_t *skeleton,
                      const pp_config *cfg, float *d_cifhr, pp_ann *d_anns,

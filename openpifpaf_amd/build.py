@@ -38,6 +38,7 @@ VARIANTS = {
     'selfext': ['-DPP_SELF_EXT'],        # helper self-planning in the external-helper kernel
     'noocc': ['-DPP_NO_SEED_OCC'],        # the seed loop's occupancy in the global grid
     'base': ['-DPP_NO_FUSED', '-DPP_NO_SELF_PLAN', '-DPP_NO_SEED_OCC'],  # round 3's kernels
+    'bitonic': ['-DPP_NO_SEED_RADIX'],   # seeds sorted by the bitonic network only
 }
 
 

@@ -3621,18 +3621,21 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
             rc = check_launch("pp_decode_batch(seed loop)");
             if (rc) return rc;
         }
-        if (run_rest && cfg->force_complete && !(stages & PP_STAGE_COMPLETE_SETS_EARLY)) {
+        // PP_STAGE_COMPLETE_ONLY / PP_STAGE_NMS_ONLY split the rest once more
+        const bool run_complete = run_rest && !(stages & PP_STAGE_NMS_ONLY);
+        const bool run_nms = run_rest && !(stages & PP_STAGE_COMPLETE_ONLY);
+        if (run_complete && cfg->force_complete && !(stages & PP_STAGE_COMPLETE_SETS_EARLY)) {
             // complete_annotations' CafScored(score_th=0.0001) only where phase 1 left work
             rc = launch_caf_bucketed(h, hr, n_img, K, C, skeleton, cfg, cfg->complete_caf_threshold,
                                      cols[1], offs[1], g.need_complete, true, s);
             if (rc) return rc;
         }
-        if (run_rest && cfg->force_complete) {
+        if (run_complete && cfg->force_complete) {
             hipLaunchKernelGGL(complete_kernel, dim3(n_img, kCompleteWays), dim3(64), 0, s, g);
             rc = check_launch("pp_decode_batch(force complete)");
             if (rc) return rc;
         }
-        if (run_rest) {
+        if (run_nms) {
             hipLaunchKernelGGL(nms_kernel, dim3(n_img), dim3(64 * kNmsWaves), 0, s, g);
             rc = check_launch("pp_decode_batch(nms)");
         }

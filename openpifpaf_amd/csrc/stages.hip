@@ -388,12 +388,118 @@ __device__ __forceinline__ int block_scan_1024(int v, int *s_w, int &total) {
     return before + incl - v;
 }
 
-// 33 KB of LDS (keys + segment offsets; x / y / s stay in the emission buffer), so a
-// workgroup fits beside the seed loop's 104 KB on one CU (DecodePipeline overlaps them)
+// LSD radix sort of up to kSortLds keys, descending on key >> 27 = (v bits, field) and
+// stable: equal (v, field) keep their order, emission order, which is what the low 27 bits
+// (the inverted emission index) give the full-key sort too.  Keys are held 4 per thread,
+// striped: key[e] of thread (wave w, lane l) is element 256 w + 64 e + l; padding keys are
+// 0 and stay last.  Digits are 7 bits of (key >> 27) - min over the keys, as many passes
+// as that range needs (4 for seeds above 0.5: 23 mantissa bits + 5 field bits).  A pass:
+// each wave ranks its 256 keys by digit with 7 ballots (peers = the lanes holding the same
+// digit) and a per-wave count per digit in LDS, one block scan over (digit, wave), a
+// scatter into s_key.  The bitonic network needs 78 compare-exchange stages for 4096 keys
+// (56k of its 77k cycles per planted image, PP_STAMPS); this needs 4 passes.  Leaves the
+// sorted keys in s_key[0, n).
+constexpr int kRadixBits = 7, kRadixDigits = 1 << kRadixBits;
+// per-wave digit counts, a row per wave: a wave's lanes read / write their digits' counts
+// in one row (2 u16 per bank word), and the row pitch of 65 words spreads the scan's
+// (digit, wave) column reads over the banks; [digit][wave] put 16 lanes on one bank
+constexpr int kRadixPitch = kRadixDigits + 2;
+constexpr int kRadixMin = 256;  // up to here the bitonic network stays inside one wave
+#ifdef PP_NO_SEED_RADIX
+constexpr bool kSeedRadix = false;
+#else
+constexpr bool kSeedRadix = true;
+#endif
+
+__device__ void radix_desc(uint64_t key[4], uint64_t *s_key, uint16_t *s_rh, int *s_scan) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    // range of key >> 27 over the real keys
+    uint64_t lo = ~0ull, hi = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++)
+        if (key[e]) {
+            lo = min(lo, key[e] >> 27);
+            hi = max(hi, key[e] >> 27);
+        }
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) {
+        lo = min(lo, shfl_xor64(lo, m));
+        hi = max(hi, shfl_xor64(hi, m));
+    }
+    uint64_t *s_mm = reinterpret_cast<uint64_t *>(s_rh);
+    if (lane == 0) {
+        s_mm[w] = lo;
+        s_mm[16 + w] = hi;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        lo = min(lo, s_mm[q]);
+        hi = max(hi, s_mm[16 + q]);
+    }
+    const uint64_t range = hi > lo ? hi - lo : 0;
+    const int passes = range ? (64 - __clzll(range) + kRadixBits - 1) / kRadixBits : 0;
+    const uint64_t below_mask = (1ull << lane) - 1;
+    // the scan's entries of thread t: (digit t / 8, waves 2 (t % 8) and 2 (t % 8) + 1)
+    uint16_t *own = s_rh + 2 * (t & 7) * kRadixPitch + (t >> 3);
+    uint16_t *row = s_rh + w * kRadixPitch;
+    for (int p = 0; p < passes; p++) {  // block-uniform
+        const int sh = p * kRadixBits;
+        __syncthreads();  // s_rh's previous readers are done
+        own[0] = 0;
+        own[kRadixPitch] = 0;
+        __syncthreads();
+        uint32_t dg[4], rk[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const uint64_t dk = key[e] ? (key[e] >> 27) - lo : 0ull;
+            const uint32_t d = (kRadixDigits - 1) - (uint32_t)((dk >> sh) & (kRadixDigits - 1));
+            uint64_t peers = ~0ull;
+#pragma unroll
+            for (int b = 0; b < kRadixBits; b++) {
+                const bool bit = (d >> b) & 1u;
+                const uint64_t bal = __ballot(bit);
+                peers &= bit ? bal : ~bal;
+            }
+            uint16_t *c = row + d;
+            const uint32_t old = *c;
+            rk[e] = old + (uint32_t)__popcll(peers & below_mask);
+            dg[e] = d;
+            if (lane == 63 - __clzll(peers)) *c = (uint16_t)(old + (uint32_t)__popcll(peers));
+        }
+        __syncthreads();
+        // exclusive offsets over (digit, wave): thread t owns entries 2t and 2t + 1
+        const int c0 = own[0], c1 = own[kRadixPitch];
+        int total;
+        const int base = block_scan_1024(c0 + c1, s_scan, total);
+        own[0] = (uint16_t)base;
+        own[kRadixPitch] = (uint16_t)(base + c0);
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < 4; e++) s_key[row[dg[e]] + rk[e]] = key[e];
+        __syncthreads();
+        if (p + 1 < passes) {
+#pragma unroll
+            for (int e = 0; e < 4; e++) key[e] = s_key[256 * w + 64 * e + lane];
+        }
+    }
+    if (passes == 0) {  // one (v, field) value: emission order is the order
+#pragma unroll
+        for (int e = 0; e < 4; e++) s_key[256 * w + 64 * e + lane] = key[e];
+        __syncthreads();
+    }
+}
+
+// 38 KB of LDS (keys, radix counts, segment offsets; x / y / s stay in the emission
+// buffer), so a workgroup fits beside the seed loop's 121 KB on one CU (DecodePipeline
+// overlaps them)
 __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
     __shared__ uint64_t s_key[kSortLds];
+    __shared__ __attribute__((aligned(16))) uint16_t s_rh[16 * kRadixPitch];
     __shared__ int s_off[kMaxHeads * PP_MAX_KP + 1];
     __shared__ int s_scan[16];
+    static_assert(kRadixDigits * 16 == 2 * 1024, "radix_desc: two counts per thread");
+    static_assert(16 * kRadixPitch * sizeof(uint16_t) >= 32 * sizeof(uint64_t), "min / max scratch");
     static_assert(kMaxHeads * PP_MAX_KP < 1024, "one thread per segment");
     const int img = blockIdx.x;
     SORT_STAMP(0);
@@ -475,6 +581,27 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
             out[i] = r;
         }
     };
+    if (n > kRadixMin && n <= kSortLds && kSeedRadix) {
+        // thread (w, l) gathers seeds 256 w + 64 e + l (one round trip), then radix_desc
+        uint64_t key[4];
+        const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int i = 256 * w + 64 * e + l;
+            key[e] = 0ull;
+            if (i < n) {
+                const int64_t k = slot(i);
+                key[e] = seed_key(gv[k], gf[k], i);
+            }
+        }
+        SORT_STAMP(2);
+        radix_desc(key, s_key, s_rh, s_scan);
+        SORT_STAMP(3);
+        finish(s_key);
+        __syncthreads();
+        SORT_STAMP(4);
+        return;
+    }
     if (n <= kSortLds) {
         // thread t gathers seeds 4t .. 4t + 3 (all loads independent: one round trip), the
         // keys straight into registers

@@ -26,6 +26,8 @@ STAGE_ALL = 15
 STAGE_COMPLETE_EARLY = 16
 # PP_STAGE_SEED_LOOP_ONLY / PP_STAGE_AFTER_SEED_LOOP: stage 8 in two calls (same slot)
 STAGE_SEED_LOOP_ONLY, STAGE_AFTER_SEED_LOOP = 32, 64
+# PP_STAGE_COMPLETE_ONLY / PP_STAGE_NMS_ONLY: the after-seed-loop part in two calls
+STAGE_COMPLETE_ONLY, STAGE_NMS_ONLY = 128, 256
 
 
 def default_ann_capacity(h, w):
@@ -483,12 +485,17 @@ class PendingRecords:
 # PP_PIPE_BFIRST=1 / 0 / lazy forces the force-complete set order of DecodePipeline (auto
 # below); lazy: gated after the seed loop, on the tail stream
 _B_FIRST = {'1': True, '0': False, 'lazy': 'lazy'}.get(os.environ.get('PP_PIPE_BFIRST', ''))
-# auto: sets first once a batch averaged this many annotations per image.  0: always (round
-# 3, after the seeds kernels shrank: planted 0.838 vs 0.868 ms and 0.845 vs 0.898 ms per
-# step on two boxes; uniform was already sets-first)
-_B_FIRST_DENSITY = 0.0
+# auto: lazy sets (only the (field, direction) pairs force-complete needs, on the tail
+# stream) until a batch averaged this many annotations per image, then sets first.  Round 4,
+# with the tail split: planted cfg3 0.687-0.691 (lazy) vs 0.801-0.811 ms (first) per step,
+# uniform 14.7k vs 15.1-15.2k images/s, cfg5 planted equal, cfg5 uniform 1180 vs 1200
+_B_FIRST_DENSITY = 32.0
 # workspaces in flight (PP_PIPE_DEPTH): batch i + depth's front half waits for batch i's tail
 _PIPE_DEPTH = 2
+# the tail as two calls (force-complete, then NMS): a workspace's next front half waits only
+# for the force-complete, its next seed loop for the NMS (PP_SPLIT_TAIL=0: one call, the
+# front half waits for both)
+_SPLIT_TAIL = os.environ.get('PP_SPLIT_TAIL', '1') != '0'
 
 
 class DecodePipeline:
@@ -503,15 +510,18 @@ class DecodePipeline:
     seed loop, and batch i + 1's seed loop beside batch i's tail.  Two engines (two
     workspaces) alternate; a workspace's front half waits until the tail that last used it
     is done, and its output slots are released by their record packs as in DecodeEngine.
+    The tail is two calls (STAGE_COMPLETE_ONLY, then STAGE_NMS_ONLY): the workspace's next
+    front half waits only for the force-complete (the last reader of the stage 1-4 buffers),
+    its next seed loop for the NMS.
     (The front half stays on the current stream and the pack on the tail stream so that
     the streams in use -- current, back, tail, the library's CafScored side stream -- each
     get a hardware queue of their own: HIP shares 4 per process between streams.)
 
-    The force-complete sets go first, on the side stream before the CifHr map (they read
-    only the CAF fields), then set A after them, beside the CifHr map and the seeds on the
-    current stream (PP_PIPE_BFIRST=0 puts them after set A, lazy gates them after the seed
-    loop on the tail stream).  Measured in round 3: planted 0.838 vs 0.868 ms (after set
-    A) vs 0.837 ms (lazy), uniform 18.2-18.9 vs 19.0 vs 19.2 ms per step.  Either order
+    The force-complete sets are lazy for sparse batches (built after the seed loop on the
+    tail stream, only for the (field, direction) pairs an annotation left unset), and go
+    first for dense ones, on the side stream before the CifHr map (they read only the CAF
+    fields), then set A after them, beside the CifHr map and the seeds on the current
+    stream (PP_PIPE_BFIRST=1 / 0 / lazy forces first / after set A / lazy).  Every order
     gives the same records.
 
     submit() returns (buffers, PendingRecords of the batch: DecodeEngine.fetch_async).
@@ -530,6 +540,7 @@ class DecodePipeline:
         self.back = torch.cuda.Stream(device=self.device)
         self.tail = torch.cuda.Stream(device=self.device)
         self._back_done = [None] * self.depth
+        self._sets_done = [None] * self.depth  # end of force-complete (last reader of 1-4)
         self._i = 0
         self.density = 0.0  # annotations per image of the last batch whose records were read
 
@@ -549,12 +560,13 @@ class DecodePipeline:
                 return eng.launch(cif, caf, skeleton, cfg, cap=cap, stages=stages)
             return eng.launch_multi(heads, skeleton, cfg, cap=cap, stages=stages)
 
-        if self._back_done[par] is not None:  # the workspace's previous back half
-            front.wait_event(self._back_done[par])
+        if self._sets_done[par] is not None:  # the workspace's previous force-complete
+            front.wait_event(self._sets_done[par])
         with torch.cuda.stream(front):
             if events:
                 events[0].record()
-            b_first = _B_FIRST if _B_FIRST is not None else self.density >= _B_FIRST_DENSITY
+            b_first = _B_FIRST if _B_FIRST is not None else (
+                True if self.density >= _B_FIRST_DENSITY else 'lazy')
             early = 0 if b_first == 'lazy' else STAGE_COMPLETE_EARLY
             if b_first == 'lazy':
                 launch(STAGE_CIFHR)
@@ -572,6 +584,8 @@ class DecodePipeline:
             front_done = torch.cuda.Event()
             front_done.record()
         self.back.wait_event(front_done)
+        if self._back_done[par] is not None:  # the workspace's previous NMS (records)
+            self.back.wait_event(self._back_done[par])
         with torch.cuda.stream(self.back):
             if events:
                 events[3].record()
@@ -580,7 +594,14 @@ class DecodePipeline:
             loop_done.record()
         self.tail.wait_event(loop_done)
         with torch.cuda.stream(self.tail):
-            b = launch(STAGE_GROW | early | STAGE_AFTER_SEED_LOOP)
+            if _SPLIT_TAIL:
+                launch(STAGE_GROW | early | STAGE_AFTER_SEED_LOOP | STAGE_COMPLETE_ONLY)
+                sets_done = torch.cuda.Event()
+                sets_done.record()
+                b = launch(STAGE_GROW | early | STAGE_AFTER_SEED_LOOP | STAGE_NMS_ONLY)
+            else:
+                b = launch(STAGE_GROW | early | STAGE_AFTER_SEED_LOOP)
+                sets_done = None
             if events:
                 events[4].record()
             back_done = torch.cuda.Event()
@@ -589,6 +610,7 @@ class DecodePipeline:
                                                stream=self.tail)
         pending.on_counts = self._note_counts
         self._back_done[par] = back_done
+        self._sets_done[par] = sets_done or back_done
         return b, pending
 
     def _note_counts(self, counts):

@@ -422,11 +422,13 @@ def _tie_fields(hw, distinct):
 
 
 # the DEVICE order of the seeds (the seed loop's order; the API's get() re-sorts on the
-# host), one image and a batch of 17: seeds_sort_kernel with 4 keys per thread up to 4096
-# seeds (ties re-sorted in LDS), 8 up to 8192 (ties through global scratch), the global
-# network beyond
+# host), one image and a batch of 17: seeds_sort_kernel's bitonic network up to 256 seeds
+# (3: 153), the radix sort up to 4096 (4: 272, 10: 1700, 12: all tied, 15: 3825; ties
+# re-sorted in LDS), 8 keys per thread up to 8192 (ties through global scratch), the
+# global network beyond
 @pytest.mark.parametrize('n_img', [1, 17])
-@pytest.mark.parametrize('hw,distinct', [(12, False), (18, True), (20, False), (24, False)])
+@pytest.mark.parametrize('hw,distinct', [(3, True), (4, True), (10, True), (12, False),
+                                         (15, True), (18, True), (20, False), (24, False)])
 def test_seeds_device_order(dec, n_img, hw, distinct):
     import torch
     from openpifpaf_amd import _device

@@ -8,12 +8,16 @@ from openpifpaf_amd._abi import EVAL_CONFIG, PACK_ALL, make_config
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('b_first', [False, True, 'lazy'])
-def test_pipeline_matches_engine_decode(b_first, monkeypatch):
+@pytest.mark.parametrize('split', [True, False])
+@pytest.mark.parametrize('b_first', [None, False, True, 'lazy'])
+def test_pipeline_matches_engine_decode(b_first, split, monkeypatch):
+    """Every placement of the force-complete sets (None: the density rule, which switches
+    between lazy and first across these batches), the tail in one call or two."""
     import torch
     from openpifpaf_amd import engine
     from openpifpaf_amd.engine import DecodeEngine, DecodePipeline
-    monkeypatch.setattr(engine, '_B_FIRST', b_first)  # every placement of the force-complete sets
+    monkeypatch.setattr(engine, '_B_FIRST', b_first)
+    monkeypatch.setattr(engine, '_SPLIT_TAIL', split)
     skel = constants.COCO_PERSON_SKELETON
     cfg = make_config(**EVAL_CONFIG)
     compact = (17, len(skel), PACK_ALL)
