@@ -17,11 +17,12 @@
 // from that XCD's L2.  Template MODE selects the functional.pyx primitive.
 #include "pp_common.hpp"
 
+#include <stdlib.h>
+
 #include <algorithm>
 
 #ifdef PP_STAMPS
 #include <stdio.h>
-#include <stdlib.h>
 
 #include <vector>
 #endif
@@ -662,6 +663,14 @@ __global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
 // the clamp maps NaN to max_value), so it is skipped.
 constexpr int kChunkTiles = 1;  // tiles per workgroup: 1.209 ms vs 1.409 ms at 32 (cfg3)
 constexpr int kHrPad = 68;    // stripe row pitch (floats)
+// units per touched tile of a split field (small batches): 8 = one block row (8 blocks)
+// per unit, 4 = a 16-row stripe
+#ifdef PP_SPLIT_PARTS4
+constexpr int kSplitParts = 4;
+#else
+constexpr int kSplitParts = 8;
+#endif
+static_assert(kSplitParts == 4 || kSplitParts == 8, "unit masks are written as u16 / u8 parts");
 
 struct HrTileArgs {
     float *field;           // dense (n_fields, h, pitch)
@@ -888,12 +897,22 @@ __device__ __forceinline__ float nan_max(float a, float b) {  // np.maximum
 // diagnostic build: per workgroup [start, phase 1 done, wave 0..3 done, hw_id, xcc_id, splats]
 // in s_memrealtime ticks (100 MHz), dumped to $PP_HR_STAMPS_OUT by cifhr_sparse_launch
 __device__ uint64_t *g_hr_stamps;
+// per workgroup: [start, phase 1 done, end of waves 0-3, hw id, xcc id, list length,
+// wave 0's shader cycles staging candidates, folding, its units]
+constexpr int kHrSt = 12;
+#define HR_ADD(slot, v)                                                                     \
+    do {                                                                                    \
+        if (g_hr_stamps && wave == 0 && lane == 0) g_hr_stamps[blockIdx.x * kHrSt + (slot)] += (v); \
+    } while (0)
 #define HR_STAMP(slot)                                                                      \
     do {                                                                                    \
         if (g_hr_stamps && lane == 0)                                                       \
-            g_hr_stamps[blockIdx.x * 9 + (slot)] = __builtin_amdgcn_s_memrealtime();        \
+            g_hr_stamps[blockIdx.x * kHrSt + (slot)] = __builtin_amdgcn_s_memrealtime();        \
     } while (0)
 #else
+#define HR_ADD(slot, v) \
+    do {                \
+    } while (0)
 #define HR_STAMP(slot) \
     do {               \
     } while (0)
@@ -1095,9 +1114,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
     if (wave == 0) {
         HR_STAMP(1);
         if (g_hr_stamps && lane == 0) {
-            g_hr_stamps[blockIdx.x * 9 + 6] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
-            g_hr_stamps[blockIdx.x * 9 + 7] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
-            g_hr_stamps[blockIdx.x * 9 + 8] = total;
+            g_hr_stamps[blockIdx.x * kHrSt + 6] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+            g_hr_stamps[blockIdx.x * kHrSt + 7] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
+            g_hr_stamps[blockIdx.x * kHrSt + 8] = total;
         }
     }
 #endif
@@ -1110,7 +1129,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
     // stripe of one: the four stripes of a busy tile then fold on four waves.  (Stripes for
     // every batch measured slower: each stripe re-scans the tile's candidates; uniform cfg3
     // CifHr 7.6 -> 9.1 ms per overlapped step.)
-    const int kParts = (!MULTI && a.split > 1) ? 4 : 1;
+    const int kParts = (!MULTI && a.split > 1) ? kSplitParts : 1;
     FoldCand *cand = s_cand[wave];
     const int lx = lane & 7, ly = lane >> 3;
     const int nwords = (a.tiles + 31) >> 5;
@@ -1141,7 +1160,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
         const int tx0 = (t % a.tiles_x) * kTile, ty0 = (t / a.tiles_x) * kTile;
         const int kRows = kTile / kParts;
         const int wy0 = ty0 + q * kRows;  // the unit's rows [wy0, wy0 + kRows)
-        const uint64_t unit_blocks = kParts == 1 ? ~0ull : (0xFFFFull << (16 * q));
+        const int kUnitBlocks = 64 / kParts;
+        const uint64_t unit_blocks =
+            kParts == 1 ? ~0ull : (((1ull << kUnitBlocks) - 1) << (kUnitBlocks * q));
         float *mp = a.map + (fld * a.tiles + t) * (int64_t)(kTile * kTile);
         float *ap = MULTI ? a.aux + (fld * a.tiles + t) * (int64_t)(kTile * kTile) : nullptr;
         uint64_t done = 0;  // blocks written by earlier passes
@@ -1151,7 +1172,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
         const FoldCand *src = rc >= 0 ? a.bins + slot * a.bins_cap + s_rowoff[row] : glist;
         const int src_n = rc >= 0 ? rc : total;
         int cursor = 0;
+        HR_ADD(11, 1);
         while (true) {
+#ifdef PP_STAMPS
+            const uint64_t t_a = __builtin_amdgcn_s_memtime();
+#endif
             // ---- this tile's candidates, in list order ----
             int n = 0;
             while (cursor < src_n) {
@@ -1190,6 +1215,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
             }
             const uint64_t slow = __ballot(slow_l);
             const uint64_t live = wave_or64(cl, &s_live[wave]);
+#ifdef PP_STAMPS
+            const uint64_t t_b = __builtin_amdgcn_s_memtime();
+            HR_ADD(9, t_b - t_a);
+#endif
             // ---- fold: block by block, lane = pixel, candidates ascending ----
             for (uint64_t rest = live; rest; rest &= rest - 1) {
                 const int blk = __builtin_ctzll(rest);
@@ -1235,6 +1264,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
                     if (lane == 0) s_bg[wave][blk] = (int8_t)gcur;
                 }
             }
+#ifdef PP_STAMPS
+            HR_ADD(10, __builtin_amdgcn_s_memtime() - t_b);
+#endif
             done |= live;
             if (last) {
                 if (MULTI) {  // blocks of earlier passes the last pass did not touch
@@ -1250,8 +1282,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
         if (lane == 0) {
             if (kParts == 1)
                 a.masks[fld * a.tiles + t] = done;
-            else  // the unit's 16 bits of the tile's mask (blocks 16 q .. 16 q + 15)
+            else if (kSplitParts == 4)  // the unit's 16 bits of the tile's mask
                 reinterpret_cast<uint16_t *>(&a.masks[fld * a.tiles + t])[q] = (uint16_t)(done >> (16 * q));
+            else  // the unit's 8 bits (one block row)
+                reinterpret_cast<uint8_t *>(&a.masks[fld * a.tiles + t])[q] = (uint8_t)(done >> (8 * q));
         }
     }
     HR_STAMP(2 + wave);
@@ -1757,7 +1791,11 @@ template int cifhr_heads_launch<false>(const Heads &, int32_t, int32_t, const pp
 // field's tiles over several workgroups (each builds its own copy of the field's list: a
 // re-read of its confidences, no extra round trip, no shared writes)
 static int sparse_split(int64_t nf) {
-    return (int)std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, kSplitSlots / std::max<int64_t>(1, nf)));
+    static const int64_t slots = [] {  // PP_SPLIT_SLOTS: diagnostics (tools/cfg2_split.py)
+        const char *e = getenv("PP_SPLIT_SLOTS");
+        return e && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)kSplitSlots;
+    }();
+    return (int)std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, slots / std::max<int64_t>(1, nf)));
 }
 
 size_t cifhr_sparse_workspace_size(const Heads &h, int n_img, int K) {
@@ -1851,7 +1889,8 @@ int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_confi
     }
 #ifdef PP_STAMPS
     uint64_t *st = nullptr;
-    hipMalloc((void **)&st, (size_t)nblocks * 9 * sizeof(uint64_t));
+    hipMalloc((void **)&st, (size_t)nblocks * kHrSt * sizeof(uint64_t));
+    hipMemsetAsync(st, 0, (size_t)nblocks * kHrSt * sizeof(uint64_t), s);
     hipMemcpyToSymbolAsync(HIP_SYMBOL(g_hr_stamps), &st, sizeof(st), 0, hipMemcpyHostToDevice, s);
 #endif
     if (h.n_groups > 1)
@@ -1861,7 +1900,7 @@ int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_confi
 #ifdef PP_STAMPS
     {
         hipStreamSynchronize(s);
-        std::vector<uint64_t> hbuf((size_t)nblocks * 9);
+        std::vector<uint64_t> hbuf((size_t)nblocks * kHrSt);
         hipMemcpy(hbuf.data(), st, hbuf.size() * sizeof(uint64_t), hipMemcpyDeviceToHost);
         const char *path = getenv("PP_HR_STAMPS_OUT");
         FILE *fo = fopen(path ? path : "pp_hr_stamps.bin", "ab");

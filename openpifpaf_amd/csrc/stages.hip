@@ -411,8 +411,32 @@ constexpr bool kSeedRadix = false;
 constexpr bool kSeedRadix = true;
 #endif
 
-__device__ void radix_desc(uint64_t key[4], uint64_t *s_key, uint16_t *s_rh, int *s_scan) {
+// inclusive prefix sum over the wave on DPP (row shifts, then row_bcast15 / row_bcast31
+// carry the row totals), no LDS round trip
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return v;
+}
+
+// radix_desc's LDS: s_rh (16 rows of kRadixPitch u16), s_w (2 x 16 wave totals, one half
+// per pass parity so a pass's scan needs no barrier after reading them), s_mm (32 u64)
+__device__ void radix_desc(uint64_t key[4], int n, uint64_t *s_key, uint16_t *s_rh, int *s_w,
+                           uint64_t *s_mm) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    // waves past the last key hold padding only, in every pass (padding stays at positions
+    // >= n): they count nothing (their rows are zero when scanned, which only moves the
+    // offsets of their own padding) and neither scatter nor reload; the others reload
+    // positions >= n as 0
+    const bool keys_here = 256 * w < n;
+    uint16_t *row = s_rh + w * kRadixPitch;  // wave w's counts; only wave w writes them
+    // zero this wave's row (65 words), before the range reduction's barrier
+    reinterpret_cast<uint32_t *>(row)[lane] = 0u;
+    if (lane == 0) reinterpret_cast<uint32_t *>(row)[64] = 0u;
     // range of key >> 27 over the real keys
     uint64_t lo = ~0ull, hi = 0;
 #pragma unroll
@@ -426,7 +450,6 @@ __device__ void radix_desc(uint64_t key[4], uint64_t *s_key, uint16_t *s_rh, int
         lo = min(lo, shfl_xor64(lo, m));
         hi = max(hi, shfl_xor64(hi, m));
     }
-    uint64_t *s_mm = reinterpret_cast<uint64_t *>(s_rh);
     if (lane == 0) {
         s_mm[w] = lo;
         s_mm[16 + w] = hi;
@@ -442,16 +465,12 @@ __device__ void radix_desc(uint64_t key[4], uint64_t *s_key, uint16_t *s_rh, int
     const uint64_t below_mask = (1ull << lane) - 1;
     // the scan's entries of thread t: (digit t / 8, waves 2 (t % 8) and 2 (t % 8) + 1)
     uint16_t *own = s_rh + 2 * (t & 7) * kRadixPitch + (t >> 3);
-    uint16_t *row = s_rh + w * kRadixPitch;
     for (int p = 0; p < passes; p++) {  // block-uniform
         const int sh = p * kRadixBits;
-        __syncthreads();  // s_rh's previous readers are done
-        own[0] = 0;
-        own[kRadixPitch] = 0;
-        __syncthreads();
+        // ---- rank: wave w's 256 keys by digit, counts in row w (zero: see below) ----
         uint32_t dg[4], rk[4];
 #pragma unroll
-        for (int e = 0; e < 4; e++) {
+        for (int e = 0; e < 4 && keys_here; e++) {
             const uint64_t dk = key[e] ? (key[e] >> 27) - lo : 0ull;
             const uint32_t d = (kRadixDigits - 1) - (uint32_t)((dk >> sh) & (kRadixDigits - 1));
             uint64_t peers = ~0ull;
@@ -467,20 +486,42 @@ __device__ void radix_desc(uint64_t key[4], uint64_t *s_key, uint16_t *s_rh, int
             dg[e] = d;
             if (lane == 63 - __clzll(peers)) *c = (uint16_t)(old + (uint32_t)__popcll(peers));
         }
-        __syncthreads();
-        // exclusive offsets over (digit, wave): thread t owns entries 2t and 2t + 1
+        __syncthreads();  // every row counted
+        // ---- exclusive offsets over (digit, wave) ----
         const int c0 = own[0], c1 = own[kRadixPitch];
-        int total;
-        const int base = block_scan_1024(c0 + c1, s_scan, total);
+        const int v = c0 + c1;
+        const int incl = wave_incl_scan(v);
+        int *sw = s_w + 16 * (p & 1);
+        if (lane == 63) sw[w] = incl;
+        __syncthreads();
+        int before = 0;
+#pragma unroll
+        for (int q = 0; q < 16; q++) before += q < w ? sw[q] : 0;
+        const int base = before + incl - v;
         own[0] = (uint16_t)base;
         own[kRadixPitch] = (uint16_t)(base + c0);
-        __syncthreads();
+        __syncthreads();  // offsets written
+        // ---- scatter; then wave w zeroes its row for the next pass (its own reads of the
+        // row are done: LDS operations of one wave complete in order) ----
+        if (keys_here) {
+            uint32_t pos[4];
 #pragma unroll
-        for (int e = 0; e < 4; e++) s_key[row[dg[e]] + rk[e]] = key[e];
-        __syncthreads();
-        if (p + 1 < passes) {
+            for (int e = 0; e < 4; e++) pos[e] = row[dg[e]] + rk[e];
 #pragma unroll
-            for (int e = 0; e < 4; e++) key[e] = s_key[256 * w + 64 * e + lane];
+            for (int e = 0; e < 4; e++)
+                if (pos[e] < (uint32_t)n) s_key[pos[e]] = key[e];  // padding lands at >= n
+        }
+        // every wave: the scan wrote offsets into every row
+        reinterpret_cast<uint32_t *>(row)[lane] = 0u;
+        if (lane == 0) reinterpret_cast<uint32_t *>(row)[64] = 0u;
+        __syncthreads();  // s_key complete
+        if (p + 1 < passes && keys_here) {
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int i = 256 * w + 64 * e + lane;
+                key[e] = i < n ? s_key[i] : 0ull;
+            }
+            // the next pass's scatter comes after its first barrier: these reads are done
         }
     }
     if (passes == 0) {  // one (v, field) value: emission order is the order
@@ -496,10 +537,11 @@ __device__ void radix_desc(uint64_t key[4], uint64_t *s_key, uint16_t *s_rh, int
 __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
     __shared__ uint64_t s_key[kSortLds];
     __shared__ __attribute__((aligned(16))) uint16_t s_rh[16 * kRadixPitch];
+    __shared__ int s_rw[32];
+    __shared__ uint64_t s_mm[32];
     __shared__ int s_off[kMaxHeads * PP_MAX_KP + 1];
     __shared__ int s_scan[16];
     static_assert(kRadixDigits * 16 == 2 * 1024, "radix_desc: two counts per thread");
-    static_assert(16 * kRadixPitch * sizeof(uint16_t) >= 32 * sizeof(uint64_t), "min / max scratch");
     static_assert(kMaxHeads * PP_MAX_KP < 1024, "one thread per segment");
     const int img = blockIdx.x;
     SORT_STAMP(0);
@@ -595,7 +637,7 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
             }
         }
         SORT_STAMP(2);
-        radix_desc(key, s_key, s_rh, s_scan);
+        radix_desc(key, n, s_key, s_rh, s_rw, s_mm);
         SORT_STAMP(3);
         finish(s_key);
         __syncthreads();

@@ -31,3 +31,12 @@ if [ "${KT:-0}" = "1" ]; then
     > "$R/gpurun_out/kt_${TAG}_bench.json" 2> "$R/gpurun_out/kt_${TAG}.err" || exit $?
   echo kernel trace done
 fi
+# KTU=1: the same for the uniform generator (cfg3 uniform, 6 steps)
+if [ "${KTU:-0}" = "1" ]; then
+  R="$GRAFT_REPO_ROOT"
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/ktu_$TAG" -o run --output-format csv \
+    -- python3 "$R/bench.py" --generator uniform --steps 6 --warmup 2 --no-cpu-baseline --no-uniform --no-multi --no-configs \
+    > "$R/gpurun_out/ktu_${TAG}_bench.json" 2> "$R/gpurun_out/ktu_${TAG}.err" || exit $?
+  echo uniform kernel trace done
+fi

@@ -24,7 +24,7 @@ for kind, n in cases:
     for _ in range(3):
         cifhr_sparse_device(c, 8, 0.1, 16)
     torch.cuda.synchronize()
-    st = np.fromfile(out, dtype=np.uint64).reshape(3, -1, 9)[-1].astype(np.int64)
+    st = np.fromfile(out, dtype=np.uint64).reshape(3, -1, 12)[-1].astype(np.int64)
     t0 = st[:, 0].min()
     start, p1, ends = st[:, 0] - t0, st[:, 1] - t0, st[:, 2:6] - t0
     end = ends.max(axis=1)
@@ -46,6 +46,11 @@ for kind, n in cases:
     xcc = st[:, 7] & 0xF
     print('  distinct (xcc, se, cu):', len(set(zip(xcc.tolist(), se.tolist(), cu.tolist()))))
     print('  splats per field mean {:.1f} max {}'.format(st[:, 8].mean(), st[:, 8].max()))
+    u = np.maximum(st[:, 11], 1)
+    print('  wave 0: units mean {:.2f} max {}; per unit shader cycles: staging {:.0f}, fold {:.0f}'
+          .format(st[:, 11].mean(), st[:, 11].max(), (st[:, 9] / u).mean(), (st[:, 10] / u).mean()))
+    print('  wave 0 cycles per workgroup: staging {:.0f} fold {:.0f} (p90 {:.0f} / {:.0f})'.format(
+        st[:, 9].mean(), st[:, 10].mean(), np.percentile(st[:, 9], 90), np.percentile(st[:, 10], 90)))
     order = np.argsort(start)
     print('  start of wg 0/1000/2000/3000/last: ',
           [round(start[order[i]] / 100, 1) for i in (0, 1000, 2000, 3000, len(st) - 1)
