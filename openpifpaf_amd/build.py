@@ -39,7 +39,7 @@ VARIANTS = {
     'noocc': ['-DPP_NO_SEED_OCC'],        # the seed loop's occupancy in the global grid
     'base': ['-DPP_NO_FUSED', '-DPP_NO_SELF_PLAN', '-DPP_NO_SEED_OCC'],  # round 3's kernels
     'bitonic': ['-DPP_NO_SEED_RADIX'],   # seeds sorted by the bitonic network only
-    'parts4': ['-DPP_SPLIT_PARTS4'],     # split-field CifHr units of 16 rows (8 rows default)
+    'parts8': ['-DPP_SPLIT_PARTS8'],     # split-field CifHr units of 8 rows (16 rows default)
 }
 
 

@@ -663,12 +663,12 @@ __global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
 // the clamp maps NaN to max_value), so it is skipped.
 constexpr int kChunkTiles = 1;  // tiles per workgroup: 1.209 ms vs 1.409 ms at 32 (cfg3)
 constexpr int kHrPad = 68;    // stripe row pitch (floats)
-// units per touched tile of a split field (small batches): 8 = one block row (8 blocks)
-// per unit, 4 = a 16-row stripe
-#ifdef PP_SPLIT_PARTS4
-constexpr int kSplitParts = 4;
-#else
+// units per touched tile of a split field (small batches): 4 = a 16-row stripe, 8 = one
+// block row (PP_SPLIT_PARTS8; cfg2 uniform CifHr kernel 76.7 vs 69.6 us, planted equal)
+#ifdef PP_SPLIT_PARTS8
 constexpr int kSplitParts = 8;
+#else
+constexpr int kSplitParts = 4;
 #endif
 static_assert(kSplitParts == 4 || kSplitParts == 8, "unit masks are written as u16 / u8 parts");
 

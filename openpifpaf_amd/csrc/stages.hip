@@ -346,6 +346,14 @@ __device__ __forceinline__ void bitonic_desc_np(uint64_t key[KPT], uint64_t *s_b
     BitonicMerge<KPT, 2, NP>::run(key, s_buf);
 }
 
+// seeds_sort_kernel sorts 257..4096 seeds with radix_desc (below); PP_NO_SEED_RADIX: with
+// the bitonic network (whose instances for 512..4096 keys are then compiled in)
+#ifdef PP_NO_SEED_RADIX
+constexpr bool kSeedRadix = false;
+#else
+constexpr bool kSeedRadix = true;
+#endif
+
 // the sort of the first np keys (np a power of two, rounded up to 4), 4 keys per thread;
 // block-uniform np
 __device__ void bitonic_desc(uint64_t key[4], uint64_t *s_buf, int np) {
@@ -357,10 +365,16 @@ __device__ void bitonic_desc(uint64_t key[4], uint64_t *s_buf, int np) {
     case 64: bitonic_desc_np<4, 64>(key, s_buf); break;
     case 128: bitonic_desc_np<4, 128>(key, s_buf); break;
     case 256: bitonic_desc_np<4, 256>(key, s_buf); break;
-    case 512: bitonic_desc_np<4, 512>(key, s_buf); break;
-    case 1024: bitonic_desc_np<4, 1024>(key, s_buf); break;
-    case 2048: bitonic_desc_np<4, 2048>(key, s_buf); break;
-    default: bitonic_desc_np<4, 4096>(key, s_buf); break;
+    default:
+        if constexpr (!kSeedRadix) {
+            switch (np) {
+            case 512: bitonic_desc_np<4, 512>(key, s_buf); break;
+            case 1024: bitonic_desc_np<4, 1024>(key, s_buf); break;
+            case 2048: bitonic_desc_np<4, 2048>(key, s_buf); break;
+            default: bitonic_desc_np<4, 4096>(key, s_buf); break;
+            }
+        }
+        break;
     }
 }
 
@@ -405,11 +419,6 @@ constexpr int kRadixBits = 7, kRadixDigits = 1 << kRadixBits;
 // (digit, wave) column reads over the banks; [digit][wave] put 16 lanes on one bank
 constexpr int kRadixPitch = kRadixDigits + 2;
 constexpr int kRadixMin = 256;  // up to here the bitonic network stays inside one wave
-#ifdef PP_NO_SEED_RADIX
-constexpr bool kSeedRadix = false;
-#else
-constexpr bool kSeedRadix = true;
-#endif
 
 // inclusive prefix sum over the wave on DPP (row shifts, then row_bcast15 / row_bcast31
 // carry the row totals), no LDS round trip
