@@ -880,6 +880,8 @@ struct HrSparseArgs {
     int tiles_x, tiles, tiles_y;
     int split;        // workgroups per field (small batches): each folds every split-th
                       // touched tile of the field
+    int split_list;   // prebuilt lists: a field uses ceil(list length / split_list) of its
+                      // split workgroups (at most split), the others return at once
     // split > 1: the field's list, bins and tile bits are built once by
     // cifhr_list_kernel (prebuilt; NULL: every split workgroup builds its own copy)
     int *pre_total;         // (n_img * K) list lengths
@@ -1090,13 +1092,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
     if (threadIdx.x == 0) s_next = 0;
     int total;
     bool use_bins;
+    int split = a.split;  // workgroups of this field that fold
     if (pre) {
+        total = a.pre_total[fld];
+        split = min(a.split, max(1, (total + a.split_list - 1) / a.split_list));
+        if (part >= split) return;  // block-uniform: this field needs fewer workgroups
         if (threadIdx.x < kTileBits / 32) s_bits[threadIdx.x] = a.pre_bits[fld * (kTileBits / 32) + threadIdx.x];
         if (threadIdx.x < kMaxBinRows) {
             s_rowcnt[threadIdx.x] = a.pre_rowcnt[fld * kMaxBinRows + threadIdx.x];
             s_rowoff[threadIdx.x] = a.pre_rowoff[fld * kMaxBinRows + threadIdx.x];
         }
-        total = a.pre_total[fld];
         use_bins = a.bins_cap > 0 && total > kBinMin;
         __syncthreads();
     } else {
@@ -1140,7 +1145,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
         if (lane == 0) claim = atomicAdd(&s_next, 1);
         // this workgroup's claim-th unit is the field's (claim * split + part)-th one: stripe
         // unit % kParts of the (unit / kParts)-th touched tile
-        const int unit = __builtin_amdgcn_readfirstlane(claim) * a.split + part;
+        const int unit = __builtin_amdgcn_readfirstlane(claim) * split + part;
         const int target = unit / kParts, q = unit % kParts;
         // advance to the target-th touched tile (claims grow, so the walk only moves on)
         int t = -1;
@@ -1798,6 +1803,19 @@ static int sparse_split(int64_t nf) {
     return (int)std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, slots / std::max<int64_t>(1, nf)));
 }
 
+// candidates per split workgroup of a prebuilt field list: all of a field's split
+// workgroups read the same bins, so a short list on many workgroups only queues them on
+// the same L2 lines (cfg2 planted, 125 candidates per field: fold kernel 35.1 us on 60
+// workgroups per field, 22.1 us on 3); PP_SPLIT_LIST overrides (diagnostics)
+constexpr int kSplitList = 48;
+static int split_list_len() {
+    static const int v = [] {
+        const char *e = getenv("PP_SPLIT_LIST");
+        return e && atoi(e) > 0 ? atoi(e) : kSplitList;
+    }();
+    return v;
+}
+
 size_t cifhr_sparse_workspace_size(const Heads &h, int n_img, int K) {
     const size_t nf = (size_t)n_img * K * sparse_split((int64_t)n_img * K);
     size_t bytes = round_up((int64_t)(nf * (size_t)h.cif_cells() * sizeof(FoldCand)), 256);
@@ -1853,6 +1871,7 @@ int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_confi
     a.masks = d_masks;
     const int64_t nf = (int64_t)n_img * K;
     a.split = sparse_split(nf);
+    a.split_list = split_list_len();
     const unsigned nblocks = (unsigned)(nf * a.split);
     // one workgroup per field, one CIF head: the list-in-LDS kernel (with the seeds when a
     // sink is given); fields of small batches split over several workgroups, and
