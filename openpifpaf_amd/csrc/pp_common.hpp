@@ -250,9 +250,10 @@ struct SeedSink {
 };
 // the seeds scratch of launch_seeds as a SeedSink (stages.hip)
 SeedSink seed_sink(int n_img, int K, const pp_config *cfg, int cap, void *scratch);
-// whether the decoder emits the seeds inside its CifHr kernel for this batch: one CIF head,
-// fields not split over workgroups (sparse_split == 1), seed threshold >= CifHr threshold
-// (every seed cell is then a splat of the field's list); launch_seeds then only sorts
+// whether the decoder emits the seeds inside its CifHr kernels for this batch: one CIF head,
+// one workgroup per field or split fields with a prebuilt list (the fold's last workgroup
+// per field emits them), seed threshold >= CifHr threshold (every seed cell is then a
+// splat of the field's list); launch_seeds then only sorts
 bool cifhr_fuses_seeds(const Heads &h, int n_img, int K, const pp_config *cfg);
 
 // `sink` (NULL: none): emit the seeds too (cifhr_fuses_seeds must hold)

@@ -888,8 +888,16 @@ struct HrSparseArgs {
     uint32_t *pre_bits;     // (n_img * K, kTileBits / 32) touched tiles
     int *pre_rowcnt;        // (n_img * K, kMaxBinRows) bin sizes (-1: none), offsets
     int *pre_rowoff;
-    SeedSink seeds;         // cifhr_fused_kernel<true>: where the field's seeds go
+    SeedSink seeds;         // cifhr_fused_kernel<true> / cifhr_list_kernel<true>: where the
+                            // field's seeds go
+    int *done;              // split fields with seeds: (n_img * K) workgroups finished
 };
+
+// a generic pointer as a global-address-space one (agent-scope atomics as global_ ops)
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(1))) T *as_global(T *p) {
+    return (__attribute__((address_space(1))) T *)p;
+}
 
 __device__ __forceinline__ float nan_max(float a, float b) {  // np.maximum
     return (a != a || b != b) ? NAN : (a > b ? a : b);
@@ -920,6 +928,70 @@ constexpr int kHrSt = 12;
     } while (0)
 #endif
 
+// Phase 3 of the seed emission (cif_seeds.py:35-47) for field `fld`, whose n_seed
+// candidates (c, x, y, s; c > threshold, in cell order) are in the sink's segment: v =
+// 0.9 * CifHr(x, y) + 0.1 * c from the finished block-sparse map, the seeds with v above
+// the threshold compacted in place, in order; their count into f_counts.  Block-uniform.
+__device__ void seeds_from_map(const HrSparseArgs &a, int64_t fld, int n_seed, int *s_tmp) {
+    const SeedSink &ss = a.seeds;
+    const int hw = a.h.cH[0] * a.h.cW[0];
+    const int f = (int)(fld % ss.K);
+    const int64_t img = fld / ss.K;
+    float *sv = ss.g_keys + img * 4 * ss.cap + (int64_t)f * hw;
+    float *sx = sv + ss.cap, *sy = sx + ss.cap, *sz = sy + ss.cap;
+    HrMap hm{};
+    hm.base = a.map;
+    hm.masks = a.masks;
+    hm.hh = a.hh;
+    hm.ww = a.ww;
+    hm.tiles_x = a.tiles_x;
+    hm.tiles = a.tiles;
+    int kept = 0;
+    int *sf = ss.g_f + img * ss.cap + (int64_t)f * hw;
+    // kSeedPer candidates per thread in flight (candidate e0 + 256 k + t), then one
+    // compaction per k in candidate order
+    constexpr int kSeedPer = 8;
+    for (int e0 = 0; e0 < n_seed; e0 += 256 * kSeedPer) {  // block-uniform
+        float v[kSeedPer], x[kSeedPer], y[kSeedPer], sc[kSeedPer];
+        bool ok[kSeedPer];
+#pragma unroll
+        for (int k = 0; k < kSeedPer; k++) {
+            const int e = e0 + 256 * k + (int)threadIdx.x;
+            ok[k] = false;
+            v[k] = x[k] = y[k] = sc[k] = 0.0f;
+            if (e < n_seed) {
+                const float c = sv[e];
+                x[k] = sx[e];
+                y[k] = sy[e];
+                sc[k] = sz[e];
+                const float hv = hm.at(fld, x[k], y[k], 0.0f);
+                float vv = 0.9f * hv + 0.1f * c;  // 0.9 * v + 0.1 * c
+                if (ss.score_scale != 1.0f) vv = vv * ss.score_scale;
+                v[k] = vv;
+                ok[k] = vv > ss.th;
+            }
+        }
+        // every candidate of this pass is in registers before the first write below
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kSeedPer; k++) {
+            if (e0 + 256 * k >= n_seed) break;  // block-uniform
+            int tot;
+            const int slot = block_compact<4>(ok[k], s_tmp, tot);
+            if (ok[k]) {
+                const int pos = kept + slot;  // <= its candidate index: earlier slots only
+                sv[pos] = v[k];
+                sx[pos] = x[k];
+                sy[pos] = y[k];
+                sz[pos] = sc[k];
+                sf[pos] = f;
+            }
+            kept += tot;
+        }
+    }
+    if (threadIdx.x == 0) ss.f_counts[fld] = kept;
+}
+
 // Phase 1 of the CifHr kernel: the field's splat list in the reference's order (every
 // group, cif_hr.py:26-40, 55-57) as fold candidates in the field's global list.  A round
 // covers 256 * kSpU cells: each thread loads its kSpU confidences at once (plus the scale
@@ -930,13 +1002,40 @@ constexpr int kHrSt = 12;
 // keeps (a round keeping more than kSpStage reads them per batch instead).  s_bits marks
 // the 64x64 tiles the boxes touch (cleared by the caller before the first barrier).
 // Returns the list length; s_gbeg[g] = start of group g's entries.  Ends with a barrier.
-template <bool MULTI>
+// SEEDS (one CIF head, one group): also the field's seed candidates (c > seed threshold,
+// cif_seeds.py:28-33) into a.seeds' segment in cell order, their count into f_counts[fld]
+// (seeds_from_map finishes them); s_tmp: 4 ints of LDS.
+template <bool MULTI, bool SEEDS = false, int STAGE = kSpStage>
 __device__ int hr_splat_list(const HrSparseArgs &a, int64_t fld, int64_t slot, uint32_t *s_bits,
-                             int (*s_cnt)[kSpU][4], int *s_gbeg, int *stage) {
+                             int (*s_cnt)[kSpU][4], int *s_gbeg, int *stage,
+                             int *s_tmp = nullptr) {
+    static_assert(!(MULTI && SEEDS), "seed candidates of one CIF head only");
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ng = MULTI ? a.h.n_groups : 1;
     FoldCand *glist = a.list + slot * a.list_cap;  // this workgroup's own copy
     int running = 0, buf = 0;
+    const SeedSink &ss = a.seeds;
+    const int sfield = SEEDS ? (int)(fld % ss.K) : 0;
+    const bool seeding = SEEDS && !((ss.skip >> sfield) & 1u);
+    const int shw = a.h.cH[0] * a.h.cW[0];
+    float *sv = SEEDS ? ss.g_keys + (fld / (SEEDS ? ss.K : 1)) * 4 * ss.cap + (int64_t)sfield * shw
+                      : nullptr;
+    int n_seed = 0;
+    // block-uniform: one seed-candidate compaction over the threads' (flag, cell)
+    auto seed_cand = [&](bool cand, const float *p, int hw, int cell, float c, float stride) {
+        if constexpr (SEEDS) {
+            int tot;
+            const int at = block_compact<4>(cand, s_tmp, tot);
+            if (cand) {
+                float *q = sv + n_seed + at;
+                q[0] = c;
+                q[ss.cap] = p[hw + cell] * stride;
+                q[2 * ss.cap] = p[2 * hw + cell] * stride;
+                q[3 * ss.cap] = p[4 * hw + cell] * stride;
+            }
+            n_seed += tot;
+        }
+    };
     for (int g = 0; g < ng; g++) {
         if (threadIdx.x == 0) s_gbeg[g] = running;
         const float stride = (float)a.h.cstride[g];
@@ -1008,24 +1107,41 @@ __device__ int hr_splat_list(const HrSparseArgs &a, int64_t fld, int64_t slot, u
                         o += q.x + q.y + q.z + q.w;
                     }
                 };
-                if (off <= kSpStage) {
+                if (off <= STAGE) {
                     place([&](int cell, int pos) { stage[pos] = cell; });
                     __syncthreads();
-                    for (int e = threadIdx.x; e < off; e += 256) {
-                        const int cell = stage[e];
-                        emit(p, hw, cell, p[cell], running + e);
+                    if constexpr (SEEDS) {
+                        for (int e0 = 0; e0 < off; e0 += 256) {  // block-uniform
+                            const int e = e0 + (int)threadIdx.x;
+                            int cell = 0;
+                            float c = 0.0f;
+                            if (e < off) {
+                                cell = stage[e];
+                                c = p[cell];
+                                emit(p, hw, cell, c, running + e);
+                            }
+                            seed_cand(seeding && e < off && c > ss.th, p, hw, cell, c, stride);
+                        }
+                    } else {
+                        for (int e = threadIdx.x; e < off; e += 256) {
+                            const int cell = stage[e];
+                            emit(p, hw, cell, p[cell], running + e);
+                        }
                     }
                 } else {  // more than the stage holds: batch by batch (not unrolled)
                     int o = 0;
                     for (int k = 0; k < kSpU; k++) {
                         const int4 q = *reinterpret_cast<const int4 *>(&s_cnt[buf][k][0]);
                         const uint64_t bal = __ballot((keep >> k) & 1u);
+                        const int cell = base + k * 256 + (int)threadIdx.x;
+                        float c = 0.0f;
                         if ((keep >> k) & 1u) {
-                            const int cell = base + k * 256 + (int)threadIdx.x;
-                            emit(p, hw, cell, p[cell],
+                            c = p[cell];
+                            emit(p, hw, cell, c,
                                  running + o + (wave > 0 ? q.x : 0) + (wave > 1 ? q.y : 0) +
                                      (wave > 2 ? q.z : 0) + lane_prefix(bal));
                         }
+                        seed_cand(seeding && ((keep >> k) & 1u) && c > ss.th, p, hw, cell, c, stride);
                         o += q.x + q.y + q.z + q.w;
                     }
                 }
@@ -1036,6 +1152,7 @@ __device__ int hr_splat_list(const HrSparseArgs &a, int64_t fld, int64_t slot, u
         }
     }
     if (threadIdx.x == 0) s_gbeg[ng] = running;
+    if (SEEDS && threadIdx.x == 0) ss.f_counts[fld] = n_seed;  // candidates (seeds_from_map)
     __syncthreads();
     return running;
 }
@@ -1046,15 +1163,24 @@ __device__ int hr_splat_list(const HrSparseArgs &a, int64_t fld, int64_t slot, u
 // cifhr_tile_kernel, in HrSplatArgs' layout (masks NULL).  Untouched tiles of the sparse map
 // get their empty block masks here.  8 waves per SIMD (64 VGPRs, as cifhr_sparse_kernel):
 // uniform dense map 5.36 -> 5.32 ms per 256 images against 98 VGPRs, planted unchanged.
+// SEEDS: the seed candidates too (hr_splat_list), and the field's completion counter of
+// cifhr_sparse_kernel<false, true> zeroed (the kernel boundary orders it before that launch).
+template <bool SEEDS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void cifhr_list_kernel(HrSparseArgs a) {
     __shared__ uint32_t s_bits[kTileBits / 32];
     __shared__ RowBinLds s_rb;
     __shared__ __attribute__((aligned(16))) int s_cnt[2][kSpU][4];
     __shared__ int s_gbeg[kMaxHeads + 1];
-    __shared__ int s_stage[kSpStage];
+    // with seeds a whole round's kept cells (uniform 80x80: ~2800) stay staged: the batch-by-
+    // batch path would compact seed candidates once per 256-cell batch
+    constexpr int kStage = SEEDS ? 256 * kSpU : kSpStage;
+    __shared__ int s_stage[kStage];
+    __shared__ int s_tmp[4];
     const int64_t fld = blockIdx.x;
     if (threadIdx.x < kTileBits / 32) s_bits[threadIdx.x] = 0u;
-    const int total = hr_splat_list<false>(a, fld, fld, s_bits, s_cnt, s_gbeg, s_stage);
+    if (SEEDS && threadIdx.x == 0) a.done[fld] = 0;
+    const int total =
+        hr_splat_list<false, SEEDS, kStage>(a, fld, fld, s_bits, s_cnt, s_gbeg, s_stage, s_tmp);
     int *rowcnt = a.pre_rowcnt + fld * kMaxBinRows, *rowoff = a.pre_rowoff + fld * kMaxBinRows;
     if (a.bins_cap > 0 && total > kBinMin)
         hr_row_bins(a.list + fld * a.list_cap, total, a.bins + fld * a.bins_cap, a.bins_cap,
@@ -1068,9 +1194,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
             if (!((s_bits[t >> 5] >> (t & 31)) & 1u)) a.masks[fld * a.tiles + t] = 0ull;
 }
 
-template <bool MULTI>
+// SEEDS (split fields with a prebuilt list and seed candidates, cifhr_list_kernel<true>):
+// the field's last workgroup to finish its fold emits the field's seeds (seeds_from_map).
+// Completion is the write-through counter form of cdna_hip_programming.md Guideline 16: the
+// map's blocks and the units' mask bits are stored sc1 (relaxed agent-scope atomic stores),
+// so no release fence is needed; every wave drains its
+// stores, the workgroup's barrier, one lane's relaxed agent-scope ticket; the last arriver
+// acquires at agent scope, then reads the map with plain loads.  (With a release fence in
+// every workgroup instead, cfg2 uniform's fold kernel took 99-110 vs 70 us.)
+template <bool MULTI, bool SEEDS = false>
 // 8 waves per SIMD (<= 64 VGPRs): the kernel is latency-bound, occupancy hides it
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void cifhr_sparse_kernel(HrSparseArgs a) {
+    static_assert(!(MULTI && SEEDS), "seeds of one CIF head only");
     __shared__ uint32_t s_bits[kTileBits / 32];
     __shared__ RowBinLds s_rb;
     __shared__ int s_rowcnt[kMaxBinRows], s_rowoff[kMaxBinRows];  // bins (hr_row_bins)
@@ -1259,7 +1394,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
                 }
                 // nontemporal: the map is read by later kernels only, and streaming it past
                 // L2 keeps the row bins the next tiles scan resident there
-                if (!MULTI) {
+                if (!MULTI && SEEDS) {
+                    __hip_atomic_store(as_global(&mp[blk * 64 + lane]),
+                                       acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else if (!MULTI) {
                     __builtin_nontemporal_store(acc, &mp[blk * 64 + lane]);
                 } else if (last) {
                     __builtin_nontemporal_store(nan_max(acc, res), &mp[blk * 64 + lane]);
@@ -1285,7 +1423,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
             wave_sync();  // candidate arrays are rewritten by the next pass
         }
         if (lane == 0) {
-            if (kParts == 1)
+            if (SEEDS && kSplitParts == 4)  // the unit's 16 bits, write-through (sc1)
+                __hip_atomic_store(
+                    as_global(reinterpret_cast<unsigned short *>(&a.masks[fld * a.tiles + t]) + q),
+                    (unsigned short)(done >> (16 * q)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if (SEEDS)  // the unit's 8 bits
+                __hip_atomic_store(
+                    as_global(reinterpret_cast<unsigned char *>(&a.masks[fld * a.tiles + t]) + q),
+                    (unsigned char)(done >> (8 * q)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if (kParts == 1)
                 a.masks[fld * a.tiles + t] = done;
             else if (kSplitParts == 4)  // the unit's 16 bits of the tile's mask
                 reinterpret_cast<uint16_t *>(&a.masks[fld * a.tiles + t])[q] = (uint16_t)(done >> (16 * q));
@@ -1294,6 +1440,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
         }
     }
     HR_STAMP(2 + wave);
+    if constexpr (SEEDS) {
+        __shared__ int s_last;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's blocks and masks
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int old = __hip_atomic_fetch_add(
+                as_global(&a.done[fld]), 1,
+                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = old == split - 1;
+            if (old == split - 1) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+        __syncthreads();
+        if (s_last) {
+            int *s_tmp = reinterpret_cast<int *>(&s_cand[0][0]);  // the fold's LDS is free
+            seeds_from_map(a, fld, a.seeds.f_counts[fld], s_tmp);
+        }
+    }
 }
 
 // -------------------------------------------------------------------------------------
@@ -1595,44 +1761,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
     // ---- phase 3: the seeds (cif_seeds.py:35-47) from the finished map ----
     if constexpr (SEEDS) {
         __syncthreads();  // every wave's blocks and masks are stored
-        HrMap hm{};
-        hm.base = a.map;
-        hm.masks = a.masks;
-        hm.hh = a.hh;
-        hm.ww = a.ww;
-        hm.tiles_x = a.tiles_x;
-        hm.tiles = a.tiles;
-        int kept = 0;
-        int *sf = ss.g_f + img * ss.cap + (int64_t)f * hw;
-        for (int e0 = 0; e0 < n_seed; e0 += 256) {  // block-uniform
-            const int e = e0 + (int)threadIdx.x;
-            float v = 0.0f, x = 0.0f, y = 0.0f, sc = 0.0f;
-            bool ok = false;
-            if (e < n_seed) {
-                const float c = sv[e];
-                x = sx[e];
-                y = sy[e];
-                sc = sz[e];
-                const float hv = hm.at(fld, x, y, 0.0f);
-                float vv = 0.9f * hv + 0.1f * c;  // 0.9 * v + 0.1 * c
-                if (ss.score_scale != 1.0f) vv = vv * ss.score_scale;
-                v = vv;
-                ok = vv > ss.th;
-            }
-            int tot;
-            // every candidate of this round is in registers before the first write below
-            const int slot = block_compact<4>(ok, s_tmp, tot);
-            if (ok) {
-                const int pos = kept + slot;  // <= e: earlier candidates only
-                sv[pos] = v;
-                sx[pos] = x;
-                sy[pos] = y;
-                sz[pos] = sc;
-                sf[pos] = f;
-            }
-            kept += tot;
-        }
-        if (threadIdx.x == 0) ss.f_counts[fld] = kept;
+        if (seeding) seeds_from_map(a, fld, n_seed, s_tmp);
+        else if (threadIdx.x == 0) ss.f_counts[fld] = 0;
     }
 }
 
@@ -1755,7 +1885,7 @@ int cifhr_heads_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config
         la.pre_rowcnt = sa.rowcnt;
         la.pre_rowoff = sa.rowoff;
         if (sa.tiles > kTileBits) return fail(PP_ESHAPE, std::string(who) + ": CifHr map too large");
-        hipLaunchKernelGGL(cifhr_list_kernel, dim3((unsigned)nf), dim3(256), 0, s, la);
+        hipLaunchKernelGGL(cifhr_list_kernel<false>, dim3((unsigned)nf), dim3(256), 0, s, la);
     } else {
         hipLaunchKernelGGL(cifhr_splats_kernel<DET>, dim3((unsigned)(nf * h.n_groups)), dim3(256), 0, s, sa);
     }
@@ -1824,12 +1954,27 @@ size_t cifhr_sparse_workspace_size(const Heads &h, int n_img, int K) {
     return bytes;
 }
 
+// the prebuilt-list mode of split fields: the field's list, lengths, tile bits, bin sizes
+// and completion counters go past the nf lists (the workspace holds nf * split of them)
+static size_t prebuilt_bytes(int64_t nf) {
+    return (size_t)nf * (2 + kTileBits / 32 + 2 * kMaxBinRows) * sizeof(int);
+}
+static bool sparse_prebuilt(const Heads &h, int64_t nf) {
+    const int split = sparse_split(nf);
+    return split > 1 && h.n_groups == 1 &&
+           (size_t)nf * (split - 1) * h.cif_cells() * sizeof(FoldCand) >= prebuilt_bytes(nf);
+}
+
 bool cifhr_fuses_seeds(const Heads &h, int n_img, int K, const pp_config *cfg) {
 #ifdef PP_NO_FUSED  // A/B builds (openpifpaf_amd.build variants)
     return false;
 #endif
+    const int64_t nf = (int64_t)n_img * K;
+    // one workgroup per field: cifhr_fused_kernel<true>; split fields with a prebuilt list:
+    // cifhr_list_kernel<true> + cifhr_sparse_kernel<false, true>
     return h.n_cif == 1 && h.n_groups == 1 && h.group_size() == 1 && n_img > 0 && K > 0 &&
-           sparse_split((int64_t)n_img * K) == 1 && cfg->seed_threshold >= cfg->cif_threshold;
+           (sparse_split(nf) == 1 || sparse_prebuilt(h, nf)) &&
+           cfg->seed_threshold >= cfg->cif_threshold;
 }
 
 int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config *cfg,
@@ -1889,22 +2034,27 @@ int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_confi
         return check_launch(who);
     }
 #endif
-    if (sink) return fail(PP_EINVAL, std::string(who) + ": seeds cannot be fused here");
     // split fields: one list per field, built before the fold (cifhr_list_kernel);
-    // its lengths, tile bits and bin sizes go past the nf lists the prebuilt mode uses (the
-    // workspace holds nf * split of them)
-    const size_t pre_bytes = (size_t)nf * (1 + kTileBits / 32 + 2 * kMaxBinRows) * sizeof(int);
     // (cfg2 uniform: CifHr stage 0.173 -> 0.125 ms with the prebuilt list and stripe units;
-    // planted unchanged within noise)
-    const bool prebuilt = a.split > 1 && h.n_groups == 1 &&
-                          (size_t)nf * (a.split - 1) * a.list_cap * sizeof(FoldCand) >= pre_bytes;
+    // planted unchanged within noise).  With a sink the list kernel also writes the seed
+    // candidates and the fold's last workgroup per field emits the seeds (cfg2: no
+    // seeds_emit_kernel launch)
+    const bool prebuilt = sparse_prebuilt(h, nf);
+    if (sink && (!prebuilt || !cifhr_fuses_seeds(h, n_img, K, cfg) || sink->K != K))
+        return fail(PP_EINVAL, std::string(who) + ": seeds cannot be fused here");
     if (prebuilt) {
         int *p = reinterpret_cast<int *>(a.list + nf * a.list_cap);
         a.pre_total = p;
         a.pre_bits = reinterpret_cast<uint32_t *>(p + nf);
         a.pre_rowcnt = p + nf * (1 + kTileBits / 32);
         a.pre_rowoff = a.pre_rowcnt + nf * kMaxBinRows;
-        hipLaunchKernelGGL(cifhr_list_kernel, dim3((unsigned)nf), dim3(256), 0, s, a);
+        a.done = a.pre_rowoff + nf * kMaxBinRows;
+        if (sink) {
+            a.seeds = *sink;
+            hipLaunchKernelGGL(cifhr_list_kernel<true>, dim3((unsigned)nf), dim3(256), 0, s, a);
+        } else {
+            hipLaunchKernelGGL(cifhr_list_kernel<false>, dim3((unsigned)nf), dim3(256), 0, s, a);
+        }
     }
 #ifdef PP_STAMPS
     uint64_t *st = nullptr;
@@ -1914,6 +2064,8 @@ int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_confi
 #endif
     if (h.n_groups > 1)
         hipLaunchKernelGGL(cifhr_sparse_kernel<true>, dim3(nblocks), dim3(256), 0, s, a);
+    else if (sink)
+        hipLaunchKernelGGL((cifhr_sparse_kernel<false, true>), dim3(nblocks), dim3(256), 0, s, a);
     else
         hipLaunchKernelGGL(cifhr_sparse_kernel<false>, dim3(nblocks), dim3(256), 0, s, a);
 #ifdef PP_STAMPS
