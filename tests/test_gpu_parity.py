@@ -460,9 +460,12 @@ def test_seeds_device_order(dec, n_img, hw, distinct):
 
 # the decoder's own seeds at a batch whose fields get one workgroup each (64 images x 17
 # fields >= 1024): emitted by the CifHr kernel itself (cifhr_fused_kernel<true>), then
-# sorted; saturated and tied confidences, the full decode against the oracle
+# sorted; and at 2 images, whose fields split over several workgroups (the list kernel
+# writes the seed candidates, the fold's last workgroup per field finishes them);
+# saturated and tied confidences, the full decode against the oracle
+@pytest.mark.parametrize('n', [64, 2])
 @pytest.mark.parametrize('hw,distinct', [(12, False), (18, True), (20, False)])
-def test_fused_seeds_decode_ties(dec, hw, distinct):
+def test_fused_seeds_decode_ties(dec, hw, distinct, n):
     import torch
     from openpifpaf_amd import constants
     from openpifpaf_amd._abi import make_config
@@ -472,11 +475,10 @@ def test_fused_seeds_decode_ties(dec, hw, distinct):
     caf = np.zeros((19, 9, hw, hw), np.float32)
     skel = constants.COCO_PERSON_SKELETON
     ref = oracle.decode(cif, caf, skel, cfg)
-    n = 64
     c = torch.from_numpy(np.ascontiguousarray(np.broadcast_to(cif, (n,) + cif.shape))).cuda()
     f = torch.from_numpy(np.ascontiguousarray(np.broadcast_to(caf, (n,) + caf.shape))).cuda()
     recs, offs, _ = DecodeEngine().decode(c, f, skel, cfg)
-    for i in (0, 1, 31, 63):
+    for i in sorted({0, 1, n // 2 - 1, n - 1}):
         got = recs[offs[i]:offs[i + 1]]
         assert len(got) == len(ref) > 0, (i, len(got), len(ref))
         for name in ('data', 'joint_scales', 'decoding_pairs'):
