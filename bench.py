@@ -326,7 +326,8 @@ def main():
     value = images / elapsed
     ms_step = 1e3 * elapsed / args.steps
     hh, ww = (h - 1) * 8 + 1, (w - 1) * 8 + 1
-    cifhr_bytes, hr_tiles = cifhr_stage_bytes(cif_h, 8, cfg.cif_threshold)
+    cifhr_bytes, hr_tiles, sector_bytes = cifhr_stage_bytes(cif_h, 8, cfg.cif_threshold,
+                                                            cfg.seed_threshold)
     achieved = cifhr_bytes / (stage_avg[0] * 1e-3) / 1e9
     dense_ms = dense_cifhr_ms(cif, cfg, stream, args.steps, args.warmup)
     dense_bytes = 4 * k * (5 * h * w + hh * ww) * batch  # SURVEY.md §8d, per launch
@@ -377,10 +378,13 @@ def main():
         # the decoder's own CifHr (inside `value`): the block-sparse map, written only where
         # splat boxes land; latency-bound per field, far below the dense byte count
         'roofline_decoder_cifhr': {
-            'bound': 'hbm', 'kernel': 'cifhr_sparse_kernel',
+            'bound': 'hbm', 'kernel': 'cifhr_fused_kernel (CifHr + seed emission)',
             'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBS, 'unit': 'GB/s',
             'frac': round(achieved / PEAK_HBM_GBS, 4),
             'algorithmic_bytes_per_launch': cifhr_bytes, 'traffic': None,
+            # the same bytes counted in the 64-B lines they live in: the x / y / scale rows
+            # of kept cells are 4-B gathers, a line per run of kept cells
+            'line_granular_bytes_per_launch': sector_bytes,
             'written_block_frac': round(hr_tiles, 6),
             'us_per_image': round(1e3 * stage_avg[0] / batch, 4),
             'dense_equivalent_gbs': round(dense_bytes / (stage_avg[0] * 1e-3) / 1e9, 1),
@@ -490,13 +494,17 @@ def main():
         dist.destroy_process_group()
 
 
-def cifhr_stage_bytes(cif, stride, v_th, tile=64, block=8, lds_list=256):
-    """Algorithmic HBM bytes of the decoder's CifHr stage (cifhr_sparse_kernel) over a
-    batch (n, K, 5, H, W): the confidence plane of every cell, the x / y / scale rows of
-    passing cells, the splat records beyond the field's LDS-resident list written and read
-    once (32 B each), the 8x8 blocks of the block-sparse map that splat boxes touch (256 B
-    each, the same box arithmetic as splat_box in csrc/splat.hip) and one u64 block mask per
-    64x64 tile.  Returns (bytes, fraction of the map's blocks written)."""
+def cifhr_stage_bytes(cif, stride, v_th, seed_th=None, tile=64, block=8, lds_list=256):
+    """Algorithmic HBM bytes of the decoder's CifHr stage (cifhr_fused_kernel: the
+    block-sparse map and the seed emission) over a batch (n, K, 5, H, W): the confidence
+    plane of every cell, the x / y / scale rows of passing cells, the splat records beyond
+    the field's LDS-resident list written and read once (32 B each), the 8x8 blocks of the
+    block-sparse map that splat boxes touch (256 B each, the same box arithmetic as
+    splat_box in csrc/splat.hip), one u64 block mask per 64x64 tile, and per seed candidate
+    (c > seed_th) its 16-B record written, read back with the CifHr block value and mask at
+    its position, and the kept seed's 20 B written.  Returns (bytes, fraction of the map's
+    blocks written, the same bytes with the x / y / scale gathers counted as the 64-B lines
+    they touch)."""
     n, k, _, h, w = cif.shape
     hh, ww = (h - 1) * stride + 1, (w - 1) * stride + 1
     tiles_x = (-(-ww // 32) * 32 + tile - 1) // tile
@@ -526,9 +534,13 @@ def cifhr_stage_bytes(cif, stride, v_th, tile=64, block=8, lds_list=256):
             touched[img[m], fld[m], by0[m] + dy, bx0[m] + dx] = True
     n_blocks = int(touched.sum())
     overflow = int(np.maximum(per_field - lds_list, 0).sum())
-    nbytes = (4 * n * k * h * w + 12 * len(img) + 64 * overflow +
-              n_blocks * 4 * block * block + 8 * n * k * tiles_x * tiles_y)
-    return nbytes, n_blocks / touched.size
+    n_seed = int((c > np.float32(seed_th)).sum()) if seed_th is not None else 0
+    seed_bytes = n_seed * (16 + 16 + 4 + 8 + 20)
+    rest = (4 * n * k * h * w + 64 * overflow + n_blocks * 4 * block * block +
+            8 * n * k * tiles_x * tiles_y + seed_bytes)
+    # kept cells' rows at 64-B line granularity: distinct (plane row, 16-cell segment) pairs
+    lines = len(np.unique(((img * k + fld) * h + cy_i) * ((w + 15) // 16) + cx_i // 16))
+    return rest + 12 * len(img), n_blocks / touched.size, rest + 3 * 64 * lines
 
 
 def dense_cifhr_ms(cif, cfg, stream, steps, warmup):
@@ -565,7 +577,7 @@ def dense_cifhr_ms(cif, cfg, stream, steps, warmup):
 
 # roofline key -> the kernels whose PMC bytes it reports (tools/prof_summary.py)
 TRAFFIC_KERNELS = {'roofline': 'cifhr_list_kernel+cifhr_tile_kernel',
-                   'roofline_decoder_cifhr': 'cifhr_sparse_kernel'}
+                   'roofline_decoder_cifhr': 'cifhr_fused_kernel'}
 
 
 def committed_traffic():

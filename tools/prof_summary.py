@@ -20,7 +20,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # (the dense map's phase 1 is cifhr_list_kernel from round 3 on, cifhr_splats_kernel before;
 # at 256 images the decoder does not use cifhr_list_kernel, so in the cfg3 bench it is the
 # dense map's alone)
-KERNEL_SETS = (('cifhr_list_kernel', 'cifhr_tile_kernel'), ('cifhr_sparse_kernel',))
+KERNEL_SETS = (('cifhr_list_kernel', 'cifhr_tile_kernel'), ('cifhr_sparse_kernel',),
+               ('cifhr_fused_kernel',))
 CALIB_BYTES = 1 << 30
 
 
@@ -82,9 +83,9 @@ def main():
     # with (tools/calib_counters.hip): 4 B field reads, 16 B nontemporal dense-map stores,
     # 4 B block stores of the sparse map
     read_width = {'cifhr_splats_kernel': 'read4', 'cifhr_list_kernel': 'read4', 'cifhr_tile_kernel': 'read16',
-                  'cifhr_sparse_kernel': 'read4'}
+                  'cifhr_sparse_kernel': 'read4', 'cifhr_fused_kernel': 'read4'}
     write_width = {'cifhr_splats_kernel': 'write16', 'cifhr_list_kernel': 'write16', 'cifhr_tile_kernel': 'write16',
-                   'cifhr_sparse_kernel': 'write4'}
+                   'cifhr_sparse_kernel': 'write4', 'cifhr_fused_kernel': 'write4'}
     sha_path = os.path.join(src, 'src_sha.txt')
     summary = {
         'tag': tag,
