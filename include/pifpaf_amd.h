@@ -73,6 +73,11 @@ typedef struct pp_config {
     int32_t occupancy_min_scale;
     uint32_t seed_skip_mask;      /* bit f set: field f emits no seeds, FieldConfig.seed_mask[f]
                                      falsy (cif_seeds.py:28-29); 0 = every field seeds       */
+    const float *confidence_scales; /* HOST array (C): CifCaf(confidence_scales=...)
+                                     (cifcaf.py:39,52), each CAF's weight on the frontier
+                                     priorities of _grow (cifcaf.py:259-260, 282-284), f32
+                                     products as NumPy forms them from a list of Python
+                                     floats; NULL = none (the default)                       */
 } pp_config;
 
 /*

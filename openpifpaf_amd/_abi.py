@@ -92,6 +92,7 @@ class PPConfig(ctypes.Structure):
         ('occupancy_reduction', ctypes.c_int32),
         ('occupancy_min_scale', ctypes.c_int32),
         ('seed_skip_mask', ctypes.c_uint32),
+        ('confidence_scales', ctypes.POINTER(ctypes.c_float)),
     ]
 
 
@@ -100,17 +101,26 @@ def make_config(*, cif_threshold=0.1, seed_threshold=0.2, seed_score_scale=1.0,
                 keypoint_threshold=0.0, nms_keypoint_threshold=0.0,
                 nms_instance_threshold=0.0, nms_suppression=0.0, stride=8, cif_neighbors=16,
                 force_complete=True, greedy=False, connection_method='blend', apply_nms=True,
-                occupancy_reduction=2, occupancy_min_scale=4, seed_mask=None):
-    """Defaults = eval_coco defaults (decoder/factory.py:17-22, eval_coco.py:215)."""
+                occupancy_reduction=2, occupancy_min_scale=4, seed_mask=None,
+                confidence_scales=None):
+    """Defaults = eval_coco defaults (decoder/factory.py:17-22, eval_coco.py:215).
+    confidence_scales: CifCaf's per-CAF frontier weights (cifcaf.py:259-260, 282-284) as
+    float32, the type NumPy multiplies a float32 score by a Python float in; the array is
+    kept alive on the returned struct."""
     if connection_method not in ('blend', 'max'):
         raise Exception('connection method not known')
-    return PPConfig(
+    cfg = PPConfig(
         cif_threshold, seed_threshold, seed_score_scale, caf_threshold,
         complete_caf_threshold, cif_floor, keypoint_threshold, nms_keypoint_threshold,
         nms_instance_threshold, nms_suppression, int(stride), int(cif_neighbors),
         int(bool(force_complete)), int(bool(greedy)),
         0 if connection_method == 'blend' else 1, int(bool(apply_nms)),
         int(occupancy_reduction), int(occupancy_min_scale), seed_skip_mask(seed_mask))
+    if confidence_scales is not None:
+        cs = np.ascontiguousarray([float(v) for v in confidence_scales], dtype=np.float32)
+        cfg._confidence_scales = cs  # the struct points into it
+        cfg.confidence_scales = cs.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    return cfg
 
 
 def check_seed_mask(seed_mask, k):

@@ -113,6 +113,10 @@ struct GrowArgs {
     int nd;
     uint8_t j_off[kKP + 1];
     uint8_t d_j[kSlots], d_k[kSlots], d_caf[kSlots], d_fwd[kSlots];
+    // CifCaf(confidence_scales=...) (cifcaf.py:259-260, 282-284): the slot's CAF weight on
+    // its frontier priorities when has_cs (pp_config.confidence_scales), else unused
+    int has_cs;
+    float slot_cs[kSlots];
     // workspace (per image regions)
     uint8_t *occ;
     int64_t occ_cap;          // bytes per image
@@ -789,7 +793,8 @@ __device__ __forceinline__ void add_to_frontier(const GrowArgs &g, LDS &L, Front
         const uint64_t m = __ballot(elig);
         if (elig) {
             F.st[r] = 1;
-            F.neg[r] = neg;
+            // max_possible_score *= confidence_scales[caf_i] (cifcaf.py:258-261)
+            F.neg[r] = g.has_cs ? -(sqrtf(start_v) * g.slot_cs[d]) : neg;
             F.added[r] = 1;
             const int t = nfr + lane_prefix(m);
             if (t < PP_MAX_FRONTIER) {
@@ -1299,7 +1304,8 @@ __device__ __forceinline__ void grow(const GrowArgs &g, LDS &L, int img, int set
             }
             if (nx[3] == 0.0f) continue;
             e.eval = 1;
-            e.neg = -nx[3];
+            // score *= confidence_scales[caf_i] (cifcaf.py:282-284; not on the greedy return)
+            e.neg = g.has_cs ? -(nx[3] * g.slot_cs[e.slot]) : -nx[3];
             e.x = nx[0];
             e.y = nx[1];
             e.s = nx[2];
@@ -3567,6 +3573,9 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
             }
             g.j_off[K] = (uint8_t)d;
             g.nd = d;
+            g.has_cs = cfg->confidence_scales != nullptr;
+            for (int e = 0; e < kSlots; e++)
+                g.slot_cs[e] = (g.has_cs && e < d) ? cfg->confidence_scales[g.d_caf[e]] : 1.0f;
         }
         g.occ = (uint8_t *)(ws + d.off_occ);
         g.occ_cap = d.occ_cap;

@@ -136,6 +136,7 @@ void pp_default_config(pp_config *c) {
     c->occupancy_reduction = 2;
     c->occupancy_min_scale = 4;
     c->seed_skip_mask = 0u;
+    c->confidence_scales = nullptr;
 }
 
 }  // extern "C"

@@ -44,11 +44,18 @@ class CifCaf(Generator):
         super().__init__(worker_pool)
         if nms is True:
             nms = nms_module.Keypoints()
-        if nms is not None and not isinstance(nms, nms_module.Keypoints):
-            raise NotImplementedError('only nms.Keypoints runs inside the device decode')
-        if confidence_scales is not None:
-            raise NotImplementedError('confidence_scales (dense coupling) is not implemented; '
-                                      'factory_decode never passes it (factory.py:184-211)')
+        # nms.Keypoints (its own annotations()) runs inside the device decode; any other
+        # object with an annotations(list) method (cifcaf.py:117-118) runs on the host over
+        # each image's decoded list, which the device then leaves unsuppressed
+        if nms is not None and not callable(getattr(nms, 'annotations', None)):
+            raise TypeError('nms must provide annotations(annotations)')
+        # confidence_scales (cifcaf.py:39,52): per-CAF weights on the frontier priorities
+        # of _grow (cifcaf.py:259-260, 282-284), applied on the device (pp_config).  The
+        # reference indexes it per CAF while growing; a list shorter than the skeleton
+        # raises its IndexError here, before any decode.
+        if confidence_scales is not None and len(confidence_scales) < len(skeleton):
+            raise IndexError('list index out of range (confidence_scales has {} entries for '
+                             '{} CAF fields)'.format(len(confidence_scales), len(skeleton)))
         self.field_config = field_config
         self.keypoints = keypoints
         self.skeleton = skeleton
@@ -73,7 +80,7 @@ class CifCaf(Generator):
         stride = int(self.field_config.cif_strides[0])  # multi-scale heads carry their own
         if CifSeeds.threshold is None:
             raise TypeError('CifSeeds.threshold is not configured (decoder.configure sets it)')
-        nms = self.nms
+        nms = self.nms if self._device_nms() else None
         check_seed_mask(self.field_config.seed_mask, len(self.keypoints))
         return make_config(
             cif_threshold=CifHr.v_threshold,
@@ -92,7 +99,19 @@ class CifCaf(Generator):
             connection_method=self.connection_method,
             apply_nms=nms is not None,
             seed_mask=self.field_config.seed_mask,
+            confidence_scales=self.confidence_scales,
         )
+
+    def _device_nms(self):
+        """nms.Keypoints (not a subclass overriding annotations()) runs on the device."""
+        return (isinstance(self.nms, nms_module.Keypoints) and
+                type(self.nms).annotations is nms_module.Keypoints.annotations)
+
+    def _host_nms(self, anns):
+        """cifcaf.py:117-118 for an NMS object other than nms.Keypoints."""
+        if self.nms is None or self._device_nms():
+            return anns
+        return self.nms.annotations(anns)
 
     # -- decoding ------------------------------------------------------------------------
     def __call__(self, fields, initial_annotations=None):
@@ -148,7 +167,7 @@ class CifCaf(Generator):
         if dropped:
             for i, rec in zip(dropped, b.work_records(0, dropped)):
                 initial[i].update_from_record(rec)
-        return out
+        return self._host_nms(out)
 
     def decode_records(self, cif_batch, caf_batch, keep_cifhr=False, compact=None):
         """Device decode of a batch -> (packed records, per-image offsets, buffers): full
@@ -170,8 +189,8 @@ class CifCaf(Generator):
         """Full or compact records + per-image offsets -> one list of Annotation per image."""
         out = []
         for i in range(len(offsets) - 1):
-            out.append([Annotation.from_any(r, self.keypoints, self.out_skeleton)
-                        for r in recs[offsets[i]:offsets[i + 1]]])
+            out.append(self._host_nms([Annotation.from_any(r, self.keypoints, self.out_skeleton)
+                                       for r in recs[offsets[i]:offsets[i + 1]]]))
         return out
 
     def decode_heads(self, heads, *, group=None, dst=0, local=False):

@@ -660,7 +660,10 @@ static void grow(const dec_t *d, pp_ann *a, int reverse_match) {
             if (a->data[end_][2] > 0.0f) continue;                                            \
             if (in_frontier[(start_i)][end_]) continue;                                       \
             fentry x_;                                                                        \
-            x_.neg = -sqrtf(a->data[(start_i)][2]);                                           \
+            /* max_possible_score *= confidence_scales[caf_i] (cifcaf.py:258-260) */         \
+            x_.neg = d->cfg->confidence_scales                                                \
+                         ? -(sqrtf(a->data[(start_i)][2]) * d->cfg->confidence_scales[b_->caf[e_]]) \
+                         : -sqrtf(a->data[(start_i)][2]);                                     \
             x_.eval = 0;                                                                      \
             x_.j = (start_i);                                                                 \
             x_.k = end_;                                                                      \
@@ -695,6 +698,13 @@ static void grow(const dec_t *d, pp_ann *a, int reverse_match) {
             if (nx[3] == 0.0f) continue;
             fentry ev;
             ev.neg = -nx[3];
+            if (d->cfg->confidence_scales && !d->cfg->greedy) { /* cifcaf.py:282-284 */
+                const by_source_t *b = &d->bs[en.j];
+                int caf = 0;
+                for (int e = 0; e < b->n; e++)
+                    if (b->k[e] == en.k) caf = b->caf[e];
+                ev.neg = -(nx[3] * d->cfg->confidence_scales[caf]);
+            }
             ev.eval = 1;
             memcpy(ev.xysv, nx, sizeof(nx));
             ev.j = en.j;

@@ -25,6 +25,8 @@ Fixtures:
   api_initial_<mode>.npz  CifCaf.__call__(fields, initial_annotations) (cifcaf.py:95-98):
                        the initial annotations, the output list and which outputs are them
   api_seedmask_<mode>.npz  CifCaf with FieldConfig(seed_mask=...) (cif_seeds.py:28-29)
+  api_confscales_<case>.npz  CifCaf(confidence_scales=...) decodes (cifcaf.py:259-260,
+                       282-284): the weights, inputs by generator parameters, annotations
   api_stages.npz       CifSeeds.fill_cif min_scale / seed_mask and two heads, CafScored
                        fill_caf distance masks and two calls, CifHr fill_cif min_scale,
                        fill_multiple over three heads and into an existing map
@@ -697,6 +699,40 @@ def gen_api(op):
     CifSeeds.threshold = None
 
 
+# (name, generator, H, W, seed, mode, skeleton name, n_people, confidence_scales)
+CONFSCALE_CASES = [
+    ('p40_eval', 'planted', 40, 40, 6, 'eval', 'coco', 8,
+     [0.5 + 0.37 * (i % 5) for i in range(19)]),
+    ('u20_eval', 'uniform', 20, 20, 3, 'eval', 'coco', 8,
+     [0.01 if i % 3 == 0 else 1.0 + 0.1 * i for i in range(19)]),
+    # the dense-coupling weights factory.py:184-188 stores on the FieldConfig
+    ('dense_p80_eval', 'planted', 80, 80, 7, 'eval', 'dense', 8, [1.0] * 19 + [0.01] * 25),
+]
+
+
+def gen_confscales(op):
+    """CifCaf(confidence_scales=...) through the whole decode: the weights scale the
+    frontier priorities of the seed loop's and force-complete's _grow."""
+    from openpifpaf import decoder  # pylint: disable=import-outside-toplevel
+    for name, gen, h, w, seed, mode, skel_name, n_people, scales in CONFSCALE_CASES:
+        skeleton = list(SKELETONS[skel_name])
+        configure(decoder, mode, {})
+        cif, caf = make_inputs(gen, h, w, seed, skeleton, {'n_people': n_people})
+        dec = decoder.CifCaf(decoder.FieldConfig(), keypoints=constants.COCO_KEYPOINTS,
+                             skeleton=skeleton, out_skeleton=constants.COCO_PERSON_SKELETON,
+                             confidence_scales=scales)
+        anns = dec([cif, caf])
+        out = {'generator': np.array(gen), 'H': h, 'W': w, 'seed': seed, 'mode': np.array(mode),
+               'skeleton': np.asarray(skeleton, np.int32), 'n_people': n_people,
+               'confidence_scales': np.array(scales, np.float64),
+               'connection_method': np.array('blend'), 'greedy': 0,
+               'input_sha': np.array(sha(cif, caf))}
+        out.update(ann_arrays(anns, len(skeleton)))
+        np.savez_compressed(os.path.join(HERE, 'api_confscales_%s.npz' % name), **out)
+        print('api confidence_scales', name, len(anns))
+    decoder.CifSeeds.threshold = None
+
+
 def main():
     op = ref_loader.load()
     import Cython  # pylint: disable=import-outside-toplevel
@@ -727,6 +763,10 @@ def main():
         return
     if only == ['api']:
         gen_api(op)
+        gen_confscales(op)
+        return
+    if only == ['confscales']:
+        gen_confscales(op)
         return
     if only == ['det']:
         gen_det(op)
@@ -741,6 +781,7 @@ def main():
     gen_inverse(op)
     gen_multi(op)
     gen_api(op)
+    gen_confscales(op)
     for case in CASES:
         if only and case[0] not in only:
             continue

@@ -99,6 +99,19 @@ def case_config(g):
     return make_config(**kw)
 
 
+def confscale_config(g):
+    """case_config plus an api_confscales fixture's CifCaf(confidence_scales=...)."""
+    cfg = case_config(g)
+    scales = [float(v) for v in g['confidence_scales']]
+    out = make_config(**dict(EVAL_CONFIG if str(g['mode']) == 'eval' else PREDICT_CONFIG,
+                             confidence_scales=scales))
+    assert bytes(memoryview(out))[:-8] == bytes(memoryview(cfg))[:-8]  # only the weights differ
+    return out
+
+
+CONFSCALE_NAMES = ('p40_eval', 'u20_eval', 'dense_p80_eval')
+
+
 def configure_decoder(dec, g):
     """Decoder class attributes of a fixture's mode (what decoder.configure() writes)."""
     mode = str(g['mode'])

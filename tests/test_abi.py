@@ -41,7 +41,10 @@ def test_version_and_defaults(lib):
     cfg = _abi.PPConfig()
     lib.pp_default_config(ctypes.byref(cfg))
     ref = _abi.make_config()
-    for name, _ in _abi.PPConfig._fields_:
+    for name, typ in _abi.PPConfig._fields_:
+        if issubclass(typ, ctypes._Pointer):  # confidence_scales: NULL in both
+            assert not getattr(cfg, name) and not getattr(ref, name), name
+            continue
         assert getattr(cfg, name) == pytest.approx(getattr(ref, name)), name
 
 

@@ -84,9 +84,52 @@ def test_unsupported_configurations_raise():
                              caf_min_distances=[0.0, 36.0], caf_max_distances=[None, None])
     with pytest.raises(NotImplementedError):
         fc.single_scale()
-    with pytest.raises(NotImplementedError):
-        decoder.CifCaf(decoder.FieldConfig(), keypoints=['a'], skeleton=[(1, 1)],
+    with pytest.raises(IndexError):  # one weight per CAF (cifcaf.py:260, 284)
+        decoder.CifCaf(decoder.FieldConfig(), keypoints=['a', 'b'], skeleton=[(1, 2), (2, 1)],
                        confidence_scales=[1.0])
+    cc = decoder.CifCaf(decoder.FieldConfig(), keypoints=['a', 'b'], skeleton=[(1, 2)],
+                        confidence_scales=[0.1])
+    assert cc.confidence_scales == [0.1]
+    cfg = make_config(confidence_scales=cc.confidence_scales)
+    assert cfg.confidence_scales[0] == np.float32(0.1)
+    assert not make_config().confidence_scales
+    with pytest.raises(TypeError):  # cifcaf.py:117-118 calls nms.annotations
+        decoder.CifCaf(decoder.FieldConfig(), keypoints=['a'], skeleton=[(1, 1)], nms=object())
+
+
+def test_nms_objects_choose_device_or_host():
+    """nms.Keypoints runs inside the device decode (pp_config.apply_nms); another object
+    with annotations() runs on the host over the unsuppressed device list."""
+    from openpifpaf_amd import decoder
+
+    class Top2:
+        def annotations(self, anns):
+            return sorted(anns, key=lambda a: -a.score())[:2]
+
+    class Sub(decoder.nms.Keypoints):
+        instance_threshold = 0.25
+
+    class Own(decoder.nms.Keypoints):
+        def annotations(self, anns):
+            return anns[:1]
+
+    kw = dict(keypoints=['a', 'b'], skeleton=[(1, 2)])
+    old = decoder.CifSeeds.threshold
+    decoder.CifSeeds.threshold = 0.2
+    try:
+        dev = decoder.CifCaf(decoder.FieldConfig(), **kw)
+        assert dev._device_nms() and dev.config().apply_nms == 1
+        sub = decoder.CifCaf(decoder.FieldConfig(), nms=Sub(), **kw)
+        assert sub._device_nms() and sub.config().nms_instance_threshold == np.float32(0.25)
+        for nms in (Top2(), Own()):
+            host = decoder.CifCaf(decoder.FieldConfig(), nms=nms, **kw)
+            assert not host._device_nms() and host.config().apply_nms == 0
+            stubs = [argparse.Namespace(score=lambda v=v: v) for v in (0.3, 0.9, 0.5)]
+            assert host._host_nms(stubs) == nms.annotations(stubs)
+        off = decoder.CifCaf(decoder.FieldConfig(), nms=None, **kw)
+        assert off.config().apply_nms == 0 and off._host_nms([3, 1]) == [3, 1]
+    finally:
+        decoder.CifSeeds.threshold = old
 
 
 def test_generators_deterministic():

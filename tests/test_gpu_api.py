@@ -204,3 +204,77 @@ def test_seed_mask_decode_vs_reference(dec, mode):
     anns = cc([cif, caf])
     errs = gu.compare_annotations(g, gu.annotations_as_records(anns))
     assert not errs, errs[:10]
+
+
+@pytest.mark.parametrize('name', gu.CONFSCALE_NAMES)
+def test_confidence_scales_decode_vs_reference(dec, name):
+    """CifCaf(confidence_scales=...) (cifcaf.py:259-260, 282-284): the per-CAF weights on
+    the frontier priorities of every _grow (seed loop and force-complete), through the
+    whole device decode, against the reference (tests/golden/api_confscales_*.npz) and
+    bit-exact against the oracle."""
+    g = gu.load_api('confscales_' + name)
+    cif, caf, skeleton = gu.case_inputs(g)
+    gu.configure_decoder(dec, g)
+    cc = dec.CifCaf(dec.FieldConfig(), keypoints=gu.constants.COCO_KEYPOINTS,
+                    skeleton=skeleton, out_skeleton=SKEL,
+                    confidence_scales=[float(v) for v in g['confidence_scales']])
+    got = gu.annotations_as_records(cc([cif, caf]))
+    errs = gu.compare_annotations(g, got)
+    assert not errs, errs[:10]
+    ref = oracle.decode(cif, caf, skeleton, gu.confscale_config(g))
+    for field in ('data', 'joint_scales', 'decoding_pairs', 'decoding_xyv', 'frontier_pairs'):
+        assert got[field].tobytes() == ref[field].tobytes(), field
+
+
+@pytest.mark.parametrize('n_img', [6, 136])
+def test_confidence_scales_batch_vs_oracle(n_img):
+    """The weights on a batch: 6 images (seed_loop_ext_kernel) and 136 (the one-CU
+    seed_loop_kernel), every image's records byte-equal to the oracle's."""
+    import torch
+    from openpifpaf_amd import synthetic
+    from openpifpaf_amd._abi import EVAL_CONFIG, make_config
+    from openpifpaf_amd.engine import DecodeEngine
+    scales = [0.5 + 0.37 * (i % 5) for i in range(len(SKEL))]
+    cfg = make_config(**dict(EVAL_CONFIG, confidence_scales=scales))
+    cif, caf = synthetic.batch('planted', n_img, 40, 40, first_seed=70)
+    recs, offs, _ = DecodeEngine().decode(torch.from_numpy(cif).cuda(),
+                                          torch.from_numpy(caf).cuda(), SKEL, cfg)
+    for i in range(n_img):
+        ref = oracle.decode(cif[i], caf[i], SKEL, cfg)
+        got = recs[offs[i]:offs[i + 1]]
+        assert len(got) == len(ref), i
+        for field in ('data', 'joint_scales', 'n_decoding', 'decoding_pairs', 'decoding_xyv',
+                      'n_frontier', 'frontier_pairs'):
+            assert got[field].tobytes() == ref[field].tobytes(), (i, field)
+
+
+def test_custom_nms_runs_on_host(dec):
+    """An NMS object other than nms.Keypoints (cifcaf.py:117-118): the device decodes
+    without suppression and the object's annotations() gets each image's list; the result
+    equals the nms=None decode passed through the same object, and nms=None matches the
+    oracle with apply_nms off."""
+    from openpifpaf_amd._abi import EVAL_CONFIG, make_config
+
+    class KeepStrong:
+        def __init__(self):
+            self.calls = 0
+
+        def annotations(self, anns):
+            self.calls += 1
+            return [a for a in anns if a.score() > 0.2][::-1]
+
+    cif, caf = gu.synthetic.planted(40, 40, n_people=8, seed=5)
+    gu.configure_decoder(dec, _mode_fixture('eval'))
+    kw = dict(keypoints=gu.constants.COCO_KEYPOINTS, skeleton=SKEL)
+    nms = KeepStrong()
+    got = dec.CifCaf(dec.FieldConfig(), nms=nms, **kw)([cif, caf])
+    assert nms.calls == 1
+    plain = dec.CifCaf(dec.FieldConfig(), nms=None, **kw)([cif, caf])
+    ref = oracle.decode(cif, caf, SKEL, make_config(**dict(EVAL_CONFIG, apply_nms=False)))
+    mine = gu.annotations_as_records(plain)
+    assert len(mine) == len(ref)
+    for field in ('data', 'joint_scales', 'decoding_pairs', 'decoding_xyv', 'frontier_pairs'):
+        assert mine[field].tobytes() == ref[field].tobytes(), field
+    want = KeepStrong().annotations(plain)
+    assert 0 < len(got) < len(plain)
+    assert gu.annotations_as_records(got).tobytes() == gu.annotations_as_records(want).tobytes()

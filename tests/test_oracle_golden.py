@@ -135,6 +135,17 @@ def test_decode(name):
     assert not errs, errs[:10]
 
 
+@pytest.mark.parametrize('name', gu.CONFSCALE_NAMES)
+def test_oracle_confidence_scales(name):
+    """CifCaf(confidence_scales=...) (cifcaf.py:259-260, 282-284) against the reference;
+    the same decode without the weights differs from the fixture (the case exercises them)."""
+    g = gu.load_api('confscales_' + name)
+    cif, caf, skeleton = gu.case_inputs(g)
+    errs = gu.compare_annotations(g, oracle.decode(cif, caf, skeleton, gu.confscale_config(g)))
+    assert not errs, errs[:10]
+    assert gu.compare_annotations(g, oracle.decode(cif, caf, skeleton, gu.case_config(g)))
+
+
 # ---- standalone keypoint NMS (nms.py:17-57) ----------------------------------------------
 
 NMS_NAMES = ('eval', 'predict', 'supp', 'dense', 'zeros')
