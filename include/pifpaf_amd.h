@@ -575,6 +575,45 @@ int pp_center_filter(const float *d_field, int64_t rows, int64_t n, int64_t pitc
 int pp_grow_connection(const float *d_cols, int64_t n, int64_t pitch, float x, float y,
                        float xy_scale, int32_t method, float *d_out, void *stream);
 
+/* ---------------------------------------------------------------------------------
+ * Host twins of the functional.pyx primitives above (SURVEY.md §8(b) `_cpu` variants):
+ * the same arguments as the device entry points minus the stream, HOST pointers, run
+ * sequentially on the calling thread in the reference's loop order (functional.pyx is
+ * CPU-only Cython), bit-exact with it and with the kernels.  Explicit entry points only:
+ * nothing in the library or its Python API falls back to them.
+ * --------------------------------------------------------------------------------- */
+int pp_scalar_square_add_gauss_with_max_cpu(float *field, int64_t h, int64_t w, int64_t pitch,
+                                            const float *x, const float *y, const float *sigma,
+                                            const float *v, int64_t n, float truncate,
+                                            float max_value);
+int pp_scalar_square_add_gauss_cpu(float *field, int64_t h, int64_t w, int64_t pitch,
+                                   const float *x, const float *y, const float *sigma,
+                                   const float *v, int64_t n, float truncate);
+int pp_scalar_square_max_gauss_cpu(float *field, int64_t h, int64_t w, int64_t pitch,
+                                   const float *x, const float *y, const float *sigma,
+                                   const float *v, int64_t n, float truncate);
+int pp_scalar_square_add_constant_cpu(float *field, int64_t h, int64_t w, int64_t pitch,
+                                      const float *x, const float *y, const float *width,
+                                      const float *v, int64_t n);
+int pp_cumulative_average_cpu(float *cuma, float *cumw, int64_t h, int64_t w, int64_t pitch,
+                              const float *x, const float *y, const float *width,
+                              const float *v, const float *w_, int64_t n);
+/* out_steps (optional, 1 int64) = iterations run */
+int pp_weiszfeld_nd_cpu(const float *x, int64_t n, int64_t d, int64_t x_pitch, float *y,
+                        const float *weights, float epsilon, int64_t max_steps, float *denom,
+                        int64_t *out_steps);
+int pp_scalar_values_cpu(const float *field, int64_t h, int64_t w, int64_t pitch, const float *x,
+                         const float *y, int64_t n, float default_value, float *out);
+int pp_scalar_lookup_cpu(const void *field, int64_t h, int64_t w, int64_t pitch, int32_t mode,
+                         const float *x, const float *y, int64_t n, float default_value,
+                         float reduction, void *out);
+int pp_occupancy_set_cpu(uint8_t *occ, int32_t n_planes, int64_t h, int64_t w, int64_t pitch,
+                         const int32_t *f, const float *x, const float *y, const float *sigma,
+                         int64_t n, float reduction, float min_scale_reduced);
+int pp_center_filter_cpu(const float *field, int64_t rows, int64_t n, int64_t pitch, int32_t mode,
+                         float x, float y, float sigma, void *out, int64_t out_pitch,
+                         int32_t *count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -97,6 +97,26 @@ _SIGNATURES = {
                          ctypes.c_int),
     'pp_center_filter': ([_vp, _i64, _i64, _i64, _i32, _f, _f, _f, _vp, _i64, _vp, _vp],
                          ctypes.c_int),
+    # host twins of the functional primitives (csrc/functional_cpu.hip): host pointers
+    'pp_scalar_square_add_gauss_with_max_cpu': ([_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp,
+                                                 _i64, _f, _f], ctypes.c_int),
+    'pp_scalar_square_add_gauss_cpu': ([_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _f],
+                                       ctypes.c_int),
+    'pp_scalar_square_max_gauss_cpu': ([_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _f],
+                                       ctypes.c_int),
+    'pp_scalar_square_add_constant_cpu': ([_vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64],
+                                          ctypes.c_int),
+    'pp_cumulative_average_cpu': ([_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _i64],
+                                  ctypes.c_int),
+    'pp_weiszfeld_nd_cpu': ([_vp, _i64, _i64, _i64, _vp, _vp, _f, _i64, _vp, _vp],
+                            ctypes.c_int),
+    'pp_scalar_values_cpu': ([_vp, _i64, _i64, _i64, _vp, _vp, _i64, _f, _vp], ctypes.c_int),
+    'pp_scalar_lookup_cpu': ([_vp, _i64, _i64, _i64, _i32, _vp, _vp, _i64, _f, _f, _vp],
+                             ctypes.c_int),
+    'pp_occupancy_set_cpu': ([_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _f, _f],
+                             ctypes.c_int),
+    'pp_center_filter_cpu': ([_vp, _i64, _i64, _i64, _i32, _f, _f, _f, _vp, _i64, _vp],
+                             ctypes.c_int),
 }
 
 EXPORTED = tuple(_SIGNATURES)

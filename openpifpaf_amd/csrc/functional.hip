@@ -19,7 +19,7 @@ __global__ __launch_bounds__(256) void scalar_values_kernel(const float *__restr
 }
 
 // mode: 0 scalar_value, 1 scalar_value_clipped, 2 scalar_nonzero, 3 scalar_nonzero_clipped,
-//       4 scalar_nonzero_clipped_with_reduction
+//       4 scalar_nonzero_clipped_with_reduction (lookup_at, pp_common.hpp)
 __global__ __launch_bounds__(256) void scalar_lookup_kernel(const void *field, int h, int w,
                                                             int64_t pitch, int mode,
                                                             const float *__restrict__ xs,
@@ -28,29 +28,7 @@ __global__ __launch_bounds__(256) void scalar_lookup_kernel(const void *field, i
                                                             void *out) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    float x = xs[i], y = ys[i];
-    const float maxx = (float)(w - 1), maxy = (float)(h - 1);
-    if (mode == 0 || mode == 2) {
-        const bool oob = x < 0.0f || y < 0.0f || x > maxx || y > maxy || x != x || y != y;
-        if (mode == 0) {
-            ((float *)out)[i] = oob ? dflt : ((const float *)field)[(int64_t)(int)y * pitch + (int)x];
-        } else {
-            ((uint8_t *)out)[i] =
-                oob ? (uint8_t)(int)dflt : ((const uint8_t *)field)[(int64_t)(int)y * pitch + (int)x];
-        }
-        return;
-    }
-    if (mode == 4) {
-        x = x / r;
-        y = y / r;
-    }
-    x = clip_ref(x, 0.0f, maxx);
-    y = clip_ref(y, 0.0f, maxy);
-    const int64_t at = (int64_t)(int)y * pitch + (int)x;
-    if (mode == 1)
-        ((float *)out)[i] = ((const float *)field)[at];
-    else
-        ((uint8_t *)out)[i] = ((const uint8_t *)field)[at];
+    lookup_at(field, h, w, pitch, mode, xs[i], ys[i], dflt, r, out, i);
 }
 
 // one workgroup, 1024 threads: order-preserving compaction of the kept columns
@@ -61,19 +39,11 @@ __global__ __launch_bounds__(1024) void center_filter_kernel(const float *__rest
                                                              int *count) {
     __shared__ int s_tmp[16];
     int64_t running = 0;
-    const float lo_x = x - sigma, hi_x = x + sigma, lo_y = y - sigma, hi_y = y + sigma;
     for (int64_t base = 0; base < n; base += 1024) {
         const int64_t i = base + threadIdx.x;
         bool take = false;
         if (i < n) {
-            const float r1 = f[pitch + i], r2 = f[2 * pitch + i];
-            if (mode == 0 || mode == 1) {
-                take = !(r1 < lo_x) && !(r1 > hi_x) && !(r2 < lo_y) && !(r2 > hi_y);
-            } else {
-                const float r3 = f[3 * pitch + i];
-                take = r1 > x - sigma * r3 && r1 < x + sigma * r3 && r2 > y - sigma * r3 &&
-                       r2 < y + sigma * r3;
-            }
+            take = center_take(f, pitch, i, mode, x, y, sigma);
             if (mode == 3) ((uint8_t *)out)[i] = take ? 1 : 0;
         }
         int total;
@@ -92,25 +62,7 @@ __global__ void weiszfeld_kernel(const float *__restrict__ x, int64_t n, int64_t
                                  float *y, const float *__restrict__ wts, float eps,
                                  int64_t max_steps, float *denom) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    float prev0, prev1;
-    for (int64_t s = 0; s < max_steps; s++) {
-        prev0 = y[0];
-        prev1 = y[1];
-        for (int64_t i = 0; i < n; i++) {
-            const float ax = x[i * xp] - prev0, ay = x[i * xp + 1] - prev1;
-            denom[i] = (float)(sqrt((double)(ax * ax + ay * ay)) + (double)eps);
-        }
-        float top0 = 0.0f, top1 = 0.0f, bottom = 0.0f;
-        for (int64_t j = 0; j < n; j++) {
-            const float w = wts[j];
-            top0 += (w * x[j * xp + 0]) / denom[j];  // weights_x[j, 0] / denom[j]
-            top1 += (w * x[j * xp + 1]) / denom[j];
-            bottom = bottom + w / denom[j];
-        }
-        y[0] = top0 / bottom;
-        y[1] = top1 / bottom;
-        if (fabs((double)(y[0] - prev0)) + fabs((double)(y[1] - prev1)) < 1e-2) return;
-    }
+    weiszfeld_run(x, n, xp, y, wts, eps, max_steps, denom);
 }
 
 }  // namespace pp
@@ -126,23 +78,12 @@ __global__ __launch_bounds__(256) void occupancy_set_kernel(uint8_t *occ, int n_
                                                             const float *ys, const float *sig,
                                                             int64_t n, float r, float msr) {
     for (int64_t i = 0; i < n; i++) {
-        const int f = fs[i];
-        const float x = xs[i], y = ys[i], s = sig[i];
-        // round(x / reduction) etc.: float32 scalar division (NEP 50), half-to-even rounding;
-        // Python's max(min_scale_reduced, s) keeps the first argument unless s is larger
-        const float xr = x / r, yr = y / r, sr = s / r;
-        const float sm = sr > msr ? sr : msr;
-        const bool ok = f >= 0 && f < n_planes && fabsf(xr) < 0x1p60f && fabsf(yr) < 0x1p60f &&
-                        fabsf(sm) < 0x1p60f;  // NaN / inf: the reference's round() raises
-        if (ok) {
-            const int64_t xi = (int64_t)rintf(xr), yi = (int64_t)rintf(yr), si = (int64_t)rintf(sm);
-            const int64_t minx = max((int64_t)0, xi - si), miny = max((int64_t)0, yi - si);
-            const int64_t maxx = min(max(minx + 1, min(w, xi + si + 1)), w);
-            const int64_t maxy = min(max(miny + 1, min(h, yi + si + 1)), h);
-            const int64_t bw = maxx - minx, cells = bw > 0 && maxy > miny ? bw * (maxy - miny) : 0;
-            uint8_t *plane = occ + (int64_t)f * h * pitch;
+        int64_t x0, x1, y0, y1;
+        if (occupancy_mark_box(fs[i], n_planes, h, w, xs[i], ys[i], sig[i], r, msr, x0, x1, y0, y1)) {
+            const int64_t bw = x1 - x0, cells = bw * (y1 - y0);
+            uint8_t *plane = occ + (int64_t)fs[i] * h * pitch;
             for (int64_t c = threadIdx.x; c < cells; c += 256) {
-                uint8_t *p = plane + (miny + c / bw) * pitch + minx + c % bw;
+                uint8_t *p = plane + (y0 + c / bw) * pitch + x0 + c % bw;
                 *p = (uint8_t)(*p + 1);
             }
         }

@@ -34,13 +34,13 @@ constexpr int kMaxHrSide = 32768;
 
 // functional.pyx:67-68 clip(): fmax(minv, fmin(maxv, v)); the double round trip of the
 // generated C is exact for float inputs, and NaN behaves the same (fmin/fmax drop NaN).
-__device__ __forceinline__ float clip_ref(float v, float minv, float maxv) {
+__host__ __device__ __forceinline__ float clip_ref(float v, float minv, float maxv) {
     return fmaxf(minv, fminf(maxv, v));
 }
 
 // functional.pyx:57-64 approx_exp.  (float)(1.0 + (double)x / 8.0) == fl32(1 + x*0.125f):
 // x/8 is exact and double rounding of a single add is innocuous (53 >= 2*24+2).
-__device__ __forceinline__ float approx_exp_ref(float x) {
+__host__ __device__ __forceinline__ float approx_exp_ref(float x) {
     if (x > 2.0f || x < -2.0f) return 0.0f;
     x = 1.0f + x * 0.125f;
     x = x * x;
@@ -50,12 +50,105 @@ __device__ __forceinline__ float approx_exp_ref(float x) {
 }
 
 // functional.pyx:231-244 scalar_values for one point (bounds inclusive of W'-1, truncation)
-__device__ __forceinline__ float hr_lookup(const float *field, int hh, int ww, int64_t pitch,
-                                           float x, float y, float dflt) {
+__host__ __device__ __forceinline__ float hr_lookup(const float *field, int hh, int ww,
+                                                    int64_t pitch, float x, float y, float dflt) {
     const float maxx = (float)ww - 1.0f, maxy = (float)hh - 1.0f;
     if (x < 0.0f || y < 0.0f || x > maxx || y > maxy) return dflt;
     if (x != x || y != y) return dflt;  // NaN: the reference indexes with (Py_ssize_t)NaN (UB)
     return field[(int64_t)(int)y * pitch + (int)x];
+}
+
+// The functional.pyx primitives' per-element bodies, shared by the gfx950 kernels
+// (functional.hip) and their host twins (functional_cpu.hip).
+
+// functional.pyx:247-286 point lookup i into out[i]; mode: 0 scalar_value, 1
+// scalar_value_clipped (float field), 2 scalar_nonzero, 3 scalar_nonzero_clipped,
+// 4 scalar_nonzero_clipped_with_reduction (u8 field)
+__host__ __device__ __forceinline__ void lookup_at(const void *field, int h, int w, int64_t pitch,
+                                                   int mode, float x, float y, float dflt, float r,
+                                                   void *out, int64_t i) {
+    const float maxx = (float)(w - 1), maxy = (float)(h - 1);
+    if (mode == 0 || mode == 2) {
+        const bool oob = x < 0.0f || y < 0.0f || x > maxx || y > maxy || x != x || y != y;
+        if (mode == 0)
+            ((float *)out)[i] = oob ? dflt : ((const float *)field)[(int64_t)(int)y * pitch + (int)x];
+        else
+            ((uint8_t *)out)[i] =
+                oob ? (uint8_t)(int)dflt : ((const uint8_t *)field)[(int64_t)(int)y * pitch + (int)x];
+        return;
+    }
+    if (mode == 4) {
+        x = x / r;
+        y = y / r;
+    }
+    x = clip_ref(x, 0.0f, maxx);
+    y = clip_ref(y, 0.0f, maxy);
+    const int64_t at = (int64_t)(int)y * pitch + (int)x;
+    if (mode == 1)
+        ((float *)out)[i] = ((const float *)field)[at];
+    else
+        ((uint8_t *)out)[i] = ((const uint8_t *)field)[at];
+}
+
+// column i of a (rows, n) field passes the filter (functional.pyx:214-228 paf_mask_center
+// (3), 289-310 paf_center_b (2), 313-335 paf_center (1), 338-359 caf_center_s (0))
+__host__ __device__ __forceinline__ bool center_take(const float *f, int64_t pitch, int64_t i,
+                                                     int mode, float x, float y, float sigma) {
+    const float r1 = f[pitch + i], r2 = f[2 * pitch + i];
+    if (mode == 0 || mode == 1)
+        return !(r1 < x - sigma) && !(r1 > x + sigma) && !(r2 < y - sigma) && !(r2 > y + sigma);
+    const float r3 = f[3 * pitch + i];
+    return r1 > x - sigma * r3 && r1 < x + sigma * r3 && r2 > y - sigma * r3 &&
+           r2 < y + sigma * r3;
+}
+
+// functional.pyx:172-211, sequential sums in the reference's order; returns the steps run
+__host__ __device__ inline int64_t weiszfeld_run(const float *x, int64_t n, int64_t xp, float *y,
+                                                 const float *wts, float eps, int64_t max_steps,
+                                                 float *denom) {
+    for (int64_t s = 0; s < max_steps; s++) {
+        const float prev0 = y[0], prev1 = y[1];
+        for (int64_t i = 0; i < n; i++) {
+            const float ax = x[i * xp] - prev0, ay = x[i * xp + 1] - prev1;
+            denom[i] = (float)(sqrt((double)(ax * ax + ay * ay)) + (double)eps);
+        }
+        float top0 = 0.0f, top1 = 0.0f, bottom = 0.0f;
+        for (int64_t j = 0; j < n; j++) {
+            const float w = wts[j];
+            top0 += (w * x[j * xp + 0]) / denom[j];  // weights_x[j, 0] / denom[j]
+            top1 += (w * x[j * xp + 1]) / denom[j];
+            bottom = bottom + w / denom[j];
+        }
+        y[0] = top0 / bottom;
+        y[1] = top1 / bottom;
+        if (fabs((double)(y[0] - prev0)) + fabs((double)(y[1] - prev1)) < 1e-2) return s + 1;
+    }
+    return max_steps > 0 ? max_steps : 0;
+}
+
+// Occupancy.set (occupancy.py:36-44) + scalar_square_add_single (decoder/utils.py:61-66):
+// the box [x0, x1) x [y0, y1) of one mark, false when the reference marks nothing.
+// round(x / reduction) etc.: float32 scalar division (NEP 50), half-to-even rounding;
+// Python's max(min_scale_reduced, s) keeps the first argument unless s is larger
+__host__ __device__ __forceinline__ bool occupancy_mark_box(int f, int n_planes, int64_t h,
+                                                            int64_t w, float x, float y, float s,
+                                                            float r, float msr, int64_t &x0,
+                                                            int64_t &x1, int64_t &y0,
+                                                            int64_t &y1) {
+    const float xr = x / r, yr = y / r, sr = s / r;
+    const float sm = sr > msr ? sr : msr;
+    const bool ok = f >= 0 && f < n_planes && fabsf(xr) < 0x1p60f && fabsf(yr) < 0x1p60f &&
+                    fabsf(sm) < 0x1p60f;  // NaN / inf: the reference's round() raises
+    if (!ok) return false;
+    const int64_t xi = (int64_t)rintf(xr), yi = (int64_t)rintf(yr), si = (int64_t)rintf(sm);
+    x0 = xi - si > 0 ? xi - si : 0;
+    y0 = yi - si > 0 ? yi - si : 0;
+    const int64_t hx = xi + si + 1 < w ? xi + si + 1 : w, hy = yi + si + 1 < h ? yi + si + 1 : h;
+    x1 = x0 + 1 > hx ? x0 + 1 : hx;
+    y1 = y0 + 1 > hy ? y0 + 1 : hy;
+    x1 = x1 < w ? x1 : w;
+    y1 = y1 < h ? y1 : h;
+    return x1 > x0 && y1 > y0;
 }
 
 // The CifHr map as the decode stages read it: dense row-major (n_img * K, hh, pitch) — the
