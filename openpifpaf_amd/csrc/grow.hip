@@ -779,7 +779,7 @@ __device__ __forceinline__ bool frontier_pop(Frontier &F, Entry &e) {
 }
 
 // add_to_frontier (cifcaf.py:251-263): the start joint's slots in dict order, one pass
-template <typename LDS>
+template <bool CS, typename LDS>
 __device__ __forceinline__ void add_to_frontier(const GrowArgs &g, LDS &L, Frontier &F, float av, int start,
                                 float start_v, int &nfr, uint64_t added[2]) {
     const int lane = threadIdx.x & 63;
@@ -794,7 +794,7 @@ __device__ __forceinline__ void add_to_frontier(const GrowArgs &g, LDS &L, Front
         if (elig) {
             F.st[r] = 1;
             // max_possible_score *= confidence_scales[caf_i] (cifcaf.py:258-261)
-            F.neg[r] = g.has_cs ? -(sqrtf(start_v) * g.slot_cs[d]) : neg;
+            F.neg[r] = CS ? -(sqrtf(start_v) * g.slot_cs[d]) : neg;
             F.added[r] = 1;
             const int t = nfr + lane_prefix(m);
             if (t < PP_MAX_FRONTIER) {
@@ -1211,7 +1211,7 @@ __device__ __forceinline__ void eval_ahead_raw(const GrowArgs &g, Frontier &F, i
 // no reverse matching) via eval_ahead_raw.
 // `abort` (a seed-loop helper's speculative grow): stop at the next pop once *abort is set
 // (wave 0 is done: the result would never be read)
-template <bool AHEAD, typename LDS, bool RAW_AHEAD = false>
+template <bool AHEAD, bool CS, typename LDS, bool RAW_AHEAD = false>
 __device__ __forceinline__ void grow(const GrowArgs &g, LDS &L, int img, int set, bool reverse_match,
                                      const ColStage &cs = ColStage{}, int *abort = nullptr) {
     const int lane = threadIdx.x & 63;
@@ -1263,7 +1263,7 @@ __device__ __forceinline__ void grow(const GrowArgs &g, LDS &L, int img, int set
         const float vj = rl_f(av, j);
         if (vj == 0.0f) continue;
         uint64_t added[2];
-        add_to_frontier(g, L, F, av, j, vj, nfr, added);
+        add_to_frontier<CS>(g, L, F, av, j, vj, nfr, added);
         ahead(added);
     }
     for (;;) {
@@ -1305,7 +1305,7 @@ __device__ __forceinline__ void grow(const GrowArgs &g, LDS &L, int img, int set
             if (nx[3] == 0.0f) continue;
             e.eval = 1;
             // score *= confidence_scales[caf_i] (cifcaf.py:282-284; not on the greedy return)
-            e.neg = g.has_cs ? -(nx[3] * g.slot_cs[e.slot]) : -nx[3];
+            e.neg = CS ? -(nx[3] * g.slot_cs[e.slot]) : -nx[3];
             e.x = nx[0];
             e.y = nx[1];
             e.s = nx[2];
@@ -1356,7 +1356,7 @@ __device__ __forceinline__ void grow(const GrowArgs &g, LDS &L, int img, int set
         uint64_t added[2];
         {
             FSTAMP_BEGIN
-            add_to_frontier(g, L, F, av, jti, got.v, nfr, added);
+            add_to_frontier<CS>(g, L, F, av, jti, got.v, nfr, added);
             FSTAMP_END(L, 2)
         }
         ahead(added);
@@ -2095,6 +2095,7 @@ __device__ __forceinline__ void plan_unlock(SeedLoopSharedT<NS> &S) {
 // overlapped step; 4 waves per SIMD (128 VGPRs, 532 spills): 1.37 ms.
 // Grid: n_img image workgroups, then n_ext * n_img external helper workgroups (helper
 // workgroup x of image i is block n_img * (1 + x) + i, on image i's XCD when n_img % 8 == 0).
+template <bool CS>
 __global__ __launch_bounds__(64 * kSeedWaves) __attribute__((amdgpu_waves_per_eu(3)))
 void seed_loop_kernel(GrowArgs g) {
     __shared__ SeedLDS Ls[kSeedWaves];
@@ -2200,7 +2201,7 @@ void seed_loop_kernel(GrowArgs g) {
             if (my < 0) break;
             const int q = S.task_slot[wave];
             ann_from_seed(L, seeds[my], K, img);
-            grow<true>(g, L, img, 0, true, cstage, &S.done);
+            grow<true, CS>(g, L, img, 0, true, cstage, &S.done);
             if (lds_acquire(&S.done)) break;  // nobody reads the cache any more
             copy_ann(&cache[q], &L.a);
             if (lane < kKP)
@@ -2242,7 +2243,7 @@ void seed_loop_kernel(GrowArgs g) {
                 L.a.n_keypoints = K;
             }
             wave_sync();
-            grow<true>(g, L, img, 0, true, cstage);
+            grow<true, CS>(g, L, img, 0, true, cstage);
             commit(&L.a, lane < K ? L.a.data[lane][0] : 0.0f, lane < K ? L.a.data[lane][1] : 0.0f,
                    lane < K ? L.a.data[lane][2] : 0.0f, lane < K ? L.a.joint_scales[lane] : 0.0f);
         }
@@ -2312,7 +2313,7 @@ void seed_loop_kernel(GrowArgs g) {
 #endif
             STAMP(1);
             ann_from_seed(L, st, K, img);
-            grow<true>(g, L, img, 0, true, cstage);
+            grow<true, CS>(g, L, img, 0, true, cstage);
             STAMP(2);
             commit(&L.a, lane < K ? L.a.data[lane][0] : 0.0f, lane < K ? L.a.data[lane][1] : 0.0f,
                    lane < K ? L.a.data[lane][2] : 0.0f, lane < K ? L.a.joint_scales[lane] : 0.0f);
@@ -2348,6 +2349,7 @@ void seed_loop_kernel(GrowArgs g) {
 // The same loop with external helpers (n_ext > 0).  A separate kernel: the big-batch one
 // above carries none of the hand-off state, whose registers cost it 4% per planted cfg3
 // step when merged into it (spills inside the grow).
+template <bool CS>
 __global__ __launch_bounds__(64 * kSeedWaves) __attribute__((amdgpu_waves_per_eu(3)))
 void seed_loop_ext_kernel(GrowArgs g) {
     constexpr int NS = kCacheSlots;
@@ -2487,7 +2489,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
                 my = (int)(v >> 32);
             }
             ann_from_seed(L, seeds[my], K, img);
-            grow<true>(g, L, img, 0, true, cstage, external ? nullptr : &S.done);
+            grow<true, CS>(g, L, img, 0, true, cstage, external ? nullptr : &S.done);
             if (!external && lds_acquire(&S.done)) break;  // nobody reads the cache any more
             if (external) {
                 publish_ann(&xrec[q], &L.a);
@@ -2539,7 +2541,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
                 L.a.n_keypoints = K;
             }
             wave_sync();
-            grow<true>(g, L, img, 0, true, cstage);
+            grow<true, CS>(g, L, img, 0, true, cstage);
             commit(&L.a, false, lane < K ? L.a.data[lane][0] : 0.0f,
                    lane < K ? L.a.data[lane][1] : 0.0f, lane < K ? L.a.data[lane][2] : 0.0f,
                    lane < K ? L.a.joint_scales[lane] : 0.0f);
@@ -2741,7 +2743,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
 #endif
             STAMP(1);
             ann_from_seed(L, st, K, img);
-            grow<true>(g, L, img, 0, true, cstage);
+            grow<true, CS>(g, L, img, 0, true, cstage);
             STAMP(2);
             commit(&L.a, false, lane < K ? L.a.data[lane][0] : 0.0f,
                    lane < K ? L.a.data[lane][1] : 0.0f, lane < K ? L.a.data[lane][2] : 0.0f,
@@ -2786,6 +2788,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
 // set are unchanged by it (their frontier is empty) and are skipped, and images the seed
 // loop did not flag return at once.
 // (5 or 6 waves per SIMD via amdgpu_waves_per_eu: 21 / 46 spills, slower)
+template <bool CS>
 __global__ __launch_bounds__(64) void complete_kernel(GrowArgs g) {
     __shared__ GrowLDS L;
     const int img = blockIdx.x;
@@ -2817,7 +2820,7 @@ __global__ __launch_bounds__(64) void complete_kernel(GrowArgs g) {
         copy_ann(&L.a, &work[i]);
         uint32_t unfilled = 0;
         for (int j = 0; j < K; j++) unfilled |= (L.a.data[j][2] == 0.0f) ? (1u << j) : 0u;
-        grow<false, GrowLDS, kCompleteAhead>(g, L, img, 1, false);
+        grow<false, CS, GrowLDS, kCompleteAhead>(g, L, img, 1, false);
         bool any0 = false;
         for (int j = 0; j < K; j++) {
             float &v = L.a.data[j][2];
@@ -3621,12 +3624,20 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
                 return fail(PP_EHIP, "pp_decode_batch: seed-loop hand-off reset failed");
             const size_t dyn = kColLds * sizeof(float) +
                                (g.n_ext > 0 ? (size_t)kExtCache * kKP * sizeof(float4) : 0);
-            if (g.n_ext > 0)
-                hipLaunchKernelGGL(seed_loop_ext_kernel, dim3(n_img * (1 + g.n_ext)),
-                                   dim3(64 * kSeedWaves), dyn, s, g);
-            else
-                hipLaunchKernelGGL(seed_loop_kernel, dim3(n_img), dim3(64 * kSeedWaves),
-                                   dyn, s, g);
+            // confidence_scales: their own kernel instances (the default ones carry no
+            // registers for them: complete_kernel stays at 128 VGPRs, 4 waves per SIMD)
+            const dim3 blk(64 * kSeedWaves);
+            if (g.n_ext > 0) {
+                const dim3 grid(n_img * (1 + g.n_ext));
+                if (g.has_cs)
+                    hipLaunchKernelGGL(seed_loop_ext_kernel<true>, grid, blk, dyn, s, g);
+                else
+                    hipLaunchKernelGGL(seed_loop_ext_kernel<false>, grid, blk, dyn, s, g);
+            } else if (g.has_cs) {
+                hipLaunchKernelGGL(seed_loop_kernel<true>, dim3(n_img), blk, dyn, s, g);
+            } else {
+                hipLaunchKernelGGL(seed_loop_kernel<false>, dim3(n_img), blk, dyn, s, g);
+            }
             rc = check_launch("pp_decode_batch(seed loop)");
             if (rc) return rc;
         }
@@ -3640,7 +3651,10 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
             if (rc) return rc;
         }
         if (run_complete && cfg->force_complete) {
-            hipLaunchKernelGGL(complete_kernel, dim3(n_img, kCompleteWays), dim3(64), 0, s, g);
+            if (g.has_cs)
+                hipLaunchKernelGGL(complete_kernel<true>, dim3(n_img, kCompleteWays), dim3(64), 0, s, g);
+            else
+                hipLaunchKernelGGL(complete_kernel<false>, dim3(n_img, kCompleteWays), dim3(64), 0, s, g);
             rc = check_launch("pp_decode_batch(force complete)");
             if (rc) return rc;
         }
