@@ -481,6 +481,11 @@ int pp_pack_compact(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img
  * (128: force-complete), then PP_STAGE_AFTER_SEED_LOOP | PP_STAGE_NMS_ONLY (256).  NMS reads
  * only the annotation records and NMS scratch, none of which stages 1-4 write, so the
  * workspace's next stages 1-4 need wait only for the force-complete call.
+ * PP_STAGE_NMS_WIDE (512, a hint for dense batches): NMS in workgroups of 8 waves instead of
+ * 4 when the batch runs the one-CU seed loop (at least about CUs / 2 images).  The 4-wave
+ * form fits on a CU beside a seed-loop workgroup, so an overlapped caller's NMS runs beside
+ * the next batch's seed loop; the 8-wave form is faster per image on dense input
+ * (hundreds of annotations per image).  Same results either way.
  *
  * Workspace contract: bytes [pp_decode_workspace_zero_offset(), end) must be zero before
  * the first call (e.g. hipMemset once at allocation); every call leaves them zero again.
@@ -490,6 +495,7 @@ int pp_pack_compact(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img
 #define PP_STAGE_AFTER_SEED_LOOP 64u
 #define PP_STAGE_COMPLETE_ONLY 128u
 #define PP_STAGE_NMS_ONLY 256u
+#define PP_STAGE_NMS_WIDE 512u
 int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int32_t K,
                      int32_t C, int32_t H, int32_t W, const int32_t *skeleton,
                      const pp_config *cfg, float *d_cifhr, pp_ann *d_anns,

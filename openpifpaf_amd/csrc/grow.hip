@@ -2843,7 +2843,15 @@ __global__ __launch_bounds__(64) void complete_kernel(GrowArgs g) {
 // and keeps the plane's marked boxes in a list instead of a u8 grid.  A joint is
 // "occupied" iff the number of earlier marked boxes covering its cell is non-zero mod 256
 // (the grid's u8 += 1 wraps), which is exactly what the grid lookup returns.
-constexpr int kNmsWaves = 8;
+// Workgroups of kNmsWaves (8) waves for dense batches on the one-CU seed loop
+// (PP_STAGE_NMS_WIDE), else kNmsNarrow (4): at 155 VGPRs a 4-wave workgroup (one wave per
+// SIMD) fits on a CU beside a seed-loop workgroup (two waves per SIMD at 168), an 8-wave one
+// does not, so in the overlapped pipeline the narrow NMS of batch i runs beside batch i + 1's
+// seed loop instead of waiting for its CUs.  A/B on one box: planted cfg3 370-375k ->
+// 385-394k images/s, cfg5 uniform 1356-1365 -> 1434-1443; uniform cfg3 (400 annotations per
+// image, 17 planes on 4 waves) 15.1-15.3k -> 14.4-14.5k, hence the wide form there.
+constexpr int kNmsWaves = 8;   // also the per-image stride of the box-list scratch
+constexpr int kNmsNarrow = 4;
 // boxes per plane kept in REGISTERS, kNmsRegBoxes per lane (box i: lane i % 64, slot
 // i / 64), global scratch beyond: a check is ALU over the lane's slots plus one wave sum,
 // and the kernel needs no LDS for them (it fits beside the seed loop's 104 KB).  With the
@@ -2893,8 +2901,9 @@ __device__ __forceinline__ int occ_cell(const OccGrid &o, int f, float x, float 
     return -1;
 }
 
-__global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
-    __shared__ ScoreLDS Ls[kNmsWaves];
+template <int W>
+__global__ __launch_bounds__(64 * W) void nms_kernel(GrowArgs g) {
+    __shared__ ScoreLDS Ls[W];
     __shared__ int s_m, s_m2, s_status;
     __shared__ float s_mx, s_my;
     const int img = blockIdx.x;
@@ -2929,7 +2938,7 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
     STAMP_DECL
 
     if (!g.cfg.apply_nms) {
-        for (int i = wave; i < n_anns; i += kNmsWaves) {
+        for (int i = wave; i < n_anns; i += W) {
             copy_ann(&out[i], &work[i]);
             const double sc = ann_score_w(L, work[i].data, K);
             if (lane == 0) {
@@ -2946,7 +2955,7 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
     }
 
     // nms.py:20-22: zero joints below keypoint_threshold, drop low scores (per annotation)
-    for (int i = wave; i < n_anns; i += kNmsWaves) {
+    for (int i = wave; i < n_anns; i += W) {
         pp_ann &a = work[i];
         if (lane < K && a.data[lane][2] < kt) {
             a.data[lane][0] = 0.0f;
@@ -3028,7 +3037,7 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
         if (lane < m) wi0 = keep[perm[lane]];
 #pragma unroll
         for (int u = 0; u < kNmsPre; u++) {
-            const int f = wave + u * kNmsWaves;
+            const int f = wave + u * W;
             pre[u][0] = pre[u][1] = pre[u][2] = pre[u][3] = 0.0f;
             if (f < K && lane < m) {
                 pre[u][0] = work[wi0].data[f][0];
@@ -3037,7 +3046,7 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
                 pre[u][3] = work[wi0].joint_scales[f];
             }
         }
-        for (int f = wave, u = 0; f < K; f += kNmsWaves, u++) {  // nms.py:34-45, one plane per pass
+        for (int f = wave, u = 0; f < K; f += W, u++) {  // nms.py:34-45, one plane per pass
             int nbox = 0;
             int2 rb[kNmsRegBoxes];  // (x0 | x1 << 16, y0 | y1 << 16); zero: covers nothing
 #pragma unroll
@@ -3115,7 +3124,7 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
         __syncthreads();
         STAMP(4);
         // nms.py:51-53 in sorted order: zero low joints, drop low scores
-        for (int r = wave; r < m; r += kNmsWaves) {
+        for (int r = wave; r < m; r += W) {
             pp_ann &a = work[keep[perm[r]]];
             if (lane < K && a.data[lane][2] < kt) {
                 a.data[lane][0] = 0.0f;
@@ -3161,7 +3170,7 @@ __global__ __launch_bounds__(64 * kNmsWaves) void nms_kernel(GrowArgs g) {
         __syncthreads();
         STAMP(7);
         n_out = s_m2;
-        for (int r = wave; r < n_out; r += kNmsWaves) {
+        for (int r = wave; r < n_out; r += W) {
             copy_ann(&out[r], &work[surv[perm[r]]]);
             if (lane == 0) {
                 out[r].score = kscore[perm[r]];
@@ -3659,7 +3668,10 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
             if (rc) return rc;
         }
         if (run_nms) {
-            hipLaunchKernelGGL(nms_kernel, dim3(n_img), dim3(64 * kNmsWaves), 0, s, g);
+            if ((stages & PP_STAGE_NMS_WIDE) && g.n_ext == 0)
+                hipLaunchKernelGGL(nms_kernel<kNmsWaves>, dim3(n_img), dim3(64 * kNmsWaves), 0, s, g);
+            else
+                hipLaunchKernelGGL(nms_kernel<kNmsNarrow>, dim3(n_img), dim3(64 * kNmsNarrow), 0, s, g);
             rc = check_launch("pp_decode_batch(nms)");
         }
 #ifdef PP_STAMPS
@@ -3807,7 +3819,7 @@ int pp_nms_keypoints(pp_ann *d_anns, const int32_t *d_counts, int32_t n_img, int
     g.out_idx = d_out_index;
     if (hipMemsetAsync(g.status, 0, (size_t)n_img * sizeof(int), s) != hipSuccess)
         return fail(PP_EHIP, "pp_nms_keypoints: memset failed");
-    hipLaunchKernelGGL(nms_kernel, dim3(n_img), dim3(64 * kNmsWaves), 0, s, g);
+    hipLaunchKernelGGL(nms_kernel<kNmsWaves>, dim3(n_img), dim3(64 * kNmsWaves), 0, s, g);
     return check_launch("pp_nms_keypoints");
 }
 

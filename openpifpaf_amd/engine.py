@@ -28,6 +28,9 @@ STAGE_COMPLETE_EARLY = 16
 STAGE_SEED_LOOP_ONLY, STAGE_AFTER_SEED_LOOP = 32, 64
 # PP_STAGE_COMPLETE_ONLY / PP_STAGE_NMS_ONLY: the after-seed-loop part in two calls
 STAGE_COMPLETE_ONLY, STAGE_NMS_ONLY = 128, 256
+# PP_STAGE_NMS_WIDE: NMS in 8-wave workgroups (dense batches; the 4-wave default fits beside
+# a seed loop on a CU)
+STAGE_NMS_WIDE = 512
 
 
 def default_ann_capacity(h, w):
@@ -565,8 +568,12 @@ class DecodePipeline:
         with torch.cuda.stream(front):
             if events:
                 events[0].record()
-            b_first = _B_FIRST if _B_FIRST is not None else (
-                True if self.density >= _B_FIRST_DENSITY else 'lazy')
+            dense = self.density >= _B_FIRST_DENSITY
+            b_first = _B_FIRST if _B_FIRST is not None else (True if dense else 'lazy')
+            # dense batches: the 8-wave NMS (uniform cfg3 15.1-15.3k vs 14.4-14.5k images/s);
+            # sparse ones: the 4-wave NMS runs beside the next seed loop (planted 370-375k
+            # vs 385-394k, A/B on one box)
+            wide = STAGE_NMS_WIDE if dense else 0
             early = 0 if b_first == 'lazy' else STAGE_COMPLETE_EARLY
             if b_first == 'lazy':
                 launch(STAGE_CIFHR)
@@ -598,9 +605,9 @@ class DecodePipeline:
                 launch(STAGE_GROW | early | STAGE_AFTER_SEED_LOOP | STAGE_COMPLETE_ONLY)
                 sets_done = torch.cuda.Event()
                 sets_done.record()
-                b = launch(STAGE_GROW | early | STAGE_AFTER_SEED_LOOP | STAGE_NMS_ONLY)
+                b = launch(STAGE_GROW | early | STAGE_AFTER_SEED_LOOP | STAGE_NMS_ONLY | wide)
             else:
-                b = launch(STAGE_GROW | early | STAGE_AFTER_SEED_LOOP)
+                b = launch(STAGE_GROW | early | STAGE_AFTER_SEED_LOOP | wide)
                 sets_done = None
             if events:
                 events[4].record()

@@ -70,3 +70,27 @@ def test_pipeline_multi_scale_matches_engine_decode(name):
         recs, offsets = p.result()
         np.testing.assert_array_equal(offsets, w_off)
         assert recs.tobytes() == w_bytes
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('n_img', [8, 136])
+def test_pipeline_wide_nms_matches_engine_decode(n_img):
+    """Dense batches in the pipeline take the 8-wave NMS (PP_STAGE_NMS_WIDE) when the batch
+    runs the one-CU seed loop (136 images; 8 images keep the 4-wave form): records byte for
+    byte as the one-stream decode with the default 4-wave NMS."""
+    import torch
+    from openpifpaf_amd.engine import DecodeEngine, DecodePipeline
+    skel = constants.COCO_PERSON_SKELETON
+    cfg = make_config(**EVAL_CONFIG)
+    cif, caf = synthetic.batch('uniform', n_img, 40, 40, first_seed=7, n_caf=len(skel))
+    cif, caf = torch.from_numpy(cif).cuda(), torch.from_numpy(caf).cuda()
+    recs0, off0, _ = DecodeEngine().decode(cif, caf, skel, cfg, cap=1024, compact=PACK_ALL)
+    assert off0[-1] / n_img >= 32  # dense: the pipeline's rule picks the wide NMS
+    pipe = DecodePipeline()
+    pipe.density = float(off0[-1]) / n_img
+    pend = [pipe.submit(cif, caf, skel, cfg, cap=1024, compact=(17, len(skel), PACK_ALL))[1]
+            for _ in range(3)]
+    for p in pend:
+        recs, offsets = p.result()
+        np.testing.assert_array_equal(offsets, off0)
+        assert recs.tobytes() == recs0.tobytes()
