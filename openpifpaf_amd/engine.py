@@ -499,10 +499,6 @@ _PIPE_DEPTH = 2
 # for the force-complete, its next seed loop for the NMS (PP_SPLIT_TAIL=0: one call, the
 # front half waits for both)
 _SPLIT_TAIL = os.environ.get('PP_SPLIT_TAIL', '1') != '0'
-# PP_PIPE_PRIO=back / tail / front (diagnostics): that stream of the pipeline at high HIP
-# priority (the front half then runs on a pipeline stream of its own, which waits for the
-# caller's stream)
-_PIPE_PRIO = os.environ.get('PP_PIPE_PRIO', '')
 
 
 class DecodePipeline:
@@ -544,11 +540,10 @@ class DecodePipeline:
         # one back stream: consecutive seed loops serialise.  Two (one per workspace, so the
         # next batch's images fill the CUs whose image of this batch finished) measured
         # slower: planted 0.91-1.01 vs 0.84-0.85 ms per step, uniform unchanged (round 3)
-        hi = {'priority': -1}
-        self.back = torch.cuda.Stream(device=self.device, **(hi if _PIPE_PRIO == 'back' else {}))
-        self.tail = torch.cuda.Stream(device=self.device, **(hi if _PIPE_PRIO == 'tail' else {}))
-        self.front = (torch.cuda.Stream(device=self.device, **hi) if _PIPE_PRIO == 'front'
-                      else None)
+        # (a high HIP priority for the back, tail or a separate front stream measured no
+        # better: planted 385-389k / 373-382k / 365-389k vs 390-391k images/s, round 4)
+        self.back = torch.cuda.Stream(device=self.device)
+        self.tail = torch.cuda.Stream(device=self.device)
         self._back_done = [None] * self.depth
         self._sets_done = [None] * self.depth  # end of force-complete (last reader of 1-4)
         self._i = 0
@@ -564,9 +559,6 @@ class DecodePipeline:
         self._i += 1
         eng = self.engines[par]
         front = torch.cuda.current_stream(self.device)
-        if self.front is not None:
-            self.front.wait_stream(front)
-            front = self.front
 
         def launch(stages):
             if heads is None:
