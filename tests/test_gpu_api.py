@@ -278,3 +278,28 @@ def test_custom_nms_runs_on_host(dec):
     want = KeepStrong().annotations(plain)
     assert 0 < len(got) < len(plain)
     assert gu.annotations_as_records(got).tobytes() == gu.annotations_as_records(want).tobytes()
+
+
+@pytest.mark.parametrize('extra', [{'connection_method': 'max'}, {'greedy': True},
+                                   {'force_complete': False}])
+def test_confidence_scales_variants_vs_oracle(extra):
+    """confidence_scales with the max connection method, greedy growth (the reference
+    returns a greedy entry before weighting it, cifcaf.py:280-284) and without
+    force-complete: every image's records byte-equal to the oracle's (the oracle is pinned
+    to the reference's api_confscales fixtures)."""
+    import torch
+    from openpifpaf_amd import synthetic
+    from openpifpaf_amd._abi import EVAL_CONFIG, make_config
+    from openpifpaf_amd.engine import DecodeEngine
+    scales = [0.01 if i % 4 == 1 else 0.4 + 0.3 * (i % 3) for i in range(len(SKEL))]
+    cfg = make_config(**dict(EVAL_CONFIG, confidence_scales=scales, **extra))
+    cif, caf = synthetic.batch('planted', 5, 48, 48, first_seed=80)
+    recs, offs, _ = DecodeEngine().decode(torch.from_numpy(cif).cuda(),
+                                          torch.from_numpy(caf).cuda(), SKEL, cfg)
+    for i in range(len(cif)):
+        ref = oracle.decode(cif[i], caf[i], SKEL, cfg)
+        got = recs[offs[i]:offs[i + 1]]
+        assert len(got) == len(ref), i
+        for field in ('data', 'joint_scales', 'n_decoding', 'decoding_pairs', 'decoding_xyv',
+                      'n_frontier', 'frontier_pairs'):
+            assert got[field].tobytes() == ref[field].tobytes(), (i, field)
