@@ -162,6 +162,9 @@ def _buffer_key(n, k, c, shape, cap, cfg):
 class DecodeEngine:
     def __init__(self):
         self._bufs = None
+        # annotations per image of the last checked decode: dense batches (>= 32) get the
+        # 8-wave NMS (PP_STAGE_NMS_WIDE) in the next one, as DecodePipeline does
+        self.density = 0.0
 
     def buffers(self, n, k, c, h, w, cfg, cap, heads=None):
         shape = (h, w) if heads is None else heads.shape_key
@@ -252,14 +255,17 @@ class DecodeEngine:
         complete.  Raises PPError on the overflows a retry cannot fix."""
         h, w = (cif.shape[3], cif.shape[4]) if heads is None else (heads.h, heads.w)
         cap = cap or default_ann_capacity(h, w)
+        stages = STAGE_ALL | (STAGE_NMS_WIDE if self.density >= _B_FIRST_DENSITY else 0)
         while True:
             if heads is None:
                 b = self.launch(cif, caf, skeleton, cfg, cap=cap, keep_cifhr=keep_cifhr,
-                                initial=initial)
+                                stages=stages, initial=initial)
             else:
                 b = self.launch_multi(heads, skeleton, cfg, cap=cap, keep_cifhr=keep_cifhr,
-                                      initial=initial)
+                                      stages=stages, initial=initial)
             status = b.status.cpu().numpy()
+            if len(status):
+                self.density = float(b.counts[:len(status)].float().mean())
             if not (status & PP_ST_ANN_OVERFLOW).any():
                 break
             cap *= 2
