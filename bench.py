@@ -197,6 +197,7 @@ def main():
                for _ in range(depth)]
 
     comm = torch.cuda.Stream(device=dev) if world > 1 and args.backend == 'nccl' else None
+    per_rank = []  # multi-rank: each rank's timings of the last timed_run (rank 0's view)
     counters = {'refetch_steps': 0, 'pack_bytes': 0}
     gather = {'steps': 0, 'verified_steps': 0, 'ranks_seen': world, 'full_record_steps': 0,
               'bytes': 0}
@@ -211,6 +212,10 @@ def main():
         n_img = heads.n if heads is not None else cif.shape[0]
         compact = (k_img, len(skel), PACK_ALL)
         stage_ms = np.zeros(len(ev_pairs))
+        # this rank's own view of the timed steps (the multi-rank line reports every rank's):
+        # device ms from the step's first event to its last, host ms blocked on the records
+        # (pack done), host ms inside the record gather
+        rank_ms = {'decode': 0.0, 'records_wait': 0.0, 'gather': 0.0}
 
         def step(timed, k=0):
             """Enqueue one decode and its record fetch; returns (PendingRecords, events)."""
@@ -241,6 +246,7 @@ def main():
             comm stream, which waits only for this step's pack)."""
             pending, ev = step_out
             n_recs = 0
+            t_wait = time.perf_counter()
             if pending is None:
                 torch.cuda.synchronize()
             elif world == 1 or local:
@@ -250,6 +256,9 @@ def main():
                 n_recs = len(recs)
             else:
                 counts = pending.wait()
+                t_gather = time.perf_counter()
+                if timed:
+                    rank_ms['records_wait'] += 1e3 * (t_gather - t_wait)
                 if not pending.fits(int(counts.sum())):
                     raise SystemExit('record block too small after warmup')
                 if comm is not None:
@@ -267,6 +276,8 @@ def main():
                                         device=comm_dev, stream=comm, full=full, k=k_img,
                                         c=len(skel), report=rep)
                 n_recs = len(recs) if recs is not None else 0
+                if timed:
+                    rank_ms['gather'] += 1e3 * (time.perf_counter() - t_gather)
                 if rank == 0:
                     # every step's transfers are checked: each sender's digest of its record
                     # bytes against rank 0's digest of what arrived
@@ -280,6 +291,7 @@ def main():
                 ev[last].synchronize()
                 for si, (i, j) in enumerate(ev_pairs):
                     stage_ms[si] += ev[i].elapsed_time(ev[j])
+                rank_ms['decode'] += ev[0].elapsed_time(ev[last])
             return n_recs
 
         for _ in range(warmup):
@@ -326,9 +338,18 @@ def main():
             dist.barrier()
         elapsed = time.perf_counter() - t0
         if world > 1:
-            t = torch.tensor([elapsed], dtype=torch.float64, device=comm_dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = float(t.item())
+            # every rank's own numbers to rank 0 (for the line's per_rank list), then the
+            # max over ranks of the wall clock
+            mine = torch.tensor([elapsed, rank_ms['decode'] / steps,
+                                 rank_ms['records_wait'] / steps, rank_ms['gather'] / steps],
+                                dtype=torch.float64, device=comm_dev)
+            every = torch.empty(world * 4, dtype=torch.float64, device=comm_dev)
+            dist.all_gather_into_tensor(every, mine)
+            per_rank[:] = [dict(zip(('elapsed_s', 'decode_ms_per_step',
+                                     'records_wait_ms_per_step', 'gather_ms_per_step'),
+                                    (round(float(v), 4) for v in row)), rank=r)
+                           for r, row in enumerate(every.cpu().numpy().reshape(world, 4))]
+            elapsed = max(p['elapsed_s'] for p in per_rank)
         return elapsed, stage_ms / steps, n_anns
 
     log('rank {}/{}: {} on {}'.format(rank, world, args.workload, dev))
@@ -412,6 +433,10 @@ def main():
         line['gather'] = {'steps': gather['steps'], 'verified_steps': gather['verified_steps'],
                           'full_record_steps': gather['full_record_steps'],
                           'bytes_per_step_rank0': gather['bytes']}
+        # per rank: wall clock of the timed steps, device ms per step (first to last event of
+        # a step; overlapped steps share the device), host ms per step blocked on the
+        # step's records, host ms per step in the gather (rank 0: receiving and checking)
+        line['per_rank'] = per_rank
     default_run = (args.workload in ('cfg3', 'cfg4') and args.generator == 'planted' and
                    args.mode == 'eval' and batch == WORKLOADS['cfg3']['batch'])
     if default_run:
@@ -419,6 +444,8 @@ def main():
         for key in ('roofline', 'roofline_decoder_cifhr'):
             if key in tr:
                 line[key].update(tr[key])
+        reconcile_trace(line['roofline'], dense_bytes)
+        reconcile_trace(line['roofline_decoder_cifhr'], cifhr_bytes)
     if default_run and world == 1 and not args.no_uniform:
         # the same workload on the uniform generator (SURVEY.md §8d cfg3 names both):
         # dense random fields, ~400 annotations per image
@@ -620,10 +647,37 @@ def committed_traffic():
         if t is not None:
             out[key] = {'traffic': t, 'traffic_source': 'profiles/{} (src_sha {})'.format(
                 os.path.basename(used), want)}
+            # the same profile's kernel-trace average (rocprofv3 --kernel-trace, the
+            # kernels' summed AverageNs in <tag>_kernel_stats.csv)
+            avg = summ.get('avg_ns', {}).get(kernels)
+            if avg:
+                out[key]['trace_ms_per_launch'] = round(avg * 1e-6, 4)
         else:
             out[key] = {'traffic': None, 'traffic_stale': 'no committed profile of library '
                         '{} (newest: profiles/{})'.format(want, os.path.basename(paths[-1]))}
     return out
+
+
+def reconcile_trace(roof, alg_bytes, tol=0.05):
+    """Put the committed kernel trace's figure beside the live HIP-event one: `frac_events`
+    (this run's events), `frac_trace` (algorithmic bytes over the trace average of the
+    profile named in `traffic_source`).  When they differ by more than `tol`, `achieved` /
+    `frac` report the lower one and `frac_source` says which; boxes differ by 10-20 %
+    (DESIGN.md §4), so the headline never rests on the faster box alone."""
+    ev_gbs = roof['achieved']
+    roof['frac_events'] = roof['frac']
+    trace_ms = roof.get('trace_ms_per_launch')
+    if not trace_ms:
+        roof['frac_source'] = 'events (no committed trace of this library)'
+        return
+    tr_gbs = alg_bytes / (trace_ms * 1e-3) / 1e9
+    roof['frac_trace'] = round(tr_gbs / roof['peak'], 4)
+    if abs(tr_gbs - ev_gbs) > tol * max(tr_gbs, ev_gbs) and tr_gbs < ev_gbs:
+        roof['achieved'] = round(tr_gbs, 1)
+        roof['frac'] = roof['frac_trace']
+        roof['frac_source'] = 'trace (lower than events by more than {:.0%})'.format(tol)
+    else:
+        roof['frac_source'] = 'events (within {:.0%} of the trace, or lower)'.format(tol)
 
 
 def cfg2_latency(gen, cfg, dev, calls=200):

@@ -21,6 +21,12 @@
 
 #include <algorithm>
 
+// cifhr_fused_kernel<SEEDS>'s last-workgroup hand-off relies on gfx9's store accounting
+// (stores count under vmcnt); this library is built for gfx950 only.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "splat.hip: device code assumes gfx950 (see cifhr_fused_kernel's completion counter)"
+#endif
+
 #ifdef PP_STAMPS
 #include <stdio.h>
 
@@ -1441,6 +1447,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
     }
     HR_STAMP(2 + wave);
     if constexpr (SEEDS) {
+        // Completion without a release fence: the blocks and masks above are
+        // write-through (sc1 / nontemporal) stores, and on gfx9 stores count under vmcnt, so
+        // the s_waitcnt below drains them to L2-coherent memory before the counter's atomic;
+        // the last arriver's agent acquire then sees every unit's writes.  An agent release
+        // fence would add a buffer_wbl2 of the whole L2 per workgroup on gfx950 (per-XCD
+        // L2s).  This holds only where stores count under vmcnt: the guard at the top of this
+        // file refuses any other device target.
         __shared__ int s_last;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's blocks and masks
         __syncthreads();

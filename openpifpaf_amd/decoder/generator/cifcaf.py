@@ -35,6 +35,7 @@ class CifCaf(Generator):
     :param: nms: set to None to switch off non-maximum suppression.
     """
     connection_method = 'blend'
+    supports_sharding = True
     force_complete = False
     greedy = False
     keypoint_threshold = 0.0
@@ -52,7 +53,8 @@ class CifCaf(Generator):
         # confidence_scales (cifcaf.py:39,52): per-CAF weights on the frontier priorities
         # of _grow (cifcaf.py:259-260, 282-284), applied on the device (pp_config).  The
         # reference indexes it per CAF while growing; a list shorter than the skeleton
-        # raises its IndexError here, before any decode.
+        # raises its IndexError here, before any decode -- deliberately stricter than the
+        # reference (see config(), which checks again for lists replaced after __init__).
         if confidence_scales is not None and len(confidence_scales) < len(skeleton):
             raise IndexError('list index out of range (confidence_scales has {} entries for '
                              '{} CAF fields)'.format(len(confidence_scales), len(skeleton)))
@@ -82,6 +84,15 @@ class CifCaf(Generator):
             raise TypeError('CifSeeds.threshold is not configured (decoder.configure sets it)')
         nms = self.nms if self._device_nms() else None
         check_seed_mask(self.field_config.seed_mask, len(self.keypoints))
+        # Deliberately stricter than the reference: it indexes confidence_scales per CAF
+        # inside _grow and raises IndexError only when a grow reaches an edge past the end
+        # of the list (cifcaf.py:259-260, 282-284), so a decode that never grows such an
+        # edge succeeds there.  The device table needs every edge's weight up front, so a
+        # short list raises the same IndexError here, at the start of every decode.
+        cs = self.confidence_scales
+        if cs is not None and len(cs) < len(self.skeleton):
+            raise IndexError('list index out of range (confidence_scales has {} entries for '
+                             '{} CAF fields)'.format(len(cs), len(self.skeleton)))
         return make_config(
             cif_threshold=CifHr.v_threshold,
             seed_threshold=CifSeeds.threshold,
@@ -210,7 +221,8 @@ class CifCaf(Generator):
         """(B, K, 5, H, W) + (B, C, 9, H, W) -> one list of Annotation per image.
 
         With a torch.distributed process `group` (e.g. `dist.group.WORLD`: one rank per
-        GPU, nccl = RCCL over xGMI, or gloo), the batch is image-sharded: each rank decodes
+        GPU, nccl = RCCL over xGMI, or gloo; the nccl leg has not yet run on hardware with
+        more than one GPU), the batch is image-sharded: each rank decodes
         its contiguous `distributed.shard` of the B images (every rank passes the whole
         batch; `local=True`: the arguments are already this rank's images, possibly None
         for none), and rank `dst` returns the annotation lists of all images in rank order,

@@ -31,6 +31,7 @@ def det_nms_config(cls=None):
 
 class CifDet(Generator):
     occupancy_visualizer = None
+    supports_sharding = True
 
     def __init__(self, field_config: FieldConfig, categories, *, worker_pool=None):
         super().__init__(worker_pool)
@@ -80,17 +81,53 @@ class CifDet(Generator):
         recs = np.concatenate([host[i, :counts[i]].reshape(-1) for i in range(b)])
         return np.frombuffer(recs.tobytes(), dtype=DET_DTYPE), offsets
 
-    def decode_batch(self, det_batch):
-        recs, offsets = self.decode_records(det_batch)
+    def annotations_from_records(self, recs, offsets):
         return [[AnnotationDet.from_record(r, self.categories)
                  for r in recs[offsets[i]:offsets[i + 1]]] for i in range(len(offsets) - 1)]
 
-    def decode_heads(self, heads, *, group=None, **_):
-        """Generator.batch: the model's head list (each (B, ...)); reads the CifDet head."""
-        if group is not None:
-            raise NotImplementedError('image-sharded decoding is implemented for CifCaf only')
+    def decode_batch(self, det_batch, *, group=None, dst=0, local=False):
+        """(B, K, 7, H, W) -> one list of AnnotationDet per image.
+
+        With a torch.distributed process `group`, the batch is image-sharded as in
+        CifCaf.decode_batch: each rank decodes its contiguous `distributed.shard` of the
+        images (`local=True`: det_batch is already this rank's share, possibly None), and
+        rank `dst` returns the detections of all images in rank order, gathered as pp_det
+        records whose digests it checks (distributed.gather_records; GatherMismatch on a
+        mismatch).  Other ranks return None.  Replaces the reference's
+        worker_pool.starmap over the batch (generator.py:96-97)."""
+        if group is None:
+            return self.annotations_from_records(*self.decode_records(det_batch))
+        import torch.distributed as dist  # pylint: disable=import-outside-toplevel
+        from ...distributed import GatherMismatch, gather_records, shard
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        n = 0 if det_batch is None else len(det_batch)
+        a, b = (0, n) if local else shard(n, rank, world)
+        if b > a:
+            recs, offsets = self.decode_records(det_batch[a:b])
+        else:
+            recs, offsets = np.zeros(0, DET_DTYPE), np.zeros(1, np.int64)
+        nccl = dist.get_backend(group) == 'nccl'
+        device = (torch.device('cuda', torch.cuda.current_device()) if nccl
+                  else torch.device('cpu'))
+        self.last_gather = {}
+        recs, offsets = gather_records(recs, offsets, dist, device, dst=dst,
+                                       report=self.last_gather, group=group)
+        if recs is None:
+            return None
+        if self.last_gather['ranks_verified'] != world:
+            raise GatherMismatch('gathered detections of {} of {} ranks do not match their '
+                                 'digests'.format(world - self.last_gather['ranks_verified'],
+                                                  world))
+        return self.annotations_from_records(recs, offsets)
+
+    def decode_heads(self, heads, *, group=None, dst=0, local=False):
+        """Generator.batch: the model's head list (each (B, ...)); reads the CifDet head
+        (`group` / `dst` / `local`: image-sharded, as decode_batch)."""
+        kw = {} if group is None else {'group': group, 'dst': dst, 'local': local}
+        if heads is None:  # this rank's shard of a sharded batch is empty
+            return self.decode_batch(None, **kw)
         cif_i, _, _ = self.field_config.single_scale()
-        return self.decode_batch(heads[cif_i])
+        return self.decode_batch(heads[cif_i], **kw)
 
     def __call__(self, fields):
         cif_i, _, _ = self.field_config.single_scale()

@@ -40,6 +40,10 @@ class DummyPool():
 
 
 class Generator:
+    # decode_heads(heads, group=, dst=, local=) is implemented (checked by batch() before
+    # the model runs on a rank's share)
+    supports_sharding = False
+
     def __init__(self, worker_pool=None):
         self.worker_pool = DummyPool() if not worker_pool else worker_pool
         self.last_decoder_time = 0.0
@@ -87,6 +91,9 @@ class Generator:
         decodes them, and rank `dst` returns the annotation lists of the whole batch
         (CifCaf.decode_batch); the other ranks return None."""
         if group is not None:
+            if not self.supports_sharding:
+                raise NotImplementedError('image-sharded decoding is not implemented for '
+                                          + type(self).__name__)
             import torch.distributed as dist  # pylint: disable=import-outside-toplevel
             a, b = shard(len(image_batch), dist.get_rank(group), dist.get_world_size(group))
             image_batch = image_batch[a:b]

@@ -21,8 +21,8 @@ import contextlib
 import numpy as np
 import torch
 
-from ._abi import (ANN_DTYPE, PACK_ALL, PP_MAX_FRONTIER, PP_MAX_KP, PP_PACK_DECODING,
-                   PP_PACK_FRONTIER, packed_dtype)
+from ._abi import (ANN_DTYPE, DET_DTYPE, PACK_ALL, PP_MAX_FRONTIER, PP_MAX_KP,
+                   PP_PACK_DECODING, PP_PACK_FRONTIER, packed_dtype)
 
 # digest of a record block: two sums of ((word + 1) * w_i mod p) over its 32-bit words, with
 # per-position weights w_i < p < 2**31 (products < 2**63, sums of < 2**32 terms fit int64)
@@ -121,6 +121,25 @@ def expand_compact(recs, k=None, c=None):
 
 
 _META = 6  # per-rank header: images, records, full?, then the compact dtype's K, F, flags
+_META_DET = -1  # K slot of a rank sending pp_det records (CifDet, _abi.DET_DTYPE)
+
+
+def _meta_format(dtype, full):
+    """The header's (K, F, flags) for a rank's record format (zeros: full pp_ann)."""
+    if full or dtype is None or dtype == ANN_DTYPE:
+        return (0, 0, 0)
+    if dtype == DET_DTYPE:
+        return (_META_DET, 0, 0)
+    return compact_spec(dtype)
+
+
+def _meta_dtype(m):
+    """A rank's record dtype from its header row (inverse of _meta_format)."""
+    if m[2] or not m[5] and not m[3]:
+        return ANN_DTYPE
+    if m[3] == _META_DET:
+        return DET_DTYPE
+    return compact_dtype(*m[3:6])
 
 
 def _ranks(dist, group):
@@ -158,8 +177,7 @@ def gather_packed(records, counts, dist, *, n_max, dtype, device, dst=0, stream=
         # metadata: (images, records, full?, K, F, flags, counts[n_max]) of every rank
         meta = np.zeros(n_max + _META, np.int64)
         meta[0], meta[1], meta[2] = len(counts), int(counts.sum()), int(full)
-        if not full and dtype is not None and dtype != ANN_DTYPE:
-            meta[3:6] = compact_spec(dtype)
+        meta[3:6] = _meta_format(dtype, full)
         meta[_META:_META + len(counts)] = counts
         t = torch.from_numpy(meta)
         if device.type == 'cuda':
@@ -178,8 +196,7 @@ def gather_packed(records, counts, dist, *, n_max, dtype, device, dst=0, stream=
             return None, None
         metas = gathered.cpu().numpy().reshape(world, n_max + _META)
         # each rank's record dtype: full records, or the compact layout it announced
-        dtypes = [ANN_DTYPE if m[2] or not m[5] and not m[3] else compact_dtype(*m[3:6])
-                  for m in metas]
+        dtypes = [_meta_dtype(m) for m in metas]
         widths = np.array([d.itemsize for d in dtypes], np.int64)
         totals = metas[:, 1]
         bufs, sums, ops = {}, {}, []
@@ -209,6 +226,9 @@ def gather_packed(records, counts, dist, *, n_max, dtype, device, dst=0, stream=
             torch.cuda.current_stream(device).synchronize()
     # ranks with records decide the output format (an empty rank's format does not matter)
     live = [r for r in range(world) if totals[r]]
+    any_det = any(dtypes[r] == DET_DTYPE for r in live)
+    if any_det and any(dtypes[r] != DET_DTYPE for r in live):
+        raise ValueError('ranks sent detection and keypoint records to one gather')
     any_full = any(dtypes[r] == ANN_DTYPE for r in live)
     out_dtype = ANN_DTYPE if any_full else (dtypes[live[0]] if live else
                                             (dtype if dtype is not None else ANN_DTYPE))

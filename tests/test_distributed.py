@@ -297,6 +297,87 @@ def test_gather_mixed_full_and_compact(n_imgs):
     mp.spawn(_worker, args=(world, _free_port(), n_imgs, 'mixed'), nprocs=world, join=True)
 
 
+def _fake_det_records(det_batch):
+    """Stand-in for CifDet.decode_records (the device decode): image i of the batch holds
+    int(det[i, 0, 0, 0, 0]) detections whose values are read from its fields."""
+    from openpifpaf_amd._abi import DET_DTYPE
+    det = np.asarray(det_batch)
+    counts = det[:, 0, 0, 0, 0].astype(np.int64)
+    recs = np.zeros(int(counts.sum()), DET_DTYPE)
+    o = 0
+    for i, c in enumerate(counts):
+        for r in range(c):
+            recs[o] = (r % det.shape[1], det[i, 0, 1, 0, r], det[i, 0, 2, 0, r:r + 4], i, 0)
+            o += 1
+    return recs, np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+
+
+def _det_batch(n):
+    rng = np.random.default_rng(5)
+    det = rng.random((n, 3, 7, 2, 8), dtype=np.float32)
+    det[:, 0, 0, 0, 0] = rng.integers(0, 4, n)  # 0-3 detections per image
+    return torch.from_numpy(det)
+
+
+class _DetModel(torch.nn.Module):
+    """Generator.batch's model: the 'images' are the CifDet fields themselves; counts the
+    images it sees (a rank runs the model on its shard only)."""
+    seen = 0
+
+    def forward(self, x):
+        _DetModel.seen += len(x)
+        return [x]
+
+
+def _det_worker(rank, world, port, n_img):
+    """CifDet.decode_batch / Generator.batch with group=: each rank decodes its shard, rank 0
+    returns every image's detections, in order, digests checked (ref generator.py:84-101)."""
+    dist.init_process_group('gloo', init_method='tcp://127.0.0.1:{}'.format(port),
+                            rank=rank, world_size=world)
+    try:
+        from openpifpaf_amd import constants
+        from openpifpaf_amd.decoder import FieldConfig
+        from openpifpaf_amd.decoder.generator.cifdet import CifDet
+        det = _det_batch(n_img)
+        dec = CifDet(FieldConfig(), ['a', 'b', 'c'])
+        dec.decode_records = _fake_det_records
+        want = dec.annotations_from_records(*_fake_det_records(det))
+
+        def key(lists):
+            return [[(a.field_i, float(a.score), tuple(np.asarray(a.bbox).tolist()))
+                     for a in anns] for anns in lists]
+        for run in ('decode_batch', 'batch'):
+            if run == 'decode_batch':
+                got = dec.decode_batch(det, group=dist.group.WORLD)
+            else:
+                _DetModel.seen = 0
+                got = dec.batch(_DetModel(), det, group=dist.group.WORLD)
+                a, b = shard(n_img, rank, world)
+                assert _DetModel.seen == b - a
+            if rank != 0:
+                assert got is None
+                continue
+            assert dec.last_gather['ranks_seen'] == world
+            assert dec.last_gather['ranks_verified'] == world
+            assert key(got) == key(want)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,n_img', [(2, 7), (2, 1), (3, 5)])
+def test_cifdet_sharded_gloo(world, n_img):
+    mp.spawn(_det_worker, args=(world, _free_port(), n_img), nprocs=world, join=True)
+
+
+def test_batch_refuses_unsharded_generator_before_model():
+    """A generator without sharding support raises before the model runs."""
+    from openpifpaf_amd.decoder.generator.generator import Generator
+    _DetModel.seen = 0
+    with pytest.raises(NotImplementedError):
+        Generator().batch(_DetModel(), _det_batch(4), group=object())
+    assert _DetModel.seen == 0
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(('127.0.0.1', 0))
