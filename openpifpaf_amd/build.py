@@ -40,6 +40,7 @@ VARIANTS = {
     'base': ['-DPP_NO_FUSED', '-DPP_NO_SELF_PLAN', '-DPP_NO_SEED_OCC'],  # round 3's kernels
     'bitonic': ['-DPP_NO_SEED_RADIX'],   # seeds sorted by the bitonic network only
     'parts8': ['-DPP_SPLIT_PARTS8'],     # split-field CifHr units of 8 rows (16 rows default)
+    'w0plan': ['-DPP_W0_PLAN'],          # seed loop: wave 0 plans the idle helpers itself
 }
 
 

@@ -1762,6 +1762,16 @@ constexpr int kSpecScan = 128;     // seeds after the committed one examined per
 // Throughput is flat for 0-4 (both generators) and drops beyond 8.
 constexpr float kSpecFar = 4.0f;
 constexpr int kSelfScan = 256;     // seeds after the decided ones a finished helper examines
+// Who plans the idle helpers when wave 0 has to grow a seed itself: wave 0, before its grow
+// (PP_W0_PLAN builds), or (default) an idle helper, so that wave 0 starts its grow at once
+// and the plan (a scan of kSpecScan seeds against the cache, about 50k cycles, stamps) is
+// off the committer's path.  Wave 0 then publishes its seed without the plan lock: a plan
+// that misses it only grows a seed twice, which never changes a result.
+#ifdef PP_W0_PLAN
+constexpr bool kW0Plan = true;
+#else
+constexpr bool kW0Plan = false;
+#endif
 #ifdef PP_NO_SELF_PLAN  // A/B builds
 constexpr bool kSelfPlan = false;
 #else
@@ -1886,6 +1896,8 @@ struct SeedLoopSharedT {
     // grows itself now (own_on)
     int plan_lock, decided, own_on;
     float own_x, own_y, own_s;
+    // seed_loop_kernel: wave 0 started a grow of its own; an idle helper plans the others
+    int plan_req;
 };
 using SeedLoopShared = SeedLoopSharedT<kSpecCache>;
 struct SeedLoopSharedX : SeedLoopSharedT<kCacheSlots> {
@@ -2089,25 +2101,16 @@ __device__ __forceinline__ void plan_unlock(SeedLoopSharedT<NS> &S) {
     if ((threadIdx.x & 63) == 0) lds_release(&S.plan_lock, 0);
 }
 
-// <= 168 VGPRs (3 waves per SIMD; a few spills) and the column stage in dynamic LDS: the
-// image's workgroup leaves room on its CU for the next batch's CifHr / seeds / CafScored
-// workgroups (DecodePipeline).  Planted 1.031 -> 1.013 ms, uniform 21.7 -> 20.4 ms per
-// overlapped step; 4 waves per SIMD (128 VGPRs, 532 spills): 1.37 ms.
-// Grid: n_img image workgroups, then n_ext * n_img external helper workgroups (helper
-// workgroup x of image i is block n_img * (1 + x) + i, on image i's XCD when n_img % 8 == 0).
-template <bool CS>
-__global__ __launch_bounds__(64 * kSeedWaves) __attribute__((amdgpu_waves_per_eu(3)))
-void seed_loop_kernel(GrowArgs g) {
-    __shared__ SeedLDS Ls[kSeedWaves];
-    __shared__ SeedLoopShared S;
-    __shared__ int s_ncol[2 * PP_MAX_EDGES];  // set-A column counts per (CAF, direction)
-    __shared__ int s_cofs[2 * PP_MAX_EDGES];  // their LDS offsets in s_cols (-1: global)
-    __shared__ SeedOcc s_occ;  // per-seed occupancy (images of at most kOccSeeds seeds)
-    extern __shared__ float s_cols[];  // kColLds floats (dynamic: the launch sizes it)
-    const int img = blockIdx.x;
-    const int K = g.K;
+// ---- pieces both seed-loop kernels share (force-inlined: each takes GrowArgs by
+// reference, which a real call would copy to scratch) ----
+
+// The image's small set-A column sets (<= kFlatCols columns, in (CAF, direction) order
+// while they fit kColLds floats) into LDS, column-major, kColPad floats per column: their
+// counts into s_ncol, LDS offsets into s_cofs (-1: read from global memory).  Every wave of
+// the workgroup takes part; no barrier after the copy (the caller's init barrier follows).
+__device__ __forceinline__ ColStage stage_small_sets(const GrowArgs &g, int img, int *s_ncol,
+                                                     int *s_cofs, float *s_cols) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    SeedLDS &L = Ls[wave];
     for (int q = threadIdx.x; q < 2 * g.C; q += blockDim.x) s_ncol[q] = col_offs(g, 0, img, q >> 1, q & 1)[g.nb];
     __syncthreads();
     if (threadIdx.x == 0) {  // LDS placement of the small sets, in order while they fit
@@ -2134,7 +2137,111 @@ void seed_loop_kernel(GrowArgs g) {
             o[1] = make_float4(c[4], c[5], c[6], 0.0f);
         }
     }
-    const ColStage cstage{s_ncol, s_cofs, s_cols};
+    return ColStage{s_ncol, s_cofs, s_cols};
+}
+
+// The next free seed from index s on (cifcaf.py:100-104), 64 occupancy tests per step (the
+// per-seed LDS counters `socc`, or the global grid); -1 when none is left.  s advances past
+// the all-occupied steps.  Wave 0.
+__device__ __forceinline__ int next_free_seed(int &s, int n_seeds, const uint8_t *socc,
+                                              const pp_seed *seeds, const OccGrid &occ,
+                                              float red) {
+    const int lane = threadIdx.x & 63;
+    while (s < n_seeds) {
+        const int idx = s + lane;
+        bool is_free = false;
+        if (idx < n_seeds) {
+            if (socc) {
+                is_free = socc[idx] == 0;
+            } else {
+                const pp_seed c = seeds[idx];
+                is_free = !occ_get(occ, c.field, c.x, c.y, red);
+            }
+        }
+        const uint64_t m = __ballot(is_free);
+        if (m) return s + __ffsll((unsigned long long)m) - 1;
+        s += 64;
+    }
+    return -1;
+}
+
+// Initial annotations (cifcaf.py:95-98): each is grown with set A and reverse matching from
+// all its set joints (its decoding / frontier orders are appended to), then committed
+// (appended and marked occupied, `commit(record)`), in order, before any seed is looked
+// at.  Wave 0.
+template <bool CS, typename Commit>
+__device__ __forceinline__ void grow_initial(const GrowArgs &g, SeedLDS &L, int img,
+                                             const ColStage &cstage, const int &n_anns,
+                                             Commit commit) {
+    const int lane = threadIdx.x & 63;
+    const int n_init = g.init ? min(g.init_counts[img], g.init_cap) : 0;
+    for (int i = 0; i < n_init; i++) {
+        if (n_anns >= g.ann_cap) {
+            if (lane == 0) L.status |= PP_ST_ANN_OVERFLOW;
+            break;
+        }
+        copy_ann(&L.a, &g.init[(int64_t)img * g.init_cap + i]);
+        if (lane == 0) {
+            L.a.image = img;
+            L.a.n_keypoints = g.K;
+        }
+        wave_sync();
+        grow<true, CS>(g, L, img, 0, true, cstage);
+        commit(&L.a);
+    }
+}
+
+// A helper wave's finished grow into this CU's cache slot q: the record (global memory),
+// its joints (LDS), then the slot's state 2 (grown).  The record's global stores complete
+// before the flag (the workgroup-scope release alone does not wait for them).
+template <int NS>
+__device__ __forceinline__ void publish_cached(SeedLoopSharedT<NS> &S, pp_ann *cache, int q,
+                                               const SeedLDS &L) {
+    const int lane = threadIdx.x & 63;
+    copy_ann(&cache[q], &L.a);
+    if (lane < kKP)
+        S.cache_j[q][lane] = make_float4(L.a.data[lane][0], L.a.data[lane][1],
+                                         L.a.data[lane][2], L.a.joint_scales[lane]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+    if (lane == 0) lds_release(&S.cache_state[q], 2);
+    wave_sync();
+}
+
+// The end of a seed loop (wave 0, after the barrier that drains the helpers): the image's
+// occupancy marks cleared (the grid stays zero between launches), then its annotation
+// count, the joints force-complete must fill, and the waves' status bits.
+__device__ __forceinline__ void seed_loop_outputs(const GrowArgs &g, const SeedLDS *Ls, int img,
+                                                  int n_anns, uint32_t unset_mask) {
+    if ((threadIdx.x & 63) == 0) {
+        int st = 0;
+        for (int w = 0; w < kSeedWaves; w++) st |= Ls[w].status;
+        g.n_work[img] = n_anns;
+        g.need_complete[img] = g.cfg.force_complete ? (int)unset_mask : 0;
+        g.status[img] = st;
+    }
+}
+
+// <= 168 VGPRs (3 waves per SIMD; a few spills) and the column stage in dynamic LDS: the
+// image's workgroup leaves room on its CU for the next batch's CifHr / seeds / CafScored
+// workgroups (DecodePipeline).  Planted 1.031 -> 1.013 ms, uniform 21.7 -> 20.4 ms per
+// overlapped step; 4 waves per SIMD (128 VGPRs, 532 spills): 1.37 ms.
+// Grid: n_img image workgroups, then n_ext * n_img external helper workgroups (helper
+// workgroup x of image i is block n_img * (1 + x) + i, on image i's XCD when n_img % 8 == 0).
+template <bool CS>
+__global__ __launch_bounds__(64 * kSeedWaves) __attribute__((amdgpu_waves_per_eu(3)))
+void seed_loop_kernel(GrowArgs g) {
+    __shared__ SeedLDS Ls[kSeedWaves];
+    __shared__ SeedLoopShared S;
+    __shared__ int s_ncol[2 * PP_MAX_EDGES];  // set-A column counts per (CAF, direction)
+    __shared__ int s_cofs[2 * PP_MAX_EDGES];  // their LDS offsets in s_cols (-1: global)
+    __shared__ SeedOcc s_occ;  // per-seed occupancy (images of at most kOccSeeds seeds)
+    extern __shared__ float s_cols[];  // kColLds floats (dynamic: the launch sizes it)
+    const int img = blockIdx.x;
+    const int K = g.K;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    SeedLDS &L = Ls[wave];
+    const ColStage cstage = stage_small_sets(g, img, s_ncol, s_cofs, s_cols);
     if (lane == 0) {
         L.status = 0;
         L.log_n = 0;
@@ -2152,6 +2259,7 @@ void seed_loop_kernel(GrowArgs g) {
         S.plan_lock = 0;
         S.decided = 0;
         S.own_on = 0;
+        S.plan_req = 0;
     }
     __syncthreads();
 
@@ -2196,6 +2304,22 @@ void seed_loop_kernel(GrowArgs g) {
             for (;;) {
                 my = lds_acquire(&S.task[wave]);
                 if (my >= 0 || lds_acquire(&S.done)) break;
+                if (!kW0Plan && lds_acquire(&S.plan_req)) {
+                    // wave 0 is growing a seed of its own: plan every idle helper (this one
+                    // included) around it, as wave 0 did before its grow (PP_W0_PLAN)
+                    plan_lock(S);
+                    if (lds_acquire(&S.plan_req) && !lds_acquire(&S.done)) {
+                        if (lane == 0) lds_release(&S.plan_req, 0);
+                        const int tk = lane > 0 && lane < kSeedWaves ? lds_acquire(&S.task[lane]) : 0;
+                        const uint64_t idle = __ballot(lane > 0 && lane < kSeedWaves && tk < 0);
+                        const int dec = lds_acquire(&S.decided);
+                        if (idle)
+                            spec_plan(S, nullptr, seeds, n_seeds, dec, dec, kSpecScan, occ, red,
+                                      occ_msr(g), g.spec_far, idle, socc);
+                    }
+                    plan_unlock(S);
+                    continue;
+                }
                 __builtin_amdgcn_s_sleep(1);
             }
             if (my < 0) break;
@@ -2203,16 +2327,7 @@ void seed_loop_kernel(GrowArgs g) {
             ann_from_seed(L, seeds[my], K, img);
             grow<true, CS>(g, L, img, 0, true, cstage, &S.done);
             if (lds_acquire(&S.done)) break;  // nobody reads the cache any more
-            copy_ann(&cache[q], &L.a);
-            if (lane < kKP)
-                S.cache_j[q][lane] = make_float4(L.a.data[lane][0], L.a.data[lane][1],
-                                                 L.a.data[lane][2], L.a.joint_scales[lane]);
-            // the record's global stores complete before the flag (the workgroup-scope
-            // release alone does not wait for them)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            wave_sync();
-            if (lane == 0) lds_release(&S.cache_state[q], 2);
-            wave_sync();
+            publish_cached(S, cache, q, L);
             // plan this wave's next grow itself, with its own annotation now in the cache (its
             // occupancy boxes rule out the other seeds of the same person); wave 0 plans only
             // when it has to grow a seed itself
@@ -2228,47 +2343,12 @@ void seed_loop_kernel(GrowArgs g) {
         }
     } else {
         __builtin_amdgcn_s_setprio(3);  // the committer is the critical path: issue first
-        // initial annotations (cifcaf.py:95-98): each is grown with set A and reverse
-        // matching from all its set joints (its decoding / frontier orders are appended to),
-        // appended and marked occupied, in order, before any seed is looked at
-        const int n_init = g.init ? min(g.init_counts[img], g.init_cap) : 0;
-        for (int i = 0; i < n_init; i++) {
-            if (n_anns >= g.ann_cap) {
-                if (lane == 0) L.status |= PP_ST_ANN_OVERFLOW;
-                break;
-            }
-            copy_ann(&L.a, &g.init[(int64_t)img * g.init_cap + i]);
-            if (lane == 0) {
-                L.a.image = img;
-                L.a.n_keypoints = K;
-            }
-            wave_sync();
-            grow<true, CS>(g, L, img, 0, true, cstage);
-            commit(&L.a, lane < K ? L.a.data[lane][0] : 0.0f, lane < K ? L.a.data[lane][1] : 0.0f,
-                   lane < K ? L.a.data[lane][2] : 0.0f, lane < K ? L.a.joint_scales[lane] : 0.0f);
-        }
+        grow_initial<CS>(g, L, img, cstage, n_anns, [&](const pp_ann *a) {
+            commit(a, lane < K ? a->data[lane][0] : 0.0f, lane < K ? a->data[lane][1] : 0.0f,
+                   lane < K ? a->data[lane][2] : 0.0f, lane < K ? a->joint_scales[lane] : 0.0f);
+        });
         for (;;) {
-            // the next free seed (cifcaf.py:100-104): 64 occupancy tests per step
-            int t = -1;
-            while (s < n_seeds) {
-                const int idx = s + lane;
-                bool is_free = false;
-                if (idx < n_seeds) {
-                    if (socc_on) {
-                        is_free = s_occ.cnt[idx] == 0;
-                    } else {
-                        const pp_seed c = seeds[idx];
-                        is_free = !occ_get(occ, c.field, c.x, c.y, red);
-                    }
-                }
-                const uint64_t m = __ballot(is_free);
-                if (m == 0) {
-                    s += 64;
-                    continue;
-                }
-                t = s + __ffsll((unsigned long long)m) - 1;
-                break;
-            }
+            const int t = next_free_seed(s, n_seeds, socc_on ? s_occ.cnt : nullptr, seeds, occ, red);
             STAMP(0);
             if (t < 0 || n_anns >= g.ann_cap) {
                 if (lane == 0 && t >= 0) L.status |= PP_ST_ANN_OVERFLOW;
@@ -2289,25 +2369,27 @@ void seed_loop_kernel(GrowArgs g) {
                 STAMP(4);
                 continue;
             }
-            // hand far-away free seeds to the idle helpers, then grow t here
+            // hand far-away free seeds to the idle helpers (an idle helper plans them, or
+            // wave 0 itself with PP_W0_PLAN), then grow t here
             const pp_seed st = seeds[t];
-            plan_lock(S);
+            if (kW0Plan) plan_lock(S);
             if (lane == 0) {
                 S.own_x = st.x;
                 S.own_y = st.y;
                 S.own_s = st.s;
                 lds_release(&S.own_on, 1);
                 lds_release(&S.decided, t);
+                if (!kW0Plan) lds_release(&S.plan_req, 1);
             }
             wave_sync();
-            {
+            if (kW0Plan) {
                 const int tk = lane > 0 && lane < kSeedWaves ? lds_acquire(&S.task[lane]) : 0;
                 const uint64_t idle = __ballot(lane > 0 && lane < kSeedWaves && tk < 0);
                 if (idle)
                     spec_plan(S, nullptr, seeds, n_seeds, t + 1, t, kSpecScan, occ, red, occ_msr(g),
                               g.spec_far, idle, socc);
+                plan_unlock(S);
             }
-            plan_unlock(S);
 #ifdef PP_STAMPS
             n_rounds++;
 #endif
@@ -2335,13 +2417,7 @@ void seed_loop_kernel(GrowArgs g) {
         st_acc[7] = n_hits;
 #endif
         STAMP_FLUSH(1);
-        if (lane == 0) {
-            int st = 0;
-            for (int w = 0; w < kSeedWaves; w++) st |= Ls[w].status;
-            g.n_work[img] = n_anns;
-            g.need_complete[img] = g.cfg.force_complete ? (int)unset_mask : 0;
-            g.status[img] = st;
-        }
+        seed_loop_outputs(g, Ls, img, n_anns, unset_mask);
     }
 }
 
@@ -2367,33 +2443,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
     const int K = g.K;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     SeedLDS &L = Ls[wave];
-    for (int q = threadIdx.x; q < 2 * g.C; q += blockDim.x) s_ncol[q] = col_offs(g, 0, img, q >> 1, q & 1)[g.nb];
-    __syncthreads();
-    if (threadIdx.x == 0) {  // LDS placement of the small sets, in order while they fit
-        int o = 0;
-        for (int q = 0; q < 2 * g.C; q++) {
-            const int sz = kColPad * s_ncol[q];
-            const bool fit = s_ncol[q] <= kFlatCols && o + sz <= kColLds;
-            s_cofs[q] = fit ? o : -1;
-            o += fit ? sz : 0;
-        }
-    }
-    __syncthreads();
-    for (int q = wave; q < 2 * g.C; q += kSeedWaves) {  // one set per wave
-        const int n = s_ncol[q];
-        if (s_cofs[q] < 0 || n == 0) continue;
-        const float *cf = col_set(g, 0, img, q >> 1, q & 1);
-        float *dst = s_cols + s_cofs[q];
-        for (int k = lane; k < n; k += 64) {
-            float c[kColRows];
-#pragma unroll
-            for (int r = 0; r < kColRows; r++) c[r] = cf[r * g.col_cap + k];
-            float4 *o = reinterpret_cast<float4 *>(dst + k * kColPad);
-            o[0] = make_float4(c[0], c[1], c[2], c[3]);
-            o[1] = make_float4(c[4], c[5], c[6], 0.0f);
-        }
-    }
-    const ColStage cstage{s_ncol, s_cofs, s_cols};
+    const ColStage cstage = stage_small_sets(g, img, s_ncol, s_cofs, s_cols);
     if (lane == 0) {
         L.status = 0;
         L.log_n = 0;
@@ -2501,16 +2551,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
                 t0 = __builtin_amdgcn_s_memrealtime();
                 continue;
             }
-            copy_ann(&cache[q], &L.a);
-            if (lane < kKP)
-                S.cache_j[q][lane] = make_float4(L.a.data[lane][0], L.a.data[lane][1],
-                                                 L.a.data[lane][2], L.a.joint_scales[lane]);
-            // the record's global stores complete before the flag (the workgroup-scope
-            // release alone does not wait for them)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            wave_sync();
-            if (lane == 0) lds_release(&S.cache_state[q], 2);
-            wave_sync();
+            publish_cached(S, cache, q, L);
             // plan this wave's next grow itself (as in seed_loop_kernel), into this CU's slots
             plan_lock(S);
             uint64_t left = 1ull << wave;
@@ -2526,48 +2567,13 @@ void seed_loop_ext_kernel(GrowArgs g) {
         if (external) return;
     } else {
         __builtin_amdgcn_s_setprio(3);  // the committer is the critical path: issue first
-        // initial annotations (cifcaf.py:95-98): each is grown with set A and reverse
-        // matching from all its set joints (its decoding / frontier orders are appended to),
-        // appended and marked occupied, in order, before any seed is looked at
-        const int n_init = g.init ? min(g.init_counts[img], g.init_cap) : 0;
-        for (int i = 0; i < n_init; i++) {
-            if (n_anns >= g.ann_cap) {
-                if (lane == 0) L.status |= PP_ST_ANN_OVERFLOW;
-                break;
-            }
-            copy_ann(&L.a, &g.init[(int64_t)img * g.init_cap + i]);
-            if (lane == 0) {
-                L.a.image = img;
-                L.a.n_keypoints = K;
-            }
-            wave_sync();
-            grow<true, CS>(g, L, img, 0, true, cstage);
-            commit(&L.a, false, lane < K ? L.a.data[lane][0] : 0.0f,
-                   lane < K ? L.a.data[lane][1] : 0.0f, lane < K ? L.a.data[lane][2] : 0.0f,
-                   lane < K ? L.a.joint_scales[lane] : 0.0f);
-        }
+        grow_initial<CS>(g, L, img, cstage, n_anns, [&](const pp_ann *a) {
+            commit(a, false, lane < K ? a->data[lane][0] : 0.0f,
+                   lane < K ? a->data[lane][1] : 0.0f, lane < K ? a->data[lane][2] : 0.0f,
+                   lane < K ? a->joint_scales[lane] : 0.0f);
+        });
         for (;;) {
-            // the next free seed (cifcaf.py:100-104): 64 occupancy tests per step
-            int t = -1;
-            while (s < n_seeds) {
-                const int idx = s + lane;
-                bool is_free = false;
-                if (idx < n_seeds) {
-                    if (socc_on) {
-                        is_free = s_occ.cnt[idx] == 0;
-                    } else {
-                        const pp_seed c = seeds[idx];
-                        is_free = !occ_get(occ, c.field, c.x, c.y, red);
-                    }
-                }
-                const uint64_t m = __ballot(is_free);
-                if (m == 0) {
-                    s += 64;
-                    continue;
-                }
-                t = s + __ffsll((unsigned long long)m) - 1;
-                break;
-            }
+            const int t = next_free_seed(s, n_seeds, socc_on ? s_occ.cnt : nullptr, seeds, occ, red);
             STAMP(0);
             if (t < 0 || n_anns >= g.ann_cap) {
                 if (lane == 0 && t >= 0) L.status |= PP_ST_ANN_OVERFLOW;
@@ -2769,13 +2775,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
         st_acc[7] = n_hits;
 #endif
         STAMP_FLUSH(1);
-        if (lane == 0) {
-            int st = 0;
-            for (int w = 0; w < kSeedWaves; w++) st |= Ls[w].status;
-            g.n_work[img] = n_anns;
-            g.need_complete[img] = g.cfg.force_complete ? (int)unset_mask : 0;
-            g.status[img] = st;
-        }
+        seed_loop_outputs(g, Ls, img, n_anns, unset_mask);
     }
 }
 

@@ -22,6 +22,7 @@ p = argparse.ArgumentParser()
 p.add_argument('--generator', default='planted')
 p.add_argument('--n', type=int, default=256)
 p.add_argument('--steps', type=int, default=60)
+p.add_argument('--depth', type=int, default=3, help='steps in flight on the host')
 args = p.parse_args()
 
 cif, caf = synthetic.batch(args.generator, args.n, 80, 80)
@@ -70,7 +71,7 @@ for k in range(args.steps):
     a = time.perf_counter()
     inflight.append(pipe.submit(c, f, sk, cfg, compact=compact)[1])
     t_sub.append(time.perf_counter() - a)
-    if len(inflight) >= 3:
+    if len(inflight) >= args.depth:
         q = inflight.pop(0)
         a = time.perf_counter()
         q.wait()
@@ -82,7 +83,8 @@ while inflight:
     inflight.pop(0).result()
 torch.cuda.synchronize()
 total = time.perf_counter() - t0
-print('{} n={}: {:.3f} ms per step'.format(args.generator, args.n, 1e3 * total / args.steps))
+print('{} n={} depth={}: {:.3f} ms per step'.format(args.generator, args.n, args.depth,
+                                                    1e3 * total / args.steps))
 for name, v in (('submit (host)', t_sub), ('blocked on records', t_wait),
                 ('result after wait (host)', t_res)):
     v = 1e3 * np.array(v)
