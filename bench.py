@@ -180,9 +180,10 @@ def main():
     # call; --stage-breakdown: one call per stage
     overlap = not (args.no_overlap or args.stage_breakdown) and stages == 15
     pipe = DecodePipeline(dev) if overlap else None
-    # steps in flight on the host: 3 with the overlapped pipeline (two workspaces x two
-    # output slots), 2 on one stream (two output slots)
-    depth = 3 if overlap else 2
+    # steps in flight on the host: one more than the pipeline's workspaces (3 with the
+    # default two; PP_PIPE_DEPTH=3 needs 4, tools/pipe_gaps.py), 2 on one stream (two
+    # output slots)
+    depth = pipe.depth + 1 if overlap else 2
     groups = ((STAGE_CIFHR, STAGE_SEEDS, STAGE_CAF, STAGE_GROW) if args.stage_breakdown else
               (STAGE_CIFHR, STAGE_SEEDS | STAGE_CAF | STAGE_GROW))
     names = (('cifhr', 'seeds', 'caf_scored', 'grow_nms') if args.stage_breakdown else

@@ -485,7 +485,12 @@ int pp_pack_compact(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img
  * 4 when the batch runs the one-CU seed loop (at least about CUs / 2 images).  The 4-wave
  * form fits on a CU beside a seed-loop workgroup, so an overlapped caller's NMS runs beside
  * the next batch's seed loop; the 8-wave form is faster per image on dense input
- * (hundreds of annotations per image).  Same results either way.
+ * (hundreds of annotations per image).  With force-complete it also selects the number of
+ * force-complete workgroups per image (more for dense batches).  Same results either way.
+ * PP_STAGE_NMS_BITMAP (1024): NMS as three launches whose middle one decides each (image,
+ * joint plane) with the plane's occupancy as a bitmap in LDS (one wave each) instead of
+ * one launch walking box lists.  Same results; faster one step at a time, slower beside
+ * another batch's seed loop (the many one-wave workgroups), hence opt-in.
  *
  * Workspace contract: bytes [pp_decode_workspace_zero_offset(), end) must be zero before
  * the first call (e.g. hipMemset once at allocation); every call leaves them zero again.
@@ -496,6 +501,7 @@ int pp_pack_compact(const pp_ann *d_anns, const int32_t *d_counts, int32_t n_img
 #define PP_STAGE_COMPLETE_ONLY 128u
 #define PP_STAGE_NMS_ONLY 256u
 #define PP_STAGE_NMS_WIDE 512u
+#define PP_STAGE_NMS_BITMAP 1024u
 int pp_decode_stages(const float *d_cif, const float *d_caf, int32_t n_img, int32_t K,
                      int32_t C, int32_t H, int32_t W, const int32_t *skeleton,
                      const pp_config *cfg, float *d_cifhr, pp_ann *d_anns,

@@ -41,6 +41,8 @@ VARIANTS = {
     'bitonic': ['-DPP_NO_SEED_RADIX'],   # seeds sorted by the bitonic network only
     'parts8': ['-DPP_SPLIT_PARTS8'],     # split-field CifHr units of 8 rows (16 rows default)
     'w0plan': ['-DPP_W0_PLAN'],          # seed loop: wave 0 plans the idle helpers itself
+    'nopartial': ['-DPP_NO_PARTIAL'],    # seed-loop plans without the in-flight grows' joints
+    'hprio': ['-DPP_HELPER_PRIO'],       # seed-loop helper waves at issue priority 2
 }
 
 

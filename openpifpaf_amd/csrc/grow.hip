@@ -73,7 +73,8 @@ constexpr int kSlots = 2 * PP_MAX_EDGES;   // directed edges (two lanes' worth o
 // entries, so a fill pushes at most 2C <= 2 * PP_MAX_EDGES entries
 constexpr int kHeap = 2 * PP_MAX_EDGES + 8;
 constexpr int kOccMargin = 64;              // NMS occupancy slack beyond the main grid
-constexpr int kCompleteWays = 64;           // force-complete workgroups per image
+constexpr int kCompleteWays = 64;           // force-complete workgroups per image (dense hint)
+constexpr int kCompleteWaysSparse = 64;     // ... without it (PP_COMPLETE_WAYS overrides)
 
 struct FFEntry {  // _flood_fill frontier entry (-v, end_i, start_xyv, s)
     float neg;
@@ -131,7 +132,7 @@ struct GrowArgs {
     double *nms_score;        // (n_img, 2 * ann_cap)
     int *nms_idx;             // (n_img, 4 * ann_cap + ann_np)
     float *nms_f;             // (n_img, 2 * ann_cap) per-annotation max x, max y
-    int2 *nms_box;            // (n_img, kNmsWaves, ann_cap) plane box lists beyond LDS
+    int2 *nms_box;            // (n_img, kNmsBoxLists, ann_cap) plane box lists beyond registers
     int ann_np;               // next pow2 >= ann_cap
     int ann_cap;
     uint64_t *stamps;         // diagnostic build: (n_img, 3, 12) cycle sums, else NULL
@@ -1213,7 +1214,8 @@ __device__ __forceinline__ void eval_ahead_raw(const GrowArgs &g, Frontier &F, i
 // (wave 0 is done: the result would never be read)
 template <bool AHEAD, bool CS, typename LDS, bool RAW_AHEAD = false>
 __device__ __forceinline__ void grow(const GrowArgs &g, LDS &L, int img, int set, bool reverse_match,
-                                     const ColStage &cs = ColStage{}, int *abort = nullptr) {
+                                     const ColStage &cs = ColStage{}, int *abort = nullptr,
+                                     float4 *pub = nullptr, uint32_t *pub_mask = nullptr) {
     const int lane = threadIdx.x & 63;
     const int K = g.K;
     float ax = 0.0f, ay = 0.0f, av = 0.0f, as = 0.0f;
@@ -1259,6 +1261,14 @@ __device__ __forceinline__ void grow(const GrowArgs &g, LDS &L, int img, int set
         }
         FSTAMP_END(L, 1)
     };
+    // `pub` (the seed loop): every joint the annotation holds, as (x, y, v, scale) in LDS as
+    // soon as it is set, and its bit in *pub_mask -- a grow in flight shows the helpers'
+    // plans which seeds its person's occupancy will cover (joints never change once set)
+    if (pub) {
+        if (lane < K && av > 0.0f) pub[lane] = make_float4(ax, ay, av, as);
+        const uint32_t m0 = (uint32_t)__ballot(lane < K && av > 0.0f);
+        if (lane == 0) __hip_atomic_store(pub_mask, m0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     for (int j = 0; j < K; j++) {  // seeding the frontier (cifcaf.py:288-291)
         const float vj = rl_f(av, j);
         if (vj == 0.0f) continue;
@@ -1337,7 +1347,10 @@ __device__ __forceinline__ void grow(const GrowArgs &g, LDS &L, int img, int set
             ay = got.y;
             av = got.v;
             as = got.s;
+            if (pub) pub[jti] = make_float4(got.x, got.y, got.v, got.s);
         }
+        if (pub && lane == 0)
+            __hip_atomic_fetch_or(pub_mask, 1u << jti, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (lane == 0) {
             if (ndec < kKP) {
                 L.a.decoding_pairs[ndec][0] = (uint8_t)jsi;
@@ -1772,6 +1785,20 @@ constexpr bool kW0Plan = true;
 #else
 constexpr bool kW0Plan = false;
 #endif
+// Grows in flight publish their joints as they are set (grow's `pub`), and the plans keep
+// seeds their occupancy boxes will cover away from the helpers (PP_NO_PARTIAL builds: only
+// the in-flight seeds' positions, kSpecFar apart).  Planted cfg3 (stamps, serial): at kernel
+// start about 4 of the 7 first picks are seeds the loop commits (tools/spec_sim.py).
+#ifdef PP_NO_PARTIAL
+constexpr bool kPartial = false;
+#else
+constexpr bool kPartial = true;
+#endif
+#ifdef PP_HELPER_PRIO
+constexpr bool kHelperPrio = true;
+#else
+constexpr bool kHelperPrio = false;
+#endif
 #ifdef PP_NO_SELF_PLAN  // A/B builds
 constexpr bool kSelfPlan = false;
 #else
@@ -1890,6 +1917,11 @@ struct SeedLoopSharedT {
     int cache_state[NSLOT];
     float4 cache_j[kSpecCache][kKP];  // its joints (x, y, v, scale); the external slots'
                                       // after the column stage in dynamic LDS (cache_joints)
+    // seed_loop_kernel: joints of a slot still being grown that are set already (bit j:
+    // cache_j[q][j] holds joint j; grow's `pub`), and the same for wave 0's own grow
+    uint32_t cache_pm[kSpecCache];
+    float4 own_j[kKP];
+    uint32_t own_pm;
     int done;
     // seed_loop_kernel's helper self-planning (spec_plan): the plan lock, the first seed not
     // yet decided by wave 0 (seeds before it were committed or skipped), and the seed wave 0
@@ -1917,6 +1949,9 @@ __device__ __forceinline__ int lds_acquire(int *p) {
 }
 __device__ __forceinline__ void lds_release(int *p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t lds_acquire_u(uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 __device__ __forceinline__ bool spec_far(float far, float xa, float ya, float sa, float xb,
@@ -1999,7 +2034,7 @@ __device__ __forceinline__ void ext_refresh(SeedLoopSharedX &S, float *s_cols, c
 // the grow's.
 // NS > kSpecCache (seed_loop_ext_kernel): slots kSpecCache.. are the external helpers'
 // (joints at xj, cache_joints); they are avoided like the others but never claimed here.
-template <int NS>
+template <int NS, bool PARTIAL = false>
 __device__ __noinline__ uint64_t spec_plan(SeedLoopSharedT<NS> &S, const float4 *xj,
                                            const pp_seed *seeds, int n_seeds, int first,
                                            int decided, int scan, OccGrid occ, float red,
@@ -2025,6 +2060,15 @@ __device__ __noinline__ uint64_t spec_plan(SeedLoopSharedT<NS> &S, const float4 
         // still being grown
         const int cxi = (int)clip_ref(c.x / red, 0.0f, (float)(occ.w - 1));
         const int cyi = (int)clip_ref(c.y / red, 0.0f, (float)(occ.h - 1));
+        // inside the occupancy box joint jq of an annotation will mark (occupancy.py:31-39)
+        auto covered = [&](const float4 &jq) {
+            int box[4];
+            return jq.z != 0.0f && occ_box_r(red, msr, occ, c.field, jq.x, jq.y, jq.w, box) &&
+                   cxi >= box[0] && cxi < box[1] && cyi >= box[2] && cyi < box[3];
+        };
+        if (ok && PARTIAL && own && ((lds_acquire_u(&S.own_pm) >> c.field) & 1u) &&
+            covered(S.own_j[c.field]))
+            ok = false;  // wave 0's own annotation in flight covers it
         for (int q = 0; q < NS; q++) {
             const int sq = S.cache_seed[q];
             const int st = S.cache_state[q];
@@ -2033,14 +2077,14 @@ __device__ __noinline__ uint64_t spec_plan(SeedLoopSharedT<NS> &S, const float4 
             if (!ok) continue;
             if ((fly >> q) & 1) {
                 ok = spec_far(far_k, c.x, c.y, c.s, S.cache_x[q], S.cache_y[q], S.cache_s[q]);
+                // the joints its grow has set so far
+                if (ok && PARTIAL && q < kSpecCache &&
+                    ((lds_acquire_u(&S.cache_pm[q]) >> c.field) & 1u) && covered(S.cache_j[q][c.field]))
+                    ok = false;
                 continue;
             }
             if (st != 2) continue;
-            const float4 jq = q < kSpecCache ? S.cache_j[q][c.field]
-                                             : xj[(q - kSpecCache) * kKP + c.field];
-            int box[4];
-            if (jq.z != 0.0f && occ_box_r(red, msr, occ, c.field, jq.x, jq.y, jq.w, box) &&
-                cxi >= box[0] && cxi < box[1] && cyi >= box[2] && cyi < box[3])
+            if (covered(q < kSpecCache ? S.cache_j[q][c.field] : xj[(q - kSpecCache) * kKP + c.field]))
                 ok = false;
         }
         uint64_t m = __ballot(ok);
@@ -2071,6 +2115,7 @@ __device__ __noinline__ uint64_t spec_plan(SeedLoopSharedT<NS> &S, const float4 
                 S.cache_x[q] = cx;
                 S.cache_y[q] = cy;
                 S.cache_s[q] = csc;
+                if (q < kSpecCache) S.cache_pm[q] = 0u;  // no joints of the new grow yet
                 lds_release(&S.cache_state[q], 1);
                 lds_release(&S.cache_seed[q], base + l);
                 S.task_slot[w] = q;
@@ -2252,6 +2297,7 @@ void seed_loop_kernel(GrowArgs g) {
     if (threadIdx.x < kSpecCache) {
         S.cache_seed[threadIdx.x] = -1;
         S.cache_state[threadIdx.x] = 0;
+        S.cache_pm[threadIdx.x] = 0u;
     }
     if (threadIdx.x < kSeedWaves) S.task[threadIdx.x] = -1;
     if (threadIdx.x == 0) {
@@ -2260,6 +2306,7 @@ void seed_loop_kernel(GrowArgs g) {
         S.decided = 0;
         S.own_on = 0;
         S.plan_req = 0;
+        S.own_pm = 0u;
     }
     __syncthreads();
 
@@ -2299,6 +2346,9 @@ void seed_loop_kernel(GrowArgs g) {
     };
 
     if (wave > 0) {  // helper: grow the seeds wave 0 hands over until it is done
+        // above the other kernels' waves sharing the CU (the front half and tail of the
+        // neighbouring batches), below the committer
+        if (kHelperPrio) __builtin_amdgcn_s_setprio(2);
         for (;;) {
             int my;
             for (;;) {
@@ -2314,8 +2364,9 @@ void seed_loop_kernel(GrowArgs g) {
                         const uint64_t idle = __ballot(lane > 0 && lane < kSeedWaves && tk < 0);
                         const int dec = lds_acquire(&S.decided);
                         if (idle)
-                            spec_plan(S, nullptr, seeds, n_seeds, dec, dec, kSpecScan, occ, red,
-                                      occ_msr(g), g.spec_far, idle, socc);
+                            spec_plan<kSpecCache, kPartial>(S, nullptr, seeds, n_seeds, dec, dec,
+                                                            kSpecScan, occ, red, occ_msr(g),
+                                                            g.spec_far, idle, socc);
                     }
                     plan_unlock(S);
                     continue;
@@ -2324,8 +2375,18 @@ void seed_loop_kernel(GrowArgs g) {
             }
             if (my < 0) break;
             const int q = S.task_slot[wave];
+#ifdef PP_STAMPS
+            const uint64_t hg0 = __builtin_amdgcn_s_memtime();
+#endif
             ann_from_seed(L, seeds[my], K, img);
-            grow<true, CS>(g, L, img, 0, true, cstage, &S.done);
+            grow<true, CS>(g, L, img, 0, true, cstage, &S.done, kPartial ? S.cache_j[q] : nullptr,
+                           kPartial ? &S.cache_pm[q] : nullptr);
+#ifdef PP_STAMPS
+            if (lane == 0) {  // helper grows and their cycles (phase-1 slots 8 and 5)
+                L.fst[4] += 1;
+                L.fst[5] += __builtin_amdgcn_s_memtime() - hg0;
+            }
+#endif
             if (lds_acquire(&S.done)) break;  // nobody reads the cache any more
             publish_cached(S, cache, q, L);
             // plan this wave's next grow itself, with its own annotation now in the cache (its
@@ -2335,8 +2396,8 @@ void seed_loop_kernel(GrowArgs g) {
             uint64_t left = 1ull << wave;
             if (kSelfPlan && !lds_acquire(&S.done)) {
                 const int dec = lds_acquire(&S.decided);
-                left = spec_plan(S, nullptr, seeds, n_seeds, dec, dec, kSelfScan, occ, red, occ_msr(g),
-                                 g.spec_far, left, socc);
+                left = spec_plan<kSpecCache, kPartial>(S, nullptr, seeds, n_seeds, dec, dec, kSelfScan,
+                                                       occ, red, occ_msr(g), g.spec_far, left, socc);
             }
             if (left && lane == 0) lds_release(&S.task[wave], -1);
             plan_unlock(S);
@@ -2374,6 +2435,7 @@ void seed_loop_kernel(GrowArgs g) {
             const pp_seed st = seeds[t];
             if (kW0Plan) plan_lock(S);
             if (lane == 0) {
+                S.own_pm = 0u;  // (grow publishes the seed joint first)
                 S.own_x = st.x;
                 S.own_y = st.y;
                 S.own_s = st.s;
@@ -2386,8 +2448,8 @@ void seed_loop_kernel(GrowArgs g) {
                 const int tk = lane > 0 && lane < kSeedWaves ? lds_acquire(&S.task[lane]) : 0;
                 const uint64_t idle = __ballot(lane > 0 && lane < kSeedWaves && tk < 0);
                 if (idle)
-                    spec_plan(S, nullptr, seeds, n_seeds, t + 1, t, kSpecScan, occ, red, occ_msr(g),
-                              g.spec_far, idle, socc);
+                    spec_plan<kSpecCache, kPartial>(S, nullptr, seeds, n_seeds, t + 1, t, kSpecScan,
+                                                    occ, red, occ_msr(g), g.spec_far, idle, socc);
                 plan_unlock(S);
             }
 #ifdef PP_STAMPS
@@ -2395,7 +2457,8 @@ void seed_loop_kernel(GrowArgs g) {
 #endif
             STAMP(1);
             ann_from_seed(L, st, K, img);
-            grow<true, CS>(g, L, img, 0, true, cstage);
+            grow<true, CS>(g, L, img, 0, true, cstage, nullptr, kPartial ? S.own_j : nullptr,
+                           kPartial ? &S.own_pm : nullptr);
             STAMP(2);
             commit(&L.a, lane < K ? L.a.data[lane][0] : 0.0f, lane < K ? L.a.data[lane][1] : 0.0f,
                    lane < K ? L.a.data[lane][2] : 0.0f, lane < K ? L.a.joint_scales[lane] : 0.0f);
@@ -2415,6 +2478,15 @@ void seed_loop_kernel(GrowArgs g) {
 #ifdef PP_STAMPS
         st_acc[6] = n_rounds;
         st_acc[7] = n_hits;
+        {  // helpers' grows (count into slot 8, cycles into slot 5 in place of occ_clear)
+            uint64_t hn = 0, hc = 0;
+            for (int w = 1; w < kSeedWaves; w++) {
+                hn += Ls[w].fst[4];
+                hc += Ls[w].fst[5];
+            }
+            L.fst[3] = hn;
+            st_acc[5] = hc;
+        }
 #endif
         STAMP_FLUSH(1);
         seed_loop_outputs(g, Ls, img, n_anns, unset_mask);
@@ -2850,8 +2922,12 @@ __global__ __launch_bounds__(64) void complete_kernel(GrowArgs g) {
 // seed loop instead of waiting for its CUs.  A/B on one box: planted cfg3 370-375k ->
 // 385-394k images/s, cfg5 uniform 1356-1365 -> 1434-1443; uniform cfg3 (400 annotations per
 // image, 17 planes on 4 waves) 15.1-15.3k -> 14.4-14.5k, hence the wide form there.
-constexpr int kNmsWaves = 8;   // also the per-image stride of the box-list scratch
+constexpr int kNmsWaves = 8;
 constexpr int kNmsNarrow = 4;
+// box-list scratch per image: one list per wave of nms_kernel, or per plane of
+// nms_planes_kernel's fallback
+constexpr int kNmsBoxLists = PP_MAX_KP;
+static_assert(kNmsBoxLists >= kNmsWaves, "one box list per NMS wave");
 // boxes per plane kept in REGISTERS, kNmsRegBoxes per lane (box i: lane i % 64, slot
 // i / 64), global scratch beyond: a check is ALU over the lane's slots plus one wave sum,
 // and the kernel needs no LDS for them (it fits beside the seed loop's 104 KB).  With the
@@ -2901,7 +2977,79 @@ __device__ __forceinline__ int occ_cell(const OccGrid &o, int f, float x, float 
     return -1;
 }
 
-template <int W>
+// nms.py:34-45 for plane f: the m kept annotations in sorted order, whose joint f
+// `load(r0, wi, x, y, v, s)` gives per lane (annotation r0 + lane: work index, joint f; v = 0
+// beyond m).  The plane's marked boxes are kept in a list instead of a u8 grid: kNmsRegBoxes
+// per lane in registers, `gbox` beyond.  A joint is "occupied" iff the number of earlier
+// marked boxes covering its cell is non-zero mod 256 (the grid's u8 += 1 wraps).  Suppressed
+// joints are written (v * suppression) as they are found.
+template <typename Load>
+__device__ __forceinline__ void nms_plane_boxes(const GrowArgs &g, pp_ann *work, int m, int f,
+                                                const OccGrid &no, float red, int2 *gbox,
+                                                Load load) {
+    const int lane = threadIdx.x & 63;
+    int nbox = 0;
+    int2 rb[kNmsRegBoxes];  // (x0 | x1 << 16, y0 | y1 << 16); zero: covers nothing
+#pragma unroll
+    for (int q = 0; q < kNmsRegBoxes; q++) rb[q] = make_int2(0, 0);
+    for (int r0 = 0; r0 < m; r0 += 64) {
+        int wi = 0;
+        float jx = 0.0f, jy = 0.0f, jv = 0.0f, js = 0.0f;
+        load(r0, wi, jx, jy, jv, js);
+        const int nr = min(64, m - r0);
+        for (int l = 0; l < nr; l++) {
+            const float v = rl_f(jv, l);
+            if (v == 0.0f) continue;
+            const float x = rl_f(jx, l), y = rl_f(jy, l);
+            int xi = 0, yi = 0;
+            const int fixed = occ_cell(no, f, x, y, red, xi, yi);
+            int cnt = 0;
+            if (fixed < 0) {
+#pragma unroll
+                for (int q = 0; q < kNmsRegBoxes; q += 4) {  // unused slots are zero
+                    if (q * 64 >= nbox) continue;  // uniform: skip empty groups
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int2 b = rb[q + u];
+                        cnt += (xi >= (b.x & 0xFFFF) && xi < (b.x >> 16) &&
+                                yi >= (b.y & 0xFFFF) && yi < (b.y >> 16));
+                    }
+                }
+                for (int q = kNmsRegBoxes * 64 + lane; q < nbox; q += 64) {
+                    const int2 b = gbox[q];
+                    cnt += (xi >= (b.x & 0xFFFF) && xi < (b.x >> 16) &&
+                            yi >= (b.y & 0xFFFF) && yi < (b.y >> 16));
+                }
+                cnt = wave_total(cnt);
+            }
+            const bool occupied = fixed < 0 ? (cnt & 255) != 0 : fixed == 1;
+            if (occupied) {
+                if (lane == 0) work[rl_i(wi, l)].data[f][2] = v * g.cfg.nms_suppression;
+            } else {
+                int box[4];
+                if (occ_box(g, no, f, x, y, rl_f(js, l), box)) {
+                    const int2 nb = make_int2(box[0] | (box[1] << 16), box[2] | (box[3] << 16));
+                    if (nbox < kNmsRegBoxes * 64) {
+#pragma unroll
+                        for (int q = 0; q < kNmsRegBoxes; q++)
+                            if (q == (nbox >> 6) && lane == (nbox & 63)) rb[q] = nb;
+                    } else if (lane == 0) {
+                        gbox[nbox] = nb;
+                    }
+                    nbox++;
+                    // only a box in global memory needs the fence (a fence here waits
+                    // for every outstanding store, e.g. the suppressed v above)
+                    if (nbox > kNmsRegBoxes * 64) wave_sync();
+                }
+            }
+        }
+    }
+}
+
+// PHASE 0: the whole of nms.Keypoints.annotations in one launch (suppression planes by
+// nms_plane_boxes); 1: up to the sorted keep list, whose count and occupancy-grid shape go
+// to the meta words (nms_planes_kernel runs the planes); 3: from the suppressed planes on.
+template <int W, int PHASE = 0>
 __global__ __launch_bounds__(64 * W) void nms_kernel(GrowArgs g) {
     __shared__ ScoreLDS Ls[W];
     __shared__ int s_m, s_m2, s_status;
@@ -2917,12 +3065,12 @@ __global__ __launch_bounds__(64 * W) void nms_kernel(GrowArgs g) {
     int *keep = g.nms_idx + (int64_t)img * (4 * cap + g.ann_np);  // kept work indices
     int *surv = keep + cap;                                           // survivors
     int *flag = surv + cap;                                           // per-index pass flags
-    int *perm2 = flag + cap;                                          // (unused pad)
+    int *perm2 = flag + cap;                                          // meta: m, grid h, w
     int *perm = perm2 + cap;                                          // sort permutation
     double *score = g.nms_score + (int64_t)img * 2 * cap;             // by work index
     double *kscore = score + cap;                                     // by kept / survivor rank
     float *amax = g.nms_f + (int64_t)img * 2 * cap;                   // per-ann max x, max y
-    int2 *gbox = g.nms_box + ((int64_t)img * kNmsWaves + wave) * cap;
+    int2 *gbox = g.nms_box + ((int64_t)img * kNmsBoxLists + wave) * cap;
     const float red = (float)g.cfg.occupancy_reduction;
     const float kt = g.cfg.nms_keypoint_threshold;
     const double it = (double)g.cfg.nms_instance_threshold;
@@ -2937,7 +3085,7 @@ __global__ __launch_bounds__(64 * W) void nms_kernel(GrowArgs g) {
     __syncthreads();
     STAMP_DECL
 
-    if (!g.cfg.apply_nms) {
+    if (PHASE == 0 && !g.cfg.apply_nms) {
         for (int i = wave; i < n_anns; i += W) {
             copy_ann(&out[i], &work[i]);
             const double sc = ann_score_w(L, work[i].data, K);
@@ -2954,6 +3102,8 @@ __global__ __launch_bounds__(64 * W) void nms_kernel(GrowArgs g) {
         return;
     }
 
+    int m = 0;
+    if constexpr (PHASE != 3) {
     // nms.py:20-22: zero joints below keypoint_threshold, drop low scores (per annotation)
     for (int i = wave; i < n_anns; i += W) {
         pp_ann &a = work[i];
@@ -3022,9 +3172,26 @@ __global__ __launch_bounds__(64 * W) void nms_kernel(GrowArgs g) {
     }
     __syncthreads();
     STAMP(3);
-    const int m = s_m;
+    m = s_m;
+    } else {
+        m = perm2[0];
+    }
+    if constexpr (PHASE == 1) {
+        if (threadIdx.x == 0) {
+            perm2[0] = m;
+            perm2[1] = perm2[2] = 0;
+            if (m > 0) {  // Occupancy((K, int(max y + 1), int(max x + 1)), 2, min_scale=4)
+                const long oh = (long)((double)(long)(s_my + 1.0f) / g.cfg.occupancy_reduction);
+                const long ow = (long)((double)(long)(s_mx + 1.0f) / g.cfg.occupancy_reduction);
+                perm2[1] = (int)(oh > 0 ? oh : 0);
+                perm2[2] = (int)(ow > 0 ? ow : 0);
+            }
+        }
+        return;
+    }
     int n_out = 0;
     if (m > 0) {
+        if constexpr (PHASE == 0) {
         // Occupancy((K, int(max y + 1), int(max x + 1)), 2, min_scale=4)
         const long oh = (long)((double)(long)(s_my + 1.0f) / g.cfg.occupancy_reduction);
         const long ow = (long)((double)(long)(s_mx + 1.0f) / g.cfg.occupancy_reduction);
@@ -3047,14 +3214,9 @@ __global__ __launch_bounds__(64 * W) void nms_kernel(GrowArgs g) {
             }
         }
         for (int f = wave, u = 0; f < K; f += W, u++) {  // nms.py:34-45, one plane per pass
-            int nbox = 0;
-            int2 rb[kNmsRegBoxes];  // (x0 | x1 << 16, y0 | y1 << 16); zero: covers nothing
-#pragma unroll
-            for (int q = 0; q < kNmsRegBoxes; q++) rb[q] = make_int2(0, 0);
-            for (int r0 = 0; r0 < m; r0 += 64) {
+            nms_plane_boxes(g, work, m, f, no, red, gbox, [&](int r0, int &wi, float &jx, float &jy,
+                                                                float &jv, float &js) {
                 const int r = r0 + lane;
-                int wi = 0;
-                float jx = 0.0f, jy = 0.0f, jv = 0.0f, js = 0.0f;
                 if (r0 == 0 && u < kNmsPre) {  // prefetched (selects: no dynamic index)
                     wi = wi0;
 #pragma unroll
@@ -3072,57 +3234,11 @@ __global__ __launch_bounds__(64 * W) void nms_kernel(GrowArgs g) {
                     jv = work[wi].data[f][2];
                     js = work[wi].joint_scales[f];
                 }
-                const int nr = min(64, m - r0);
-                for (int l = 0; l < nr; l++) {
-                    const float v = rl_f(jv, l);
-                    if (v == 0.0f) continue;
-                    const float x = rl_f(jx, l), y = rl_f(jy, l);
-                    int xi = 0, yi = 0;
-                    const int fixed = occ_cell(no, f, x, y, red, xi, yi);
-                    int cnt = 0;
-                    if (fixed < 0) {
-#pragma unroll
-                        for (int q = 0; q < kNmsRegBoxes; q += 4) {  // unused slots are zero
-                            if (q * 64 >= nbox) continue;  // uniform: skip empty groups
-#pragma unroll
-                            for (int u = 0; u < 4; u++) {
-                                const int2 b = rb[q + u];
-                                cnt += (xi >= (b.x & 0xFFFF) && xi < (b.x >> 16) &&
-                                        yi >= (b.y & 0xFFFF) && yi < (b.y >> 16));
-                            }
-                        }
-                        for (int q = kNmsRegBoxes * 64 + lane; q < nbox; q += 64) {
-                            const int2 b = gbox[q];
-                            cnt += (xi >= (b.x & 0xFFFF) && xi < (b.x >> 16) &&
-                                    yi >= (b.y & 0xFFFF) && yi < (b.y >> 16));
-                        }
-                        cnt = wave_total(cnt);
-                    }
-                    const bool occupied = fixed < 0 ? (cnt & 255) != 0 : fixed == 1;
-                    if (occupied) {
-                        if (lane == 0) work[rl_i(wi, l)].data[f][2] = v * g.cfg.nms_suppression;
-                    } else {
-                        int box[4];
-                        if (occ_box(g, no, f, x, y, rl_f(js, l), box)) {
-                            const int2 nb = make_int2(box[0] | (box[1] << 16), box[2] | (box[3] << 16));
-                            if (nbox < kNmsRegBoxes * 64) {
-#pragma unroll
-                                for (int q = 0; q < kNmsRegBoxes; q++)
-                                    if (q == (nbox >> 6) && lane == (nbox & 63)) rb[q] = nb;
-                            } else if (lane == 0) {
-                                gbox[nbox] = nb;
-                            }
-                            nbox++;
-                            // only a box in global memory needs the fence (a fence here waits
-                            // for every outstanding store, e.g. the suppressed v above)
-                            if (nbox > kNmsRegBoxes * 64) wave_sync();
-                        }
-                    }
-                }
-            }
+            });
         }
         __syncthreads();
         STAMP(4);
+        }
         // nms.py:51-53 in sorted order: zero low joints, drop low scores
         for (int r = wave; r < m; r += W) {
             pp_ann &a = work[keep[perm[r]]];
@@ -3187,6 +3303,128 @@ __global__ __launch_bounds__(64 * W) void nms_kernel(GrowArgs g) {
         g.counts[img] = n_out;
         g.status[img] = s_status;
     }
+}
+
+}  // namespace pp
+
+namespace pp {
+
+// ---- nms.py:34-45 per (image, plane), the plane's occupancy as a bitmap in LDS ----
+// Between nms_kernel<W, 1> (the sorted keep list, its count and grid shape in the meta words)
+// and nms_kernel<W, 3> (the refilter and output): one wave per (image, joint plane), walking
+// the image's kept annotations in sorted order.  The reference's grid holds u8 counts and a
+// joint is occupied iff its cell's count is non-zero (mod 256: += 1 wraps).  Here a cell is
+// one bit, set when a marked box covers it: the same answer while no cell is covered by 256
+// boxes or more.  Counts of the boxes meeting each 32 x 32-cell block (never below any of
+// its cells' counts) guard that: a plane where a block reaches 256 boxes is decided again by
+// nms_plane_boxes (the exact counting form), which also takes grids larger than the LDS
+// bitmap (keypoints far outside the field).  Suppressed joints are written only after the
+// plane is decided.  A check is one LDS word, a mark one OR per (box row, word): O(m) per
+// plane instead of nms_plane_boxes' O(m * marked boxes / 64).
+constexpr int kNmsBlk = 32;
+
+struct NmsBitmapGeo {  // the LDS bitmap's capacity (the launch's dynamic LDS)
+    int cap_h, cap_w;  // grid rows and columns it holds
+    __host__ __device__ int wpr() const { return (cap_w + 31) >> 5; }
+    __host__ __device__ int blocks() const {
+        return ((cap_h + kNmsBlk - 1) / kNmsBlk) * ((cap_w + kNmsBlk - 1) / kNmsBlk);
+    }
+    __host__ __device__ size_t bytes(int ann_cap) const {
+        return sizeof(uint32_t) * ((size_t)cap_h * wpr() + blocks() + (ann_cap + 31) / 32);
+    }
+};
+
+__global__ __launch_bounds__(64) void nms_planes_kernel(GrowArgs g, NmsBitmapGeo geo) {
+    extern __shared__ uint32_t s_bm[];
+    const int img = blockIdx.x, f = blockIdx.y;
+    const int lane = threadIdx.x;
+    const int K = g.K, cap = g.ann_cap;
+    pp_ann *work = g.work + (int64_t)img * cap;
+    const int *keep = g.nms_idx + (int64_t)img * (4 * cap + g.ann_np);
+    const int *meta = keep + 3 * cap;  // nms_kernel<W, 1>: m, grid h, grid w
+    const int *perm = meta + cap;
+    const int m = meta[0], oh = meta[1], ow = meta[2];
+    if (m <= 0 || f >= K) return;
+    const float red = (float)g.cfg.occupancy_reduction;
+    const OccGrid no = occ_grid(nullptr, K, oh, ow);
+    auto load = [&](int r0, int &wi, float &jx, float &jy, float &jv, float &js) {
+        const int r = r0 + lane;
+        if (r < m) {
+            wi = keep[perm[r]];
+            jx = work[wi].data[f][0];
+            jy = work[wi].data[f][1];
+            jv = work[wi].data[f][2];
+            js = work[wi].joint_scales[f];
+        }
+    };
+    int2 *gbox = g.nms_box + ((int64_t)img * kNmsBoxLists + f) * cap;
+    if (oh <= 0 || ow <= 0 || oh > geo.cap_h || ow > geo.cap_w) {
+        nms_plane_boxes(g, work, m, f, no, red, gbox, load);
+        return;
+    }
+    const int wpr = (ow + 31) >> 5;
+    const int bcols = (ow + kNmsBlk - 1) / kNmsBlk;
+    uint32_t *bits = s_bm;                                // oh rows of wpr words
+    uint32_t *bcnt = s_bm + (size_t)geo.cap_h * geo.wpr();  // boxes per block
+    uint32_t *supp = bcnt + geo.blocks();                   // suppressed ranks
+    const int nbits = oh * wpr, nblk = ((oh + kNmsBlk - 1) / kNmsBlk) * bcols;
+    for (int i = lane; i < nbits; i += 64) bits[i] = 0u;
+    for (int i = lane; i < nblk; i += 64) bcnt[i] = 0u;
+    for (int i = lane; i < (m + 31) / 32; i += 64) supp[i] = 0u;
+    wave_sync();
+    bool over = false;
+    for (int r0 = 0; r0 < m; r0 += 64) {
+        int wi = 0;
+        float jx = 0.0f, jy = 0.0f, jv = 0.0f, js = 0.0f;
+        load(r0, wi, jx, jy, jv, js);
+        // per lane: its joint's cell, and the box it marks when free (0: none)
+        int xi = 0, yi = 0;
+        (void)occ_cell(no, f, jx, jy, red, xi, yi);  // -1: f < K and a non-empty grid
+        int box[4] = {0, 0, 0, 0};
+        const bool hb = r0 + lane < m && jv != 0.0f && occ_box(g, no, f, jx, jy, js, box);
+        const int cellp = xi | (yi << 16);
+        const int bxp = hb ? box[0] | (box[1] << 16) : 0;  // x1 >= 1 when hb: nonzero
+        const int byp = box[2] | (box[3] << 16);
+        const int nr = min(64, m - r0);
+        for (int l = 0; l < nr; l++) {
+            if (rl_f(jv, l) == 0.0f) continue;
+            const int cp = rl_i(cellp, l);
+            const int cx = cp & 0xFFFF, cy = cp >> 16;
+            if ((bits[cy * wpr + (cx >> 5)] >> (cx & 31)) & 1u) {  // occupied
+                if (lane == 0) atomicOr(&supp[(r0 + l) >> 5], 1u << ((r0 + l) & 31));
+                continue;
+            }
+            const int bx = rl_i(bxp, l);
+            if (bx == 0) continue;  // no box (empty after clipping)
+            const int by = rl_i(byp, l);
+            const int x0 = bx & 0xFFFF, x1 = bx >> 16, y0 = by & 0xFFFF, y1 = by >> 16;
+            const int w0 = x0 >> 5, nw = ((x1 - 1) >> 5) - w0 + 1;
+            const int items = (y1 - y0) * nw;
+            for (int t = lane; t < items; t += 64) {  // (box row, word) pairs
+                const int ry = y0 + t / nw, wq = w0 + t % nw;
+                const int lo = max(x0 - 32 * wq, 0), hi = min(x1 - 32 * wq, 32);
+                const uint32_t mk = (hi - lo >= 32) ? ~0u : (((1u << (hi - lo)) - 1u) << lo);
+                atomicOr(&bits[ry * wpr + wq], mk);
+            }
+            const int bx0 = x0 / kNmsBlk, bx1 = (x1 - 1) / kNmsBlk;
+            const int by0 = y0 / kNmsBlk, by1 = (y1 - 1) / kNmsBlk;
+            const int nbk = (bx1 - bx0 + 1) * (by1 - by0 + 1);
+            for (int t = lane; t < nbk; t += 64) {  // the guard: boxes per block
+                const int bq = (by0 + t / (bx1 - bx0 + 1)) * bcols + bx0 + t % (bx1 - bx0 + 1);
+                over |= atomicAdd(&bcnt[bq], 1u) >= 255u;
+            }
+            wave_sync();  // the marks before the next check
+        }
+    }
+    if (__ballot(over)) {  // a cell may have wrapped: decide the plane by counting
+        nms_plane_boxes(g, work, m, f, no, red, gbox, load);
+        return;
+    }
+    for (int r = lane; r < m; r += 64)  // nms.py:43: data[f, 2] *= suppression
+        if ((supp[r >> 5] >> (r & 31)) & 1u) {
+            float *v = &work[keep[perm[r]]].data[f][2];
+            *v = *v * g.cfg.nms_suppression;
+        }
 }
 
 }  // namespace pp
@@ -3272,7 +3510,7 @@ static DecodeLayout make_layout(int n_img, int K, int C, const Heads &h, const p
     d.off_nms_score = take(n * 2 * ann_cap * sizeof(double));
     d.off_nms_idx = take(n * (4 * ann_cap + d.ann_np) * sizeof(int));
     d.off_nms_f = take(n * 2 * ann_cap * sizeof(float));
-    d.off_nms_box = take(n * kNmsWaves * ann_cap * sizeof(int2));
+    d.off_nms_box = take(n * kNmsBoxLists * ann_cap * sizeof(int2));
     d.total = o;
     return d;
 }
@@ -3398,6 +3636,61 @@ static int seed_ext_per_image(int n_img) {
     }
     if (n_img <= 0 || cus[dev] <= 0) return 0;
     return std::max(0, std::min(kExtWgMax, cus[dev] / n_img - 1));
+}
+
+// Force-complete workgroups per image: kCompleteWays for batches the caller marks dense
+// (PP_STAGE_NMS_WIDE), else kCompleteWaysSparse; PP_COMPLETE_WAYS overrides the latter
+// (A/B builds).  The workgroups pull annotations from a per-image counter, so any count
+// gives the same result.
+static int complete_ways(uint32_t stages) {
+    static const int env = [] {
+        const char *e = getenv("PP_COMPLETE_WAYS");
+        return e ? atoi(e) : 0;
+    }();
+    if (stages & PP_STAGE_NMS_WIDE) return kCompleteWays;
+    return env > 0 ? std::min(env, 1024) : kCompleteWaysSparse;
+}
+
+// nms.Keypoints (nms.py:17-57) of a decode: nms_kernel<W> in one launch, or with `bitmap`
+// (PP_STAGE_NMS_BITMAP, or PP_NMS_BITMAP=1 for every call) nms_kernel<W, 1>, the planes as
+// bitmaps (nms_planes_kernel, one wave per (image, plane)), nms_kernel<W, 3> -- unless NMS
+// is off or the bitmap would not fit kNmsBitmapLds.  `wide`: 8-wave workgroups
+// (PP_STAGE_NMS_WIDE).  The bitmap holds the nominal grid (CifHr map / reduction) plus
+// kNmsMargin cells; an image whose keypoints reach further takes nms_plane_boxes in the
+// plane kernel.  Measured (round 5, one box): the three launches take 60 vs 76 us per planted
+// cfg3 step and 1.48 vs 2.51 ms per uniform one, one step at a time; but in the overlapped
+// pipeline planted 397k-402k vs 405k-410k and uniform 14.7k vs 15.5k-15.8k images/s (the
+// 4352 one-wave workgroups of the plane kernel beside the next batch's seed loop), so the
+// single launch stays the default.
+constexpr int kNmsMargin = 16;
+constexpr size_t kNmsBitmapLds = 64 * 1024;
+
+static int launch_nms(const GrowArgs &g, int n_img, bool wide, bool bitmap, hipStream_t s) {
+    static const bool bitmap_env = [] {
+        const char *e = getenv("PP_NMS_BITMAP");
+        return e && e[0] == '1';
+    }();
+    NmsBitmapGeo geo{};
+    geo.cap_h = (int)((double)g.hh / g.cfg.occupancy_reduction) + kNmsMargin;
+    geo.cap_w = (int)((double)g.ww / g.cfg.occupancy_reduction) + kNmsMargin;
+    const size_t lds = geo.bytes(g.ann_cap);
+    if ((bitmap || bitmap_env) && g.cfg.apply_nms && lds <= kNmsBitmapLds) {
+        if (wide)
+            hipLaunchKernelGGL((nms_kernel<kNmsWaves, 1>), dim3(n_img), dim3(64 * kNmsWaves), 0, s, g);
+        else
+            hipLaunchKernelGGL((nms_kernel<kNmsNarrow, 1>), dim3(n_img), dim3(64 * kNmsNarrow), 0, s, g);
+        hipLaunchKernelGGL(nms_planes_kernel, dim3(n_img, g.K), dim3(64), lds, s, g, geo);
+        if (wide)
+            hipLaunchKernelGGL((nms_kernel<kNmsWaves, 3>), dim3(n_img), dim3(64 * kNmsWaves), 0, s, g);
+        else
+            hipLaunchKernelGGL((nms_kernel<kNmsNarrow, 3>), dim3(n_img), dim3(64 * kNmsNarrow), 0, s, g);
+        return check_launch("pp_decode_batch(nms)");
+    }
+    if (wide)
+        hipLaunchKernelGGL(nms_kernel<kNmsWaves>, dim3(n_img), dim3(64 * kNmsWaves), 0, s, g);
+    else
+        hipLaunchKernelGGL(nms_kernel<kNmsNarrow>, dim3(n_img), dim3(64 * kNmsNarrow), 0, s, g);
+    return check_launch("pp_decode_batch(nms)");
 }
 
 // optional inputs of pp_decode_initial
@@ -3660,20 +3953,17 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
             if (rc) return rc;
         }
         if (run_complete && cfg->force_complete) {
+            const dim3 grid(n_img, complete_ways(stages));
             if (g.has_cs)
-                hipLaunchKernelGGL(complete_kernel<true>, dim3(n_img, kCompleteWays), dim3(64), 0, s, g);
+                hipLaunchKernelGGL(complete_kernel<true>, grid, dim3(64), 0, s, g);
             else
-                hipLaunchKernelGGL(complete_kernel<false>, dim3(n_img, kCompleteWays), dim3(64), 0, s, g);
+                hipLaunchKernelGGL(complete_kernel<false>, grid, dim3(64), 0, s, g);
             rc = check_launch("pp_decode_batch(force complete)");
             if (rc) return rc;
         }
-        if (run_nms) {
-            if ((stages & PP_STAGE_NMS_WIDE) && g.n_ext == 0)
-                hipLaunchKernelGGL(nms_kernel<kNmsWaves>, dim3(n_img), dim3(64 * kNmsWaves), 0, s, g);
-            else
-                hipLaunchKernelGGL(nms_kernel<kNmsNarrow>, dim3(n_img), dim3(64 * kNmsNarrow), 0, s, g);
-            rc = check_launch("pp_decode_batch(nms)");
-        }
+        if (run_nms)
+            rc = launch_nms(g, n_img, (stages & PP_STAGE_NMS_WIDE) && g.n_ext == 0,
+                            (stages & PP_STAGE_NMS_BITMAP) != 0, s);
 #ifdef PP_STAMPS
         hipStreamSynchronize(s);
         const size_t nst = (size_t)n_img * 3 * 12;

@@ -31,6 +31,8 @@ STAGE_COMPLETE_ONLY, STAGE_NMS_ONLY = 128, 256
 # PP_STAGE_NMS_WIDE: NMS in 8-wave workgroups (dense batches; the 4-wave default fits beside
 # a seed loop on a CU)
 STAGE_NMS_WIDE = 512
+# PP_STAGE_NMS_BITMAP: NMS planes as LDS bitmaps, one wave per (image, plane) (opt-in)
+STAGE_NMS_BITMAP = 1024
 
 
 def default_ann_capacity(h, w):
@@ -560,7 +562,7 @@ class DecodePipeline:
         """Enqueue one batch (cif / caf, or a multi-scale HeadSet `heads`).  `events`
         (five torch.cuda.Events, optional) are recorded around the CifHr stage, the other
         front stages (front stream), at the seed loop's start (back stream) and at the end
-        of NMS (tail stream)."""
+        of NMS (tail stream); a sixth one, if given, at the seed loop's end (back stream)."""
         par = self._i % self.depth
         self._i += 1
         eng = self.engines[par]
@@ -605,12 +607,14 @@ class DecodePipeline:
             if events:
                 events[3].record()
             launch(STAGE_GROW | early | STAGE_SEED_LOOP_ONLY)
+            if events and len(events) > 5:
+                events[5].record()
             loop_done = torch.cuda.Event()
             loop_done.record()
         self.tail.wait_event(loop_done)
         with torch.cuda.stream(self.tail):
             if _SPLIT_TAIL:
-                launch(STAGE_GROW | early | STAGE_AFTER_SEED_LOOP | STAGE_COMPLETE_ONLY)
+                launch(STAGE_GROW | early | STAGE_AFTER_SEED_LOOP | STAGE_COMPLETE_ONLY | wide)
                 sets_done = torch.cuda.Event()
                 sets_done.record()
                 b = launch(STAGE_GROW | early | STAGE_AFTER_SEED_LOOP | STAGE_NMS_ONLY | wide)

@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 
 from openpifpaf_amd import constants, synthetic
-from openpifpaf_amd._abi import EVAL_CONFIG, PACK_ALL, make_config
+from openpifpaf_amd._abi import EVAL_CONFIG, PACK_ALL, make_config, packed_dtype
 
 
 @pytest.mark.gpu
@@ -94,3 +94,34 @@ def test_pipeline_wide_nms_matches_engine_decode(n_img):
         recs, offsets = p.result()
         np.testing.assert_array_equal(offsets, off0)
         assert recs.tobytes() == recs0.tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('kind', ['planted', 'uniform', 'far'])
+def test_nms_bitmap_matches_box_lists(kind):
+    """PP_STAGE_NMS_BITMAP (the occupancy planes as LDS bitmaps, one wave per (image, plane),
+    nms_planes_kernel) gives the single-launch NMS's records byte for byte; 'far' moves CAF
+    targets far right so force-complete puts joints beyond the bitmap's grid, which those
+    planes decide with the box lists instead."""
+    import torch
+    from openpifpaf_amd.engine import STAGE_ALL, STAGE_NMS_BITMAP, DecodeEngine
+    skel = constants.COCO_PERSON_SKELETON
+    cfg = make_config(**EVAL_CONFIG)
+    kw = {'n_caf': len(skel)} if kind == 'uniform' else {'skeleton': skel, 'n_people': 8}
+    cif, caf = synthetic.batch('uniform' if kind == 'uniform' else 'planted', 6, 40, 40,
+                               first_seed=31, **kw)
+    if kind == 'far':
+        caf[:, 3:6, 5, :, 20:] += 120.0  # x2 of three limbs, right half of the field
+    cif, caf = torch.from_numpy(cif).cuda(), torch.from_numpy(caf).cuda()
+    recs = []
+    for stages in (STAGE_ALL, STAGE_ALL | STAGE_NMS_BITMAP):
+        eng = DecodeEngine()
+        b = eng.launch(cif, caf, skel, cfg, cap=1024, stages=stages)
+        r, off = DecodeEngine.fetch(b, (17, len(skel), PACK_ALL))
+        recs.append((r.tobytes(), off.copy(), b.status.cpu().numpy().copy()))
+    assert not recs[0][2].any()
+    np.testing.assert_array_equal(recs[0][1], recs[1][1])
+    assert recs[0][0] == recs[1][0]
+    if kind == 'far':
+        r = np.frombuffer(recs[0][0], dtype=packed_dtype(17, len(skel), PACK_ALL))
+        assert (r['data'][:, :, 0] > 400).any()  # joints beyond the nominal 160-px map

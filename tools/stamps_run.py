@@ -15,7 +15,8 @@ from openpifpaf_amd import constants, synthetic  # noqa: E402
 from openpifpaf_amd._abi import EVAL_CONFIG, make_config  # noqa: E402
 from openpifpaf_amd.engine import DecodeEngine  # noqa: E402
 
-P1 = ['seed_scan', 'plan', 'round_grow', 'commit+mark', 'cache_commit', 'occ_clear']
+P1 = ['seed_scan', 'plan', 'round_grow', 'commit+mark', 'cache_commit', 'helper grow cyc']
+# (seed_loop_kernel: slot 5 = the helpers' grow cycles, slot 8 = their grow count)
 # phase 1 slots 6 / 7: rounds (grows on wave 0) and annotations taken from the cache
 P2 = ['load', 'complete']  # summed over the image's kCompleteWays workgroups
 P3 = ['load', '-', 'nms_filter', 'nms_sort', 'nms_occ', 'nms_clear', 'nms_refilter',
@@ -45,14 +46,14 @@ for case in cases:
     st = np.fromfile(out, dtype=np.uint64).reshape(-1, n, 3, 12)[-1].astype(np.float64)
     print('== {} (mean shader cycles per image)'.format(case))
     for ph, names in ((0, P1), (1, P2), (2, P3)):
-        tot = st[:, ph, :min(len(names), 6 if ph == 0 else 8)].sum(axis=1).mean()
+        tot = st[:, ph, :min(len(names), 5 if ph == 0 else 8)].sum(axis=1).mean()
         print('  phase {} total {:.3e}'.format(ph + 1, tot))
         for i, name in enumerate(names):
             m = st[:, ph, i].mean()
             print('    {:14s} {:12.0f}  {:5.1f}%'.format(name, m, 100 * m / max(tot, 1)))
         if ph == 0:
             print('    rounds {:.1f}  cache hits {:.1f}'.format(st[:, 0, 6].mean(), st[:, 0, 7].mean()))
-            per = st[:, 0, :6].sum(axis=1)
+            per = st[:, 0, :5].sum(axis=1)
             w = int(np.argmax(per))
             print('    per-image total: p50 {:.3e} p90 {:.3e} max {:.3e} (image {}: rounds {:.0f}, '
                   'hits {:.0f}, round_grow {:.3e})'.format(
@@ -66,6 +67,6 @@ for case in cases:
             print('    corr(cycles, anns) {:.2f}  corr(cycles, rounds) {:.2f}  corr(cycles, seed cells) {:.2f}'.format(
                 np.corrcoef(per, n_ann)[0, 1], np.corrcoef(per, st[:, 0, 6])[0, 1],
                 np.corrcoef(per, n_seed_cells)[0, 1]))
-        for i, name in ((8, 'n connection'), (9, 'in-grow pop'), (10, 'in-grow connection'),
+        for i, name in ((8, 'n connection' if ph else 'helper grows'), (9, 'in-grow pop'), (10, 'in-grow connection'),
                         (11, 'in-grow add')):
             print('    {:14s} {:12.0f}'.format(name, st[:, ph, i].mean()))
