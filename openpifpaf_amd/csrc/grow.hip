@@ -3944,8 +3944,14 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
             if (rc) return rc;
         }
         // PP_STAGE_COMPLETE_ONLY / PP_STAGE_NMS_ONLY split the rest once more
-        const bool run_complete = run_rest && !(stages & PP_STAGE_NMS_ONLY);
-        const bool run_nms = run_rest && !(stages & PP_STAGE_COMPLETE_ONLY);
+        // PP_DIAG_SKIP (diagnostics only, wrong results): bit 1 skips force-complete and its
+        // lazy sets, bit 2 NMS -- how much of a pipelined step each stage costs
+        static const int diag_skip = [] {
+            const char *e = getenv("PP_DIAG_SKIP");
+            return e ? atoi(e) : 0;
+        }();
+        const bool run_complete = run_rest && !(stages & PP_STAGE_NMS_ONLY) && !(diag_skip & 1);
+        const bool run_nms = run_rest && !(stages & PP_STAGE_COMPLETE_ONLY) && !(diag_skip & 2);
         if (run_complete && cfg->force_complete && !(stages & PP_STAGE_COMPLETE_SETS_EARLY)) {
             // complete_annotations' CafScored(score_th=0.0001) only where phase 1 left work
             rc = launch_caf_bucketed(h, hr, n_img, K, C, skeleton, cfg, cfg->complete_caf_threshold,

@@ -1,7 +1,7 @@
 # A/B of library variants on one box (openpifpaf_amd.build VARIANTS; '-' = the product):
 # the default bench line without the CPU leg, each variant twice in alternation.
 # Usage (via gpurun): bash tools/gpu_ab.sh <tag> - base noself PP_PIPE_BFIRST=lazy ...
-# (an item with '=' is an environment setting for the product library)
+# (an item with '=' is an environment setting for the product library; several joined by ',')
 set -u
 TAG=$1
 shift
@@ -11,8 +11,8 @@ for rep in 1 2; do
   for v in "$@"; do
     lv="$v"; ev="PP_AB_NONE=1"
     [ "$v" = "-" ] && lv=""
-    case "$v" in *=*) ev="$v"; lv="";; esac
-    env "$ev" PP_LIB_VARIANT=$lv timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-multi \
+    case "$v" in *=*) ev="${v//,/ }"; lv="";; esac
+    env $ev PP_LIB_VARIANT=$lv timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-multi \
       > gpurun_out/ab_${TAG}_${v}_${rep}.json 2> gpurun_out/ab_${TAG}_${v}_${rep}.err || exit $?
     python3 - gpurun_out/ab_${TAG}_${v}_${rep}.json "$v" <<'PY'
 import json, sys
