@@ -408,13 +408,32 @@ int pp_fields_from_conv(const float *d_conv, int32_t n_img, int32_t n_fields, in
  * d_out (n_img, ann_capacity) with their score set, d_out_counts (n_img), and optionally
  * d_out_index (n_img, ann_capacity) = the input index of each survivor.  Uses cfg's
  * nms_* thresholds and occupancy_reduction / occupancy_min_scale.  Scores are the
- * default Annotation.score() (no fixed_score, no suppress_score_index).
+ * default Annotation.score() (annotation.py:60-71 without fixed_score or
+ * suppress_score_index).
  */
 size_t pp_nms_workspace_size(int32_t n_img, int32_t ann_capacity);
 int pp_nms_keypoints(pp_ann *d_anns, const int32_t *d_counts, int32_t n_img, int32_t K,
                      int32_t ann_capacity, const pp_config *cfg, pp_ann *d_out,
                      int32_t *d_out_counts, int32_t *d_out_index, void *d_workspace,
                      size_t workspace_bytes, void *stream);
+
+/*
+ * pp_nms_keypoints with each record's own Annotation.score() (annotation.py:60-71), for
+ * annotations carrying fixed_score, suppress_score_index or non-default score_weights
+ * (nms.py:21, 33, 53-54 sort and filter by it).  Per (image, record), laid out like d_anns:
+ * d_score_spec -2 = fixed_score (d_fixed_score holds it), -1 = none, j in [0, K) =
+ * suppress_score_index (v[j] reads as 0, negative Python indices normalised by the
+ * caller); d_score_weights (n_img, ann_capacity, K) float64 = the record's score_weights;
+ * d_fixed_score (n_img, ann_capacity) float64.  instance_threshold replaces cfg's float32
+ * nms_instance_threshold: the reference compares score() >= it in float64 (a fixed_score
+ * equal to the threshold is kept).  NULL d_score_spec = the default score().
+ */
+int pp_nms_keypoints_scored(pp_ann *d_anns, const int32_t *d_counts, int32_t n_img, int32_t K,
+                            int32_t ann_capacity, const pp_config *cfg,
+                            double instance_threshold, const int32_t *d_score_spec, const double *d_score_weights,
+                            const double *d_fixed_score, pp_ann *d_out, int32_t *d_out_counts,
+                            int32_t *d_out_index, void *d_workspace, size_t workspace_bytes,
+                            void *stream);
 
 /*
  * Packs a decode's records (d_anns (n_img, ann_capacity), d_counts[i] valid in slot row i)

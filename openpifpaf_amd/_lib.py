@@ -22,6 +22,7 @@ _i32 = ctypes.c_int32
 _i64 = ctypes.c_int64
 _u32 = ctypes.c_uint32
 _f = ctypes.c_float
+_f64 = ctypes.c_double
 _sz = ctypes.c_size_t
 
 _SIGNATURES = {
@@ -93,6 +94,8 @@ _SIGNATURES = {
     'pp_fields_from_conv': ([_vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp], ctypes.c_int),
     'pp_nms_keypoints': ([_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _sz, _vp],
                          ctypes.c_int),
+    'pp_nms_keypoints_scored': ([_vp, _vp, _i32, _i32, _i32, _vp, _f64, _vp, _vp, _vp, _vp,
+                                 _vp, _vp, _vp, _sz, _vp], ctypes.c_int),
     'pp_occupancy_set': ([_vp, _i32, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _f, _f, _vp],
                          ctypes.c_int),
     'pp_center_filter': ([_vp, _i64, _i64, _i64, _i32, _f, _f, _f, _vp, _i64, _vp, _vp],

@@ -130,6 +130,13 @@ struct GrowArgs {
     SeedExt *xext;            // (n_img) their hand-off words (zeroed before each launch)
     pp_ann *xrec;             // (n_img, kExtCache) their published annotations
     double *nms_score;        // (n_img, 2 * ann_cap)
+    // standalone NMS over caller annotations (pp_nms_keypoints_scored), else NULL: per
+    // (image, record) -2 fixed_score, -1 none, j >= 0 suppress_score_index; the record's
+    // score_weights (K each) and fixed scores (annotation.py:60-71)
+    const int32_t *nms_spec;
+    const double *nms_sw;
+    const double *nms_fixed;
+    double nms_it;            // nms.Keypoints.instance_threshold as the float64 it compares in
     int *nms_idx;             // (n_img, 4 * ann_cap + ann_np)
     float *nms_f;             // (n_img, 2 * ann_cap) per-annotation max x, max y
     int2 *nms_box;            // (n_img, kNmsBoxLists, ann_cap) plane box lists beyond registers
@@ -2945,18 +2952,20 @@ struct ScoreLDS {
 
 // Annotation.score() (annotation.py:24-28, 60-71) in float64, collective over one wave:
 // lane j finds the rank of v_j in descending order, the rank-ordered products go to LDS
-// and lane 0 adds them in NumPy's pairwise order
-__device__ double ann_score_w(ScoreLDS &L, const float (*data)[3], int K) {
+// and lane 0 adds them in NumPy's pairwise order.  `zero_j` (suppress_score_index, >= 0)
+// reads as v = 0; `w` (the record's own score_weights) replaces the default weights.
+__device__ double ann_score_w(ScoreLDS &L, const float (*data)[3], int K, int zero_j = -1,
+                              const double *w = nullptr) {
     const int lane = threadIdx.x & 63;
     const double ws = (double)(3 * min(K, 3) + (K - min(K, 3)));
     if (lane < K) {
-        const float vj = data[lane][2];
+        const float vj = lane == zero_j ? 0.0f : data[lane][2];
         int rank = 0;
         for (int i = 0; i < K; i++) {
-            const float vi = data[i][2];
+            const float vi = i == zero_j ? 0.0f : data[i][2];
             rank += (vi > vj) || (vi == vj && i < lane);
         }
-        L.prod[rank] = ((rank < 3 ? 3.0 : 1.0) / ws) * (double)vj;
+        L.prod[rank] = (w ? w[rank] : (rank < 3 ? 3.0 : 1.0) / ws) * (double)vj;
     }
     wave_sync();
     if (lane == 0) L.score_bc = pw_sum(L.prod, K);
@@ -2964,6 +2973,18 @@ __device__ double ann_score_w(ScoreLDS &L, const float (*data)[3], int K) {
     const double res = L.score_bc;
     wave_sync();
     return res;
+}
+
+// the score nms.Keypoints sorts and filters record i of image img by: the default
+// Annotation.score(), or with the caller's per-record fixed_score / suppress_score_index /
+// score_weights (standalone NMS)
+__device__ double nms_ann_score(const GrowArgs &g, ScoreLDS &L, int img, int i,
+                                const float (*data)[3], int K) {
+    if (!g.nms_spec) return ann_score_w(L, data, K);
+    const int64_t gi = (int64_t)img * g.ann_cap + i;
+    const int spec = g.nms_spec[gi];
+    if (spec == -2) return g.nms_fixed[gi];
+    return ann_score_w(L, data, K, spec, g.nms_sw + gi * K);
 }
 
 // the grid cell occ_get reads: 1 = occupied whatever the grid holds (f beyond the planes),
@@ -3073,7 +3094,7 @@ __global__ __launch_bounds__(64 * W) void nms_kernel(GrowArgs g) {
     int2 *gbox = g.nms_box + ((int64_t)img * kNmsBoxLists + wave) * cap;
     const float red = (float)g.cfg.occupancy_reduction;
     const float kt = g.cfg.nms_keypoint_threshold;
-    const double it = (double)g.cfg.nms_instance_threshold;
+    const double it = g.nms_it;
     if (threadIdx.x == 0) {
         s_status = g.status[img];
         g.complete_next[img] = 0;  // workspace contract: left zero
@@ -3088,7 +3109,7 @@ __global__ __launch_bounds__(64 * W) void nms_kernel(GrowArgs g) {
     if (PHASE == 0 && !g.cfg.apply_nms) {
         for (int i = wave; i < n_anns; i += W) {
             copy_ann(&out[i], &work[i]);
-            const double sc = ann_score_w(L, work[i].data, K);
+            const double sc = nms_ann_score(g, L, img, i, work[i].data, K);
             if (lane == 0) {
                 out[i].score = sc;
                 if (g.out_idx) g.out_idx[(int64_t)img * cap + i] = i;
@@ -3113,7 +3134,7 @@ __global__ __launch_bounds__(64 * W) void nms_kernel(GrowArgs g) {
             a.data[lane][2] = 0.0f;
         }
         wave_sync();
-        const double sc = ann_score_w(L, a.data, K);
+        const double sc = nms_ann_score(g, L, img, i, a.data, K);
         if (lane == 0) {
             float ax = a.data[0][0], ay = a.data[0][1];
             for (int j = 1; j < K; j++) {
@@ -3241,14 +3262,15 @@ __global__ __launch_bounds__(64 * W) void nms_kernel(GrowArgs g) {
         }
         // nms.py:51-53 in sorted order: zero low joints, drop low scores
         for (int r = wave; r < m; r += W) {
-            pp_ann &a = work[keep[perm[r]]];
+            const int wi = keep[perm[r]];
+            pp_ann &a = work[wi];
             if (lane < K && a.data[lane][2] < kt) {
                 a.data[lane][0] = 0.0f;
                 a.data[lane][1] = 0.0f;
                 a.data[lane][2] = 0.0f;
             }
             wave_sync();
-            const double sc = ann_score_w(L, a.data, K);
+            const double sc = nms_ann_score(g, L, img, wi, a.data, K);
             if (lane == 0) {
                 flag[r] = sc >= it;
                 score[r] = sc;  // by sorted rank now (the work-index scores are consumed)
@@ -3838,6 +3860,7 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
         g.ww = d.ww;
         g.col_cap = d.hw;
         g.cfg = *cfg;
+        g.nms_it = (double)cfg->nms_instance_threshold;
         g.heads = h;
         g.hr = hr;
         g.cif_floor = cfg->cif_floor;
@@ -4087,8 +4110,24 @@ int pp_nms_keypoints(pp_ann *d_anns, const int32_t *d_counts, int32_t n_img, int
                      int32_t ann_capacity, const pp_config *cfg, pp_ann *d_out,
                      int32_t *d_out_counts, int32_t *d_out_index, void *d_workspace,
                      size_t workspace_bytes, void *stream) {
+    if (!cfg) return fail(PP_EINVAL, "pp_nms_keypoints: NULL argument");
+    return pp_nms_keypoints_scored(d_anns, d_counts, n_img, K, ann_capacity, cfg,
+                                   (double)cfg->nms_instance_threshold, nullptr, nullptr,
+                                   nullptr, d_out, d_out_counts, d_out_index, d_workspace,
+                                   workspace_bytes, stream);
+}
+
+int pp_nms_keypoints_scored(pp_ann *d_anns, const int32_t *d_counts, int32_t n_img, int32_t K,
+                            int32_t ann_capacity, const pp_config *cfg,
+                            double instance_threshold, const int32_t *d_score_spec, const double *d_score_weights,
+                            const double *d_fixed_score, pp_ann *d_out, int32_t *d_out_counts,
+                            int32_t *d_out_index, void *d_workspace, size_t workspace_bytes,
+                            void *stream) {
     if (!d_anns || !d_counts || !cfg || !d_out || !d_out_counts || !d_workspace)
         return fail(PP_EINVAL, "pp_nms_keypoints: NULL argument");
+    if (d_score_spec && (!d_score_weights || !d_fixed_score))
+        return fail(PP_EINVAL, "pp_nms_keypoints_scored: d_score_spec needs the weights and "
+                               "fixed scores");
     if (n_img < 0 || K <= 0 || K > PP_MAX_KP || ann_capacity <= 0 || cfg->occupancy_reduction <= 0)
         return fail(PP_ESHAPE, "pp_nms_keypoints: shape outside the supported envelope");
     if (n_img == 0) return PP_OK;
@@ -4110,6 +4149,10 @@ int pp_nms_keypoints(pp_ann *d_anns, const int32_t *d_counts, int32_t n_img, int
     g.nms_idx = (int *)(ws + l.off_idx);
     g.nms_f = (float *)(ws + l.off_f);
     g.nms_box = (int2 *)(ws + l.off_box);
+    g.nms_spec = d_score_spec;
+    g.nms_sw = d_score_weights;
+    g.nms_fixed = d_fixed_score;
+    g.nms_it = instance_threshold;
     g.out = d_out;
     g.counts = d_out_counts;
     g.out_idx = d_out_index;

@@ -4,7 +4,9 @@ Inside the device decode the suppression runs after the seed loop and force-comp
 (csrc/grow.hip, nms_kernel), configured from these class attributes exactly as the
 reference's CifCaf(nms=nms.Keypoints()) is.  `Keypoints().annotations(anns)` runs the
 same kernel over a host list of Annotation objects (pp_nms_keypoints): it mutates their
-data in place as the reference does and returns the survivors, sorted by -score.
+data in place as the reference does and returns the survivors, sorted by -score.  Each
+annotation's own score() is honoured (fixed_score, suppress_score_index, score_weights:
+pp_nms_keypoints_scored).
 """
 import ctypes
 
@@ -15,6 +17,49 @@ from .. import _device
 from .._abi import ANN_DTYPE, DET_DTYPE, DetNms, make_config
 from .._lib import call, load
 from ..annotation import NOTSET
+
+
+def _default_weights(k):
+    w = np.ones((k,))
+    w[:3] = 3.0
+    return w / np.sum(w)
+
+
+def _score_spec(anns, k):
+    """Each annotation's Annotation.score() inputs (annotation.py:60-71) for
+    pp_nms_keypoints_scored: (spec int32 (n,), score_weights float64 (n, k), fixed float64
+    (n,)), or None when every annotation scores the default way."""
+    default = _default_weights(k)
+    custom = False
+    for ann in anns:
+        w = getattr(ann, 'score_weights', None)
+        if (ann.fixed_score != NOTSET or ann.suppress_score_index is not None
+                or w is None or not np.array_equal(np.asarray(w, np.float64), default)):
+            custom = True
+            break
+    if not custom:
+        return None
+    n = len(anns)
+    spec = np.full(n, -1, np.int32)
+    sw = np.zeros((n, k), np.float64)
+    fixed = np.zeros(n, np.float64)
+    for i, ann in enumerate(anns):
+        if ann.fixed_score != NOTSET:
+            spec[i] = -2
+            fixed[i] = float(ann.fixed_score)
+            continue
+        w = np.asarray(ann.score_weights, np.float64)
+        if w.shape != (k,):
+            raise ValueError('score_weights of length {} for {} keypoints'.format(len(w), k))
+        sw[i] = w
+        j = ann.suppress_score_index
+        if j is not None:
+            j = int(j)
+            if not -k <= j < k:  # v[j] = 0.0 raises in the reference too
+                raise IndexError('suppress_score_index {} is out of bounds for {} keypoints'
+                                 .format(j, k))
+            spec[i] = j % k
+    return spec, sw, fixed
 
 
 class Keypoints:
@@ -33,14 +78,12 @@ class Keypoints:
             return anns
         k = len(anns[0].data)
         for ann in anns:
-            if ann.fixed_score != NOTSET or ann.suppress_score_index is not None:
-                raise NotImplementedError('device NMS scores with the default Annotation.score()'
-                                          ' (no fixed_score / suppress_score_index)')
             if len(ann.data) != k:
                 raise ValueError('annotations with different keypoint counts')
         if k > ANN_DTYPE['data'].shape[0]:
             raise ValueError('more keypoints than PP_MAX_KP')
         n = len(anns)
+        spec = _score_spec(anns, k)
         recs = np.zeros(n, ANN_DTYPE)
         for i, ann in enumerate(anns):
             recs['data'][i, :k] = ann.data
@@ -55,10 +98,15 @@ class Keypoints:
         d_out_index = torch.empty(n, dtype=torch.int32, device=dev)
         ws = torch.empty(int(load().pp_nms_workspace_size(1, n)), dtype=torch.uint8, device=dev)
         cfg = self.config()
-        call('pp_nms_keypoints', _device.ptr(d_in), _device.ptr(d_counts), 1, k, n,
-             ctypes.byref(cfg), _device.ptr(d_out), _device.ptr(d_out_counts),
-             _device.ptr(d_out_index), _device.ptr(ws), ctypes.c_size_t(ws.numel()),
-             _device.stream())
+        # the float64 instance threshold the reference compares score() with (nms.py:21, 53)
+        d_spec = d_sw = d_fixed = None
+        if spec is not None:
+            d_spec, d_sw, d_fixed = (torch.from_numpy(a).to(dev) for a in spec)
+        call('pp_nms_keypoints_scored', _device.ptr(d_in), _device.ptr(d_counts), 1, k, n,
+             ctypes.byref(cfg), float(self.instance_threshold), _device.ptr(d_spec),
+             _device.ptr(d_sw), _device.ptr(d_fixed), _device.ptr(d_out),
+             _device.ptr(d_out_counts), _device.ptr(d_out_index), _device.ptr(ws),
+             ctypes.c_size_t(ws.numel()), _device.stream())
         mutated = np.frombuffer(d_in.cpu().numpy().tobytes(), dtype=ANN_DTYPE)
         m = int(d_out_counts.cpu().item())
         order = d_out_index[:m].cpu().numpy()

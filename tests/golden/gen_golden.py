@@ -22,6 +22,7 @@ Fixtures:
                        CifCafCollector / CifdetCollector on random conv outputs, quad 0-2
   nms.npz              nms.Keypoints().annotations on random overlapping Annotation lists
                        (inputs, output order as input indices, mutated data), per config
+  nms_scored.npz       the same with fixed_score / suppress_score_index annotations
   api_initial_<mode>.npz  CifCaf.__call__(fields, initial_annotations) (cifcaf.py:95-98):
                        the initial annotations, the output list and which outputs are them
   api_seedmask_<mode>.npz  CifCaf with FieldConfig(seed_mask=...) (cif_seeds.py:28-29)
@@ -370,6 +371,60 @@ def gen_nms(op):
         out[name + '_score'] = np.array([a.score() for a in res], np.float64)
         print('nms', name, n, '->', len(res))
     np.savez_compressed(os.path.join(HERE, 'nms.npz'), **out)
+
+
+NMS_SCORED_CASES = [  # (name, n, spread, seed, keypoint_th, instance_th, suppression)
+    ('mixed', 160, 150.0, 5, 0.05, 0.15, 0.0),
+    ('fixed_ties', 60, 90.0, 6, 0.0, 0.2, 0.3),
+]
+NO_INDEX = -999  # suppress_score_index None in the fixture
+
+
+def gen_nms_scored(op):
+    """nms.Keypoints over annotations carrying fixed_score and suppress_score_index
+    (annotation.py:24-28, 60-71; nms.py:21, 33, 53-54 filter and sort by score())."""
+    from openpifpaf.annotation import Annotation  # pylint: disable=import-outside-toplevel
+    from openpifpaf.decoder import nms  # pylint: disable=import-outside-toplevel
+    out = {}
+    kps, skel = constants.COCO_KEYPOINTS, constants.COCO_PERSON_SKELETON
+    for name, n, spread, seed, kt, it, sup in NMS_SCORED_CASES:
+        rng = np.random.default_rng(200 + seed)
+        base = rng.uniform(10.0, spread, (n, 1, 2)).astype(np.float32)
+        xy = (base + rng.normal(0.0, 12.0, (n, 17, 2))).astype(np.float32)
+        v = rng.uniform(0.0, 1.0, (n, 17)).astype(np.float32)
+        v[rng.uniform(0.0, 1.0, (n, 17)) < 0.2] = 0.0
+        data = np.concatenate([xy, v[:, :, None]], axis=2).astype(np.float32)
+        scales = rng.uniform(0.5, 24.0, (n, 17)).astype(np.float32)
+        kind = rng.integers(0, 3, n) if name == 'mixed' else np.full(n, 1)
+        fixed = np.full(n, np.nan)
+        supp = np.full(n, NO_INDEX, np.int64)
+        anns = []
+        for i in range(n):
+            if kind[i] == 2:  # suppress_score_index, Python indices incl. negative and 0
+                supp[i] = [-1, 0, 5, 16, -3][i % 5]
+                a = Annotation(kps, skel, suppress_score_index=int(supp[i]))
+            else:
+                a = Annotation(kps, skel)
+            a.data = data[i].copy()
+            a.joint_scales = scales[i].copy()
+            if kind[i] == 1:  # fixed_score: ties, the threshold itself, below it
+                fixed[i] = [it, 0.5, 0.25, 0.9, it * 0.5, float(rng.uniform())][i % 6]
+                a.fixed_score = float(fixed[i])
+            anns.append(a)
+        k = nms.Keypoints()
+        k.keypoint_threshold, k.instance_threshold, k.suppression = kt, it, sup
+        ids = {id(a): i for i, a in enumerate(anns)}
+        res = k.annotations(list(anns))
+        out[name + '_data_in'] = data
+        out[name + '_scales'] = scales
+        out[name + '_cfg'] = np.array([kt, it, sup], np.float64)
+        out[name + '_fixed'] = fixed
+        out[name + '_supp'] = supp
+        out[name + '_order'] = np.array([ids[id(a)] for a in res], np.int64)
+        out[name + '_data_out'] = np.stack([a.data for a in anns]).astype(np.float32)
+        out[name + '_score'] = np.array([a.score() for a in res], np.float64)
+        print('nms scored', name, n, '->', len(res))
+    np.savez_compressed(os.path.join(HERE, 'nms_scored.npz'), **out)
 
 
 def gen_heads(op):
@@ -751,6 +806,7 @@ def main():
     only = sys.argv[1:]
     if only == ['nms']:
         gen_nms(op)
+        gen_nms_scored(op)
         return
     if only == ['heads']:
         gen_heads(op)
@@ -775,6 +831,7 @@ def main():
     gen_primitives(op)
     gen_errors()
     gen_nms(op)
+    gen_nms_scored(op)
     gen_heads(op)
     gen_det(op)
     gen_det_nms(op)

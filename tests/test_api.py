@@ -263,3 +263,24 @@ def test_short_seed_mask_raises_index_error():
     check_seed_mask(None, 17)
     with pytest.raises(IndexError):
         check_seed_mask([0] * 16, 17)
+
+
+def test_nms_score_spec_host_logic():
+    """nms.Keypoints' per-annotation score() inputs for pp_nms_keypoints_scored."""
+    from openpifpaf_amd import constants
+    from openpifpaf_amd.annotation import Annotation
+    from openpifpaf_amd.decoder.nms import _score_spec
+
+    def ann(**kw):
+        return Annotation(constants.COCO_KEYPOINTS, constants.COCO_PERSON_SKELETON, **kw)
+
+    assert _score_spec([ann(), ann()], 17) is None  # default score(): the plain entry
+    a_fixed, a_last, a_zero = ann(), ann(suppress_score_index=-1), ann(suppress_score_index=0)
+    a_fixed.fixed_score = 0.25
+    spec, sw, fixed = _score_spec([ann(), a_fixed, a_last, a_zero], 17)
+    assert spec.tolist() == [-1, -2, 16, 0]
+    assert fixed[1] == 0.25
+    assert sw[2, 16] == 0.0 and sw[3, 16] > 0.0  # `if suppress_score_index:` (annotation.py:25)
+    assert np.array_equal(sw[0], ann().score_weights)
+    with pytest.raises(IndexError):
+        _score_spec([ann(suppress_score_index=17)], 17)

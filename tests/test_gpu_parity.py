@@ -557,6 +557,33 @@ def test_nms_keypoints_vs_reference(dec, name):
     assert np.array_equal(np.array([a.score() for a in res]), g[name + '_score'])
 
 
+@pytest.mark.parametrize('name', ['mixed', 'fixed_ties'])
+def test_nms_keypoints_scored_vs_reference(dec, name):
+    """Annotations with fixed_score / suppress_score_index (annotation.py:60-71): the
+    reference's filter, order and in-place edits (pp_nms_keypoints_scored)."""
+    from openpifpaf_amd import constants
+    from openpifpaf_amd.annotation import Annotation
+    g = np.load(os.path.join(gu.GOLDEN, 'nms_scored.npz'))
+    kt, it, sup = (float(t) for t in g[name + '_cfg'])
+    anns = []
+    for d, sc, fx, sp in zip(g[name + '_data_in'], g[name + '_scales'], g[name + '_fixed'],
+                             g[name + '_supp']):
+        a = Annotation(constants.COCO_KEYPOINTS, constants.COCO_PERSON_SKELETON,
+                       suppress_score_index=None if sp == -999 else int(sp))
+        a.data = d.copy()
+        a.joint_scales = sc.copy()
+        if not np.isnan(fx):
+            a.fixed_score = float(fx)
+        anns.append(a)
+    k = dec.nms.Keypoints()
+    k.keypoint_threshold, k.instance_threshold, k.suppression = kt, it, sup
+    res = k.annotations(list(anns))
+    ids = {id(a): i for i, a in enumerate(anns)}
+    assert [ids[id(a)] for a in res] == g[name + '_order'].tolist()
+    assert np.array_equal(np.stack([a.data for a in anns]), g[name + '_data_out'])
+    assert np.array_equal(np.array([a.score() for a in res]), g[name + '_score'])
+
+
 def test_nms_keypoints_many_vs_oracle(dec):
     """More kept annotations than the LDS box lists hold (global-memory path)."""
     rng = np.random.default_rng(7)
