@@ -43,6 +43,7 @@ VARIANTS = {
     'w0plan': ['-DPP_W0_PLAN'],          # seed loop: wave 0 plans the idle helpers itself
     'nopartial': ['-DPP_NO_PARTIAL'],    # seed-loop plans without the in-flight grows' joints
     'hprio': ['-DPP_HELPER_PRIO'],       # seed-loop helper waves at issue priority 2
+    'radix7': ['-DPP_SEED_RADIX7'],      # seeds sorted by the stable 7-bit radix passes
 }
 
 

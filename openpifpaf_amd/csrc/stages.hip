@@ -540,12 +540,106 @@ __device__ void radix_desc(uint64_t key[4], int n, uint64_t *s_key, uint16_t *s_
     }
 }
 
-// 38 KB of LDS (keys, radix counts, segment offsets; x / y / s stay in the emission
-// buffer), so a workgroup fits beside the seed loop's 121 KB on one CU (DecodePipeline
+// The default sort of 257..4096 keys (PP_SEED_RADIX7: radix_desc).  The full 64-bit keys
+// are distinct (the low 27 bits hold the inverted emission index), so the order needs no
+// stable pass: one bucket pass on the top kBucketBits bits of (key >> 27) - min (LDS
+// atomics; positions inside a bucket arbitrary), then each key's rank inside its bucket by
+// counting the bucket's larger keys.  Five barriers and one LDS round trip per key, where
+// radix_desc's four or five stable 7-bit passes took 32k of a planted image's 55k sort
+// cycles (tools/sort_stamps.py).  A bucket holds the keys of one (v, field) value or of a
+// narrow range of them: runs of equal (v, field) (planted fields) cost their length squared
+// in LDS reads.  s_hist: kBuckets + 1 ints; s_w: 16 ints.  Leaves s_key[0, n) sorted.
+#ifdef PP_SEED_RADIX7
+constexpr bool kSeedBucket = false;
+#else
+constexpr bool kSeedBucket = true;
+#endif
+constexpr int kBucketBits = 11, kBuckets = 1 << kBucketBits;
+static_assert(kBuckets == 2 * 1024, "bucket_desc: two bucket counts per thread");
+
+__device__ void bucket_desc(uint64_t key[4], int n, uint64_t *s_key, int *s_hist, int *s_w,
+                            uint64_t *s_mm) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    s_hist[2 * t] = 0;
+    s_hist[2 * t + 1] = 0;
+    uint64_t lo = ~0ull, hi = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++)
+        if (256 * w + 64 * e + lane < n) {
+            lo = min(lo, key[e] >> 27);
+            hi = max(hi, key[e] >> 27);
+        }
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) {
+        lo = min(lo, shfl_xor64(lo, m));
+        hi = max(hi, shfl_xor64(hi, m));
+    }
+    if (lane == 0) {
+        s_mm[w] = lo;
+        s_mm[16 + w] = hi;
+    }
+    __syncthreads();  // range parts + zeroed counts
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        lo = min(lo, s_mm[q]);
+        hi = max(hi, s_mm[16 + q]);
+    }
+    const uint64_t range = hi > lo ? hi - lo : 0;
+    const int bits = range ? 64 - __clzll(range) : 0;
+    const int sh = bits > kBucketBits ? bits - kBucketBits : 0;
+    // bucket, descending: larger keys in lower buckets
+    int bk[4], at[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        bk[e] = -1;
+        if (256 * w + 64 * e + lane < n) {
+            bk[e] = (kBuckets - 1) - (int)(((key[e] >> 27) - lo) >> sh);
+            at[e] = atomicAdd(&s_hist[bk[e]], 1);
+        }
+    }
+    __syncthreads();  // counts complete
+    // bucket starts: thread t scans buckets 2t, 2t + 1 (block_scan_1024 has two barriers,
+    // after which nobody reads the counts again)
+    const int c0 = s_hist[2 * t], c1 = s_hist[2 * t + 1];
+    int total;
+    const int base = block_scan_1024(c0 + c1, s_w, total);
+    s_hist[2 * t] = base;
+    s_hist[2 * t + 1] = base + c0;
+    if (t == 0) s_hist[kBuckets] = total;
+    __syncthreads();  // starts written
+    int st[4], en[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++)
+        if (bk[e] >= 0) {
+            st[e] = s_hist[bk[e]];
+            en[e] = s_hist[bk[e] + 1];
+            s_key[st[e] + at[e]] = key[e];
+        }
+    __syncthreads();  // bucketed
+    int pos[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++)
+        if (bk[e] >= 0) {
+            int r = 0;
+            for (int j = st[e]; j < en[e]; j++) r += s_key[j] > key[e];
+            pos[e] = st[e] + r;
+        }
+    __syncthreads();  // every rank counted
+#pragma unroll
+    for (int e = 0; e < 4; e++)
+        if (bk[e] >= 0) s_key[pos[e]] = key[e];
+    __syncthreads();
+}
+
+// 41 KB of LDS (keys, bucket counts, segment offsets; x / y / s stay in the emission
+// buffer), so a workgroup fits beside a seed-loop workgroup on one CU (DecodePipeline
 // overlaps them)
 __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
     __shared__ uint64_t s_key[kSortLds];
-    __shared__ __attribute__((aligned(16))) uint16_t s_rh[16 * kRadixPitch];
+    // radix_desc's per-wave digit rows (u16) or bucket_desc's kBuckets + 1 counts
+    __shared__ __attribute__((aligned(16))) int s_rh_i[kSeedBucket ? kBuckets + 1
+                                                                  : 16 * kRadixPitch / 2];
+    uint16_t *s_rh = reinterpret_cast<uint16_t *>(s_rh_i);
     __shared__ int s_rw[32];
     __shared__ uint64_t s_mm[32];
     __shared__ int s_off[kMaxHeads * PP_MAX_KP + 1];
@@ -646,7 +740,10 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
             }
         }
         SORT_STAMP(2);
-        radix_desc(key, n, s_key, s_rh, s_rw, s_mm);
+        if constexpr (kSeedBucket)
+            bucket_desc(key, n, s_key, s_rh_i, s_rw, s_mm);
+        else
+            radix_desc(key, n, s_key, s_rh, s_rw, s_mm);
         SORT_STAMP(3);
         finish(s_key);
         __syncthreads();
