@@ -61,7 +61,7 @@ struct SeedKeys {
 };
 
 template <typename Perm>
-__device__ void bitonic_sort(Perm *p, int np, const SeedKeys &keys) {
+__device__ __forceinline__ void bitonic_sort(Perm *p, int np, const SeedKeys &keys) {
     for (int k = 2; k <= np; k <<= 1) {
         for (int j = k >> 1; j > 0; j >>= 1) {
             for (int i = threadIdx.x; i < np; i += blockDim.x) {
@@ -98,6 +98,17 @@ struct SeedArgs {
     // first slot of segment (CIF head m, field f): K * cif_off[m] + f * H_m * W_m
     __device__ __forceinline__ int64_t seg_base(int m, int f) const {
         return (int64_t)K * h.cif_off[m] + (int64_t)f * h.cif_hw(m);
+    }
+    // seg_base of concatenated segment q = m * K + f with the head picked by selects: a
+    // dynamic index into the kernel-argument struct makes the compiler copy the whole
+    // struct to scratch for every lane
+    __device__ __forceinline__ int64_t seg_base_q(int q) const {
+        const int m = q / K, f = q % K;
+        int64_t b = 0;
+#pragma unroll
+        for (int c = 0; c < kMaxHeads; c++)
+            if (c == m) b = seg_base(c, f);
+        return b;
     }
 };
 
@@ -557,33 +568,46 @@ constexpr bool kSeedBucket = true;
 constexpr int kBucketBits = 11, kBuckets = 1 << kBucketBits;
 static_assert(kBuckets == 2 * 1024, "bucket_desc: two bucket counts per thread");
 
+// min / max over the wave on DPP (prefix within rows, then row_bcast15 / row_bcast31, as
+// wave_incl_scan), read from lane 63
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x111, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x112, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x114, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x118, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xA, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x143, 0xC, 0xF, false));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 __device__ void bucket_desc(uint64_t key[4], int n, uint64_t *s_key, int *s_hist, int *s_w,
                             uint64_t *s_mm) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     s_hist[2 * t] = 0;
     s_hist[2 * t + 1] = 0;
-    uint64_t lo = ~0ull, hi = 0;
+    // the range of key >> 27 bounded through the v bits (key >> 32) alone: lo = min v << 5,
+    // hi = max v << 5 | 31 (32-bit reductions; at most one bit wider than the exact range)
+    uint32_t lo32 = ~0u, hi32n = ~0u;  // min of v, min of ~v
 #pragma unroll
     for (int e = 0; e < 4; e++)
         if (256 * w + 64 * e + lane < n) {
-            lo = min(lo, key[e] >> 27);
-            hi = max(hi, key[e] >> 27);
+            lo32 = min(lo32, (uint32_t)(key[e] >> 32));
+            hi32n = min(hi32n, ~(uint32_t)(key[e] >> 32));
         }
-#pragma unroll
-    for (int m = 32; m > 0; m >>= 1) {
-        lo = min(lo, shfl_xor64(lo, m));
-        hi = max(hi, shfl_xor64(hi, m));
-    }
+    lo32 = wave_min_u32(lo32);
+    hi32n = wave_min_u32(hi32n);
+    uint32_t *s_mm32 = reinterpret_cast<uint32_t *>(s_mm);
     if (lane == 0) {
-        s_mm[w] = lo;
-        s_mm[16 + w] = hi;
+        s_mm32[w] = lo32;
+        s_mm32[16 + w] = hi32n;
     }
     __syncthreads();  // range parts + zeroed counts
 #pragma unroll
     for (int q = 0; q < 16; q++) {
-        lo = min(lo, s_mm[q]);
-        hi = max(hi, s_mm[16 + q]);
+        lo32 = min(lo32, s_mm32[q]);
+        hi32n = min(hi32n, s_mm32[16 + q]);
     }
+    const uint64_t lo = (uint64_t)lo32 << 5, hi = ((uint64_t)~hi32n << 5) | 31u;
     const uint64_t range = hi > lo ? hi - lo : 0;
     const int bits = range ? 64 - __clzll(range) : 0;
     const int sh = bits > kBucketBits ? bits - kBucketBits : 0;
@@ -643,6 +667,7 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
     __shared__ int s_rw[32];
     __shared__ uint64_t s_mm[32];
     __shared__ int s_off[kMaxHeads * PP_MAX_KP + 1];
+    __shared__ int s_sb[kMaxHeads * PP_MAX_KP];  // seg_base of each segment
     __shared__ int s_scan[16];
     static_assert(kRadixDigits * 16 == 2 * 1024, "radix_desc: two counts per thread");
     static_assert(kMaxHeads * PP_MAX_KP < 1024, "one thread per segment");
@@ -661,6 +686,7 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
         int total;
         const int pre = block_scan_1024(cnt, s_scan, total);
         if (q <= nseg) s_off[q] = pre;
+        if (q < nseg) s_sb[q] = (int)a.seg_base_q(q);
         if (q == 0) a.counts[img] = total;
     }
     __syncthreads();
@@ -673,7 +699,7 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
     while (np < n) np <<= 1;
     pp_seed *out = a.seeds + (int64_t)img * cap;
     // emission slot of concatenated seed i: its segment by binary search over the offsets
-    auto slot = [&](int i) {
+    auto slot = [&](int i) __attribute__((always_inline)) {
         int lo = 0, hi = nseg - 1;  // largest segment with s_off[seg] <= i
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
@@ -682,7 +708,7 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
             else
                 hi = mid - 1;
         }
-        return a.seg_base(lo / a.K, lo % a.K) + (i - s_off[lo]);
+        return (int64_t)s_sb[lo] + (i - s_off[lo]);
     };
     // the sorted keys kb[0 .. n) (LDS, or global scratch for more than kSortLds keys):
     // runs of equal (v, field) re-sorted by (x, y, s) descending, then emission order (one
@@ -714,16 +740,40 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
             }
         }
         __syncthreads();
-        for (int i = threadIdx.x; i < n; i += blockDim.x) {
-            const uint64_t k = kb[i];
-            const int64_t e = slot(key_emit(k));
-            pp_seed r;
-            r.v = __uint_as_float((uint32_t)(k >> 32));
-            r.field = (int)((k >> 27) & 31u);
-            r.x = gx[e];
-            r.y = gy[e];
-            r.s = gs[e];
-            out[i] = r;
+        // four records per thread per round: every slot search and load issued before the
+        // stores (one global round trip per round, not per record)
+        for (int i0 = 0; i0 < n; i0 += 4 * (int)blockDim.x) {
+            uint64_t k[4];
+            int64_t e[4];
+            float x[4], y[4], z[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = i0 + u * (int)blockDim.x + (int)threadIdx.x;
+                k[u] = i < n ? kb[i] : 0ull;
+                e[u] = i < n ? slot(key_emit(k[u])) : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = i0 + u * (int)blockDim.x + (int)threadIdx.x;
+                if (i < n) {
+                    x[u] = gx[e[u]];
+                    y[u] = gy[e[u]];
+                    z[u] = gs[e[u]];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = i0 + u * (int)blockDim.x + (int)threadIdx.x;
+                if (i < n) {
+                    pp_seed r;
+                    r.v = __uint_as_float((uint32_t)(k[u] >> 32));
+                    r.field = (int)((k[u] >> 27) & 31u);
+                    r.x = x[u];
+                    r.y = y[u];
+                    r.s = z[u];
+                    out[i] = r;
+                }
+            }
         }
     };
     if (n > kRadixMin && n <= kSortLds && kSeedRadix) {
@@ -842,7 +892,7 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
         int *loc = perm + np;  // second half of the permutation buffer
         for (int q = 0; q < nseg; q++) {
             const int o = s_off[q], c = s_off[q + 1] - o;
-            const int64_t sb = a.seg_base(q / a.K, q % a.K);
+            const int64_t sb = s_sb[q];
             for (int i = threadIdx.x; i < c; i += blockDim.x) loc[o + i] = (int)(sb + i);
         }
         for (int i = threadIdx.x; i < np; i += blockDim.x) perm[i] = i;
