@@ -1621,6 +1621,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
 
     const int64_t fld = blockIdx.x;  // image * K + field
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (wave == 0) HR_STAMP(0);
     if (threadIdx.x == 0) s_next = 0;
     if (threadIdx.x < kTileBits / 32) s_bits[threadIdx.x] = 0u;
     FoldCand *glist = a.list + fld * a.list_cap;
@@ -1749,6 +1750,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
         __syncthreads();  // the stage is rewritten by the next round
     }
     const int total = running;
+    if (wave == 0) {
+        HR_STAMP(1);
+        HR_ADD(8, total);
+        HR_ADD(9, n_seed);
+    }
     const bool lds = total <= kFuList;
     bool use_bins = false;
     if (!lds) {
@@ -1774,9 +1780,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void c
     // ---- phase 3: the seeds (cif_seeds.py:35-47) from the finished map ----
     if constexpr (SEEDS) {
         __syncthreads();  // every wave's blocks and masks are stored
+        if (wave == 0) HR_STAMP(2);
         if (seeding) seeds_from_map(a, fld, n_seed, s_tmp);
         else if (threadIdx.x == 0) ss.f_counts[fld] = 0;
     }
+#ifdef PP_STAMPS
+    __syncthreads();
+    if (wave == 0) HR_STAMP(3);
+    if (g_hr_stamps && threadIdx.x == 0) {
+        g_hr_stamps[blockIdx.x * kHrSt + 6] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+        g_hr_stamps[blockIdx.x * kHrSt + 7] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11));
+    }
+#endif
 }
 
 // -------------------------------------------------------------------------------------
@@ -2034,6 +2049,27 @@ int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_confi
     // one workgroup per field, one CIF head: the list-in-LDS kernel (with the seeds when a
     // sink is given); fields of small batches split over several workgroups, and
     // multi-scale groups, take cifhr_sparse_kernel
+#ifdef PP_STAMPS
+    uint64_t *st = nullptr;
+    hipMalloc((void **)&st, (size_t)nblocks * kHrSt * sizeof(uint64_t));
+    hipMemsetAsync(st, 0, (size_t)nblocks * kHrSt * sizeof(uint64_t), s);
+    hipMemcpyToSymbolAsync(HIP_SYMBOL(g_hr_stamps), &st, sizeof(st), 0, hipMemcpyHostToDevice, s);
+    // [start, ...]: dumped to $PP_HR_STAMPS_OUT after the launch (the stream synchronised)
+    auto dump = [&]() {
+        hipStreamSynchronize(s);
+        std::vector<uint64_t> hbuf((size_t)nblocks * kHrSt);
+        hipMemcpy(hbuf.data(), st, hbuf.size() * sizeof(uint64_t), hipMemcpyDeviceToHost);
+        const char *path = getenv("PP_HR_STAMPS_OUT");
+        FILE *fo = fopen(path ? path : "pp_hr_stamps.bin", "ab");
+        if (fo) {
+            fwrite(hbuf.data(), sizeof(uint64_t), hbuf.size(), fo);
+            fclose(fo);
+        }
+        uint64_t *nul = nullptr;
+        hipMemcpyToSymbol(HIP_SYMBOL(g_hr_stamps), &nul, sizeof(nul));
+        hipFree(st);
+    };
+#endif
 #ifndef PP_NO_FUSED
     if (a.split == 1 && h.n_cif == 1 && h.n_groups == 1 && h.group_size() == 1) {
         if (sink) {
@@ -2044,6 +2080,9 @@ int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_confi
         } else {
             hipLaunchKernelGGL(cifhr_fused_kernel<false>, dim3(nblocks), dim3(256), 0, s, a);
         }
+#ifdef PP_STAMPS
+        dump();
+#endif
         return check_launch(who);
     }
 #endif
@@ -2069,12 +2108,6 @@ int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_confi
             hipLaunchKernelGGL(cifhr_list_kernel<false>, dim3((unsigned)nf), dim3(256), 0, s, a);
         }
     }
-#ifdef PP_STAMPS
-    uint64_t *st = nullptr;
-    hipMalloc((void **)&st, (size_t)nblocks * kHrSt * sizeof(uint64_t));
-    hipMemsetAsync(st, 0, (size_t)nblocks * kHrSt * sizeof(uint64_t), s);
-    hipMemcpyToSymbolAsync(HIP_SYMBOL(g_hr_stamps), &st, sizeof(st), 0, hipMemcpyHostToDevice, s);
-#endif
     if (h.n_groups > 1)
         hipLaunchKernelGGL(cifhr_sparse_kernel<true>, dim3(nblocks), dim3(256), 0, s, a);
     else if (sink)
@@ -2082,20 +2115,7 @@ int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_confi
     else
         hipLaunchKernelGGL(cifhr_sparse_kernel<false>, dim3(nblocks), dim3(256), 0, s, a);
 #ifdef PP_STAMPS
-    {
-        hipStreamSynchronize(s);
-        std::vector<uint64_t> hbuf((size_t)nblocks * kHrSt);
-        hipMemcpy(hbuf.data(), st, hbuf.size() * sizeof(uint64_t), hipMemcpyDeviceToHost);
-        const char *path = getenv("PP_HR_STAMPS_OUT");
-        FILE *fo = fopen(path ? path : "pp_hr_stamps.bin", "ab");
-        if (fo) {
-            fwrite(hbuf.data(), sizeof(uint64_t), hbuf.size(), fo);
-            fclose(fo);
-        }
-        uint64_t *nul = nullptr;
-        hipMemcpyToSymbol(HIP_SYMBOL(g_hr_stamps), &nul, sizeof(nul));
-        hipFree(st);
-    }
+    dump();
 #endif
     return check_launch(who);
 }
