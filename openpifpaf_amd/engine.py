@@ -507,6 +507,13 @@ _PIPE_DEPTH = 2
 # for the force-complete, its next seed loop for the NMS (PP_SPLIT_TAIL=0: one call, the
 # front half waits for both)
 _SPLIT_TAIL = os.environ.get('PP_SPLIT_TAIL', '1') != '0'
+# Sparse batches: batch i's seed loop and tail share the back stream of its workspace
+# (i % 2), so a seed loop starts beside the previous batch's slowest images (cfg5 planted
+# 30.5k -> 41.7k images/s, cfg3 planted equal); dense ones: one stream for the seed loops
+# and one for the tails (cfg3 uniform 15.5k vs 14.6k images/s).  PP_PIPE_BACK2=1 / 0 forces
+# either.  The same two streams serve both (current + the library's side stream + two:
+# four hardware queues).
+_BACK2 = {'1': True, '0': False}.get(os.environ.get('PP_PIPE_BACK2', ''))
 
 
 class DecodePipeline:
@@ -527,6 +534,10 @@ class DecodePipeline:
     (The front half stays on the current stream and the pack on the tail stream so that
     the streams in use -- current, back, tail, the library's CafScored side stream -- each
     get a hardware queue of their own: HIP shares 4 per process between streams.)
+    For sparse batches the same two streams are used per workspace instead: batch i's seed
+    loop and its tail both go on stream i % 2, so batch i + 1's seed loop can start on the
+    CUs that batch i's finished images left (the loop ends with its slowest image); every
+    order between batches is an event either way.
 
     The force-complete sets are lazy for sparse batches (built after the seed loop on the
     tail stream, only for the (field, direction) pairs an annotation left unset), and go
@@ -600,10 +611,15 @@ class DecodePipeline:
                 events[2].record()
             front_done = torch.cuda.Event()
             front_done.record()
-        self.back.wait_event(front_done)
+        per_ws = _BACK2 if _BACK2 is not None else not dense
+        if per_ws:  # loop + tail on the workspace's stream (every cross-batch order is an event)
+            back = tail = (self.back, self.tail)[par % 2]
+        else:
+            back, tail = self.back, self.tail
+        back.wait_event(front_done)
         if self._back_done[par] is not None:  # the workspace's previous NMS (records)
-            self.back.wait_event(self._back_done[par])
-        with torch.cuda.stream(self.back):
+            back.wait_event(self._back_done[par])
+        with torch.cuda.stream(back):
             if events:
                 events[3].record()
             launch(STAGE_GROW | early | STAGE_SEED_LOOP_ONLY)
@@ -611,8 +627,9 @@ class DecodePipeline:
                 events[5].record()
             loop_done = torch.cuda.Event()
             loop_done.record()
-        self.tail.wait_event(loop_done)
-        with torch.cuda.stream(self.tail):
+        if tail is not back:
+            tail.wait_event(loop_done)
+        with torch.cuda.stream(tail):
             if _SPLIT_TAIL:
                 launch(STAGE_GROW | early | STAGE_AFTER_SEED_LOOP | STAGE_COMPLETE_ONLY | wide)
                 sets_done = torch.cuda.Event()
@@ -626,7 +643,7 @@ class DecodePipeline:
             back_done = torch.cuda.Event()
             back_done.record()
             pending = DecodeEngine.fetch_async(b, compact, device_out=device_out,
-                                               stream=self.tail)
+                                               stream=tail)
         pending.on_counts = self._note_counts
         self._back_done[par] = back_done
         self._sets_done[par] = sets_done or back_done
