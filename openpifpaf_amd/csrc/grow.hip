@@ -849,6 +849,11 @@ __device__ __forceinline__ void flat_load(const float *__restrict__ cf, int64_t 
 // column: two 16-byte reads).  cofs[q] = its offset, -1 = global.
 constexpr int kColPad = 8;
 constexpr int kColLds = 20480;  // 80 KB (64 KB: 1-2% slower per planted cfg3 step)
+// the external-helper kernel (seed_loop_ext_kernel: images with helpers on other CUs, e.g.
+// cfg5) stages 48 KB: the LDS it leaves lets the other batch's kernels share its CUs (cfg5
+// uniform 1452-1473 -> 1583-1585 images/s, planted 41.3k -> 43.1k-43.7k; 80 KB for the
+// one-CU kernel, where 48 / 64 KB measured 1 % slower, A/B on one box)
+constexpr int kColLdsExt = 12288;
 struct ColStage {
     const int *ncol;   // set-A column counts per (CAF, direction)
     const int *cofs;
@@ -1945,10 +1950,10 @@ struct SeedLoopSharedX : SeedLoopSharedT<kCacheSlots> {
 };
 
 // joints of cache slot q (LDS): this CU's slots in SeedLoopShared, the external ones in the
-// dynamic LDS after the kColLds column floats (launched only when n_ext > 0)
+// dynamic LDS after the kColLdsExt column floats (launched only when n_ext > 0)
 __device__ __forceinline__ float4 *cache_joints(SeedLoopSharedX &S, float *s_cols, int q) {
     return q < kSpecCache ? S.cache_j[q]
-                          : reinterpret_cast<float4 *>(s_cols + kColLds) + (q - kSpecCache) * kKP;
+                          : reinterpret_cast<float4 *>(s_cols + kColLdsExt) + (q - kSpecCache) * kKP;
 }
 
 __device__ __forceinline__ int lds_acquire(int *p) {
@@ -2161,7 +2166,7 @@ __device__ __forceinline__ void plan_unlock(SeedLoopSharedT<NS> &S) {
 // counts into s_ncol, LDS offsets into s_cofs (-1: read from global memory).  Every wave of
 // the workgroup takes part; no barrier after the copy (the caller's init barrier follows).
 __device__ __forceinline__ ColStage stage_small_sets(const GrowArgs &g, int img, int *s_ncol,
-                                                     int *s_cofs, float *s_cols) {
+                                                     int *s_cofs, float *s_cols, int cap) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int q = threadIdx.x; q < 2 * g.C; q += blockDim.x) s_ncol[q] = col_offs(g, 0, img, q >> 1, q & 1)[g.nb];
     __syncthreads();
@@ -2169,7 +2174,7 @@ __device__ __forceinline__ ColStage stage_small_sets(const GrowArgs &g, int img,
         int o = 0;
         for (int q = 0; q < 2 * g.C; q++) {
             const int sz = kColPad * s_ncol[q];
-            const bool fit = s_ncol[q] <= kFlatCols && o + sz <= kColLds;
+            const bool fit = s_ncol[q] <= kFlatCols && o + sz <= cap;
             s_cofs[q] = fit ? o : -1;
             o += fit ? sz : 0;
         }
@@ -2293,7 +2298,7 @@ void seed_loop_kernel(GrowArgs g) {
     const int K = g.K;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     SeedLDS &L = Ls[wave];
-    const ColStage cstage = stage_small_sets(g, img, s_ncol, s_cofs, s_cols);
+    const ColStage cstage = stage_small_sets(g, img, s_ncol, s_cofs, s_cols, kColLds);
     if (lane == 0) {
         L.status = 0;
         L.log_n = 0;
@@ -2513,8 +2518,8 @@ void seed_loop_ext_kernel(GrowArgs g) {
     __shared__ int s_ncol[2 * PP_MAX_EDGES];  // set-A column counts per (CAF, direction)
     __shared__ int s_cofs[2 * PP_MAX_EDGES];  // their LDS offsets in s_cols (-1: global)
     __shared__ SeedOcc s_occ;  // per-seed occupancy (the image's own workgroup)
-    // kColLds floats (dynamic: the launch sizes it), then with n_ext > 0 the external
-    // slots' joints (cache_joints)
+    // kColLdsExt floats (dynamic: the launch sizes it), then the external slots' joints
+    // (cache_joints)
     extern __shared__ float s_cols[];
     const int n_img = (int)gridDim.x / (1 + g.n_ext);
     const bool external = (int)blockIdx.x >= n_img;
@@ -2522,7 +2527,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
     const int K = g.K;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     SeedLDS &L = Ls[wave];
-    const ColStage cstage = stage_small_sets(g, img, s_ncol, s_cofs, s_cols);
+    const ColStage cstage = stage_small_sets(g, img, s_ncol, s_cofs, s_cols, kColLdsExt);
     if (lane == 0) {
         L.status = 0;
         L.log_n = 0;
@@ -2636,7 +2641,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
             uint64_t left = 1ull << wave;
             if (kSelfPlanExt && !lds_acquire(&S.done)) {
                 const int dec = lds_acquire(&S.decided);
-                left = spec_plan(S, reinterpret_cast<const float4 *>(s_cols + kColLds), seeds,
+                left = spec_plan(S, reinterpret_cast<const float4 *>(s_cols + kColLdsExt), seeds,
                                  n_seeds, dec, dec, kSelfScan, occ, red, occ_msr(g), g.spec_far,
                                  left, socc_on ? s_occ.cnt : nullptr);
             }
@@ -3947,8 +3952,9 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
             if (g.n_ext > 0 &&
                 hipMemsetAsync(g.xext, 0, (size_t)n_img * sizeof(SeedExt), s) != hipSuccess)
                 return fail(PP_EHIP, "pp_decode_batch: seed-loop hand-off reset failed");
-            const size_t dyn = kColLds * sizeof(float) +
-                               (g.n_ext > 0 ? (size_t)kExtCache * kKP * sizeof(float4) : 0);
+            const size_t dyn = g.n_ext > 0
+                                   ? kColLdsExt * sizeof(float) + (size_t)kExtCache * kKP * sizeof(float4)
+                                   : kColLds * sizeof(float);
             // confidence_scales: their own kernel instances (the default ones carry no
             // registers for them: complete_kernel stays at 128 VGPRs, 4 waves per SIMD)
             const dim3 blk(64 * kSeedWaves);
