@@ -127,7 +127,7 @@ struct GrowArgs {
     pp_ann *spec;             // (n_img, kSpecCache) speculatively grown annotations
     float spec_far;           // seed-loop speculation distance, in joint scales
     int n_ext;                // external helper workgroups per image (seed loop)
-    SeedExt *xext;            // (n_img) their hand-off words (zeroed before each launch)
+    SeedExt *xext;            // (n_img) their hand-off words (zero at launch; NMS re-zeroes)
     pp_ann *xrec;             // (n_img, kExtCache) their published annotations
     double *nms_score;        // (n_img, 2 * ann_cap)
     // standalone NMS over caller annotations (pp_nms_keypoints_scored), else NULL: per
@@ -1855,7 +1855,7 @@ constexpr int kExtHeavyAnns = 8;
 constexpr uint64_t kExtIdleLight = 30000ull, kExtIdleHeavy = 100000000ull;
 constexpr uint64_t kExtWaitMax = 200000000ull;
 
-struct SeedExt {  // per image; zeroed before every launch that has external helpers
+struct SeedExt {  // per image; zero at every launch (workspace zero region; nms_kernel re-zeroes)
     unsigned long long task[kExtHelpers];  // 0 absent, 1 idle, 3 left; assigned: 2 |
                                            // slot << 8 | seed << 32
     unsigned int tag[kExtCache];           // seed + 1 of the record published in the slot
@@ -3104,6 +3104,12 @@ __global__ __launch_bounds__(64 * W) void nms_kernel(GrowArgs g) {
         s_status = g.status[img];
         g.complete_next[img] = 0;  // workspace contract: left zero
     }
+    // the external-helper seed loop's hand-off words of this image: zero for the
+    // workspace's next seed loop (workspace contract; a memset before each loop launch
+    // waited for a free CU behind the other batch's kernels: 3.2 ms per cfg5 uniform step)
+    if (g.xext && threadIdx.x < (int)(sizeof(SeedExt) / 4)) {
+        reinterpret_cast<uint32_t *>(g.xext + img)[threadIdx.x] = 0u;
+    }
 #ifdef PP_STAMPS
     if (lane == 0)
         for (int q = 0; q < 8; q++) L.fst[q] = 0;
@@ -3949,9 +3955,8 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
         // PP_STAGE_SEED_LOOP_ONLY / PP_STAGE_AFTER_SEED_LOOP split stage 8 in two calls
         const bool run_rest = !(stages & PP_STAGE_SEED_LOOP_ONLY);
         if (!(stages & PP_STAGE_AFTER_SEED_LOOP)) {
-            if (g.n_ext > 0 &&
-                hipMemsetAsync(g.xext, 0, (size_t)n_img * sizeof(SeedExt), s) != hipSuccess)
-                return fail(PP_EHIP, "pp_decode_batch: seed-loop hand-off reset failed");
+            // g.xext is zero: the workspace's zero region, left zero by the NMS kernel that
+            // ends every decode on it
             const size_t dyn = g.n_ext > 0
                                    ? kColLdsExt * sizeof(float) + (size_t)kExtCache * kKP * sizeof(float4)
                                    : kColLds * sizeof(float);
