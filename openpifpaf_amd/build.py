@@ -23,10 +23,11 @@ CFLAGS = [
 ]
 
 
-# per-file flags: splat.hip's fold gains nothing from packed f32 (v_pk_* costs what its two
-# halves cost on gfx950, plus the v_movs that form register pairs); without the SLP
-# vectorizer the uniform CifHr runs 2-3 % faster (dense 5.41 -> 5.31 ms, sparse 4.36 -> 4.14-4.25
-# ms per 256 images, A/B on one box)
+# per-file flags: splat.hip's fold gains nothing from packed f32; without the SLP vectorizer
+# the uniform CifHr runs 2-3 % faster (dense 5.41 -> 5.31 ms, sparse 4.36 -> 4.14-4.25 ms per
+# 256 images, A/B on one box).  Hand-written packed folds measured slower too (dense uniform
+# 5.48 -> 5.86-5.99 ms, profiles/r05p_fold_packed_ab.txt), although an isolated stream of
+# v_pk_fma_f32 runs 1.6-1.9x the element rate of v_fma_f32 (tools/ubench/pk_rate.hip)
 FILE_FLAGS = {'splat.hip': ['-fno-slp-vectorize']}
 
 

@@ -18,11 +18,11 @@ for rep in 1 2; do
 import json, sys
 d = json.load(open(sys.argv[1]))
 c5, c2 = d.get('cfg5', {}), d.get('cfg2', {})
-print('{:8s} planted {:8.0f} ({:.4f} ms) uniform {:7.0f} cfg5 p/u {:6.0f} / {:5.0f} cfg2 p/u {} / {} us  hr {:.3f} ms'.format(
+print('{:8s} planted {:8.0f} ({:.4f} ms) uniform {:7.0f} cfg5 p/u {:6.0f} / {:5.0f} cfg2 p/u {} / {} us  hr {:.3f} ms hr_u {:.3f} ms'.format(
     sys.argv[2], d['value'], d['ms_per_step'], d.get('uniform', {}).get('value', 0),
     c5.get('planted', {}).get('value', 0), c5.get('uniform', {}).get('value', 0),
     c2.get('planted', {}).get('us_per_call_device'), c2.get('uniform', {}).get('us_per_call_device'),
-    d['roofline']['ms_per_launch']))
+    d['roofline']['ms_per_launch'], d.get('roofline_uniform', {}).get('ms_per_launch', 0)))
 PY
   done
 done
