@@ -645,6 +645,28 @@ int pp_center_filter_cpu(const float *field, int64_t rows, int64_t n, int64_t pi
                          float x, float y, float sigma, void *out, int64_t out_pitch,
                          int32_t *count);
 
+/* ---------------------------------------------------------------------------------
+ * Host twins of the front stages (csrc/stages_cpu.hip): pp_cifhr / pp_seeds /
+ * pp_caf_scored for one CIF and one CAF head with the same layouts, HOST pointers, run on
+ * the calling thread in the reference's order (the stage classes are CPU-only NumPy code).
+ * Explicit entry points only, as the primitives' twins above.
+ *   pp_cifhr_cpu       CifHr.fill / fill_cif (cif_hr.py:23-81): cifhr (n_img, K, H', pitch),
+ *                      pitch = pp_cifhr_pitch(W'), zeroed then accumulated
+ *   pp_seeds_cpu       CifSeeds.fill + get (cif_seeds.py:23-64): seeds (n_img, seed_capacity)
+ *                      sorted as sorted(seeds, reverse=True), counts (n_img); PP_ESHAPE when
+ *                      an image has more than seed_capacity seeds
+ *   pp_caf_scored_cpu  CafScored.fill (caf_scored.py:32-98) at score_th: cols
+ *                      (n_img, C, 2, 9, H*W), dir 0 backward, 1 forward; counts (n_img, C, 2)
+ * --------------------------------------------------------------------------------- */
+int pp_cifhr_cpu(const float *cif, int32_t n_img, int32_t K, int32_t H, int32_t W,
+                 const pp_config *cfg, float *cifhr);
+int pp_seeds_cpu(const float *cif, const float *cifhr, int32_t n_img, int32_t K, int32_t H,
+                 int32_t W, const pp_config *cfg, pp_seed *seeds, int32_t seed_capacity,
+                 int32_t *counts);
+int pp_caf_scored_cpu(const float *caf, const float *cifhr, int32_t n_img, int32_t K, int32_t C,
+                      int32_t H, int32_t W, const int32_t *skeleton, float score_th,
+                      const pp_config *cfg, float *cols, int32_t *counts);
+
 #ifdef __cplusplus
 }
 #endif

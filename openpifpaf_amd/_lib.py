@@ -120,6 +120,11 @@ _SIGNATURES = {
                              ctypes.c_int),
     'pp_center_filter_cpu': ([_vp, _i64, _i64, _i64, _i32, _f, _f, _f, _vp, _i64, _vp],
                              ctypes.c_int),
+    # host twins of the front stages (csrc/stages_cpu.hip)
+    'pp_cifhr_cpu': ([_vp, _i32, _i32, _i32, _i32, _vp, _vp], ctypes.c_int),
+    'pp_seeds_cpu': ([_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp], ctypes.c_int),
+    'pp_caf_scored_cpu': ([_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _f, _vp, _vp, _vp],
+                          ctypes.c_int),
 }
 
 EXPORTED = tuple(_SIGNATURES)

@@ -1,0 +1,79 @@
+"""Host twins of the decoder's front stages on NumPy arrays: pp_cifhr_cpu, pp_seeds_cpu and
+pp_caf_scored_cpu (csrc/stages_cpu.hip) -- CifHr.fill (cif_hr.py:23-81), CifSeeds.fill + get
+(cif_seeds.py:23-64) and CafScored.fill (caf_scored.py:32-98) for one CIF and one CAF head,
+on the calling thread.
+
+An explicit host API, like openpifpaf_amd.functional_cpu: the decoder classes compute on the
+device and never fall back to it, and it raises when the library is missing.  `cfg` is a
+pp_config (openpifpaf_amd._abi.make_config); the outputs match the device stages bit for bit
+(tests/test_stages_cpu.py pins them to the reference's own fixtures).
+"""
+import ctypes
+
+import numpy as np
+
+from ._abi import SEED_DTYPE
+from ._lib import call
+
+
+def _f32(a, ndim, what):
+    if not isinstance(a, np.ndarray) or a.ndim != ndim:
+        raise ValueError('{} must be a {}-d NumPy array'.format(what, ndim))
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _hr_shape(h, w, stride):
+    hh, ww = (h - 1) * stride + 1, (w - 1) * stride + 1
+    return hh, ww, (ww + 31) // 32 * 32
+
+
+def cifhr(cif, cfg):
+    """cif (n, K, 5, H, W) -> the CifHr maps (n, K, H', pitch) float32 (columns past W' are
+    zero); `[..., :W']` is CifHr.accumulated of each image."""
+    cif = _f32(cif, 5, 'cif')
+    n, k, _, h, w = cif.shape
+    hh, _, pitch = _hr_shape(h, w, cfg.stride)
+    out = np.empty((n, k, hh, pitch), np.float32)
+    call('pp_cifhr_cpu', cif.ctypes.data, n, k, h, w, ctypes.byref(cfg), out.ctypes.data)
+    return out
+
+
+def seeds(cif, hr, cfg):
+    """cif (n, K, 5, H, W), hr (n, K, H', pitch) from cifhr() -> per image a SEED_DTYPE array
+    in CifSeeds.get() order (v, field, x, y, s)."""
+    cif = _f32(cif, 5, 'cif')
+    hr = _f32(hr, 4, 'hr')
+    n, k, _, h, w = cif.shape
+    if hr.shape != (n, k) + _hr_shape(h, w, cfg.stride)[::2]:
+        raise ValueError('hr must be (n, K, H\', pitch) for these fields')
+    cap = max(1, k * h * w)
+    out = np.empty((n, cap), SEED_DTYPE)
+    counts = np.empty(n, np.int32)
+    call('pp_seeds_cpu', cif.ctypes.data, hr.ctypes.data, n, k, h, w, ctypes.byref(cfg),
+         out.ctypes.data, cap, counts.ctypes.data)
+    return [out[i, :counts[i]].copy() for i in range(n)]
+
+
+def caf_scored(caf, hr, skeleton, score_th, cfg):
+    """caf (n, C, 9, H, W), hr (n, K, H', pitch), 1-based skeleton (C, 2) -> per image
+    (forward, backward): lists over the C fields of (9, N) float32 column sets, as
+    CafScored(score_th=...).fill() holds them."""
+    caf = _f32(caf, 5, 'caf')
+    hr = _f32(hr, 4, 'hr')
+    n, c, _, h, w = caf.shape
+    k = hr.shape[1]
+    if hr.shape != (n, k) + _hr_shape(h, w, cfg.stride)[::2]:
+        raise ValueError('hr must be (n, K, H\', pitch) for these fields')
+    sk = np.ascontiguousarray(skeleton, dtype=np.int32).reshape(-1, 2)
+    if len(sk) != c:
+        raise ValueError('skeleton has {} pairs for {} CAF fields'.format(len(sk), c))
+    cols = np.empty((n, c, 2, 9, h * w), np.float32)
+    counts = np.empty((n, c, 2), np.int32)
+    call('pp_caf_scored_cpu', caf.ctypes.data, hr.ctypes.data, n, k, c, h, w, sk.ctypes.data,
+         ctypes.c_float(score_th), ctypes.byref(cfg), cols.ctypes.data, counts.ctypes.data)
+    out = []
+    for i in range(n):
+        fwd = [cols[i, f, 1, :, :counts[i, f, 1]].copy() for f in range(c)]
+        bwd = [cols[i, f, 0, :, :counts[i, f, 0]].copy() for f in range(c)]
+        out.append((fwd, bwd))
+    return out
