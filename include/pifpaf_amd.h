@@ -666,6 +666,12 @@ int pp_seeds_cpu(const float *cif, const float *cifhr, int32_t n_img, int32_t K,
 int pp_caf_scored_cpu(const float *caf, const float *cifhr, int32_t n_img, int32_t K, int32_t C,
                       int32_t H, int32_t W, const int32_t *skeleton, float score_th,
                       const pp_config *cfg, float *cols, int32_t *counts);
+/* nms.Keypoints.annotations (nms.py:17-57) as pp_nms_keypoints, on host records (no workspace):
+ * anns edited in place, survivors sorted by -score in out with their score, out_counts,
+ * out_index (optional) = each survivor's input index. */
+int pp_nms_keypoints_cpu(pp_ann *anns, const int32_t *counts, int32_t n_img, int32_t K,
+                         int32_t ann_capacity, const pp_config *cfg, pp_ann *out,
+                         int32_t *out_counts, int32_t *out_index);
 
 #ifdef __cplusplus
 }

@@ -125,6 +125,7 @@ _SIGNATURES = {
     'pp_seeds_cpu': ([_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp], ctypes.c_int),
     'pp_caf_scored_cpu': ([_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _f, _vp, _vp, _vp],
                           ctypes.c_int),
+    'pp_nms_keypoints_cpu': ([_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp], ctypes.c_int),
 }
 
 EXPORTED = tuple(_SIGNATURES)

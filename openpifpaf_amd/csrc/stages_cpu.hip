@@ -41,9 +41,141 @@ uint32_t f32_bits(float v) {
     return u;
 }
 
+// numpy's pairwise sum (n <= 128), as Annotation.score()'s np.sum adds its K products
+double pw_sum_cpu(const double *a, int n) {
+    if (n < 8) {
+        double res = 0.0;
+        for (int i = 0; i < n; i++) res += a[i];
+        return res;
+    }
+    double r[8];
+    for (int j = 0; j < 8; j++) r[j] = a[j];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8)
+        for (int j = 0; j < 8; j++) r[j] += a[i + j];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; i++) res += a[i];
+    return res;
+}
+
+// Annotation.score() (annotation.py:60-71) with the default weights: 3 / (3 min(K, 3) +
+// K - min(K, 3)) for the three largest v, 1 / (...) for the rest, np.sort(v)[::-1] order
+double ann_score_cpu(const pp_ann &a, int K) {
+    float v[PP_MAX_KP];
+    for (int j = 0; j < K; j++) v[j] = a.data[j][2];
+    std::stable_sort(v, v + K, [](float p, float q) { return p > q; });
+    const double ws = (double)(3 * std::min(K, 3) + (K - std::min(K, 3)));
+    double prod[PP_MAX_KP];
+    for (int r = 0; r < K; r++) prod[r] = ((r < 3 ? 3.0 : 1.0) / ws) * (double)v[r];
+    return pw_sum_cpu(prod, K);
+}
+
+// Occupancy of nms.Keypoints (nms.py:27-31): (K, int(max y + 1) / r, int(max x + 1) / r) u8
+struct NmsOcc {
+    std::vector<uint8_t> p;
+    int64_t h = 0, w = 0;
+    int K = 0;
+    float red = 2.0f, msr = 2.0f;
+    bool get(int f, float x, float y) const {  // occupancy.py:41-47
+        if (f >= K) return true;
+        if (h <= 0 || w <= 0) return false;
+        const int64_t xi = (int64_t)pp::clip_ref(x / red, 0.0f, (float)(w - 1));
+        const int64_t yi = (int64_t)pp::clip_ref(y / red, 0.0f, (float)(h - 1));
+        return p[((int64_t)f * h + yi) * w + xi] != 0;
+    }
+    void set(int f, float x, float y, float s) {  // occupancy.py:31-39, utils.py:61-66
+        int64_t x0, x1, y0, y1;
+        if (!pp::occupancy_mark_box(f, K, h, w, x, y, s, red, msr, x0, x1, y0, y1)) return;
+        for (int64_t yy = y0; yy < y1; yy++)
+            for (int64_t xx = x0; xx < x1; xx++) {
+                uint8_t &c = p[((int64_t)f * h + yy) * w + xx];
+                c = (uint8_t)(c + 1);
+            }
+    }
+};
+
 }  // namespace
 
 extern "C" {
+
+// nms.Keypoints.annotations (nms.py:17-57) per group of records, as pp_nms_keypoints: anns
+// edited in place (joints below keypoint_threshold zeroed, suppressed v scaled), survivors
+// sorted by -score into out with their score, out_counts, out_index (optional) = input index.
+int pp_nms_keypoints_cpu(pp_ann *anns, const int32_t *counts, int32_t n_img, int32_t K,
+                         int32_t ann_capacity, const pp_config *cfg, pp_ann *out,
+                         int32_t *out_counts, int32_t *out_index) {
+    if (!anns || !counts || !cfg || !out || !out_counts)
+        return pp::fail(PP_EINVAL, "pp_nms_keypoints_cpu: NULL argument");
+    if (n_img < 0 || K <= 0 || K > PP_MAX_KP || ann_capacity <= 0 || cfg->occupancy_reduction <= 0)
+        return pp::fail(PP_ESHAPE, "pp_nms_keypoints_cpu: bad shape");
+    const float kt = cfg->nms_keypoint_threshold;
+    const double it = (double)cfg->nms_instance_threshold;
+    std::vector<int> keep;
+    std::vector<double> score;
+    for (int img = 0; img < n_img; img++) {
+        pp_ann *a = anns + (int64_t)img * ann_capacity;
+        const int n = std::min(counts[img], ann_capacity);
+        if (n < 0) return pp::fail(PP_ESHAPE, "pp_nms_keypoints_cpu: negative count");
+        auto threshold_filter = [&](std::vector<int> &idx) {  // nms.py:20-21 / 47-49
+            std::vector<int> kept;
+            for (int i : idx) {
+                for (int j = 0; j < K; j++)
+                    if (a[i].data[j][2] < kt) a[i].data[j][0] = a[i].data[j][1] = a[i].data[j][2] = 0.0f;
+                score[i] = ann_score_cpu(a[i], K);
+                if (score[i] >= it) kept.push_back(i);
+            }
+            std::stable_sort(kept.begin(), kept.end(),
+                             [&](int p, int q) { return -score[p] < -score[q]; });
+            idx.swap(kept);
+        };
+        keep.resize(n);
+        score.assign(n, 0.0);
+        for (int i = 0; i < n; i++) keep[i] = i;
+        threshold_filter(keep);
+        if (!keep.empty()) {
+            NmsOcc occ;
+            occ.K = K;
+            occ.red = (float)cfg->occupancy_reduction;
+            occ.msr = (float)((double)cfg->occupancy_min_scale / cfg->occupancy_reduction);
+            float mx = 0.0f, my = 0.0f;
+            bool first = true;
+            for (int i = 0; i < n; i++) {  // max over the kept annotations in input order
+                if (std::find(keep.begin(), keep.end(), i) == keep.end()) continue;
+                float ax = a[i].data[0][0], ay = a[i].data[0][1];
+                for (int j = 1; j < K; j++) {
+                    ax = a[i].data[j][0] > ax ? a[i].data[j][0] : ax;
+                    ay = a[i].data[j][1] > ay ? a[i].data[j][1] : ay;
+                }
+                if (first || ax > mx) mx = ax;
+                if (first || ay > my) my = ay;
+                first = false;
+            }
+            const int64_t oh = (int64_t)((double)(int64_t)(my + 1.0f) / cfg->occupancy_reduction);
+            const int64_t ow = (int64_t)((double)(int64_t)(mx + 1.0f) / cfg->occupancy_reduction);
+            occ.h = oh > 0 ? oh : 0;
+            occ.w = ow > 0 ? ow : 0;
+            occ.p.assign((size_t)(K * occ.h * occ.w), 0);
+            for (int i : keep)  // nms.py:33-45, in score order
+                for (int f = 0; f < K; f++) {
+                    float *xyv = a[i].data[f];
+                    if (xyv[2] == 0.0f) continue;
+                    if (occ.get(f, xyv[0], xyv[1]))
+                        xyv[2] = xyv[2] * cfg->nms_suppression;
+                    else
+                        occ.set(f, xyv[0], xyv[1], a[i].joint_scales[f]);
+                }
+            threshold_filter(keep);
+        }
+        pp_ann *o = out + (int64_t)img * ann_capacity;
+        for (size_t r = 0; r < keep.size(); r++) {
+            o[r] = a[keep[r]];
+            o[r].score = score[keep[r]];
+            if (out_index) out_index[(int64_t)img * ann_capacity + r] = keep[r];
+        }
+        out_counts[img] = (int32_t)keep.size();
+    }
+    return PP_OK;
+}
 
 // CifHr.fill (cif_hr.py:23-81) for one head: per image and field, the cells with
 // c > v_threshold in row-major order as truncate-1 splats of v / neighbors / len_cifs at

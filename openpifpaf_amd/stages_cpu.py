@@ -1,7 +1,8 @@
-"""Host twins of the decoder's front stages on NumPy arrays: pp_cifhr_cpu, pp_seeds_cpu and
-pp_caf_scored_cpu (csrc/stages_cpu.hip) -- CifHr.fill (cif_hr.py:23-81), CifSeeds.fill + get
-(cif_seeds.py:23-64) and CafScored.fill (caf_scored.py:32-98) for one CIF and one CAF head,
-on the calling thread.
+"""Host twins of decoder stages on NumPy arrays: pp_cifhr_cpu, pp_seeds_cpu,
+pp_caf_scored_cpu and pp_nms_keypoints_cpu (csrc/stages_cpu.hip) -- CifHr.fill
+(cif_hr.py:23-81), CifSeeds.fill + get (cif_seeds.py:23-64) and CafScored.fill
+(caf_scored.py:32-98) for one CIF and one CAF head, and nms.Keypoints.annotations
+(nms.py:17-57), on the calling thread.
 
 An explicit host API, like openpifpaf_amd.functional_cpu: the decoder classes compute on the
 device and never fall back to it, and it raises when the library is missing.  `cfg` is a
@@ -12,7 +13,7 @@ import ctypes
 
 import numpy as np
 
-from ._abi import SEED_DTYPE
+from ._abi import ANN_DTYPE, SEED_DTYPE
 from ._lib import call
 
 
@@ -77,3 +78,25 @@ def caf_scored(caf, hr, skeleton, score_th, cfg):
         bwd = [cols[i, f, 0, :, :counts[i, f, 0]].copy() for f in range(c)]
         out.append((fwd, bwd))
     return out
+
+
+def nms_keypoints(data, joint_scales, cfg):
+    """nms.Keypoints.annotations over one list of annotations given as data (N, K, 3) float32
+    (edited in place as the reference edits ann.data) and joint_scales (N, K), with cfg's
+    nms_* thresholds -> (input indices of the survivors in output order, their scores)."""
+    if not isinstance(data, np.ndarray) or data.dtype != np.float32 or data.ndim != 3:
+        raise ValueError('data must be a float32 (N, K, 3) NumPy array')
+    n, k, _ = data.shape
+    recs = np.zeros(max(1, n), ANN_DTYPE)
+    recs['data'][:n, :k] = data
+    recs['joint_scales'][:n, :k] = joint_scales
+    recs['n_keypoints'] = k
+    out = np.zeros_like(recs)
+    counts = np.array([n], np.int32)
+    out_counts = np.zeros(1, np.int32)
+    index = np.zeros(len(recs), np.int32)
+    call('pp_nms_keypoints_cpu', recs.ctypes.data, counts.ctypes.data, 1, k, len(recs),
+         ctypes.byref(cfg), out.ctypes.data, out_counts.ctypes.data, index.ctypes.data)
+    data[...] = recs['data'][:n, :k]
+    m = int(out_counts[0])
+    return index[:m].tolist(), out['score'][:m].copy()

@@ -68,3 +68,19 @@ def test_stages_cpu_errors(sc):
         sc.caf_scored(np.zeros((1, 2, 9, 4, 4), np.float32), sc.cifhr(cif, cfg), [(1, 2)], 0.1, cfg)
     with pytest.raises(PPError, match='1-based'):
         sc.caf_scored(np.zeros((1, 1, 9, 4, 4), np.float32), sc.cifhr(cif, cfg), [(0, 2)], 0.1, cfg)
+
+
+@pytest.mark.parametrize('name', ['eval', 'predict', 'supp', 'dense', 'zeros'])
+def test_nms_keypoints_cpu_vs_reference(sc, name):
+    """pp_nms_keypoints_cpu against nms.Keypoints runs of the reference (tests/golden/nms.npz):
+    survivor order, in-place edits of every annotation, scores."""
+    import os
+    from openpifpaf_amd._abi import make_config
+    g = np.load(os.path.join(gu.GOLDEN, 'nms.npz'))
+    kt, it, sup = (float(t) for t in g[name + '_cfg'])
+    cfg = make_config(nms_keypoint_threshold=kt, nms_instance_threshold=it, nms_suppression=sup)
+    data = g[name + '_data_in'].astype(np.float32).copy()
+    order, scores = sc.nms_keypoints(data, g[name + '_scales'].astype(np.float32), cfg)
+    assert order == g[name + '_order'].tolist()
+    assert np.array_equal(data, g[name + '_data_out'])
+    assert np.array_equal(scores, g[name + '_score'])
