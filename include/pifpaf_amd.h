@@ -672,6 +672,12 @@ int pp_caf_scored_cpu(const float *caf, const float *cifhr, int32_t n_img, int32
 int pp_nms_keypoints_cpu(pp_ann *anns, const int32_t *counts, int32_t n_img, int32_t K,
                          int32_t ann_capacity, const pp_config *cfg, pp_ann *out,
                          int32_t *out_counts, int32_t *out_index);
+/* pp_nms_keypoints_scored on host records (each record's own Annotation.score()). */
+int pp_nms_keypoints_scored_cpu(pp_ann *anns, const int32_t *counts, int32_t n_img, int32_t K,
+                                int32_t ann_capacity, const pp_config *cfg,
+                                double instance_threshold, const int32_t *score_spec,
+                                const double *score_weights, const double *fixed_score,
+                                pp_ann *out, int32_t *out_counts, int32_t *out_index);
 
 #ifdef __cplusplus
 }

@@ -126,6 +126,8 @@ _SIGNATURES = {
     'pp_caf_scored_cpu': ([_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _f, _vp, _vp, _vp],
                           ctypes.c_int),
     'pp_nms_keypoints_cpu': ([_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp], ctypes.c_int),
+    'pp_nms_keypoints_scored_cpu': ([_vp, _vp, _i32, _i32, _i32, _vp, _f64, _vp, _vp, _vp, _vp,
+                                     _vp, _vp], ctypes.c_int),
 }
 
 EXPORTED = tuple(_SIGNATURES)

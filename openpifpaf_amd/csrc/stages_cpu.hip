@@ -60,13 +60,14 @@ double pw_sum_cpu(const double *a, int n) {
 
 // Annotation.score() (annotation.py:60-71) with the default weights: 3 / (3 min(K, 3) +
 // K - min(K, 3)) for the three largest v, 1 / (...) for the rest, np.sort(v)[::-1] order
-double ann_score_cpu(const pp_ann &a, int K) {
+// (zero_j >= 0: suppress_score_index, v[zero_j] reads as 0; w: the record's own score_weights)
+double ann_score_cpu(const pp_ann &a, int K, int zero_j = -1, const double *w = nullptr) {
     float v[PP_MAX_KP];
-    for (int j = 0; j < K; j++) v[j] = a.data[j][2];
+    for (int j = 0; j < K; j++) v[j] = j == zero_j ? 0.0f : a.data[j][2];
     std::stable_sort(v, v + K, [](float p, float q) { return p > q; });
     const double ws = (double)(3 * std::min(K, 3) + (K - std::min(K, 3)));
     double prod[PP_MAX_KP];
-    for (int r = 0; r < K; r++) prod[r] = ((r < 3 ? 3.0 : 1.0) / ws) * (double)v[r];
+    for (int r = 0; r < K; r++) prod[r] = (w ? w[r] : (r < 3 ? 3.0 : 1.0) / ws) * (double)v[r];
     return pw_sum_cpu(prod, K);
 }
 
@@ -101,15 +102,11 @@ extern "C" {
 // nms.Keypoints.annotations (nms.py:17-57) per group of records, as pp_nms_keypoints: anns
 // edited in place (joints below keypoint_threshold zeroed, suppressed v scaled), survivors
 // sorted by -score into out with their score, out_counts, out_index (optional) = input index.
-int pp_nms_keypoints_cpu(pp_ann *anns, const int32_t *counts, int32_t n_img, int32_t K,
-                         int32_t ann_capacity, const pp_config *cfg, pp_ann *out,
-                         int32_t *out_counts, int32_t *out_index) {
-    if (!anns || !counts || !cfg || !out || !out_counts)
-        return pp::fail(PP_EINVAL, "pp_nms_keypoints_cpu: NULL argument");
-    if (n_img < 0 || K <= 0 || K > PP_MAX_KP || ann_capacity <= 0 || cfg->occupancy_reduction <= 0)
-        return pp::fail(PP_ESHAPE, "pp_nms_keypoints_cpu: bad shape");
+static int nms_keypoints_host(pp_ann *anns, const int32_t *counts, int32_t n_img, int32_t K,
+                              int32_t ann_capacity, const pp_config *cfg, double it,
+                              const int32_t *spec, const double *sw, const double *fixed,
+                              pp_ann *out, int32_t *out_counts, int32_t *out_index) {
     const float kt = cfg->nms_keypoint_threshold;
-    const double it = (double)cfg->nms_instance_threshold;
     std::vector<int> keep;
     std::vector<double> score;
     for (int img = 0; img < n_img; img++) {
@@ -121,7 +118,13 @@ int pp_nms_keypoints_cpu(pp_ann *anns, const int32_t *counts, int32_t n_img, int
             for (int i : idx) {
                 for (int j = 0; j < K; j++)
                     if (a[i].data[j][2] < kt) a[i].data[j][0] = a[i].data[j][1] = a[i].data[j][2] = 0.0f;
-                score[i] = ann_score_cpu(a[i], K);
+                const int64_t gi = (int64_t)img * ann_capacity + i;
+                if (spec && spec[gi] == -2)
+                    score[i] = fixed[gi];  // fixed_score
+                else if (spec)
+                    score[i] = ann_score_cpu(a[i], K, spec[gi], sw + gi * K);
+                else
+                    score[i] = ann_score_cpu(a[i], K);
                 if (score[i] >= it) kept.push_back(i);
             }
             std::stable_sort(kept.begin(), kept.end(),
@@ -175,6 +178,35 @@ int pp_nms_keypoints_cpu(pp_ann *anns, const int32_t *counts, int32_t n_img, int
         out_counts[img] = (int32_t)keep.size();
     }
     return PP_OK;
+}
+
+int pp_nms_keypoints_cpu(pp_ann *anns, const int32_t *counts, int32_t n_img, int32_t K,
+                         int32_t ann_capacity, const pp_config *cfg, pp_ann *out,
+                         int32_t *out_counts, int32_t *out_index) {
+    if (!anns || !counts || !cfg || !out || !out_counts)
+        return pp::fail(PP_EINVAL, "pp_nms_keypoints_cpu: NULL argument");
+    if (n_img < 0 || K <= 0 || K > PP_MAX_KP || ann_capacity <= 0 || cfg->occupancy_reduction <= 0)
+        return pp::fail(PP_ESHAPE, "pp_nms_keypoints_cpu: bad shape");
+    return nms_keypoints_host(anns, counts, n_img, K, ann_capacity, cfg,
+                              (double)cfg->nms_instance_threshold, nullptr, nullptr, nullptr, out,
+                              out_counts, out_index);
+}
+
+// pp_nms_keypoints_scored on host records: each record's own Annotation.score()
+// (annotation.py:60-71; spec -2 fixed_score, -1 none, j suppress_score_index), the instance
+// threshold compared in float64
+int pp_nms_keypoints_scored_cpu(pp_ann *anns, const int32_t *counts, int32_t n_img, int32_t K,
+                                int32_t ann_capacity, const pp_config *cfg,
+                                double instance_threshold, const int32_t *score_spec,
+                                const double *score_weights, const double *fixed_score,
+                                pp_ann *out, int32_t *out_counts, int32_t *out_index) {
+    if (!anns || !counts || !cfg || !out || !out_counts ||
+        (score_spec && (!score_weights || !fixed_score)))
+        return pp::fail(PP_EINVAL, "pp_nms_keypoints_scored_cpu: NULL argument");
+    if (n_img < 0 || K <= 0 || K > PP_MAX_KP || ann_capacity <= 0 || cfg->occupancy_reduction <= 0)
+        return pp::fail(PP_ESHAPE, "pp_nms_keypoints_scored_cpu: bad shape");
+    return nms_keypoints_host(anns, counts, n_img, K, ann_capacity, cfg, instance_threshold,
+                              score_spec, score_weights, fixed_score, out, out_counts, out_index);
 }
 
 // CifHr.fill (cif_hr.py:23-81) for one head: per image and field, the cells with

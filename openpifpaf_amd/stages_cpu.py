@@ -80,10 +80,13 @@ def caf_scored(caf, hr, skeleton, score_th, cfg):
     return out
 
 
-def nms_keypoints(data, joint_scales, cfg):
+def nms_keypoints(data, joint_scales, cfg, *, score_spec=None, instance_threshold=None):
     """nms.Keypoints.annotations over one list of annotations given as data (N, K, 3) float32
     (edited in place as the reference edits ann.data) and joint_scales (N, K), with cfg's
-    nms_* thresholds -> (input indices of the survivors in output order, their scores)."""
+    nms_* thresholds -> (input indices of the survivors in output order, their scores).
+    score_spec = (spec (N,) int32, score_weights (N, K) float64, fixed (N,) float64) as
+    decoder.nms builds it: each annotation's own score() (pp_nms_keypoints_scored_cpu), with
+    instance_threshold (float64) replacing cfg's float32 one."""
     if not isinstance(data, np.ndarray) or data.dtype != np.float32 or data.ndim != 3:
         raise ValueError('data must be a float32 (N, K, 3) NumPy array')
     n, k, _ = data.shape
@@ -95,8 +98,19 @@ def nms_keypoints(data, joint_scales, cfg):
     counts = np.array([n], np.int32)
     out_counts = np.zeros(1, np.int32)
     index = np.zeros(len(recs), np.int32)
-    call('pp_nms_keypoints_cpu', recs.ctypes.data, counts.ctypes.data, 1, k, len(recs),
-         ctypes.byref(cfg), out.ctypes.data, out_counts.ctypes.data, index.ctypes.data)
+    if score_spec is None:
+        call('pp_nms_keypoints_cpu', recs.ctypes.data, counts.ctypes.data, 1, k, len(recs),
+             ctypes.byref(cfg), out.ctypes.data, out_counts.ctypes.data, index.ctypes.data)
+    else:
+        spec, sw, fixed = (np.ascontiguousarray(a, t) for a, t in
+                           zip(score_spec, (np.int32, np.float64, np.float64)))
+        if spec.shape != (n,) or sw.shape != (n, k) or fixed.shape != (n,):
+            raise ValueError('score_spec must be (N,), (N, K), (N,) arrays')
+        it = (float(cfg.nms_instance_threshold) if instance_threshold is None
+              else float(instance_threshold))
+        call('pp_nms_keypoints_scored_cpu', recs.ctypes.data, counts.ctypes.data, 1, k,
+             len(recs), ctypes.byref(cfg), it, spec.ctypes.data, sw.ctypes.data,
+             fixed.ctypes.data, out.ctypes.data, out_counts.ctypes.data, index.ctypes.data)
     data[...] = recs['data'][:n, :k]
     m = int(out_counts[0])
     return index[:m].tolist(), out['score'][:m].copy()

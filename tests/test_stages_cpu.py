@@ -84,3 +84,33 @@ def test_nms_keypoints_cpu_vs_reference(sc, name):
     assert order == g[name + '_order'].tolist()
     assert np.array_equal(data, g[name + '_data_out'])
     assert np.array_equal(scores, g[name + '_score'])
+
+
+@pytest.mark.parametrize('name', ['mixed', 'fixed_ties'])
+def test_nms_keypoints_scored_cpu_vs_reference(sc, name):
+    """pp_nms_keypoints_scored_cpu with fixed_score / suppress_score_index annotations
+    against the reference's runs (tests/golden/nms_scored.npz)."""
+    import os
+    from openpifpaf_amd import constants
+    from openpifpaf_amd._abi import make_config
+    from openpifpaf_amd.annotation import Annotation
+    from openpifpaf_amd.decoder.nms import _score_spec
+    g = np.load(os.path.join(gu.GOLDEN, 'nms_scored.npz'))
+    kt, it, sup = (float(t) for t in g[name + '_cfg'])
+    anns = []
+    for d, scl, fx, sp in zip(g[name + '_data_in'], g[name + '_scales'], g[name + '_fixed'],
+                              g[name + '_supp']):
+        a = Annotation(constants.COCO_KEYPOINTS, constants.COCO_PERSON_SKELETON,
+                       suppress_score_index=None if sp == -999 else int(sp))
+        if not np.isnan(fx):
+            a.fixed_score = float(fx)
+        anns.append(a)
+    spec = _score_spec(anns, 17)
+    assert spec is not None
+    cfg = make_config(nms_keypoint_threshold=kt, nms_instance_threshold=it, nms_suppression=sup)
+    data = g[name + '_data_in'].astype(np.float32).copy()
+    order, scores = sc.nms_keypoints(data, g[name + '_scales'].astype(np.float32), cfg,
+                                     score_spec=spec, instance_threshold=it)
+    assert order == g[name + '_order'].tolist()
+    assert np.array_equal(data, g[name + '_data_out'])
+    assert np.array_equal(scores, g[name + '_score'])
