@@ -364,6 +364,15 @@ def main():
     cifhr_bytes, hr_tiles, sector_bytes = cifhr_stage_bytes(cif_h, 8, cfg.cif_threshold,
                                                             cfg.seed_threshold)
     achieved = cifhr_bytes / (stage_avg[0] * 1e-3) / 1e9
+    if world > 1 and args.backend == 'gloo':
+        # the rehearsal's ranks share one GPU: 8 ranks x two 14.3 GB workspaces fill most of
+        # its 288 GB, so the decode workspaces go before the dense map's 9.6 GB per rank
+        # (memory budget)
+        import gc
+        pipe, eng = None, None
+        gc.collect()
+        torch.cuda.empty_cache()
+        dist.barrier()
     dense_ms = dense_cifhr_ms(cif, cfg, stream, args.steps, args.warmup)
     dense_bytes = 4 * k * (5 * h * w + hh * ww) * batch  # SURVEY.md §8d, per launch
     dense_gbs = dense_bytes / (dense_ms * 1e-3) / 1e9
@@ -529,10 +538,32 @@ def main():
         uc = synthetic.batch('uniform', 64, h, w, n_caf=len(skeleton)) if default_run else None
         line['cpu_baseline'] = cpu_baseline(cif_h, caf_h, skeleton, cfg, args.cpu_seconds,
                                             *(uc or (None, None)))
+    line['library'] = library_identity()
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def library_identity():
+    """Which library the line measured: `src_sha` (openpifpaf_amd.build.source_digest of
+    csrc/* and the header, the key profiles/<tag>_summary.json files are matched by), the
+    sha256 of the loaded .so itself, its variant ('product' unless PP_LIB_VARIANT loaded a
+    diagnostic or A/B build), and every PP_* environment variable this process saw.  The
+    product library reads none of them (diagnostic builds read their stamp paths); the
+    Python pipeline's PP_PIPE_* / PP_SPLIT_TAIL scheduling knobs change the order of
+    launches, never what is computed.  `headline` is false when the line did not run the
+    product library with the default schedule."""
+    import hashlib
+    from openpifpaf_amd import _lib
+    from openpifpaf_amd.build import source_digest
+    with open(_lib.LIB_PATH, 'rb') as f:
+        so_sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    env = {k: v for k, v in sorted(os.environ.items()) if k.startswith('PP_')}
+    variant = os.environ.get('PP_LIB_VARIANT') or 'product'
+    return {'src_sha': source_digest(), 'so_sha256_16': so_sha,
+            'so': os.path.relpath(_lib.LIB_PATH, REPO), 'variant': variant, 'pp_env': env,
+            'headline': variant == 'product' and not env}
 
 
 def cifhr_stage_bytes(cif, stride, v_th, seed_th=None, tile=64, block=8, lds_list=256):

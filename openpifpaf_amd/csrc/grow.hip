@@ -73,8 +73,7 @@ constexpr int kSlots = 2 * PP_MAX_EDGES;   // directed edges (two lanes' worth o
 // entries, so a fill pushes at most 2C <= 2 * PP_MAX_EDGES entries
 constexpr int kHeap = 2 * PP_MAX_EDGES + 8;
 constexpr int kOccMargin = 64;              // NMS occupancy slack beyond the main grid
-constexpr int kCompleteWays = 64;           // force-complete workgroups per image (dense hint)
-constexpr int kCompleteWaysSparse = 64;     // ... without it (PP_COMPLETE_WAYS overrides)
+constexpr int kCompleteWays = 64;           // force-complete workgroups per image
 
 struct FFEntry {  // _flood_fill frontier entry (-v, end_i, start_xyv, s)
     float neg;
@@ -127,7 +126,8 @@ struct GrowArgs {
     pp_ann *spec;             // (n_img, kSpecCache) speculatively grown annotations
     float spec_far;           // seed-loop speculation distance, in joint scales
     int n_ext;                // external helper workgroups per image (seed loop)
-    SeedExt *xext;            // (n_img) their hand-off words (zero at launch; NMS re-zeroes)
+    SeedExt *xext;            // (n_img) their hand-off words (zero at launch; the loop's last
+                              // workgroup out re-zeroes them, ext_exit)
     pp_ann *xrec;             // (n_img, kExtCache) their published annotations
     double *nms_score;        // (n_img, 2 * ann_cap)
     // standalone NMS over caller annotations (pp_nms_keypoints_scored), else NULL: per
@@ -1834,8 +1834,9 @@ constexpr bool kSelfPlanExt = false;
 // with sc1 loads.  A helper announces itself (task word 1 = idle) before wave 0 may hand
 // it a seed (CAS 1 -> assigned), so a workgroup that is not resident never holds one; an
 // idle helper leaves when wave 0 finishes (fin) or after kExtIdleTicks without work (CAS
-// 1 -> 3; losing that CAS to an assignment means: grow it).  Every polled word is zeroed
-// by a memset before each launch.
+// 1 -> 3; losing that CAS to an assignment means: grow it).  The image's workgroups count
+// themselves out (SeedExt.exited) after their last access to these words, and the last one
+// out zeroes them, so every launch finds them zero whatever runs between two seed loops.
 constexpr int kExtWgMax = 3;
 constexpr int kExtHelpers = kExtWgMax * kSeedWaves;
 constexpr int kExtCache = 32;
@@ -1855,13 +1856,15 @@ constexpr int kExtHeavyAnns = 8;
 constexpr uint64_t kExtIdleLight = 30000ull, kExtIdleHeavy = 100000000ull;
 constexpr uint64_t kExtWaitMax = 200000000ull;
 
-struct SeedExt {  // per image; zero at every launch (workspace zero region; nms_kernel re-zeroes)
+struct SeedExt {  // per image; zero at every launch (workspace zero region; the launch's
+                  // last workgroup out re-zeroes it, ext_exit)
     unsigned long long task[kExtHelpers];  // 0 absent, 1 idle, 3 left; assigned: 2 |
                                            // slot << 8 | seed << 32
     unsigned int tag[kExtCache];           // seed + 1 of the record published in the slot
     unsigned int fin;                      // wave 0 is done
     unsigned int heavy;                    // wave 0 switched to the heavy regime
-    unsigned int pad[2];
+    unsigned int exited;                   // workgroups of the image done with these words
+    unsigned int pad;
 };
 static_assert(sizeof(SeedExt) % 16 == 0, "memset block of whole 16-byte units");
 
@@ -1890,6 +1893,23 @@ __device__ __forceinline__ bool cas_agent_wave(unsigned long long *p, unsigned l
     int ok = 0;
     if ((threadIdx.x & 63) == 0) ok = cas_agent(p, expect, v) ? 1 : 0;
     return __builtin_amdgcn_readfirstlane(ok) != 0;
+}
+
+// One of an image's 1 + n_ext workgroups is done with its SeedExt words (called by every
+// thread after a __syncthreads that follows the workgroup's last access to them): it counts
+// itself out, and the last one out zeroes the words for the workspace's next seed loop.
+// Every workgroup of the image runs (a helper that was not resident before wave 0 finished
+// starts later, sees fin and leaves), so exactly one sees the count reach n_ext, after
+// every other workgroup's last access.  The workspace contract (zero at each launch) then
+// holds after any stage split (PP_STAGE_SEED_LOOP_ONLY with or without the NMS call).
+__device__ __forceinline__ void ext_exit(SeedExt *X, int n_ext) {
+    if (!X || threadIdx.x != 0) return;
+    __atomic_thread_fence(__ATOMIC_RELEASE);
+    const unsigned int before = __hip_atomic_fetch_add((gu32 *)&X->exited, 1u, __ATOMIC_ACQ_REL,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+    if (before != (unsigned int)n_ext) return;
+    unsigned int *w = reinterpret_cast<unsigned int *>(X);
+    for (int t = 0; t < (int)(sizeof(SeedExt) / 4); t++) st_agent(w + t, 0u);
 }
 
 // an LDS record to global memory, write-through (sc1), drained
@@ -2648,7 +2668,11 @@ void seed_loop_ext_kernel(GrowArgs g) {
             if (left && lane == 0) lds_release(&S.task[wave], -1);
             plan_unlock(S);
         }
-        if (external) return;
+        if (external) {  // every wave of an external workgroup is a helper
+            __syncthreads();
+            ext_exit(X, g.n_ext);
+            return;
+        }
     } else {
         __builtin_amdgcn_s_setprio(3);  // the committer is the critical path: issue first
         grow_initial<CS>(g, L, img, cstage, n_anns, [&](const pp_ann *a) {
@@ -2851,6 +2875,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
         }
     }
     __syncthreads();  // helpers drained: no wave of this CU is still growing into the cache
+    ext_exit(X, g.n_ext);
     if (wave == 0) {
         occ_clear(g, L, log, occ);
         STAMP(5);
@@ -3103,12 +3128,6 @@ __global__ __launch_bounds__(64 * W) void nms_kernel(GrowArgs g) {
     if (threadIdx.x == 0) {
         s_status = g.status[img];
         g.complete_next[img] = 0;  // workspace contract: left zero
-    }
-    // the external-helper seed loop's hand-off words of this image: zero for the
-    // workspace's next seed loop (workspace contract; a memset before each loop launch
-    // waited for a free CU behind the other batch's kernels: 3.2 ms per cfg5 uniform step)
-    if (g.xext && threadIdx.x < (int)(sizeof(SeedExt) / 4)) {
-        reinterpret_cast<uint32_t *>(g.xext + img)[threadIdx.x] = 0u;
     }
 #ifdef PP_STAMPS
     if (lane == 0)
@@ -3617,8 +3636,7 @@ size_t pp_decode_multi_workspace_zero_offset(const pp_scale *scales, int32_t n_s
 namespace pp {
 
 // One non-blocking side stream (+ fork / join events) per device, created on first use;
-// the mutex keeps concurrent host threads' fork / join pairs from interleaving.  PP_SIDE=0
-// turns the overlap off (diagnostics).
+// the mutex keeps concurrent host threads' fork / join pairs from interleaving.
 struct SideStream {
     hipStream_t stream;
     hipEvent_t fork, join;
@@ -3628,11 +3646,6 @@ struct SideStream {
 static const SideStream *side_stream() {
     static std::mutex create_mu;
     static SideStream *per_dev[64] = {};
-    static const bool off = [] {
-        const char *e = getenv("PP_SIDE");
-        return e && e[0] == '0';
-    }();
-    if (off) return nullptr;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
     std::lock_guard<std::mutex> lock(create_mu);
@@ -3651,15 +3664,9 @@ static const SideStream *side_stream() {
 }
 
 // External helper workgroups per image for the seed loop: enough to give every CU a seed
-// loop workgroup when the batch has fewer images than CUs (at most kExtWgMax); PP_SEED_EXT
-// overrides (diagnostics: 0 = none).
+// loop workgroup when the batch has fewer images than CUs (at most kExtWgMax).
 static int seed_ext_per_image(int n_img) {
     static int cus[64] = {};
-    static const int env = [] {
-        const char *e = getenv("PP_SEED_EXT");
-        return e ? atoi(e) : -1;
-    }();
-    if (env >= 0) return std::min(env, kExtWgMax);
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
     if (cus[dev] <= 0 &&
@@ -3671,21 +3678,13 @@ static int seed_ext_per_image(int n_img) {
     return std::max(0, std::min(kExtWgMax, cus[dev] / n_img - 1));
 }
 
-// Force-complete workgroups per image: kCompleteWays for batches the caller marks dense
-// (PP_STAGE_NMS_WIDE), else kCompleteWaysSparse; PP_COMPLETE_WAYS overrides the latter
-// (A/B builds).  The workgroups pull annotations from a per-image counter, so any count
-// gives the same result.
-static int complete_ways(uint32_t stages) {
-    static const int env = [] {
-        const char *e = getenv("PP_COMPLETE_WAYS");
-        return e ? atoi(e) : 0;
-    }();
-    if (stages & PP_STAGE_NMS_WIDE) return kCompleteWays;
-    return env > 0 ? std::min(env, 1024) : kCompleteWaysSparse;
-}
+// Force-complete workgroups per image.  The workgroups pull annotations from a per-image
+// counter, so any count gives the same result; 8 or 16 for sparse batches measured no
+// better than 64 (round 5).
+static int complete_ways(uint32_t) { return kCompleteWays; }
 
 // nms.Keypoints (nms.py:17-57) of a decode: nms_kernel<W> in one launch, or with `bitmap`
-// (PP_STAGE_NMS_BITMAP, or PP_NMS_BITMAP=1 for every call) nms_kernel<W, 1>, the planes as
+// (PP_STAGE_NMS_BITMAP) nms_kernel<W, 1>, the planes as
 // bitmaps (nms_planes_kernel, one wave per (image, plane)), nms_kernel<W, 3> -- unless NMS
 // is off or the bitmap would not fit kNmsBitmapLds.  `wide`: 8-wave workgroups
 // (PP_STAGE_NMS_WIDE).  The bitmap holds the nominal grid (CifHr map / reduction) plus
@@ -3699,15 +3698,11 @@ constexpr int kNmsMargin = 16;
 constexpr size_t kNmsBitmapLds = 64 * 1024;
 
 static int launch_nms(const GrowArgs &g, int n_img, bool wide, bool bitmap, hipStream_t s) {
-    static const bool bitmap_env = [] {
-        const char *e = getenv("PP_NMS_BITMAP");
-        return e && e[0] == '1';
-    }();
     NmsBitmapGeo geo{};
     geo.cap_h = (int)((double)g.hh / g.cfg.occupancy_reduction) + kNmsMargin;
     geo.cap_w = (int)((double)g.ww / g.cfg.occupancy_reduction) + kNmsMargin;
     const size_t lds = geo.bytes(g.ann_cap);
-    if ((bitmap || bitmap_env) && g.cfg.apply_nms && lds <= kNmsBitmapLds) {
+    if (bitmap && g.cfg.apply_nms && lds <= kNmsBitmapLds) {
         if (wide)
             hipLaunchKernelGGL((nms_kernel<kNmsWaves, 1>), dim3(n_img), dim3(64 * kNmsWaves), 0, s, g);
         else
@@ -3955,8 +3950,8 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
         // PP_STAGE_SEED_LOOP_ONLY / PP_STAGE_AFTER_SEED_LOOP split stage 8 in two calls
         const bool run_rest = !(stages & PP_STAGE_SEED_LOOP_ONLY);
         if (!(stages & PP_STAGE_AFTER_SEED_LOOP)) {
-            // g.xext is zero: the workspace's zero region, left zero by the NMS kernel that
-            // ends every decode on it
+            // g.xext is zero: the workspace's zero region, which every external-helper seed
+            // loop leaves zero (ext_exit)
             const size_t dyn = g.n_ext > 0
                                    ? kColLdsExt * sizeof(float) + (size_t)kExtCache * kKP * sizeof(float4)
                                    : kColLds * sizeof(float);
@@ -3978,14 +3973,8 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
             if (rc) return rc;
         }
         // PP_STAGE_COMPLETE_ONLY / PP_STAGE_NMS_ONLY split the rest once more
-        // PP_DIAG_SKIP (diagnostics only, wrong results): bit 1 skips force-complete and its
-        // lazy sets, bit 2 NMS -- how much of a pipelined step each stage costs
-        static const int diag_skip = [] {
-            const char *e = getenv("PP_DIAG_SKIP");
-            return e ? atoi(e) : 0;
-        }();
-        const bool run_complete = run_rest && !(stages & PP_STAGE_NMS_ONLY) && !(diag_skip & 1);
-        const bool run_nms = run_rest && !(stages & PP_STAGE_COMPLETE_ONLY) && !(diag_skip & 2);
+        const bool run_complete = run_rest && !(stages & PP_STAGE_NMS_ONLY);
+        const bool run_nms = run_rest && !(stages & PP_STAGE_COMPLETE_ONLY);
         if (run_complete && cfg->force_complete && !(stages & PP_STAGE_COMPLETE_SETS_EARLY)) {
             // complete_annotations' CafScored(score_th=0.0001) only where phase 1 left work
             rc = launch_caf_bucketed(h, hr, n_img, K, C, skeleton, cfg, cfg->complete_caf_threshold,

@@ -1954,24 +1954,32 @@ template int cifhr_heads_launch<false>(const Heads &, int32_t, int32_t, const pp
 // field's tiles over several workgroups (each builds its own copy of the field's list: a
 // re-read of its confidences, no extra round trip, no shared writes)
 static int sparse_split(int64_t nf) {
-    static const int64_t slots = [] {  // PP_SPLIT_SLOTS: diagnostics (tools/cfg2_split.py)
+#ifdef PP_STAMPS  // the diagnostic build only: PP_SPLIT_SLOTS (tools/cfg2_split.py)
+    static const int64_t slots = [] {
         const char *e = getenv("PP_SPLIT_SLOTS");
         return e && atoi(e) > 0 ? (int64_t)atoi(e) : (int64_t)kSplitSlots;
     }();
+#else
+    constexpr int64_t slots = kSplitSlots;
+#endif
     return (int)std::max<int64_t>(1, std::min<int64_t>(kMaxSplit, slots / std::max<int64_t>(1, nf)));
 }
 
 // candidates per split workgroup of a prebuilt field list: all of a field's split
 // workgroups read the same bins, so a short list on many workgroups only queues them on
 // the same L2 lines (cfg2 planted, 125 candidates per field: fold kernel 35.1 us on 60
-// workgroups per field, 22.1 us on 3); PP_SPLIT_LIST overrides (diagnostics)
+// workgroups per field, 22.1 us on 3); PP_SPLIT_LIST overrides it in the diagnostic build
 constexpr int kSplitList = 48;
 static int split_list_len() {
+#ifdef PP_STAMPS
     static const int v = [] {
         const char *e = getenv("PP_SPLIT_LIST");
         return e && atoi(e) > 0 ? atoi(e) : kSplitList;
     }();
     return v;
+#else
+    return kSplitList;
+#endif
 }
 
 size_t cifhr_sparse_workspace_size(const Heads &h, int n_img, int K) {

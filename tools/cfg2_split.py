@@ -1,5 +1,7 @@
 """Diagnostic: cfg2 (one 80x80 image: CifHr + seeds, the decoder's stages 1 | 2) device time
-for several split-field settings (PP_SPLIT_SLOTS: workgroups per field = slots / 17).
+for several split-field settings (PP_SPLIT_SLOTS: workgroups per field = slots / 17).  The
+product library ignores PP_SPLIT_SLOTS; it is read by the diagnostic build only
+(`python -m openpifpaf_amd.build --stamps`, loaded with PP_LIB_VARIANT=stamps).
 
     python tools/cfg2_split.py [planted|uniform] [slots ...]
 """
@@ -28,5 +30,5 @@ for _ in range(200): eng.launch(c, f, sk, cfg, stages=STAGE_CIFHR | STAGE_SEEDS)
 e1.record(); torch.cuda.synchronize()
 print('slots %d: %%.2f us per call' %% (e0.elapsed_time(e1) / 200 * 1e3))
 ''' % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))), kind, slots)
-    env = dict(os.environ, PP_SPLIT_SLOTS=str(slots))
+    env = dict(os.environ, PP_SPLIT_SLOTS=str(slots), PP_LIB_VARIANT='stamps')
     subprocess.run([sys.executable, '-c', code], env=env, check=True, timeout=120)
