@@ -125,3 +125,37 @@ def test_nms_bitmap_matches_box_lists(kind):
     if kind == 'far':
         r = np.frombuffer(recs[0][0], dtype=packed_dtype(17, len(skel), PACK_ALL))
         assert (r['data'][:, :, 0] > 400).any()  # joints beyond the nominal 160-px map
+
+
+@pytest.mark.gpu
+def test_seed_loop_only_twice_then_decode():
+    """The workspace contract after a split stage 8: two PP_STAGE_SEED_LOOP_ONLY
+    calls on one workspace with external helper workgroups (8 images: n_ext 3), with no
+    force-complete or NMS call between or after them, then a whole decode of another batch
+    on the same workspace: its records equal a fresh engine's byte for byte, so the
+    external-helper hand-off words the seed loops left (SeedExt) were zero again.  Nothing
+    is skipped in the checked decode."""
+    import torch
+    from openpifpaf_amd.engine import (STAGE_CAF, STAGE_CIFHR, STAGE_GROW, STAGE_SEEDS,
+                                       STAGE_SEED_LOOP_ONLY, DecodeEngine)
+    skel = constants.COCO_PERSON_SKELETON
+    cfg = make_config(**EVAL_CONFIG)
+    fields = []
+    for i, kind in enumerate(('planted', 'uniform', 'planted')):
+        kw = {'n_caf': len(skel)} if kind == 'uniform' else {'skeleton': skel, 'n_people': 8}
+        cif, caf = synthetic.batch(kind, 8, 80, 80, first_seed=300 + 10 * i, **kw)
+        fields.append((torch.from_numpy(cif).cuda(), torch.from_numpy(caf).cuda()))
+    eng = DecodeEngine()
+    for cif, caf in fields[:2]:
+        eng.launch(cif, caf, skel, cfg, cap=1024, stages=STAGE_CIFHR | STAGE_SEEDS | STAGE_CAF)
+        eng.launch(cif, caf, skel, cfg, cap=1024, stages=STAGE_GROW | STAGE_SEED_LOOP_ONLY)
+    torch.cuda.synchronize()
+    got, got_off, _ = eng.decode(*fields[2], skel, cfg, cap=1024, compact=PACK_ALL)
+    want, want_off, _ = DecodeEngine().decode(*fields[2], skel, cfg, cap=1024, compact=PACK_ALL)
+    np.testing.assert_array_equal(got_off, want_off)
+    assert got.tobytes() == want.tobytes()
+    # and the first batch again, whole, on the same workspace
+    got1, off1, _ = eng.decode(*fields[0], skel, cfg, cap=1024, compact=PACK_ALL)
+    want1, woff1, _ = DecodeEngine().decode(*fields[0], skel, cfg, cap=1024, compact=PACK_ALL)
+    np.testing.assert_array_equal(off1, woff1)
+    assert got1.tobytes() == want1.tobytes()
