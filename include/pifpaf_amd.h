@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PP_ABI_VERSION 3
+#define PP_ABI_VERSION 4
 
 /* capacities of one annotation record (COCO person: 17 keypoints, 19 or 44 edges) */
 #define PP_MAX_KP 24
@@ -73,6 +73,11 @@ typedef struct pp_config {
     int32_t occupancy_min_scale;
     uint32_t seed_skip_mask;      /* bit f set: field f emits no seeds, FieldConfig.seed_mask[f]
                                      falsy (cif_seeds.py:28-29); 0 = every field seeds       */
+    int32_t exp_mode;             /* np.exp of the CAF scores (cifcaf.py:139): 0 = NumPy's
+                                     float32 SIMD exp (the FMA3 / AVX512F routine NumPy runs on
+                                     any x86-64 since 2013; bit-exact over every float32 in
+                                     [-104, 0], tests/test_np_exp.py), 1 = correctly rounded
+                                     (NumPy's scalar loop on CPUs without FMA3)              */
     const float *confidence_scales; /* HOST array (C): CifCaf(confidence_scales=...)
                                      (cifcaf.py:39,52), each CAF's weight on the frontier
                                      priorities of _grow (cifcaf.py:259-260, 282-284), f32
@@ -600,11 +605,27 @@ int pp_center_filter(const float *d_field, int64_t rows, int64_t n, int64_t pitc
 /*
  * CifCaf._grow_connection + _target_with_blend / _target_with_maxscore
  * (cifcaf.py:124-192; the north star's "grow_connection_blend") for one query point on a
- * (9, n) column set with row pitch `pitch`.  method 0 blend, 1 max.  d_out = 4 floats
- * (x, y, scale, score); all zero when no column lies in the 2*xy_scale box.
+ * (9, n) column set with row pitch `pitch`.  method bit 0: 0 blend, 1 max; bit 1: the
+ * scores' np.exp correctly rounded (pp_config.exp_mode 1) instead of NumPy's SIMD exp.
+ * d_out = 4 floats (x, y, scale, score); all zero when no column lies in the 2*xy_scale box.
  */
 int pp_grow_connection(const float *d_cols, int64_t n, int64_t pitch, float x, float y,
                        float xy_scale, int32_t method, float *d_out, void *stream);
+
+/*
+ * np.exp of float32 values as the decoder's CAF scores take it (cifcaf.py:139, the
+ * score's exp): d_y[i] = exp(d_x[i]) with pp_config.exp_mode's rounding (0 NumPy's SIMD
+ * float32 routine, 1 correctly rounded).  The device form of the decoder's own function
+ * (caf_exp, pp_common.hpp), for checking it against np.exp.
+ */
+int pp_np_exp(const float *d_x, float *d_y, int64_t n, int32_t exp_mode, void *stream);
+
+/*
+ * d_y[i] = d_x[i] ** 2 as NumPy computes it for a float32 SCALAR (cifcaf.py:139 `sigma**2`):
+ * the C library's powf(x, 2.0f), glibc 2.35's FMA build, which differs from x * x in about
+ * 0.07 % of inputs.  The device form of the decoder's own function (np_pow2_f32).
+ */
+int pp_np_square(const float *d_x, float *d_y, int64_t n, void *stream);
 
 /* ---------------------------------------------------------------------------------
  * Host twins of the functional.pyx primitives above (SURVEY.md §8(b) `_cpu` variants):
@@ -629,6 +650,9 @@ int pp_scalar_square_add_constant_cpu(float *field, int64_t h, int64_t w, int64_
 int pp_cumulative_average_cpu(float *cuma, float *cumw, int64_t h, int64_t w, int64_t pitch,
                               const float *x, const float *y, const float *width,
                               const float *v, const float *w_, int64_t n);
+/* pp_np_exp / pp_np_square on host pointers */
+int pp_np_exp_cpu(const float *x, float *y, int64_t n, int32_t exp_mode);
+int pp_np_square_cpu(const float *x, float *y, int64_t n);
 /* out_steps (optional, 1 int64) = iterations run */
 int pp_weiszfeld_nd_cpu(const float *x, int64_t n, int64_t d, int64_t x_pitch, float *y,
                         const float *weights, float epsilon, int64_t max_steps, float *denom,

@@ -3,7 +3,7 @@ import ctypes
 
 import numpy as np
 
-PP_ABI_VERSION = 3
+PP_ABI_VERSION = 4
 PP_MAX_KP = 24
 PP_MAX_EDGES = 64
 PP_MAX_FRONTIER = 4 * PP_MAX_EDGES
@@ -92,8 +92,12 @@ class PPConfig(ctypes.Structure):
         ('occupancy_reduction', ctypes.c_int32),
         ('occupancy_min_scale', ctypes.c_int32),
         ('seed_skip_mask', ctypes.c_uint32),
+        ('exp_mode', ctypes.c_int32),
         ('confidence_scales', ctypes.POINTER(ctypes.c_float)),
     ]
+
+
+EXP_MODES = {'numpy_simd': 0, 'correct': 1}
 
 
 def make_config(*, cif_threshold=0.1, seed_threshold=0.2, seed_score_scale=1.0,
@@ -102,20 +106,26 @@ def make_config(*, cif_threshold=0.1, seed_threshold=0.2, seed_score_scale=1.0,
                 nms_instance_threshold=0.0, nms_suppression=0.0, stride=8, cif_neighbors=16,
                 force_complete=True, greedy=False, connection_method='blend', apply_nms=True,
                 occupancy_reduction=2, occupancy_min_scale=4, seed_mask=None,
-                confidence_scales=None):
+                confidence_scales=None, exp_mode='numpy_simd'):
     """Defaults = eval_coco defaults (decoder/factory.py:17-22, eval_coco.py:215).
     confidence_scales: CifCaf's per-CAF frontier weights (cifcaf.py:259-260, 282-284) as
     float32, the type NumPy multiplies a float32 score by a Python float in; the array is
-    kept alive on the returned struct."""
+    kept alive on the returned struct.  exp_mode: how np.exp of the CAF scores rounds
+    (cifcaf.py:139): 'numpy_simd' (default) is NumPy's float32 SIMD exp, the routine the
+    reference runs on any x86-64 with FMA3; 'correct' rounds correctly (NumPy's scalar
+    loop)."""
     if connection_method not in ('blend', 'max'):
         raise Exception('connection method not known')
+    if exp_mode not in EXP_MODES:
+        raise ValueError('exp_mode must be one of {}'.format(sorted(EXP_MODES)))
     cfg = PPConfig(
         cif_threshold, seed_threshold, seed_score_scale, caf_threshold,
         complete_caf_threshold, cif_floor, keypoint_threshold, nms_keypoint_threshold,
         nms_instance_threshold, nms_suppression, int(stride), int(cif_neighbors),
         int(bool(force_complete)), int(bool(greedy)),
         0 if connection_method == 'blend' else 1, int(bool(apply_nms)),
-        int(occupancy_reduction), int(occupancy_min_scale), seed_skip_mask(seed_mask))
+        int(occupancy_reduction), int(occupancy_min_scale), seed_skip_mask(seed_mask),
+        EXP_MODES[exp_mode])
     if confidence_scales is not None:
         cs = np.ascontiguousarray([float(v) for v in confidence_scales], dtype=np.float32)
         cfg._confidence_scales = cs  # the struct points into it

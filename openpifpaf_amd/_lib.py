@@ -78,6 +78,8 @@ _SIGNATURES = {
     'pp_scalar_lookup': ([_vp, _i64, _i64, _i64, _i32, _vp, _vp, _i64, _f, _f, _vp, _vp],
                          ctypes.c_int),
     'pp_grow_connection': ([_vp, _i64, _i64, _f, _f, _f, _i32, _vp, _vp], ctypes.c_int),
+    'pp_np_exp': ([_vp, _vp, _i64, _i32, _vp], ctypes.c_int),
+    'pp_np_square': ([_vp, _vp, _i64, _vp], ctypes.c_int),
     'pp_nms_workspace_size': ([_i32, _i32], _sz),
     'pp_fields_dim': ([_i64, _i32], _i64),
     'pp_default_det_nms': ([_vp], None),
@@ -120,6 +122,8 @@ _SIGNATURES = {
                              ctypes.c_int),
     'pp_center_filter_cpu': ([_vp, _i64, _i64, _i64, _i32, _f, _f, _f, _vp, _i64, _vp],
                              ctypes.c_int),
+    'pp_np_exp_cpu': ([_vp, _vp, _i64, _i32], ctypes.c_int),
+    'pp_np_square_cpu': ([_vp, _vp, _i64], ctypes.c_int),
     # host twins of the front stages (csrc/stages_cpu.hip)
     'pp_cifhr_cpu': ([_vp, _i32, _i32, _i32, _i32, _vp, _vp], ctypes.c_int),
     'pp_seeds_cpu': ([_vp, _vp, _i32, _i32, _i32, _i32, _vp, _vp, _i32, _vp], ctypes.c_int),

@@ -57,6 +57,13 @@ __global__ __launch_bounds__(1024) void center_filter_kernel(const float *__rest
     if (threadIdx.x == 0 && count) *count = (int)(mode == 3 ? n : running);
 }
 
+// the decoder's CAF-score exp (caf_exp; mode 2: its sigma**2, np_pow2_f32) over an array
+__global__ void np_exp_kernel(const float *__restrict__ x, float *__restrict__ y, int64_t n,
+                              int mode) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] = mode == 2 ? np_pow2_f32(x[i]) : caf_exp(x[i], mode);
+}
+
 // functional.pyx:172-211, sequential sums in the reference's order (one lane)
 __global__ void weiszfeld_kernel(const float *__restrict__ x, int64_t n, int64_t d, int64_t xp,
                                  float *y, const float *__restrict__ wts, float eps,
@@ -141,6 +148,25 @@ int pp_center_filter(const float *d_field, int64_t rows, int64_t n, int64_t pitc
     hipLaunchKernelGGL(center_filter_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, d_field,
                        (int)rows, n, pitch, mode, x, y, sigma, d_out, out_pitch, d_count);
     return check_launch("pp_center_filter");
+}
+
+int pp_np_exp(const float *d_x, float *d_y, int64_t n, int32_t exp_mode, void *stream) {
+    if (!d_x || !d_y) return fail(PP_EINVAL, "pp_np_exp: NULL argument");
+    if (n < 0 || n > ((int64_t)1 << 38)) return fail(PP_ESHAPE, "pp_np_exp: bad length");
+    if (exp_mode != 0 && exp_mode != 1) return fail(PP_EINVAL, "pp_np_exp: bad exp_mode");
+    if (n == 0) return PP_OK;
+    hipLaunchKernelGGL(np_exp_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, d_x, d_y, n, exp_mode);
+    return check_launch("pp_np_exp");
+}
+
+int pp_np_square(const float *d_x, float *d_y, int64_t n, void *stream) {
+    if (!d_x || !d_y) return fail(PP_EINVAL, "pp_np_square: NULL argument");
+    if (n < 0 || n > ((int64_t)1 << 38)) return fail(PP_ESHAPE, "pp_np_square: bad length");
+    if (n == 0) return PP_OK;
+    hipLaunchKernelGGL(np_exp_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, d_x, d_y, n, 2);
+    return check_launch("pp_np_square");
 }
 
 int pp_weiszfeld_nd(const float *d_x, int64_t n, int64_t d, int64_t x_pitch, float *d_y,

@@ -195,6 +195,21 @@ int pp_occupancy_set_cpu(uint8_t *occ, int32_t n_planes, int64_t h, int64_t w, i
     return PP_OK;
 }
 
+int pp_np_exp_cpu(const float *x, float *y, int64_t n, int32_t exp_mode) {
+    if (!x || !y) return pp::fail(PP_EINVAL, "pp_np_exp_cpu: NULL argument");
+    if (n < 0) return pp::fail(PP_ESHAPE, "pp_np_exp_cpu: bad length");
+    if (exp_mode != 0 && exp_mode != 1) return pp::fail(PP_EINVAL, "pp_np_exp_cpu: bad exp_mode");
+    for (int64_t i = 0; i < n; i++) y[i] = pp::caf_exp(x[i], exp_mode);
+    return PP_OK;
+}
+
+int pp_np_square_cpu(const float *x, float *y, int64_t n) {
+    if (!x || !y) return pp::fail(PP_EINVAL, "pp_np_square_cpu: NULL argument");
+    if (n < 0) return pp::fail(PP_ESHAPE, "pp_np_square_cpu: bad length");
+    for (int64_t i = 0; i < n; i++) y[i] = pp::np_pow2_f32(x[i]);
+    return PP_OK;
+}
+
 // functional.pyx:214-228, 289-359 (mode as pp_center_filter); *count = kept columns
 int pp_center_filter_cpu(const float *field, int64_t rows, int64_t n, int64_t pitch, int32_t mode,
                          float x, float y, float sigma, void *out, int64_t out_pitch,

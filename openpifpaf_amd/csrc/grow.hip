@@ -395,10 +395,12 @@ __device__ __forceinline__ Best2 top2_wave(const Top2 &t) {
 
 struct ColQuery {
     float x, y, lo_x, hi_x, lo_y, hi_y, sigma2;
+    int exp_mode;  // pp_config.exp_mode (caf_exp)
 };
 
-__device__ __forceinline__ ColQuery make_query(float x, float y, float xy_scale) {
+__device__ __forceinline__ ColQuery make_query(float x, float y, float xy_scale, int exp_mode) {
     ColQuery q;
+    q.exp_mode = exp_mode;
     const float sbox = 2.0f * xy_scale;  // caf_center_s(..., sigma=2.0 * xy_scale)
     q.x = x;
     q.y = y;
@@ -407,7 +409,7 @@ __device__ __forceinline__ ColQuery make_query(float x, float y, float xy_scale)
     q.lo_y = y - sbox;
     q.hi_y = y + sbox;
     const float sigma = 0.5f * xy_scale;
-    q.sigma2 = sigma * sigma;
+    q.sigma2 = np_pow2_f32(sigma);  // `sigma**2` of a NumPy float32 scalar: libm powf
     return q;
 }
 
@@ -421,7 +423,7 @@ __device__ __forceinline__ void consider_vals(const ColQuery &q, float c0, float
     const float dx = q.x - c1, dy = q.y - c2;
     const float dd = sqrtf(dx * dx + dy * dy);  // np.linalg.norm(axis=0)
     const float qq = (-0.5f * (dd * dd)) / q.sigma2;
-    const float score = (float)exp((double)qq) * c0;  // np.exp, correctly rounded
+    const float score = caf_exp(qq, q.exp_mode) * c0;  // np.exp
     top2_insert(t, cand_key<MAXM>(score, o), tx, ty, tc);
 }
 
@@ -472,7 +474,7 @@ __device__ __forceinline__ void consider_raw(const GrowArgs &g, const RawSet &r,
     const float dx = q.x - c1, dy = q.y - c2;
     const float dd = sqrtf(dx * dx + dy * dy);
     const float qq = (-0.5f * (dd * dd)) / q.sigma2;
-    const float score = (float)exp((double)qq) * c0;
+    const float score = caf_exp(qq, q.exp_mode) * c0;
     top2_insert(t, cand_key<MAXM>(score, key), tx, ty, tc);
 }
 
@@ -527,9 +529,9 @@ __device__ __forceinline__ Top2 top2_empty() {
 // column set in the reference's order, n columns (the functional API entry point)
 template <bool MAXM>
 __device__ void grow_connection_flat(const float *__restrict__ cf, int n, int64_t hw, float x,
-                                     float y, float xy_scale, float out[4]) {
+                                     float y, float xy_scale, int exp_mode, float out[4]) {
     const int lane = threadIdx.x & 63;
-    const ColQuery q = make_query(x, y, xy_scale);
+    const ColQuery q = make_query(x, y, xy_scale, exp_mode);
     Top2 t = top2_empty();
     for (int i = lane; i < n; i += 64) consider<MAXM, false>(cf, hw, q, i, t);
     finish_connection<MAXM>(t, out);
@@ -558,7 +560,7 @@ __device__ __forceinline__ void grow_connection(const GrowArgs &g, const float *
     uint64_t gs_t = __builtin_amdgcn_s_memtime();
 #endif
     const int64_t hw = g.col_cap;
-    const ColQuery q = make_query(x, y, xy_scale);
+    const ColQuery q = make_query(x, y, xy_scale, g.cfg.exp_mode);
     Top2 t = top2_empty();
     int bx0, bx1, by0, by1;
     if (q.lo_x != q.lo_x || q.hi_x != q.hi_x || q.lo_y != q.lo_y || q.hi_y != q.hi_y) {
@@ -922,9 +924,9 @@ __device__ __forceinline__ SlotSets slot_sets(const GrowArgs &g, const ColStage 
 // as through the buckets; the merge is independent of visiting order: unique keys)
 template <bool MAXM>
 __device__ __forceinline__ void flat_query(const float v[kFlatPer][kColRows], int n, float x, float y,
-                                           float xy_scale, float out[4]) {
+                                           float xy_scale, int exp_mode, float out[4]) {
     const int lane = threadIdx.x & 63;
-    const ColQuery q = make_query(x, y, xy_scale);
+    const ColQuery q = make_query(x, y, xy_scale, exp_mode);
     Top2 t = top2_empty();
 #pragma unroll
     for (int p = 0; p < kFlatPer; p++)
@@ -982,13 +984,13 @@ __device__ __forceinline__ void eval_ahead(const GrowArgs &g, Frontier &F, int i
             const int d = sl[b], j = jj[b];
             const float jx = rl_f(ax, j), jy = rl_f(ay, j), jv = rl_f(av, j), js = rl_f(as, j);
             float nx[4];
-            flat_query<MAXM>(vf[b], nf[b], jx, jy, max0(js), nx);
+            flat_query<MAXM>(vf[b], nf[b], jx, jy, max0(js), g.cfg.exp_mode, nx);
             float res[4] = {0.0f, 0.0f, 0.0f, 0.0f};
             const float ks = sqrtf(nx[3] * jv);
             if (!(ks < g.cfg.keypoint_threshold) && nx[3] != 0.0f) {
                 // reverse query from the new point (cifcaf.py:210-214)
                 float rv[4];
-                flat_query<MAXM>(vb[b], nb[b], nx[0], nx[1], max0(nx[2]), rv);
+                flat_query<MAXM>(vb[b], nb[b], nx[0], nx[1], max0(nx[2]), g.cfg.exp_mode, rv);
                 if (rv[2] != 0.0f && !(fabsf(jx - rv[0]) + fabsf(jy - rv[1]) > max0(js))) {
                     res[0] = nx[0];
                     res[1] = nx[1];
@@ -1075,7 +1077,7 @@ __device__ __forceinline__ void eval_ahead_raw(const GrowArgs &g, Frontier &F, i
             const int dir = __builtin_amdgcn_readfirstlane(rl_i(h ? F.sfwd[1] : F.sfwd[0], l)) ? 1 : 0;
             const int j = __builtin_amdgcn_readfirstlane(rl_i(h ? F.sj[1] : F.sj[0], l));
             jv_b[b] = rl_f(av, j);
-            q[b] = make_query(rl_f(ax, j), rl_f(ay, j), max0(rl_f(as, j)));
+            q[b] = make_query(rl_f(ax, j), rl_f(ay, j), max0(rl_f(as, j)), g.cfg.exp_mode);
             rs[b] = raw_set(g, img, caf, dir);
             int bx0, bx1, by0, by1;
             const ColQuery &qq = q[b];
@@ -1180,7 +1182,7 @@ __device__ __forceinline__ void eval_ahead_raw(const GrowArgs &g, Frontier &F, i
                 const float dx = qq.x - c1[b], dy = qq.y - c2[b];
                 const float dd = sqrtf(dx * dx + dy * dy);
                 const float qv = (-0.5f * (dd * dd)) / qq.sigma2;
-                const float score = (float)exp((double)qv) * c0;
+                const float score = caf_exp(qv, qq.exp_mode) * c0;
                 top2_insert(t[b], cand_key<MAXM>(score, key[b]), tx[b], ty[b], tc[b]);
             }
         }
@@ -4180,9 +4182,9 @@ namespace pp {
 template <bool MAXM>
 __global__ __launch_bounds__(64) void grow_connection_kernel(const float *cf, int n, int64_t pitch,
                                                              float x, float y, float xy_scale,
-                                                             float *out) {
+                                                             int exp_mode, float *out) {
     float r[4];
-    grow_connection_flat<MAXM>(cf, n, pitch, x, y, xy_scale, r);
+    grow_connection_flat<MAXM>(cf, n, pitch, x, y, xy_scale, exp_mode, r);
     if (threadIdx.x < 4) out[threadIdx.x] = r[threadIdx.x];
 }
 }  // namespace pp
@@ -4191,14 +4193,17 @@ extern "C" int pp_grow_connection(const float *d_cols, int64_t n, int64_t pitch,
                                   float xy_scale, int32_t method, float *d_out, void *stream) {
     if (!d_cols || !d_out) return fail(PP_EINVAL, "pp_grow_connection: NULL argument");
     if (n < 0 || pitch < n || n > INT32_MAX) return fail(PP_ESHAPE, "pp_grow_connection: bad shape");
-    if (method != 0 && method != 1) return fail(PP_EINVAL, "connection method not known");
+    // bit 0: connection method (0 blend, 1 max); bit 1: pp_config.exp_mode 1 (correctly
+    // rounded np.exp instead of NumPy's SIMD one)
+    if (method < 0 || method > 3) return fail(PP_EINVAL, "connection method not known");
     hipStream_t s = (hipStream_t)stream;
-    if (method == 1)
+    const int exp_mode = (method >> 1) & 1;
+    if (method & 1)
         hipLaunchKernelGGL(grow_connection_kernel<true>, dim3(1), dim3(64), 0, s, d_cols, (int)n,
-                           pitch, x, y, xy_scale, d_out);
+                           pitch, x, y, xy_scale, exp_mode, d_out);
     else
         hipLaunchKernelGGL(grow_connection_kernel<false>, dim3(1), dim3(64), 0, s, d_cols, (int)n,
-                           pitch, x, y, xy_scale, d_out);
+                           pitch, x, y, xy_scale, exp_mode, d_out);
     return check_launch("pp_grow_connection");
 }
 

@@ -49,6 +49,130 @@ __host__ __device__ __forceinline__ float approx_exp_ref(float x) {
     return x;
 }
 
+// np.exp of a float32 (cifcaf.py:139) as NumPy computes it on x86-64 with FMA3 or AVX512F:
+// NumPy 2.2's simd_exp_f32 (numpy/_core/src/umath/loops_exponent_log.dispatch.c.src, the
+// constants of npy_simd_data.h).  The quadrant q = rint(x * log2 e) by the 1.5 * 2^23 trick,
+// Cody-Waite reduction with two fused multiply-adds, a rational approximation (degree 5
+// over degree 2, Horner with fused multiply-adds), one IEEE division, times 2^q (exact, or
+// correctly rounded to a subnormal, as scalef / ldexp).  Bit-exact against np.exp over every
+// float32 in [-104, 0] (tests/test_np_exp.py, host and device); it differs from a correctly
+// rounded exp in about a third of its results (by one ulp).
+__host__ __device__ __forceinline__ float np_exp_f32(float x) {
+    if (x != x) return x;
+    if (x >= 88.72283935546875f) return __builtin_inff();
+    if (x <= -103.97208404541015625f) return 0.0f;
+    float q = x * 1.442695040888963407359924681001892137f;
+    q = q + 0x1.800000p+23f;
+    q = q - 0x1.800000p+23f;
+    float r = fmaf(q, -6.93145752e-1f, x);
+    r = fmaf(q, -1.42860677e-6f, r);
+    r = fmaf(q, 0.0f, r);
+    float num = fmaf(5.082762527590693718096e-04f, r, 6.757896990527504603057e-03f);
+    num = fmaf(num, r, 5.114512081637298353406e-02f);
+    num = fmaf(num, r, 2.473615434895520810817e-01f);
+    num = fmaf(num, r, 7.257664613233124478488e-01f);
+    num = fmaf(num, r, 9.999999999980870924916e-01f);
+    float den = fmaf(2.159509375685829852307e-02f, r, -2.742335390411667452936e-01f);
+    den = fmaf(den, r, 1.0f);
+    return ldexpf(num / den, (int)q);
+}
+
+// np.float32 ** 2 (cifcaf.py:139 `sigma**2`, sigma a NumPy float32 scalar): NumPy's scalar
+// power calls the C library's powf(x, 2.0f), here glibc 2.35's (sysdeps/ieee754/flt-32/
+// e_powf.c, the FMA3 build the x86-64 ifunc selects on any CPU with FMA), which is NOT
+// x * x: it rounds a double approximation of 2 log2|x| -> exp2, whose relative error is
+// below 2^-33.03 over every normal result, and so differs from the correctly rounded square
+// in about 0.07 % of inputs (tests/test_np_exp.py: bit-exact over every float32 x >= 0).
+// Fast path: when every value within 2^-32 of the exact square x * x (a double, exact)
+// rounds to the same float, that float is powf's result; otherwise the routine itself: a
+// 16-entry log2 table (1/c, log2 c) with a degree-5 polynomial in r = z/c - 1, then a
+// 32-entry exp2 table and a degree-3 polynomial, every multiply-add fused as the FMA build
+// has it.  The table and coefficient values are glibc's (__powf_log2_data, __exp2f_data).
+// bit casts usable on the host and on the device
+__host__ __device__ __forceinline__ uint32_t u32_of(float f) { return __builtin_bit_cast(uint32_t, f); }
+__host__ __device__ __forceinline__ float f32_of(uint32_t u) { return __builtin_bit_cast(float, u); }
+__host__ __device__ __forceinline__ uint64_t u64_of(double d) { return __builtin_bit_cast(uint64_t, d); }
+__host__ __device__ __forceinline__ double f64_of(uint64_t u) { return __builtin_bit_cast(double, u); }
+
+__host__ __device__ inline double glibc_powf2_double(uint32_t ix, double *ylogx_out) {
+    static constexpr double kInvc[16] = {
+        0x1.661ec79f8f3bep+0, 0x1.571ed4aaf883dp+0, 0x1.49539f0f010b0p+0, 0x1.3c995b0b80385p+0,
+        0x1.30d190c8864a5p+0, 0x1.25e227b0b8ea0p+0, 0x1.1bb4a4a1a343fp+0, 0x1.12358f08ae5bap+0,
+        0x1.0953f419900a7p+0, 0x1.0000000000000p+0, 0x1.e608cfd9a47acp-1, 0x1.ca4b31f026aa0p-1,
+        0x1.b2036576afce6p-1, 0x1.9c2d163a1aa2dp-1, 0x1.886e6037841edp-1, 0x1.767dcf5534862p-1};
+    static constexpr double kLogc[16] = {
+        -0x1.efec65b963019p-2, -0x1.b0b6832d4fca4p-2, -0x1.7418b0a1fb77bp-2, -0x1.39de91a6dcf7bp-2,
+        -0x1.01d9bf3f2b631p-2, -0x1.97c1d1b3b7af0p-3, -0x1.2f9e393af3c9fp-3, -0x1.960cbbf788d5cp-4,
+        -0x1.a6f9db6475fcep-5, 0.0, 0x1.338ca9f24f53dp-4, 0x1.476a9543891bap-3,
+        0x1.e840b4ac4e4d2p-3, 0x1.40645f0c6651cp-2, 0x1.88e9c2c1b9ff8p-2, 0x1.ce0a44eb17bccp-2};
+    static constexpr uint64_t kExp2[32] = {
+        0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
+        0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
+        0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
+        0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
+        0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
+        0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
+        0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
+        0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
+    // log2_inline: x = 2^k z, z in [0x3f330000, 2 * 0x3f330000), c near the subinterval's centre
+    const uint32_t tmp = ix - 0x3f330000u;
+    const int i = (int)((tmp >> 19) & 15u);
+    const uint32_t top = tmp & 0xff800000u;
+    const int k = (int32_t)top >> 23;
+    const double z = (double)f32_of(ix - top);
+    const double r = fma(z, kInvc[i], -1.0);
+    const double y0 = kLogc[i] + (double)k;
+    double y = fma(r, 0x1.27616c9496e0bp-2, -0x1.71969a075c67ap-2);
+    const double p = fma(r, 0x1.ec70a6ca7baddp-2, -0x1.7154748bef6c8p-1);
+    const double r2 = r * r;
+    double q = fma(r, 0x1.71547652ab82bp+0, y0);
+    const double r4 = r2 * r2;
+    q = fma(r2, p, q);
+    y = fma(y, r4, q);
+    const double ylogx = 2.0 * y;  // y * log2|x| with y = 2
+    *ylogx_out = ylogx;
+    // exp2_inline: ylogx = k/32 + r, 2^(k/32) from the table (exponent bits added)
+    double kd = ylogx + 0x1.8p+47;
+    const uint64_t ki = u64_of(kd);
+    kd -= 0x1.8p+47;
+    const double rr = ylogx - kd;
+    const double s = f64_of(kExp2[ki & 31u] + (ki << 47));
+    const double zz = fma(rr, 0x1.c6af84b912394p-5, 0x1.ebfce50fac4f3p-3);
+    const double rr2 = rr * rr;
+    double yy = fma(rr, 0x1.62e42ff0c52d6p-1, 1.0);
+    yy = fma(zz, rr2, yy);
+    return yy * s;
+}
+
+__host__ __device__ inline float np_pow2_f32(float x) {
+    const double xd = (double)x;
+    const double sq = xd * xd;  // exact (48 significant bits)
+    if (sq >= 0x1p-126 && sq <= 0x1p+127) {
+        const float lo = (float)(sq * (1.0 - 0x1p-32)), hi = (float)(sq * (1.0 + 0x1p-32));
+        if (lo == hi) return lo;
+    }
+    uint32_t ix = u32_of(x) & 0x7fffffffu;  // y = 2 is even: the sign drops out
+    if (ix == 0u || ix >= 0x7f800000u) return fabsf(x) * fabsf(x);  // 0, inf, NaN
+    if (ix < 0x800000u) {  // subnormal: normalised (x 2^23, exponent -23)
+        ix = u32_of(f32_of(ix) * 0x1p23f) & 0x7fffffffu;
+        ix -= 23u << 23;
+    }
+    double ylogx;
+    const double yd = glibc_powf2_double(ix, &ylogx);
+    if (((u64_of(ylogx) >> 47) & 0xffffu) >= 0x80bfu) {  // |ylogx| >= 126
+        if (ylogx > 0x1.fffffffd1d571p+6) return __builtin_inff();  // overflow
+        if (ylogx <= -150.0) return 0.0f;                            // underflow
+        if (ylogx < -149.0) return 0x1p-149f;                        // may underflow
+    }
+    return (float)yd;
+}
+
+// the CAF score's np.exp under pp_config.exp_mode: 0 NumPy's SIMD routine, 1 correctly
+// rounded (through f64; NumPy's scalar loop on CPUs without FMA3)
+__host__ __device__ __forceinline__ float caf_exp(float q, int mode) {
+    return mode ? (float)exp((double)q) : np_exp_f32(q);
+}
+
 // functional.pyx:231-244 scalar_values for one point (bounds inclusive of W'-1, truncation)
 __host__ __device__ __forceinline__ float hr_lookup(const float *field, int hh, int ww,
                                                     int64_t pitch, float x, float y, float dflt) {

@@ -12,6 +12,7 @@ import numpy as np
 import torch
 
 from . import _device
+from ._abi import EXP_MODES
 from ._lib import call
 
 _CTYPE_NAMES = {
@@ -255,15 +256,21 @@ __all__ = [
 ]
 
 
-def grow_connection_blend(caf_field, x, y, xy_scale, connection_method='blend'):
+def grow_connection_blend(caf_field, x, y, xy_scale, connection_method='blend',
+                          exp_mode='numpy_simd'):
     """CifCaf._grow_connection + _target_with_blend (cifcaf.py:124-192), named
     `grow_connection_blend` by the north star.  caf_field: (9, N) column set (a CafScored
     forward/backward entry).  Returns (x, y, scale, score) as float32 scalars, or
-    (0, 0, 0, 0) when no column lies within 2 * xy_scale of (x, y)."""
+    (0, 0, 0, 0) when no column lies within 2 * xy_scale of (x, y).  exp_mode: the
+    scores' np.exp ('numpy_simd', NumPy's float32 SIMD routine, or 'correct';
+    _abi.make_config)."""
     caf_field = _buf(caf_field, 2)
     method = {'blend': 0, 'max': 1}.get(connection_method)
     if method is None:
         raise Exception('connection method not known')
+    if exp_mode not in EXP_MODES:
+        raise ValueError('exp_mode must be one of {}'.format(sorted(EXP_MODES)))
+    method |= EXP_MODES[exp_mode] << 1
     f = _device.to_device(caf_field)
     if f.shape[0] != 9:
         raise AssertionError('caf_field must have 9 rows')

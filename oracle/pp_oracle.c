@@ -18,8 +18,14 @@
  *   - the Python decoder runs NumPy float32 arithmetic; under NumPy 2 (NEP 50) Python
  *     float scalars are cast to float32, so each expression below is one f32 op per
  *     NumPy op, in the reference's evaluation order.
- *   - np.exp(float32): correctly rounded here ((float)exp((double)x)); the reference's
- *     SIMD exp is within 2 ulp of it -> floats agree to ~1e-6 relative.
+ *   - np.exp(float32): NumPy's SIMD float32 exp (np_exp_f32 below, the AVX2 / AVX512F
+ *     routine NumPy dispatches to on any x86-64 with FMA3, which is what produced the
+ *     fixtures: tests/golden/meta.json records AVX512_SKX), bit-exact against np.exp over
+ *     every float32 in [-104, 0] (tests/test_np_exp.py); pp_config.exp_mode 1 selects a
+ *     correctly rounded exp instead (NumPy's scalar path on CPUs without FMA3).
+ *   - `sigma**2` of a float32 scalar is the C library's powf(sigma, 2) (np_scalar_square),
+ *     as NumPy's scalar power computes it.  With both, every decode fixture matches the
+ *     reference bit for bit.
  *   - Annotation.score(): float64, NumPy pairwise summation replicated (pw_sum below).
  */
 #include <math.h>
@@ -477,7 +483,57 @@ static int by_source_find(const dec_t *d, int j, int k) {
     return -1;
 }
 
-static inline float exp_cr(float q) { return (float)exp((double)q); }
+/* NumPy 2.2's float32 exp for x86 SIMD (numpy/_core/src/umath/
+ * loops_exponent_log.dispatch.c.src, simd_exp_f32 for FMA3 / AVX512F, with the constants of
+ * npy_simd_data.h): x * log2(e) rounded to an integer quadrant by the 1.5 * 2^23 trick,
+ * Cody-Waite reduction r = x + q * (-ln2 hi) + q * (-ln2 lo) (fused), the rational
+ * approximation p5..p0 / q2..q0 in Horner form with fused multiply-adds, one correctly
+ * rounded division, times 2^q (scalef / ldexp: exact, or correctly rounded to a subnormal).
+ * x >= 88.72283935546875 -> inf, x <= -103.97208404541015625 -> 0, NaN -> NaN. */
+static float np_exp_f32(float x) {
+    if (x != x) return x;
+    if (x >= 88.72283935546875f) return INFINITY;
+    if (x <= -103.97208404541015625f) return 0.0f;
+    float q = x * 1.442695040888963407359924681001892137f;
+    q = q + 0x1.800000p+23f;
+    q = q - 0x1.800000p+23f;
+    float r = fmaf(q, -6.93145752e-1f, x);
+    r = fmaf(q, -1.42860677e-6f, r);
+    r = fmaf(q, 0.0f, r);
+    float num = fmaf(5.082762527590693718096e-04f, r, 6.757896990527504603057e-03f);
+    num = fmaf(num, r, 5.114512081637298353406e-02f);
+    num = fmaf(num, r, 2.473615434895520810817e-01f);
+    num = fmaf(num, r, 7.257664613233124478488e-01f);
+    num = fmaf(num, r, 9.999999999980870924916e-01f);
+    float den = fmaf(2.159509375685829852307e-02f, r, -2.742335390411667452936e-01f);
+    den = fmaf(den, r, 1.0f);
+    return ldexpf(num / den, (int)q);
+}
+
+/* exported for tests/test_np_exp.py (exhaustive check against np.exp) */
+EXPORT void orc_np_exp(const float *x, float *y, long n) {
+    for (long i = 0; i < n; i++) y[i] = np_exp_f32(x[i]);
+}
+
+/* `sigma**2` of a NumPy float32 scalar (cifcaf.py:139): NumPy's scalar power calls the C
+ * library's powf (numpy/_core/src/umath/scalarmath.c.src, npy_powf), glibc 2.35's here,
+ * which is not always x * x.  Called through a volatile pointer: the compiler would
+ * otherwise fold powf(x, 2) into x * x. */
+static float np_scalar_square(float x) {
+    float (*volatile powf_p)(float, float) = powf;
+    return powf_p(x, 2.0f);
+}
+
+/* exported for tests/test_np_exp.py */
+EXPORT void orc_np_square(const float *x, float *y, long n) {
+    float (*volatile powf_p)(float, float) = powf;
+    for (long i = 0; i < n; i++) y[i] = powf_p(x[i], 2.0f);
+}
+
+/* np.exp of the decoder's scores (cifcaf.py:139) under pp_config.exp_mode */
+static inline float exp_cr(float q, int mode) {
+    return mode ? (float)exp((double)q) : np_exp_f32(q);
+}
 
 /* cifcaf.py:124-192: _grow_connection + _target_with_blend / _target_with_maxscore.
  * caf_field = (9, n) column set with row stride hw.  Returns x, y, s, score. */
@@ -487,7 +543,7 @@ static void grow_connection(const dec_t *d, float x, float y, float xy_scale, co
     float sigma_box = 2.0f * xy_scale;
     float lo_x = x - sigma_box, hi_x = x + sigma_box, lo_y = y - sigma_box, hi_y = y + sigma_box;
     float sigma = 0.5f * xy_scale;
-    float sigma2 = sigma * sigma;
+    float sigma2 = np_scalar_square(sigma);
     long m = 0, i1 = -1, i2 = -1;
     float s1 = 0.0f, s2 = 0.0f;
     int method_max = d->cfg->connection_method == 1;
@@ -496,7 +552,7 @@ static void grow_connection(const dec_t *d, float x, float y, float xy_scale, co
         if (c1 < lo_x || c1 > hi_x || c2 < lo_y || c2 > hi_y) continue; /* caf_center_s */
         float dx = x - c1, dy = y - c2;
         float dd = sqrtf(dx * dx + dy * dy);
-        float score = exp_cr((-0.5f * (dd * dd)) / sigma2) * cf[i];
+        float score = exp_cr((-0.5f * (dd * dd)) / sigma2, d->cfg->exp_mode) * cf[i];
         m++;
         if (method_max) {
             if (i1 < 0 || score > s1) { /* np.argmax: first maximum */

@@ -77,10 +77,10 @@ def test_struct_layout_matches_header(tmp_path):
 #include <stddef.h>
 #include "pifpaf_amd.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(pp_ann), offsetof(pp_ann, score),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(pp_ann), offsetof(pp_ann, score),
          offsetof(pp_ann, decoding_pairs), offsetof(pp_ann, decoding_xyv),
          offsetof(pp_ann, frontier_pairs), sizeof(pp_seed), sizeof(pp_config),
-         offsetof(pp_ann, n_frontier));
+         offsetof(pp_ann, n_frontier), offsetof(pp_config, exp_mode));
   return 0;
 }
 ''')
@@ -91,7 +91,7 @@ int main(void) {
     assert vals == [d.itemsize, d.fields['score'][1], d.fields['decoding_pairs'][1],
                     d.fields['decoding_xyv'][1], d.fields['frontier_pairs'][1],
                     _abi.SEED_DTYPE.itemsize, ctypes.sizeof(_abi.PPConfig),
-                    d.fields['n_frontier'][1]]
+                    d.fields['n_frontier'][1], _abi.PPConfig.exp_mode.offset]
 
 
 def test_no_oracle_in_product():

@@ -1,8 +1,8 @@
 """Pin the oracle (oracle/pp_oracle.c) against the reference's own outputs.
 
 The golden fixtures were produced by running the reference decoder
-(tests/golden/gen_golden.py).  Bit-exact for CifHr, seeds, CafScored and every
-functional primitive; tolerance (golden_util: XY_ULPS, ATOL, SCORE_ATOL) for the grow-stage floats.
+(tests/golden/gen_golden.py).  Bit-exact for CifHr, seeds, CafScored, every functional
+primitive and (golden_util's tolerances are zero) the decoded annotations.
 """
 import os
 
