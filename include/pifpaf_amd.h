@@ -703,6 +703,22 @@ int pp_nms_keypoints_scored_cpu(pp_ann *anns, const int32_t *counts, int32_t n_i
                                 const double *score_weights, const double *fixed_score,
                                 pp_ann *out, int32_t *out_counts, int32_t *out_index);
 
+/*
+ * Host twin of pp_decode_batch (CifCaf.__call__, cifcaf.py:67-122, for a batch of one-head
+ * fields; no initial annotations): CifHr, seeds and both CafScored sets through the front
+ * stages' twins, the seed loop with its occupancy, _grow, complete_annotations with
+ * _flood_fill (force_complete) and nms.Keypoints (apply_nms), on HOST pointers, one image
+ * per task on n_threads host threads (0: one per hardware thread).  Outputs as
+ * pp_decode_batch: per image ann_capacity records (counts[i] of them used, sorted by
+ * nms.Keypoints) and status flags (PP_ST_*; PP_ST_ANN_OVERFLOW: more annotations than
+ * ann_capacity, retry with a larger one).  Bit-exact with the device decode and with the
+ * reference's fixtures (tests/test_decode_cpu.py).
+ */
+int pp_decode_batch_cpu(const float *cif, const float *caf, int32_t n_img, int32_t K, int32_t C,
+                        int32_t H, int32_t W, const int32_t *skeleton, const pp_config *cfg,
+                        pp_ann *anns, int32_t ann_capacity, int32_t *counts, int32_t *status,
+                        int32_t n_threads);
+
 #ifdef __cplusplus
 }
 #endif

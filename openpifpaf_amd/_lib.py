@@ -132,6 +132,9 @@ _SIGNATURES = {
     'pp_nms_keypoints_cpu': ([_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp], ctypes.c_int),
     'pp_nms_keypoints_scored_cpu': ([_vp, _vp, _i32, _i32, _i32, _vp, _f64, _vp, _vp, _vp, _vp,
                                      _vp, _vp], ctypes.c_int),
+    # host twin of the whole decode (csrc/decode_cpu.hip)
+    'pp_decode_batch_cpu': ([_vp, _vp, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _i32, _vp,
+                             _vp, _i32], ctypes.c_int),
 }
 
 EXPORTED = tuple(_SIGNATURES)

@@ -20,6 +20,9 @@ constexpr int kWave = 64;
 // host-side error plumbing (thread-local message, pp_status codes)
 // -------------------------------------------------------------------------------------
 void set_error(const std::string &msg);
+// Annotation.score() of a host record (stages_cpu.hip): zero_j >= 0 suppress_score_index,
+// w the record's own score_weights (NULL: the default weights)
+double ann_score_cpu(const pp_ann &a, int K, int zero_j = -1, const double *w = nullptr);
 int fail(int status, const std::string &msg);
 int check_launch(const char *what);
 

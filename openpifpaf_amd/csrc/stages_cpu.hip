@@ -58,10 +58,13 @@ double pw_sum_cpu(const double *a, int n) {
     return res;
 }
 
+}  // namespace
+
+namespace pp {
 // Annotation.score() (annotation.py:60-71) with the default weights: 3 / (3 min(K, 3) +
 // K - min(K, 3)) for the three largest v, 1 / (...) for the rest, np.sort(v)[::-1] order
 // (zero_j >= 0: suppress_score_index, v[zero_j] reads as 0; w: the record's own score_weights)
-double ann_score_cpu(const pp_ann &a, int K, int zero_j = -1, const double *w = nullptr) {
+double ann_score_cpu(const pp_ann &a, int K, int zero_j, const double *w) {
     float v[PP_MAX_KP];
     for (int j = 0; j < K; j++) v[j] = j == zero_j ? 0.0f : a.data[j][2];
     std::stable_sort(v, v + K, [](float p, float q) { return p > q; });
@@ -70,6 +73,10 @@ double ann_score_cpu(const pp_ann &a, int K, int zero_j = -1, const double *w = 
     for (int r = 0; r < K; r++) prod[r] = (w ? w[r] : (r < 3 ? 3.0 : 1.0) / ws) * (double)v[r];
     return pw_sum_cpu(prod, K);
 }
+}  // namespace pp
+
+namespace {
+using pp::ann_score_cpu;
 
 // Occupancy of nms.Keypoints (nms.py:27-31): (K, int(max y + 1) / r, int(max x + 1) / r) u8
 struct NmsOcc {
@@ -142,8 +149,10 @@ static int nms_keypoints_host(pp_ann *anns, const int32_t *counts, int32_t n_img
             occ.msr = (float)((double)cfg->occupancy_min_scale / cfg->occupancy_reduction);
             float mx = 0.0f, my = 0.0f;
             bool first = true;
+            std::vector<char> kept(n, 0);
+            for (int i : keep) kept[i] = 1;
             for (int i = 0; i < n; i++) {  // max over the kept annotations in input order
-                if (std::find(keep.begin(), keep.end(), i) == keep.end()) continue;
+                if (!kept[i]) continue;
                 float ax = a[i].data[0][0], ay = a[i].data[0][1];
                 for (int j = 1; j < K; j++) {
                     ax = a[i].data[j][0] > ax ? a[i].data[j][0] : ax;

@@ -2,7 +2,9 @@
 pp_caf_scored_cpu and pp_nms_keypoints_cpu (csrc/stages_cpu.hip) -- CifHr.fill
 (cif_hr.py:23-81), CifSeeds.fill + get (cif_seeds.py:23-64) and CafScored.fill
 (caf_scored.py:32-98) for one CIF and one CAF head, and nms.Keypoints.annotations
-(nms.py:17-57), on the calling thread.
+(nms.py:17-57), on the calling thread -- and the whole decode, pp_decode_batch_cpu
+(csrc/decode_cpu.hip: CifCaf.__call__, cifcaf.py:67-122, with the seed loop, _grow,
+complete_annotations and the NMS), on host threads.
 
 An explicit host API, like openpifpaf_amd.functional_cpu: the decoder classes compute on the
 device and never fall back to it, and it raises when the library is missing.  `cfg` is a
@@ -13,8 +15,8 @@ import ctypes
 
 import numpy as np
 
-from ._abi import ANN_DTYPE, SEED_DTYPE
-from ._lib import call
+from ._abi import ANN_DTYPE, PP_ST_ANN_OVERFLOW, PP_ST_DEC_OVERFLOW, SEED_DTYPE
+from ._lib import PPError, call
 
 
 def _f32(a, ndim, what):
@@ -114,3 +116,39 @@ def nms_keypoints(data, joint_scales, cfg, *, score_spec=None, instance_threshol
     data[...] = recs['data'][:n, :k]
     m = int(out_counts[0])
     return index[:m].tolist(), out['score'][:m].copy()
+
+
+def decode_batch(cif, caf, skeleton, cfg, *, n_threads=0, cap=None):
+    """The whole CifCaf decode on host threads (pp_decode_batch_cpu, csrc/decode_cpu.hip):
+    cif (n, K, 5, H, W), caf (n, C, 9, H, W), 1-based skeleton (C, 2) -> (records, offsets)
+    as engine.DecodeEngine.decode returns them: ANN_DTYPE records of all images packed in
+    image order (each image's in nms.Keypoints order, `score` = Annotation.score()) and
+    per-image offsets (n + 1).  n_threads 0: one per hardware thread.  The annotation
+    capacity doubles until no image overflows, as the device decode's does."""
+    from .engine import default_ann_capacity  # pylint: disable=import-outside-toplevel
+    cif = _f32(cif, 5, 'cif')
+    caf = _f32(caf, 5, 'caf')
+    n, k, _, h, w = cif.shape
+    c = caf.shape[1]
+    if caf.shape[0] != n or caf.shape[3:] != cif.shape[3:]:
+        raise ValueError('cif and caf batch / spatial shapes differ')
+    sk = np.ascontiguousarray(skeleton, dtype=np.int32).reshape(-1, 2)
+    if len(sk) != c:
+        raise ValueError('skeleton has {} pairs for {} CAF fields'.format(len(sk), c))
+    cap = cap or default_ann_capacity(h, w)
+    while True:
+        anns = np.zeros((max(1, n), cap), ANN_DTYPE)
+        counts = np.zeros(max(1, n), np.int32)
+        status = np.zeros(max(1, n), np.int32)
+        call('pp_decode_batch_cpu', cif.ctypes.data, caf.ctypes.data, n, k, c, h, w,
+             sk.ctypes.data, ctypes.byref(cfg), anns.ctypes.data, cap, counts.ctypes.data,
+             status.ctypes.data, int(n_threads))
+        if not (status[:n] & PP_ST_ANN_OVERFLOW).any():
+            break
+        cap *= 2
+    if (status[:n] & PP_ST_DEC_OVERFLOW).any():
+        raise PPError('decoding/frontier order exceeded the record capacity')
+    offsets = np.concatenate([[0], np.cumsum(counts[:n])]).astype(np.int64)
+    recs = np.concatenate([anns[i, :counts[i]] for i in range(n)]) if n else \
+        np.zeros(0, ANN_DTYPE)
+    return recs, offsets
