@@ -21,7 +21,8 @@ over its launch time.  `roofline_decoder_cifhr` is the decoder's own block-spars
 stage inside `value` (its bytes: bench.cifhr_stage_bytes).
 `cpu_baseline` is the oracle (oracle/pp_oracle.c, C restatement of the reference decoder)
 on one host core, then on every CPU of the job's share, over bounded samples of the same
-workload (planted, and a uniform leg).
+workload (planted, and a uniform leg); `cpu_baseline.twin` is the build's own C++ twin of the
+decode (pp_decode_batch_cpu, csrc/decode_cpu.hip) on the same threads.
 """
 import argparse
 import json
@@ -818,6 +819,22 @@ def cpu_baseline(cif, caf, skeleton, cfg, budget_s, ucif=None, ucaf=None):
             'all_cores': round(allc / r['ratio'], 2),
             'source': 'profiles/cpu_ratio.json (reference vs oracle total time over {} planted '
                       '80x80 eval images, one thread, build container)'.format(r['images'])}
+    # the build's own C++ twin of the decode (pp_decode_batch_cpu, csrc/decode_cpu.hip:
+    # bit-exact with the device and the reference, SURVEY.md §8d's CPU comparator) on the
+    # same threads, whole chunks of the planted batch per call
+    from openpifpaf_amd import stages_cpu
+    chunk = max(4 * cores, 16)
+    nt, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s / 4:
+        i = (nt % len(cif))
+        c, a = cif[i:i + chunk], caf[i:i + chunk]
+        stages_cpu.decode_batch(c, a, skeleton, cfg, n_threads=cores)
+        nt += len(c)
+    dtt = time.perf_counter() - t0
+    out['twin'] = {'value': round(nt / dtt, 2), 'unit': 'images/s', 'cores': cores,
+                   'kind': 'twin',
+                   'sample': '{} planted decodes by pp_decode_batch_cpu on {} threads in '
+                             '{:.1f} s'.format(nt, cores, dtt)}
     if ucif is not None:
         nu, dtu = all_threads(ucif, ucaf, budget_s / 3)
         out['uniform'] = {'value': round(nu / dtu, 2), 'unit': 'images/s', 'cores': cores,

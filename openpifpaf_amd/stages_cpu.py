@@ -125,7 +125,6 @@ def decode_batch(cif, caf, skeleton, cfg, *, n_threads=0, cap=None):
     image order (each image's in nms.Keypoints order, `score` = Annotation.score()) and
     per-image offsets (n + 1).  n_threads 0: one per hardware thread.  The annotation
     capacity doubles until no image overflows, as the device decode's does."""
-    from .engine import default_ann_capacity  # pylint: disable=import-outside-toplevel
     cif = _f32(cif, 5, 'cif')
     caf = _f32(caf, 5, 'caf')
     n, k, _, h, w = cif.shape
@@ -135,7 +134,7 @@ def decode_batch(cif, caf, skeleton, cfg, *, n_threads=0, cap=None):
     sk = np.ascontiguousarray(skeleton, dtype=np.int32).reshape(-1, 2)
     if len(sk) != c:
         raise ValueError('skeleton has {} pairs for {} CAF fields'.format(len(sk), c))
-    cap = cap or default_ann_capacity(h, w)
+    cap = cap or int(min(8192, max(128, (h * w) // 8)))  # engine.default_ann_capacity
     while True:
         anns = np.zeros((max(1, n), cap), ANN_DTYPE)
         counts = np.zeros(max(1, n), np.int32)
