@@ -32,20 +32,14 @@ FILE_FLAGS = {'splat.hip': ['-fno-slp-vectorize']}
 
 
 VARIANTS = {
+    # the diagnostic build: per-section cycle stamps (tools/stamps_run.py, hr_stamps.py,
+    # sort_stamps.py) and the PP_SPLIT_* overrides of tools/cfg2_split.py
     'stamps': ['-DPP_STAMPS'],
-    'nofuse': ['-DPP_NO_FUSED'],         # CifHr without the LDS list / fused seed emission
-    'noself': ['-DPP_NO_SELF_PLAN'],     # seed-loop helpers planned by wave 0 only
-    'ahead': ['-DPP_RAW_AHEAD'],         # force-complete set-B connections evaluated ahead
-    'selfext': ['-DPP_SELF_EXT'],        # helper self-planning in the external-helper kernel
-    'noocc': ['-DPP_NO_SEED_OCC'],        # the seed loop's occupancy in the global grid
-    'base': ['-DPP_NO_FUSED', '-DPP_NO_SELF_PLAN', '-DPP_NO_SEED_OCC'],  # round 3's kernels
-    'bitonic': ['-DPP_NO_SEED_RADIX'],   # seeds sorted by the bitonic network only
-    'parts8': ['-DPP_SPLIT_PARTS8'],     # split-field CifHr units of 8 rows (16 rows default)
-    'w0plan': ['-DPP_W0_PLAN'],          # seed loop: wave 0 plans the idle helpers itself
-    'nopartial': ['-DPP_NO_PARTIAL'],    # seed-loop plans without the in-flight grows' joints
-    'hprio': ['-DPP_HELPER_PRIO'],       # seed-loop helper waves at issue priority 2
-    'radix7': ['-DPP_SEED_RADIX7'],      # seeds sorted by the stable 7-bit radix passes
 }
+# Round 6 dropped the A/B variants whose changes lost (nofuse, noself, ahead, selfext, noocc,
+# base, bitonic, parts8, w0plan, nopartial, hprio, radix7; DESIGN.md §4 has their numbers):
+# the product library has no other build switch.  tools/src_variant.py builds a patched copy
+# of csrc/ for new A/B runs.
 
 
 def sources():
@@ -91,8 +85,7 @@ def build(force=False, verbose=True, variant=''):
     os.makedirs(bdir, exist_ok=True)
     if (not force and os.path.exists(lib) and os.path.getmtime(lib) >= _deps_mtime()):
         return lib
-    # diagnostic variants (never loaded by default): 'stamps' (in-kernel cycle stamps), and
-    # A/B builds with one round-4 change off each (PP_LIB_VARIANT=<name> selects one)
+    # the diagnostic variant (never loaded by default): 'stamps' (in-kernel cycle stamps)
     extra = VARIANTS.get(variant, [])
     workers = min(8, len(sources()))
     with concurrent.futures.ThreadPoolExecutor(workers) as ex:

@@ -1017,216 +1017,15 @@ __device__ __forceinline__ void eval_ahead(const GrowArgs &g, Frontier &F, int i
     }
 }
 
-// ---------------------------------------------------------------------------------------
-// force-complete: the set-B connections of a joint's new frontier entries, batched
-// ---------------------------------------------------------------------------------------
-// complete_annotations' _grow (reverse_match=False, cifcaf.py:339-344) evaluates each
-// unevaluated entry when it is popped: one set-B query, a chain of four dependent memory
-// round trips (bucket offsets, cell indices, raw CAF rows, CifHr rescoring) of ~22k cycles
-// on dense input.  As eval_ahead does for set A, the entries a joint adds are evaluated
-// when it enters the frontier, kRawAhead edges at a time with their loads interleaved: the
-// batch costs the round trips of one query.  Lanes 16 b .. 16 b + 15 hold edge b's
-// bucket-row segments (<= kRawSegs), every lane one column of every edge per pass.  An edge
-// whose box spans more bucket rows stays lazy.
-constexpr int kRawAhead = 4;
-// complete_kernel evaluates set B ahead (PP_RAW_AHEAD builds): off by default -- with it the
-// kernel needs 224 VGPRs (2 waves per SIMD instead of 4), and the lost occupancy costs more
-// than the batched round trips save: planted cfg3 323k vs 331k images/s, uniform 12.4k vs
-// 15.1-15.7k, cfg5 uniform 725 vs 800-807 (A/B on one box, round 4)
-#ifdef PP_RAW_AHEAD
-constexpr bool kCompleteAhead = true;
-#else
-constexpr bool kCompleteAhead = false;
-#endif
-constexpr int kRawSegs = 64 / kRawAhead;
-
-template <bool MAXM>
-__device__ __forceinline__ void eval_ahead_raw(const GrowArgs &g, Frontier &F, int img, uint64_t r0,
-                                               uint64_t r1, float ax, float ay, float av,
-                                               float as) {
-    const int lane = threadIdx.x & 63;
-    if (g.heads.n_caf != 1) return;  // several CAF heads: every entry stays lazy
-    while (r0 | r1) {
-        int sl[kRawAhead];
-#pragma unroll
-        for (int b = 0; b < kRawAhead; b++) {  // the next kRawAhead slots
-            sl[b] = -1;
-            if (r0) {
-                sl[b] = __ffsll((unsigned long long)r0) - 1;
-                r0 &= r0 - 1;
-            } else if (r1) {
-                sl[b] = 64 + __ffsll((unsigned long long)r1) - 1;
-                r1 &= r1 - 1;
-            }
-        }
-        // per edge: the query (scalar), its set, and this lane's bucket-row segment
-        ColQuery q[kRawAhead];
-        RawSet rs[kRawAhead];
-        float jv_b[kRawAhead];
-        bool ok[kRawAhead];
-        int my_st = 0, my_len = 0;
-#pragma unroll
-        for (int b = 0; b < kRawAhead; b++) {
-            ok[b] = sl[b] >= 0;
-            if (!ok[b]) continue;
-            const int d = sl[b], l = d & 63;
-            const bool h = d >= 64;
-            // wave-uniform values, kept scalar: a per-lane index into GrowArgs' tables would
-            // copy the struct to scratch
-            const int caf = __builtin_amdgcn_readfirstlane(rl_i(h ? F.scaf[1] : F.scaf[0], l));
-            const int dir = __builtin_amdgcn_readfirstlane(rl_i(h ? F.sfwd[1] : F.sfwd[0], l)) ? 1 : 0;
-            const int j = __builtin_amdgcn_readfirstlane(rl_i(h ? F.sj[1] : F.sj[0], l));
-            jv_b[b] = rl_f(av, j);
-            q[b] = make_query(rl_f(ax, j), rl_f(ay, j), max0(rl_f(as, j)), g.cfg.exp_mode);
-            rs[b] = raw_set(g, img, caf, dir);
-            int bx0, bx1, by0, by1;
-            const ColQuery &qq = q[b];
-            if (qq.lo_x != qq.lo_x || qq.hi_x != qq.hi_x || qq.lo_y != qq.lo_y || qq.hi_y != qq.hi_y) {
-                ok[b] = false;  // NaN bounds: the lazy path scans every bucket
-                continue;
-            }
-            bx0 = (int)fminf(fmaxf(floorf(qq.lo_x * g.inv_e), 0.0f), (float)(g.bw - 1));
-            bx1 = (int)fminf(fmaxf(floorf(qq.hi_x * g.inv_e), 0.0f), (float)(g.bw - 1));
-            by0 = (int)fminf(fmaxf(floorf(qq.lo_y * g.inv_e), 0.0f), (float)(g.bh - 1));
-            by1 = (int)fminf(fmaxf(floorf(qq.hi_y * g.inv_e), 0.0f), (float)(g.bh - 1));
-            const int nseg = (by1 - by0 + 1) + 1;  // bucket rows + the NaN bucket
-            if (nseg > kRawSegs) {
-                ok[b] = false;
-                continue;
-            }
-            const int r = lane - kRawSegs * b;
-            if (r >= 0 && r < nseg) {
-                int lo, hi;
-                if (r == nseg - 1) {
-                    lo = g.nb - 1;
-                    hi = g.nb;
-                } else {
-                    lo = (by0 + r) * g.bw + bx0;
-                    hi = (by0 + r) * g.bw + bx1 + 1;
-                }
-                const int *off = col_offs(g, 1, img, caf, dir);
-                my_st = off[lo];
-                my_len = off[hi] - my_st;
-            }
-        }
-        // per edge: its column count (scalar), then passes of 64 columns over all edges
-        int tot[kRawAhead], npass = 0;
-#pragma unroll
-        for (int b = 0; b < kRawAhead; b++) {
-            tot[b] = 0;
-            if (!ok[b]) continue;
-            for (int r = 0; r < kRawSegs; r++) tot[b] += rl_i(my_len, kRawSegs * b + r);
-            npass = max(npass, (tot[b] + 63) >> 6);
-        }
-        Top2 t[kRawAhead];
-#pragma unroll
-        for (int b = 0; b < kRawAhead; b++) t[b] = top2_empty();
-        for (int p = 0; p < npass; p++) {
-            // column of every edge for this lane (-1: none), all loads of a stage together
-            int kc[kRawAhead];
-#pragma unroll
-            for (int b = 0; b < kRawAhead; b++) {
-                kc[b] = -1;
-                if (!ok[b]) continue;
-                const int tt = p * 64 + lane;
-                int run = 0;
-                for (int r = 0; r < kRawSegs; r++) {  // the segment holding tt (uniform loop)
-                    const int l = rl_i(my_len, kRawSegs * b + r);
-                    if (tt >= run && tt < run + l) kc[b] = rl_i(my_st, kRawSegs * b + r) + (tt - run);
-                    run += l;
-                }
-            }
-            int key[kRawAhead];
-#pragma unroll
-            for (int b = 0; b < kRawAhead; b++)
-                key[b] = kc[b] >= 0 ? (rs[b].idx16 ? (int)rs[b].idx16[kc[b]] : rs[b].idx[kc[b]]) : -1;
-            float c[kRawAhead], c1[kRawAhead], c2[kRawAhead], tx[kRawAhead], ty[kRawAhead],
-                tc[kRawAhead];
-#pragma unroll
-            for (int b = 0; b < kRawAhead; b++) {
-                c[b] = c1[b] = c2[b] = tx[b] = ty[b] = tc[b] = 0.0f;
-                if (key[b] < 0) continue;
-                // one CAF head (eval_ahead_raw is not used with several: a per-lane head
-                // index into GrowArgs would copy the struct to scratch)
-                const Heads &hh = g.heads;
-                const int cell = key[b];
-                const int64_t hw = (int64_t)hh.aH[0] * hh.aW[0];
-                const float stride = (float)hh.astride[0];
-                const float *caf9 = hh.caf[0] + rs[b].fld * 9 * hw;
-                c[b] = caf9[cell];
-                c1[b] = caf9[rs[b].src * hw + cell] * stride;
-                c2[b] = caf9[(rs[b].src + 1) * hw + cell] * stride;
-                tx[b] = caf9[rs[b].tgt * hw + cell] * stride;
-                ty[b] = caf9[(rs[b].tgt + 1) * hw + cell] * stride;
-                tc[b] = caf9[rs[b].tsc * hw + cell] * stride;
-            }
-            float hv[kRawAhead];
-#pragma unroll
-            for (int b = 0; b < kRawAhead; b++) {
-                hv[b] = 0.0f;
-                const ColQuery &qq = q[b];
-                if (key[b] < 0 || c1[b] < qq.lo_x || c1[b] > qq.hi_x || c2[b] < qq.lo_y ||
-                    c2[b] > qq.hi_y) {
-                    key[b] = -1;  // outside caf_center_s's box (consider_raw's order of tests)
-                    continue;
-                }
-                if (rs[b].hrt >= 0) hv[b] = g.hr.at(rs[b].hrt, tx[b], ty[b], 0.0f);
-            }
-#pragma unroll
-            for (int b = 0; b < kRawAhead; b++) {
-                if (key[b] < 0) continue;
-                float c0 = c[b];
-                if (rs[b].hrt >= 0) c0 = c[b] * (g.cif_floor + g.one_minus_floor * hv[b]);
-                if (!(c0 > g.th_b)) continue;
-                const ColQuery &qq = q[b];
-                const float dx = qq.x - c1[b], dy = qq.y - c2[b];
-                const float dd = sqrtf(dx * dx + dy * dy);
-                const float qv = (-0.5f * (dd * dd)) / qq.sigma2;
-                const float score = caf_exp(qv, qq.exp_mode) * c0;
-                top2_insert(t[b], cand_key<MAXM>(score, key[b]), tx[b], ty[b], tc[b]);
-            }
-        }
-        // connection_value without reverse matching (cifcaf.py:194-208)
-#pragma unroll
-        for (int b = 0; b < kRawAhead; b++) {
-            if (!ok[b]) continue;
-            float nx[4];
-            finish_connection<MAXM>(t[b], nx);
-            float res[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            const float ks = sqrtf(nx[3] * jv_b[b]);
-            if (!(ks < g.cfg.keypoint_threshold) && nx[3] != 0.0f) {
-                res[0] = nx[0];
-                res[1] = nx[1];
-                res[2] = nx[2];
-                res[3] = ks;
-            }
-            const int d = sl[b];
-            if (lane == (d & 63)) {
-                if (d < 64) {
-                    F.pc[0] = 1;
-                    F.px[0] = res[0];
-                    F.py[0] = res[1];
-                    F.ps[0] = res[2];
-                    F.pv[0] = res[3];
-                } else {
-                    F.pc[1] = 1;
-                    F.px[1] = res[0];
-                    F.py[1] = res[1];
-                    F.ps[1] = res[2];
-                    F.pv[1] = res[3];
-                }
-            }
-        }
-    }
-}
-
 // _grow (cifcaf.py:247-307) on the record in L.a (joint data mirrored into registers).
 // AHEAD (seed loop: set A, reverse_match): new entries' connections via eval_ahead from
-// the image's set-A column counts and LDS-staged sets; RAW_AHEAD (force-complete: set B,
-// no reverse matching) via eval_ahead_raw.
+// the image's set-A column counts and LDS-staged sets.  Force-complete (set B, no reverse
+// matching) evaluates each entry when it is popped: evaluating set-B connections ahead, a
+// few edges per memory round trip, needed 224 VGPRs (2 waves per SIMD instead of 4) and
+// measured slower (planted cfg3 323k vs 331k, uniform 12.4k vs 15.1k-15.7k images/s, round 4).
 // `abort` (a seed-loop helper's speculative grow): stop at the next pop once *abort is set
 // (wave 0 is done: the result would never be read)
-template <bool AHEAD, bool CS, typename LDS, bool RAW_AHEAD = false>
+template <bool AHEAD, bool CS, typename LDS>
 __device__ __forceinline__ void grow(const GrowArgs &g, LDS &L, int img, int set, bool reverse_match,
                                      const ColStage &cs = ColStage{}, int *abort = nullptr,
                                      float4 *pub = nullptr, uint32_t *pub_mask = nullptr) {
@@ -1260,19 +1059,12 @@ __device__ __forceinline__ void grow(const GrowArgs &g, LDS &L, int img, int set
     SlotSets ss{};
     if (AHEAD) ss = slot_sets(g, cs);
     auto ahead = [&](const uint64_t added[2]) {
-        if (!(AHEAD || RAW_AHEAD) || !(added[0] | added[1])) return;
+        if (!AHEAD || !(added[0] | added[1])) return;
         FSTAMP_BEGIN
-        if constexpr (RAW_AHEAD) {
-            if (maxm)
-                eval_ahead_raw<true>(g, F, img, added[0], added[1], ax, ay, av, as);
-            else
-                eval_ahead_raw<false>(g, F, img, added[0], added[1], ax, ay, av, as);
-        } else {
-            if (maxm)
-                eval_ahead<true>(g, F, img, cs, ss, added[0], added[1], ax, ay, av, as);
-            else
-                eval_ahead<false>(g, F, img, cs, ss, added[0], added[1], ax, ay, av, as);
-        }
+        if (maxm)
+            eval_ahead<true>(g, F, img, cs, ss, added[0], added[1], ax, ay, av, as);
+        else
+            eval_ahead<false>(g, F, img, cs, ss, added[0], added[1], ax, ay, av, as);
         FSTAMP_END(L, 1)
     };
     // `pub` (the seed loop): every joint the annotation holds, as (x, y, v, scale) in LDS as
@@ -1312,7 +1104,7 @@ __device__ __forceinline__ void grow(const GrowArgs &g, LDS &L, int img, int set
             }
             if (rl_f(av, e.k) > 0.0f) continue;
             float nx[4];
-            if ((AHEAD || RAW_AHEAD) && e.pc) {  // computed ahead when joint e.j entered
+            if (AHEAD && e.pc) {  // computed ahead when joint e.j entered
                 nx[0] = e.px;
                 nx[1] = e.py;
                 nx[2] = e.ps;
@@ -1603,11 +1395,6 @@ __device__ __forceinline__ void occ_mark(const GrowArgs &g, LDS &L, OccLog *log,
 // joint's box, and a seed is occupied iff its counter is nonzero -- exactly the grid's
 // cell value there.  Marks and tests stay in LDS: no global read-modify-write, no clearing.
 constexpr int kOccSeeds = 2560;
-#ifdef PP_NO_SEED_OCC  // A/B builds
-constexpr bool kSeedOcc = false;
-#else
-constexpr bool kSeedOcc = true;
-#endif
 struct SeedOcc {
     uint8_t cnt[kOccSeeds];     // counter per seed index
     uint32_t cell[kOccSeeds];   // grid cell (yi << 16 | xi) per seed index
@@ -1789,42 +1576,17 @@ constexpr int kSpecScan = 128;     // seeds after the committed one examined per
 // Throughput is flat for 0-4 (both generators) and drops beyond 8.
 constexpr float kSpecFar = 4.0f;
 constexpr int kSelfScan = 256;     // seeds after the decided ones a finished helper examines
-// Who plans the idle helpers when wave 0 has to grow a seed itself: wave 0, before its grow
-// (PP_W0_PLAN builds), or (default) an idle helper, so that wave 0 starts its grow at once
-// and the plan (a scan of kSpecScan seeds against the cache, about 50k cycles, stamps) is
-// off the committer's path.  Wave 0 then publishes its seed without the plan lock: a plan
-// that misses it only grows a seed twice, which never changes a result.
-#ifdef PP_W0_PLAN
-constexpr bool kW0Plan = true;
-#else
-constexpr bool kW0Plan = false;
-#endif
+// Who plans the idle helpers when wave 0 has to grow a seed itself: an idle helper, so that
+// wave 0 starts its grow at once and the plan (a scan of kSpecScan seeds against the cache,
+// about 50k cycles, stamps) is off the committer's path (wave 0 planning before its grow
+// measured no faster, round 5).  Wave 0 publishes its seed without the plan lock: a plan
+// that misses it only grows a seed twice, which never changes a result.  A helper that
+// finishes plans its own next grow (the external helpers of seed_loop_ext_kernel do not:
+// cfg5 uniform 725 vs 1080 images/s with it, round 4).
 // Grows in flight publish their joints as they are set (grow's `pub`), and the plans keep
-// seeds their occupancy boxes will cover away from the helpers (PP_NO_PARTIAL builds: only
-// the in-flight seeds' positions, kSpecFar apart).  Planted cfg3 (stamps, serial): at kernel
-// start about 4 of the 7 first picks are seeds the loop commits (tools/spec_sim.py).
-#ifdef PP_NO_PARTIAL
-constexpr bool kPartial = false;
-#else
-constexpr bool kPartial = true;
-#endif
-#ifdef PP_HELPER_PRIO
-constexpr bool kHelperPrio = true;
-#else
-constexpr bool kHelperPrio = false;
-#endif
-#ifdef PP_NO_SELF_PLAN  // A/B builds
-constexpr bool kSelfPlan = false;
-#else
-constexpr bool kSelfPlan = true;
-#endif
-// the same in seed_loop_ext_kernel (PP_SELF_EXT builds): off -- cfg5 uniform (1370
-// annotations per image, external helpers) 725 vs 1080 images/s with it
-#ifdef PP_SELF_EXT
-constexpr bool kSelfPlanExt = true;
-#else
-constexpr bool kSelfPlanExt = false;
-#endif
+// seeds their occupancy boxes will cover away from the helpers.  Planted cfg3 (stamps,
+// serial): at kernel start about 4 of the 7 first picks are seeds the loop commits
+// (tools/spec_sim.py).  (Helper waves at issue priority 2 measured no faster, round 5.)
 
 // External helpers.  A batch of fewer images than CUs leaves CUs without a seed loop, so
 // each image may get n_ext (<= kExtWgMax) more workgroups whose waves are all helpers.
@@ -2355,7 +2117,7 @@ void seed_loop_kernel(GrowArgs g) {
     const int n_seeds = min(g.seed_counts[img], g.seed_cap);
     const pp_seed *seeds = g.seeds + (int64_t)img * g.seed_cap;
     // the occupancy at the seeds in LDS (seed_occ_*), or the global grid for more seeds
-    const bool socc_on = kSeedOcc && n_seeds <= kOccSeeds;
+    const bool socc_on = n_seeds <= kOccSeeds;
     if (socc_on) seed_occ_init(s_occ, seeds, n_seeds, K, occ, red);
     const uint8_t *socc = socc_on ? s_occ.cnt : nullptr;
 
@@ -2380,17 +2142,14 @@ void seed_loop_kernel(GrowArgs g) {
     };
 
     if (wave > 0) {  // helper: grow the seeds wave 0 hands over until it is done
-        // above the other kernels' waves sharing the CU (the front half and tail of the
-        // neighbouring batches), below the committer
-        if (kHelperPrio) __builtin_amdgcn_s_setprio(2);
         for (;;) {
             int my;
             for (;;) {
                 my = lds_acquire(&S.task[wave]);
                 if (my >= 0 || lds_acquire(&S.done)) break;
-                if (!kW0Plan && lds_acquire(&S.plan_req)) {
+                if (lds_acquire(&S.plan_req)) {
                     // wave 0 is growing a seed of its own: plan every idle helper (this one
-                    // included) around it, as wave 0 did before its grow (PP_W0_PLAN)
+                    // included) around it
                     plan_lock(S);
                     if (lds_acquire(&S.plan_req) && !lds_acquire(&S.done)) {
                         if (lane == 0) lds_release(&S.plan_req, 0);
@@ -2398,7 +2157,7 @@ void seed_loop_kernel(GrowArgs g) {
                         const uint64_t idle = __ballot(lane > 0 && lane < kSeedWaves && tk < 0);
                         const int dec = lds_acquire(&S.decided);
                         if (idle)
-                            spec_plan<kSpecCache, kPartial>(S, nullptr, seeds, n_seeds, dec, dec,
+                            spec_plan<kSpecCache, true>(S, nullptr, seeds, n_seeds, dec, dec,
                                                             kSpecScan, occ, red, occ_msr(g),
                                                             g.spec_far, idle, socc);
                     }
@@ -2413,8 +2172,7 @@ void seed_loop_kernel(GrowArgs g) {
             const uint64_t hg0 = __builtin_amdgcn_s_memtime();
 #endif
             ann_from_seed(L, seeds[my], K, img);
-            grow<true, CS>(g, L, img, 0, true, cstage, &S.done, kPartial ? S.cache_j[q] : nullptr,
-                           kPartial ? &S.cache_pm[q] : nullptr);
+            grow<true, CS>(g, L, img, 0, true, cstage, &S.done, S.cache_j[q], &S.cache_pm[q]);
 #ifdef PP_STAMPS
             if (lane == 0) {  // helper grows and their cycles (phase-1 slots 8 and 5)
                 L.fst[4] += 1;
@@ -2428,9 +2186,9 @@ void seed_loop_kernel(GrowArgs g) {
             // when it has to grow a seed itself
             plan_lock(S);
             uint64_t left = 1ull << wave;
-            if (kSelfPlan && !lds_acquire(&S.done)) {
+            if (!lds_acquire(&S.done)) {
                 const int dec = lds_acquire(&S.decided);
-                left = spec_plan<kSpecCache, kPartial>(S, nullptr, seeds, n_seeds, dec, dec, kSelfScan,
+                left = spec_plan<kSpecCache, true>(S, nullptr, seeds, n_seeds, dec, dec, kSelfScan,
                                                        occ, red, occ_msr(g), g.spec_far, left, socc);
             }
             if (left && lane == 0) lds_release(&S.task[wave], -1);
@@ -2464,10 +2222,9 @@ void seed_loop_kernel(GrowArgs g) {
                 STAMP(4);
                 continue;
             }
-            // hand far-away free seeds to the idle helpers (an idle helper plans them, or
-            // wave 0 itself with PP_W0_PLAN), then grow t here
+            // hand far-away free seeds to the idle helpers (an idle helper plans them), then
+            // grow t here
             const pp_seed st = seeds[t];
-            if (kW0Plan) plan_lock(S);
             if (lane == 0) {
                 S.own_pm = 0u;  // (grow publishes the seed joint first)
                 S.own_x = st.x;
@@ -2475,24 +2232,15 @@ void seed_loop_kernel(GrowArgs g) {
                 S.own_s = st.s;
                 lds_release(&S.own_on, 1);
                 lds_release(&S.decided, t);
-                if (!kW0Plan) lds_release(&S.plan_req, 1);
+                lds_release(&S.plan_req, 1);
             }
             wave_sync();
-            if (kW0Plan) {
-                const int tk = lane > 0 && lane < kSeedWaves ? lds_acquire(&S.task[lane]) : 0;
-                const uint64_t idle = __ballot(lane > 0 && lane < kSeedWaves && tk < 0);
-                if (idle)
-                    spec_plan<kSpecCache, kPartial>(S, nullptr, seeds, n_seeds, t + 1, t, kSpecScan,
-                                                    occ, red, occ_msr(g), g.spec_far, idle, socc);
-                plan_unlock(S);
-            }
 #ifdef PP_STAMPS
             n_rounds++;
 #endif
             STAMP(1);
             ann_from_seed(L, st, K, img);
-            grow<true, CS>(g, L, img, 0, true, cstage, nullptr, kPartial ? S.own_j : nullptr,
-                           kPartial ? &S.own_pm : nullptr);
+            grow<true, CS>(g, L, img, 0, true, cstage, nullptr, S.own_j, &S.own_pm);
             STAMP(2);
             commit(&L.a, lane < K ? L.a.data[lane][0] : 0.0f, lane < K ? L.a.data[lane][1] : 0.0f,
                    lane < K ? L.a.data[lane][2] : 0.0f, lane < K ? L.a.joint_scales[lane] : 0.0f);
@@ -2587,7 +2335,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
                                  (int)((double)g.ww / g.cfg.occupancy_reduction));
     const int n_help = kSeedWaves + (X ? g.n_ext * kSeedWaves : 0);  // helper lanes 1 .. n_help-1
     // the occupancy at the seeds in LDS (seed_occ_*), or the global grid for more seeds
-    const bool socc_on = kSeedOcc && !external && n_seeds <= kOccSeeds;  // block-uniform
+    const bool socc_on = !external && n_seeds <= kOccSeeds;  // block-uniform
     if (socc_on) seed_occ_init(s_occ, seeds, n_seeds, K, occ, red);
 
     // committer state (wave 0)
@@ -2658,16 +2406,9 @@ void seed_loop_ext_kernel(GrowArgs g) {
                 continue;
             }
             publish_cached(S, cache, q, L);
-            // plan this wave's next grow itself (as in seed_loop_kernel), into this CU's slots
+            // idle again: wave 0 plans this CU's helpers (no self-planning here, above)
             plan_lock(S);
-            uint64_t left = 1ull << wave;
-            if (kSelfPlanExt && !lds_acquire(&S.done)) {
-                const int dec = lds_acquire(&S.decided);
-                left = spec_plan(S, reinterpret_cast<const float4 *>(s_cols + kColLdsExt), seeds,
-                                 n_seeds, dec, dec, kSelfScan, occ, red, occ_msr(g), g.spec_far,
-                                 left, socc_on ? s_occ.cnt : nullptr);
-            }
-            if (left && lane == 0) lds_release(&S.task[wave], -1);
+            if (lane == 0) lds_release(&S.task[wave], -1);
             plan_unlock(S);
         }
         if (external) {  // every wave of an external workgroup is a helper
@@ -2740,7 +2481,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
             }
             // a miss: hand far-away free seeds to the idle helpers, then grow t here
             const pp_seed st = seeds[t];
-            plan_lock(S);  // this CU's helpers plan for themselves too
+            plan_lock(S);  // wave 0 plans every idle helper, this CU's and the external ones
             if (lane == 0) {
                 S.own_x = st.x;
                 S.own_y = st.y;
@@ -2931,7 +2672,7 @@ __global__ __launch_bounds__(64) void complete_kernel(GrowArgs g) {
         copy_ann(&L.a, &work[i]);
         uint32_t unfilled = 0;
         for (int j = 0; j < K; j++) unfilled |= (L.a.data[j][2] == 0.0f) ? (1u << j) : 0u;
-        grow<false, CS, GrowLDS, kCompleteAhead>(g, L, img, 1, false);
+        grow<false, CS, GrowLDS>(g, L, img, 1, false);
         bool any0 = false;
         for (int j = 0; j < K; j++) {
             float &v = L.a.data[j][2];

@@ -669,13 +669,9 @@ __global__ __launch_bounds__(256) void splat_tile_kernel(TileArgs a) {
 // the clamp maps NaN to max_value), so it is skipped.
 constexpr int kChunkTiles = 1;  // tiles per workgroup: 1.209 ms vs 1.409 ms at 32 (cfg3)
 constexpr int kHrPad = 68;    // stripe row pitch (floats)
-// units per touched tile of a split field (small batches): 4 = a 16-row stripe, 8 = one
-// block row (PP_SPLIT_PARTS8; cfg2 uniform CifHr kernel 76.7 vs 69.6 us, planted equal)
-#ifdef PP_SPLIT_PARTS8
-constexpr int kSplitParts = 8;
-#else
+// units per touched tile of a split field (small batches): 4 = a 16-row stripe (8, one block
+// row each, measured slower: cfg2 uniform CifHr kernel 76.7 vs 69.6 us, planted equal)
 constexpr int kSplitParts = 4;
-#endif
 static_assert(kSplitParts == 4 || kSplitParts == 8, "unit masks are written as u16 / u8 parts");
 
 struct HrTileArgs {
@@ -2002,9 +1998,6 @@ static bool sparse_prebuilt(const Heads &h, int64_t nf) {
 }
 
 bool cifhr_fuses_seeds(const Heads &h, int n_img, int K, const pp_config *cfg) {
-#ifdef PP_NO_FUSED  // A/B builds (openpifpaf_amd.build variants)
-    return false;
-#endif
     const int64_t nf = (int64_t)n_img * K;
     // one workgroup per field: cifhr_fused_kernel<true>; split fields with a prebuilt list:
     // cifhr_list_kernel<true> + cifhr_sparse_kernel<false, true>
@@ -2078,7 +2071,6 @@ int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_confi
         hipFree(st);
     };
 #endif
-#ifndef PP_NO_FUSED
     if (a.split == 1 && h.n_cif == 1 && h.n_groups == 1 && h.group_size() == 1) {
         if (sink) {
             if (!cifhr_fuses_seeds(h, n_img, K, cfg) || sink->K != K)
@@ -2093,7 +2085,6 @@ int cifhr_sparse_launch(const Heads &h, int32_t n_img, int32_t K, const pp_confi
 #endif
         return check_launch(who);
     }
-#endif
     // split fields: one list per field, built before the fold (cifhr_list_kernel);
     // (cfg2 uniform: CifHr stage 0.173 -> 0.125 ms with the prebuilt list and stripe units;
     // planted unchanged within noise).  With a sink the list kernel also writes the seed

@@ -357,13 +357,9 @@ __device__ __forceinline__ void bitonic_desc_np(uint64_t key[KPT], uint64_t *s_b
     BitonicMerge<KPT, 2, NP>::run(key, s_buf);
 }
 
-// seeds_sort_kernel sorts 257..4096 seeds with radix_desc (below); PP_NO_SEED_RADIX: with
-// the bitonic network (whose instances for 512..4096 keys are then compiled in)
-#ifdef PP_NO_SEED_RADIX
-constexpr bool kSeedRadix = false;
-#else
-constexpr bool kSeedRadix = true;
-#endif
+// seeds_sort_kernel sorts up to 256 seeds with the bitonic network inside one wave, and
+// 257..4096 with bucket_desc (or radix_desc, below); the network for 512..4096 keys took 56k
+// of a planted image's 77k sort cycles (round 4)
 
 // the sort of the first np keys (np a power of two, rounded up to 4), 4 keys per thread;
 // block-uniform np
@@ -375,17 +371,7 @@ __device__ void bitonic_desc(uint64_t key[4], uint64_t *s_buf, int np) {
     case 32: bitonic_desc_np<4, 32>(key, s_buf); break;
     case 64: bitonic_desc_np<4, 64>(key, s_buf); break;
     case 128: bitonic_desc_np<4, 128>(key, s_buf); break;
-    case 256: bitonic_desc_np<4, 256>(key, s_buf); break;
-    default:
-        if constexpr (!kSeedRadix) {
-            switch (np) {
-            case 512: bitonic_desc_np<4, 512>(key, s_buf); break;
-            case 1024: bitonic_desc_np<4, 1024>(key, s_buf); break;
-            case 2048: bitonic_desc_np<4, 2048>(key, s_buf); break;
-            default: bitonic_desc_np<4, 4096>(key, s_buf); break;
-            }
-        }
-        break;
+    default: bitonic_desc_np<4, 256>(key, s_buf); break;  // np <= 256 here
     }
 }
 
@@ -551,21 +537,20 @@ __device__ void radix_desc(uint64_t key[4], int n, uint64_t *s_key, uint16_t *s_
     }
 }
 
-// The default sort of 257..4096 keys (PP_SEED_RADIX7: radix_desc).  The full 64-bit keys
-// are distinct (the low 27 bits hold the inverted emission index), so the order needs no
-// stable pass: one bucket pass on the top kBucketBits bits of (key >> 27) - min (LDS
-// atomics; positions inside a bucket arbitrary), then each key's rank inside its bucket by
-// counting the bucket's larger keys.  Five barriers and one LDS round trip per key, where
-// radix_desc's four or five stable 7-bit passes took 32k of a planted image's 55k sort
-// cycles (tools/sort_stamps.py).  A bucket holds the keys of one (v, field) value or of a
-// narrow range of them: runs of equal (v, field) (planted fields) cost their length squared
-// in LDS reads.  s_hist: kBuckets + 1 ints; s_w: 16 ints.  Leaves s_key[0, n) sorted.
-#ifdef PP_SEED_RADIX7
-constexpr bool kSeedBucket = false;
-#else
-constexpr bool kSeedBucket = true;
-#endif
+// The sort of 257..4096 keys.  The full 64-bit keys are distinct (the low 27 bits hold the
+// inverted emission index), so the order needs no stable pass: one bucket pass on the top
+// kBucketBits bits of (key >> 27) - min (LDS atomics; positions inside a bucket arbitrary),
+// then each key's rank inside its bucket by counting the bucket's larger keys.  Five barriers
+// and one LDS round trip per key, where radix_desc's four or five stable 7-bit passes took
+// 32k of a planted image's 55k sort cycles (tools/sort_stamps.py).  A bucket holds the keys
+// of one (v, field) value or of a narrow range of them, and ranking costs its length squared
+// in LDS reads: the bench's fields put at most 23 keys in a bucket, but saturated fields
+// (many seeds of one v) can put thousands in one.  So when a bucket passes kBucketMax keys,
+// bucket_desc returns false before it writes anything, and the caller sorts with radix_desc
+// (its cost does not depend on ties).  s_hist: kBuckets + 1 ints; s_w: 16 ints; s_flag: 1
+// int.  Leaves s_key[0, n) sorted when it returns true.
 constexpr int kBucketBits = 11, kBuckets = 1 << kBucketBits;
+constexpr int kBucketMax = 256;
 static_assert(kBuckets == 2 * 1024, "bucket_desc: two bucket counts per thread");
 
 // min / max over the wave on DPP (prefix within rows, then row_bcast15 / row_bcast31, as
@@ -580,11 +565,12 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
-__device__ void bucket_desc(uint64_t key[4], int n, uint64_t *s_key, int *s_hist, int *s_w,
-                            uint64_t *s_mm) {
+__device__ bool bucket_desc(uint64_t key[4], int n, uint64_t *s_key, int *s_hist, int *s_w,
+                            uint64_t *s_mm, int *s_flag) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     s_hist[2 * t] = 0;
     s_hist[2 * t + 1] = 0;
+    if (t == 0) *s_flag = 0;
     // the range of key >> 27 bounded through the v bits (key >> 32) alone: lo = min v << 5,
     // hi = max v << 5 | 31 (32-bit reductions; at most one bit wider than the exact range)
     uint32_t lo32 = ~0u, hi32n = ~0u;  // min of v, min of ~v
@@ -619,9 +605,11 @@ __device__ void bucket_desc(uint64_t key[4], int n, uint64_t *s_key, int *s_hist
         if (256 * w + 64 * e + lane < n) {
             bk[e] = (kBuckets - 1) - (int)(((key[e] >> 27) - lo) >> sh);
             at[e] = atomicAdd(&s_hist[bk[e]], 1);
+            if (at[e] == kBucketMax) *s_flag = 1;  // a crowded bucket: radix_desc instead
         }
     }
     __syncthreads();  // counts complete
+    if (*s_flag) return false;  // block-uniform; nothing written but the counts
     // bucket starts: thread t scans buckets 2t, 2t + 1 (block_scan_1024 has two barriers,
     // after which nobody reads the counts again)
     const int c0 = s_hist[2 * t], c1 = s_hist[2 * t + 1];
@@ -653,6 +641,7 @@ __device__ void bucket_desc(uint64_t key[4], int n, uint64_t *s_key, int *s_hist
     for (int e = 0; e < 4; e++)
         if (bk[e] >= 0) s_key[pos[e]] = key[e];
     __syncthreads();
+    return true;
 }
 
 // 41 KB of LDS (keys, bucket counts, segment offsets; x / y / s stay in the emission
@@ -661,8 +650,9 @@ __device__ void bucket_desc(uint64_t key[4], int n, uint64_t *s_key, int *s_hist
 __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
     __shared__ uint64_t s_key[kSortLds];
     // radix_desc's per-wave digit rows (u16) or bucket_desc's kBuckets + 1 counts
-    __shared__ __attribute__((aligned(16))) int s_rh_i[kSeedBucket ? kBuckets + 1
-                                                                  : 16 * kRadixPitch / 2];
+    __shared__ __attribute__((aligned(16))) int s_rh_i[kBuckets + 1];
+    static_assert(kBuckets + 1 >= 16 * kRadixPitch / 2, "radix_desc's rows fit the counts");
+    __shared__ int s_flag;
     uint16_t *s_rh = reinterpret_cast<uint16_t *>(s_rh_i);
     __shared__ int s_rw[32];
     __shared__ uint64_t s_mm[32];
@@ -776,7 +766,7 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
             }
         }
     };
-    if (n > kRadixMin && n <= kSortLds && kSeedRadix) {
+    if (n > kRadixMin && n <= kSortLds) {
         // thread (w, l) gathers seeds 256 w + 64 e + l (one round trip), then radix_desc
         uint64_t key[4];
         const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -790,10 +780,10 @@ __global__ __launch_bounds__(1024) void seeds_sort_kernel(SeedArgs a) {
             }
         }
         SORT_STAMP(2);
-        if constexpr (kSeedBucket)
-            bucket_desc(key, n, s_key, s_rh_i, s_rw, s_mm);
-        else
+        if (!bucket_desc(key, n, s_key, s_rh_i, s_rw, s_mm, &s_flag)) {
+            __syncthreads();  // every thread has read the flag before radix_desc's rows
             radix_desc(key, n, s_key, s_rh, s_rw, s_mm);
+        }
         SORT_STAMP(3);
         finish(s_key);
         __syncthreads();

@@ -153,7 +153,8 @@ def test_grow_connection_blend_matches_oracle_decode(F):
 
 
 def _oracle_grow_connection(cols, x, y, s):
-    """Direct restatement of cifcaf.py:124-192 in numpy float32 (small n)."""
+    """Direct restatement of cifcaf.py:124-192 in numpy float32 (small n), with NumPy's own
+    scalar power and exp."""
     sb = np.float32(2.0) * s
     m = ~((cols[1] < x - sb) | (cols[1] > x + sb) | (cols[2] < y - sb) | (cols[2] > y + sb))
     c = cols[:, m]
@@ -163,8 +164,10 @@ def _oracle_grow_connection(cols, x, y, s):
     dy = y - c[2]
     d = np.sqrt(dx * dx + dy * dy)
     sig = np.float32(0.5) * s
-    q = (np.float32(-0.5) * (d * d)) / (sig * sig)
-    scores = np.exp(q.astype(np.float64)).astype(np.float32) * c[0]
+    # as the reference evaluates `np.exp(-0.5 * d**2 / sigma**2)`: sigma**2 of a float32
+    # scalar is libm powf, np.exp of a float32 array NumPy's SIMD routine
+    q = (np.float32(-0.5) * (d * d)) / (sig ** 2)
+    scores = np.exp(q) * c[0]
     order = np.argsort(scores, kind='stable')
     t = c[5:]
     if len(scores) == 1:
@@ -431,13 +434,13 @@ def _tie_fields(hw, distinct):
 @pytest.mark.parametrize('n_img', [1, 17])
 @pytest.mark.parametrize('hw,distinct', [(3, True), (4, True), (10, True), (12, False),
                                          (15, True), (18, True), (20, False), (24, False)])
-def test_seeds_device_order(dec, n_img, hw, distinct):
+def test_seeds_device_order(dec, n_img, hw, distinct, seed_mask=None):
     import torch
     from openpifpaf_amd import _device
     from openpifpaf_amd._abi import SEED_DTYPE, make_config, scale_list
     from openpifpaf_amd._lib import call
     from openpifpaf_amd.decoder._fields import cfg_ptr, pitched_hr, with_geometry
-    cfg = make_config()
+    cfg = make_config(seed_mask=seed_mask)
     cif = _tie_fields(hw, distinct)
     hr = oracle.cifhr(cif)
     ref = oracle.seeds(cif, hr, cfg)
@@ -458,6 +461,15 @@ def test_seeds_device_order(dec, n_img, hw, distinct):
         assert len(got) == len(ref), (i, len(got), len(ref))
         for name in ('v', 'field', 'x', 'y', 's'):
             assert np.array_equal(got[name], ref[name]), (i, name)
+
+
+@pytest.mark.parametrize('n_img', [1, 3])
+def test_seeds_crowded_bucket_falls_back(dec, n_img):
+    """seeds_sort_kernel's bucket pass ranks a key by scanning its bucket, so a
+    bucket of b keys costs b^2 LDS reads.  9 seeding fields of 17 x 17 cells, every cell of
+    a field at one v: 289 keys per bucket, above kBucketMax, so the sort falls back to the
+    radix passes (2601 keys <= 4096); the device order equals the oracle's."""
+    test_seeds_device_order(dec, n_img, 17, False, seed_mask=[f % 2 == 0 for f in range(17)])
 
 
 # the decoder's own seeds at a batch whose fields get one workgroup each (64 images x 17
