@@ -97,7 +97,9 @@ __host__ __device__ __forceinline__ float f32_of(uint32_t u) { return __builtin_
 __host__ __device__ __forceinline__ uint64_t u64_of(double d) { return __builtin_bit_cast(uint64_t, d); }
 __host__ __device__ __forceinline__ double f64_of(uint64_t u) { return __builtin_bit_cast(double, u); }
 
-__host__ __device__ inline double glibc_powf2_double(uint32_t ix, double *ylogx_out) {
+// (not inlined: the slow path is rare, and inlined at every query it cost the grow kernels
+// registers -- the seed loop's spills 61 -> 90, force-complete 128 -> 140 VGPRs)
+inline __host__ __device__ __noinline__ double glibc_powf2_double(uint32_t ix, double *ylogx_out) {
     static constexpr double kInvc[16] = {
         0x1.661ec79f8f3bep+0, 0x1.571ed4aaf883dp+0, 0x1.49539f0f010b0p+0, 0x1.3c995b0b80385p+0,
         0x1.30d190c8864a5p+0, 0x1.25e227b0b8ea0p+0, 0x1.1bb4a4a1a343fp+0, 0x1.12358f08ae5bap+0,
@@ -170,10 +172,13 @@ __host__ __device__ inline float np_pow2_f32(float x) {
     return (float)yd;
 }
 
+// correctly rounded float32 exp through f64 (not inlined: exp_mode 1 is the rare mode)
+inline __host__ __device__ __noinline__ float exp_cr_f32(float q) { return (float)exp((double)q); }
+
 // the CAF score's np.exp under pp_config.exp_mode: 0 NumPy's SIMD routine, 1 correctly
 // rounded (through f64; NumPy's scalar loop on CPUs without FMA3)
 __host__ __device__ __forceinline__ float caf_exp(float q, int mode) {
-    return mode ? (float)exp((double)q) : np_exp_f32(q);
+    return mode ? exp_cr_f32(q) : np_exp_f32(q);
 }
 
 // functional.pyx:231-244 scalar_values for one point (bounds inclusive of W'-1, truncation)
