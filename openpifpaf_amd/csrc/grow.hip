@@ -36,7 +36,7 @@
 // to nothing.
 #ifdef PP_STAMPS
 #define STAMP_DECL                                                                          \
-    uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};                              \
+    uint64_t st_acc[kStampSlots] = {};                                                     \
     uint64_t st_t = __builtin_amdgcn_s_memtime();
 #define STAMP(i)                                                                            \
     do {                                                                                    \
@@ -50,11 +50,21 @@
         st_acc[10] = L.fst[1];                                                              \
         st_acc[11] = L.fst[2];                                                              \
         st_acc[8] = L.fst[3];                                                               \
-        for (int q_ = 0; q_ < 12; q_++)                                                     \
-            atomicAdd((unsigned long long *)&g.stamps[((int64_t)img * 3 + (ph)-1) * 12 + q_], \
+        st_acc[12] = L.fst[6];                                                              \
+        st_acc[13] = L.fst[7];                                                              \
+        for (int q_ = 0; q_ < kStampSlots; q_++)                                            \
+            atomicAdd((unsigned long long *)&g.stamps[((int64_t)img * 3 + (ph)-1) * kStampSlots + q_], \
                       (unsigned long long)st_acc[q_]);                                      \
     }
 #define FSTAMP_BEGIN const uint64_t fst_t0 = __builtin_amdgcn_s_memtime();
+// eval_ahead's sections on wave 0 (fst[6]: from the column loads to their data, fst[7]: the
+// forward query), with a vmcnt / lgkmcnt drain after the loads so the wait is attributed
+#define ESTAMP(L, i, t)                                                                     \
+    do {                                                                                    \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();                                   \
+        if ((threadIdx.x & 63) == 0) (L).fst[i] += t_ - (t);                                \
+        (t) = t_;                                                                           \
+    } while (0)
 #define FSTAMP_END(L, i)                                                                    \
     if ((threadIdx.x & 63) == 0) (L).fst[i] += __builtin_amdgcn_s_memtime() - fst_t0;
 #else
@@ -63,7 +73,9 @@
 #define STAMP_FLUSH(ph)
 #define FSTAMP_BEGIN
 #define FSTAMP_END(L, i)
+#define ESTAMP(L, i, t)
 #endif
+constexpr int kStampSlots = 16;  // per (image, phase) in the diagnostic build
 
 namespace pp {
 
@@ -142,7 +154,7 @@ struct GrowArgs {
     int2 *nms_box;            // (n_img, kNmsBoxLists, ann_cap) plane box lists beyond registers
     int ann_np;               // next pow2 >= ann_cap
     int ann_cap;
-    uint64_t *stamps;         // diagnostic build: (n_img, 3, 12) cycle sums, else NULL
+    uint64_t *stamps;         // diagnostic build: (n_img, 3, kStampSlots) cycle sums, else NULL
     int *n_work;              // (n_img) annotations after the seed loop (phase 1 -> 2)
     int *complete_next;       // (n_img) force-complete work counters (zero region; the NMS
                               // kernel, ordered after completion, resets them)
@@ -938,15 +950,18 @@ __device__ __forceinline__ void flat_query(const float v[kFlatPer][kColRows], in
 
 // the new entries `added` (slot masks, add_to_frontier) of a start joint: connection_value
 // with reverse_match (cifcaf.py:194-217) for those whose two column sets are small
-template <bool MAXM>
+template <bool MAXM, typename LDS>
 __device__ __forceinline__ void eval_ahead(const GrowArgs &g, Frontier &F, int img, const ColStage &cs,
                                            const SlotSets &ss, uint64_t r0, uint64_t r1, float ax,
-                                           float ay, float av, float as) {
+                                           float ay, float av, float as, LDS &L) {
     const int lane = threadIdx.x & 63;
     const int64_t hw = g.col_cap;
     r0 &= ss.small[0];  // the others stay lazy
     r1 &= ss.small[1];
     while (r0 | r1) {
+#ifdef PP_STAMPS
+        uint64_t et = __builtin_amdgcn_s_memtime();
+#endif
         int sl[kAhead];
 #pragma unroll
         for (int b = 0; b < kAhead; b++) {  // the next kAhead slots
@@ -978,6 +993,10 @@ __device__ __forceinline__ void eval_ahead(const GrowArgs &g, Frontier &F, int i
             flat_load_set(col_set(g, 0, img, caf, 1 - df), hw, nb[b], cs.lds, (pb & 0xFFFF) - 1,
                           vb[b]);
         }
+#ifdef PP_STAMPS
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        ESTAMP(L, 6, et);
+#endif
 #pragma unroll
         for (int b = 0; b < kAhead; b++) {
             if (sl[b] < 0) continue;
@@ -985,6 +1004,9 @@ __device__ __forceinline__ void eval_ahead(const GrowArgs &g, Frontier &F, int i
             const float jx = rl_f(ax, j), jy = rl_f(ay, j), jv = rl_f(av, j), js = rl_f(as, j);
             float nx[4];
             flat_query<MAXM>(vf[b], nf[b], jx, jy, max0(js), g.cfg.exp_mode, nx);
+#ifdef PP_STAMPS
+            ESTAMP(L, 7, et);
+#endif
             float res[4] = {0.0f, 0.0f, 0.0f, 0.0f};
             const float ks = sqrtf(nx[3] * jv);
             if (!(ks < g.cfg.keypoint_threshold) && nx[3] != 0.0f) {
@@ -1062,9 +1084,9 @@ __device__ __forceinline__ void grow(const GrowArgs &g, LDS &L, int img, int set
         if (!AHEAD || !(added[0] | added[1])) return;
         FSTAMP_BEGIN
         if (maxm)
-            eval_ahead<true>(g, F, img, cs, ss, added[0], added[1], ax, ay, av, as);
+            eval_ahead<true>(g, F, img, cs, ss, added[0], added[1], ax, ay, av, as, L);
         else
-            eval_ahead<false>(g, F, img, cs, ss, added[0], added[1], ax, ay, av, as);
+            eval_ahead<false>(g, F, img, cs, ss, added[0], added[1], ax, ay, av, as, L);
         FSTAMP_END(L, 1)
     };
     // `pub` (the seed loop): every joint the annotation holds, as (x, y, v, scale) in LDS as
@@ -3672,8 +3694,8 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
         g.ann_cap = ann_capacity;
         g.stamps = nullptr;
 #ifdef PP_STAMPS
-        hipMalloc((void **)&g.stamps, (size_t)n_img * 3 * 12 * sizeof(uint64_t));
-        hipMemsetAsync(g.stamps, 0, (size_t)n_img * 3 * 12 * sizeof(uint64_t), s);
+        hipMalloc((void **)&g.stamps, (size_t)n_img * 3 * kStampSlots * sizeof(uint64_t));
+        hipMemsetAsync(g.stamps, 0, (size_t)n_img * 3 * kStampSlots * sizeof(uint64_t), s);
         uint64_t *gcs = nullptr;
         hipMalloc((void **)&gcs, (size_t)n_img * 4 * sizeof(uint64_t));
         hipMemsetAsync(gcs, 0, (size_t)n_img * 4 * sizeof(uint64_t), s);
@@ -3738,7 +3760,7 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
                             (stages & PP_STAGE_NMS_BITMAP) != 0, s);
 #ifdef PP_STAMPS
         hipStreamSynchronize(s);
-        const size_t nst = (size_t)n_img * 3 * 12;
+        const size_t nst = (size_t)n_img * 3 * kStampSlots;
         uint64_t *h = (uint64_t *)malloc(nst * sizeof(uint64_t));
         hipMemcpy(h, g.stamps, nst * sizeof(uint64_t), hipMemcpyDeviceToHost);
         const char *path = getenv("PP_STAMPS_OUT");

@@ -43,7 +43,7 @@ for case in cases:
     torch.cuda.synchronize()
     n_ann = b.counts.cpu().numpy()
     n_seed_cells = (cif[:, :, 0] > cfg.seed_threshold).reshape(n, -1).sum(axis=1)
-    st = np.fromfile(out, dtype=np.uint64).reshape(-1, n, 3, 12)[-1].astype(np.float64)
+    st = np.fromfile(out, dtype=np.uint64).reshape(-1, n, 3, 16)[-1].astype(np.float64)
     print('== {} (mean shader cycles per image)'.format(case))
     for ph, names in ((0, P1), (1, P2), (2, P3)):
         tot = st[:, ph, :min(len(names), 5 if ph == 0 else 8)].sum(axis=1).mean()
@@ -68,5 +68,5 @@ for case in cases:
                 np.corrcoef(per, n_ann)[0, 1], np.corrcoef(per, st[:, 0, 6])[0, 1],
                 np.corrcoef(per, n_seed_cells)[0, 1]))
         for i, name in ((8, 'n connection' if ph else 'helper grows'), (9, 'in-grow pop'), (10, 'in-grow connection'),
-                        (11, 'in-grow add')):
+                        (11, 'in-grow add'), (12, ' eval: loads'), (13, ' eval: forward')):
             print('    {:14s} {:12.0f}'.format(name, st[:, ph, i].mean()))
