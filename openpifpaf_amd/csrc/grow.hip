@@ -408,6 +408,11 @@ __device__ __forceinline__ Best2 top2_wave(const Top2 &t) {
 struct ColQuery {
     float x, y, lo_x, hi_x, lo_y, hi_y, sigma2;
     int exp_mode;  // pp_config.exp_mode (caf_exp)
+    // sigma2's refined reciprocal (div_refined) for every column's -0.5 d^2 / sigma2, when
+    // the query is in its domain: sigma2 in [1, 2^90] and finite box bounds (a column that
+    // passes the box test then has |-0.5 d^2| <= 16 sigma2 <= 2^94); else IEEE division
+    Recip sr;
+    bool fast;
 };
 
 __device__ __forceinline__ ColQuery make_query(float x, float y, float xy_scale, int exp_mode) {
@@ -422,7 +427,16 @@ __device__ __forceinline__ ColQuery make_query(float x, float y, float xy_scale,
     q.hi_y = y + sbox;
     const float sigma = 0.5f * xy_scale;
     q.sigma2 = np_pow2_f32(sigma);  // `sigma**2` of a NumPy float32 scalar: libm powf
+    q.sr = recip_of(q.sigma2);
+    q.fast = q.sigma2 >= 1.0f && q.sigma2 <= 0x1p90f && fabsf(q.lo_x) <= 0x1p100f &&
+             fabsf(q.hi_x) <= 0x1p100f && fabsf(q.lo_y) <= 0x1p100f && fabsf(q.hi_y) <= 0x1p100f;
     return q;
+}
+
+// -0.5 d^2 / sigma^2 of a column inside the query's box (cifcaf.py:139), IEEE-rounded
+__device__ __forceinline__ float score_arg(const ColQuery &q, float dd) {
+    const float n = -0.5f * (dd * dd);
+    return q.fast ? div_refined(n, q.sr) : n / q.sigma2;
 }
 
 // column k (all rows loaded in one round): caf_center_s test, score (cifcaf.py:134-139).
@@ -434,8 +448,7 @@ __device__ __forceinline__ void consider_vals(const ColQuery &q, float c0, float
     if (c1 < q.lo_x || c1 > q.hi_x || c2 < q.lo_y || c2 > q.hi_y) return;
     const float dx = q.x - c1, dy = q.y - c2;
     const float dd = sqrtf(dx * dx + dy * dy);  // np.linalg.norm(axis=0)
-    const float qq = (-0.5f * (dd * dd)) / q.sigma2;
-    const float score = caf_exp(qq, q.exp_mode) * c0;  // np.exp
+    const float score = caf_exp(score_arg(q, dd), q.exp_mode) * c0;  // np.exp
     top2_insert(t, cand_key<MAXM>(score, o), tx, ty, tc);
 }
 
@@ -485,8 +498,7 @@ __device__ __forceinline__ void consider_raw(const GrowArgs &g, const RawSet &r,
     if (!(c0 > g.th_b)) return;
     const float dx = q.x - c1, dy = q.y - c2;
     const float dd = sqrtf(dx * dx + dy * dy);
-    const float qq = (-0.5f * (dd * dd)) / q.sigma2;
-    const float score = caf_exp(qq, q.exp_mode) * c0;
+    const float score = caf_exp(score_arg(q, dd), q.exp_mode) * c0;
     top2_insert(t, cand_key<MAXM>(score, key), tx, ty, tc);
 }
 

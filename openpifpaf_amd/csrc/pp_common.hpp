@@ -52,6 +52,31 @@ __host__ __device__ __forceinline__ float approx_exp_ref(float x) {
     return x;
 }
 
+// Correctly rounded n / d with a reciprocal refined once per divisor: the compiler's IEEE
+// f32 division (v_div_scale, v_rcp, Newton step, two fma corrections, v_div_fmas,
+// v_div_fixup) minus the scaling and special-case steps, which are the identity when
+// d is in [1, 2^100] and n is finite or NaN with |n| <= 2^100 (no operand scaling is
+// needed there; vcc = 0 makes v_div_fmas a plain fma).  Bit-identical to `n / d` on that
+// domain (tests/hip/div_check.hip checks it exhaustively over sampled ranges); callers
+// keep `n / d` for divisors outside it.
+struct Recip {
+    float d, r;
+};
+__device__ __forceinline__ Recip recip_of(float d) {
+    float r = __builtin_amdgcn_rcpf(d);
+    const float e = __builtin_fmaf(-d, r, 1.0f);
+    r = __builtin_fmaf(e, r, r);
+    return {d, r};
+}
+__device__ __forceinline__ bool recip_ok(float d) { return d >= 1.0f && d <= 0x1p100f; }
+__device__ __forceinline__ float div_refined(float n, const Recip &R) {
+    float q = n * R.r;
+    float rem = __builtin_fmaf(-R.d, q, n);
+    q = __builtin_fmaf(rem, R.r, q);
+    rem = __builtin_fmaf(-R.d, q, n);
+    return __builtin_fmaf(rem, R.r, q);
+}
+
 // np.exp of a float32 (cifcaf.py:139) as NumPy computes it on x86-64 with FMA3 or AVX512F:
 // NumPy 2.2's simd_exp_f32 (numpy/_core/src/umath/loops_exponent_log.dispatch.c.src, the
 // constants of npy_simd_data.h).  The quadrant q = rint(x * log2 e) by the 1.5 * 2^23 trick,
@@ -77,7 +102,16 @@ __host__ __device__ __forceinline__ float np_exp_f32(float x) {
     num = fmaf(num, r, 9.999999999980870924916e-01f);
     float den = fmaf(2.159509375685829852307e-02f, r, -2.742335390411667452936e-01f);
     den = fmaf(den, r, 1.0f);
-    return ldexpf(num / den, (int)q);
+#ifdef __HIP_DEVICE_COMPILE__
+    // num / den correctly rounded through the refined reciprocal: |r| <= ln 2 / 2 puts den
+    // in [0.9, 1.1], so 2 den lies in div_refined's divisor domain [1, 2^100] and 2 num
+    // (< 3) in its dividend domain; (2 num) / (2 den) is the same quotient, and the
+    // reciprocal (v_rcp + two fma) runs beside num's Horner steps
+    const float quo = div_refined(2.0f * num, recip_of(2.0f * den));
+#else
+    const float quo = num / den;
+#endif
+    return ldexpf(quo, (int)q);
 }
 
 // np.float32 ** 2 (cifcaf.py:139 `sigma**2`, sigma a NumPy float32 scalar): NumPy's scalar
@@ -332,31 +366,6 @@ inline HrMap dense_hr(const float *base, int hh, int ww) {
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     __builtin_amdgcn_wave_barrier();
-}
-
-// Correctly rounded n / d with a reciprocal refined once per divisor: the compiler's IEEE
-// f32 division (v_div_scale, v_rcp, Newton step, two fma corrections, v_div_fmas,
-// v_div_fixup) minus the scaling and special-case steps, which are the identity when
-// d is in [1, 2^100] and n is finite or NaN with |n| <= 2^100 (no operand scaling is
-// needed there; vcc = 0 makes v_div_fmas a plain fma).  Bit-identical to `n / d` on that
-// domain (tests/hip/div_check.hip checks it exhaustively over sampled ranges); callers
-// keep `n / d` for divisors outside it.
-struct Recip {
-    float d, r;
-};
-__device__ __forceinline__ Recip recip_of(float d) {
-    float r = __builtin_amdgcn_rcpf(d);
-    const float e = __builtin_fmaf(-d, r, 1.0f);
-    r = __builtin_fmaf(e, r, r);
-    return {d, r};
-}
-__device__ __forceinline__ bool recip_ok(float d) { return d >= 1.0f && d <= 0x1p100f; }
-__device__ __forceinline__ float div_refined(float n, const Recip &R) {
-    float q = n * R.r;
-    float rem = __builtin_fmaf(-R.d, q, n);
-    q = __builtin_fmaf(rem, R.r, q);
-    rem = __builtin_fmaf(-R.d, q, n);
-    return __builtin_fmaf(rem, R.r, q);
 }
 
 // count of set bits of `mask` below this lane (v_mbcnt)

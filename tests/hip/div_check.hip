@@ -1,6 +1,11 @@
 // div_check.hip — div_refined (pp_common.hpp) vs the compiler's IEEE f32 division, bit for
-// bit, over the domain the CifHr fold uses it on: divisors d = sigma^2 in [1, 2^100],
-// numerators n = -0.5 * (dx^2 + dy^2) with sum in [0.25, d] (plus NaN numerators).
+// bit, over the domains it is used on:
+//  - the CifHr fold: divisors d = sigma^2 in [1, 2^100], numerators n = -0.5 * (dx^2 + dy^2)
+//    with sum in [0.25, d] (plus NaN numerators);
+//  - the CAF score (grow.hip score_arg): d = sigma^2 in [1, 2^90], n = -0.5 d^2 with
+//    d^2 in [0, 128 sigma^2], log-uniform down to the subnormals, and exact zeros;
+//  - NumPy's exp (pp_common.hpp np_exp_f32): (2 num) / (2 den) with den in [0.9, 1.1] and
+//    num in [0.7, 1.5].
 // Exhaustive over d's float grid in [1, 64) x sampled numerators, random elsewhere.
 // Build + run: tests/test_gpu_divcheck.py.  Prints the mismatch count; exit 1 if any.
 #include "../../openpifpaf_amd/csrc/pp_common.hpp"
@@ -35,6 +40,57 @@ __global__ void check(unsigned long long *bad, unsigned long long *done, uint32_
     atomicAdd(done, nd);
 }
 
+// numerators log-uniform over [2^-149, hi] (and 0), negated: the CAF score's domain
+__global__ void check_wide(unsigned long long *bad, unsigned long long *done, uint32_t d_lo,
+                           uint32_t d_n, int n_per_d, uint32_t seed, float hi_scale) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= d_n) return;
+    const float d = __uint_as_float(d_lo + (uint32_t)t);
+    volatile float dv = d;
+    const Recip R = recip_of(d);
+    uint32_t x = seed ^ (uint32_t)(t * 2654435761u);
+    unsigned long long nb = 0, nd = 0;
+    const float hi = hi_scale * d;
+    for (int k = 0; k < n_per_d; k++) {
+        x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+        const uint32_t hb = __float_as_uint(hi);
+        // a random float bit pattern in [1 (subnormal), hi]
+        const uint32_t u = 1u + (uint32_t)(((uint64_t)x * (uint64_t)(hb - 1u)) >> 32);
+        float sum = __uint_as_float(u);
+        if (k == 0) sum = 0.0f;
+        if (k == 1) sum = hi;
+        const float num = -0.5f * sum;
+        const float a = num / dv;
+        const float b = div_refined(num, R);
+        nb += __float_as_uint(a) != __float_as_uint(b);
+        nd++;
+    }
+    if (nb) atomicAdd(bad, nb);
+    atomicAdd(done, nd);
+}
+
+// np_exp_f32's (2 num) / (2 den): den in [0.9, 1.1] (every float), num random in [0.7, 1.5]
+__global__ void check_exp(unsigned long long *bad, unsigned long long *done, uint32_t d_lo,
+                          uint32_t d_n, int n_per_d, uint32_t seed) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= d_n) return;
+    const float den = __uint_as_float(d_lo + (uint32_t)t);
+    volatile float dv = den;
+    const Recip R = recip_of(2.0f * den);
+    uint32_t x = seed ^ (uint32_t)(t * 2654435761u);
+    unsigned long long nb = 0, nd = 0;
+    for (int k = 0; k < n_per_d; k++) {
+        x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+        const float num = 0.7f + (float)(x >> 8) * 0x1p-24f * 0.8f;
+        const float a = num / dv;
+        const float b = div_refined(2.0f * num, R);
+        nb += __float_as_uint(a) != __float_as_uint(b);
+        nd++;
+    }
+    if (nb) atomicAdd(bad, nb);
+    atomicAdd(done, nd);
+}
+
 int main() {
     unsigned long long *bad, *done;
     (void)hipMalloc(&bad, 8);
@@ -50,6 +106,22 @@ int main() {
     for (float st : starts) {
         const uint32_t l = __builtin_bit_cast(uint32_t, st);
         hipLaunchKernelGGL(check, dim3((1u << 20) / 256), dim3(256), 0, 0, bad, done, l, 1u << 20, 64, 777u);
+    }
+    // the CAF score: every float in [1, 16), and sampled divisors up to 2^90
+    {
+        const uint32_t l1 = __builtin_bit_cast(uint32_t, 1.0f), h1 = __builtin_bit_cast(uint32_t, 16.0f);
+        hipLaunchKernelGGL(check_wide, dim3((h1 - l1 + 255) / 256), dim3(256), 0, 0, bad, done, l1,
+                           h1 - l1, 32, 4242u, 64.0f);
+        const float wide[] = {16.0f, 777.0f, 1e6f, 1e12f, 1e20f, 1e26f};
+        for (float st : wide) {
+            const uint32_t l = __builtin_bit_cast(uint32_t, st);
+            hipLaunchKernelGGL(check_wide, dim3((1u << 20) / 256), dim3(256), 0, 0, bad, done, l,
+                               1u << 20, 32, 99u, 64.0f);
+        }
+        // np_exp_f32's quotients: every den in [0.9, 1.1]
+        const uint32_t le = __builtin_bit_cast(uint32_t, 0.9f), he = __builtin_bit_cast(uint32_t, 1.1f);
+        hipLaunchKernelGGL(check_exp, dim3((he - le + 255) / 256), dim3(256), 0, 0, bad, done, le,
+                           he - le, 32, 31337u);
     }
     unsigned long long hb = 0, hd = 0;
     (void)hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost);
