@@ -51,6 +51,7 @@ __global__ void check_wide(unsigned long long *bad, unsigned long long *done, ui
     uint32_t x = seed ^ (uint32_t)(t * 2654435761u);
     unsigned long long nb = 0, nd = 0;
     const float hi = hi_scale * d;
+    float worst = 0.0f;
     for (int k = 0; k < n_per_d; k++) {
         x ^= x << 13; x ^= x >> 17; x ^= x << 5;
         const uint32_t hb = __float_as_uint(hi);
@@ -62,10 +63,15 @@ __global__ void check_wide(unsigned long long *bad, unsigned long long *done, ui
         const float num = -0.5f * sum;
         const float a = num / dv;
         const float b = div_refined(num, R);
-        nb += __float_as_uint(a) != __float_as_uint(b);
+        const bool miss = __float_as_uint(a) != __float_as_uint(b);
+        nb += miss;
+        if (miss) worst = fmaxf(worst, sum);
         nd++;
     }
-    if (nb) atomicAdd(bad, nb);
+    if (nb) {
+        atomicAdd(bad, nb);
+        atomicMax((unsigned int *)(bad + 1), __float_as_uint(worst));  // largest failing sum
+    }
     atomicAdd(done, nd);
 }
 
@@ -92,11 +98,15 @@ __global__ void check_exp(unsigned long long *bad, unsigned long long *done, uin
 }
 
 int main() {
-    unsigned long long *bad, *done;
+    unsigned long long *bad, *done, *bad_w, *bad_e;
     (void)hipMalloc(&bad, 8);
     (void)hipMalloc(&done, 8);
+    (void)hipMalloc(&bad_w, 16);
+    (void)hipMalloc(&bad_e, 8);
     (void)hipMemset(bad, 0, 8);
     (void)hipMemset(done, 0, 8);
+    (void)hipMemset(bad_w, 0, 16);
+    (void)hipMemset(bad_e, 0, 8);
     // every float in [1, 64): 6 * 2^23 divisors, 64 numerators each
     const uint32_t lo = __builtin_bit_cast(uint32_t, 1.0f), hi = __builtin_bit_cast(uint32_t, 64.0f);
     const uint32_t n = hi - lo;
@@ -110,22 +120,28 @@ int main() {
     // the CAF score: every float in [1, 16), and sampled divisors up to 2^90
     {
         const uint32_t l1 = __builtin_bit_cast(uint32_t, 1.0f), h1 = __builtin_bit_cast(uint32_t, 16.0f);
-        hipLaunchKernelGGL(check_wide, dim3((h1 - l1 + 255) / 256), dim3(256), 0, 0, bad, done, l1,
+        hipLaunchKernelGGL(check_wide, dim3((h1 - l1 + 255) / 256), dim3(256), 0, 0, bad_w, done, l1,
                            h1 - l1, 32, 4242u, 64.0f);
         const float wide[] = {16.0f, 777.0f, 1e6f, 1e12f, 1e20f, 1e26f};
         for (float st : wide) {
             const uint32_t l = __builtin_bit_cast(uint32_t, st);
-            hipLaunchKernelGGL(check_wide, dim3((1u << 20) / 256), dim3(256), 0, 0, bad, done, l,
+            hipLaunchKernelGGL(check_wide, dim3((1u << 20) / 256), dim3(256), 0, 0, bad_w, done, l,
                                1u << 20, 32, 99u, 64.0f);
         }
         // np_exp_f32's quotients: every den in [0.9, 1.1]
         const uint32_t le = __builtin_bit_cast(uint32_t, 0.9f), he = __builtin_bit_cast(uint32_t, 1.1f);
-        hipLaunchKernelGGL(check_exp, dim3((he - le + 255) / 256), dim3(256), 0, 0, bad, done, le,
+        hipLaunchKernelGGL(check_exp, dim3((he - le + 255) / 256), dim3(256), 0, 0, bad_e, done, le,
                            he - le, 32, 31337u);
     }
-    unsigned long long hb = 0, hd = 0;
+    unsigned long long hb = 0, hd = 0, hw[2] = {0, 0}, he = 0;
     (void)hipMemcpy(&hb, bad, 8, hipMemcpyDeviceToHost);
     (void)hipMemcpy(&hd, done, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(hw, bad_w, 16, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(&he, bad_e, 8, hipMemcpyDeviceToHost);
+    const uint32_t ws = (uint32_t)hw[1];
+    printf("fold domain mismatches %llu; score domain mismatches %llu (largest failing sum %a); "
+           "exp quotient mismatches %llu\n", hb, hw[0], __builtin_bit_cast(float, ws), he);
+    hb += hw[0] + he;
     printf("checked %llu divisions, mismatches %llu\n", hd, hb);
     return hb == 0 && hd > 0 ? 0 : 1;
 }
