@@ -3,7 +3,9 @@
 //  - the CifHr fold: divisors d = sigma^2 in [1, 2^100], numerators n = -0.5 * (dx^2 + dy^2)
 //    with sum in [0.25, d] (plus NaN numerators);
 //  - the CAF score (grow.hip score_arg): d = sigma^2 in [1, 2^90], n = -0.5 d^2 with
-//    d^2 in [0, 128 sigma^2], log-uniform down to the subnormals, and exact zeros;
+//    d^2 in [0, 128 sigma^2], log-uniform down to the subnormals, and exact zeros: the
+//    quotient bit for bit where |n| >= 2^-60, np.exp of it below (both quotients round
+//    np.exp to 1 there);
 //  - NumPy's exp (pp_common.hpp np_exp_f32): (2 num) / (2 den) with den in [0.9, 1.1] and
 //    num in [0.7, 1.5].
 // Exhaustive over d's float grid in [1, 64) x sampled numerators, random elsewhere.
@@ -63,7 +65,10 @@ __global__ void check_wide(unsigned long long *bad, unsigned long long *done, ui
         const float num = -0.5f * sum;
         const float a = num / dv;
         const float b = div_refined(num, R);
-        const bool miss = __float_as_uint(a) != __float_as_uint(b);
+        // the quotient itself where |num| >= 2^-60; below, the score only needs the same
+        // np.exp (both quotients are < 2^-59 in magnitude, where exp rounds to 1)
+        const bool miss = sum >= 0x1p-59f ? __float_as_uint(a) != __float_as_uint(b)
+                                          : __float_as_uint(np_exp_f32(a)) != __float_as_uint(np_exp_f32(b));
         nb += miss;
         if (miss) worst = fmaxf(worst, sum);
         nd++;
