@@ -2524,7 +2524,13 @@ void seed_loop_ext_kernel(GrowArgs g) {
                 lds_release(&S.decided, t);
             }
             wave_sync();
+#ifdef PP_STAMPS
+            const uint64_t xr0 = __builtin_amdgcn_s_memtime();
+#endif
             ext_refresh(S, s_cols, X, xrec, -1);
+#ifdef PP_STAMPS
+            st_acc[14] += __builtin_amdgcn_s_memtime() - xr0;  // plan: the external slots' refresh
+#endif
             int tk = 0;
             if (lane > 0 && lane < kSeedWaves)
                 tk = lds_acquire(&S.task[lane]) < 0 ? 1 : 0;
@@ -2606,7 +2612,14 @@ void seed_loop_ext_kernel(GrowArgs g) {
                     if (!use_l) {  // the helper may have just left: then skip it
                         const unsigned long long job = 2ull | ((unsigned long long)(q - kSpecCache) << 8) |
                                                        ((unsigned long long)sd << 32);
-                        if (!cas_agent_wave(&X->task[w - kSeedWaves], 1ull, job)) {
+#ifdef PP_STAMPS
+                        const uint64_t xc0 = __builtin_amdgcn_s_memtime();
+#endif
+                        const bool got = cas_agent_wave(&X->task[w - kSeedWaves], 1ull, job);
+#ifdef PP_STAMPS
+                        st_acc[15] += __builtin_amdgcn_s_memtime() - xc0;  // plan: hand-off CAS
+#endif
+                        if (!got) {
                             m |= 1ull << l;  // the seed is still unassigned
                             continue;
                         }
