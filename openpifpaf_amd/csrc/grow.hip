@@ -1773,6 +1773,27 @@ __device__ __forceinline__ float4 *cache_joints(SeedLoopSharedX &S, float *s_col
     return q < kSpecCache ? S.cache_j[q]
                           : reinterpret_cast<float4 *>(s_cols + kColLdsExt) + (q - kSpecCache) * kKP;
 }
+// The occupancy boxes a grown slot's joints will mark once committed (occ_box_r), for the
+// plan of seed_loop_ext_kernel: written with the joints, before the slot's state 2, so a
+// plan tests a seed against a slot with one LDS read.  Packed x0 | x1 << 16, y0 | y1 << 16
+// (the launch checks that the occupancy grid is narrower than 2^16); an empty box is 0, 0.
+// After the external joints in the dynamic LDS, one row of kKP per slot (all kCacheSlots).
+constexpr size_t kExtDynLds = kColLdsExt * sizeof(float) + (size_t)kExtCache * kKP * sizeof(float4) +
+                              (size_t)kCacheSlots * kKP * sizeof(uint2);
+__device__ __forceinline__ uint2 *cache_boxes(float *s_cols, int q) {
+    return reinterpret_cast<uint2 *>(reinterpret_cast<float4 *>(s_cols + kColLdsExt) + kExtCache * kKP) +
+           q * kKP;
+}
+__device__ __forceinline__ uint2 plan_box(float red, float msr, const OccGrid &o, int f, float4 j) {
+    int box[4];
+    if (j.z == 0.0f || !occ_box_r(red, msr, o, f, j.x, j.y, j.w, box)) return make_uint2(0u, 0u);
+    return make_uint2((uint32_t)box[0] | ((uint32_t)box[1] << 16),
+                      (uint32_t)box[2] | ((uint32_t)box[3] << 16));
+}
+__device__ __forceinline__ bool in_plan_box(uint2 b, int cx, int cy) {
+    return cx >= (int)(b.x & 0xFFFFu) && cx < (int)(b.x >> 16) && cy >= (int)(b.y & 0xFFFFu) &&
+           cy < (int)(b.y >> 16);
+}
 
 __device__ __forceinline__ int lds_acquire(int *p) {
     return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1811,7 +1832,8 @@ __device__ __forceinline__ void ann_from_seed(LDS &L, const pp_seed &sd, int K, 
 // wave 0: external slots being grown whose tag has arrived become grown (joints into LDS);
 // `only` >= 0 restricts the check to that slot
 __device__ __forceinline__ void ext_refresh(SeedLoopSharedX &S, float *s_cols, const SeedExt *X,
-                                            const pp_ann *xrec, int only) {
+                                            const pp_ann *xrec, int only, float red, float msr,
+                                            const OccGrid &occ) {
     const int lane = threadIdx.x & 63;
     const int q = kSpecCache + lane;
     bool ready = false;
@@ -1840,10 +1862,12 @@ __device__ __forceinline__ void ext_refresh(SeedLoopSharedX &S, float *s_cols, c
         const pp_ann *r = xrec + e;
         if (lane < kKP) {
             const unsigned int *d = reinterpret_cast<const unsigned int *>(&r->data[lane][0]);
-            cache_joints(S, s_cols, kSpecCache + e)[lane] = make_float4(
+            const float4 j = make_float4(
                 __uint_as_float(ld_agent(d)), __uint_as_float(ld_agent(d + 1)),
                 __uint_as_float(ld_agent(d + 2)),
                 __uint_as_float(ld_agent(reinterpret_cast<const unsigned int *>(&r->joint_scales[lane]))));
+            cache_joints(S, s_cols, kSpecCache + e)[lane] = j;
+            cache_boxes(s_cols, kSpecCache + e)[lane] = plan_box(red, msr, occ, lane, j);
         }
         wave_sync();
         if (lane == 0) S.cache_state[kSpecCache + e] = 2;
@@ -2365,6 +2389,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
     pp_ann *work = g.work + (int64_t)img * g.ann_cap;
     pp_ann *cache = g.spec + (int64_t)img * kSpecCache;
     const float red = (float)g.cfg.occupancy_reduction;
+    const float msr = occ_msr(g);
     const OccGrid occ = occ_grid(occ_base, K, (int)((double)g.hh / g.cfg.occupancy_reduction),
                                  (int)((double)g.ww / g.cfg.occupancy_reduction));
     const int n_help = kSeedWaves + (X ? g.n_ext * kSeedWaves : 0);  // helper lanes 1 .. n_help-1
@@ -2439,7 +2464,11 @@ void seed_loop_ext_kernel(GrowArgs g) {
                 t0 = __builtin_amdgcn_s_memrealtime();
                 continue;
             }
-            publish_cached(S, cache, q, L);
+            if (lane < kKP)
+                cache_boxes(s_cols, q)[lane] = plan_box(
+                    red, msr, occ, lane,
+                    make_float4(L.a.data[lane][0], L.a.data[lane][1], L.a.data[lane][2], L.a.joint_scales[lane]));
+            publish_cached(S, cache, q, L);  // (its release orders the boxes too)
             // idle again: wave 0 plans this CU's helpers (no self-planning here, above)
             plan_lock(S);
             if (lane == 0) lds_release(&S.task[wave], -1);
@@ -2475,6 +2504,9 @@ void seed_loop_ext_kernel(GrowArgs g) {
             int hslot = -1;
             if (hit) {  // a helper grew it, or is growing it
                 const int slot = __ffsll((unsigned long long)hit) - 1;
+#ifdef PP_STAMPS
+                uint64_t hw0 = __builtin_amdgcn_s_memtime();
+#endif
                 if (slot < kSpecCache) {
                     while (lds_acquire(&S.cache_state[slot]) != 2) __builtin_amdgcn_s_sleep(1);
                 } else {
@@ -2485,7 +2517,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
                     const uint64_t limit =
                         (S.ext_ticks == 0u || el >= S.ext_ticks / 2u) ? kExtWaitMax : 0ull;
                     for (;;) {
-                        ext_refresh(S, s_cols, X, xrec, slot);
+                        ext_refresh(S, s_cols, X, xrec, slot, red, msr, occ);
                         if (S.cache_state[slot] == 2) break;
                         if (__builtin_amdgcn_s_memrealtime() - w0 >= limit) {
                             if (lane == 0) S.cache_state[slot] = 4;  // grow it here instead
@@ -2497,6 +2529,9 @@ void seed_loop_ext_kernel(GrowArgs g) {
                 }
                 taken = S.cache_state[slot] == 2;
                 hslot = slot;
+#ifdef PP_STAMPS
+                ESTAMP(L, 7, hw0);  // a hit: waiting for the helper
+#endif
             }
             if (taken) {
                 const float4 jq = lane < kKP ? cache_joints(S, s_cols, hslot)[lane]
@@ -2527,7 +2562,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
 #ifdef PP_STAMPS
             const uint64_t xr0 = __builtin_amdgcn_s_memtime();
 #endif
-            ext_refresh(S, s_cols, X, xrec, -1);
+            ext_refresh(S, s_cols, X, xrec, -1, red, msr, occ);
 #ifdef PP_STAMPS
             st_acc[14] += __builtin_amdgcn_s_memtime() - xr0;  // plan: the external slots' refresh
 #endif
@@ -2537,13 +2572,20 @@ void seed_loop_ext_kernel(GrowArgs g) {
             else if (lane >= kSeedWaves && lane < n_help)
                 tk = ld_agent(&X->task[lane - kSeedWaves]) == 1ull ? 1 : 0;
             uint64_t idle = __ballot(tk != 0);
+            // The slots, one lane each: a snapshot (only wave 0 claims slots; a helper turning
+            // 1 into 2 meanwhile at most keeps this plan from reusing or testing that slot),
+            // kept current for this plan's own picks.
+            const bool sl = lane < NS;
+            int r_st = sl ? lds_acquire(&S.cache_state[lane]) : 0;
+            int r_seed = sl ? S.cache_seed[lane] : -1;
+            float r_x = sl ? S.cache_x[lane] : 0.0f, r_y = sl ? S.cache_y[lane] : 0.0f,
+                  r_s = sl ? S.cache_s[lane] : 0.0f;
             // the seeds in flight: later picks keep kSpecFar from them
-            const int cst = lane < NS ? lds_acquire(&S.cache_state[lane]) : 0;
-            uint64_t fly = __ballot(lane < NS && cst == 1);
+            uint64_t fly = __ballot(sl && r_st == 1);
             const int scan_end = min(n_seeds, t + 1 + kSpecScan);
-            // the slots holding seeds after t (the others are free or passed)
-            const int csd = lane < NS ? S.cache_seed[lane] : -1;
-            uint64_t ahead = __ballot(lane < NS && csd > t);
+#ifdef PP_STAMPS
+            uint64_t pf0 = __builtin_amdgcn_s_memtime();
+#endif
             for (int base = t + 1; base < scan_end && idle; base += 64) {
                 const int idx = base + lane;
                 bool ok = idx < scan_end;
@@ -2553,48 +2595,51 @@ void seed_loop_ext_kernel(GrowArgs g) {
                     ok = spec_far(g.spec_far, c.x, c.y, c.s, st.x, st.y, st.s) &&
                          !(socc_on ? s_occ.cnt[idx] != 0 : occ_get(occ, c.field, c.x, c.y, red));
                 }
-                // cache entries (uniform loop): skip seeds they hold, seeds that a grown
-                // annotation's occupancy boxes will cover once committed, and seeds near
-                // one still being grown
+                // the slots holding seeds after t (the others are free or passed): skip the
+                // seeds they hold, seeds near one still being grown, and seeds that a grown
+                // annotation's occupancy boxes will cover once committed
+                const uint64_t ahead = __ballot(sl && r_seed > t);
+                const uint64_t held = __ballot(sl && r_seed >= base && r_seed < base + 64) & ahead;
+                for (uint64_t hq = held; hq; hq &= hq - 1)
+                    if (idx == __builtin_amdgcn_readlane(r_seed, __ffsll((unsigned long long)hq) - 1)) ok = false;
+                for (uint64_t fq = ahead & fly; fq; fq &= fq - 1) {
+                    const int q = __ffsll((unsigned long long)fq) - 1;
+                    ok = ok && spec_far(g.spec_far, c.x, c.y, c.s, rl_f(r_x, q), rl_f(r_y, q), rl_f(r_s, q));
+                }
                 const int cxi = (int)clip_ref(c.x / red, 0.0f, (float)(occ.w - 1));
                 const int cyi = (int)clip_ref(c.y / red, 0.0f, (float)(occ.h - 1));
-                for (uint64_t aq = ahead; aq; aq &= aq - 1) {
-                    const int q = __ffsll((unsigned long long)aq) - 1;
-                    const int sq = S.cache_seed[q];
-                    if (sq == idx) ok = false;
-                    if (!ok) continue;
-                    if ((fly >> q) & 1) {
-                        ok = spec_far(g.spec_far, c.x, c.y, c.s, S.cache_x[q], S.cache_y[q],
-                                      S.cache_s[q]);
-                        continue;
+                const int cf = ok ? c.field : 0;
+                uint64_t gq = ahead & __ballot(sl && r_st == 2);
+                while (gq) {  // four slots' boxes per LDS round trip
+                    int qs[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        qs[u] = gq ? __ffsll((unsigned long long)gq) - 1 : -1;
+                        gq &= gq ? gq - 1 : 0ull;
                     }
-                    if (S.cache_state[q] != 2) continue;
-                    const float4 jq = cache_joints(S, s_cols, q)[c.field];
-                    int box[4];
-                    if (jq.z != 0.0f && occ_box(g, occ, c.field, jq.x, jq.y, jq.w, box) &&
-                        cxi >= box[0] && cxi < box[1] && cyi >= box[2] && cyi < box[3])
-                        ok = false;
+                    uint2 b[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        b[u] = qs[u] >= 0 ? cache_boxes(s_cols, qs[u])[cf] : make_uint2(0u, 0u);
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        if (in_plan_box(b[u], cxi, cyi)) ok = false;
                 }
                 uint64_t m = __ballot(ok);
+#ifdef PP_STAMPS
+                ESTAMP(L, 6, pf0);  // plan: the seed filter
+#endif
                 while (m && idle) {
                     const int l = __ffsll((unsigned long long)m) - 1;
                     m &= m - 1;
                     const float cx = rl_f(c.x, l), cy = rl_f(c.y, l), csc = rl_f(c.s, l);
-                    bool far = true;  // from this plan's earlier picks (now in flight too)
-                    uint64_t f2 = fly;
-                    while (f2) {
-                        const int q = __ffsll((unsigned long long)f2) - 1;
-                        f2 &= f2 - 1;
-                        far = far && spec_far(g.spec_far, cx, cy, csc, S.cache_x[q],
-                                              S.cache_y[q], S.cache_s[q]);
-                    }
-                    if (!far) continue;
+                    // far from every seed in flight, this plan's earlier picks included (a
+                    // lane per slot)
+                    if (__ballot(((fly >> lane) & 1ull) && !spec_far(g.spec_far, cx, cy, csc, r_x, r_y, r_s)))
+                        continue;
                     // a free slot of the helper's kind (this CU's: 0 .. kSpecCache-1; the
                     // external ones after): never grown into, or grown for a seed passed
-                    const int cq = lane < NS ? S.cache_seed[lane] : 0;
-                    const int cst2 = lane < NS ? S.cache_state[lane] : 1;
-                    const uint64_t freeq = __ballot(lane < NS &&
-                                                    (cst2 == 0 || (cst2 == 2 && cq < t)));
+                    const uint64_t freeq = __ballot(sl && (r_st == 0 || (r_st == 2 && r_seed < t)));
                     const uint64_t free_l = freeq & ((1ull << kSpecCache) - 1ull);
                     const uint64_t free_x = freeq & ~((1ull << kSpecCache) - 1ull);
                     const uint64_t idle_l = idle & ((1ull << kSeedWaves) - 1ull);
@@ -2625,7 +2670,13 @@ void seed_loop_ext_kernel(GrowArgs g) {
                         }
                     }
                     fly |= 1ull << q;
-                    ahead |= 1ull << q;
+                    if (lane == q) {
+                        r_st = 1;
+                        r_seed = sd;
+                        r_x = cx;
+                        r_y = cy;
+                        r_s = csc;
+                    }
                     if (lane == 0) {
                         S.cache_x[q] = cx;
                         S.cache_y[q] = cy;
@@ -2640,6 +2691,9 @@ void seed_loop_ext_kernel(GrowArgs g) {
                     }
                     wave_sync();
                 }
+#ifdef PP_STAMPS
+                ESTAMP(L, 6, pf0);  // plan: the picks
+#endif
             }
             plan_unlock(S);
 #ifdef PP_STAMPS
@@ -3708,7 +3762,10 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
         g.work = (pp_ann *)(ws + d.off_work);
         g.spec = (pp_ann *)(ws + d.off_spec);
         g.spec_far = kSpecFar;
-        g.n_ext = seed_ext_per_image(n_img);
+        // (the external helpers' plan packs occupancy boxes in 16 bits: cache_boxes)
+        g.n_ext = (d.hh / cfg->occupancy_reduction < 65535.0 && d.ww / cfg->occupancy_reduction < 65535.0)
+                      ? seed_ext_per_image(n_img)
+                      : 0;
         g.xext = (SeedExt *)(ws + d.off_xext);
         g.xrec = (pp_ann *)(ws + d.off_xrec);
         g.nms_score = (double *)(ws + d.off_nms_score);
@@ -3742,9 +3799,7 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
         if (!(stages & PP_STAGE_AFTER_SEED_LOOP)) {
             // g.xext is zero: the workspace's zero region, which every external-helper seed
             // loop leaves zero (ext_exit)
-            const size_t dyn = g.n_ext > 0
-                                   ? kColLdsExt * sizeof(float) + (size_t)kExtCache * kKP * sizeof(float4)
-                                   : kColLds * sizeof(float);
+            const size_t dyn = g.n_ext > 0 ? kExtDynLds : kColLds * sizeof(float);
             // confidence_scales: their own kernel instances (the default ones carry no
             // registers for them: complete_kernel stays at 128 VGPRs, 4 waves per SIMD)
             const dim3 blk(64 * kSeedWaves);

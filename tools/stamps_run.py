@@ -68,7 +68,8 @@ for case in cases:
                 np.corrcoef(per, n_ann)[0, 1], np.corrcoef(per, st[:, 0, 6])[0, 1],
                 np.corrcoef(per, n_seed_cells)[0, 1]))
         for i, name in ((8, 'n connection' if ph else 'helper grows'), (9, 'in-grow pop'), (10, 'in-grow connection'),
-                        (11, 'in-grow add'), (12, ' eval: loads'), (13, ' eval: forward'),
+                        (11, 'in-grow add'), (12, ' eval: loads / ext plan: filter+picks'),
+                        (13, ' eval: forward / ext hit: wait'),
                         (14, ' plan: ext refresh' if ph == 0 else '-'),
                         (15, ' plan: ext CAS' if ph == 0 else '-')):
             print('    {:14s} {:12.0f}'.format(name, st[:, ph, i].mean()))
