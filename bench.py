@@ -182,7 +182,7 @@ def main():
     overlap = not (args.no_overlap or args.stage_breakdown) and stages == 15
     pipe = DecodePipeline(dev) if overlap else None
     # steps in flight on the host: one more than the pipeline's workspaces (3 with the
-    # default two; PP_PIPE_DEPTH=3 needs 4, tools/pipe_gaps.py), 2 on one stream (two
+    # default two; a depth-3 pipeline needs 4, tools/pipe_gaps.py), 2 on one stream (two
     # output slots)
     depth = pipe.depth + 1 if overlap else 2
     groups = ((STAGE_CIFHR, STAGE_SEEDS, STAGE_CAF, STAGE_GROW) if args.stage_breakdown else
@@ -551,10 +551,9 @@ def library_identity():
     csrc/* and the header, the key profiles/<tag>_summary.json files are matched by), the
     sha256 of the loaded .so itself, its variant ('product' unless PP_LIB_VARIANT loaded a
     diagnostic or A/B build), and every PP_* environment variable this process saw.  The
-    product library reads none of them (diagnostic builds read their stamp paths); the
-    Python pipeline's PP_PIPE_* / PP_SPLIT_TAIL scheduling knobs change the order of
-    launches, never what is computed.  `headline` is false when the line did not run the
-    product library with the default schedule."""
+    product library reads none of them (diagnostic builds read their stamp paths), and the
+    Python pipeline's scheduling choices are constants (engine._B_FIRST ...).  `headline`
+    is false when the line did not run the product library."""
     import hashlib
     from openpifpaf_amd import _lib
     from openpifpaf_amd.build import source_digest

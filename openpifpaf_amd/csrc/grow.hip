@@ -183,7 +183,7 @@ struct GrowLDST {
     int log_n;
     int status;
 #ifdef PP_STAMPS
-    uint64_t fst[8];  // inside-grow section sums (diagnostic build)
+    uint64_t fst[10];  // inside-grow section sums (diagnostic build); [8], [9]: seed loop
 #endif
 };
 using GrowLDS = GrowLDST<true>;
@@ -874,7 +874,10 @@ __device__ __forceinline__ void flat_load(const float *__restrict__ cf, int64_t 
 // that fits kColLds floats, in (CAF, direction) order, column-major (kColPad floats per
 // column: two 16-byte reads).  cofs[q] = its offset, -1 = global.
 constexpr int kColPad = 8;
-constexpr int kColLds = 20480;  // 80 KB (64 KB: 1-2% slower per planted cfg3 step)
+// 77 KB (64 KB: 1-2% slower per planted cfg3 step).  With the seed loop's static LDS this
+// leaves 39 KB of the CU's 160 KB for the next batch's kernels (DecodePipeline): CafScored
+// (caf_bucketed_kernel, 37 KB) must fit beside it (3 KB less: uniform cfg3 4% slower).
+constexpr int kColLds = 19712;
 // the external-helper kernel (seed_loop_ext_kernel: images with helpers on other CUs, e.g.
 // cfg5) stages 48 KB: the LDS it leaves lets the other batch's kernels share its CUs (cfg5
 // uniform 1452-1473 -> 1583-1585 images/s, planted 41.3k -> 43.1k-43.7k; 80 KB for the
@@ -1616,7 +1619,11 @@ constexpr int kSelfScan = 256;     // seeds after the decided ones a finished he
 // measured no faster, round 5).  Wave 0 publishes its seed without the plan lock: a plan
 // that misses it only grows a seed twice, which never changes a result.  A helper that
 // finishes plans its own next grow (the external helpers of seed_loop_ext_kernel do not:
-// cfg5 uniform 725 vs 1080 images/s with it, round 4).
+// cfg5 uniform 725 vs 1080 images/s with it, round 4), and a helper whose plan found
+// nothing plans again once wave 0 has committed or passed a seed (idle_dec): a wave 0 that
+// only takes cached annotations never misses, so never requests a plan.  Uniform cfg3
+// (round 6, A/B on one box): the slot-register plan alone 15.2-15.3k images/s, with the
+// re-plan 16.3-16.5k, the round-5 plan 15.7-15.9k.
 // Grows in flight publish their joints as they are set (grow's `pub`), and the plans keep
 // seeds their occupancy boxes will cover away from the helpers.  Planted cfg3 (stamps,
 // serial): at kernel start about 4 of the 7 first picks are seeds the loop commits
@@ -1653,6 +1660,9 @@ static_assert(kCacheSlots <= 64 && kSeedWaves + kExtHelpers <= 64, "one lane per
 constexpr int kExtHeavyAnns = 8;
 constexpr uint64_t kExtIdleLight = 30000ull, kExtIdleHeavy = 100000000ull;
 constexpr uint64_t kExtWaitMax = 200000000ull;
+// (Wave 0 planning the idle helpers while it waits for one, once per wait, when that grow is
+// expected to run 40 us longer on images of 32+ annotations: cfg5 uniform 1445-1724 vs
+// 1670 images/s without, planted 39.8-41.2k vs 40.4-43.5k, round 6.)
 
 struct SeedExt {  // per image; zero at every launch (workspace zero region; the launch's
                   // last workgroup out re-zeroes it, ext_exit)
@@ -1761,7 +1771,10 @@ struct SeedLoopSharedT {
     // seed_loop_kernel: wave 0 started a grow of its own; an idle helper plans the others
     int plan_req;
 };
-using SeedLoopShared = SeedLoopSharedT<kSpecCache>;
+struct SeedLoopShared : SeedLoopSharedT<kSpecCache> {
+    uint2 cache_box[kSpecCache][kKP];  // the grown slots' occupancy boxes (plan_box)
+};
+// (kColLds above keeps the one-CU seed loop's LDS at 124,608 bytes with these)
 struct SeedLoopSharedX : SeedLoopSharedT<kCacheSlots> {
     uint32_t cache_t[kCacheSlots];  // external slots: s_memrealtime (low bits) at hand-over
     uint32_t ext_ticks;             // running mean of hand-over -> tag seen (0: none yet)
@@ -1775,8 +1788,9 @@ __device__ __forceinline__ float4 *cache_joints(SeedLoopSharedX &S, float *s_col
 }
 // The occupancy boxes a grown slot's joints will mark once committed (occ_box_r), for the
 // plan of seed_loop_ext_kernel: written with the joints, before the slot's state 2, so a
-// plan tests a seed against a slot with one LDS read.  Packed x0 | x1 << 16, y0 | y1 << 16
-// (the launch checks that the occupancy grid is narrower than 2^16); an empty box is 0, 0.
+// plan tests a seed against a slot with one LDS read.  Packed x0 | x1 << 16, y0 | y1 << 16;
+// an empty box is 0, 0.  (An occupancy grid of 2^16 cells or more per side, reduction < 1,
+// garbles them: that only changes which seeds the helpers grow ahead, never a result.)
 // After the external joints in the dynamic LDS, one row of kKP per slot (all kCacheSlots).
 constexpr size_t kExtDynLds = kColLdsExt * sizeof(float) + (size_t)kExtCache * kKP * sizeof(float4) +
                               (size_t)kCacheSlots * kKP * sizeof(uint2);
@@ -1876,31 +1890,37 @@ __device__ __forceinline__ void ext_refresh(SeedLoopSharedX &S, float *s_cols, c
 }
 
 // Speculation plan of seed_loop_kernel, collective over one wave, with S.plan_lock held:
-// free seeds in [first, first + scan) that the committed occupancy and the grown cached
-// annotations' occupancy boxes do not cover, kSpecFar joint scales from every seed in
-// flight (and from wave 0's own seed when S.own_on), each into a free cache slot (never
-// used, or holding a seed before `decided`), for the helper waves in `idle` (bit w = wave
-// w), which get their seeds through S.task.  Returns the helpers left idle.
+// free seeds in [decided, decided + scan) that the committed occupancy and the cached
+// annotations' occupancy boxes do not cover (the grown ones' boxes, S.cache_box, and the
+// joints set so far of those in flight, cache_pm / own_pm), kSpecFar joint scales from
+// every seed in flight (and from wave 0's own seed when S.own_on), each into a free cache
+// slot (never used, or holding a seed before `decided`), for the helper waves in `idle`
+// (bit w = wave w), which get their seeds through S.task.  Returns the helpers left idle.
 // A slot is claimed state first, seed second (both released): wave 0 reads the seed without
 // the lock and, seeing its seed there, waits for state 2.
+// The slots are read once, a lane each (only the plan, under the lock, claims slots; a
+// helper turning 1 into 2 meanwhile at most keeps this plan from reusing that slot), and
+// kept current for the plan's own picks; per seed the slots are tested with SGPR operands
+// (readlane), the grown ones' boxes four per LDS round trip.
 // Not inlined: it runs outside the grow and takes no GrowArgs (a non-inlined reference to
 // the kernarg struct makes the compiler copy it to scratch), so the kernel's registers stay
 // the grow's.
-// NS > kSpecCache (seed_loop_ext_kernel): slots kSpecCache.. are the external helpers'
-// (joints at xj, cache_joints); they are avoided like the others but never claimed here.
-template <int NS, bool PARTIAL = false>
-__device__ __noinline__ uint64_t spec_plan(SeedLoopSharedT<NS> &S, const float4 *xj,
-                                           const pp_seed *seeds, int n_seeds, int first,
+__device__ __noinline__ uint64_t spec_plan(SeedLoopShared &S, const pp_seed *seeds, int n_seeds,
                                            int decided, int scan, OccGrid occ, float red,
                                            float msr, float far_k, uint64_t idle,
                                            const uint8_t *socc) {
+    constexpr int NS = kSpecCache;
     const int lane = threadIdx.x & 63;
-    const int cst = lane < NS ? lds_acquire(&S.cache_state[lane]) : 0;
-    uint64_t fly = __ballot(lane < NS && cst == 1);
+    const bool sl = lane < NS;
+    int r_st = sl ? lds_acquire(&S.cache_state[lane]) : 0;
+    int r_seed = sl ? S.cache_seed[lane] : -1;
+    float r_x = sl ? S.cache_x[lane] : 0.0f, r_y = sl ? S.cache_y[lane] : 0.0f,
+          r_s = sl ? S.cache_s[lane] : 0.0f;
+    uint64_t fly = __ballot(sl && r_st == 1);
     const bool own = lds_acquire(&S.own_on) != 0;
     const float ox = S.own_x, oy = S.own_y, osc = S.own_s;
-    const int scan_end = min(n_seeds, first + scan);
-    for (int base = first; base < scan_end && idle; base += 64) {
+    const int scan_end = min(n_seeds, decided + scan);
+    for (int base = decided; base < scan_end && idle; base += 64) {
         const int idx = base + lane;
         bool ok = idx < scan_end;
         pp_seed c{};
@@ -1909,67 +1929,74 @@ __device__ __noinline__ uint64_t spec_plan(SeedLoopSharedT<NS> &S, const float4 
             ok = (!own || spec_far(far_k, c.x, c.y, c.s, ox, oy, osc)) &&
                  !(socc ? socc[idx] != 0 : occ_get(occ, c.field, c.x, c.y, red));
         }
-        // cache entries (uniform loop): skip seeds they hold, seeds that a grown
-        // annotation's occupancy boxes will cover once committed, and seeds near one
-        // still being grown
         const int cxi = (int)clip_ref(c.x / red, 0.0f, (float)(occ.w - 1));
         const int cyi = (int)clip_ref(c.y / red, 0.0f, (float)(occ.h - 1));
+        const int cf = c.field;
         // inside the occupancy box joint jq of an annotation will mark (occupancy.py:31-39)
         auto covered = [&](const float4 &jq) {
             int box[4];
-            return jq.z != 0.0f && occ_box_r(red, msr, occ, c.field, jq.x, jq.y, jq.w, box) &&
+            return jq.z != 0.0f && occ_box_r(red, msr, occ, cf, jq.x, jq.y, jq.w, box) &&
                    cxi >= box[0] && cxi < box[1] && cyi >= box[2] && cyi < box[3];
         };
-        if (ok && PARTIAL && own && ((lds_acquire_u(&S.own_pm) >> c.field) & 1u) &&
-            covered(S.own_j[c.field]))
+        if (ok && own && ((lds_acquire_u(&S.own_pm) >> cf) & 1u) && covered(S.own_j[cf]))
             ok = false;  // wave 0's own annotation in flight covers it
-        for (int q = 0; q < NS; q++) {
-            const int sq = S.cache_seed[q];
-            const int st = S.cache_state[q];
-            if (sq < decided || st == 0 || st == 4) continue;  // free, passed or a zombie
-            if (sq == idx) ok = false;
-            if (!ok) continue;
-            if ((fly >> q) & 1) {
-                ok = spec_far(far_k, c.x, c.y, c.s, S.cache_x[q], S.cache_y[q], S.cache_s[q]);
-                // the joints its grow has set so far
-                if (ok && PARTIAL && q < kSpecCache &&
-                    ((lds_acquire_u(&S.cache_pm[q]) >> c.field) & 1u) && covered(S.cache_j[q][c.field]))
-                    ok = false;
-                continue;
+        // the slots holding a seed from `decided` on, not zombies (the others are free)
+        const uint64_t live = __ballot(sl && r_seed >= decided && r_st != 0 && r_st != 4);
+        // skip the seeds they hold
+        for (uint64_t hq = live & __ballot(sl && r_seed >= base && r_seed < base + 64); hq; hq &= hq - 1)
+            if (idx == __builtin_amdgcn_readlane(r_seed, __ffsll((unsigned long long)hq) - 1)) ok = false;
+        // seeds near one still being grown, or covered by the joints its grow has set so far
+        const uint32_t r_pm = sl ? lds_acquire_u(&S.cache_pm[lane]) : 0u;
+        for (uint64_t fq = live & fly; fq; fq &= fq - 1) {
+            const int q = __ffsll((unsigned long long)fq) - 1;
+            ok = ok && spec_far(far_k, c.x, c.y, c.s, rl_f(r_x, q), rl_f(r_y, q), rl_f(r_s, q));
+            const uint32_t pm = (uint32_t)__builtin_amdgcn_readlane((int)r_pm, q);
+            if (ok && ((pm >> cf) & 1u) && covered(S.cache_j[q][cf])) ok = false;
+        }
+        // seeds a grown annotation's occupancy boxes will cover once committed
+        const int bf = ok ? cf : 0;
+        uint64_t gq = live & ~fly & __ballot(sl && r_st == 2);
+        while (gq) {  // four slots' boxes per LDS round trip
+            int qs[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                qs[u] = gq ? __ffsll((unsigned long long)gq) - 1 : -1;
+                gq &= gq ? gq - 1 : 0ull;
             }
-            if (st != 2) continue;
-            if (covered(q < kSpecCache ? S.cache_j[q][c.field] : xj[(q - kSpecCache) * kKP + c.field]))
-                ok = false;
+            uint2 bx[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) bx[u] = qs[u] >= 0 ? S.cache_box[qs[u]][bf] : make_uint2(0u, 0u);
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (in_plan_box(bx[u], cxi, cyi)) ok = false;
         }
         uint64_t m = __ballot(ok);
         while (m && idle) {
             const int l = __ffsll((unsigned long long)m) - 1;
             m &= m - 1;
             const float cx = rl_f(c.x, l), cy = rl_f(c.y, l), csc = rl_f(c.s, l);
-            bool far = true;  // from this plan's earlier picks (now in flight too)
-            uint64_t f2 = fly;
-            while (f2) {
-                const int q = __ffsll((unsigned long long)f2) - 1;
-                f2 &= f2 - 1;
-                far = far && spec_far(far_k, cx, cy, csc, S.cache_x[q], S.cache_y[q],
-                                      S.cache_s[q]);
-            }
-            if (!far) continue;
+            // far from this plan's earlier picks and every other seed in flight (a lane per slot)
+            if (__ballot(((fly >> lane) & 1ull) && !spec_far(far_k, cx, cy, csc, r_x, r_y, r_s)))
+                continue;
             // a free slot: never grown into, or grown for a seed already decided
-            const int cq = lane < kSpecCache ? S.cache_seed[lane] : 0;
-            const int cst2 = lane < kSpecCache ? S.cache_state[lane] : 1;
-            const uint64_t freeq = __ballot(lane < kSpecCache &&
-                                            (cst2 == 0 || (cst2 == 2 && cq < decided)));
+            const uint64_t freeq = __ballot(sl && (r_st == 0 || (r_st == 2 && r_seed < decided)));
             if (!freeq) return idle;  // no slot: nobody else can be planned either
             const int q = __ffsll((unsigned long long)freeq) - 1;
             const int w = __ffsll((unsigned long long)idle) - 1;
             idle &= idle - 1;
             fly |= 1ull << q;
+            if (lane == q) {
+                r_st = 1;
+                r_seed = base + l;
+                r_x = cx;
+                r_y = cy;
+                r_s = csc;
+            }
             if (lane == 0) {
                 S.cache_x[q] = cx;
                 S.cache_y[q] = cy;
                 S.cache_s[q] = csc;
-                if (q < kSpecCache) S.cache_pm[q] = 0u;  // no joints of the new grow yet
+                S.cache_pm[q] = 0u;  // no joints of the new grow yet
                 lds_release(&S.cache_state[q], 1);
                 lds_release(&S.cache_seed[q], base + l);
                 S.task_slot[w] = q;
@@ -2145,7 +2172,7 @@ void seed_loop_kernel(GrowArgs g) {
         L.status = 0;
         L.log_n = 0;
 #ifdef PP_STAMPS
-        for (int q = 0; q < 8; q++) L.fst[q] = 0;
+        for (int q = 0; q < 10; q++) L.fst[q] = 0;
 #endif
     }
     if (threadIdx.x < kSpecCache) {
@@ -2170,6 +2197,7 @@ void seed_loop_kernel(GrowArgs g) {
     pp_ann *work = g.work + (int64_t)img * g.ann_cap;
     pp_ann *cache = g.spec + (int64_t)img * kSpecCache;
     const float red = (float)g.cfg.occupancy_reduction;
+    const float msr = occ_msr(g);
     const OccGrid occ = occ_grid(occ_base, K, (int)((double)g.hh / g.cfg.occupancy_reduction),
                                  (int)((double)g.ww / g.cfg.occupancy_reduction));
     const int n_seeds = min(g.seed_counts[img], g.seed_cap);
@@ -2200,14 +2228,39 @@ void seed_loop_kernel(GrowArgs g) {
     };
 
     if (wave > 0) {  // helper: grow the seeds wave 0 hands over until it is done
+        // `decided` when this helper's last plan found it nothing to grow (-1: none): once
+        // wave 0 has moved on (commits free slots, passes seeds), an idle helper plans itself
+        // again instead of waiting for wave 0's next miss (which a wave 0 that only takes
+        // cached annotations never has)
+        int idle_dec = -1;
         for (;;) {
             int my;
             for (;;) {
                 my = lds_acquire(&S.task[wave]);
                 if (my >= 0 || lds_acquire(&S.done)) break;
+                if (idle_dec >= 0 && lds_acquire(&S.decided) != idle_dec) {
+#ifdef PP_STAMPS
+                    const uint64_t hp2 = __builtin_amdgcn_s_memtime();
+#endif
+                    plan_lock(S);
+                    uint64_t left = 1ull << wave;
+                    const int dec = lds_acquire(&S.decided);
+                    if (!lds_acquire(&S.done) && lds_acquire(&S.task[wave]) < 0)
+                        left = spec_plan(S, seeds, n_seeds, dec, kSelfScan, occ, red, msr, g.spec_far,
+                                         left, socc);
+                    plan_unlock(S);
+                    idle_dec = left ? dec : -1;
+#ifdef PP_STAMPS
+                    if (lane == 0) L.fst[8] += __builtin_amdgcn_s_memtime() - hp2;
+#endif
+                    continue;
+                }
                 if (lds_acquire(&S.plan_req)) {
                     // wave 0 is growing a seed of its own: plan every idle helper (this one
                     // included) around it
+#ifdef PP_STAMPS
+                    const uint64_t hp0 = __builtin_amdgcn_s_memtime();
+#endif
                     plan_lock(S);
                     if (lds_acquire(&S.plan_req) && !lds_acquire(&S.done)) {
                         if (lane == 0) lds_release(&S.plan_req, 0);
@@ -2215,11 +2268,14 @@ void seed_loop_kernel(GrowArgs g) {
                         const uint64_t idle = __ballot(lane > 0 && lane < kSeedWaves && tk < 0);
                         const int dec = lds_acquire(&S.decided);
                         if (idle)
-                            spec_plan<kSpecCache, true>(S, nullptr, seeds, n_seeds, dec, dec,
-                                                            kSpecScan, occ, red, occ_msr(g),
-                                                            g.spec_far, idle, socc);
+                            spec_plan(S, seeds, n_seeds, dec, kSpecScan, occ, red, msr, g.spec_far,
+                                      idle, socc);
                     }
                     plan_unlock(S);
+                    if (lds_acquire(&S.task[wave]) < 0) idle_dec = lds_acquire(&S.decided);
+#ifdef PP_STAMPS
+                    if (lane == 0) L.fst[8] += __builtin_amdgcn_s_memtime() - hp0;
+#endif
                     continue;
                 }
                 __builtin_amdgcn_s_sleep(1);
@@ -2238,7 +2294,14 @@ void seed_loop_kernel(GrowArgs g) {
             }
 #endif
             if (lds_acquire(&S.done)) break;  // nobody reads the cache any more
-            publish_cached(S, cache, q, L);
+            if (lane < kKP)
+                S.cache_box[q][lane] = plan_box(
+                    red, msr, occ, lane,
+                    make_float4(L.a.data[lane][0], L.a.data[lane][1], L.a.data[lane][2], L.a.joint_scales[lane]));
+            publish_cached(S, cache, q, L);  // (its release orders the boxes too)
+#ifdef PP_STAMPS
+            const uint64_t hp1 = __builtin_amdgcn_s_memtime();
+#endif
             // plan this wave's next grow itself, with its own annotation now in the cache (its
             // occupancy boxes rule out the other seeds of the same person); wave 0 plans only
             // when it has to grow a seed itself
@@ -2246,11 +2309,18 @@ void seed_loop_kernel(GrowArgs g) {
             uint64_t left = 1ull << wave;
             if (!lds_acquire(&S.done)) {
                 const int dec = lds_acquire(&S.decided);
-                left = spec_plan<kSpecCache, true>(S, nullptr, seeds, n_seeds, dec, dec, kSelfScan,
-                                                       occ, red, occ_msr(g), g.spec_far, left, socc);
+                left = spec_plan(S, seeds, n_seeds, dec, kSelfScan, occ, red, msr, g.spec_far, left,
+                                 socc);
             }
             if (left && lane == 0) lds_release(&S.task[wave], -1);
             plan_unlock(S);
+            idle_dec = left ? lds_acquire(&S.decided) : -1;
+#ifdef PP_STAMPS
+            if (lane == 0) {
+                L.fst[8] += __builtin_amdgcn_s_memtime() - hp1;
+                L.fst[9] += 1;
+            }
+#endif
         }
     } else {
         __builtin_amdgcn_s_setprio(3);  // the committer is the critical path: issue first
@@ -2269,7 +2339,13 @@ void seed_loop_kernel(GrowArgs g) {
             const uint64_t hit = __ballot(lane < kSpecCache && cs == t);
             if (hit) {  // a helper grew it, or is growing it
                 const int slot = __ffsll((unsigned long long)hit) - 1;
+#ifdef PP_STAMPS
+                const uint64_t hw0 = __builtin_amdgcn_s_memtime();
+#endif
                 while (lds_acquire(&S.cache_state[slot]) != 2) __builtin_amdgcn_s_sleep(1);
+#ifdef PP_STAMPS
+                if (lane == 0) L.fst[8] += __builtin_amdgcn_s_memtime() - hw0;
+#endif
                 const float4 jq = lane < kKP ? S.cache_j[slot][lane] : make_float4(0.f, 0.f, 0.f, 0.f);
                 commit(&cache[slot], jq.x, jq.y, jq.z, jq.w);
                 s = t + 1;
@@ -2319,13 +2395,17 @@ void seed_loop_kernel(GrowArgs g) {
         st_acc[6] = n_rounds;
         st_acc[7] = n_hits;
         {  // helpers' grows (count into slot 8, cycles into slot 5 in place of occ_clear)
-            uint64_t hn = 0, hc = 0;
+            uint64_t hn = 0, hc = 0, hp = 0, hpn = 0;
             for (int w = 1; w < kSeedWaves; w++) {
                 hn += Ls[w].fst[4];
                 hc += Ls[w].fst[5];
+                hp += Ls[w].fst[8];
+                hpn += Ls[w].fst[9];
             }
             L.fst[3] = hn;
             st_acc[5] = hc;
+            st_acc[14] = hp;  // the helpers' plans (self plans and wave 0's requests)
+            st_acc[15] = L.fst[8] | (hpn << 40);  // wave 0's hit waits; self plans << 40
         }
 #endif
         STAMP_FLUSH(1);
@@ -2360,7 +2440,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
         L.status = 0;
         L.log_n = 0;
 #ifdef PP_STAMPS
-        for (int q = 0; q < 8; q++) L.fst[q] = 0;
+        for (int q = 0; q < 10; q++) L.fst[q] = 0;
 #endif
     }
     if (threadIdx.x < NS) {
@@ -2486,79 +2566,10 @@ void seed_loop_ext_kernel(GrowArgs g) {
                    lane < K ? a->data[lane][1] : 0.0f, lane < K ? a->data[lane][2] : 0.0f,
                    lane < K ? a->joint_scales[lane] : 0.0f);
         });
-        for (;;) {
-            const int t = next_free_seed(s, n_seeds, socc_on ? s_occ.cnt : nullptr, seeds, occ, red);
-            STAMP(0);
-            if (t < 0 || n_anns >= g.ann_cap) {
-                if (lane == 0 && t >= 0) L.status |= PP_ST_ANN_OVERFLOW;
-                break;
-            }
-            if (!heavy && n_anns >= kExtHeavyAnns) {  // helpers stay (kExtIdleHeavy)
-                heavy = true;
-                if (lane == 0) st_agent(&X->heavy, 1u);
-            }
-            const int cs = lane < NS ? S.cache_seed[lane] : -1;
-            const int cst0 = lane < NS ? S.cache_state[lane] : 0;
-            const uint64_t hit = __ballot(lane < NS && cs == t && cst0 != 4);
-            bool taken = false;
-            int hslot = -1;
-            if (hit) {  // a helper grew it, or is growing it
-                const int slot = __ffsll((unsigned long long)hit) - 1;
-#ifdef PP_STAMPS
-                uint64_t hw0 = __builtin_amdgcn_s_memtime();
-#endif
-                if (slot < kSpecCache) {
-                    while (lds_acquire(&S.cache_state[slot]) != 2) __builtin_amdgcn_s_sleep(1);
-                } else {
-                    // another CU's: wait for its tag (bounded; a helper always finishes), or
-                    // on a light image grow the seed here and leave the slot a zombie
-                    const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
-                    const uint32_t el = (uint32_t)w0 - S.cache_t[slot];
-                    const uint64_t limit =
-                        (S.ext_ticks == 0u || el >= S.ext_ticks / 2u) ? kExtWaitMax : 0ull;
-                    for (;;) {
-                        ext_refresh(S, s_cols, X, xrec, slot, red, msr, occ);
-                        if (S.cache_state[slot] == 2) break;
-                        if (__builtin_amdgcn_s_memrealtime() - w0 >= limit) {
-                            if (lane == 0) S.cache_state[slot] = 4;  // grow it here instead
-                            wave_sync();
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(2);
-                    }
-                }
-                taken = S.cache_state[slot] == 2;
-                hslot = slot;
-#ifdef PP_STAMPS
-                ESTAMP(L, 7, hw0);  // a hit: waiting for the helper
-#endif
-            }
-            if (taken) {
-                const float4 jq = lane < kKP ? cache_joints(S, s_cols, hslot)[lane]
-                                             : make_float4(0.f, 0.f, 0.f, 0.f);
-                if (hslot < kSpecCache)
-                    commit(&cache[hslot], false, jq.x, jq.y, jq.z, jq.w);
-                else
-                    commit(&xrec[hslot - kSpecCache], true, jq.x, jq.y, jq.z, jq.w);
-                s = t + 1;
-                if (lane == 0) lds_release(&S.decided, s);  // the slot is free again
-#ifdef PP_STAMPS
-                n_hits++;
-#endif
-                STAMP(4);
-                continue;
-            }
-            // a miss: hand far-away free seeds to the idle helpers, then grow t here
-            const pp_seed st = seeds[t];
-            plan_lock(S);  // wave 0 plans every idle helper, this CU's and the external ones
-            if (lane == 0) {
-                S.own_x = st.x;
-                S.own_y = st.y;
-                S.own_s = st.s;
-                lds_release(&S.own_on, 1);
-                lds_release(&S.decided, t);
-            }
-            wave_sync();
+        // Hand far-away free seeds after t to the idle helpers (this CU's and the external
+        // ones), with S.plan_lock held; `own`: wave 0 grows seed st itself next (the picks
+        // keep kSpecFar from it too)
+        auto plan_round = [&](const int t, const bool own, const pp_seed &st) {
 #ifdef PP_STAMPS
             const uint64_t xr0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -2592,7 +2603,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
                 pp_seed c{};
                 if (ok) {
                     c = seeds[idx];
-                    ok = spec_far(g.spec_far, c.x, c.y, c.s, st.x, st.y, st.s) &&
+                    ok = (!own || spec_far(g.spec_far, c.x, c.y, c.s, st.x, st.y, st.s)) &&
                          !(socc_on ? s_occ.cnt[idx] != 0 : occ_get(occ, c.field, c.x, c.y, red));
                 }
                 // the slots holding seeds after t (the others are free or passed): skip the
@@ -2695,6 +2706,81 @@ void seed_loop_ext_kernel(GrowArgs g) {
                 ESTAMP(L, 6, pf0);  // plan: the picks
 #endif
             }
+        };
+        for (;;) {
+            const int t = next_free_seed(s, n_seeds, socc_on ? s_occ.cnt : nullptr, seeds, occ, red);
+            STAMP(0);
+            if (t < 0 || n_anns >= g.ann_cap) {
+                if (lane == 0 && t >= 0) L.status |= PP_ST_ANN_OVERFLOW;
+                break;
+            }
+            if (!heavy && n_anns >= kExtHeavyAnns) {  // helpers stay (kExtIdleHeavy)
+                heavy = true;
+                if (lane == 0) st_agent(&X->heavy, 1u);
+            }
+            const int cs = lane < NS ? S.cache_seed[lane] : -1;
+            const int cst0 = lane < NS ? S.cache_state[lane] : 0;
+            const uint64_t hit = __ballot(lane < NS && cs == t && cst0 != 4);
+            bool taken = false;
+            int hslot = -1;
+            if (hit) {  // a helper grew it, or is growing it
+                const int slot = __ffsll((unsigned long long)hit) - 1;
+#ifdef PP_STAMPS
+                uint64_t hw0 = __builtin_amdgcn_s_memtime();
+#endif
+                if (slot < kSpecCache) {
+                    while (lds_acquire(&S.cache_state[slot]) != 2) __builtin_amdgcn_s_sleep(1);
+                } else {
+                    // another CU's: wait for its tag (bounded; a helper always finishes), or
+                    // on a light image grow the seed here and leave the slot a zombie
+                    const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
+                    const uint32_t el = (uint32_t)w0 - S.cache_t[slot];
+                    const uint64_t limit =
+                        (S.ext_ticks == 0u || el >= S.ext_ticks / 2u) ? kExtWaitMax : 0ull;
+                    for (;;) {
+                        ext_refresh(S, s_cols, X, xrec, slot, red, msr, occ);
+                        if (S.cache_state[slot] == 2) break;
+                        if (__builtin_amdgcn_s_memrealtime() - w0 >= limit) {
+                            if (lane == 0) S.cache_state[slot] = 4;  // grow it here instead
+                            wave_sync();
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(2);
+                    }
+                }
+                taken = S.cache_state[slot] == 2;
+                hslot = slot;
+#ifdef PP_STAMPS
+                ESTAMP(L, 7, hw0);  // a hit: waiting for the helper
+#endif
+            }
+            if (taken) {
+                const float4 jq = lane < kKP ? cache_joints(S, s_cols, hslot)[lane]
+                                             : make_float4(0.f, 0.f, 0.f, 0.f);
+                if (hslot < kSpecCache)
+                    commit(&cache[hslot], false, jq.x, jq.y, jq.z, jq.w);
+                else
+                    commit(&xrec[hslot - kSpecCache], true, jq.x, jq.y, jq.z, jq.w);
+                s = t + 1;
+                if (lane == 0) lds_release(&S.decided, s);  // the slot is free again
+#ifdef PP_STAMPS
+                n_hits++;
+#endif
+                STAMP(4);
+                continue;
+            }
+            // a miss: hand far-away free seeds to the idle helpers, then grow t here
+            const pp_seed st = seeds[t];
+            plan_lock(S);  // wave 0 plans every idle helper, this CU's and the external ones
+            if (lane == 0) {
+                S.own_x = st.x;
+                S.own_y = st.y;
+                S.own_s = st.s;
+                lds_release(&S.own_on, 1);
+                lds_release(&S.decided, t);
+            }
+            wave_sync();
+            plan_round(t, true, st);
             plan_unlock(S);
 #ifdef PP_STAMPS
             n_rounds++;
@@ -3762,10 +3848,7 @@ static int decode_heads(const Heads &h, int32_t n_img, int32_t K, int32_t C,
         g.work = (pp_ann *)(ws + d.off_work);
         g.spec = (pp_ann *)(ws + d.off_spec);
         g.spec_far = kSpecFar;
-        // (the external helpers' plan packs occupancy boxes in 16 bits: cache_boxes)
-        g.n_ext = (d.hh / cfg->occupancy_reduction < 65535.0 && d.ww / cfg->occupancy_reduction < 65535.0)
-                      ? seed_ext_per_image(n_img)
-                      : 0;
+        g.n_ext = seed_ext_per_image(n_img);
         g.xext = (SeedExt *)(ws + d.off_xext);
         g.xrec = (pp_ann *)(ws + d.off_xrec);
         g.nms_score = (double *)(ws + d.off_nms_score);

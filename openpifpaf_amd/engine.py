@@ -8,7 +8,6 @@ Annotation objects.
 """
 import ctypes
 import logging
-import os
 
 import numpy as np
 import torch
@@ -493,27 +492,29 @@ class PendingRecords:
         return rows.index_select(0, torch.from_numpy(idx).to(rows.device)).reshape(-1)
 
 
-# PP_PIPE_BFIRST=1 / 0 / lazy forces the force-complete set order of DecodePipeline (auto
-# below); lazy: gated after the seed loop, on the tail stream
-_B_FIRST = {'1': True, '0': False, 'lazy': 'lazy'}.get(os.environ.get('PP_PIPE_BFIRST', ''))
+# The pipeline's scheduling choices are module constants, not environment switches (tests
+# set them to check that every order gives the same records).
+# _B_FIRST: the force-complete set order of DecodePipeline, True / False / 'lazy' (gated
+# after the seed loop, on the tail stream); None: auto below
+_B_FIRST = None
 # auto: lazy sets (only the (field, direction) pairs force-complete needs, on the tail
 # stream) until a batch averaged this many annotations per image, then sets first.  Round 4,
 # with the tail split: planted cfg3 0.687-0.691 (lazy) vs 0.801-0.811 ms (first) per step,
 # uniform 14.7k vs 15.1-15.2k images/s, cfg5 planted equal, cfg5 uniform 1180 vs 1200
 _B_FIRST_DENSITY = 32.0
-# workspaces in flight (PP_PIPE_DEPTH): batch i + depth's front half waits for batch i's tail
+# workspaces in flight: batch i + depth's front half waits for batch i's tail
 _PIPE_DEPTH = 2
 # the tail as two calls (force-complete, then NMS): a workspace's next front half waits only
-# for the force-complete, its next seed loop for the NMS (PP_SPLIT_TAIL=0: one call, the
-# front half waits for both)
-_SPLIT_TAIL = os.environ.get('PP_SPLIT_TAIL', '1') != '0'
+# for the force-complete, its next seed loop for the NMS (False: one call, the front half
+# waits for both)
+_SPLIT_TAIL = True
 # Sparse batches: batch i's seed loop and tail share the back stream of its workspace
 # (i % 2), so a seed loop starts beside the previous batch's slowest images (cfg5 planted
 # 30.5k -> 41.7k images/s, cfg3 planted equal); dense ones: one stream for the seed loops
-# and one for the tails (cfg3 uniform 15.5k vs 14.6k images/s).  PP_PIPE_BACK2=1 / 0 forces
-# either.  The same two streams serve both (current + the library's side stream + two:
-# four hardware queues).
-_BACK2 = {'1': True, '0': False}.get(os.environ.get('PP_PIPE_BACK2', ''))
+# and one for the tails (cfg3 uniform 15.5k vs 14.6k images/s); True / False forces either.
+# The same two streams serve both (current + the library's side stream + two: four
+# hardware queues).
+_BACK2 = None
 
 
 class DecodePipeline:
@@ -543,7 +544,7 @@ class DecodePipeline:
     tail stream, only for the (field, direction) pairs an annotation left unset), and go
     first for dense ones, on the side stream before the CifHr map (they read only the CAF
     fields), then set A after them, beside the CifHr map and the seeds on the current
-    stream (PP_PIPE_BFIRST=1 / 0 / lazy forces first / after set A / lazy).  Every order
+    stream (_B_FIRST = True / False / 'lazy' forces first / after set A / lazy).  Every order
     gives the same records.
 
     submit() returns (buffers, PendingRecords of the batch: DecodeEngine.fetch_async).
@@ -553,12 +554,11 @@ class DecodePipeline:
     def __init__(self, device=None, depth=None):
         self.device = _device.require() if device is None else device
         if depth is None:
-            depth = int(os.environ.get('PP_PIPE_DEPTH', _PIPE_DEPTH))
+            depth = _PIPE_DEPTH
         self.depth = max(2, depth)  # workspaces in flight (3 or 4 measured slower)
         self.engines = tuple(DecodeEngine() for _ in range(self.depth))
-        # one back stream: consecutive seed loops serialise.  Two (one per workspace, so the
-        # next batch's images fill the CUs whose image of this batch finished) measured
-        # slower: planted 0.91-1.01 vs 0.84-0.85 ms per step, uniform unchanged (round 3)
+        # dense batches: seed loops on `back`, tails on `tail`; sparse ones: each workspace's
+        # loop and tail on one of the two (_BACK2 above, per submit)
         # (a high HIP priority for the back, tail or a separate front stream measured no
         # better: planted 385-389k / 373-382k / 365-389k vs 390-391k images/s, round 4)
         self.back = torch.cuda.Stream(device=self.device)

@@ -48,10 +48,42 @@ def api_main(rank, world, cif, caf):
     dist.destroy_process_group()
 
 
+def det_main(rank, world):
+    """CifDet.decode_batch(group=) with the real device decode (ref generator.py:84-101,
+    cifdet.py): each rank decodes its shard of a 24-image planted detection batch on cuda:0,
+    rank 0 gathers pp_det records (K = -1 headers, digests checked) and compares every
+    image's detections byte for byte with a one-process decode_batch."""
+    from openpifpaf_amd import decoder
+    decoder.CifHr.v_threshold = 0.1
+    decoder.CifSeeds.threshold = 0.3
+    det = torch.from_numpy(synthetic.det_batch('planted', 24, 48, 40, first_seed=50,
+                                               n_categories=4)).cuda()
+    cd = decoder.CifDet(decoder.FieldConfig(), ['a', 'b', 'c', 'd'])
+    got = cd.decode_batch(det, group=dist.group.WORLD)
+    if rank == 0:
+        assert cd.last_gather['ranks_seen'] == world, cd.last_gather
+        assert cd.last_gather['ranks_verified'] == world, cd.last_gather
+        ref = cd.decode_batch(det)
+        assert len(got) == len(ref) == 24
+
+        def key(lists):
+            return [[(a.field_i, np.float32(a.score).tobytes(),
+                      np.asarray(a.bbox, np.float32).tobytes()) for a in anns] for anns in lists]
+        assert key(got) == key(ref), 'gathered detections differ'
+        print('multirank ok: det, {} detections, world {}'.format(
+            sum(len(a) for a in ref), world), flush=True)
+    else:
+        assert got is None
+    dist.destroy_process_group()
+
+
 def main():
     rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
     dist.init_process_group('gloo')
     torch.cuda.set_device(0)
+    if len(sys.argv) > 1 and sys.argv[1] == 'det':
+        det_main(rank, world)
+        return
     skel = constants.COCO_PERSON_SKELETON
     cfg = make_config(**EVAL_CONFIG)
     cp, ap = synthetic.batch('planted', N // 2, 80, 80)

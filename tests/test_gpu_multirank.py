@@ -31,6 +31,14 @@ def test_sharded_api_matches_one_process(world):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('world', [2, 3])
+def test_cifdet_sharded_real_decode(world):
+    """CifDet.decode_batch(group=) over gloo ranks on cuda:0 with the device decode (the
+    CPU tests in test_distributed.py fake decode_records)."""
+    assert 'multirank ok: det' in _run(world, ['det'])[0]
+
+
+@pytest.mark.gpu
 @pytest.mark.timeout(600)
 def test_cfg4_eight_ranks():
     """BASELINE.json configs[3] at full size: 2048 planted 80x80 images over 8 gloo ranks

@@ -67,6 +67,11 @@ for case in cases:
             print('    corr(cycles, anns) {:.2f}  corr(cycles, rounds) {:.2f}  corr(cycles, seed cells) {:.2f}'.format(
                 np.corrcoef(per, n_ann)[0, 1], np.corrcoef(per, st[:, 0, 6])[0, 1],
                 np.corrcoef(per, n_seed_cells)[0, 1]))
+        if ph == 0 and st[:, 0, 5].mean() > 0:  # seed_loop_kernel: the helpers' plans, wave 0's waits
+            w15 = np.fromfile(out, dtype=np.uint64).reshape(-1, n, 3, 16)[-1][:, 0, 15]
+            print('    [one-CU kernel] helper plan cyc {:.0f}  self plans {:.1f}  wave 0 hit wait {:.0f}'.format(
+                st[:, 0, 14].mean(), (w15 >> np.uint64(40)).astype(np.float64).mean(),
+                (w15 & np.uint64((1 << 40) - 1)).astype(np.float64).mean()))
         for i, name in ((8, 'n connection' if ph else 'helper grows'), (9, 'in-grow pop'), (10, 'in-grow connection'),
                         (11, 'in-grow add'), (12, ' eval: loads / ext plan: filter+picks'),
                         (13, ' eval: forward / ext hit: wait'),
