@@ -874,10 +874,10 @@ __device__ __forceinline__ void flat_load(const float *__restrict__ cf, int64_t 
 // that fits kColLds floats, in (CAF, direction) order, column-major (kColPad floats per
 // column: two 16-byte reads).  cofs[q] = its offset, -1 = global.
 constexpr int kColPad = 8;
-// 77 KB (64 KB: 1-2% slower per planted cfg3 step).  With the seed loop's static LDS this
+// 74.5 KB (64 KB: 1-2% slower per planted cfg3 step).  With the seed loop's static LDS this
 // leaves 39 KB of the CU's 160 KB for the next batch's kernels (DecodePipeline): CafScored
 // (caf_bucketed_kernel, 37 KB) must fit beside it (3 KB less: uniform cfg3 4% slower).
-constexpr int kColLds = 19712;
+constexpr int kColLds = 19072;
 // the external-helper kernel (seed_loop_ext_kernel: images with helpers on other CUs, e.g.
 // cfg5) stages 48 KB: the LDS it leaves lets the other batch's kernels share its CUs (cfg5
 // uniform 1452-1473 -> 1583-1585 images/s, planted 41.3k -> 43.1k-43.7k; 80 KB for the
@@ -1432,28 +1432,29 @@ __device__ __forceinline__ void occ_mark(const GrowArgs &g, LDS &L, OccLog *log,
 // joint's box, and a seed is occupied iff its counter is nonzero -- exactly the grid's
 // cell value there.  Marks and tests stay in LDS: no global read-modify-write, no clearing.
 constexpr int kOccSeeds = 2560;
+// Counters, cells and fields are stored by the seeds' position p in field-grouped order (pos:
+// seed index -> p), so that a mark reads one seed's cell, field and counter in one LDS round
+// trip, four seeds per lane at once, over all the marked joints' fields in one sweep.
 struct SeedOcc {
-    uint8_t cnt[kOccSeeds];     // counter per seed index
-    uint32_t cell[kOccSeeds];   // grid cell (yi << 16 | xi) per seed index
-    uint16_t byf[kOccSeeds];    // seed indices grouped by field
-    int foff[kKP + 1];          // field f's group: byf[foff[f] .. foff[f + 1])
+    uint8_t cnt[kOccSeeds];     // counter per position
+    uint8_t fld[kOccSeeds];     // field per position
+    uint32_t cell[kOccSeeds];   // grid cell (yi << 16 | xi) per position
+    uint16_t pos[kOccSeeds];    // position of each seed index
+    int foff[kKP + 1];          // field f's positions: foff[f] .. foff[f + 1]
     int fcur[kKP];
+    int n;
 };
+
+__device__ __forceinline__ bool seed_occupied(const SeedOcc &O, int idx) { return O.cnt[O.pos[idx]] != 0; }
 
 // collective over the workgroup (ends with a barrier): the counters and field groups of
 // the image's n <= kOccSeeds seeds
 __device__ __forceinline__ void seed_occ_init(SeedOcc &O, const pp_seed *seeds, int n, int K,
                                               const OccGrid &o, float red) {
     if (threadIdx.x < kKP) O.fcur[threadIdx.x] = 0;
+    if (threadIdx.x == 0) O.n = n;
     __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const pp_seed c = seeds[i];
-        const int xi = (int)clip_ref(c.x / red, 0.0f, (float)(o.w - 1));  // occ_get's cell
-        const int yi = (int)clip_ref(c.y / red, 0.0f, (float)(o.h - 1));
-        O.cell[i] = ((uint32_t)yi << 16) | (uint32_t)xi;
-        O.cnt[i] = 0;
-        atomicAdd(&O.fcur[c.field], 1);
-    }
+    for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&O.fcur[seeds[i].field], 1);
     __syncthreads();
     if (threadIdx.x == 0) {
         int a = 0;
@@ -1466,28 +1467,51 @@ __device__ __forceinline__ void seed_occ_init(SeedOcc &O, const pp_seed *seeds, 
     }
     __syncthreads();
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const int f = seeds[i].field;
-        O.byf[O.foff[f] + atomicAdd(&O.fcur[f], 1)] = (uint16_t)i;
+        const pp_seed c = seeds[i];
+        const int xi = (int)clip_ref(c.x / red, 0.0f, (float)(o.w - 1));  // occ_get's cell
+        const int yi = (int)clip_ref(c.y / red, 0.0f, (float)(o.h - 1));
+        const int p = O.foff[c.field] + atomicAdd(&O.fcur[c.field], 1);
+        O.pos[i] = (uint16_t)p;
+        O.cell[p] = ((uint32_t)yi << 16) | (uint32_t)xi;
+        O.fld[p] = (uint8_t)c.field;
+        O.cnt[p] = 0;
     }
     __syncthreads();
 }
 
-// occ_mark on the counters (one wave): lane j < K holds joint j (x, y, scale, `on`)
+// occ_mark on the counters (one wave): lane j < K holds joint j (x, y, scale, `on`).  Each
+// position is one seed of one field, so a sweep touches every counter at most once (no
+// races between lanes); a seed whose field's joint is marked gets +1 if its cell is in the
+// joint's box (the box from lane `field`, ds_bpermute).
 __device__ __forceinline__ void seed_occ_mark(const GrowArgs &g, SeedOcc &O, const OccGrid &o,
                                               float jx, float jy, float js, bool on, int K) {
     const int lane = threadIdx.x & 63;
     int box[4] = {0, 0, 0, 0};
     const bool has = lane < K && on && occ_box(g, o, lane, jx, jy, js, box);
     const uint64_t hm = __ballot(has);
-    for (uint64_t m = hm; m; m &= m - 1) {
-        const int j = __ffsll((unsigned long long)m) - 1;
-        const int x0 = rl_i(box[0], j), x1 = rl_i(box[1], j);
-        const int y0 = rl_i(box[2], j), y1 = rl_i(box[3], j);
-        for (int i = O.foff[j] + lane; i < O.foff[j + 1]; i += 64) {
-            const int sd = O.byf[i];
-            const uint32_t c = O.cell[sd];
-            const int xi = (int)(c & 0xFFFFu), yi = (int)(c >> 16);
-            if (xi >= x0 && xi < x1 && yi >= y0 && yi < y1) O.cnt[sd] = (uint8_t)(O.cnt[sd] + 1);
+    if (hm) {
+        const int n = O.n;
+        constexpr int kU = 4;
+        for (int p0 = 0; p0 < n; p0 += 64 * kU) {
+            uint32_t c[kU];
+            int f[kU], v[kU];
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                const int p = p0 + u * 64 + lane;
+                const bool in = p < n;
+                c[u] = in ? O.cell[p] : 0u;
+                f[u] = in ? (int)O.fld[p] : 0;
+                v[u] = in ? (int)O.cnt[p] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                const int p = p0 + u * 64 + lane;
+                const int x0 = __shfl(box[0], f[u]), x1 = __shfl(box[1], f[u]);
+                const int y0 = __shfl(box[2], f[u]), y1 = __shfl(box[3], f[u]);
+                const int xi = (int)(c[u] & 0xFFFFu), yi = (int)(c[u] >> 16);
+                if (p < n && ((hm >> f[u]) & 1ull) && xi >= x0 && xi < x1 && yi >= y0 && yi < y1)
+                    O.cnt[p] = (uint8_t)(v[u] + 1);
+            }
         }
     }
     wave_sync();
@@ -1774,7 +1798,7 @@ struct SeedLoopSharedT {
 struct SeedLoopShared : SeedLoopSharedT<kSpecCache> {
     uint2 cache_box[kSpecCache][kKP];  // the grown slots' occupancy boxes (plan_box)
 };
-// (kColLds above keeps the one-CU seed loop's LDS at 124,608 bytes with these)
+// (kColLds above keeps the one-CU seed loop's LDS at 124,608 bytes with these and SeedOcc)
 struct SeedLoopSharedX : SeedLoopSharedT<kCacheSlots> {
     uint32_t cache_t[kCacheSlots];  // external slots: s_memrealtime (low bits) at hand-over
     uint32_t ext_ticks;             // running mean of hand-over -> tag seen (0: none yet)
@@ -1908,7 +1932,7 @@ __device__ __forceinline__ void ext_refresh(SeedLoopSharedX &S, float *s_cols, c
 __device__ __noinline__ uint64_t spec_plan(SeedLoopShared &S, const pp_seed *seeds, int n_seeds,
                                            int decided, int scan, OccGrid occ, float red,
                                            float msr, float far_k, uint64_t idle,
-                                           const uint8_t *socc) {
+                                           const SeedOcc *socc) {
     constexpr int NS = kSpecCache;
     const int lane = threadIdx.x & 63;
     const bool sl = lane < NS;
@@ -1927,7 +1951,7 @@ __device__ __noinline__ uint64_t spec_plan(SeedLoopShared &S, const pp_seed *see
         if (ok) {
             c = seeds[idx];
             ok = (!own || spec_far(far_k, c.x, c.y, c.s, ox, oy, osc)) &&
-                 !(socc ? socc[idx] != 0 : occ_get(occ, c.field, c.x, c.y, red));
+                 !(socc ? seed_occupied(*socc, idx) : occ_get(occ, c.field, c.x, c.y, red));
         }
         const int cxi = (int)clip_ref(c.x / red, 0.0f, (float)(occ.w - 1));
         const int cyi = (int)clip_ref(c.y / red, 0.0f, (float)(occ.h - 1));
@@ -2069,7 +2093,7 @@ __device__ __forceinline__ ColStage stage_small_sets(const GrowArgs &g, int img,
 // The next free seed from index s on (cifcaf.py:100-104), 64 occupancy tests per step (the
 // per-seed LDS counters `socc`, or the global grid); -1 when none is left.  s advances past
 // the all-occupied steps.  Wave 0.
-__device__ __forceinline__ int next_free_seed(int &s, int n_seeds, const uint8_t *socc,
+__device__ __forceinline__ int next_free_seed(int &s, int n_seeds, const SeedOcc *socc,
                                               const pp_seed *seeds, const OccGrid &occ,
                                               float red) {
     const int lane = threadIdx.x & 63;
@@ -2078,7 +2102,7 @@ __device__ __forceinline__ int next_free_seed(int &s, int n_seeds, const uint8_t
         bool is_free = false;
         if (idx < n_seeds) {
             if (socc) {
-                is_free = socc[idx] == 0;
+                is_free = !seed_occupied(*socc, idx);
             } else {
                 const pp_seed c = seeds[idx];
                 is_free = !occ_get(occ, c.field, c.x, c.y, red);
@@ -2205,7 +2229,7 @@ void seed_loop_kernel(GrowArgs g) {
     // the occupancy at the seeds in LDS (seed_occ_*), or the global grid for more seeds
     const bool socc_on = n_seeds <= kOccSeeds;
     if (socc_on) seed_occ_init(s_occ, seeds, n_seeds, K, occ, red);
-    const uint8_t *socc = socc_on ? s_occ.cnt : nullptr;
+    const SeedOcc *socc = socc_on ? &s_occ : nullptr;
 
     // committer state (wave 0)
     int n_anns = 0, s = 0;
@@ -2217,7 +2241,13 @@ void seed_loop_kernel(GrowArgs g) {
     // append one finished annotation and mark_occupied (cifcaf.py:87-93): wave 0 only
     // (lane j < K holds joint j of the record: x, y, v, scale, from LDS)
     auto commit = [&](const pp_ann *src, float jx, float jy, float jv, float js) {
+#ifdef PP_STAMPS
+        uint64_t ct0 = __builtin_amdgcn_s_memtime();
+#endif
         copy_ann(&work[n_anns], src);
+#ifdef PP_STAMPS
+        ESTAMP(L, 4, ct0);  // (wave 0) the record copy
+#endif
         n_anns++;
         const uint32_t set = (uint32_t)__ballot(lane < K && jv > 0.0f);
         unset_mask |= ~set & (K >= 32 ? 0xFFFFFFFFu : ((1u << K) - 1u));
@@ -2225,6 +2255,9 @@ void seed_loop_kernel(GrowArgs g) {
             seed_occ_mark(g, s_occ, occ, jx, jy, js, jv != 0.0f, K);
         else
             occ_mark(g, L, log, occ, jx, jy, js, jv != 0.0f, K);
+#ifdef PP_STAMPS
+        ESTAMP(L, 5, ct0);  // (wave 0) the occupancy marks
+#endif
     };
 
     if (wave > 0) {  // helper: grow the seeds wave 0 hands over until it is done
@@ -2329,7 +2362,7 @@ void seed_loop_kernel(GrowArgs g) {
                    lane < K ? a->data[lane][2] : 0.0f, lane < K ? a->joint_scales[lane] : 0.0f);
         });
         for (;;) {
-            const int t = next_free_seed(s, n_seeds, socc_on ? s_occ.cnt : nullptr, seeds, occ, red);
+            const int t = next_free_seed(s, n_seeds, socc_on ? &s_occ : nullptr, seeds, occ, red);
             STAMP(0);
             if (t < 0 || n_anns >= g.ann_cap) {
                 if (lane == 0 && t >= 0) L.status |= PP_ST_ANN_OVERFLOW;
@@ -2406,6 +2439,8 @@ void seed_loop_kernel(GrowArgs g) {
             st_acc[5] = hc;
             st_acc[14] = hp;  // the helpers' plans (self plans and wave 0's requests)
             st_acc[15] = L.fst[8] | (hpn << 40);  // wave 0's hit waits; self plans << 40
+            L.fst[6] = L.fst[4];  // (diagnostic: wave 0's copy / mark cycles in slots 12 / 13)
+            L.fst[7] = L.fst[5];
         }
 #endif
         STAMP_FLUSH(1);
@@ -2604,7 +2639,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
                 if (ok) {
                     c = seeds[idx];
                     ok = (!own || spec_far(g.spec_far, c.x, c.y, c.s, st.x, st.y, st.s)) &&
-                         !(socc_on ? s_occ.cnt[idx] != 0 : occ_get(occ, c.field, c.x, c.y, red));
+                         !(socc_on ? seed_occupied(s_occ, idx) : occ_get(occ, c.field, c.x, c.y, red));
                 }
                 // the slots holding seeds after t (the others are free or passed): skip the
                 // seeds they hold, seeds near one still being grown, and seeds that a grown
@@ -2708,7 +2743,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
             }
         };
         for (;;) {
-            const int t = next_free_seed(s, n_seeds, socc_on ? s_occ.cnt : nullptr, seeds, occ, red);
+            const int t = next_free_seed(s, n_seeds, socc_on ? &s_occ : nullptr, seeds, occ, red);
             STAMP(0);
             if (t < 0 || n_anns >= g.ann_cap) {
                 if (lane == 0 && t >= 0) L.status |= PP_ST_ANN_OVERFLOW;
