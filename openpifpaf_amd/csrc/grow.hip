@@ -1565,6 +1565,31 @@ __device__ double pw_sum(const double *a, int K) {
 
 // all loads first, then all stores: one round trip (the two records may alias as far as the
 // compiler knows, so a plain copy loop waits for every load in turn)
+// a record copy in two halves, so that other work overlaps the loads' latency: the loads
+// into registers (per lane kAnnWords words), then the stores
+constexpr int kAnnWords = (int)((sizeof(pp_ann) / 4 + 63) / 64);
+struct AnnRegs {
+    uint32_t v[kAnnWords];
+};
+__device__ __forceinline__ AnnRegs ann_load(const pp_ann *src) {
+    const uint32_t *s = reinterpret_cast<const uint32_t *>(src);
+    constexpr int nw = sizeof(pp_ann) / 4;
+    const int lane = threadIdx.x & 63;
+    AnnRegs r;
+#pragma unroll
+    for (int u = 0; u < kAnnWords; u++) r.v[u] = (u * 64 + lane < nw) ? s[u * 64 + lane] : 0u;
+    return r;
+}
+__device__ __forceinline__ void ann_store(pp_ann *dst, const AnnRegs &r) {
+    uint32_t *d = reinterpret_cast<uint32_t *>(dst);
+    constexpr int nw = sizeof(pp_ann) / 4;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int u = 0; u < kAnnWords; u++)
+        if (u * 64 + lane < nw) d[u * 64 + lane] = r.v[u];
+    wave_sync();
+}
+
 __device__ __forceinline__ void copy_ann(pp_ann *dst, const pp_ann *src) {
     const uint32_t *s = reinterpret_cast<const uint32_t *>(src);
     uint32_t *d = reinterpret_cast<uint32_t *>(dst);
@@ -2240,15 +2265,13 @@ void seed_loop_kernel(GrowArgs g) {
 
     // append one finished annotation and mark_occupied (cifcaf.py:87-93): wave 0 only
     // (lane j < K holds joint j of the record: x, y, v, scale, from LDS)
+    // (the record's loads are issued first and stored after the marks: the marks hide
+    // their latency)
     auto commit = [&](const pp_ann *src, float jx, float jy, float jv, float js) {
 #ifdef PP_STAMPS
         uint64_t ct0 = __builtin_amdgcn_s_memtime();
 #endif
-        copy_ann(&work[n_anns], src);
-#ifdef PP_STAMPS
-        ESTAMP(L, 4, ct0);  // (wave 0) the record copy
-#endif
-        n_anns++;
+        const AnnRegs rec = ann_load(src);
         const uint32_t set = (uint32_t)__ballot(lane < K && jv > 0.0f);
         unset_mask |= ~set & (K >= 32 ? 0xFFFFFFFFu : ((1u << K) - 1u));
         if (socc_on)
@@ -2257,6 +2280,11 @@ void seed_loop_kernel(GrowArgs g) {
             occ_mark(g, L, log, occ, jx, jy, js, jv != 0.0f, K);
 #ifdef PP_STAMPS
         ESTAMP(L, 5, ct0);  // (wave 0) the occupancy marks
+#endif
+        ann_store(&work[n_anns], rec);
+        n_anns++;
+#ifdef PP_STAMPS
+        ESTAMP(L, 4, ct0);  // (wave 0) the record's stores (after the marks)
 #endif
     };
 
