@@ -63,6 +63,8 @@ def parse():
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--no-uniform', action='store_true',
                    help='skip the uniform-generator line added to the default run')
+    p.add_argument('--no-predict', action='store_true',
+                   help='skip the predict-defaults line added to the default run')
     p.add_argument('--no-multi', action='store_true',
                    help='skip the multi-scale (pp_decode_multi) lines added to the default run')
     p.add_argument('--backend', default='nccl', choices=('nccl', 'gloo'),
@@ -204,10 +206,12 @@ def main():
     gather = {'steps': 0, 'verified_steps': 0, 'ranks_seen': world, 'full_record_steps': 0,
               'bytes': 0}
 
-    def timed_run(cif, caf, steps, warmup, heads=None, skel=None, n_stages=None):
+    def timed_run(cif, caf, steps, warmup, heads=None, skel=None, n_stages=None, run_cfg=None):
         """warmup + `steps` timed decode steps of one resident batch (cif / caf, or a
-        multi-scale HeadSet): (elapsed s, max over ranks; per-group event ms per step;
-        annotations decoded, on rank 0 those of all ranks)."""
+        multi-scale HeadSet) under `run_cfg` (default: the line's config): (elapsed s, max
+        over ranks; per-group event ms per step; annotations decoded, on rank 0 those of all
+        ranks)."""
+        cfg_r = cfg if run_cfg is None else run_cfg
         skel = skeleton if skel is None else skel
         n_stages = stages if n_stages is None else n_stages
         k_img = heads.k if heads is not None else cif.shape[1]
@@ -223,7 +227,7 @@ def main():
             """Enqueue one decode and its record fetch; returns (PendingRecords, events)."""
             ev = ev_sets[k % len(ev_sets)]
             if pipe is not None and n_stages == 15:
-                b, pending = pipe.submit(cif, caf, skel, cfg, heads=heads, compact=compact,
+                b, pending = pipe.submit(cif, caf, skel, cfg_r, heads=heads, compact=compact,
                                          device_out=world > 1 and rank != 0,
                                          events=ev if timed else None)
                 return b, (pending, ev)
@@ -232,9 +236,9 @@ def main():
                 if timed:
                     ev[si].record(stream)
                 if n_stages & bits and heads is not None:
-                    b = eng.launch_multi(heads, skel, cfg, stages=n_stages & bits)
+                    b = eng.launch_multi(heads, skel, cfg_r, stages=n_stages & bits)
                 elif n_stages & bits:
-                    b = eng.launch(cif, caf, skel, cfg, stages=n_stages & bits)
+                    b = eng.launch(cif, caf, skel, cfg_r, stages=n_stages & bits)
             if timed:
                 ev[len(groups)].record(stream)
             # compact records -> pinned host memory (rank 0) or device memory (ranks that
@@ -457,6 +461,19 @@ def main():
                 line[key].update(tr[key])
         reconcile_trace(line['roofline'], dense_bytes)
         reconcile_trace(line['roofline_decoder_cifhr'], cifhr_bytes)
+    if default_run and world == 1 and not args.no_predict:
+        # the same planted batch in predict defaults (SURVEY.md §8d cfg3 names eval and
+        # predict defaults; PREDICT_CONFIG: the CLI's predict thresholds, force-complete off)
+        p_steps = max(3, args.steps // 2)
+        p_el, p_stage, p_anns = timed_run(cif, caf, p_steps, 2,
+                                          run_cfg=make_config(**PREDICT_CONFIG))
+        log('predict done')
+        line['predict'] = {
+            'value': round(batch * p_steps / p_el, 1), 'unit': 'images/s',
+            'ms_per_step': round(1e3 * p_el / p_steps, 4),
+            'stage_ms': {n: round(float(v), 4) for n, v in zip(names, p_stage)},
+            'annotations_per_image': round(p_anns / (p_steps * batch), 3),
+        }
     if default_run and world == 1 and not args.no_uniform:
         # the same workload on the uniform generator (SURVEY.md §8d cfg3 names both):
         # dense random fields, ~400 annotations per image
