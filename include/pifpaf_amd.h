@@ -352,6 +352,15 @@ void pp_default_det_nms(pp_det_nms *nms);
 int pp_cifdet_hr(const float *d_det, int32_t n_img, int32_t K, int32_t H, int32_t W,
                  const pp_config *cfg, float *d_cifhr, void *d_workspace, size_t workspace_bytes,
                  void *stream);
+/* CifDetHr.fill over several detection heads (cif_hr.py:67-80 as CifDetHr inherits it: each
+ * head its own map at its stride, min-scale masks p[4] and p[5] > cif_min_scale / stride
+ * (cif_hr.py:84-90), combined by np.maximum; cif_pairs as pp_cifhr_multi for the 10-head
+ * layout).  scales: PP_ROLE_CIF entries whose `cif` points at (n_img, K, 7, H, W) detection
+ * fields; d_cifhr has head 0's size (or a PP_ROLE_HRMAP entry's); workspace
+ * pp_cifhr_multi_workspace_size of the same list. */
+int pp_cifdet_hr_multi(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs, int32_t n_img,
+                       int32_t K, const pp_config *cfg, float *d_cifhr, void *d_workspace,
+                       size_t workspace_bytes, void *stream);
 /* nms.Detection.annotations (nms.py:79-102) over caller records: n_img groups, d_in
  * (n_img, capacity) with d_counts[i] records (field, score, bbox) in list order.  Output
  * as pp_cifdet_decode; d_out_index (optional) = input index of each output record;
@@ -368,12 +377,29 @@ int pp_nms_detection(const pp_det *d_in, const int32_t *d_counts, int32_t n_img,
 int pp_cifdet_seeds(const float *d_det, const float *d_cifhr, int32_t n_img, int32_t K, int32_t H,
                     int32_t W, const pp_config *cfg, float *d_seg, int32_t *d_seg_counts,
                     void *stream);
+/* CifDetSeeds.fill over several detection heads (cif_seeds.py:56-64, 67-90: each head's
+ * cells, min-scale masks on p[4] and p[5], x / y / w / h at the head's stride, v from the
+ * one d_cifhr map), each field's seeds appended head after head: d_seg (n_img, K, 5, cells)
+ * with cells = the heads' H * W summed. */
+int pp_cifdet_seeds_multi(const pp_scale *scales, int32_t n_scales, const float *d_cifhr,
+                          int32_t n_img, int32_t K, const pp_config *cfg, float *d_seg,
+                          int32_t *d_seg_counts, void *stream);
 size_t pp_cifdet_workspace_size(int32_t n_img, int32_t K, int32_t H, int32_t W,
                                 const pp_config *cfg, int32_t det_capacity);
 int pp_cifdet_decode(const float *d_det, int32_t n_img, int32_t K, int32_t H, int32_t W,
                      const pp_config *cfg, const pp_det_nms *nms, float *d_cifhr, pp_det *d_out,
                      int32_t det_capacity, int32_t *d_counts, int32_t *d_status,
                      void *d_workspace, size_t workspace_bytes, void *stream);
+/* CifDet.__call__ (generator/cifdet.py:27-52) over a FieldConfig of several detection heads
+ * and / or min scales: CifDetHr as pp_cifdet_hr_multi, CifDetSeeds as pp_cifdet_seeds_multi,
+ * then the occupancy loop and nms.Detection as pp_cifdet_decode. */
+size_t pp_cifdet_multi_workspace_size(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs,
+                                      int32_t n_img, int32_t K, int32_t det_capacity);
+int pp_cifdet_decode_multi(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs,
+                           int32_t n_img, int32_t K, const pp_config *cfg, const pp_det_nms *nms,
+                           float *d_cifhr, pp_det *d_out, int32_t det_capacity, int32_t *d_counts,
+                           int32_t *d_status, void *d_workspace, size_t workspace_bytes,
+                           void *stream);
 
 /*
  * Preprocess.annotations_inverse (transforms/preprocess.py:35-95) on device records, one

@@ -21,18 +21,20 @@ constexpr int kDetSortLds = 4096;  // seeds of one field sorted in LDS (global b
 constexpr int kDetBoxLds = 1024;   // marked boxes of one field kept in LDS (global beyond)
 
 struct DetArgs {
-    const float *det;      // (n_img, K, 7, H, W)
-    const float *hr;       // (n_img, K, hh, pitch)
-    int K, H, W, hh, ww;
+    Heads hd;              // the detection heads (CIF role, (n_img, K, 7, H, W) each), in
+                           // cif_indices order
+    const float *hr;       // (n_img, K, hh, pitch): the CifDetHr map (head 0's size)
+    int K, hh, ww;
+    int cells;             // segment plane size: the heads' H * W summed
     int64_t pitch;
-    float stride, th, score_scale;
+    float th, score_scale;
     uint32_t skip;         // pp_config.seed_skip_mask (cif_seeds.py:70-71 seed_mask)
-    // per (image, field) segments: v, x, y, w, h (each H*W) and counts
+    // per (image, field) segments: v, x, y, w, h (each `cells`) and counts
     float *seg;
     int *seg_n;
-    uint64_t *gkeys;       // (n_img * K, H*W) global sort keys beyond kDetSortLds
-    int2 *gbox;            // (n_img * K, H*W) boxes beyond kDetBoxLds
-    int *kept;             // (n_img * K, H*W) kept seeds (emission indices), in sorted order
+    uint64_t *gkeys;       // (n_img * K, cells) global sort keys beyond kDetSortLds
+    int2 *gbox;            // (n_img * K, cells) boxes beyond kDetBoxLds
+    int *kept;             // (n_img * K, cells) kept seeds (emission indices), in sorted order
     int *kept_n;
     int oh, ow;            // occupancy grid (cifhr.shape / 2)
     // per image
@@ -47,49 +49,58 @@ struct DetArgs {
 };
 
 __device__ __forceinline__ int64_t seg_base(const DetArgs &a, int64_t fld) {
-    return fld * 5 * (int64_t)a.H * a.W;
+    return fld * 5 * (int64_t)a.cells;
 }
 
-// CifDetSeeds.fill_cif for one field, cells in row-major order
+// CifDetSeeds.fill (cif_seeds.py:56-64 over the heads, 67-90 per head) for one field: the
+// heads in order, each one's cells in row-major order, appended to the field's segment
 __global__ __launch_bounds__(256) void det_seeds_emit_kernel(DetArgs a) {
     __shared__ int s_tmp[4];
     const int64_t fld = blockIdx.x;
     const int img = (int)(fld / a.K), f = (int)(fld % a.K);
-    const int hw = a.H * a.W;
-    const float *p = a.det + fld * 7 * (int64_t)hw;
+    const int64_t cells = a.cells;
     const float *t = a.hr + ((int64_t)img * a.K + f) * a.hh * a.pitch;
-    float *sv = a.seg + seg_base(a, fld), *sx = sv + hw, *sy = sx + hw, *sw = sy + hw,
-          *sh = sw + hw;
+    float *sv = a.seg + seg_base(a, fld), *sx = sv + cells, *sy = sx + cells, *sw = sy + cells,
+          *sh = sw + cells;
     int running = 0;
-    const int hw_seed = ((a.skip >> f) & 1u) ? 0 : hw;  // a masked field emits nothing
-    for (int base = 0; base < hw_seed; base += 256) {
-        const int cell = base + threadIdx.x;
-        bool keep = false;
-        float v = 0.0f, x = 0.0f, y = 0.0f, w = 0.0f, h = 0.0f;
-        if (cell < hw) {
-            const float c = p[cell];
-            if (c > a.th) {  // p[:, p[0] > threshold]
-                x = p[hw + cell] * a.stride;
-                y = p[2 * hw + cell] * a.stride;
-                const float hv = hr_lookup(t, a.hh, a.ww, a.pitch, x, y, 0.0f);
-                v = 0.9f * hv + 0.1f * c;
-                if (a.score_scale != 1.0f) v = v * a.score_scale;
-                keep = v > a.th;
-                w = p[4 * hw + cell] * a.stride;
-                h = p[5 * hw + cell] * a.stride;
+    const int n_heads = ((a.skip >> f) & 1u) ? 0 : a.hd.n_cif;  // a masked field emits nothing
+    for (int m = 0; m < n_heads; m++) {
+        const int hw = a.hd.cH[m] * a.hd.cW[m];
+        const float *p = a.hd.cif[m] + fld * 7 * (int64_t)hw;
+        const float stride = (float)a.hd.cstride[m];
+        // `if min_scale:` p[4] > min_scale / stride, then p[5] (cif_seeds.py:75-77)
+        const bool ms_on = (a.hd.ms_on >> m) & 1u;
+        const float ms_th = a.hd.ms_th[m];
+        for (int base = 0; base < hw; base += 256) {
+            const int cell = base + threadIdx.x;
+            bool keep = false;
+            float v = 0.0f, x = 0.0f, y = 0.0f, w = 0.0f, h = 0.0f;
+            if (cell < hw) {
+                const float c = p[cell];
+                // p[:, p[0] > threshold] (and the min-scale masks)
+                if (c > a.th && (!ms_on || (p[4 * hw + cell] > ms_th && p[5 * hw + cell] > ms_th))) {
+                    x = p[hw + cell] * stride;
+                    y = p[2 * hw + cell] * stride;
+                    const float hv = hr_lookup(t, a.hh, a.ww, a.pitch, x, y, 0.0f);
+                    v = 0.9f * hv + 0.1f * c;
+                    if (a.score_scale != 1.0f) v = v * a.score_scale;
+                    keep = v > a.th;
+                    w = p[4 * hw + cell] * stride;
+                    h = p[5 * hw + cell] * stride;
+                }
             }
+            int total;
+            const int slot = block_compact<4>(keep, s_tmp, total);
+            if (keep) {
+                const int q = running + slot;
+                sv[q] = v;
+                sx[q] = x;
+                sy[q] = y;
+                sw[q] = w;
+                sh[q] = h;
+            }
+            running += total;
         }
-        int total;
-        const int slot = block_compact<4>(keep, s_tmp, total);
-        if (keep) {
-            const int q = running + slot;
-            sv[q] = v;
-            sx[q] = x;
-            sy[q] = y;
-            sw[q] = w;
-            sh[q] = h;
-        }
-        running += total;
     }
     if (threadIdx.x == 0) a.seg_n[fld] = running;
 }
@@ -123,7 +134,7 @@ __global__ __launch_bounds__(256) void det_select_kernel(DetArgs a) {
     __shared__ uint64_t s_key[kDetSortLds];
     __shared__ int2 s_box[kDetBoxLds];
     const int64_t fld = blockIdx.x;
-    const int hw = a.H * a.W;
+    const int hw = a.cells;
     const int n = a.seg_n[fld];
     const float *sv = a.seg + seg_base(a, fld), *sx = sv + hw, *sy = sx + hw, *sw = sy + hw,
                 *sh = sw + hw;
@@ -374,7 +385,7 @@ __device__ int det_nms_output(const DetArgs &a, int img, float *cand, int *perm,
 __global__ __launch_bounds__(256) void det_output_kernel(DetArgs a) {
     __shared__ int s_n, s_status;
     const int img = blockIdx.x;
-    const int hw = a.H * a.W;
+    const int hw = a.cells;
     float *cand = a.cand + (int64_t)img * a.cap * kCand;
     int *perm = a.perm + (int64_t)img * 3 * a.np_cap, *perm2 = perm + a.np_cap,
         *order = perm2 + a.np_cap;
@@ -471,11 +482,11 @@ struct DetLayout {
     int np_cap;
 };
 
-static DetLayout det_layout(int n_img, int K, int H, int W, const pp_config *cfg, int cap) {
+static DetLayout det_layout(const Heads &h, int n_img, int K, int cap) {
     DetLayout d{};
-    const int hh = (int)hr_dim(H, cfg->stride), ww = (int)hr_dim(W, cfg->stride);
+    const int hh = h.hr_hh, ww = h.hr_ww;
     d.pitch = pp_cifhr_pitch(ww);
-    d.hr_ws = pp_cifhr_workspace_size(n_img, K, H, W);
+    d.hr_ws = cifhr_heads_workspace_size(h, n_img, K);
     d.np_cap = 1;
     while (d.np_cap < 2 * cap) d.np_cap <<= 1;
     size_t o = 0;
@@ -484,19 +495,99 @@ static DetLayout det_layout(int n_img, int K, int H, int W, const pp_config *cfg
         o += align_up(bytes);
         return at;
     };
-    const size_t nf = (size_t)n_img * K, hw = (size_t)H * W;
+    const size_t nf = (size_t)n_img * K, cells = (size_t)h.cif_cells();
     d.off_hr = take((size_t)n_img * K * hh * d.pitch * sizeof(float));
     d.off_hr_ws = take(d.hr_ws);
-    d.off_seg = take(nf * 5 * hw * sizeof(float));
+    d.off_seg = take(nf * 5 * cells * sizeof(float));
     d.off_seg_n = take(nf * sizeof(int));
-    d.off_keys = take(nf * hw * sizeof(uint64_t));
-    d.off_box = take(nf * hw * sizeof(int2));
-    d.off_kept = take(nf * hw * sizeof(int));
+    d.off_keys = take(nf * cells * sizeof(uint64_t));
+    d.off_box = take(nf * cells * sizeof(int2));
+    d.off_kept = take(nf * cells * sizeof(int));
     d.off_kept_n = take(nf * sizeof(int));
     d.off_cand = take((size_t)n_img * cap * 10 * sizeof(float));
     d.off_perm = take((size_t)n_img * 3 * d.np_cap * sizeof(int));
     d.total = o;
     return d;
+}
+
+// the seeds' arguments over a head list (pp_cifdet_seeds*, pp_cifdet_decode*)
+static DetArgs det_seed_args(const Heads &h, const float *hr, int K, const pp_config *cfg,
+                             float *seg, int *seg_n) {
+    DetArgs a{};
+    a.hd = h;
+    a.hr = hr;
+    a.K = K;
+    a.hh = h.hr_hh;
+    a.ww = h.hr_ww;
+    a.cells = (int)h.cif_cells();
+    a.pitch = pp_cifhr_pitch(a.ww);
+    a.th = cfg->seed_threshold;
+    a.skip = cfg->seed_skip_mask;
+    a.score_scale = cfg->seed_score_scale;
+    a.seg = seg;
+    a.seg_n = seg_n;
+    return a;
+}
+
+static int det_seeds_launch(const Heads &h, const float *d_cifhr, int32_t n_img, int32_t K,
+                            const pp_config *cfg, float *d_seg, int32_t *d_seg_counts,
+                            hipStream_t s, const char *who) {
+    if (!d_cifhr || !cfg || !d_seg || !d_seg_counts)
+        return fail(PP_EINVAL, std::string(who) + ": NULL argument");
+    for (int m = 0; m < h.n_cif; m++)
+        if (!h.cif[m]) return fail(PP_EINVAL, std::string(who) + ": NULL field");
+    if (n_img < 0 || K <= 0) return fail(PP_ESHAPE, std::string(who) + ": bad shape");
+    if (h.cif_cells() >= (int64_t)1 << 31) return fail(PP_ESHAPE, std::string(who) + ": too many cells");
+    if (n_img == 0) return PP_OK;
+    const DetArgs a = det_seed_args(h, d_cifhr, K, cfg, d_seg, d_seg_counts);
+    hipLaunchKernelGGL(det_seeds_emit_kernel, dim3((unsigned)((int64_t)n_img * K)), dim3(256), 0,
+                       s, a);
+    return check_launch(who);
+}
+
+static int det_decode_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config *cfg,
+                             const pp_det_nms *nms, float *d_cifhr, pp_det *d_out,
+                             int32_t det_capacity, int32_t *d_counts, int32_t *d_status,
+                             void *d_workspace, size_t workspace_bytes, hipStream_t s,
+                             const char *who) {
+    if (!cfg || !nms || !d_out || !d_counts || !d_status || !d_workspace)
+        return fail(PP_EINVAL, std::string(who) + ": NULL argument");
+    for (int m = 0; m < h.n_cif; m++)
+        if (!h.cif[m]) return fail(PP_EINVAL, std::string(who) + ": NULL field");
+    if (n_img < 0 || K <= 0 || K > 4096 || det_capacity <= 0)
+        return fail(PP_ESHAPE, std::string(who) + ": bad shape");
+    if (h.cif_cells() >= (int64_t)1 << 31) return fail(PP_ESHAPE, std::string(who) + ": too many cells");
+    if (!(cfg->seed_threshold >= 0.0f))
+        return fail(PP_EINVAL, std::string(who) + ": seed_threshold must be >= 0");
+    if (n_img == 0) return PP_OK;
+    const DetLayout d = det_layout(h, n_img, K, det_capacity);
+    if (workspace_bytes < d.total) return fail(PP_ENOMEM, std::string(who) + ": workspace too small");
+    const int hh = h.hr_hh, ww = h.hr_ww;
+    if (hh >= 65535 || ww >= 65535) return fail(PP_ESHAPE, std::string(who) + ": field too large");
+    char *ws = (char *)d_workspace;
+    float *hr = d_cifhr ? d_cifhr : (float *)(ws + d.off_hr);
+    int rc = cifhr_heads_launch<true>(h, n_img, K, cfg, hr, ws + d.off_hr_ws, d.hr_ws, s, who);
+    if (rc) return rc;
+    DetArgs a = det_seed_args(h, hr, K, cfg, (float *)(ws + d.off_seg), (int *)(ws + d.off_seg_n));
+    a.gkeys = (uint64_t *)(ws + d.off_keys);
+    a.gbox = (int2 *)(ws + d.off_box);
+    a.kept = (int *)(ws + d.off_kept);
+    a.kept_n = (int *)(ws + d.off_kept_n);
+    a.oh = (int)((double)hh / 2.0);  // Occupancy(cifhr.shape, 2, min_scale=2.0)
+    a.ow = (int)((double)ww / 2.0);
+    a.cap = det_capacity;
+    a.cand = (float *)(ws + d.off_cand);
+    a.perm = (int *)(ws + d.off_perm);
+    a.np_cap = d.np_cap;
+    a.nms = *nms;
+    a.out = d_out;
+    a.counts = d_counts;
+    a.status = d_status;
+    const unsigned nf = (unsigned)((int64_t)n_img * K);
+    hipLaunchKernelGGL(det_seeds_emit_kernel, dim3(nf), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(det_select_kernel, dim3(nf), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(det_output_kernel, dim3((unsigned)n_img), dim3(256), 0, s, a);
+    return check_launch(who);
 }
 
 }  // namespace pp
@@ -518,29 +609,20 @@ void pp_default_det_nms(pp_det_nms *z) {
 int pp_cifdet_seeds(const float *d_det, const float *d_cifhr, int32_t n_img, int32_t K, int32_t H,
                     int32_t W, const pp_config *cfg, float *d_seg, int32_t *d_seg_counts,
                     void *stream) {
-    if (!d_det || !d_cifhr || !cfg || !d_seg || !d_seg_counts)
-        return fail(PP_EINVAL, "pp_cifdet_seeds: NULL argument");
-    if (n_img < 0 || K <= 0 || H <= 0 || W <= 0 || cfg->stride <= 0)
-        return fail(PP_ESHAPE, "pp_cifdet_seeds: bad shape");
-    if (n_img == 0) return PP_OK;
-    DetArgs a{};
-    a.det = d_det;
-    a.hr = d_cifhr;
-    a.K = K;
-    a.H = H;
-    a.W = W;
-    a.hh = (int)hr_dim(H, cfg->stride);
-    a.ww = (int)hr_dim(W, cfg->stride);
-    a.pitch = pp_cifhr_pitch(a.ww);
-    a.stride = (float)cfg->stride;
-    a.th = cfg->seed_threshold;
-    a.skip = cfg->seed_skip_mask;
-    a.score_scale = cfg->seed_score_scale;
-    a.seg = d_seg;
-    a.seg_n = d_seg_counts;
-    hipLaunchKernelGGL(det_seeds_emit_kernel, dim3((unsigned)((int64_t)n_img * K)), dim3(256), 0,
-                       (hipStream_t)stream, a);
-    return check_launch("pp_cifdet_seeds");
+    if (!d_det || !cfg) return fail(PP_EINVAL, "pp_cifdet_seeds: NULL argument");
+    if (H <= 0 || W <= 0 || cfg->stride <= 0) return fail(PP_ESHAPE, "pp_cifdet_seeds: bad shape");
+    return det_seeds_launch(single_head(d_det, nullptr, H, W, cfg->stride), d_cifhr, n_img, K, cfg,
+                            d_seg, d_seg_counts, (hipStream_t)stream, "pp_cifdet_seeds");
+}
+
+int pp_cifdet_seeds_multi(const pp_scale *scales, int32_t n_scales, const float *d_cifhr,
+                          int32_t n_img, int32_t K, const pp_config *cfg, float *d_seg,
+                          int32_t *d_seg_counts, void *stream) {
+    Heads h;
+    const int rc = make_heads(scales, n_scales, 0, PP_ROLE_CIF, &h, "pp_cifdet_seeds_multi");
+    if (rc) return rc;
+    return det_seeds_launch(h, d_cifhr, n_img, K, cfg, d_seg, d_seg_counts, (hipStream_t)stream,
+                            "pp_cifdet_seeds_multi");
 }
 
 size_t pp_nms_detection_workspace_size(int32_t n_img, int32_t capacity) {
@@ -579,64 +661,40 @@ size_t pp_cifdet_workspace_size(int32_t n_img, int32_t K, int32_t H, int32_t W,
                                 const pp_config *cfg, int32_t det_capacity) {
     if (!cfg || n_img < 0 || K <= 0 || H <= 0 || W <= 0 || det_capacity <= 0 || cfg->stride <= 0)
         return 0;
-    return det_layout(n_img, K, H, W, cfg, det_capacity).total;
+    return det_layout(single_head(nullptr, nullptr, H, W, cfg->stride), n_img, K, det_capacity).total;
 }
 
 int pp_cifdet_decode(const float *d_det, int32_t n_img, int32_t K, int32_t H, int32_t W,
                      const pp_config *cfg, const pp_det_nms *nms, float *d_cifhr, pp_det *d_out,
                      int32_t det_capacity, int32_t *d_counts, int32_t *d_status,
                      void *d_workspace, size_t workspace_bytes, void *stream) {
-    if (!d_det || !cfg || !nms || !d_out || !d_counts || !d_status || !d_workspace)
-        return fail(PP_EINVAL, "pp_cifdet_decode: NULL argument");
-    if (n_img < 0 || K <= 0 || K > 4096 || H <= 0 || W <= 0 || det_capacity <= 0 ||
-        cfg->stride <= 0)
-        return fail(PP_ESHAPE, "pp_cifdet_decode: bad shape");
-    if (!(cfg->seed_threshold >= 0.0f))
-        return fail(PP_EINVAL, "pp_cifdet_decode: seed_threshold must be >= 0");
-    if (n_img == 0) return PP_OK;
-    const DetLayout d = det_layout(n_img, K, H, W, cfg, det_capacity);
-    if (workspace_bytes < d.total) return fail(PP_ENOMEM, "pp_cifdet_decode: workspace too small");
-    const int hh = (int)hr_dim(H, cfg->stride), ww = (int)hr_dim(W, cfg->stride);
-    if (hh >= 65535 || ww >= 65535) return fail(PP_ESHAPE, "pp_cifdet_decode: field too large");
-    char *ws = (char *)d_workspace;
-    hipStream_t s = (hipStream_t)stream;
-    float *hr = d_cifhr ? d_cifhr : (float *)(ws + d.off_hr);
-    int rc = pp_cifdet_hr(d_det, n_img, K, H, W, cfg, hr, ws + d.off_hr_ws, d.hr_ws, stream);
+    if (!d_det || !cfg) return fail(PP_EINVAL, "pp_cifdet_decode: NULL argument");
+    if (H <= 0 || W <= 0 || cfg->stride <= 0) return fail(PP_ESHAPE, "pp_cifdet_decode: bad shape");
+    return det_decode_launch(single_head(d_det, nullptr, H, W, cfg->stride), n_img, K, cfg, nms,
+                             d_cifhr, d_out, det_capacity, d_counts, d_status, d_workspace,
+                             workspace_bytes, (hipStream_t)stream, "pp_cifdet_decode");
+}
+
+size_t pp_cifdet_multi_workspace_size(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs,
+                                      int32_t n_img, int32_t K, int32_t det_capacity) {
+    Heads h;
+    if (make_heads(scales, n_scales, cif_pairs, PP_ROLE_CIF, &h, "pp_cifdet_multi_workspace_size") ||
+        n_img < 0 || K <= 0 || det_capacity <= 0)
+        return 0;
+    return det_layout(h, n_img, K, det_capacity).total;
+}
+
+int pp_cifdet_decode_multi(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs,
+                           int32_t n_img, int32_t K, const pp_config *cfg, const pp_det_nms *nms,
+                           float *d_cifhr, pp_det *d_out, int32_t det_capacity, int32_t *d_counts,
+                           int32_t *d_status, void *d_workspace, size_t workspace_bytes,
+                           void *stream) {
+    Heads h;
+    const int rc = make_heads(scales, n_scales, cif_pairs, PP_ROLE_CIF, &h, "pp_cifdet_decode_multi");
     if (rc) return rc;
-    DetArgs a{};
-    a.det = d_det;
-    a.hr = hr;
-    a.K = K;
-    a.H = H;
-    a.W = W;
-    a.hh = hh;
-    a.ww = ww;
-    a.pitch = d.pitch;
-    a.stride = (float)cfg->stride;
-    a.th = cfg->seed_threshold;
-    a.skip = cfg->seed_skip_mask;
-    a.score_scale = cfg->seed_score_scale;
-    a.seg = (float *)(ws + d.off_seg);
-    a.seg_n = (int *)(ws + d.off_seg_n);
-    a.gkeys = (uint64_t *)(ws + d.off_keys);
-    a.gbox = (int2 *)(ws + d.off_box);
-    a.kept = (int *)(ws + d.off_kept);
-    a.kept_n = (int *)(ws + d.off_kept_n);
-    a.oh = (int)((double)hh / 2.0);  // Occupancy(cifhr.shape, 2, min_scale=2.0)
-    a.ow = (int)((double)ww / 2.0);
-    a.cap = det_capacity;
-    a.cand = (float *)(ws + d.off_cand);
-    a.perm = (int *)(ws + d.off_perm);
-    a.np_cap = d.np_cap;
-    a.nms = *nms;
-    a.out = d_out;
-    a.counts = d_counts;
-    a.status = d_status;
-    const unsigned nf = (unsigned)((int64_t)n_img * K);
-    hipLaunchKernelGGL(det_seeds_emit_kernel, dim3(nf), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(det_select_kernel, dim3(nf), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(det_output_kernel, dim3((unsigned)n_img), dim3(256), 0, s, a);
-    return check_launch("pp_cifdet_decode");
+    return det_decode_launch(h, n_img, K, cfg, nms, d_cifhr, d_out, det_capacity, d_counts,
+                             d_status, d_workspace, workspace_bytes, (hipStream_t)stream,
+                             "pp_cifdet_decode_multi");
 }
 
 }  // extern "C"

@@ -374,7 +374,8 @@ __device__ void hr_row_bins(const FoldCand *list, int total, FoldCand *bins, int
 constexpr int kTileBits = 1024;  // per-field tile bitmap capacity (32x32 tiles of 64x64 px)
 
 // DET: CifDetHr.accumulate (cif_hr.py:84-100) on 7-channel fields [c, x, y, b, w, h, b2],
-// sigma = max(1, 0.1 * min(w, h) * stride); else CifHr (cif_hr.py:26-40), 5 channels.
+// min-scale masks on w and h, sigma = max(1, 0.1 * min(w, h) * stride); else CifHr
+// (cif_hr.py:26-40), 5 channels.
 //
 // One workgroup per (image, field, CifHr group).  A group's members (cif_hr.py:42-57
 // fill_multiple: one head, or heads g and g + n/2 with pairs) are compacted one after the
@@ -440,7 +441,8 @@ __global__ __launch_bounds__(256) void cifhr_splats_kernel(HrSplatArgs a) {
 #pragma unroll
             for (int k = 0; k < kU; k++) {
                 bool keep = c[k] > a.v_th;
-                if (keep && !DET && ms_on) keep = s4[k] > ms_th;  // p[4] > min_scale / stride
+                if (keep && ms_on)  // p[4] (and for detections p[5]) > min_scale / stride
+                    keep = DET ? (s4[k] > ms_th && s5[k] > ms_th) : s4[k] > ms_th;
                 int total;
                 const int slot = block_compact<4>(keep, s_tmp, total);
                 if (keep) {
@@ -1945,6 +1947,8 @@ int cifhr_heads_launch(const Heads &h, int32_t n_img, int32_t K, const pp_config
 
 template int cifhr_heads_launch<false>(const Heads &, int32_t, int32_t, const pp_config *, float *,
                                        void *, size_t, hipStream_t, const char *);
+template int cifhr_heads_launch<true>(const Heads &, int32_t, int32_t, const pp_config *, float *,
+                                      void *, size_t, hipStream_t, const char *);
 
 // workgroups per field of cifhr_sparse_kernel: fewer fields than kSplitSlots split each
 // field's tiles over several workgroups (each builds its own copy of the field's list: a
@@ -2169,6 +2173,16 @@ size_t pp_cifhr_multi_workspace_size(const pp_scale *scales, int32_t n_scales, i
         n_img < 0 || K <= 0)
         return 0;
     return cifhr_heads_workspace_size(h, n_img, K);
+}
+
+int pp_cifdet_hr_multi(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs, int32_t n_img,
+                       int32_t K, const pp_config *cfg, float *d_cifhr, void *d_workspace,
+                       size_t workspace_bytes, void *stream) {
+    Heads h;
+    const int rc = make_heads(scales, n_scales, cif_pairs, PP_ROLE_CIF, &h, "pp_cifdet_hr_multi");
+    if (rc) return rc;
+    return cifhr_heads_launch<true>(h, n_img, K, cfg, d_cifhr, d_workspace, workspace_bytes,
+                                    (hipStream_t)stream, "pp_cifdet_hr_multi");
 }
 
 int pp_cifhr_multi(const pp_scale *scales, int32_t n_scales, int32_t cif_pairs, int32_t n_img,

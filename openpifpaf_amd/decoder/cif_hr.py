@@ -83,6 +83,7 @@ def cifdet_hr_device(det, stride, v_threshold, neighbors):
 class CifHr:
     neighbors = 16
     v_threshold = 0.1
+    _multi_entry = 'pp_cifhr_multi'  # the head-list launcher (_run_multi)
 
     def __init__(self, config: FieldConfig):
         self.config = config
@@ -133,7 +134,8 @@ class CifHr:
         return self
 
     def _run_multi(self, arr, groups, k, hh, ww, device):
-        """pp_cifhr_multi -> the (K, hh, ww) device view of its pitched output."""
+        """pp_cifhr_multi (pp_cifdet_hr_multi for CifDetHr) -> the (K, hh, ww) device view
+        of its pitched output."""
         lib = load()
         pitch = int(lib.pp_cifhr_pitch(ww))
         out = torch.empty((1, k, hh, pitch), dtype=torch.float32, device=device)
@@ -141,7 +143,7 @@ class CifHr:
                                                                       k))),
                          dtype=torch.uint8, device=device)
         cfg = make_config(cif_threshold=self.v_threshold, cif_neighbors=self.neighbors)
-        call('pp_cifhr_multi', arr, len(arr), groups, 1, k, ctypes.byref(cfg), _device.ptr(out),
+        call(self._multi_entry, arr, len(arr), groups, 1, k, ctypes.byref(cfg), _device.ptr(out),
              _device.ptr(ws), ctypes.c_size_t(ws.numel()), _device.stream())
         return out[0, :, :, :ww]
 
@@ -174,7 +176,11 @@ class CifHr:
 
 
 class CifDetHr(CifHr):
-    """cif_hr.py:84-100: detection fields (K, 7, H, W), sigma = max(1, 0.1 min(w, h) stride)."""
+    """cif_hr.py:84-100: detection fields (K, 7, H, W), min-scale masks on w and h,
+    sigma = max(1, 0.1 min(w, h) stride).  fill_cif / fill_multiple / fill are CifHr's (the
+    reference's CifDetHr inherits them): one head, several heads combined by np.maximum, the
+    10-head pairs, on pp_cifdet_hr_multi."""
+    _multi_entry = 'pp_cifdet_hr_multi'
 
     def accumulate(self, len_cifs, t, p, stride, min_scale):
         p = p[:, p[0] > self.v_threshold]
@@ -187,27 +193,3 @@ class CifDetHr(CifHr):
         sigma = np.maximum(1.0, 0.1 * np.minimum(w, h) * stride)
         scalar_square_add_gauss_with_max(t, x, y, sigma, v / self.neighbors / len_cifs,
                                          truncate=1.0)
-
-    def fill_cif(self, cif, stride, min_scale=0.0):
-        if min_scale:
-            raise NotImplementedError('min_scale masks (multi-scale) are not implemented')
-        if self.accumulated is not None:
-            raise NotImplementedError('accumulating several CifDet heads is not implemented')
-        hr = cifdet_hr_device(batch1(cif), int(stride), self.v_threshold, self.neighbors)
-        ww = (cif.shape[3] - 1) * int(stride) + 1
-        acc = hr[0, :, :, :ww]
-        self.accumulated = acc if _device.is_device(cif) else np.ascontiguousarray(
-            acc.cpu().numpy())
-        return self
-
-    def fill_multiple(self, cifs, stride, min_scale=0.0):
-        """One detection head (the reference's CifDet decodes a single head, cifdet.py:39)."""
-        if len(cifs) != 1:
-            raise NotImplementedError('several CifDet heads are not implemented')
-        return self.fill_cif(cifs[0], stride, min_scale)
-
-    def fill(self, fields):
-        for cif_i, stride, min_scale in zip(self.config.cif_indices, self.config.cif_strides,
-                                            self.config.cif_min_scales):
-            self.fill_cif(fields[cif_i], stride, min_scale=min_scale)
-        return self

@@ -76,22 +76,33 @@ class CifDetSeeds(CifSeeds):
     """cif_seeds.py:67-90: (v, field, x, y, w, h) seeds of detection fields."""
 
     def fill_cif(self, cif, stride, *, min_scale=0.0, seed_mask=None):
+        """cif_seeds.py:68-90 for one detection head at `stride` (min-scale masks on p[4] and
+        p[5]; CifHr lookups through the map's own geometry, which may be another head's),
+        appended to the seeds of earlier calls (pp_cifdet_seeds_multi)."""
         if self.threshold is None:
             raise TypeError("'>' not supported between instances of 'float' and 'NoneType' "
                             "(CifSeeds.threshold is not configured)")
-        if min_scale:
-            raise NotImplementedError('min_scale masks of detection heads are not implemented')
         c = batch1(cif)
         _, k, _, h, w = c.shape
         hr = pitched_hr(self.cifhr)
+        arr = scale_list([(c.data_ptr(), h, w)], [], [int(stride)], [], [min_scale])
+        arr = with_geometry(arr, self.cifhr.shape)
         seg = torch.empty((k, 5, h * w), dtype=torch.float32, device=c.device)
         counts = torch.zeros(k, dtype=torch.int32, device=c.device)
         cfg = make_config(seed_threshold=self.threshold, seed_score_scale=self.score_scale,
                           stride=int(stride), seed_mask=seed_mask)
-        call('pp_cifdet_seeds', _device.ptr(c), _device.ptr(hr), 1, k, h, w, cfg_ptr(cfg),
+        call('pp_cifdet_seeds_multi', arr, len(arr), _device.ptr(hr), 1, k, cfg_ptr(cfg),
              _device.ptr(seg), _device.ptr(counts), _device.stream())
         seg, counts = seg.cpu().numpy(), counts.cpu().numpy()
         for f in range(k):  # emission order: fields in order, cells in row-major order
             n = int(counts[f])
             self.seeds.extend((v, f, x, y, ww, hh) for v, x, y, ww, hh in zip(*seg[f, :, :n]))
+        return self
+
+    def fill(self, fields):
+        """cif_seeds.py:56-64: every detection head of the FieldConfig, in order."""
+        for cif_i, stride, min_scale in zip(self.config.cif_indices, self.config.cif_strides,
+                                            self.config.cif_min_scales):
+            self.fill_cif(fields[cif_i], stride, min_scale=min_scale,
+                          seed_mask=self.config.seed_mask)
         return self

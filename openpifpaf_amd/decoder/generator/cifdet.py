@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from ... import _device
-from ..._abi import DET_DTYPE, DetNms, check_seed_mask, make_config
+from ..._abi import DET_DTYPE, DetNms, check_seed_mask, make_config, scale_list
 from ..._lib import PPError, call, load
 from ...annotation import AnnotationDet
 from .. import nms
@@ -39,42 +39,77 @@ class CifDet(Generator):
         self.categories = categories
         self._ws = None
 
+    def single_head(self):
+        """One detection head without a min scale: pp_cifdet_decode; anything else (several
+        heads, min-scale masks) runs pp_cifdet_decode_multi."""
+        fc = self.field_config
+        return len(fc.cif_indices) == 1 and not fc.cif_min_scales[0]
+
+    def head_fields(self, fields):
+        """The FieldConfig's detection heads of a field list, in cif_indices order."""
+        return [fields[i] for i in self.field_config.cif_indices]
+
     def config(self):
         if CifSeeds.threshold is None:
             raise TypeError("'>' not supported between instances of 'float' and 'NoneType' "
                             "(CifSeeds.threshold is not configured)")
-        _, _, stride = self.field_config.single_scale()
+        stride = int(self.field_config.cif_strides[0])
         check_seed_mask(self.field_config.seed_mask, len(self.categories))
         return make_config(cif_threshold=CifHr.v_threshold, seed_threshold=CifSeeds.threshold,
                            seed_score_scale=CifSeeds.score_scale, stride=int(stride),
                            cif_neighbors=CifHr.neighbors, seed_mask=self.field_config.seed_mask)
 
     def decode_records(self, det_batch, cap=None):
-        """det_batch (B, K, 7, H, W) -> (pp_det records, per-image offsets)."""
-        det = _device.to_device(det_batch)
-        if det.dim() != 5 or det.shape[2] != 7:
-            raise ValueError('expected CifDet fields (B, K, 7, H, W)')
+        """det_batch (B, K, 7, H, W), or with several heads / min scales the list of the
+        FieldConfig's heads (each (B, K, 7, H_m, W_m), cif_indices order) -> (pp_det
+        records, per-image offsets)."""
+        heads = [_device.to_device(t) for t in
+                 (det_batch if isinstance(det_batch, (list, tuple)) else [det_batch])]
+        for det in heads:
+            if det.dim() != 5 or det.shape[2] != 7:
+                raise ValueError('expected CifDet fields (B, K, 7, H, W)')
+        if len(heads) != len(self.field_config.cif_indices):
+            raise ValueError('expected {} CifDet heads, got {}'.format(
+                len(self.field_config.cif_indices), len(heads)))
+        det = heads[0]
         b, k, _, h, w = det.shape
+        if any(t.shape[:3] != det.shape[:3] for t in heads):
+            raise ValueError('CifDet heads differ in batch or field count')
         cfg = self.config()
         z = det_nms_config()
+        cells = sum(t.shape[3] * t.shape[4] for t in heads)
+        fc = self.field_config
+        multi = not self.single_head()
+        arr = scale_list([(t.data_ptr(), t.shape[3], t.shape[4]) for t in heads], [],
+                         fc.cif_strides, [], fc.cif_min_scales) if multi else None
+        pairs = int(len(heads) == 10)  # CifHr.fill's 10-head layout (cif_hr.py:68-73)
         cap = cap or max(64, h * w)
         while True:
-            size = int(load().pp_cifdet_workspace_size(b, k, h, w, ctypes.byref(cfg), cap))
+            if multi:
+                size = int(load().pp_cifdet_multi_workspace_size(arr, len(arr), pairs, b, k, cap))
+            else:
+                size = int(load().pp_cifdet_workspace_size(b, k, h, w, ctypes.byref(cfg), cap))
             if self._ws is None or self._ws.numel() < size:
                 self._ws = torch.empty(size, dtype=torch.uint8, device=det.device)
             out = torch.empty((b, cap, DET_DTYPE.itemsize), dtype=torch.uint8, device=det.device)
             counts = torch.empty(b, dtype=torch.int32, device=det.device)
             status = torch.empty(b, dtype=torch.int32, device=det.device)
-            call('pp_cifdet_decode', _device.ptr(det), b, k, h, w, ctypes.byref(cfg),
-                 ctypes.byref(z), _device.ptr(None), _device.ptr(out), cap, _device.ptr(counts),
-                 _device.ptr(status), _device.ptr(self._ws), ctypes.c_size_t(self._ws.numel()),
-                 _device.stream())
+            if multi:
+                call('pp_cifdet_decode_multi', arr, len(arr), pairs, b, k, ctypes.byref(cfg),
+                     ctypes.byref(z), _device.ptr(None), _device.ptr(out), cap,
+                     _device.ptr(counts), _device.ptr(status), _device.ptr(self._ws),
+                     ctypes.c_size_t(self._ws.numel()), _device.stream())
+            else:
+                call('pp_cifdet_decode', _device.ptr(det), b, k, h, w, ctypes.byref(cfg),
+                     ctypes.byref(z), _device.ptr(None), _device.ptr(out), cap,
+                     _device.ptr(counts), _device.ptr(status), _device.ptr(self._ws),
+                     ctypes.c_size_t(self._ws.numel()), _device.stream())
             st = status.cpu().numpy()
             if not (st & PP_ST_ANN_OVERFLOW).any():
                 break
-            if cap >= k * h * w:
+            if cap >= k * cells:
                 raise PPError('CifDet: detection capacity overflow')
-            cap = min(k * h * w, 2 * cap)
+            cap = min(k * cells, 2 * cap)
         counts = counts.cpu().numpy().astype(np.int64)
         offsets = np.concatenate([[0], np.cumsum(counts)])
         host = out.cpu().numpy()
@@ -100,10 +135,12 @@ class CifDet(Generator):
         import torch.distributed as dist  # pylint: disable=import-outside-toplevel
         from ...distributed import GatherMismatch, gather_records, shard
         rank, world = dist.get_rank(group), dist.get_world_size(group)
-        n = 0 if det_batch is None else len(det_batch)
+        several = isinstance(det_batch, (list, tuple))
+        n = 0 if det_batch is None else len(det_batch[0] if several else det_batch)
         a, b = (0, n) if local else shard(n, rank, world)
         if b > a:
-            recs, offsets = self.decode_records(det_batch[a:b])
+            recs, offsets = self.decode_records([t[a:b] for t in det_batch] if several
+                                                else det_batch[a:b])
         else:
             recs, offsets = np.zeros(0, DET_DTYPE), np.zeros(1, np.int64)
         nccl = dist.get_backend(group) == 'nccl'
@@ -126,9 +163,10 @@ class CifDet(Generator):
         kw = {} if group is None else {'group': group, 'dst': dst, 'local': local}
         if heads is None:  # this rank's shard of a sharded batch is empty
             return self.decode_batch(None, **kw)
-        cif_i, _, _ = self.field_config.single_scale()
-        return self.decode_batch(heads[cif_i], **kw)
+        heads = self.head_fields(heads)
+        return self.decode_batch(heads[0] if self.single_head() else heads, **kw)
 
     def __call__(self, fields):
-        cif_i, _, _ = self.field_config.single_scale()
-        return self.decode_batch(_device.to_device(fields[cif_i])[None])[0]
+        """generator/cifdet.py:27-52 for one image's field list."""
+        heads = [_device.to_device(t)[None] for t in self.head_fields(fields)]
+        return self.decode_batch(heads[0] if self.single_head() else heads)[0]

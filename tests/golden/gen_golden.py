@@ -12,6 +12,8 @@ Fixtures:
   primitives.npz       known-answer tests for every openpifpaf.functional primitive
                        (small fields, full inputs and outputs, strided views, edge cases)
   errors.json          the reference's ValueError messages at the boundary
+  detm_<case>.npz      CifDet over several heads / min scales (DET_MULTI_CASES): the same
+                       records as det_<case>.npz
   det_<case>.npz       CifDet decoder (cifdet.py:27-52): CifDetHr digest + sums, the seed
                        list, and the AnnotationDet list (field, score, bbox)
   inverse.npz          Preprocess.annotations_inverse + json_data on reference-decoded poses
@@ -622,6 +624,46 @@ def gen_det(op):
     CifSeeds.threshold = None
 
 
+# CifDet over several heads and / or min scales (cif_hr.py:67-80 and cif_seeds.py:56-64 as
+# CifDetHr / CifDetSeeds inherit them, cif_hr.py:84-90, cif_seeds.py:75-77): name, generator,
+# seed threshold, categories, heads (H, W, stride, min_scale, generator seed)
+DET_MULTI_CASES = [
+    ('m2_p', 'planted', 0.5, 3, [(40, 40, 8, 0.0, 0), (20, 20, 16, 0.0, 100)]),
+    ('m2_pms', 'planted', 0.2, 3, [(40, 40, 8, 64.0, 1), (20, 20, 16, 96.0, 101)]),
+    ('m1_ums', 'uniform', 0.1, 2, [(40, 40, 8, 32.0, 2)]),
+]
+
+
+def gen_det_multi(op):
+    """The reference CifDet decoder (and its CifDetHr / CifDetSeeds stages) over
+    FieldConfigs of several detection heads and min scales (detm_<case>.npz)."""
+    from openpifpaf.decoder import CifDet, CifDetHr, FieldConfig  # pylint: disable=import-outside-toplevel
+    from openpifpaf.decoder.cif_seeds import CifDetSeeds, CifSeeds  # pylint: disable=import-outside-toplevel
+    for name, gen, th, n_cat, heads in DET_MULTI_CASES:
+        fields = [synthetic.det_batch(gen, 1, h, w, first_seed=seed, n_categories=n_cat)[0]
+                  for h, w, _, _, seed in heads]
+        fc = FieldConfig(cif_indices=list(range(len(heads))),
+                         cif_strides=[st for _, _, st, _, _ in heads],
+                         cif_min_scales=[ms for _, _, _, ms, _ in heads])
+        CifSeeds.threshold = th
+        hr = CifDetHr(fc).fill(fields).accumulated
+        seeds = CifDetSeeds(hr, fc).fill(fields).get()
+        anns = CifDet(fc, ['c%d' % i for i in range(n_cat)])(fields)
+        out = {
+            'gen': np.array(gen), 'seed_threshold': th, 'n_categories': n_cat,
+            'heads': np.array(heads, np.float64),
+            'input_sha': np.array([sha(f) for f in fields]),
+            'cifhr_sha': np.array(sha(hr)), 'cifhr_sums': hr.sum(axis=(1, 2), dtype=np.float64),
+            'seeds': np.array([[float(t) for t in sd] for sd in seeds], np.float32).reshape(-1, 6),
+            'ann_field': np.array([a.field_i for a in anns], np.int64),
+            'ann_score': np.array([a.score for a in anns], np.float32),
+            'ann_bbox': np.array([a.bbox for a in anns], np.float32).reshape(-1, 4),
+        }
+        np.savez_compressed(os.path.join(HERE, 'detm_%s.npz' % name), **out)
+        print('detm', name, 'seeds', len(seeds), 'anns', len(anns))
+    CifSeeds.threshold = None
+
+
 # initial_annotations (cifcaf.py:67-71,95-98): a decode of API_INIT_FIELDS grows three
 # annotations derived from a decode of API_INIT_PREV first
 API_INIT_FIELDS = dict(h=40, w=40, n_people=8, seed=5)
@@ -827,6 +869,10 @@ def main():
     if only == ['det']:
         gen_det(op)
         gen_det_nms(op)
+        gen_det_multi(op)
+        return
+    if only == ['detm']:
+        gen_det_multi(op)
         return
     gen_primitives(op)
     gen_errors()
@@ -835,6 +881,7 @@ def main():
     gen_heads(op)
     gen_det(op)
     gen_det_nms(op)
+    gen_det_multi(op)
     gen_inverse(op)
     gen_multi(op)
     gen_api(op)

@@ -705,6 +705,94 @@ def test_cifdet_batch_vs_oracle(dec, kind):
         assert np.array_equal(got['bbox'], ref['bbox']), i
 
 
+DETM_NAMES = sorted(os.path.basename(p)[5:-4] for p in
+                    __import__('glob').glob(os.path.join(gu.GOLDEN, 'detm_*.npz')))
+
+
+def _detm_case(dec, name):
+    """detm_<name>.npz: the reference CifDet over several heads / min scales
+    (gen_golden.DET_MULTI_CASES); (fixture, FieldConfig, per-head fields, categories)."""
+    from openpifpaf_amd import synthetic
+    g = np.load(os.path.join(gu.GOLDEN, 'detm_%s.npz' % name))
+    k = int(g['n_categories'])
+    heads = [tuple(r) for r in g['heads']]
+    fields = [synthetic.det_batch(str(g['gen']), 1, int(h), int(w), first_seed=int(seed),
+                                  n_categories=k)[0] for h, w, _, _, seed in heads]
+    assert [gu.sha(f) for f in fields] == [str(x) for x in g['input_sha']]
+    fc = dec.FieldConfig(cif_indices=list(range(len(heads))),
+                         cif_strides=[int(st) for _, _, st, _, _ in heads],
+                         cif_min_scales=[float(ms) for _, _, _, ms, _ in heads])
+    dec.CifHr.v_threshold = 0.1
+    dec.CifSeeds.threshold = float(g['seed_threshold'])
+    return g, fc, fields, ['c%d' % i for i in range(k)]
+
+
+@pytest.mark.parametrize('name', DETM_NAMES)
+def test_cifdet_multi_stages_vs_reference(dec, name):
+    """CifDetHr / CifDetSeeds over several heads and min scales (cif_hr.py:67-90,
+    cif_seeds.py:56-90): map digest and the full seed list."""
+    g, fc, fields, _ = _detm_case(dec, name)
+    hr = dec.CifDetHr(fc).fill(fields).accumulated
+    assert gu.sha(hr) == str(g['cifhr_sha'])
+    seeds = dec.CifDetSeeds(hr, fc).fill(fields).get()
+    rows = np.array([[float(t) for t in sd] for sd in seeds], np.float32).reshape(-1, 6)
+    assert np.array_equal(rows, g['seeds'])
+
+
+@pytest.mark.parametrize('name', DETM_NAMES)
+def test_cifdet_multi_vs_reference(dec, name):
+    """CifDet.__call__ over several heads / min scales (pp_cifdet_decode_multi)."""
+    g, fc, fields, cats = _detm_case(dec, name)
+    anns = dec.CifDet(fc, cats)(fields)
+    assert [a.field_i for a in anns] == g['ann_field'].tolist()
+    assert np.array_equal(np.array([a.score for a in anns], np.float32), g['ann_score'])
+    assert np.array_equal(np.array([a.bbox for a in anns], np.float32).reshape(-1, 4),
+                          g['ann_bbox'])
+
+
+def test_cifdet_multi_batch_matches_single_images(dec):
+    """decode_batch over a batch of two-head fields (one pp_cifdet_decode_multi launch) equals
+    each image's own decode, record for record; a one-head FieldConfig with a zero min scale
+    through the multi entry point equals pp_cifdet_decode."""
+    import torch
+    from openpifpaf_amd import synthetic
+    dec.CifHr.v_threshold = 0.1
+    dec.CifSeeds.threshold = 0.3
+    h0 = synthetic.det_batch('planted', 6, 40, 48, first_seed=70, n_categories=3)
+    h1 = synthetic.det_batch('planted', 6, 20, 24, first_seed=170, n_categories=3)
+    fc = dec.FieldConfig(cif_indices=[0, 1], cif_strides=[8, 16], cif_min_scales=[0.0, 48.0])
+    cd = dec.CifDet(fc, ['a', 'b', 'c'])
+    recs, offsets = cd.decode_records([torch.from_numpy(h0).cuda(), torch.from_numpy(h1).cuda()])
+    for i in range(6):
+        one, off1 = cd.decode_records([torch.from_numpy(h0[i:i + 1]).cuda(),
+                                       torch.from_numpy(h1[i:i + 1]).cuda()])
+        assert recs[offsets[i]:offsets[i + 1]].tobytes() == one.tobytes(), i
+    # the multi entry point with one plain head is the single-head decode
+    from openpifpaf_amd import _device
+    from openpifpaf_amd._abi import scale_list
+    from openpifpaf_amd._lib import call, load
+    import ctypes
+    single = dec.CifDet(dec.FieldConfig(), ['a', 'b', 'c'])
+    ref, ref_off = single.decode_records(h0)
+    cfg = single.config()
+    z = __import__('openpifpaf_amd.decoder.generator.cifdet', fromlist=['x']).det_nms_config()
+    t = torch.from_numpy(h0).cuda()
+    arr = scale_list([(t.data_ptr(), 40, 48)], [], [8], [], [0.0])
+    cap = 40 * 48
+    ws = torch.empty(int(load().pp_cifdet_multi_workspace_size(arr, 1, 0, 6, 3, cap)),
+                     dtype=torch.uint8, device='cuda')
+    out = torch.empty((6, cap, 32), dtype=torch.uint8, device='cuda')
+    counts = torch.empty(6, dtype=torch.int32, device='cuda')
+    status = torch.empty(6, dtype=torch.int32, device='cuda')
+    call('pp_cifdet_decode_multi', arr, 1, 0, 6, 3, ctypes.byref(cfg), ctypes.byref(z),
+         _device.ptr(None), _device.ptr(out), cap, _device.ptr(counts), _device.ptr(status),
+         _device.ptr(ws), ctypes.c_size_t(ws.numel()), _device.stream())
+    host, n = out.cpu().numpy(), counts.cpu().numpy()
+    assert not status.cpu().numpy().any()
+    got = np.concatenate([host[i, :n[i]].reshape(-1) for i in range(6)]).tobytes()
+    assert got == ref.tobytes()
+
+
 @pytest.mark.parametrize('name', ['few', 'many', 'ties'])
 def test_nms_detection_vs_reference(dec, name):
     from openpifpaf_amd.annotation import AnnotationDet
