@@ -91,7 +91,7 @@ _SIGNATURES = {
     'pp_cifdet_seeds_multi': ([_vp, _i32, _vp, _i32, _i32, _vp, _vp, _vp, _vp], ctypes.c_int),
     'pp_cifdet_multi_workspace_size': ([_vp, _i32, _i32, _i32, _i32, _i32], _sz),
     'pp_cifdet_decode_multi': ([_vp, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _vp,
-                                _vp, _vp, _vp, _sz, _vp], ctypes.c_int),
+                                _vp, _vp, _sz, _vp], ctypes.c_int),
     'pp_nms_detection_workspace_size': ([_i32, _i32], _sz),
     'pp_nms_detection': ([_vp, _vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp],
                          ctypes.c_int),

@@ -752,7 +752,8 @@ def test_cifdet_multi_vs_reference(dec, name):
 
 def test_cifdet_multi_batch_matches_single_images(dec):
     """decode_batch over a batch of two-head fields (one pp_cifdet_decode_multi launch) equals
-    each image's own decode, record for record; a one-head FieldConfig with a zero min scale
+    each image's own decode, record for record (but the image index); a one-head FieldConfig
+    with a zero min scale
     through the multi entry point equals pp_cifdet_decode."""
     import torch
     from openpifpaf_amd import synthetic
@@ -766,7 +767,10 @@ def test_cifdet_multi_batch_matches_single_images(dec):
     for i in range(6):
         one, off1 = cd.decode_records([torch.from_numpy(h0[i:i + 1]).cuda(),
                                        torch.from_numpy(h1[i:i + 1]).cuda()])
-        assert recs[offsets[i]:offsets[i + 1]].tobytes() == one.tobytes(), i
+        got = recs[offsets[i]:offsets[i + 1]]
+        assert (got['image'] == i).all() and (one['image'] == 0).all(), i
+        for key in ('field', 'score', 'bbox'):
+            assert got[key].tobytes() == one[key].tobytes(), (i, key)
     # the multi entry point with one plain head is the single-head decode
     from openpifpaf_amd import _device
     from openpifpaf_amd._abi import scale_list
