@@ -1,7 +1,8 @@
 """A/B builds that change a constant of the library source without touching csrc/: copies
 csrc/ to build_src_<name>/, applies literal replacements, and links
 openpifpaf_amd/libpifpaf_amd_<name>.so (PP_LIB_VARIANT=<name> loads it).
-Usage: python tools/src_variant.py <name> <file> '<old>' '<new>' [<file> '<old>' '<new>' ...]"""
+Usage: python tools/src_variant.py <name> <file> '<old>' '<new>' [<file> '<old>' '<new>' ...]
+('<old>' must occur once; '*<old>' replaces every occurrence)"""
 import os
 import shutil
 import subprocess
@@ -20,8 +21,13 @@ def main():
     for i in range(0, len(rest), 3):
         p = os.path.join(src_dir, rest[i])
         s = open(p).read()
-        assert s.count(rest[i + 1]) == 1, (rest[i], rest[i + 1], s.count(rest[i + 1]))
-        open(p, 'w').write(s.replace(rest[i + 1], rest[i + 2]))
+        old = rest[i + 1]
+        if old.startswith('*'):  # '*<text>': every occurrence (at least one)
+            old = old[1:]
+            assert s.count(old) >= 1, (rest[i], old)
+        else:
+            assert s.count(old) == 1, (rest[i], old, s.count(old))
+        open(p, 'w').write(s.replace(old, rest[i + 2]))
     bdir = src_dir + '/obj'
     os.makedirs(bdir)
     srcs = sorted(os.path.join(src_dir, f) for f in os.listdir(src_dir) if f.endswith('.hip'))
