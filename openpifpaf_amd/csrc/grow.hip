@@ -1662,6 +1662,15 @@ constexpr int kSpecScan = 128;     // seeds after the committed one examined per
 // Throughput is flat for 0-4 (both generators) and drops beyond 8.
 constexpr float kSpecFar = 4.0f;
 constexpr int kSelfScan = 256;     // seeds after the decided ones a finished helper examines
+// seeds after the committed one that wave 0 of seed_loop_ext_kernel examines per plan round
+// (cfg5 planted 42.9k-43.7k -> 45.8k-47.0k images/s with 512 instead of 128, round 6)
+constexpr int kExtScan = 512;
+// Both plans exclude a seed only for annotations that come BEFORE it in seed order: near a
+// seed in flight, inside the occupancy boxes of a grown annotation or of the joints an
+// in-flight grow has set so far, when that annotation's seed precedes it (wave 0 commits it
+// first, and its boxes then cover the seed).  An annotation whose seed comes after cannot
+// cover it at its turn, so excluding it there only made wave 0 grow it itself (cfg5 planted
+// 39.4k-40.2k -> 42.9k-43.7k, planted cfg3 406k-413k -> 415k-416k; round 6).
 // Who plans the idle helpers when wave 0 has to grow a seed itself: an idle helper, so that
 // wave 0 starts its grow at once and the plan (a scan of kSpecScan seeds against the cache,
 // about 50k cycles, stamps) is off the committer's path (wave 0 planning before its grow
@@ -1998,9 +2007,12 @@ __device__ __noinline__ uint64_t spec_plan(SeedLoopShared &S, const pp_seed *see
         const uint32_t r_pm = sl ? lds_acquire_u(&S.cache_pm[lane]) : 0u;
         for (uint64_t fq = live & fly; fq; fq &= fq - 1) {
             const int q = __ffsll((unsigned long long)fq) - 1;
-            ok = ok && spec_far(far_k, c.x, c.y, c.s, rl_f(r_x, q), rl_f(r_y, q), rl_f(r_s, q));
+            ok = ok && (__builtin_amdgcn_readlane(r_seed, q) > idx ||
+                         spec_far(far_k, c.x, c.y, c.s, rl_f(r_x, q), rl_f(r_y, q), rl_f(r_s, q)));
             const uint32_t pm = (uint32_t)__builtin_amdgcn_readlane((int)r_pm, q);
-            if (ok && ((pm >> cf) & 1u) && covered(S.cache_j[q][cf])) ok = false;
+            if (ok && ((pm >> cf) & 1u) && __builtin_amdgcn_readlane(r_seed, q) < idx &&
+                covered(S.cache_j[q][cf]))
+                ok = false;
         }
         // seeds a grown annotation's occupancy boxes will cover once committed
         const int bf = ok ? cf : 0;
@@ -2017,7 +2029,9 @@ __device__ __noinline__ uint64_t spec_plan(SeedLoopShared &S, const pp_seed *see
             for (int u = 0; u < 4; u++) bx[u] = qs[u] >= 0 ? S.cache_box[qs[u]][bf] : make_uint2(0u, 0u);
 #pragma unroll
             for (int u = 0; u < 4; u++)
-                if (in_plan_box(bx[u], cxi, cyi)) ok = false;
+                if (qs[u] >= 0 && __builtin_amdgcn_readlane(r_seed, qs[u]) < idx &&
+                    in_plan_box(bx[u], cxi, cyi))
+                    ok = false;
         }
         uint64_t m = __ballot(ok);
         while (m && idle) {
@@ -2025,7 +2039,8 @@ __device__ __noinline__ uint64_t spec_plan(SeedLoopShared &S, const pp_seed *see
             m &= m - 1;
             const float cx = rl_f(c.x, l), cy = rl_f(c.y, l), csc = rl_f(c.s, l);
             // far from this plan's earlier picks and every other seed in flight (a lane per slot)
-            if (__ballot(((fly >> lane) & 1ull) && !spec_far(far_k, cx, cy, csc, r_x, r_y, r_s)))
+            if (__ballot(((fly >> lane) & 1ull) && r_seed < base + l &&
+                         !spec_far(far_k, cx, cy, csc, r_x, r_y, r_s)))
                 continue;
             // a free slot: never grown into, or grown for a seed already decided
             const uint64_t freeq = __ballot(sl && (r_st == 0 || (r_st == 2 && r_seed < decided)));
@@ -2656,7 +2671,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
                   r_s = sl ? S.cache_s[lane] : 0.0f;
             // the seeds in flight: later picks keep kSpecFar from them
             uint64_t fly = __ballot(sl && r_st == 1);
-            const int scan_end = min(n_seeds, t + 1 + kSpecScan);
+            const int scan_end = min(n_seeds, t + 1 + kExtScan);
 #ifdef PP_STAMPS
             uint64_t pf0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -2678,7 +2693,8 @@ void seed_loop_ext_kernel(GrowArgs g) {
                     if (idx == __builtin_amdgcn_readlane(r_seed, __ffsll((unsigned long long)hq) - 1)) ok = false;
                 for (uint64_t fq = ahead & fly; fq; fq &= fq - 1) {
                     const int q = __ffsll((unsigned long long)fq) - 1;
-                    ok = ok && spec_far(g.spec_far, c.x, c.y, c.s, rl_f(r_x, q), rl_f(r_y, q), rl_f(r_s, q));
+                    ok = ok && (__builtin_amdgcn_readlane(r_seed, q) > idx ||
+                                 spec_far(g.spec_far, c.x, c.y, c.s, rl_f(r_x, q), rl_f(r_y, q), rl_f(r_s, q)));
                 }
                 const int cxi = (int)clip_ref(c.x / red, 0.0f, (float)(occ.w - 1));
                 const int cyi = (int)clip_ref(c.y / red, 0.0f, (float)(occ.h - 1));
@@ -2697,7 +2713,9 @@ void seed_loop_ext_kernel(GrowArgs g) {
                         b[u] = qs[u] >= 0 ? cache_boxes(s_cols, qs[u])[cf] : make_uint2(0u, 0u);
 #pragma unroll
                     for (int u = 0; u < 4; u++)
-                        if (in_plan_box(b[u], cxi, cyi)) ok = false;
+                        if (qs[u] >= 0 && __builtin_amdgcn_readlane(r_seed, qs[u]) < idx &&
+                            in_plan_box(b[u], cxi, cyi))
+                            ok = false;
                 }
                 uint64_t m = __ballot(ok);
 #ifdef PP_STAMPS
@@ -2709,7 +2727,8 @@ void seed_loop_ext_kernel(GrowArgs g) {
                     const float cx = rl_f(c.x, l), cy = rl_f(c.y, l), csc = rl_f(c.s, l);
                     // far from every seed in flight, this plan's earlier picks included (a
                     // lane per slot)
-                    if (__ballot(((fly >> lane) & 1ull) && !spec_far(g.spec_far, cx, cy, csc, r_x, r_y, r_s)))
+                    if (__ballot(((fly >> lane) & 1ull) && r_seed < base + l &&
+                                 !spec_far(g.spec_far, cx, cy, csc, r_x, r_y, r_s)))
                         continue;
                     // a free slot of the helper's kind (this CU's: 0 .. kSpecCache-1; the
                     // external ones after): never grown into, or grown for a seed passed
