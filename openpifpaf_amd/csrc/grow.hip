@@ -1665,6 +1665,11 @@ constexpr int kSelfScan = 256;     // seeds after the decided ones a finished he
 // seeds after the committed one that wave 0 of seed_loop_ext_kernel examines per plan round
 // (cfg5 planted 42.9k-43.7k -> 45.8k-47.0k images/s with 512 instead of 128, round 6)
 constexpr int kExtScan = 512;
+// the external-helper plan's speculation distance (joint scales): 1 instead of kSpecFar's 4
+// (cfg5 planted 45.5k-46.9k -> 50.3k-50.4k images/s, uniform 1513-1517 vs 1518-1527; with 1
+// for the one-CU kernel too, planted cfg3 was 415k vs 415k-420k and uniform 16.1k-16.3k vs
+// 16.0k; round 6, r06z_ab_spec_far.txt)
+constexpr float kExtSpecFar = 1.0f;
 // Both plans exclude a seed only for annotations that come BEFORE it in seed order: near a
 // seed in flight, inside the occupancy boxes of a grown annotation or of the joints an
 // in-flight grow has set so far, when that annotation's seed precedes it (wave 0 commits it
@@ -2681,7 +2686,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
                 pp_seed c{};
                 if (ok) {
                     c = seeds[idx];
-                    ok = (!own || spec_far(g.spec_far, c.x, c.y, c.s, st.x, st.y, st.s)) &&
+                    ok = (!own || spec_far(kExtSpecFar, c.x, c.y, c.s, st.x, st.y, st.s)) &&
                          !(socc_on ? seed_occupied(s_occ, idx) : occ_get(occ, c.field, c.x, c.y, red));
                 }
                 // the slots holding seeds after t (the others are free or passed): skip the
@@ -2694,7 +2699,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
                 for (uint64_t fq = ahead & fly; fq; fq &= fq - 1) {
                     const int q = __ffsll((unsigned long long)fq) - 1;
                     ok = ok && (__builtin_amdgcn_readlane(r_seed, q) > idx ||
-                                 spec_far(g.spec_far, c.x, c.y, c.s, rl_f(r_x, q), rl_f(r_y, q), rl_f(r_s, q)));
+                                 spec_far(kExtSpecFar, c.x, c.y, c.s, rl_f(r_x, q), rl_f(r_y, q), rl_f(r_s, q)));
                 }
                 const int cxi = (int)clip_ref(c.x / red, 0.0f, (float)(occ.w - 1));
                 const int cyi = (int)clip_ref(c.y / red, 0.0f, (float)(occ.h - 1));
@@ -2728,7 +2733,7 @@ void seed_loop_ext_kernel(GrowArgs g) {
                     // far from every seed in flight, this plan's earlier picks included (a
                     // lane per slot)
                     if (__ballot(((fly >> lane) & 1ull) && r_seed < base + l &&
-                                 !spec_far(g.spec_far, cx, cy, csc, r_x, r_y, r_s)))
+                                 !spec_far(kExtSpecFar, cx, cy, csc, r_x, r_y, r_s)))
                         continue;
                     // a free slot of the helper's kind (this CU's: 0 .. kSpecCache-1; the
                     // external ones after): never grown into, or grown for a seed passed
