@@ -2275,6 +2275,10 @@ void seed_loop_kernel(GrowArgs g) {
     const bool socc_on = n_seeds <= kOccSeeds;
     if (socc_on) seed_occ_init(s_occ, seeds, n_seeds, K, occ, red);
     const SeedOcc *socc = socc_on ? &s_occ : nullptr;
+    // the plans' speculation distance: kSpecFar, but none on images with more seeds than
+    // kOccSeeds (dense fields, where nearly every seed lies near one in flight): uniform
+    // cfg3 15.6k-16.1k -> 16.1k-16.2k images/s, planted unchanged (r06z_ab_dense_far.txt)
+    const float far_img = socc_on ? g.spec_far : 0.0f;
 
     // committer state (wave 0)
     int n_anns = 0, s = 0;
@@ -2327,7 +2331,7 @@ void seed_loop_kernel(GrowArgs g) {
                     uint64_t left = 1ull << wave;
                     const int dec = lds_acquire(&S.decided);
                     if (!lds_acquire(&S.done) && lds_acquire(&S.task[wave]) < 0)
-                        left = spec_plan(S, seeds, n_seeds, dec, kSelfScan, occ, red, msr, g.spec_far,
+                        left = spec_plan(S, seeds, n_seeds, dec, kSelfScan, occ, red, msr, far_img,
                                          left, socc);
                     plan_unlock(S);
                     idle_dec = left ? dec : -1;
@@ -2349,7 +2353,7 @@ void seed_loop_kernel(GrowArgs g) {
                         const uint64_t idle = __ballot(lane > 0 && lane < kSeedWaves && tk < 0);
                         const int dec = lds_acquire(&S.decided);
                         if (idle)
-                            spec_plan(S, seeds, n_seeds, dec, kSpecScan, occ, red, msr, g.spec_far,
+                            spec_plan(S, seeds, n_seeds, dec, kSpecScan, occ, red, msr, far_img,
                                       idle, socc);
                     }
                     plan_unlock(S);
@@ -2390,7 +2394,7 @@ void seed_loop_kernel(GrowArgs g) {
             uint64_t left = 1ull << wave;
             if (!lds_acquire(&S.done)) {
                 const int dec = lds_acquire(&S.decided);
-                left = spec_plan(S, seeds, n_seeds, dec, kSelfScan, occ, red, msr, g.spec_far, left,
+                left = spec_plan(S, seeds, n_seeds, dec, kSelfScan, occ, red, msr, far_img, left,
                                  socc);
             }
             if (left && lane == 0) lds_release(&S.task[wave], -1);
