@@ -1670,6 +1670,15 @@ constexpr int kExtScan = 512;
 // for the one-CU kernel too, planted cfg3 was 415k vs 415k-420k and uniform 16.1k-16.3k vs
 // 16.0k; round 6, r06z_ab_spec_far.txt)
 constexpr float kExtSpecFar = 1.0f;
+// Wave 0 of seed_loop_ext_kernel plans the idle helpers when it has to grow a seed itself (a
+// miss), and, on images of kExtRefillAnns annotations or more, also after a cached commit that
+// leaves fewer than kExtRefill speculated seeds ahead: a dense image otherwise ran its helpers
+// dry between misses (~77 of ~1370 seeds per cfg5 uniform image grown by wave 0 itself, each a
+// whole grow on the critical path, r06h stamps).  cfg5 uniform 1510-1545 -> 1562-1737 images/s
+// with 12 (8: 1616-1661, 16: no gain, 20: 1558-1576; planted unchanged from 32 annotations on,
+// -2 % when refilling on every image; r06z_ab_refill.txt).
+constexpr int kExtRefillAnns = 32;
+constexpr int kExtRefill = 12;
 // Both plans exclude a seed only for annotations that come BEFORE it in seed order: near a
 // seed in flight, inside the occupancy boxes of a grown annotation or of the joints an
 // in-flight grow has set so far, when that annotation's seed precedes it (wave 0 commits it
@@ -2857,6 +2866,16 @@ void seed_loop_ext_kernel(GrowArgs g) {
 #ifdef PP_STAMPS
                 n_hits++;
 #endif
+                if (n_anns >= kExtRefillAnns) {
+                    // few speculated seeds left ahead: plan a round now, not at the next miss
+                    const uint64_t aq = __ballot(lane < NS && S.cache_seed[lane] > t &&
+                                                 (S.cache_state[lane] == 1 || S.cache_state[lane] == 2));
+                    if (__popcll(aq) < kExtRefill) {
+                        plan_lock(S);
+                        plan_round(t, false, seeds[t]);
+                        plan_unlock(S);
+                    }
+                }
                 STAMP(4);
                 continue;
             }
